@@ -1,0 +1,41 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "data-compression_amd"))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+CASES = ["testfloat", "rand16k", "u10_16k", "eq16k", "himeno", "unit64k", "q2", "ramp20k", "edge"]
+BOUNDS = [1e-3, 1e-6]
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run on the GPU box)")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from pyoracle import Oracle
+    return Oracle()
+
+
+_golden_cache = {}
+
+
+def golden(bound):
+    if bound not in _golden_cache:
+        with np.load(os.path.join(GOLDEN, "golden_%g.npz" % bound), allow_pickle=False) as z:
+            _golden_cache[bound] = {k: z[k] for k in z.files}
+    return _golden_cache[bound]
+
+
+def gpu_available():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
