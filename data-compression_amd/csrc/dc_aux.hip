@@ -1,0 +1,315 @@
+// dc_aux.hip -- pre-passes and stream protection on gfx950.
+//
+//  * toSmallDataset_float (impl/dataCompression.c:3543-3562): min then x - min.  The sequential
+//    `if (data[i] < min)` keeps the FIRST occurrence of the minimum (so +0/-0 ties and NaNs resolve
+//    like the reference); the parallel reduction carries (value, index) to reproduce that.
+//  * med_dataset_float (:3593-3620): a left-to-right float sum (order-dependent rounding), so the
+//    sum runs in one lane over LDS-staged blocks; max and type are exact in parallel.
+//  * do_crc32 (:5524-5534, zlib crc32 byte by byte): per-lane table CRC of 64-byte runs, combined
+//    with GF(2) "multiply by x^(8n) mod P" operators (crc(A||B) = shift(crc(A),|B|) ^ crc(B)).
+//  * hamming_encode / hamming_decode (:5740-5778): SECDED check bits per block = XOR of the Hamming
+//    positions of the set data bits (powers of two skipped) + overall parity.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "dc_shared.h"
+
+namespace dc {
+
+// ---------------------------------------------------------------- toSmallDataset_float
+struct MinKey { float v; long long i; };
+
+__device__ __forceinline__ MinKey min_pick(MinKey a, MinKey b) {
+    const bool an = a.v != a.v, bn = b.v != b.v;        // NaN never wins (except as data[0])
+    if (an) return b;
+    if (bn) return a;
+    if (b.v < a.v) return b;
+    if (a.v < b.v) return a;
+    return a.i <= b.i ? a : b;                           // equal (incl. +0 == -0): first occurrence
+}
+
+__global__ __launch_bounds__(256) void min_partial_kernel(const float* __restrict__ x, long long n,
+                                                          float* __restrict__ pv, long long* __restrict__ pi) {
+    __shared__ float sv[256];
+    __shared__ long long si[256];
+    MinKey m = {__int_as_float(0x7fc00000), (long long)1 << 62};
+    for (long long i = 1 + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x) {
+        MinKey k = {x[i], i};
+        m = min_pick(m, k);
+    }
+    sv[threadIdx.x] = m.v; si[threadIdx.x] = m.i;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            MinKey a = {sv[threadIdx.x], si[threadIdx.x]}, b = {sv[threadIdx.x + s], si[threadIdx.x + s]};
+            const MinKey r = min_pick(a, b);
+            sv[threadIdx.x] = r.v; si[threadIdx.x] = r.i;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) { pv[blockIdx.x] = sv[0]; pi[blockIdx.x] = si[0]; }
+}
+
+__global__ void min_final_kernel(const float* __restrict__ x, const float* __restrict__ pv,
+                                 const long long* __restrict__ pi, int nparts, float* __restrict__ out_min) {
+    if (threadIdx.x != 0) return;
+    MinKey m = {__int_as_float(0x7fc00000), (long long)1 << 62};
+    for (int p = 0; p < nparts; p++) { MinKey k = {pv[p], pi[p]}; m = min_pick(m, k); }
+    const float x0 = x[0];
+    float r = x0;                                        // min = data[0]; later strictly smaller wins
+    if (!(m.v != m.v) && m.v < x0) r = m.v;
+    *out_min = r;
+}
+
+__global__ __launch_bounds__(256) void sub_min_kernel(const float* __restrict__ x, long long n,
+                                                      const float* __restrict__ mn, float* __restrict__ y) {
+    const float m = *mn;
+    const long long n4 = n >> 2;
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    float4* y4 = reinterpret_cast<float4*>(y);
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+         i += (long long)gridDim.x * blockDim.x) {
+        float4 v = x4[i];
+        v.x = __fsub_rn(v.x, m); v.y = __fsub_rn(v.y, m); v.z = __fsub_rn(v.z, m); v.w = __fsub_rn(v.w, m);
+        y4[i] = v;
+    }
+    for (long long i = (n4 << 2) + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        y[i] = __fsub_rn(x[i], m);
+}
+
+// ---------------------------------------------------------------- med_dataset_float
+constexpr int MED_BLK = 8192;
+
+__global__ __launch_bounds__(256) void med_kernel(const float* __restrict__ x, long long n,
+                                                  float* __restrict__ out_mean, int* __restrict__ out_type) {
+    __shared__ float buf[2][MED_BLK];
+    __shared__ float smax[256];
+    float mx = x[0];
+    float total = 0.0f;
+    const long long nblk = (n + MED_BLK - 1) / MED_BLK;
+    // prime buffer 0
+    for (int i = threadIdx.x; i < MED_BLK; i += 256) buf[0][i] = (i < n) ? x[i] : 0.0f;
+    __syncthreads();
+    for (long long b = 0; b < nblk; b++) {
+        const int cur = (int)(b & 1);
+        const long long nb = (b + 1) * MED_BLK;
+        if (b + 1 < nblk)                                 // stage the next block while lane 0 sums
+            for (int i = threadIdx.x; i < MED_BLK; i += 256) buf[cur ^ 1][i] = (nb + i < n) ? x[nb + i] : 0.0f;
+        const long long lim = (n - b * MED_BLK) < MED_BLK ? (n - b * MED_BLK) : MED_BLK;
+        for (int i = threadIdx.x; i < lim; i += 256) { const float v = buf[cur][i]; if (v > mx) mx = v; }
+        if (threadIdx.x == 0) {
+            const float* p = buf[cur];
+            for (int i = 0; i < (int)lim; i++) total = __fadd_rn(total, p[i]);
+        }
+        __syncthreads();
+    }
+    smax[threadIdx.x] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float m = smax[0];
+        for (int i = 1; i < 256; i++) if (smax[i] > m) m = smax[i];
+        int type = 0, add = 0;                             // :3605-3614
+        for (int i = 7; i > 0; i--) {
+            add += 1 << i;
+            if ((double)m < ldexp(1.0, add - 127)) { type = 8 - i; break; }
+        }
+        *out_type = type;
+        *out_mean = __fdiv_rn(total, (float)n);
+    }
+}
+
+// ---------------------------------------------------------------- CRC-32 (zlib)
+constexpr uint32_t CRC_POLY = 0xEDB88320u;
+constexpr int CRC_RUN = 64;                               // bytes per lane
+constexpr int CRC_BLK = CRC_RUN * 256;                    // bytes per workgroup
+
+__device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {     // a*b mod P (reflected)
+    uint32_t m = 1u << 31, p = 0;
+    for (int i = 0; i < 32; i++) {
+        if (a & m) p ^= b;
+        m >>= 1;
+        b = (b & 1u) ? (b >> 1) ^ CRC_POLY : b >> 1;
+    }
+    return p;
+}
+
+__device__ __forceinline__ uint32_t xpow8n(unsigned long long n, const uint32_t* x2n) {  // x^(8n) mod P
+    uint32_t p = 1u << 31;
+    int k = 3;
+    while (n) {
+        if (n & 1) p = multmodp(x2n[k & 31], p);
+        n >>= 1;
+        k++;
+    }
+    return p;
+}
+
+__global__ __launch_bounds__(256) void crc_blocks_kernel(const uint8_t* __restrict__ s, long long nbytes,
+                                                         const uint32_t* __restrict__ tab_g,
+                                                         const uint32_t* __restrict__ x2n_g,
+                                                         uint32_t* __restrict__ part) {
+    __shared__ uint32_t tab[256];
+    __shared__ uint32_t x2n[32];
+    __shared__ uint32_t red[256];
+    tab[threadIdx.x] = tab_g[threadIdx.x];
+    if (threadIdx.x < 32) x2n[threadIdx.x] = x2n_g[threadIdx.x];
+    __syncthreads();
+    const long long nblk = (nbytes + CRC_BLK - 1) / CRC_BLK;
+    for (long long b = blockIdx.x; b < nblk; b += gridDim.x) {
+        const long long st = b * CRC_BLK + (long long)threadIdx.x * CRC_RUN;
+        uint32_t r = 0;
+        for (int i = 0; i < CRC_RUN; i++) {               // raw CRC (init 0) of this lane's run
+            const long long p = st + i;
+            if (p < nbytes) r = tab[(r ^ s[p]) & 0xFFu] ^ (r >> 8);
+        }
+        red[threadIdx.x] = r;
+        __syncthreads();
+        for (int w = 1; w < 256; w <<= 1) {               // combine neighbours: left shifted by right's length
+            uint32_t v = 0;
+            const int t = threadIdx.x;
+            const bool act = (t % (2 * w)) == 0;
+            if (act) {
+                const long long rs = b * CRC_BLK + (long long)(t + w) * CRC_RUN;
+                long long rlen = (long long)w * CRC_RUN;
+                if (rs >= nbytes) rlen = 0;
+                else if (rs + rlen > nbytes) rlen = nbytes - rs;
+                v = (rlen ? multmodp(xpow8n((unsigned long long)rlen, x2n), red[t]) : red[t]) ^ red[t + w];
+            }
+            __syncthreads();
+            if (act) red[t] = v;
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) part[b] = red[0];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void crc_final_kernel(const uint32_t* __restrict__ part, long long nbytes,
+                                                        const uint32_t* __restrict__ x2n_g, uint32_t init,
+                                                        uint32_t* __restrict__ out) {
+    __shared__ uint32_t x2n[32];
+    __shared__ uint32_t red[256];
+    __shared__ long long rl[256];
+    if (threadIdx.x < 32) x2n[threadIdx.x] = x2n_g[threadIdx.x];
+    __syncthreads();
+    const long long nblk = (nbytes + CRC_BLK - 1) / CRC_BLK;
+    const long long per = (nblk + 255) / 256;
+    const long long b0 = threadIdx.x * per;
+    const uint32_t cfull = xpow8n((unsigned long long)CRC_BLK, x2n);
+    uint32_t r = 0;
+    long long len = 0;
+    for (long long b = b0; b < b0 + per && b < nblk; b++) {
+        long long bl = nbytes - b * CRC_BLK;
+        if (bl >= CRC_BLK) r = multmodp(cfull, r) ^ part[b];
+        else r = multmodp(xpow8n((unsigned long long)bl, x2n), r) ^ part[b];
+        len += bl < CRC_BLK ? bl : CRC_BLK;
+    }
+    red[threadIdx.x] = r;
+    rl[threadIdx.x] = len;
+    __syncthreads();
+    for (int w = 1; w < 256; w <<= 1) {                   // tree: left shifted by right's length
+        const int t = threadIdx.x;
+        const bool act = (t % (2 * w)) == 0;
+        uint32_t v = 0;
+        long long l = 0;
+        if (act) {
+            const long long rlen = rl[t + w];
+            v = (rlen ? multmodp(xpow8n((unsigned long long)rlen, x2n), red[t]) : red[t]) ^ red[t + w];
+            l = rl[t] + rlen;
+        }
+        __syncthreads();
+        if (act) { red[t] = v; rl[t] = l; }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        // zlib: crc32(init, buf) = ~(raw(buf) ^ shift(~init, n))
+        const uint32_t v = red[0] ^ multmodp(xpow8n((unsigned long long)nbytes, x2n), ~init);
+        *out = ~v;
+    }
+}
+
+// ---------------------------------------------------------------- Hamming SECDED
+// Hamming position of data bit d (0-based): the (d+1)-th positive integer that is not a power of 2.
+__device__ __forceinline__ unsigned long long ham_pos(unsigned long long d) {
+    unsigned long long j = d + 1;
+    unsigned long long k = 0;                             // powers of two <= j (grows with j)
+    while (true) {
+        const unsigned long long cand = d + 1 + k;
+        const unsigned long long pw = (unsigned long long)(64 - __clzll((long long)cand));   // #powers <= cand
+        if (pw == k) { j = cand; break; }
+        k = pw;
+    }
+    return j;
+}
+
+__global__ __launch_bounds__(256) void ham_syndrome_kernel(const uint8_t* __restrict__ s, long long nbytes,
+                                                           unsigned long long* __restrict__ out_syn,
+                                                           unsigned long long* __restrict__ out_ones) {
+    __shared__ unsigned long long ssyn[256], sones[256];
+    unsigned long long syn = 0, ones = 0;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nbytes;
+         i += (long long)gridDim.x * blockDim.x) {
+        const uint32_t byte = s[i];
+        if (!byte) continue;
+        unsigned long long j = ham_pos((unsigned long long)i * 8);
+        for (int b = 0; b < 8; b++) {
+            if (b) { j++; if ((j & (j - 1)) == 0) j++; }
+            if ((byte >> (7 - b)) & 1u) { syn ^= j; ones++; }
+        }
+    }
+    ssyn[threadIdx.x] = syn; sones[threadIdx.x] = ones;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) { ssyn[threadIdx.x] ^= ssyn[threadIdx.x + w]; sones[threadIdx.x] += sones[threadIdx.x + w]; }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) { atomicXor(out_syn, ssyn[0]); atomicAdd(out_ones, sones[0]); }
+}
+
+// ------------------------------------------------------------------------------------------------
+extern "C" int dc_launch_to_small(const float* x, long long n, float* y, float* part_v, long long* part_i,
+                                  float* d_min, hipStream_t st) {
+    if (n <= 0) return 0;
+    const int nparts = 256;
+    hipLaunchKernelGGL(min_partial_kernel, dim3(nparts), dim3(256), 0, st, x, n, part_v, part_i);
+    hipLaunchKernelGGL(min_final_kernel, dim3(1), dim3(64), 0, st, x, part_v, part_i, nparts, d_min);
+    if (y) {
+        long long g = (n / 4 + 255) / 256;
+        if (g > 2048) g = 2048;
+        if (g < 1) g = 1;
+        hipLaunchKernelGGL(sub_min_kernel, dim3((unsigned)g), dim3(256), 0, st, x, n, d_min, y);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int dc_launch_med(const float* x, long long n, float* d_mean, int* d_type, hipStream_t st) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(med_kernel, dim3(1), dim3(256), 0, st, x, n, d_mean, d_type);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" long long dc_crc_parts(long long nbytes) { return (nbytes + CRC_BLK - 1) / CRC_BLK; }
+
+extern "C" int dc_launch_crc32(const uint8_t* s, long long nbytes, const uint32_t* d_tab, const uint32_t* d_x2n,
+                               uint32_t* d_parts, uint32_t init, uint32_t* d_out, hipStream_t st) {
+    long long nblk = dc_crc_parts(nbytes);
+    if (nbytes > 0) {
+        long long g = nblk > 4096 ? 4096 : nblk;
+        hipLaunchKernelGGL(crc_blocks_kernel, dim3((unsigned)g), dim3(256), 0, st, s, nbytes, d_tab, d_x2n, d_parts);
+    }
+    hipLaunchKernelGGL(crc_final_kernel, dim3(1), dim3(256), 0, st, d_parts, nbytes, d_x2n, init, d_out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int dc_launch_ham_syndrome(const uint8_t* s, long long nbytes, unsigned long long* d_syn_ones,
+                                      hipStream_t st) {
+    (void)hipMemsetAsync(d_syn_ones, 0, 16, st);
+    long long g = (nbytes + 255) / 256;
+    if (g > 1024) g = 1024;
+    if (g < 1) g = 1;
+    hipLaunchKernelGGL(ham_syndrome_kernel, dim3((unsigned)g), dim3(256), 0, st, s, nbytes, d_syn_ones, d_syn_ones + 1);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace dc

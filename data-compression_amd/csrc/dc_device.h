@@ -1,0 +1,168 @@
+// dc_device.h -- device-side building blocks shared by the gfx950 kernels.
+//
+// Token grammar (reference impl/dataCompression.c):
+//   '100' zero, '101'/'110'/'111' predicted (:3390-3437), raw = top 9+m bits of the pattern
+//   (compress_bitwise_float :3479-3520), CT7 masked tokens (compress_bitwise_float_mask :2143-2284),
+//   CT11 verbatim 32 bits (:602-605).  Bits are MSB-first in the byte stream (add_bit_to_bytes :5456).
+// All float arithmetic uses explicit round-to-nearest intrinsics so no FMA contraction can change a
+// predictor (the reference is built by gcc for x86-64 SSE, where it cannot contract).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "dc_shared.h"
+
+namespace dc {
+
+
+
+__device__ __forceinline__ int mbits(int B, uint32_t E) {
+    int m = B + (int)E - 127;
+    return m > 23 ? 23 : (m < 0 ? 0 : m);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Encoder: token for one element.  b1..b3 are the ORIGINAL previous inputs (encoder history).
+template <int CT>
+__device__ __forceinline__ void make_token(float x, float b1, float b2, float b3, bool predict,
+                                           const Params& P, uint32_t& val, int& len) {
+    const uint32_t u = __float_as_uint(x);
+    if (CT != 6) {
+        if (fabsf(x) <= P.thr_lt) { val = 4u; len = 3; return; }              // '100'
+        if (predict) {
+            const float p1 = b1;
+            const float p2 = __fsub_rn(__fmul_rn(2.0f, b1), b2);
+            const float p3 = __fadd_rn(__fsub_rn(__fmul_rn(3.0f, b1), __fmul_rn(3.0f, b2)), b3);
+            const float d1 = fabsf(__fsub_rn(p1, x));
+            const float d2 = fabsf(__fsub_rn(p2, x));
+            const float d3 = fabsf(__fsub_rn(p3, x));
+            float dmin = d1; uint32_t code = 5u;
+            if (d2 < dmin) { dmin = d2; code = 6u; }
+            if (d3 < dmin) { dmin = d3; code = 7u; }
+            if (dmin <= P.thr_le) { val = code; len = 3; return; }
+        }
+    }
+    if (CT == 11) { val = u; len = 32; return; }
+    const int m = mbits(P.B, (u >> 23) & 0xFFu);
+    const uint32_t top = u >> (23 - m);                                       // 9+m bits
+    if (CT == 7 && (u >> 23) == (P.mask17 >> 8)) {
+        const uint32_t head = ((1u << P.type) - 1u) << 1;
+        if (((u >> 15) & 0xFFu) == (P.mask17 & 0xFFu)) {                      // flag 0
+            const int tl = m > 8 ? m - 8 : 0;
+            val = (head << tl) | (top & ((1u << tl) - 1u));
+            len = P.type + 2 + tl;
+        } else {                                                              // flag 1
+            val = ((head | 1u) << m) | (top & ((1u << m) - 1u));
+            len = P.type + 2 + m;
+        }
+        return;
+    }
+    val = top; len = 9 + m;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Decoder: token length from the next 32 stream bits (MSB-aligned).  At most 10 bits decide it.
+template <int CT>
+__device__ __forceinline__ int token_len(uint32_t t, const Params& P) {
+    if (CT == 6) return 9 + mbits(P.B, t >> 23);
+    if (t >> 31) return 3;
+    if (CT == 11) return 32;
+    if (CT == 7) {
+        const uint32_t ones = (1u << P.type) - 1u;
+        if (((t >> (31 - P.type)) & ones) == ones)
+            return P.type + 2 + (((t >> (30 - P.type)) & 1u) ? P.mm : P.mm0);
+    }
+    return 9 + mbits(P.B, (t >> 23) & 0xFFu);
+}
+
+// Value of a non-predicted token (zero / raw / masked / verbatim) from its MSB-aligned bits.
+// Predicted codes return code 1..3 in *code (101 -> 1, 110 -> 2, 111 -> 3), 0 otherwise.
+template <int CT>
+__device__ __forceinline__ uint32_t token_pattern(uint32_t t, int len, const Params& P, int* code) {
+    *code = 0;
+    if (CT != 6 && (t >> 31)) {                                               // 3-bit code
+        const uint32_t c = (t >> 29) & 3u;
+        *code = (int)c;
+        return 0u;                                                            // '100' -> 0.0f
+    }
+    if (CT == 11) return t;                                                   // verbatim
+    if (CT == 7) {
+        const uint32_t ones = (1u << P.type) - 1u;
+        if (((t >> (31 - P.type)) & ones) == ones) {
+            const int hl = P.type + 2;
+            const uint32_t rest = t << hl;                                    // bits after the head
+            if (((t >> (30 - P.type)) & 1u) == 0u) {                          // flag 0 (:1947-1961)
+                const int tl = P.mm0;
+                uint32_t u = P.mask17 << 15;
+                if (tl > 0) u |= (rest >> (32 - tl)) << (15 - tl);
+                if (tl < 15) u |= 1u << (14 - tl);
+                return u;
+            } else {                                                          // flag 1 (:1963-2010)
+                const int tl = P.mm;
+                uint32_t u = (P.mask17 >> 8) << 23;
+                if (tl > 0) u |= (rest >> (32 - tl)) << (23 - tl);
+                if (tl < 23) u |= 1u << (22 - tl);
+                return u;
+            }
+        }
+    }
+    // raw: top len bits + midpoint bit (decompress_bitwise_float :3166-3184)
+    if (len >= 32) return t;
+    return (t & ~(0xFFFFFFFFu >> len)) | (1u << (31 - len));
+}
+
+__device__ __forceinline__ float predict_value(int code, float b1, float b2, float b3) {
+    if (code == 1) return b1;
+    if (code == 2) return __fsub_rn(__fmul_rn(2.0f, b1), b2);
+    return __fadd_rn(__fsub_rn(__fmul_rn(3.0f, b1), __fmul_rn(3.0f, b2)), b3);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Per-lane MSB-first bit reader over a byte stream held as big-endian 32-bit words.
+struct BitReader {
+    const uint32_t* w;        // stream viewed as 32-bit words (4-byte aligned)
+    const uint8_t* b;
+    long long nbytes;
+    long long nwfull;         // words fully inside the stream
+    uint64_t buf;             // next bits, MSB-aligned
+    int nbuf;
+    long long wi;             // next word to load
+    long long pos;            // stream bit position of buf's MSB
+
+    __device__ __forceinline__ uint32_t load_word(long long i) const {
+        if (i < nwfull) return __builtin_bswap32(w[i]);
+        uint32_t v = 0;
+        for (int k = 0; k < 4; k++) {
+            const long long bi = 4 * i + k;
+            v = (v << 8) | (bi < nbytes ? (uint32_t)b[bi] : 0u);
+        }
+        return v;
+    }
+    __device__ __forceinline__ void refill() {
+        buf |= (uint64_t)load_word(wi++) << (32 - nbuf);
+        nbuf += 32;
+    }
+    __device__ __forceinline__ void init(const uint8_t* stream, long long nbytes_, long long p) {
+        b = stream; w = reinterpret_cast<const uint32_t*>(stream);
+        nbytes = nbytes_; nwfull = nbytes_ >> 2;
+        wi = p >> 5; buf = 0; nbuf = 0;
+        refill(); refill();
+        const int sk = (int)(p & 31);
+        buf <<= sk; nbuf -= sk;
+        if (nbuf < 32) refill();
+        pos = p;
+    }
+    __device__ __forceinline__ uint32_t peek() const { return (uint32_t)(buf >> 32); }
+    __device__ __forceinline__ void skip(int k) {
+        buf <<= k; nbuf -= k; pos += k;
+        if (nbuf < 32) refill();
+    }
+};
+
+__device__ __forceinline__ uint64_t ld_relaxed(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_relaxed(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace dc

@@ -1,0 +1,713 @@
+/*
+ * dc_host.c -- host side of libdcamd: the reference's C ABI (impl/dataCompression.h) on top of
+ * the gfx950 kernels, plus the device-pointer API of include/dc_gpu.h.
+ *
+ * Plain C.  The only bridge to HIP C++ is the extern "C" launcher set in dc_shared.h; everything
+ * else here is HIP runtime C API (memory, copies, stream) and host bookkeeping: realloc/append
+ * semantics of *data_bits, malloc'ed results owned by the caller, char-string masks.
+ * No hot-path work runs on the CPU: if the GPU is unusable the entry points report an error
+ * (dc_last_error) instead of computing anything.
+ */
+#define __HIP_PLATFORM_AMD__ 1
+#include <hip/hip_runtime_api.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "dc_shared.h"
+#include "../../include/dc_gpu.h"
+
+#ifndef DC_ABS_ERROR_BOUND
+#define DC_ABS_ERROR_BOUND 0.000001      /* impl/dataCompression.h:5 default */
+#endif
+
+/* globals of the reference (impl/dataCompression.c:21-22) */
+double absErrBound = DC_ABS_ERROR_BOUND;
+int absErrorBound_binary = -100;
+
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+    int inited, device;
+    hipStream_t st;
+    /* encoder */
+    uint64_t* enc_desc;
+    long long enc_desc_cap;
+    unsigned* enc_ctr;
+    unsigned long long* d_total;
+    unsigned* d_enc_err;
+    uint32_t enc_epoch;
+    /* decoder */
+    DecBufs D;
+    void* dec_pool;
+    long long dec_cap_chunks;
+    uint32_t dec_epoch;
+    int dec_pending;
+    Params dec_P;
+    const uint8_t* dec_s;
+    long long dec_max_chunks;
+    float* dec_out;
+    long long dec_num;
+    /* pinned host scratch */
+    unsigned long long* h_scratch;   /* [0] total bits [1] err [2..] misc */
+    /* staging for the host-pointer ABI */
+    void* d_a; size_t d_a_cap;
+    void* d_b; size_t d_b_cap;
+    /* aux */
+    float* part_v; long long* part_i;
+    float* d_f;                      /* [0] min [1] mean */
+    int* d_i;                        /* [0] type */
+    uint32_t* d_crctab; uint32_t* d_x2n; uint32_t* d_crcparts; long long crcparts_cap; uint32_t* d_crc;
+    unsigned long long* d_ham;
+    char msg[512];
+} dc_ctx;
+
+static dc_ctx G;
+
+static int seterr(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(G.msg, sizeof G.msg, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+#define HIPCHK(call)                                                                              \
+    do {                                                                                          \
+        hipError_t e_ = (call);                                                                   \
+        if (e_ != hipSuccess) return seterr(DC_ERR_HIP, "%s: %s", #call, hipGetErrorString(e_)); \
+    } while (0)
+
+const char* dc_last_error(void) { return G.msg; }
+void* dc_get_stream(void) { return (void*)G.st; }
+void dc_set_abs_error_bound(double bound) { absErrBound = bound; absErrorBound_binary = -100; }
+double dc_get_abs_error_bound(void) { return absErrBound; }
+long long dc_decode_chunk_bits_value(void) { return dc_decode_chunk_bits(); }
+
+int dc_init(int device) {
+    if (G.inited) return DC_OK;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return seterr(DC_ERR_NOGPU, "no HIP device visible");
+    if (device < 0 || device >= n) return seterr(DC_ERR_ARG, "device %d out of range", device);
+    HIPCHK(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return seterr(DC_ERR_NOGPU, "device %d is %s, libdcamd is built for gfx950", device, prop.gcnArchName);
+    G.device = device;
+    HIPCHK(hipStreamCreateWithFlags(&G.st, hipStreamNonBlocking));
+    HIPCHK(hipHostMalloc((void**)&G.h_scratch, 64 * sizeof(unsigned long long), 0));
+    HIPCHK(hipMalloc((void**)&G.enc_ctr, 64));
+    HIPCHK(hipMemset(G.enc_ctr, 0, 64));
+    HIPCHK(hipMalloc((void**)&G.d_total, 64));
+    HIPCHK(hipMalloc((void**)&G.d_enc_err, 64));
+    HIPCHK(hipMemset(G.d_enc_err, 0, 64));
+    HIPCHK(hipMalloc((void**)&G.part_v, 256 * sizeof(float)));
+    HIPCHK(hipMalloc((void**)&G.part_i, 256 * sizeof(long long)));
+    HIPCHK(hipMalloc((void**)&G.d_f, 64));
+    HIPCHK(hipMalloc((void**)&G.d_i, 64));
+    HIPCHK(hipMalloc((void**)&G.d_crc, 64));
+    HIPCHK(hipMalloc((void**)&G.d_ham, 64));
+    /* CRC tables: byte table and x^(2^k) mod P (reflected), zlib's construction */
+    uint32_t tab[256], x2n[32];
+    for (uint32_t i = 0; i < 256; i++) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+        tab[i] = c;
+    }
+    uint32_t p = 1u << 30;                          /* x^1 */
+    x2n[0] = p;
+    for (int k = 1; k < 32; k++) {
+        uint32_t a = p, b = p, m = 1u << 31, r = 0;
+        for (int i = 0; i < 32; i++) {
+            if (a & m) r ^= b;
+            m >>= 1;
+            b = (b & 1u) ? (b >> 1) ^ 0xEDB88320u : b >> 1;
+        }
+        x2n[k] = p = r;
+    }
+    HIPCHK(hipMalloc((void**)&G.d_crctab, sizeof tab));
+    HIPCHK(hipMalloc((void**)&G.d_x2n, sizeof x2n));
+    HIPCHK(hipMemcpy(G.d_crctab, tab, sizeof tab, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(G.d_x2n, x2n, sizeof x2n, hipMemcpyHostToDevice));
+    G.enc_epoch = 1;
+    G.dec_epoch = 1;
+    G.inited = 1;
+    return DC_OK;
+}
+
+static int ensure_init(void) { return G.inited ? DC_OK : dc_init(0); }
+
+int dc_synchronize(void) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(G.st));
+    return DC_OK;
+}
+
+static int grow(void** p, size_t* cap, size_t need) {
+    if (*cap >= need) return DC_OK;
+    if (*p) HIPCHK(hipFree(*p));
+    *p = NULL;
+    size_t n = need + need / 8 + 4096;
+    HIPCHK(hipMalloc(p, n));
+    *cap = n;
+    return DC_OK;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* codec parameters (bound-derived thresholds computed exactly as the reference's double compares) */
+static int bound_binary(double bound) {                     /* to_absErrorBound_binary :5512 */
+    for (int n = 0; n < 100; n++)
+        if (bound >= pow(2, -n)) return n;
+    return 100;
+}
+
+static float thr_lt(double bound) {
+    float f = (float)bound;
+    while ((double)f >= bound) f = nextafterf(f, 0.0f);
+    while ((double)nextafterf(f, INFINITY) < bound) f = nextafterf(f, INFINITY);
+    return f;
+}
+
+static float thr_le(double bound) {
+    float f = (float)bound;
+    while ((double)f > bound) f = nextafterf(f, 0.0f);
+    while ((double)nextafterf(f, INFINITY) <= bound) f = nextafterf(f, INFINITY);
+    return f;
+}
+
+static void make_params(Params* P, int ct, int type, uint32_t mask17) {
+    P->ct = ct;
+    P->B = bound_binary(absErrBound);
+    P->thr_lt = thr_lt(absErrBound);
+    P->thr_le = thr_le(absErrBound);
+    P->type = type;
+    P->mask17 = mask17 & 0x1FFFFu;
+    int m = P->B + (int)((P->mask17 >> 8) & 0xFF) - 127;
+    P->mm = m > 23 ? 23 : (m < 0 ? 0 : m);
+    P->mm0 = P->mm > 8 ? P->mm - 8 : 0;
+}
+
+static int valid_ct(int ct) { return ct == 5 || ct == 6 || ct == 7 || ct == 11; }
+
+size_t dc_stream_capacity(long long n) { return (size_t)((n * 32 + 7 + 31) / 32) * 4 + 64; }
+
+/* ------------------------------------------------------------------------------------------ */
+int dc_encode_device(int ct, const void* d_x, long long n, long long idx0, int type, uint32_t mask17,
+                     int start_bit, void* d_out, unsigned long long* d_total_bits) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (!valid_ct(ct)) return seterr(DC_ERR_ARG, "unsupported CT %d", ct);
+    if (start_bit < 0 || start_bit > 7 || n < 0) return seterr(DC_ERR_ARG, "bad start_bit/n");
+    if (ct == 7 && (type < 1 || type > 7)) return seterr(DC_ERR_ARG, "CT7 type %d outside 1..7", type);
+    if (((uintptr_t)d_x & 15u) || ((uintptr_t)d_out & 3u)) return seterr(DC_ERR_ARG, "misaligned device buffer");
+    Params P;
+    make_params(&P, ct, type, mask17);
+    long long ntiles = dc_encode_tile_count(n);
+    if (ntiles > G.enc_desc_cap) {
+        if (G.enc_desc) HIPCHK(hipFree(G.enc_desc));
+        long long cap = ntiles + 1024;
+        HIPCHK(hipMalloc((void**)&G.enc_desc, cap * sizeof(uint64_t)));
+        HIPCHK(hipMemsetAsync(G.enc_desc, 0, cap * sizeof(uint64_t), G.st));
+        G.enc_desc_cap = cap;
+        G.enc_epoch = 1;
+    }
+    if (++G.enc_epoch >= (1u << 24)) {
+        HIPCHK(hipMemsetAsync(G.enc_desc, 0, G.enc_desc_cap * sizeof(uint64_t), G.st));
+        G.enc_epoch = 1;
+    }
+    unsigned long long* tot = d_total_bits ? d_total_bits : G.d_total;
+    if (n == 0) {
+        unsigned long long v = (unsigned long long)start_bit;
+        HIPCHK(hipMemcpyAsync(tot, &v, sizeof v, hipMemcpyHostToDevice, G.st));
+        if (tot != G.d_total) HIPCHK(hipMemcpyAsync(G.d_total, &v, sizeof v, hipMemcpyHostToDevice, G.st));
+        return DC_OK;
+    }
+    if (dc_launch_encode((const float*)d_x, n, idx0, &P, (uint32_t*)d_out, G.enc_desc, G.enc_ctr, G.enc_epoch,
+                         start_bit, tot, G.d_enc_err, G.st))
+        return seterr(DC_ERR_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (tot != G.d_total) HIPCHK(hipMemcpyAsync(G.d_total, tot, 8, hipMemcpyDeviceToDevice, G.st));
+    return DC_OK;
+}
+
+int dc_encode_result(unsigned long long* total_bits) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[0], G.d_total, 8, hipMemcpyDeviceToHost, G.st));
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[1], G.d_enc_err, 4, hipMemcpyDeviceToHost, G.st));
+    HIPCHK(hipStreamSynchronize(G.st));
+    unsigned err = (unsigned)(G.h_scratch[1] & 0xFFFFFFFFu);
+    if (err) {
+        HIPCHK(hipMemsetAsync(G.d_enc_err, 0, 4, G.st));
+        if (err & 1u)
+            return seterr(DC_ERR_INPUT, "input contains -1.0f, the reference encoder's empty-history sentinel "
+                                        "(impl/dataCompression.c:2032); CT5/7/11 inputs must be >= 0 (toSmallDataset_float)");
+        return seterr(DC_ERR_HIP, "encoder look-back timed out (err=%u)", err);
+    }
+    if (total_bits) *total_bits = G.h_scratch[0];
+    return DC_OK;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+static int dec_ensure(long long max_chunks) {
+    if (max_chunks <= G.dec_cap_chunks) return DC_OK;
+    if (G.dec_pool) HIPCHK(hipFree(G.dec_pool));
+    G.dec_pool = NULL;
+    long long C = max_chunks + 4096;
+    long long GR = (C + dc_decode_group() - 1) / dc_decode_group() + 1;
+    long long S = dc_decode_slots();
+    size_t off = 0, sz[13];
+    sz[0] = 256;                          /* plan */
+    sz[1] = (size_t)C;                    /* p_exit */
+    sz[2] = (size_t)C * 2;                /* p_cnt */
+    sz[3] = (size_t)C * 4;                /* p_mask */
+    sz[4] = (size_t)C * S * 8;            /* slots */
+    sz[5] = (size_t)GR * 32 * 4;          /* fullmap */
+    sz[6] = (size_t)GR * 32 * 8;          /* gran */
+    sz[7] = (size_t)C;                    /* entry */
+    sz[8] = (size_t)C * 8;                /* tokoff */
+    sz[9] = (size_t)C * 2;                /* pend */
+    sz[10] = (size_t)C * 2;               /* done */
+    sz[11] = 64;                          /* err */
+    sz[12] = 64;                          /* ctr */
+    size_t tot = 0;
+    for (int i = 0; i < 13; i++) tot += (sz[i] + 255) & ~(size_t)255;
+    HIPCHK(hipMalloc(&G.dec_pool, tot));
+    HIPCHK(hipMemsetAsync(G.dec_pool, 0, tot, G.st));
+    char* b = (char*)G.dec_pool;
+    void* ptr[13];
+    for (int i = 0; i < 13; i++) { ptr[i] = b + off; off += (sz[i] + 255) & ~(size_t)255; }
+    G.D.plan = (Plan*)ptr[0];
+    G.D.p_exit = (uint8_t*)ptr[1];
+    G.D.p_cnt = (uint16_t*)ptr[2];
+    G.D.p_mask = (uint32_t*)ptr[3];
+    G.D.slots = (uint64_t*)ptr[4];
+    G.D.fullmap = (uint32_t*)ptr[5];
+    G.D.gran = (uint64_t*)ptr[6];
+    G.D.entry = (uint8_t*)ptr[7];
+    G.D.tokoff = (unsigned long long*)ptr[8];
+    G.D.pend = (uint16_t*)ptr[9];
+    G.D.done = (uint16_t*)ptr[10];
+    G.D.err = (unsigned*)ptr[11];
+    G.D.ctr = (unsigned*)ptr[12];
+    G.dec_cap_chunks = C;
+    G.dec_epoch = 1;
+    return DC_OK;
+}
+
+#define DEC_ROUNDS 3
+#define DEC_FIX_ITERS 3
+
+int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsigned long long* d_nbits,
+                     long long max_bytes, long long num, int type, uint32_t mask17, void* d_out) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (!valid_ct(ct)) return seterr(DC_ERR_ARG, "unsupported CT %d", ct);
+    if (ct == 7 && (type < 1 || type > 7)) return seterr(DC_ERR_ARG, "CT7 type %d outside 1..7", type);
+    if ((uintptr_t)d_stream & 3u) return seterr(DC_ERR_ARG, "stream must be 4-byte aligned");
+    if (nbytes < 0 && !d_nbits) return seterr(DC_ERR_ARG, "need nbytes or d_nbits");
+    if (max_bytes < nbytes) max_bytes = nbytes;
+    long long cb = dc_decode_chunk_bits();
+    long long max_chunks = (max_bytes * 8 + cb - 1) / cb;
+    if (max_chunks < 1) max_chunks = 1;
+    rc = dec_ensure(max_chunks);
+    if (rc) return rc;
+    if (++G.dec_epoch >= (1u << 22)) {
+        long long GR = (G.dec_cap_chunks + dc_decode_group() - 1) / dc_decode_group() + 1;
+        HIPCHK(hipMemsetAsync(G.D.gran, 0, (size_t)GR * 32 * 8, G.st));
+        G.dec_epoch = 1;
+    }
+    Params P;
+    make_params(&P, ct, type, mask17);
+    if (dc_launch_decode((const uint8_t*)d_stream, nbytes >= 0 ? NULL : d_nbits,
+                         nbytes >= 0 ? (unsigned long long)nbytes * 8ull : 0ull, max_chunks, &P, &G.D,
+                         (float*)d_out, num, G.dec_epoch, DEC_ROUNDS, DEC_FIX_ITERS, G.st))
+        return seterr(DC_ERR_HIP, "decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+    G.dec_pending = 1;
+    G.dec_P = P;
+    G.dec_s = (const uint8_t*)d_stream;
+    G.dec_max_chunks = max_chunks;
+    G.dec_out = (float*)d_out;
+    G.dec_num = num;
+    return DC_OK;
+}
+
+static int read_dec_err(unsigned* err) {
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[2], G.D.err, 4, hipMemcpyDeviceToHost, G.st));
+    HIPCHK(hipStreamSynchronize(G.st));
+    *err = (unsigned)(G.h_scratch[2] & 0xFFFFFFFFu);
+    return DC_OK;
+}
+
+int dc_decode_finish(void) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    unsigned err = 0;
+    rc = read_dec_err(&err);
+    if (rc) return rc;
+    if (!err) { G.dec_pending = 0; return DC_OK; }
+    int round = 2 + DEC_ROUNDS;
+    while ((err & 8u) && !(err & (4u | 16u)) && G.dec_pending && round < 120) {
+        HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
+        if (++G.dec_epoch >= (1u << 22)) G.dec_epoch = 1;
+        if (dc_launch_decode_more(G.dec_s, G.dec_max_chunks, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.dec_epoch,
+                                  round, 4, DEC_FIX_ITERS, G.st))
+            return seterr(DC_ERR_HIP, "decode launch failed");
+        round += 4;
+        rc = read_dec_err(&err);
+        if (rc) return rc;
+    }
+    if ((err & 32u) && !(err & (4u | 8u | 16u)) && G.dec_pending) {
+        HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
+        if (dc_launch_fixup_serial(G.dec_s, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.st))
+            return seterr(DC_ERR_HIP, "decode launch failed");
+        rc = read_dec_err(&err);
+        if (rc) return rc;
+    }
+    G.dec_pending = 0;
+    HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
+    if (err) return seterr(DC_ERR_STREAM, "decoder status 0x%x (4: >%lld parse paths in a chunk, 8: unresolved "
+                                          "entry, 16: look-back timeout, 32: prediction chain)",
+                           err, dc_decode_slots());
+    return DC_OK;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+int dc_to_small_device(const void* d_x, long long n, void* d_out, float* min_out) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (n <= 0) return seterr(DC_ERR_ARG, "empty input");
+    if (dc_launch_to_small((const float*)d_x, n, (float*)d_out, G.part_v, G.part_i, &G.d_f[0], G.st))
+        return seterr(DC_ERR_HIP, "to_small launch failed");
+    if (min_out) {
+        float h;
+        HIPCHK(hipMemcpyAsync(&h, &G.d_f[0], 4, hipMemcpyDeviceToHost, G.st));
+        HIPCHK(hipStreamSynchronize(G.st));
+        *min_out = h;
+    }
+    return DC_OK;
+}
+
+int dc_med_device(const void* d_x, long long n, float* mean_out, int* type_out) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (n <= 0) return seterr(DC_ERR_ARG, "empty input");
+    if (dc_launch_med((const float*)d_x, n, &G.d_f[1], &G.d_i[0], G.st)) return seterr(DC_ERR_HIP, "med launch failed");
+    float m;
+    int t;
+    HIPCHK(hipMemcpyAsync(&m, &G.d_f[1], 4, hipMemcpyDeviceToHost, G.st));
+    HIPCHK(hipMemcpyAsync(&t, &G.d_i[0], 4, hipMemcpyDeviceToHost, G.st));
+    HIPCHK(hipStreamSynchronize(G.st));
+    if (mean_out) *mean_out = m;
+    if (type_out) *type_out = t;
+    return DC_OK;
+}
+
+int dc_crc32_device(const void* d_s, long long nbytes, uint32_t* crc_out) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    long long parts = dc_crc_parts(nbytes) + 1;
+    if (parts > G.crcparts_cap) {
+        if (G.d_crcparts) HIPCHK(hipFree(G.d_crcparts));
+        HIPCHK(hipMalloc((void**)&G.d_crcparts, parts * 4 + 1024));
+        G.crcparts_cap = parts;
+    }
+    if (dc_launch_crc32((const uint8_t*)d_s, nbytes, G.d_crctab, G.d_x2n, G.d_crcparts, 0u, G.d_crc, G.st))
+        return seterr(DC_ERR_HIP, "crc launch failed");
+    if (crc_out) {
+        uint32_t h;
+        HIPCHK(hipMemcpyAsync(&h, G.d_crc, 4, hipMemcpyDeviceToHost, G.st));
+        HIPCHK(hipStreamSynchronize(G.st));
+        *crc_out = h;
+    }
+    return DC_OK;
+}
+
+/* ============================================================================================
+ * Reference ABI (impl/dataCompression.h).  Host buffers in, host malloc'ed buffers out.
+ * ========================================================================================== */
+static uint32_t mask_from_chars(const char* mask) {
+    uint32_t m = 0;
+    for (int i = 0; i < 17; i++) m = (m << 1) | (uint32_t)(mask[i] == '1');
+    return m;
+}
+
+static void abi_fail(const char* fn, int rc) {
+    fprintf(stderr, "libdcamd: %s failed (%d): %s\n", fn, rc, G.msg);
+}
+
+/* add_bit_to_bytes-compatible append of a GPU-encoded stream (:5456-5489 semantics) */
+static int abi_compress(const char* fn, int ct, const float* data, int num, unsigned char** data_bits, int* bytes,
+                        int* pos, int type, uint32_t mask17) {
+    int rc = ensure_init();
+    if (rc) { abi_fail(fn, rc); return rc; }
+    if (num <= 0) return DC_OK;
+    const long long used = (long long)(*bytes) * 8 - (*pos == 8 ? 0 : *pos);
+    const int sb = (int)(used & 7);
+    const long long keep = used >> 3;
+    if ((rc = grow(&G.d_a, &G.d_a_cap, (size_t)num * 4 + 64)) || (rc = grow(&G.d_b, &G.d_b_cap, dc_stream_capacity(num)))) {
+        abi_fail(fn, rc); return rc;
+    }
+    if (hipMemcpyAsync(G.d_a, data, (size_t)num * 4, hipMemcpyHostToDevice, G.st) != hipSuccess) {
+        rc = seterr(DC_ERR_HIP, "H2D copy failed"); abi_fail(fn, rc); return rc;
+    }
+    unsigned long long tb = 0;
+    if ((rc = dc_encode_device(ct, G.d_a, num, 0, type, mask17, sb, G.d_b, NULL)) || (rc = dc_encode_result(&tb))) {
+        abi_fail(fn, rc); return rc;
+    }
+    const long long nb_new = (long long)((tb + 7) >> 3);
+    const long long total = keep + nb_new;
+    const unsigned char old = sb ? (unsigned char)((*data_bits)[keep] & (0xFFu << (8 - sb))) : 0;
+    unsigned char* nb = (unsigned char*)realloc(*data_bits, total > 0 ? (size_t)total : 1);
+    if (!nb) { rc = seterr(DC_ERR_ARG, "realloc of %lld bytes failed", total); abi_fail(fn, rc); return rc; }
+    *data_bits = nb;
+    if (hipMemcpy(nb + keep, G.d_b, (size_t)nb_new, hipMemcpyDeviceToHost) != hipSuccess) {
+        rc = seterr(DC_ERR_HIP, "D2H copy failed"); abi_fail(fn, rc); return rc;
+    }
+    if (sb) nb[keep] |= old;
+    const long long tot_bits = keep * 8 + (long long)tb;
+    *bytes = (int)total;
+    *pos = (tot_bits & 7) ? (int)(8 - (tot_bits & 7)) : 8;
+    return DC_OK;
+}
+
+static float* abi_decompress(const char* fn, int ct, const unsigned char* data_bits, int bytes, int num, int type,
+                             uint32_t mask17) {
+    float* out = (float*)malloc(sizeof(float) * (size_t)(num > 0 ? num : 1));
+    int rc = ensure_init();
+    if (rc) { abi_fail(fn, rc); return out; }
+    if (num <= 0 || bytes <= 0) return out;
+    if ((rc = grow(&G.d_a, &G.d_a_cap, (size_t)bytes + 64)) || (rc = grow(&G.d_b, &G.d_b_cap, (size_t)num * 4 + 64))) {
+        abi_fail(fn, rc); return out;
+    }
+    if (hipMemcpyAsync(G.d_a, data_bits, (size_t)bytes, hipMemcpyHostToDevice, G.st) != hipSuccess) {
+        abi_fail(fn, seterr(DC_ERR_HIP, "H2D copy failed")); return out;
+    }
+    if ((rc = dc_decode_device(ct, G.d_a, bytes, NULL, bytes, num, type, mask17, G.d_b)) || (rc = dc_decode_finish())) {
+        abi_fail(fn, rc);
+    }
+    if (hipMemcpy(out, G.d_b, (size_t)num * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        abi_fail(fn, seterr(DC_ERR_HIP, "D2H copy failed"));
+    return out;
+}
+
+/* myCompress_bitwise (:3310), _np (:2645), _op (:577), _mask (:2030) */
+void myCompress_bitwise(float data[], int num, unsigned char** data_bits, int* bytes, int* pos) {
+    abi_compress("myCompress_bitwise", 5, data, num, data_bits, bytes, pos, 0, 0);
+}
+void myCompress_bitwise_np(float data[], int num, unsigned char** data_bits, int* bytes, int* pos) {
+    abi_compress("myCompress_bitwise_np", 6, data, num, data_bits, bytes, pos, 0, 0);
+}
+void myCompress_bitwise_op(float data[], int num, unsigned char** data_bits, int* bytes, int* pos) {
+    abi_compress("myCompress_bitwise_op", 11, data, num, data_bits, bytes, pos, 0, 0);
+}
+void myCompress_bitwise_mask(float data[], int num, unsigned char** data_bits, int* bytes, int* pos, int type,
+                             char mask[1 + 8 + 8]) {
+    abi_compress("myCompress_bitwise_mask", 7, data, num, data_bits, bytes, pos, type, mask_from_chars(mask));
+}
+
+/* myDecompress_bitwise (:2922), _np (:2459), _op (:698), _mask (:1703) */
+float* myDecompress_bitwise(unsigned char* data_bits, int bytes, int num) {
+    return abi_decompress("myDecompress_bitwise", 5, data_bits, bytes, num, 0, 0);
+}
+float* myDecompress_bitwise_np(unsigned char* data_bits, int bytes, int num) {
+    return abi_decompress("myDecompress_bitwise_np", 6, data_bits, bytes, num, 0, 0);
+}
+float* myDecompress_bitwise_op(unsigned char* data_bits, int bytes, int num) {
+    return abi_decompress("myDecompress_bitwise_op", 11, data_bits, bytes, num, 0, 0);
+}
+float* myDecompress_bitwise_mask(unsigned char* data_bits, int bytes, int num, int type, char mask[1 + 8 + 8]) {
+    return abi_decompress("myDecompress_bitwise_mask", 7, data_bits, bytes, num, type, mask_from_chars(mask));
+}
+
+/* toSmallDataset_float (:3543-3562): *data_small = malloc'ed data - min, returns min */
+float toSmallDataset_float(float data[], float** data_small, int num) {
+    *data_small = (float*)malloc(sizeof(float) * (size_t)(num > 0 ? num : 1));
+    int rc = ensure_init();
+    if (rc || num <= 0) { if (rc) abi_fail("toSmallDataset_float", rc); return num > 0 ? data[0] : 0.0f; }
+    if ((rc = grow(&G.d_a, &G.d_a_cap, (size_t)num * 4 + 64)) || (rc = grow(&G.d_b, &G.d_b_cap, (size_t)num * 4 + 64))) {
+        abi_fail("toSmallDataset_float", rc); return data[0];
+    }
+    float mn = data[0];
+    if (hipMemcpyAsync(G.d_a, data, (size_t)num * 4, hipMemcpyHostToDevice, G.st) != hipSuccess ||
+        (rc = dc_to_small_device(G.d_a, num, G.d_b, &mn)) ||
+        hipMemcpy(*data_small, G.d_b, (size_t)num * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        abi_fail("toSmallDataset_float", rc ? rc : DC_ERR_HIP);
+    return mn;
+}
+
+/* med_dataset_float (:3593-3620) */
+float med_dataset_float(float* data, int num, int* type) {
+    int rc = ensure_init();
+    if (rc || num <= 0) { if (rc) abi_fail("med_dataset_float", rc); return 0.0f; }
+    if ((rc = grow(&G.d_a, &G.d_a_cap, (size_t)num * 4 + 64))) { abi_fail("med_dataset_float", rc); return 0.0f; }
+    float mean = 0.0f;
+    int t = *type;
+    if (hipMemcpyAsync(G.d_a, data, (size_t)num * 4, hipMemcpyHostToDevice, G.st) != hipSuccess ||
+        (rc = dc_med_device(G.d_a, num, &mean, &t))) {
+        abi_fail("med_dataset_float", rc ? rc : DC_ERR_HIP);
+        return 0.0f;
+    }
+    if (t) *type = t;                      /* the reference leaves *type untouched if no i matches */
+    return mean;
+}
+
+/* do_crc32 (:5524-5534) */
+uint32_t do_crc32(unsigned char* data_bits, int bytes) {
+    int rc = ensure_init();
+    if (rc) { abi_fail("do_crc32", rc); return 0; }
+    if (bytes <= 0) return 0;
+    uint32_t crc = 0;
+    if ((rc = grow(&G.d_a, &G.d_a_cap, (size_t)bytes + 64)) ||
+        hipMemcpyAsync(G.d_a, data_bits, (size_t)bytes, hipMemcpyHostToDevice, G.st) != hipSuccess ||
+        (rc = dc_crc32_device(G.d_a, bytes, &crc)))
+        abi_fail("do_crc32", rc ? rc : DC_ERR_HIP);
+    return crc;
+}
+
+/* ---- Hamming SECDED (:5544-5855) -------------------------------------------------------- */
+int hmLength(int k) {                                        /* :5581-5592 */
+    int r = 0;
+    while (((1LL << r) - 1) - r - (long long)k < 0) r++;
+    return r;
+}
+
+static int ham_syndrome(const unsigned char* bits, int bytes, unsigned long long* syn, unsigned long long* ones) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if ((rc = grow(&G.d_a, &G.d_a_cap, (size_t)bytes + 64))) return rc;
+    HIPCHK(hipMemcpyAsync(G.d_a, bits, (size_t)bytes, hipMemcpyHostToDevice, G.st));
+    if (dc_launch_ham_syndrome((const uint8_t*)G.d_a, bytes, G.d_ham, G.st)) return seterr(DC_ERR_HIP, "hamming launch");
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[4], G.d_ham, 16, hipMemcpyDeviceToHost, G.st));
+    HIPCHK(hipStreamSynchronize(G.st));
+    *syn = G.h_scratch[4];
+    *ones = G.h_scratch[5];
+    return DC_OK;
+}
+
+void hamming_encode(unsigned char* bits, char** c, int bytes, int* r) {   /* :5740-5748 */
+    *r = hmLength(bytes * 8);
+    *c = (char*)malloc((size_t)(*r + 1));
+    unsigned long long syn = 0, ones = 0;
+    int rc = ham_syndrome(bits, bytes, &syn, &ones);
+    if (rc) { abi_fail("hamming_encode", rc); memset(*c, '0', (size_t)(*r + 1)); return; }
+    unsigned long long sum = ones;
+    for (int i = 0; i < *r; i++) { (*c)[i] = (char)('0' + ((syn >> i) & 1)); sum += (syn >> i) & 1; }
+    (*c)[*r] = (char)('0' + (sum & 1));
+}
+
+int hamming_decode(unsigned char* bits, char* c, int bytes, int r) {       /* :5750-5778 */
+    unsigned long long syn = 0, ones = 0;
+    int rc = ham_syndrome(bits, bytes, &syn, &ones);
+    if (rc) { abi_fail("hamming_decode", rc); return 0; }
+    long long pos = 0;
+    unsigned long long sum = ones;
+    for (int i = 0; i < r; i++) {
+        const int ci = c[i] - '0';
+        pos += (long long)((int)((syn >> i) & 1) != ci) << i;     /* hamming_verify_bit :5803 */
+        sum += (unsigned long long)ci;
+    }
+    const int vr = (int)(sum & 1) != (c[r] - '0');
+    int type = 0;                                                 /* error_info :5631-5654 */
+    if (pos > 0 && !vr) type = 1;
+    else if (pos == 0 && vr) type = 2;
+    else if (pos > 0 && vr) type = 3;
+    if (type == 1) printf("two-bit error\n");
+    if (type == 2) { printf("parity error\n"); c[r] = c[r] == '0' ? '1' : '0'; }
+    if (type == 3) {                                              /* hamming_rectify_bit :5822 */
+        printf("one bit error: pos = %lld\n", pos);
+        const long long k = (long long)bytes * 8;
+        if (pos <= r + k) {
+            if ((pos & (pos - 1)) == 0) {
+                int ci = 0;
+                while ((1LL << ci) != pos) ci++;
+                c[ci] = c[ci] == '0' ? '1' : '0';
+            } else {
+                long long npow = 0;
+                while ((1LL << npow) < pos) npow++;
+                const long long d = pos - 1 - npow;
+                bits[d >> 3] ^= (unsigned char)(1u << (7 - (d & 7)));
+            }
+        }
+    }
+    return type;
+}
+
+/* ---- small helpers of the reference ABI ------------------------------------------------- */
+int to_absErrorBound_binary(double bound) { return bound_binary(bound); }   /* :5512-5522 */
+
+#ifndef BER
+#define BER 1e-6                                                 /* impl/dataCompression.h:4 */
+#endif
+int block_size(int data_bytes) {                                 /* :5868-5879 */
+    double ber = BER;
+    uint64_t b = (uint64_t)(1 / ber);
+    uint64_t by = b / 8;
+    int bs = data_bytes;
+    if ((uint64_t)bs > by) bs = (int)by;
+    return bs;
+}
+
+void bit_flip(unsigned char* bits, int bytes) {                  /* :5858-5865, libc rand() */
+    int num = rand() % (bytes * 8);
+    bits[num / 8] ^= (unsigned char)(1 << (7 - num % 8));
+}
+
+uint64_t get_random_int(uint64_t from, uint64_t to) { return (uint64_t)rand() % (to - from + 1) + from; }
+
+void floattostr(float* a, char* str) {                           /* :5244-5252 */
+    uint32_t c;
+    memcpy(&c, a, 4);
+    for (int i = 0; i < 32; i++) str[i] = (char)('0' + ((c >> (31 - i)) & 1));
+    str[32] = '\0';
+}
+
+float strtofloat(char* str) {                                    /* :5267-5276 */
+    uint32_t u = 0;
+    for (int i = 0; i < 32; i++) u = (u << 1) + (uint32_t)(str[i] - '0');
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+
+void doubletostr(double* a, char* str) {                         /* :5256-5264 */
+    uint64_t c;
+    memcpy(&c, a, 8);
+    for (int i = 0; i < 64; i++) str[i] = (char)('0' + ((c >> (63 - i)) & 1));
+    str[64] = '\0';
+}
+
+double strtodbl(char* str) {                                     /* :5279-5288 */
+    uint64_t u = 0;
+    for (int i = 0; i < 64; i++) u = (u << 1) + (uint64_t)(str[i] - '0');
+    double d;
+    memcpy(&d, &u, 8);
+    return d;
+}
+
+void getFloatBin(float num, char bin[]) {                        /* :5220-5230 (digits 0/1, not chars) */
+    uint32_t c;
+    memcpy(&c, &num, 4);
+    for (int i = 0; i < 32; i++) bin[i] = (char)((c >> (31 - i)) & 1);
+}
+
+void bit_set(unsigned char* p_data, unsigned char position, int flag) {   /* :5492-5510 */
+    if (!p_data || position > 8 || position < 1 || (flag != 0 && flag != 1)) return;
+    if (flag != ((*p_data >> (position - 1)) & 1)) *p_data ^= (unsigned char)(1 << (position - 1));
+}
+
+void add_bit_to_bytes(unsigned char** data_bits, int* bytes, int* pos, int flag) {   /* :5456-5489 */
+    if (*pos <= 0 || *pos >= 9) return;
+    if (*pos == 8) {
+        unsigned char* more = (unsigned char*)realloc(*data_bits, (size_t)(*bytes + 1));
+        if (!more) { fprintf(stderr, "libdcamd: add_bit_to_bytes: realloc failed\n"); return; }
+        *data_bits = more;
+        (*bytes)++;
+        (*data_bits)[*bytes - 1] = 0;
+    }
+    bit_set(&(*data_bits)[*bytes - 1], (unsigned char)*pos, flag);
+    (*pos)--;
+    if (*pos == 0) *pos = 8;
+}

@@ -1,0 +1,84 @@
+/* dc_shared.h -- plain-C structs and launcher prototypes shared by the C host layer (dc_host.c)
+ * and the HIP kernels (dc_encode.hip, dc_decode.hip).  No torch or HIP C++ types. */
+#ifndef DC_SHARED_H
+#define DC_SHARED_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+namespace dc {
+#endif
+
+typedef struct Params {  /* per-call codec parameters, computed on the host */
+    int ct;              /* 5, 6, 7, 11 */
+    int B;               /* to_absErrorBound_binary(bound), impl/dataCompression.c:5512 */
+    float thr_lt;        /* largest float f with (double)f <  bound  (zero test, :2044) */
+    float thr_le;        /* largest float f with (double)f <= bound  (predictor test, :2106) */
+    int type;            /* CT7 leading-ones count (med_dataset_float :3605-3614) */
+    uint32_t mask17;     /* CT7 mask: top 17 bits of the mean's pattern (pingpong.c:202-206) */
+    int mm;              /* m(mask exponent) */
+    int mm0;             /* max(mm - 8, 0) */
+} Params;
+
+typedef struct Plan {    /* device-resident sizes of the stream being decoded */
+    unsigned long long nbits;
+    long long nbytes;
+    long long nchunks;
+    long long ngroups;
+} Plan;
+
+typedef struct DecBufs { /* decoder metadata, sized for the maximum chunk count */
+    Plan* plan;
+    uint8_t* p_exit;
+    uint16_t* p_cnt;
+    uint32_t* p_mask;
+    uint64_t* slots;     /* [chunk][DC_SLOTS] */
+    uint32_t* fullmap;   /* [group][32]  exit<<26 | count */
+    uint64_t* gran;      /* [group][32]  look-back granules */
+    uint8_t* entry;
+    unsigned long long* tokoff;
+    uint16_t* pend;
+    uint16_t* done;
+    unsigned* err;       /* 4 slot overflow, 8 unknown entry, 16 spin timeout, 32 pending left */
+    unsigned* ctr;       /* [0] group ticket, [1] exit count */
+} DecBufs;
+
+#ifdef __cplusplus
+}  /* namespace dc */
+extern "C" {
+#define DC_NS dc::
+#else
+#define DC_NS
+#endif
+
+typedef struct ihipStream_t* dc_hip_stream;
+
+int dc_launch_encode(const float* x, long long n, long long idx0, const DC_NS Params* P, uint32_t* out,
+                     uint64_t* desc, unsigned* tile_ctr, uint32_t epoch, int start_bit,
+                     unsigned long long* total_bits, unsigned* err, dc_hip_stream stream);
+long long dc_encode_tile_count(long long n);
+
+int dc_launch_decode(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                     long long max_chunks, const DC_NS Params* P, const DC_NS DecBufs* D, float* out,
+                     long long num, uint32_t epoch, int rounds, int fix_iters, dc_hip_stream st);
+int dc_launch_decode_more(const uint8_t* s, long long max_chunks, const DC_NS Params* P,
+                          const DC_NS DecBufs* D, float* out, long long num, uint32_t epoch,
+                          int first_round, int rounds, int fix_iters, dc_hip_stream st);
+int dc_launch_fixup_serial(const uint8_t* s, const DC_NS Params* P, const DC_NS DecBufs* D, float* out,
+                           long long num, dc_hip_stream st);
+long long dc_decode_chunk_bits(void);
+long long dc_decode_group(void);
+long long dc_decode_slots(void);
+
+int dc_launch_to_small(const float* x, long long n, float* y, float* part_v, long long* part_i, float* d_min,
+                       dc_hip_stream st);
+int dc_launch_med(const float* x, long long n, float* d_mean, int* d_type, dc_hip_stream st);
+long long dc_crc_parts(long long nbytes);
+int dc_launch_crc32(const uint8_t* s, long long nbytes, const uint32_t* d_tab, const uint32_t* d_x2n,
+                    uint32_t* d_parts, uint32_t init, uint32_t* d_out, dc_hip_stream st);
+int dc_launch_ham_syndrome(const uint8_t* s, long long nbytes, unsigned long long* d_syn_ones, dc_hip_stream st);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,221 @@
+"""Python binding of libdcamd (ctypes) -- used by tests/, bench.py and __graft_entry__.
+
+The library is the product: the reference's C ABI (include/dataCompression.h) implemented on
+gfx950 kernels, plus the device-pointer API of include/dc_gpu.h.  This module only marshals
+numpy arrays / torch tensors into those C entry points; it computes nothing itself and raises if
+the shared object is missing.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "lib", "libdcamd.so")
+
+_f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+_u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+_libc = C.CDLL(None)
+_libc.free.argtypes = [C.c_void_p]
+_libc.malloc.argtypes = [C.c_size_t]
+_libc.malloc.restype = C.c_void_p
+
+# symbols include/dataCompression.h + include/dc_gpu.h promise (checked by tests/test_library.py)
+ABI_SYMBOLS = [
+    "myCompress_bitwise", "myCompress_bitwise_np", "myCompress_bitwise_op", "myCompress_bitwise_mask",
+    "myDecompress_bitwise", "myDecompress_bitwise_np", "myDecompress_bitwise_op", "myDecompress_bitwise_mask",
+    "toSmallDataset_float", "med_dataset_float", "do_crc32", "hmLength", "hamming_encode", "hamming_decode",
+    "bit_flip", "block_size", "get_random_int", "floattostr", "strtofloat", "doubletostr", "strtodbl",
+    "getFloatBin", "to_absErrorBound_binary", "add_bit_to_bytes", "bit_set",
+]
+EXT_SYMBOLS = [
+    "dc_init", "dc_last_error", "dc_get_stream", "dc_synchronize", "dc_set_abs_error_bound",
+    "dc_get_abs_error_bound", "dc_stream_capacity", "dc_encode_device", "dc_encode_result",
+    "dc_decode_device", "dc_decode_finish", "dc_to_small_device", "dc_med_device", "dc_crc32_device",
+    "dc_decode_chunk_bits_value",
+]
+
+
+def build():
+    import subprocess
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+class DCError(RuntimeError):
+    pass
+
+
+class Lib:
+    """Thin ctypes view of libdcamd.so."""
+
+    def __init__(self, path=LIB):
+        if not os.path.exists(path):
+            raise ImportError(f"libdcamd.so not built ({path}); run `make -C data-compression_amd`")
+        L = self.L = C.CDLL(path)
+        self.path = path
+        vp, ll, u32 = C.c_void_p, C.c_longlong, C.c_uint32
+        L.dc_init.argtypes = [C.c_int]
+        L.dc_last_error.restype = C.c_char_p
+        L.dc_get_stream.restype = vp
+        L.dc_set_abs_error_bound.argtypes = [C.c_double]
+        L.dc_get_abs_error_bound.restype = C.c_double
+        L.dc_stream_capacity.argtypes = [ll]
+        L.dc_stream_capacity.restype = C.c_size_t
+        L.dc_encode_device.argtypes = [C.c_int, vp, ll, ll, C.c_int, u32, C.c_int, vp, vp]
+        L.dc_encode_result.argtypes = [C.POINTER(C.c_ulonglong)]
+        L.dc_decode_device.argtypes = [C.c_int, vp, ll, vp, ll, ll, C.c_int, u32, vp]
+        L.dc_to_small_device.argtypes = [vp, ll, vp, C.POINTER(C.c_float)]
+        L.dc_med_device.argtypes = [vp, ll, C.POINTER(C.c_float), C.POINTER(C.c_int)]
+        L.dc_crc32_device.argtypes = [vp, ll, C.POINTER(C.c_uint32)]
+        L.dc_decode_chunk_bits_value.restype = ll
+        pp = [_f32p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        for nm in ("myCompress_bitwise", "myCompress_bitwise_np", "myCompress_bitwise_op"):
+            getattr(L, nm).argtypes = pp
+        L.myCompress_bitwise_mask.argtypes = pp + [C.c_int, C.c_char_p]
+        for nm in ("myDecompress_bitwise", "myDecompress_bitwise_np", "myDecompress_bitwise_op"):
+            getattr(L, nm).argtypes = [_u8p, C.c_int, C.c_int]
+            getattr(L, nm).restype = vp
+        L.myDecompress_bitwise_mask.argtypes = [_u8p, C.c_int, C.c_int, C.c_int, C.c_char_p]
+        L.myDecompress_bitwise_mask.restype = vp
+        L.toSmallDataset_float.argtypes = [_f32p, C.POINTER(C.c_void_p), C.c_int]
+        L.toSmallDataset_float.restype = C.c_float
+        L.med_dataset_float.argtypes = [_f32p, C.c_int, C.POINTER(C.c_int)]
+        L.med_dataset_float.restype = C.c_float
+        L.do_crc32.argtypes = [_u8p, C.c_int]
+        L.do_crc32.restype = C.c_uint32
+        L.hamming_encode.argtypes = [_u8p, C.POINTER(C.c_void_p), C.c_int, C.POINTER(C.c_int)]
+        L.hamming_decode.argtypes = [_u8p, C.c_char_p, C.c_int, C.c_int]
+        L.hmLength.argtypes = [C.c_int]
+        L.block_size.argtypes = [C.c_int]
+
+    # ---- state
+    def init(self, device=0):
+        rc = self.L.dc_init(device)
+        if rc:
+            raise DCError(f"dc_init: {rc} {self.err()}")
+
+    def err(self):
+        m = self.L.dc_last_error()
+        return m.decode() if m else ""
+
+    def check(self, rc, what):
+        if rc:
+            raise DCError(f"{what} -> {rc}: {self.err()}")
+
+    def set_bound(self, b):
+        self.L.dc_set_abs_error_bound(b)
+
+    # ---- reference ABI on host arrays
+    @staticmethod
+    def mask_chars(mask17):
+        return "".join("1" if (mask17 >> (16 - i)) & 1 else "0" for i in range(17)).encode()
+
+    def compress(self, ct, x, type_=0, mask17=0, prefix=None, prefix_pos=8):
+        x = np.ascontiguousarray(x, np.float32)
+        p = C.c_void_p(None)
+        nb = C.c_int(0)
+        pos = C.c_int(8)
+        if prefix is not None and len(prefix):
+            buf = _libc.malloc(len(prefix))
+            C.memmove(buf, bytes(prefix), len(prefix))
+            p = C.c_void_p(buf)
+            nb.value = len(prefix)
+            pos.value = prefix_pos
+        args = (x if x.size else np.zeros(1, np.float32), x.size, C.byref(p), C.byref(nb), C.byref(pos))
+        fn = {5: self.L.myCompress_bitwise, 6: self.L.myCompress_bitwise_np, 11: self.L.myCompress_bitwise_op}
+        if ct == 7:
+            self.L.myCompress_bitwise_mask(*args, type_, self.mask_chars(mask17))
+        else:
+            fn[ct](*args)
+        out = np.frombuffer(C.string_at(p.value, nb.value), np.uint8).copy() if nb.value else np.zeros(0, np.uint8)
+        if p.value:
+            _libc.free(p)
+        return out, nb.value, pos.value
+
+    def decompress(self, ct, s, num, type_=0, mask17=0):
+        s = np.ascontiguousarray(s, np.uint8)
+        sarg = s if s.size else np.zeros(1, np.uint8)
+        if ct == 7:
+            p = self.L.myDecompress_bitwise_mask(sarg, s.size, num, type_, self.mask_chars(mask17))
+        else:
+            fn = {5: self.L.myDecompress_bitwise, 6: self.L.myDecompress_bitwise_np, 11: self.L.myDecompress_bitwise_op}
+            p = fn[ct](sarg, s.size, num)
+        out = np.frombuffer(C.string_at(p, 4 * num), np.float32).copy() if num else np.zeros(0, np.float32)
+        _libc.free(p)
+        return out
+
+    def to_small(self, x):
+        x = np.ascontiguousarray(x, np.float32)
+        p = C.c_void_p(None)
+        mn = self.L.toSmallDataset_float(x, C.byref(p), x.size)
+        out = np.frombuffer(C.string_at(p.value, 4 * x.size), np.float32).copy()
+        _libc.free(p)
+        return np.float32(mn), out
+
+    def med(self, x):
+        x = np.ascontiguousarray(x, np.float32)
+        t = C.c_int(0)
+        mean = self.L.med_dataset_float(x, x.size, C.byref(t))
+        return np.float32(mean), t.value
+
+    def crc32(self, s):
+        s = np.ascontiguousarray(s, np.uint8)
+        return int(self.L.do_crc32(s if s.size else np.zeros(1, np.uint8), s.size))
+
+    def hamming_encode(self, s):
+        s = np.ascontiguousarray(s, np.uint8)
+        p = C.c_void_p(None)
+        r = C.c_int(0)
+        self.L.hamming_encode(s, C.byref(p), s.size, C.byref(r))
+        c = C.string_at(p.value, r.value + 1)
+        _libc.free(p)
+        return r.value, c
+
+    def hamming_decode(self, s, c, r):
+        s = np.array(s, np.uint8)
+        cb = C.create_string_buffer(bytes(c), len(c) + 1)
+        t = self.L.hamming_decode(s, cb, s.size, r)
+        return t, s, cb.raw[: r + 1]
+
+    # ---- device API on torch tensors (library stream; caller synchronizes torch first)
+    def stream_capacity(self, n):
+        return int(self.L.dc_stream_capacity(n))
+
+    def encode_device(self, ct, x_ptr, n, out_ptr, idx0=0, type_=0, mask17=0, start_bit=0, total_ptr=None):
+        self.check(self.L.dc_encode_device(ct, x_ptr, n, idx0, type_, mask17, start_bit, out_ptr, total_ptr),
+                   "dc_encode_device")
+
+    def encode_result(self):
+        v = C.c_ulonglong(0)
+        self.check(self.L.dc_encode_result(C.byref(v)), "dc_encode_result")
+        return v.value
+
+    def decode_device(self, ct, s_ptr, nbytes, num, out_ptr, type_=0, mask17=0, d_nbits=None, max_bytes=None):
+        self.check(self.L.dc_decode_device(ct, s_ptr, nbytes, d_nbits, max_bytes if max_bytes is not None else nbytes,
+                                           num, type_, mask17, out_ptr), "dc_decode_device")
+
+    def decode_finish(self):
+        self.check(self.L.dc_decode_finish(), "dc_decode_finish")
+
+    def synchronize(self):
+        self.check(self.L.dc_synchronize(), "dc_synchronize")
+
+    def med_device(self, x_ptr, n):
+        m, t = C.c_float(0), C.c_int(0)
+        self.check(self.L.dc_med_device(x_ptr, n, C.byref(m), C.byref(t)), "dc_med_device")
+        return np.float32(m.value), t.value
+
+    def crc32_device(self, s_ptr, nbytes):
+        v = C.c_uint32(0)
+        self.check(self.L.dc_crc32_device(s_ptr, nbytes, C.byref(v)), "dc_crc32_device")
+        return v.value
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = Lib()
+    return _lib

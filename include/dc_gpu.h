@@ -1,0 +1,72 @@
+/*
+ * dc_gpu.h -- device-pointer extension API of libdcamd (MI355X / gfx950).
+ *
+ * The reference ABI (dataCompression.h) takes host buffers; these entry points take device
+ * buffers that are already resident in HBM, so a caller (bench.py, a GPU-resident solver, the
+ * multi-GPU all-gather path) can run the codec without PCIe copies.  Plain C, no HIP/torch types:
+ * device pointers are void*, the HIP stream is the library's per-process stream (dc_get_stream).
+ *
+ * Every function returns 0 on success or a negative DC_ERR_* code; dc_last_error() explains.
+ */
+#ifndef DC_GPU_H
+#define DC_GPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    DC_OK = 0,
+    DC_ERR_HIP = -1,          /* HIP runtime error (message in dc_last_error) */
+    DC_ERR_ARG = -2,          /* bad argument */
+    DC_ERR_INPUT = -3,        /* input outside the codec's domain (e.g. -1.0f sentinel value) */
+    DC_ERR_STREAM = -4,       /* stream could not be decoded (corrupt / truncated / unsupported) */
+    DC_ERR_NOGPU = -5         /* no usable gfx950 device */
+};
+
+/* ---- library state ---------------------------------------------------------------------- */
+int dc_init(int device);                       /* optional; first call of any entry point inits dev 0 */
+const char* dc_last_error(void);
+void* dc_get_stream(void);                     /* hipStream_t all library work is ordered on */
+int dc_synchronize(void);
+void dc_set_abs_error_bound(double bound);     /* runtime absErrorBound (default: header macro) */
+double dc_get_abs_error_bound(void);
+
+/* ---- device-pointer codec (asynchronous on dc_get_stream()) ----------------------------- */
+/* Bytes an encode of n floats may write (stream bytes + word padding). */
+size_t dc_stream_capacity(long long n);
+
+/* Encode n floats at d_x (device).  idx0 = global index of d_x[0] within the logical array; when
+ * idx0 > 0 the three floats d_x[-3..-1] must be readable (predictor halo for a shard).
+ * start_bit (0..7): number of already-used high bits in the first output byte (append mode /
+ * shard stitching); those bits are written as zero.  d_out must hold dc_stream_capacity(n) bytes.
+ * *d_total_bits (device, may be NULL) receives start_bit + bits written. */
+int dc_encode_device(int ct, const void* d_x, long long n, long long idx0, int type, uint32_t mask17,
+                     int start_bit, void* d_out, unsigned long long* d_total_bits);
+/* Wait for the last encode and return start_bit + bits written (host value). */
+int dc_encode_result(unsigned long long* total_bits);
+
+/* Decode num floats from a device stream of nbytes bytes (nbytes < 0: take the length in bits
+ * from *d_nbits, device memory, e.g. the d_total_bits of a preceding dc_encode_device).
+ * max_bytes bounds the stream size (buffer capacity).  Asynchronous: call dc_decode_finish(). */
+int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsigned long long* d_nbits,
+                     long long max_bytes, long long num, int type, uint32_t mask17, void* d_out);
+/* Wait, check the decoder's status words and complete rare slow paths (extra closure rounds,
+ * serial prediction chains).  Returns DC_OK or DC_ERR_STREAM. */
+int dc_decode_finish(void);
+
+/* Pre-passes on device data: toSmallDataset_float and med_dataset_float (exact). */
+int dc_to_small_device(const void* d_x, long long n, void* d_out, float* min_out);
+int dc_med_device(const void* d_x, long long n, float* mean_out, int* type_out);
+/* zlib-compatible CRC-32 of a device byte range. */
+int dc_crc32_device(const void* d_s, long long nbytes, uint32_t* crc_out);
+
+/* Decoder/encoder geometry (for tests and bench). */
+long long dc_decode_chunk_bits_value(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

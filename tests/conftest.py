@@ -39,3 +39,12 @@ def gpu_available():
         return torch.cuda.is_available()
     except Exception:
         return False
+
+
+@pytest.fixture(scope="session")
+def dc():
+    """libdcamd on cuda:0 -- must load and initialise on the GPU box (no fallback)."""
+    import dcamd
+    L = dcamd.Lib()
+    L.init(0)
+    return L

@@ -1,0 +1,172 @@
+"""GPU parity: libdcamd (gfx950 kernels, called through the reference C ABI) vs the golden
+vectors of the compiled reference and the CPU oracle.  Integer/byte work -> bit-exact."""
+import numpy as np
+import pytest
+
+from conftest import BOUNDS, CASES, golden
+
+pytestmark = pytest.mark.gpu
+CTS = [5, 6, 7, 11]
+
+
+def _prep(g, case):
+    return int(g[f"{case}/type"]), int(g[f"{case}/mask17"])
+
+
+@pytest.mark.parametrize("bound", BOUNDS)
+@pytest.mark.parametrize("case", CASES)
+def test_prepasses_gpu(dc, bound, case):
+    g = golden(bound)
+    x = g[f"{case}/input"]
+    mn, xs = dc.to_small(x)
+    assert mn == g[f"{case}/min"]
+    mean, t = dc.med(xs)
+    assert mean == g[f"{case}/mean"] and t == g[f"{case}/type"]
+
+
+@pytest.mark.parametrize("bound", BOUNDS)
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("ct", CTS)
+def test_encoder_golden(dc, oracle, bound, case, ct):
+    g = golden(bound)
+    dc.set_bound(bound)
+    _, xs = oracle.to_small(g[f"{case}/input"])
+    t, m17 = _prep(g, case)
+    s, nb, pos = dc.compress(ct, xs, t, m17)
+    ref = g[f"{case}/ct{ct}/stream"]
+    assert nb == ref.size and pos == g[f"{case}/ct{ct}/pos"]
+    assert np.array_equal(s, ref)
+
+
+@pytest.mark.parametrize("bound", BOUNDS)
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("ct", CTS)
+def test_decoder_golden(dc, oracle, bound, case, ct):
+    g = golden(bound)
+    dc.set_bound(bound)
+    key = f"{case}/ct{ct}"
+    s = g[key + "/stream"]
+    n = g[f"{case}/input"].size
+    t, m17 = _prep(g, case)
+    out = dc.decompress(ct, s, n, t, m17)
+    spec, got = oracle.decompress(ct, s, n, bound, t, m17)
+    assert got == n
+    assert np.array_equal(out.view(np.uint32), spec.view(np.uint32))
+    if bool(g[key + "/ref_consistent"]):
+        assert np.array_equal(out.view(np.uint32), g[key + "/ref_decoded"].view(np.uint32))
+
+
+@pytest.mark.parametrize("bound", BOUNDS)
+def test_crc_hamming_gpu(dc, bound):
+    g = golden(bound)
+    for case in CASES:
+        for ct in CTS:
+            s = g[f"{case}/ct{ct}/stream"]
+            assert dc.crc32(s) == g[f"{case}/ct{ct}/crc"]
+    s = g["hamming/stream"]
+    bs = int(g["hamming/block_size"])
+    for i in range((s.size + bs - 1) // bs):
+        blk = s[i * bs: min(s.size, (i + 1) * bs)]
+        r, c = dc.hamming_encode(blk)
+        assert r == g[f"hamming/r{i}"] and c == g[f"hamming/c{i}"].tobytes()
+        bad = blk.copy()
+        bad[4321] ^= 0x04
+        t, fixed, _ = dc.hamming_decode(bad, c, r)
+        assert t == 3 and np.array_equal(fixed, blk)
+        bad[99] ^= 0x80
+        t, _, _ = dc.hamming_decode(bad, c, r)
+        assert t == 1
+
+
+@pytest.mark.parametrize("bound", BOUNDS)
+def test_append_mode_gpu(dc, bound):
+    g = golden(bound)
+    dc.set_bound(bound)
+    xs = g["append/input"]
+    for ct in (5, 6, 11):
+        s1, nb1, pos1 = dc.compress(ct, xs[:333])
+        assert nb1 == g[f"append/ct{ct}/first_bytes"] and pos1 == g[f"append/ct{ct}/first_pos"]
+        s2, nb2, pos2 = dc.compress(ct, xs[333:], prefix=s1, prefix_pos=pos1)
+        assert np.array_equal(s2, g[f"append/ct{ct}/stream"]) and pos2 == g[f"append/ct{ct}/pos"]
+
+
+def _inputs(oracle, kind, n):
+    if kind == "u10":
+        return oracle.gen_u10(n)
+    if kind == "eq":
+        return np.full(n, np.float32(0.123456789))
+    if kind == "unit":
+        return np.random.RandomState(n).rand(n).astype(np.float32)
+    if kind == "ramp":
+        return (np.float32(0.0005) * np.arange(n, dtype=np.float32)).astype(np.float32)
+    if kind == "himeno":
+        return np.tile(oracle.gen_himeno_plane(256, 256), max(1, n // 65536))[:n]
+    if kind == "mixed":
+        rs = np.random.RandomState(3)
+        x = oracle.gen_u10(n)
+        runs = rs.randint(0, n, 64)
+        for r in runs:                    # constant runs -> long copy chains across chunks
+            x[r:r + 3000] = x[r]
+        return x
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("bound", [1e-3, 1e-6])
+@pytest.mark.parametrize("kind,n", [("u10", 1 << 20), ("eq", 1 << 20), ("unit", 300001), ("ramp", 200000),
+                                    ("himeno", 1 << 18), ("mixed", 500000)])
+@pytest.mark.parametrize("ct", CTS)
+def test_roundtrip_vs_oracle(dc, oracle, bound, kind, n, ct):
+    dc.set_bound(bound)
+    x = _inputs(oracle, kind, n)
+    _, xs = oracle.to_small(x)
+    t, m17 = oracle.type_mask(xs)
+    s, nb, pos = dc.compress(ct, xs, t, m17)
+    so, nbo, poso = oracle.compress(ct, xs, bound, t, m17)
+    assert nb == nbo and pos == poso and np.array_equal(s, so)
+    out = dc.decompress(ct, s, n, t, m17)
+    spec, got = oracle.decompress(ct, s, n, bound, t, m17)
+    assert got == n
+    assert np.array_equal(out.view(np.uint32), spec.view(np.uint32))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 63, 64, 65, 4095, 4096, 4097, 8191, 12345, 65537])
+@pytest.mark.parametrize("ct", CTS)
+def test_ragged_sizes(dc, oracle, n, ct):
+    dc.set_bound(1e-3)
+    x = oracle.gen_u10(n, seed=n)
+    x[::7] = x[0]                         # some predictable / zero tokens
+    _, xs = oracle.to_small(x)
+    t, m17 = oracle.type_mask(xs)
+    s, nb, pos = dc.compress(ct, xs, t, m17)
+    so, nbo, poso = oracle.compress(ct, xs, 1e-3, t, m17)
+    assert nb == nbo and pos == poso and np.array_equal(s, so)
+    out = dc.decompress(ct, s, n, t, m17)
+    spec, _ = oracle.decompress(ct, s, n, 1e-3, t, m17)
+    assert np.array_equal(out.view(np.uint32), spec.view(np.uint32))
+
+
+def test_empty_input(dc):
+    s, nb, pos = dc.compress(5, np.zeros(0, np.float32))
+    assert nb == 0 and pos == 8
+
+
+def test_kat_testfloat_gpu(dc, oracle):
+    import os
+    from conftest import GOLDEN
+    x = np.loadtxt(os.path.join(GOLDEN, "kat_testfloat_8_8_128.txt"), dtype=np.float32)
+    kat = np.fromfile(os.path.join(GOLDEN, "kat_testfloat_8_8_128.txt.bc"), np.uint8)
+    dc.set_bound(1e-6)
+    mn, xs = dc.to_small(x)
+    s, nb, pos = dc.compress(5, xs)
+    assert np.array_equal(s, kat)
+    dec = dc.decompress(5, kat, x.size)
+    txt = open(os.path.join(GOLDEN, "kat_testfloat_8_8_128.txt.bc.txt")).read().split()
+    assert txt == ["%f" % v for v in (dec + mn).astype(np.float32)]
+
+
+def test_negative_one_rejected(dc):
+    dc.set_bound(1e-3)
+    x = np.array([0.5, 1.0, -1.0, 2.0], np.float32)
+    import ctypes
+    s, nb, pos = dc.compress(5, x)       # the ABI reports the error and leaves the stream untouched
+    assert nb == 0
