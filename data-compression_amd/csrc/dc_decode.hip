@@ -32,20 +32,9 @@ namespace dc {
 
 constexpr int CHUNK_BITS = 2048;
 constexpr int GROUP = 256;
-constexpr int SLOTS = 6;
 constexpr int UNK = 63;
 
 
-
-// slot word: [63] valid | [62:56] round | [55:50] entry | [49:44] exit | [31:0] count
-__device__ __forceinline__ uint64_t slot_pack(int round, int e, int x, uint32_t cnt) {
-    return (1ull << 63) | ((uint64_t)(round & 0x7F) << 56) | ((uint64_t)(e & 63) << 50) |
-           ((uint64_t)(x & 63) << 44) | (uint64_t)cnt;
-}
-__device__ __forceinline__ int slot_round(uint64_t s) { return (int)((s >> 56) & 0x7F); }
-__device__ __forceinline__ int slot_entry(uint64_t s) { return (int)((s >> 50) & 63); }
-__device__ __forceinline__ int slot_exit(uint64_t s) { return (int)((s >> 44) & 63); }
-__device__ __forceinline__ uint32_t slot_cnt(uint64_t s) { return (uint32_t)s; }
 
 __global__ void plan_kernel(Plan* plan, const unsigned long long* dev_nbits, unsigned long long host_nbits,
                             long long max_chunks) {
@@ -117,7 +106,8 @@ __global__ __launch_bounds__(256) void chunk_paths_kernel(const uint8_t* __restr
         D.p_exit[c] = (uint8_t)((x >= 0 && x < 32) ? x : 0);
         D.p_cnt[c] = (uint16_t)n;
         D.p_mask[c] = mask;
-        for (int k = 0; k < SLOTS; k++) D.slots[c * SLOTS + k] = 0ull;
+        D.known[c] = 0u;
+        D.exitmask[2 * c + 1] = 1u << D.p_exit[c];               // round 1 = P_c itself
     }
 }
 
@@ -133,46 +123,56 @@ __global__ __launch_bounds__(256) void group_maps_kernel(const uint8_t* __restri
         int x; uint32_t cnt;
         walk_entry<CT>(s, pl, P, c, e, D.p_mask[c], D.p_exit[c], D.p_cnt[c], &x, &cnt);
         D.fullmap[i] = ((uint32_t)x << 26) | (cnt & 0x3FFFFFFu);
+        atomicOr(&D.exitmask[2 * c + 1], 1u << x);                 // all exits known from round 1
     }
 }
 
-// 3. one closure round: entries required by the previous chunk's known paths
+// 3. one closure round: chunk c adds every exit of chunk c-1's known entries (as of round r-1)
+//    that is not yet a known entry of its own.  exitmask is double-buffered by round parity, so a
+//    lane never reads a mask its neighbour is writing in the same round.
 template <int CT>
 __global__ __launch_bounds__(256) void closure_kernel(const uint8_t* __restrict__ s, Params P, DecBufs D, int round) {
     const Plan pl = *D.plan;
+    const int rp = round & 1, pp = rp ^ 1;
     for (long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x; c < pl.nchunks;
          c += (long long)gridDim.x * blockDim.x) {
-        if (c == 0 || (c % GROUP) == 0) continue;                  // group-first chunks are complete
-        const long long pc = c - 1;
-        uint32_t need = 1u << D.p_exit[pc];                        // exits of the previous chunk
-        if ((pc % GROUP) == 0) {
-            const uint32_t* fm = D.fullmap + (pc / GROUP) * 32;
-            for (int e = 0; e < 32; e++) {
-                const uint32_t v = fm[e];
-                if ((v >> 26) != UNK) need |= 1u << (v >> 26);
+        uint32_t mine = D.exitmask[2 * c + pp];
+        if (c != 0 && (c % GROUP) != 0) {                          // group-first chunks are complete
+            const uint32_t pmask = D.p_mask[c];
+            uint32_t known = D.known[c];
+            uint32_t need = D.exitmask[2 * (c - 1) + pp] & ~pmask & ~known;
+            while (need) {
+                const int e = __ffs(need) - 1;
+                need &= need - 1;
+                int x; uint32_t cnt;
+                walk_entry<CT>(s, pl, P, c, e, pmask, D.p_exit[c], D.p_cnt[c], &x, &cnt);
+                D.map[c * 32 + e] = ((uint32_t)x << 26) | (cnt & 0x3FFFFFFu);
+                known |= 1u << e;
+                mine |= 1u << x;
             }
-        } else {
-            for (int k = 0; k < SLOTS; k++) {
-                const uint64_t sl = ld_relaxed(&D.slots[pc * SLOTS + k]);
-                if ((sl >> 63) && slot_round(sl) < round) need |= 1u << slot_exit(sl);
-            }
+            D.known[c] = known;
         }
+        D.exitmask[2 * c + rp] = mine;
+    }
+}
+
+// 3b. slow path: complete 32-entry maps for every chunk (one lane per unknown (chunk, entry)).
+//     Bounded work (<= 32 walks per chunk) for locally periodic streams where closure rounds would
+//     propagate only one chunk per round.
+template <int CT>
+__global__ __launch_bounds__(256) void full_maps_kernel(const uint8_t* __restrict__ s, Params P, DecBufs D) {
+    const Plan pl = *D.plan;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < pl.nchunks * 32;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long c = i >> 5;
+        const int e = (int)(i & 31);
+        if ((c % GROUP) == 0) continue;
         const uint32_t pmask = D.p_mask[c];
-        need &= ~pmask;
-        int nslot = 0;
-        for (int k = 0; k < SLOTS; k++) {
-            const uint64_t sl = D.slots[c * SLOTS + k];
-            if (sl >> 63) { need &= ~(1u << slot_entry(sl)); nslot++; }
-        }
-        while (need) {
-            const int e = __ffs(need) - 1;
-            need &= need - 1;
-            if (nslot >= SLOTS) { atomicOr(D.err, 4u); break; }
-            int x; uint32_t cnt;
-            walk_entry<CT>(s, pl, P, c, e, pmask, D.p_exit[c], D.p_cnt[c], &x, &cnt);
-            st_relaxed(&D.slots[c * SLOTS + nslot], slot_pack(round, e, x, cnt));
-            nslot++;
-        }
+        if (((pmask | D.known[c]) >> e) & 1u) continue;
+        int x; uint32_t cnt;
+        walk_entry<CT>(s, pl, P, c, e, pmask, D.p_exit[c], D.p_cnt[c], &x, &cnt);
+        D.map[c * 32 + e] = ((uint32_t)x << 26) | (cnt & 0x3FFFFFFu);
+        atomicOr(&D.known[c], 1u << e);
     }
 }
 
@@ -183,10 +183,7 @@ __device__ __forceinline__ uint32_t chunk_map_entry(const DecBufs& D, const Plan
     const uint32_t pm = D.p_mask[gc];
     if ((pm >> e) & 1u)
         return ((uint32_t)D.p_exit[gc] << 26) | (uint32_t)(D.p_cnt[gc] - __popc(pm & ((1u << e) - 1u)));
-    for (int k = 0; k < SLOTS; k++) {
-        const uint64_t sl = D.slots[gc * SLOTS + k];
-        if ((sl >> 63) && slot_entry(sl) == e) return ((uint32_t)slot_exit(sl) << 26) | (slot_cnt(sl) & 0x3FFFFFFu);
-    }
+    if ((D.known[gc] >> e) & 1u) return D.map[gc * 32 + e];
     return (uint32_t)UNK << 26;
 }
 
@@ -241,18 +238,29 @@ __global__ __launch_bounds__(256) void resolve_kernel(DecBufs D, uint32_t epoch)
                 unsigned long long hc = 0;
                 long long k = g - 1;
                 while (true) {
+                    // lane 0 polls the predecessor's first granule; A records are then complete
                     uint64_t dv = 0;
                     int flag = 0;
-                    unsigned spins = 0;
-                    if (lane < 32) {
+                    if (lane == 0) {
+                        unsigned spins = 0;
                         do {
-                            dv = ld_relaxed(&D.gran[k * 32 + lane]);
+                            dv = ld_relaxed(&D.gran[k * 32]);
                             flag = (((dv >> 40) & 0x3FFFFFu) == (epoch & 0x3FFFFFu)) ? (int)(dv >> 62) : 0;
                             if (flag == 0) __builtin_amdgcn_s_sleep(1);
-                        } while (flag == 0 && ++spins < (1u << 26));
+                        } while (flag == 0 && ++spins < (1u << 24));
                         if (flag == 0) atomicOr(D.err, 16u);
                     }
                     const int flag0 = __shfl(flag, 0, 64);
+                    if (flag0 == 1 && lane > 0 && lane < 32) {
+                        unsigned spins = 0;
+                        int f = 0;
+                        do {
+                            dv = ld_relaxed(&D.gran[k * 32 + lane]);
+                            f = (((dv >> 40) & 0x3FFFFFu) == (epoch & 0x3FFFFFu)) ? (int)(dv >> 62) : 0;
+                            if (f == 0) __builtin_amdgcn_s_sleep(1);
+                        } while (f == 0 && ++spins < (1u << 24));
+                        if (f == 0) atomicOr(D.err, 16u);
+                    }
                     const int dx = (int)((dv >> 34) & 63);
                     const unsigned long long dc = dv & ((1ull << 34) - 1);
                     if (flag0 == 2 || flag0 == 0) {
@@ -454,13 +462,13 @@ extern "C" int dc_launch_decode(const uint8_t* s, const unsigned long long* dev_
 }
 
 // extra closure rounds + re-resolve + decode (slow path after an unknown entry was reported)
+// slow path after an unresolved entry: complete maps for every chunk, re-resolve, re-decode
 extern "C" int dc_launch_decode_more(const uint8_t* s, long long max_chunks, const Params* P, const DecBufs* D,
-                                     float* out, long long num, uint32_t epoch, int first_round, int rounds,
-                                     int fix_iters, hipStream_t st) {
+                                     float* out, long long num, uint32_t epoch, int fix_iters, hipStream_t st) {
     const long long max_groups = (max_chunks + GROUP - 1) / GROUP;
     const int gchunks = (int)std::min<long long>((max_chunks + 255) / 256, g_grid);
-    for (int r = first_round; r < first_round + rounds; r++)
-        DC_DISPATCH(P->ct, closure_kernel, dim3(gchunks), dim3(256), 0, st, s, *P, *D, r);
+    const int gall = (int)std::min<long long>((max_chunks * 32 + 255) / 256, 8192);
+    DC_DISPATCH(P->ct, full_maps_kernel, dim3(gall), dim3(256), 0, st, s, *P, *D);
     const int gres = (int)std::min<long long>(max_groups, 512);
     hipLaunchKernelGGL(resolve_kernel, dim3(gres > 0 ? gres : 1), dim3(256), 0, st, *D, epoch);
     DC_DISPATCH(P->ct, decode_kernel, dim3(gchunks), dim3(256), 0, st, s, *P, *D, out, num);
@@ -478,6 +486,5 @@ extern "C" int dc_launch_fixup_serial(const uint8_t* s, const Params* P, const D
 
 extern "C" long long dc_decode_chunk_bits(void) { return CHUNK_BITS; }
 extern "C" long long dc_decode_group(void) { return GROUP; }
-extern "C" long long dc_decode_slots(void) { return SLOTS; }
 
 }  // namespace dc

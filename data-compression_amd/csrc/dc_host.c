@@ -257,13 +257,12 @@ static int dec_ensure(long long max_chunks) {
     G.dec_pool = NULL;
     long long C = max_chunks + 4096;
     long long GR = (C + dc_decode_group() - 1) / dc_decode_group() + 1;
-    long long S = dc_decode_slots();
-    size_t off = 0, sz[13];
+    size_t off = 0, sz[15];
     sz[0] = 256;                          /* plan */
     sz[1] = (size_t)C;                    /* p_exit */
     sz[2] = (size_t)C * 2;                /* p_cnt */
     sz[3] = (size_t)C * 4;                /* p_mask */
-    sz[4] = (size_t)C * S * 8;            /* slots */
+    sz[4] = (size_t)C * 32 * 4;           /* map */
     sz[5] = (size_t)GR * 32 * 4;          /* fullmap */
     sz[6] = (size_t)GR * 32 * 8;          /* gran */
     sz[7] = (size_t)C;                    /* entry */
@@ -272,18 +271,22 @@ static int dec_ensure(long long max_chunks) {
     sz[10] = (size_t)C * 2;               /* done */
     sz[11] = 64;                          /* err */
     sz[12] = 64;                          /* ctr */
+    sz[13] = (size_t)C * 4;               /* known */
+    sz[14] = (size_t)C * 8;               /* exitmask */
     size_t tot = 0;
-    for (int i = 0; i < 13; i++) tot += (sz[i] + 255) & ~(size_t)255;
+    for (int i = 0; i < 15; i++) tot += (sz[i] + 255) & ~(size_t)255;
     HIPCHK(hipMalloc(&G.dec_pool, tot));
     HIPCHK(hipMemsetAsync(G.dec_pool, 0, tot, G.st));
     char* b = (char*)G.dec_pool;
-    void* ptr[13];
-    for (int i = 0; i < 13; i++) { ptr[i] = b + off; off += (sz[i] + 255) & ~(size_t)255; }
+    void* ptr[15];
+    for (int i = 0; i < 15; i++) { ptr[i] = b + off; off += (sz[i] + 255) & ~(size_t)255; }
     G.D.plan = (Plan*)ptr[0];
     G.D.p_exit = (uint8_t*)ptr[1];
     G.D.p_cnt = (uint16_t*)ptr[2];
     G.D.p_mask = (uint32_t*)ptr[3];
-    G.D.slots = (uint64_t*)ptr[4];
+    G.D.map = (uint32_t*)ptr[4];
+    G.D.known = (uint32_t*)ptr[13];
+    G.D.exitmask = (uint32_t*)ptr[14];
     G.D.fullmap = (uint32_t*)ptr[5];
     G.D.gran = (uint64_t*)ptr[6];
     G.D.entry = (uint8_t*)ptr[7];
@@ -348,18 +351,16 @@ int dc_decode_finish(void) {
     rc = read_dec_err(&err);
     if (rc) return rc;
     if (!err) { G.dec_pending = 0; return DC_OK; }
-    int round = 2 + DEC_ROUNDS;
-    while ((err & 8u) && !(err & (4u | 16u)) && G.dec_pending && round < 120) {
+    if ((err & 8u) && !(err & 16u) && G.dec_pending) {
         HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
         if (++G.dec_epoch >= (1u << 22)) G.dec_epoch = 1;
         if (dc_launch_decode_more(G.dec_s, G.dec_max_chunks, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.dec_epoch,
-                                  round, 4, DEC_FIX_ITERS, G.st))
+                                  DEC_FIX_ITERS, G.st))
             return seterr(DC_ERR_HIP, "decode launch failed");
-        round += 4;
         rc = read_dec_err(&err);
         if (rc) return rc;
     }
-    if ((err & 32u) && !(err & (4u | 8u | 16u)) && G.dec_pending) {
+    if ((err & 32u) && !(err & (8u | 16u)) && G.dec_pending) {
         HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
         if (dc_launch_fixup_serial(G.dec_s, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.st))
             return seterr(DC_ERR_HIP, "decode launch failed");
@@ -368,9 +369,8 @@ int dc_decode_finish(void) {
     }
     G.dec_pending = 0;
     HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
-    if (err) return seterr(DC_ERR_STREAM, "decoder status 0x%x (4: >%lld parse paths in a chunk, 8: unresolved "
-                                          "entry, 16: look-back timeout, 32: prediction chain)",
-                           err, dc_decode_slots());
+    if (err) return seterr(DC_ERR_STREAM, "decoder status 0x%x (8: unresolved entry, 16: look-back timeout, "
+                                          "32: prediction chain)", err);
     return DC_OK;
 }
 

@@ -32,14 +32,16 @@ typedef struct DecBufs { /* decoder metadata, sized for the maximum chunk count 
     uint8_t* p_exit;
     uint16_t* p_cnt;
     uint32_t* p_mask;
-    uint64_t* slots;     /* [chunk][DC_SLOTS] */
+    uint32_t* map;       /* [chunk][32]  exit<<26 | count for entries in known[] */
+    uint32_t* known;     /* [chunk] entries with a valid map[] word (besides P's own positions) */
+    uint32_t* exitmask;  /* [chunk][2] exits of all known entries, by closure-round parity */
     uint32_t* fullmap;   /* [group][32]  exit<<26 | count */
     uint64_t* gran;      /* [group][32]  look-back granules */
     uint8_t* entry;
     unsigned long long* tokoff;
     uint16_t* pend;
     uint16_t* done;
-    unsigned* err;       /* 4 slot overflow, 8 unknown entry, 16 spin timeout, 32 pending left */
+    unsigned* err;       /* 8 unknown entry, 16 spin timeout, 32 pending left */
     unsigned* ctr;       /* [0] group ticket, [1] exit count */
 } DecBufs;
 
@@ -63,12 +65,11 @@ int dc_launch_decode(const uint8_t* s, const unsigned long long* dev_nbits, unsi
                      long long num, uint32_t epoch, int rounds, int fix_iters, dc_hip_stream st);
 int dc_launch_decode_more(const uint8_t* s, long long max_chunks, const DC_NS Params* P,
                           const DC_NS DecBufs* D, float* out, long long num, uint32_t epoch,
-                          int first_round, int rounds, int fix_iters, dc_hip_stream st);
+                          int fix_iters, dc_hip_stream st);
 int dc_launch_fixup_serial(const uint8_t* s, const DC_NS Params* P, const DC_NS DecBufs* D, float* out,
                            long long num, dc_hip_stream st);
 long long dc_decode_chunk_bits(void);
 long long dc_decode_group(void);
-long long dc_decode_slots(void);
 
 int dc_launch_to_small(const float* x, long long n, float* y, float* part_v, long long* part_i, float* d_min,
                        dc_hip_stream st);
