@@ -1,0 +1,242 @@
+"""Benchmark: CT7 (bitmask bit-wise) compress+decompress of U10 float32 at absErrorBound=1e-3.
+
+Metric (BASELINE.json): GB/s of input float bytes, 4N / (t_compress + t_decompress), whole job
+over all ranks (weak scaling: every rank owns a contiguous 2^26-float block of one global U10
+array and runs the hot path on it; inputs are resident in HBM before the timed region).
+
+A step = dc_encode_device (1 kernel) + dc_decode_device (parse / closure / resolve / decode /
+fixup kernels) of the rank's block, all on the library's HIP stream, inputs and outputs in HBM.
+Prints ONE JSON line on rank 0 with a roofline object for the dominant kernel (HIP-event timed
+on the library stream) and a cpu_baseline leg (the reference's own impl/dataCompression.c compiled
+by oracle/build_ref.sh when present, else the C restatement), timed on the host on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "data-compression_amd"))
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--log2n", type=int, default=26, help="floats per GPU (2^log2n)")
+    ap.add_argument("--ct", type=int, default=7)
+    ap.add_argument("--bound", type=float, default=1e-3)
+    ap.add_argument("--input", default="u10", choices=["u10", "eq"])
+    ap.add_argument("--cpu-log2n", type=int, default=22, help="cpu_baseline sample size (2^k floats)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--check", action="store_true", help="verify the round trip against the oracle")
+    return ap.parse_args()
+
+
+def gen_input(kind, n, offset):
+    import dcamd
+    if kind == "u10":
+        return dcamd.gen_u10(n, 42, offset)
+    return np.full(n, np.float32(0.123456789), np.float32)
+
+
+def cpu_baseline(ct, bound, n, kind):
+    """Time the reference CPU codec on a bounded sample (1 host core, single-threaded)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    x = gen_input(kind, n, 0)
+    O = pyoracle.Oracle()
+    mn, xs = O.to_small(x)
+    mean, t = O.med(xs)
+    m17 = O.mask17(mean)
+    try:
+        R = pyoracle.RefLib(bound)
+        t0 = time.perf_counter()
+        s, nb, pos = R.compress(ct, xs, t, m17)
+        t1 = time.perf_counter()
+        R.decompress(ct, s, n, t, m17)
+        t2 = time.perf_counter()
+        kind_s = "reference"
+    except (FileNotFoundError, OSError):
+        t0 = time.perf_counter()
+        s, nb, pos = O.compress(ct, xs, bound, t, m17)
+        t1 = time.perf_counter()
+        O.decompress(ct, s, n, bound, t, m17)
+        t2 = time.perf_counter()
+        kind_s = "port"
+    gbs = 4.0 * n / (t2 - t0) / 1e9
+    return {"value": round(gbs, 6), "unit": "GB/s", "cores": 1, "kind": kind_s,
+            "sample": f"{kind.upper()} 2^{int(np.log2(n))} floats CT{ct} @{bound:g}: compress {t1 - t0:.3f} s + "
+                      f"decompress {t2 - t1:.3f} s, single-threaded impl/dataCompression.c"
+                      + (" (compiled reference)" if kind_s == "reference" else " restatement (oracle)")}
+
+
+def main():
+    args = parse()
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import dcamd
+    L = dcamd.Lib()
+    L.init(local)
+    L.set_bound(args.bound)
+    n = 1 << args.log2n
+    ct = args.ct
+
+    # ---- inputs: rank's contiguous block of one global U10 array (+3-float predictor halo)
+    xh = gen_input(args.input, n + 3, rank * n - 3) if rank > 0 else np.concatenate(
+        [np.zeros(3, np.float32), gen_input(args.input, n, 0)])
+    x_all = torch.from_numpy(xh).to(dev)
+    x_raw = x_all[3:]
+    xs_all = torch.empty(n + 4, dtype=torch.float32, device=dev)
+    xs = xs_all[4:]                                  # 16-byte aligned shard start
+    cap = L.stream_capacity(n)
+    stream = torch.empty(cap, dtype=torch.uint8, device=dev)
+    out = torch.empty(n, dtype=torch.float32, device=dev)
+    d_nbits = torch.zeros(1, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+
+    # ---- pre-passes outside the timed region (ABI inputs of the CT7 codec)
+    mn = np.float32(0)
+    import ctypes
+    mnc = ctypes.c_float(0)
+    L.check(L.L.dc_to_small_device(ctypes.c_void_p(x_raw.data_ptr()), n, ctypes.c_void_p(xs.data_ptr()),
+                                   ctypes.byref(mnc)), "to_small")
+    L.synchronize()
+    if dist is not None:      # toSmallDataset over the global array: global min, then x - min
+        gm = torch.tensor([mnc.value], dtype=torch.float32, device=dev)
+        dist.all_reduce(gm, op=dist.ReduceOp.MIN)
+        torch.sub(x_all, gm[0], out=xs_all[1:])
+        torch.cuda.synchronize()
+    t_med0 = time.perf_counter()
+    mean, typ = L.med_device(xs.data_ptr(), n)
+    t_med = time.perf_counter() - t_med0
+    mask17 = int(np.array([mean], np.float32).view(np.uint32)[0] >> 15)
+    if dist is not None:
+        tm = torch.tensor([typ, mask17], dtype=torch.int64, device=dev)
+        dist.broadcast(tm, 0)
+        typ, mask17 = int(tm[0]), int(tm[1])
+
+    ext = torch.cuda.ExternalStream(L.L.dc_get_stream())
+    idx0 = rank * n
+
+    def step(ev=None):
+        if ev:
+            ev[0].record(ext)
+        L.encode_device(ct, xs.data_ptr(), n, stream.data_ptr(), idx0=idx0, type_=typ, mask17=mask17,
+                        total_ptr=d_nbits.data_ptr())
+        if ev:
+            ev[1].record(ext)
+        L.decode_device(ct, stream.data_ptr(), -1, n, out.data_ptr(), type_=typ, mask17=mask17,
+                        d_nbits=d_nbits.data_ptr(), max_bytes=cap)
+        if ev:
+            ev[2].record(ext)
+
+    for _ in range(args.warmup):
+        step()
+    L.decode_finish()
+    nbits = L.encode_result()
+    nbytes = (nbits + 7) // 8
+
+    # ---- timed region: barrier + sync on both sides, max over ranks
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    L.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    L.synchronize()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if dist is not None:
+        dist.barrier()
+    L.decode_finish()                                 # status words: fail loudly on any slow path
+    wall = t1 - t0
+    if dist is not None:
+        w = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        wall = float(w[0])
+    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+
+    ok = None
+    if args.check and rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from pyoracle import Oracle
+        O = Oracle()
+        s_h = stream[:nbytes].cpu().numpy()
+        ref, _ = O.decompress(ct, s_h, n, args.bound, typ, mask17)
+        ok = bool(np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32)))
+
+    ms_per_step = wall / args.steps * 1e3
+    value = world * 4.0 * n / (wall / args.steps) / 1e9
+    # dominant kernel: the one-launch encoder vs the decoder chain (event-timed on the library stream)
+    enc_bytes = 4.0 * n + nbytes
+    dec_bytes = nbytes + 4.0 * n
+    if enc_ms >= dec_ms:
+        dom = {"kernel": "encode_kernel<7>", "ms": enc_ms, "bytes": enc_bytes}
+    else:
+        dom = {"kernel": "decode chain (7 kernels)", "ms": dec_ms, "bytes": dec_bytes}
+    achieved = dom["bytes"] / (dom["ms"] * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if os.path.exists(pmc):
+        try:
+            pj = json.load(open(pmc))
+            if pj.get("n") == n and pj.get("ct") == ct:
+                traffic = pj.get("traffic_bytes_per_launch", {}).get(dom["kernel"])
+        except Exception:
+            traffic = None
+    res = {
+        "metric": "GB/s (input float bytes) compress+decompress, CT=7 absErrorBound=1e-3, 1/2/4/8 GPUs",
+        "value": round(value, 3),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": f"synthetic {args.input.upper()} (counter-based splitmix64 uniform [0,10), seed 42), generated per rank",
+        "config": {"workload": f"CT{ct} bitmask bit-wise compress+decompress, {args.input.upper()} 2^{args.log2n} float32 per GPU, "
+                               f"absErrorBound={args.bound:g}", "floats_per_gpu": n, "ct": ct,
+                   "stream_bytes": int(nbytes), "ratio": round(4.0 * n / nbytes, 4), "type": typ,
+                   "mask17": f"{mask17:05x}", "parallelism": f"dp{world}"},
+        "roofline": {"bound": "hbm", "kernel": dom["kernel"], "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic,
+                     "algorithmic_bytes_per_launch": int(dom["bytes"]), "avg_launch_ms": round(dom["ms"], 4)},
+        "phases_ms": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4), "med_dataset_serial_s": round(t_med, 4)},
+        "pipeline_roofline_frac": round((8.0 * n + 2 * nbytes) / ((enc_ms + dec_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+    }
+    if ok is not None:
+        res["check_vs_oracle"] = ok
+    if rank == 0 and not args.no_cpu:
+        res["cpu_baseline"] = cpu_baseline(ct, args.bound, 1 << args.cpu_log2n, args.input)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

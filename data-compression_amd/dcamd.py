@@ -211,6 +211,19 @@ class Lib:
         return v.value
 
 
+def gen_u10(n, seed=42, offset=0):
+    """Synthetic U10 input: counter-based splitmix64 -> uniform [0,10) float32."""
+    i = np.arange(offset, offset + n, dtype=np.uint64) + np.uint64(1)
+    with np.errstate(over="ignore"):
+        z = np.uint64(0x9E3779B97F4A7C15) * i + np.uint64(seed)
+        z ^= z >> np.uint64(30)
+        z *= np.uint64(0xBF58476D1CE4E5B9)
+        z ^= z >> np.uint64(27)
+        z *= np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    return ((z >> np.uint64(40)).astype(np.float32) * np.float32(2.0 ** -24)) * np.float32(10.0)
+
+
 _lib = None
 
 
