@@ -30,8 +30,6 @@
 
 namespace dc {
 
-constexpr int CHUNK_BITS = 2048;
-constexpr int GROUP = 256;
 constexpr int UNK = 63;
 
 

@@ -1,0 +1,712 @@
+// dc_decode_fast.hip -- LDS-staged three-kernel decoder: the fast path of the bit-wise decoders of
+// impl/dataCompression.c (myDecompress_bitwise :2922, _np :2459, _mask :1703, _op :698).
+//
+// A tile = GROUP chunks of CHUNK_BITS = one workgroup, one lane per chunk.  Each kernel reads the
+// tile's stream bytes from HBM once, with coalesced 16-byte loads, into LDS rows padded to 33 words
+// (lanes reading the same offset of their own chunks hit different banks; word w sits at w + w/32).
+// All parsing runs out of LDS through a branch-free 3-word window reader with a prefetched word.
+//
+// parse_kernel : speculative path P_c per chunk; the tile's first chunk gets its complete 32-entry
+//                map; every other chunk walks the exits of its predecessor's known entries until they
+//                merge with P_c (closure rounds inside the workgroup).  The true path through a tile is
+//                a "standard" chain (entry of chunk c = exit of P_{c-1}) with rare deviations, which
+//                one lane resolves by hopping over the failure points.  Per tile it stores the chunk
+//                records and the tile map (32 entries -> exit, token count).  Tiles never wait on
+//                each other.
+// tile_scan    : one workgroup chains the tiles: in practice every tile map has a constant exit (all
+//                32 entries merge long before the tile ends), so tile t's entry is tile t-1's exit and
+//                a block scan of the counts gives every tile's first token index.
+// decode_kernel: re-resolves the chunk entries of its tile from the tile entry, decodes every chunk
+//                from its true entry (history = DECODED values, tracked symbolically where it depends
+//                on the previous chunk), scans the chunk carry functions in LDS, chains tiles through a
+//                history look-back when a pending prefix needs it, and re-decodes pending prefixes.
+// Anything outside these assumptions (closure overflow, an unresolved entry, arithmetic prediction
+// chains across chunks) is reported in D.err and finished by the exact multi-kernel path.
+#include "dc_device.h"
+#include <algorithm>
+
+namespace dc {
+
+constexpr int LROW = 33;                       // padded LDS row (words) per chunk
+constexpr int LWORDS = (GROUP + 1) * LROW;     // + one row for the words after the tile
+constexpr int KMAX = 6;                        // extra known entries per chunk (besides P_c's own)
+constexpr int RMAX = 12;                       // closure rounds inside a tile
+constexpr int CW = CHUNK_BITS / 32;            // words per chunk
+constexpr int UNKE = 63;
+
+#define STAMP(ph) do { if (D.dbg && threadIdx.x == 0 && t < 4096) D.dbg[t * 16 + (ph)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+
+__device__ __forceinline__ uint32_t ldw(const uint32_t* L, int w) { return L[w + (w >> 5)]; }
+
+// branch-free MSB-first reader: w0:w1 hold the next 64 bits from bit sh of w0, w2 the next word,
+// pf the word after it (loaded one step ahead so its LDS latency is off the critical path)
+struct Rd {
+    uint32_t w0, w1, w2, pf;
+    int sh, wi, pos;
+    __device__ __forceinline__ void init(const uint32_t* L, int p) {
+        wi = p >> 5;
+        w0 = ldw(L, wi); w1 = ldw(L, wi + 1); w2 = ldw(L, wi + 2); pf = ldw(L, wi + 3);
+        sh = p & 31;
+        pos = p;
+    }
+    __device__ __forceinline__ uint32_t peek() const {
+        return (uint32_t)(((((uint64_t)w0) << 32) | (uint64_t)w1) << sh >> 32);
+    }
+    __device__ __forceinline__ void step(const uint32_t* L, int len) {
+        sh += len;
+        pos += len;
+        const bool adv = sh >= 32;
+        w0 = adv ? w1 : w0;
+        w1 = adv ? w2 : w1;
+        w2 = adv ? pf : w2;
+        wi += adv ? 1 : 0;
+        sh -= adv ? 32 : 0;
+        pf = ldw(L, wi + 3);
+    }
+};
+
+// stage the tile's stream words [tw, tw + GROUP*CW + 4) into padded LDS rows (zeros past the end)
+__device__ __forceinline__ void stage_tile(uint32_t* L, const uint8_t* s, long long nbytes, long long tw) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(s);
+    const long long nwfull = nbytes >> 2;
+    constexpr int NW = GROUP * CW;
+    if (tw + NW + 4 <= nwfull && ((reinterpret_cast<uintptr_t>(s) & 15u) == 0) && (tw & 3) == 0) {
+        const uint4* w4 = reinterpret_cast<const uint4*>(w + tw);
+        uint4 r[NW / 4 / GROUP];
+#pragma unroll
+        for (int q = 0; q < NW / 4 / GROUP; q++) r[q] = w4[threadIdx.x + q * GROUP];
+        uint32_t tail = 0;
+        if (threadIdx.x < 4) tail = w[tw + NW + threadIdx.x];
+#pragma unroll
+        for (int q = 0; q < NW / 4 / GROUP; q++) {
+            const int i = 4 * (threadIdx.x + q * GROUP);
+            uint32_t* d = L + i + (i >> 5);
+            d[0] = __builtin_bswap32(r[q].x);
+            d[1] = __builtin_bswap32(r[q].y);
+            d[2] = __builtin_bswap32(r[q].z);
+            d[3] = __builtin_bswap32(r[q].w);
+        }
+        if (threadIdx.x < 4) L[NW + GROUP + threadIdx.x] = __builtin_bswap32(tail);
+        return;
+    }
+    for (int i = threadIdx.x; i < NW + 4; i += blockDim.x) {
+        const long long gw = tw + i;
+        uint32_t v = 0;
+        if (gw < nwfull) {
+            v = __builtin_bswap32(w[gw]);
+        } else if (4 * gw < nbytes) {
+            for (int k = 0; k < 4; k++) {
+                const long long bi = 4 * gw + k;
+                v = (v << 8) | (bi < nbytes ? (uint32_t)s[bi] : 0u);
+            }
+        }
+        L[i + (i >> 5)] = v;
+    }
+}
+
+// walk entry e of chunk c (tile-relative bits [cs, cend)) alongside P_c; the reader that is behind
+// steps.  Returns the exit relative to the next chunk and the number of tokens starting in the chunk.
+template <int CT>
+__device__ __forceinline__ void walk_lds(const uint32_t* L, const Params& P, int cs, int cend, int e,
+                                         uint32_t pmask, int pexit, int pcnt, int* out_exit, int* out_cnt) {
+    if ((pmask >> e) & 1u) {
+        *out_exit = pexit;
+        *out_cnt = pcnt - __popc(pmask & ((1u << e) - 1u));
+        return;
+    }
+    Rd A, B;
+    A.init(L, cs + e);
+    B.init(L, cs);
+    int ca = 0, cb = 0;
+    bool merged = false;
+    while (A.pos < cend) {
+        if (A.pos == B.pos) { merged = true; break; }
+        const bool sa = A.pos < B.pos || B.pos >= cend;
+        const uint32_t tk = sa ? A.peek() : B.peek();
+        const int len = token_len_bf<CT>(tk, P);
+        if (sa) { A.step(L, len); ca++; } else { B.step(L, len); cb++; }
+    }
+    if (merged) { *out_exit = pexit; *out_cnt = ca + pcnt - cb; return; }
+    const int x = A.pos - (cs + CHUNK_BITS);
+    *out_exit = (x >= 0 && x < 32) ? x : 0;
+    *out_cnt = ca;
+}
+
+// ------------------------------------------------------------------------------------------------
+struct ParseShared {
+    uint32_t L[LWORDS];
+    uint32_t ke[GROUP * KMAX];                 // entry<<16 | exit<<10 | cnt
+    uint32_t em[2][GROUP];                     // exits of all known entries, by round parity
+    uint32_t pm[GROUP];
+    uint32_t pre[GROUP + 1];                   // exclusive prefix of the standard counts
+    uint32_t fm[32];                           // complete map of chunk 0: exit<<10 | cnt
+    uint64_t bad[GROUP / 64];
+    uint16_t n[GROUP], stdcnt[GROUP];
+    uint8_t x[GROUP], nk[GROUP], stdexit[GROUP];
+    uint32_t wsum[GROUP / 64];
+};
+
+__device__ __forceinline__ int next_bad(const uint64_t* bad, int c, int nact) {
+    for (int w = c >> 6; w < GROUP / 64; w++) {
+        uint64_t m = bad[w];
+        if (w == (c >> 6)) m &= ~0ull << (c & 63);
+        if (m) { const int f = w * 64 + __ffsll((long long)m) - 1; return f < nact ? f : nact; }
+    }
+    return nact;
+}
+
+// map of chunk c at entry e from the LDS state of the parse kernel
+__device__ __forceinline__ bool lookup_entry(const ParseShared& S, int c, int e, int* ex, int* cn) {
+    const uint32_t pm = S.pm[c];
+    if ((pm >> e) & 1u) { *ex = S.x[c]; *cn = S.n[c] - __popc(pm & ((1u << e) - 1u)); return true; }
+    for (int k = 0; k < S.nk[c]; k++) {
+        const uint32_t v = S.ke[c * KMAX + k];
+        if ((int)(v >> 16) == e) { *ex = (int)((v >> 10) & 63); *cn = (int)(v & 1023); return true; }
+    }
+    return false;
+}
+
+template <int CT>
+__global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict__ s, Params P, DecBufs D) {
+    __shared__ ParseShared S;
+    const Plan pl = *D.plan;
+    const int c = threadIdx.x, lane = c & 63, wid = c >> 6;
+    for (long long t = blockIdx.x; t < pl.ngroups; t += gridDim.x) {
+        const long long tbit = t * (long long)GROUP * CHUNK_BITS;
+        STAMP(0);
+        stage_tile(S.L, s, pl.nbytes, tbit >> 5);
+        const long long gc = t * GROUP + c;
+        const long long rem = (long long)pl.nbits - tbit;
+        const int nact = (int)min((long long)GROUP, (rem + CHUNK_BITS - 1) / CHUNK_BITS);
+        const bool act = c < nact;
+        const int cs = c * CHUNK_BITS;
+        const int cend = (int)min((long long)(cs + CHUNK_BITS), rem);
+        __syncthreads();
+        STAMP(1);
+
+        // ---- round 1: P_c from the chunk's first bit
+        uint32_t pm = 0;
+        int n = 0, x = 0;
+        if (act) {
+            Rd r;
+            r.init(S.L, cs);
+            while (r.pos < cend) {
+                const int rel = r.pos - cs;
+                pm |= rel < 32 ? (1u << rel) : 0u;
+                r.step(S.L, token_len_bf<CT>(r.peek(), P));
+                n++;
+            }
+            const int xx = r.pos - (cs + CHUNK_BITS);
+            x = (xx >= 0 && xx < 32) ? xx : 0;
+        }
+        S.pm[c] = pm; S.n[c] = (uint16_t)n; S.x[c] = (uint8_t)x;
+        __syncthreads();
+        STAMP(2);
+
+        // ---- round 2: chunk 0's complete map (lanes 224..255) and P_{c-1}'s exit into chunk c
+        uint32_t em = 1u << x;
+        int nk = 0;
+        if (c >= GROUP - 32) {
+            const int e = c - (GROUP - 32);
+            int ex, cn;
+            walk_lds<CT>(S.L, P, 0, (int)min((long long)CHUNK_BITS, rem), e, S.pm[0], S.x[0], S.n[0], &ex, &cn);
+            S.fm[e] = ((uint32_t)ex << 10) | (uint32_t)cn;
+        }
+        if (act && c > 0) {
+            const int e = S.x[c - 1];
+            if (!((pm >> e) & 1u)) {
+                int ex, cn;
+                walk_lds<CT>(S.L, P, cs, cend, e, pm, x, n, &ex, &cn);
+                S.ke[c * KMAX] = ((uint32_t)e << 16) | ((uint32_t)ex << 10) | (uint32_t)cn;
+                nk = 1;
+                em |= 1u << ex;
+            }
+        }
+        S.nk[c] = (uint8_t)nk;
+        __syncthreads();
+        if (c == 0) for (int e = 0; e < 32; e++) em |= 1u << (S.fm[e] >> 10);
+        S.em[0][c] = em;
+        __syncthreads();
+        STAMP(3);
+
+        // ---- closure rounds: add every exit of the predecessor's known entries
+        int round = 3;
+        for (; round <= RMAX; round++) {
+            const int rp = round & 1, pp = rp ^ 1;
+            int added = 0;
+            if (act && c > 0) {
+                uint32_t known = pm;
+                for (int k = 0; k < nk; k++) known |= 1u << (S.ke[c * KMAX + k] >> 16);
+                uint32_t need = S.em[pp][c - 1] & ~known;
+                while (need) {
+                    const int e = __ffs(need) - 1;
+                    need &= need - 1;
+                    if (nk >= KMAX) { atomicOr(D.err, 64u); break; }
+                    int ex, cn;
+                    walk_lds<CT>(S.L, P, cs, cend, e, pm, x, n, &ex, &cn);
+                    S.ke[c * KMAX + nk] = ((uint32_t)e << 16) | ((uint32_t)ex << 10) | (uint32_t)cn;
+                    nk++;
+                    em |= 1u << ex;
+                    added = 1;
+                }
+            }
+            S.em[rp][c] = em;
+            S.nk[c] = (uint8_t)nk;
+            if (!__syncthreads_or(added)) break;
+        }
+        if (round > RMAX && c == 0) atomicOr(D.err, 64u);
+        STAMP(4);
+
+        // ---- standard chain data: entry of chunk c = exit of P_{c-1}
+        int scnt = 0, sex = x;
+        bool ok = true;
+        if (act && c > 0) {
+            int ex, cn;
+            if (lookup_entry(S, c, S.x[c - 1], &ex, &cn)) { scnt = cn; sex = ex; ok = (ex == x); }
+            else atomicOr(D.err, 8u);
+        }
+        S.stdcnt[c] = (uint16_t)scnt;
+        S.stdexit[c] = (uint8_t)sex;
+        const unsigned long long bm = __ballot(!ok);
+        if (lane == 0) S.bad[wid] = bm;
+        uint32_t inc = (uint32_t)scnt;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t tv = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += tv;
+        }
+        if (lane == 63) S.wsum[wid] = inc;
+        __syncthreads();
+        uint32_t wpre = 0;
+        for (int w = 0; w < wid; w++) wpre += S.wsum[w];
+        S.pre[c] = wpre + inc - (uint32_t)scnt;
+        if (c == GROUP - 1) S.pre[GROUP] = wpre + inc;
+        __syncthreads();
+
+        // ---- tile map (lane = entry of chunk 0): follow the chain, hopping over standard runs
+        if (c < 32) {
+            const uint32_t f = S.fm[c];
+            int e = (int)(f >> 10), cc = 1;
+            unsigned long long cnt = f & 1023;
+            bool good = true;
+            while (cc < nact) {
+                if (e == S.x[cc - 1]) {
+                    const int fb = next_bad(S.bad, cc, nact);
+                    cnt += S.pre[fb] - S.pre[cc];
+                    if (fb >= nact) { e = S.x[nact - 1]; break; }
+                    cnt += S.stdcnt[fb];
+                    e = S.stdexit[fb];
+                    cc = fb + 1;
+                } else {
+                    int ex, cn;
+                    if (!lookup_entry(S, cc, e, &ex, &cn)) { good = false; break; }
+                    cnt += (unsigned long long)cn;
+                    e = ex;
+                    cc++;
+                }
+            }
+            D.tmap[t * 32 + c] = good ? (((uint32_t)e << 26) | (uint32_t)(cnt & 0x3FFFFFFu)) : ((uint32_t)UNKE << 26);
+            D.fullmap[t * 32 + c] = ((f >> 10) << 26) | (f & 1023);
+        }
+        // ---- chunk records for the decode kernel
+        if (act) {
+            D.p_exit[gc] = (uint8_t)x;
+            D.p_cnt[gc] = (uint16_t)n;
+            D.p_mask[gc] = pm;
+            D.cmeta[gc] = (uint32_t)scnt | ((uint32_t)sex << 10) | ((uint32_t)nk << 16) | ((ok ? 1u : 0u) << 20);
+            for (int k = 0; k < nk; k++) D.map[gc * 32 + k] = S.ke[c * KMAX + k];
+        }
+        __syncthreads();
+        STAMP(7);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// chain the tiles: entry_t = exit of tile t-1 at entry_{t-1}; base_t = exclusive prefix of counts
+__global__ __launch_bounds__(1024) void tile_scan_kernel(DecBufs D) {
+    __shared__ unsigned long long part[1024];
+    __shared__ int anyunk;
+    const Plan pl = *D.plan;
+    const long long nt = pl.ngroups;
+    const int tid = threadIdx.x;
+    if (tid == 0) anyunk = 0;
+    __syncthreads();
+    for (long long t = tid; t < nt; t += 1024) {
+        int e = 0;
+        if (t > 0) {
+            const uint32_t* m = D.tmap + (t - 1) * 32;
+            const uint32_t x0 = m[0] >> 26;
+            bool cst = true;
+            for (int k = 1; k < 32; k++) cst &= (m[k] >> 26) == x0;
+            e = (cst && x0 != UNKE) ? (int)x0 : UNKE;
+            if (e == UNKE) anyunk = 1;
+        }
+        D.tentry[t] = (uint8_t)e;
+    }
+    __syncthreads();
+    if (anyunk && tid == 0) {                       // rare: varying-exit tiles, chain serially
+        for (long long t = 1; t < nt; t++) {
+            if (D.tentry[t] != UNKE) continue;
+            const int pe = D.tentry[t - 1];
+            const uint32_t v = pe == UNKE ? ((uint32_t)UNKE << 26) : D.tmap[(t - 1) * 32 + pe];
+            D.tentry[t] = (uint8_t)(v >> 26);
+        }
+    }
+    __syncthreads();
+    const long long per = (nt + 1023) / 1024;
+    const long long t0 = tid * per, t1 = min(nt, t0 + per);
+    unsigned long long sum = 0;
+    for (long long t = t0; t < t1; t++) {
+        const int e = D.tentry[t];
+        const uint32_t v = e == UNKE ? ((uint32_t)UNKE << 26) : D.tmap[t * 32 + e];
+        if (e == UNKE || ((v >> 26) == UNKE && t + 1 < nt)) atomicOr(D.err, 8u);
+        sum += e == UNKE ? 0 : (v & 0x3FFFFFFu);
+    }
+    part[tid] = sum;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {           // inclusive Hillis-Steele over 1024 partial sums
+        const unsigned long long v = tid >= d ? part[tid - d] : 0ull;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    unsigned long long run = part[tid] - sum;
+    for (long long t = t0; t < t1; t++) {
+        D.tbase[t] = run;
+        const int e = D.tentry[t];
+        run += e == UNKE ? 0 : (D.tmap[t * 32 + e] & 0x3FFFFFFu);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// decode.  kinds: 0 concrete, 1..3 = the chunk's (tile's) incoming b1..b3, 4 derived (serial)
+struct OutBuf {
+    float v0, v1, v2, v3;
+    uint32_t valid;
+    long long base;
+    __device__ __forceinline__ void flush(float* out) {
+        if (!valid) return;
+        if (valid == 0xFu) {
+            *reinterpret_cast<float4*>(out + base) = make_float4(v0, v1, v2, v3);
+        } else {
+            if (valid & 1u) out[base] = v0;
+            if (valid & 2u) out[base + 1] = v1;
+            if (valid & 4u) out[base + 2] = v2;
+            if (valid & 8u) out[base + 3] = v3;
+        }
+        valid = 0;
+    }
+    __device__ __forceinline__ void put(float* out, long long idx, float v) {
+        const long long g = idx & ~3ll;
+        if (g != base) { flush(out); base = g; }
+        const int i = (int)(idx & 3);
+        v0 = i == 0 ? v : v0; v1 = i == 1 ? v : v1; v2 = i == 2 ? v : v2; v3 = i == 3 ? v : v3;
+        valid |= 1u << i;
+    }
+};
+
+struct DecodeShared {
+    uint32_t L[LWORDS];
+    union {
+        struct {                                   // entry resolution
+            uint32_t pre[GROUP + 1];
+            uint16_t stdcnt[GROUP], devcnt[GROUP];
+            uint8_t x[GROUP], stdexit[GROUP], dev[GROUP];
+            uint32_t fm[32];
+            uint64_t bad[GROUP / 64];
+            uint32_t wsum[GROUP / 64];
+            int ein;
+            unsigned long long base;
+        } r;
+        struct {                                   // carry scan
+            uint8_t kd[2][3][GROUP];
+            float fv[2][3][GROUP];
+        } k;
+    } u;
+    float tin[3];
+    int need, cplx;
+    long long tile;
+};
+
+__device__ __forceinline__ uint64_t hpack(uint64_t flag, uint32_t epoch, uint32_t kind, float v) {
+    return (flag << 62) | ((uint64_t)(epoch & 0x3FFFFFu) << 40) | ((uint64_t)(kind & 0xFF) << 32) | (uint64_t)__float_as_uint(v);
+}
+__device__ __forceinline__ int hflag(uint64_t v, uint32_t epoch) {
+    return (((v >> 40) & 0x3FFFFFu) == (epoch & 0x3FFFFFu)) ? (int)(v >> 62) : 0;
+}
+
+// map of chunk gc at entry e from the parse kernel's global records
+__device__ __forceinline__ bool lookup_global(const DecBufs& D, long long gc, int e, int* ex, int* cn) {
+    const uint32_t pm = D.p_mask[gc];
+    if ((pm >> e) & 1u) { *ex = D.p_exit[gc]; *cn = D.p_cnt[gc] - __popc(pm & ((1u << e) - 1u)); return true; }
+    const int nk = (int)((D.cmeta[gc] >> 16) & 15);
+    for (int k = 0; k < nk; k++) {
+        const uint32_t v = D.map[gc * 32 + k];
+        if ((int)(v >> 16) == e) { *ex = (int)((v >> 10) & 63); *cn = (int)(v & 1023); return true; }
+    }
+    return false;
+}
+
+template <int CT>
+__global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __restrict__ s, Params P, DecBufs D,
+                                                            float* __restrict__ out, long long num, uint32_t epoch) {
+    __shared__ DecodeShared S;
+    const Plan pl = *D.plan;
+    const int c = threadIdx.x, lane = c & 63, wid = c >> 6;
+    while (true) {
+        if (c == 0) S.tile = (long long)atomicAdd(&D.ctr[4], 1u);
+        __syncthreads();
+        const long long t = S.tile;
+        if (t >= pl.ngroups) break;
+        const long long tbit = t * (long long)GROUP * CHUNK_BITS;
+        STAMP(8);
+        stage_tile(S.L, s, pl.nbytes, tbit >> 5);
+        const long long gc = t * GROUP + c;
+        const long long rem = (long long)pl.nbits - tbit;
+        const int nact = (int)min((long long)GROUP, (rem + CHUNK_BITS - 1) / CHUNK_BITS);
+        const bool act = c < nact;
+        const int cs = c * CHUNK_BITS;
+        const int cend = (int)min((long long)(cs + CHUNK_BITS), rem);
+        if (c == 0) { S.need = 0; S.cplx = 0; S.u.r.ein = D.tentry[t]; S.u.r.base = D.tbase[t]; }
+        // ---- chunk records -> LDS; standard counts prefix; failure mask
+        const uint32_t cm = act ? D.cmeta[gc] : 0u;
+        const int scnt = (int)(cm & 1023);
+        const bool ok = !act || c == 0 || ((cm >> 20) & 1u);
+        S.u.r.x[c] = act ? D.p_exit[gc] : 0;
+        S.u.r.stdcnt[c] = (uint16_t)scnt;
+        S.u.r.stdexit[c] = (uint8_t)((cm >> 10) & 63);
+        S.u.r.dev[c] = 0xFF;
+        if (c < 32) S.u.r.fm[c] = D.fullmap[t * 32 + c];
+        const unsigned long long bm = __ballot(!ok);
+        if (lane == 0) S.u.r.bad[wid] = bm;
+        __syncthreads();
+        // ---- true chain through the tile (one lane, hopping over standard runs)
+        if (c == 0) {
+            int e = S.u.r.ein;
+            if (e != UNKE) {
+                const uint32_t f = S.u.r.fm[e];
+                e = (int)(f >> 26);
+                int cc = 1;
+                while (cc < nact) {
+                    if (e == S.u.r.x[cc - 1]) {
+                        const int fb = next_bad(S.u.r.bad, cc, nact);
+                        if (fb >= nact) break;
+                        e = S.u.r.stdexit[fb];
+                        cc = fb + 1;
+                    } else {
+                        int ex, cn;
+                        if (!lookup_global(D, t * GROUP + cc, e, &ex, &cn)) { atomicOr(D.err, 8u); S.u.r.ein = UNKE; break; }
+                        S.u.r.dev[cc] = (uint8_t)e;
+                        S.u.r.devcnt[cc] = (uint16_t)cn;
+                        e = ex;
+                        cc++;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        const int ein = S.u.r.ein;
+        int e = ein, tc = 0;
+        if (ein != UNKE) {
+            if (c == 0) tc = (int)(S.u.r.fm[ein] & 0x3FFFFFFu);
+            else if (S.u.r.dev[c] != 0xFF) { e = S.u.r.dev[c]; tc = S.u.r.devcnt[c]; }
+            else { e = S.u.r.x[c - 1]; tc = scnt; }
+        }
+        if (!act) tc = 0;
+        uint32_t inc2 = (uint32_t)tc;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t tv = __shfl_up(inc2, d, 64);
+            if (lane >= d) inc2 += tv;
+        }
+        if (lane == 63) S.u.r.wsum[wid] = inc2;
+        __syncthreads();
+        uint32_t wp2 = 0;
+        for (int w = 0; w < wid; w++) wp2 += S.u.r.wsum[w];
+        const unsigned long long k0 = S.u.r.base + wp2 + inc2 - (uint32_t)tc;
+        if (act) { D.entry[gc] = (uint8_t)(ein == UNKE ? UNKE : e); D.tokoff[gc] = k0; }
+        if (act && ein == UNKE) atomicOr(D.err, 8u);
+        if (ein == UNKE) e = UNKE;
+        __syncthreads();
+        STAMP(9);
+
+        // ---- pass 1: decode from the true entry; concrete values are stored immediately
+        const bool first = (gc == 0);
+        float f1 = -1.0f, f2 = -1.0f, f3 = -1.0f;
+        int k1 = first ? 0 : 1, k2 = first ? 0 : 2, k3 = first ? 0 : 3;
+        int pend = 0;
+        if (act && e != UNKE) {
+            OutBuf ob;
+            ob.valid = 0; ob.base = -4;
+            Rd r;
+            r.init(S.L, cs + e);
+            unsigned long long idx = k0;
+            int j = 0;
+            while (r.pos < cend) {
+                const uint32_t tk = r.peek();
+                const int len = token_len_bf<CT>(tk, P);
+                int code;
+                const uint32_t pat = token_pattern_bf<CT>(tk, len, P, &code);
+                const float p2 = predict_value(2, f1, f2, f3), p3 = predict_value(3, f1, f2, f3);
+                const float v = code == 0 ? __uint_as_float(pat) : (code == 1 ? f1 : (code == 2 ? p2 : p3));
+                const int kind = code == 0 ? 0 : (code == 1 ? k1 : (code == 2 ? ((k1 | k2) ? 4 : 0) : ((k1 | k2 | k3) ? 4 : 0)));
+                if (kind == 0) { if (idx < (unsigned long long)num) ob.put(out, (long long)idx, v); }
+                else pend = j + 1;
+                f3 = f2; k3 = k2; f2 = f1; k2 = k1; f1 = v; k1 = kind;
+                r.step(S.L, len);
+                j++;
+                idx++;
+            }
+            ob.flush(out);
+        }
+        if (!act || e == UNKE) { k1 = 1; k2 = 2; k3 = 3; }
+        __syncthreads();                                   // resolution arrays are dead from here
+        S.u.k.kd[0][0][c] = (uint8_t)k1; S.u.k.kd[0][1][c] = (uint8_t)k2; S.u.k.kd[0][2][c] = (uint8_t)k3;
+        S.u.k.fv[0][0][c] = f1; S.u.k.fv[0][1][c] = f2; S.u.k.fv[0][2][c] = f3;
+        __syncthreads();
+        STAMP(10);
+        // ---- inclusive scan of carry functions: F_c = f_c o ... o f_0
+        int cur = 0;
+        for (int d = 1; d < GROUP; d <<= 1) {
+            for (int i = 0; i < 3; i++) {
+                const int k0i = S.u.k.kd[cur][i][c];
+                int kk = k0i;
+                float vv = S.u.k.fv[cur][i][c];
+                if (c >= d && k0i >= 1 && k0i <= 3) {
+                    kk = S.u.k.kd[cur][k0i - 1][c - d];
+                    vv = S.u.k.fv[cur][k0i - 1][c - d];
+                }
+                S.u.k.kd[cur ^ 1][i][c] = (uint8_t)kk;
+                S.u.k.fv[cur ^ 1][i][c] = vv;
+            }
+            cur ^= 1;
+            __syncthreads();
+        }
+        int ik[3];
+        float iv[3];
+        for (int i = 0; i < 3; i++) {
+            ik[i] = c == 0 ? i + 1 : S.u.k.kd[cur][i][c - 1];
+            iv[i] = c == 0 ? 0.0f : S.u.k.fv[cur][i][c - 1];
+        }
+        if (pend > 0) {
+            bool needs = false, cx = false;
+            for (int i = 0; i < 3; i++) { needs |= (ik[i] >= 1 && ik[i] <= 3); cx |= (ik[i] == 4); }
+            if (needs) S.need = 1;
+            if (cx) S.cplx = 1;
+        }
+        const int tk0 = S.u.k.kd[cur][0][GROUP - 1], tk1 = S.u.k.kd[cur][1][GROUP - 1], tk2 = S.u.k.kd[cur][2][GROUP - 1];
+        if (c == 0) {
+            for (int i = 0; i < 3; i++)
+                st_relaxed(&D.hist[t * 6 + i], hpack(1, epoch, S.u.k.kd[cur][i][GROUP - 1], S.u.k.fv[cur][i][GROUP - 1]));
+            if (tk0 == 0 && tk1 == 0 && tk2 == 0)
+                for (int i = 0; i < 3; i++)
+                    st_relaxed(&D.hist[t * 6 + 3 + i], hpack(2, epoch, 0, S.u.k.fv[cur][i][GROUP - 1]));
+            if (tk0 == 4 || tk1 == 4 || tk2 == 4) S.cplx = 1;
+        }
+        __syncthreads();
+        const int need = S.need, cplx = S.cplx;
+        if (cplx) {
+            if (c == 0) {
+                atomicOr(D.err, 32u);
+                for (int i = 0; i < 3; i++) st_relaxed(&D.hist[t * 6 + 3 + i], hpack(2, epoch, 4, 0.0f));
+            }
+            if (act) { D.pend[gc] = (uint16_t)min(pend, 65535); D.done[gc] = 0; }
+            __syncthreads();
+            continue;
+        }
+        // ---- tile incoming (history look-back), lanes 0..2 = b1..b3
+        if (need && c < 3) {
+            float val = -1.0f;
+            int j = c;
+            long long k = t - 1;
+            unsigned spins = 0;
+            bool bad = false;
+            while (k >= 0) {
+                const uint64_t pv = ld_relaxed(&D.hist[k * 6 + 3 + j]);
+                if (hflag(pv, epoch) == 2) {
+                    if (((pv >> 32) & 0xFF) == 4) bad = true;
+                    val = __uint_as_float((uint32_t)pv);
+                    break;
+                }
+                const uint64_t av = ld_relaxed(&D.hist[k * 6 + j]);
+                if (hflag(av, epoch) == 1) {
+                    const int kind = (int)((av >> 32) & 0xFF);
+                    if (kind == 0) { val = __uint_as_float((uint32_t)av); break; }
+                    if (kind >= 1 && kind <= 3) { j = kind - 1; k--; continue; }
+                }
+                if (++spins > (1u << 24)) { bad = true; atomicOr(D.err, 16u); break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (bad) atomicOr(D.err, 32u);
+            S.tin[c] = val;
+        }
+        __syncthreads();
+        if (need && c == 0 && !(tk0 == 0 && tk1 == 0 && tk2 == 0)) {
+            const int kk[3] = {tk0, tk1, tk2};
+            for (int i = 0; i < 3; i++)
+                st_relaxed(&D.hist[t * 6 + 3 + i],
+                           hpack(2, epoch, 0, kk[i] == 0 ? S.u.k.fv[cur][i][GROUP - 1] : S.tin[kk[i] - 1]));
+        }
+        // ---- fix-up: re-decode the pending prefix with concrete history
+        if (act && pend > 0) {
+            float g1 = ik[0] == 0 ? iv[0] : S.tin[ik[0] - 1];
+            float g2 = ik[1] == 0 ? iv[1] : S.tin[ik[1] - 1];
+            float g3 = ik[2] == 0 ? iv[2] : S.tin[ik[2] - 1];
+            Rd r;
+            r.init(S.L, cs + e);
+            for (int jj = 0; jj < pend; jj++) {
+                const uint32_t tk = r.peek();
+                const int len = token_len_bf<CT>(tk, P);
+                int code;
+                const uint32_t pat = token_pattern_bf<CT>(tk, len, P, &code);
+                const float v = code == 0 ? __uint_as_float(pat) : predict_value(code, g1, g2, g3);
+                if (k0 + jj < (unsigned long long)num) out[k0 + jj] = v;
+                g3 = g2; g2 = g1; g1 = v;
+                r.step(S.L, len);
+            }
+        }
+        if (act) { D.pend[gc] = (uint16_t)min(pend, 65535); D.done[gc] = pend ? 1 : 0; }
+        __syncthreads();
+        STAMP(11);
+    }
+    if (c == 0) {
+        __threadfence();
+        if (atomicAdd(&D.ctr[5], 1u) == gridDim.x - 1) { atomicExch(&D.ctr[4], 0u); atomicExch(&D.ctr[5], 0u); }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+#define DC_DISPATCH_F(CTV, KER, ...)                                                                 \
+    switch (CTV) {                                                                                   \
+        case 5: hipLaunchKernelGGL(KER<5>, __VA_ARGS__); break;                                      \
+        case 6: hipLaunchKernelGGL(KER<6>, __VA_ARGS__); break;                                      \
+        case 7: hipLaunchKernelGGL(KER<7>, __VA_ARGS__); break;                                      \
+        case 11: hipLaunchKernelGGL(KER<11>, __VA_ARGS__); break;                                    \
+        default: return -2;                                                                          \
+    }
+
+__global__ void plan_kernel_fast(Plan* plan, const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                                 long long max_chunks) {
+    const unsigned long long nbits = dev_nbits ? *dev_nbits : host_nbits;
+    Plan p;
+    p.nbits = nbits;
+    p.nbytes = (long long)((nbits + 7) >> 3);
+    long long nc = (long long)((nbits + CHUNK_BITS - 1) / CHUNK_BITS);
+    if (nc > max_chunks) nc = max_chunks;
+    p.nchunks = nc;
+    p.ngroups = (nc + GROUP - 1) / GROUP;
+    *plan = p;
+}
+
+extern "C" int dc_launch_decode_fast(const uint8_t* s, const unsigned long long* dev_nbits,
+                                     unsigned long long host_nbits, long long max_chunks, const Params* P,
+                                     const DecBufs* D, float* out, long long num, uint32_t epoch, hipStream_t st) {
+    const long long max_groups = (max_chunks + GROUP - 1) / GROUP;
+    hipLaunchKernelGGL(plan_kernel_fast, dim3(1), dim3(1), 0, st, D->plan, dev_nbits, host_nbits, max_chunks);
+    const int gparse = (int)std::min<long long>(max_groups > 0 ? max_groups : 1, 256 * 8);
+    DC_DISPATCH_F(P->ct, parse_kernel, dim3(gparse), dim3(GROUP), 0, st, s, *P, *D);
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, st, *D);
+    const int gdec = (int)std::min<long long>(max_groups > 0 ? max_groups : 1, 256 * 3);
+    DC_DISPATCH_F(P->ct, decode_kernel_fast, dim3(gdec), dim3(GROUP), 0, st, s, *P, *D, out, num, epoch);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace dc

@@ -13,6 +13,10 @@
 
 namespace dc {
 
+// decoder geometry: a chunk is the unit one lane parses; a group (tile) is one workgroup's chunks
+constexpr int CHUNK_BITS = 1024;
+constexpr int GROUP = 256;
+
 
 
 __device__ __forceinline__ int mbits(int B, uint32_t E) {
@@ -108,6 +112,50 @@ __device__ __forceinline__ uint32_t token_pattern(uint32_t t, int len, const Par
     // raw: top len bits + midpoint bit (decompress_bitwise_float :3166-3184)
     if (len >= 32) return t;
     return (t & ~(0xFFFFFFFFu >> len)) | (1u << (31 - len));
+}
+
+
+// Branch-free token length (selects only; every lane of a wave follows the same instruction stream).
+template <int CT>
+__device__ __forceinline__ int token_len_bf(uint32_t t, const Params& P) {
+    const int raw = 9 + mbits(P.B, (t >> 23) & 0xFFu);
+    if (CT == 6) return raw;
+    int len = raw;
+    if (CT == 11) len = 32;
+    if (CT == 7) {
+        const uint32_t ones = (1u << P.type) - 1u;
+        const bool msk = ((t >> (31 - P.type)) & ones) == ones;
+        const int ml = (((t >> (30 - P.type)) & 1u) ? P.mm : P.mm0) + P.type + 2;
+        len = msk ? ml : raw;
+    }
+    return (t >> 31) ? 3 : len;
+}
+
+// Branch-free non-predicted value pattern and predictor code (0 = none/'100', 1..3 = 101/110/111).
+template <int CT>
+__device__ __forceinline__ uint32_t token_pattern_bf(uint32_t t, int len, const Params& P, int* code) {
+    const bool c3 = (CT != 6) && (t >> 31);
+    *code = c3 ? (int)((t >> 29) & 3u) : 0;
+    uint32_t u;
+    if (CT == 11) {
+        u = t;
+    } else {
+        const uint32_t keep = len >= 32 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> len);
+        u = (t & keep) | (len < 32 ? (1u << (31 - len)) : 0u);                 // raw + midpoint
+        if (CT == 7) {
+            const uint32_t ones = (1u << P.type) - 1u;
+            const bool msk = ((t >> (31 - P.type)) & ones) == ones;
+            const uint32_t rest = t << (P.type + 2);
+            const bool fl = (t >> (30 - P.type)) & 1u;
+            const int tl0 = P.mm0, tl1 = P.mm;                                   // uniform
+            const uint32_t tail0 = tl0 > 0 ? (rest >> (32 - tl0)) : 0u;
+            const uint32_t tail1 = tl1 > 0 ? (rest >> (32 - tl1)) : 0u;
+            const uint32_t u0 = (P.mask17 << 15) | (tl0 > 0 ? tail0 << (15 - tl0) : 0u) | (tl0 < 15 ? 1u << (14 - tl0) : 0u);
+            const uint32_t u1 = ((P.mask17 >> 8) << 23) | (tl1 > 0 ? tail1 << (23 - tl1) : 0u) | (tl1 < 23 ? 1u << (22 - tl1) : 0u);
+            u = msk ? (fl ? u1 : u0) : u;
+        }
+    }
+    return c3 ? 0u : u;
 }
 
 __device__ __forceinline__ float predict_value(int code, float b1, float b2, float b3) {

@@ -49,6 +49,7 @@ typedef struct {
     long long dec_max_chunks;
     float* dec_out;
     long long dec_num;
+    unsigned long long dec_nbits;
     /* pinned host scratch */
     unsigned long long* h_scratch;   /* [0] total bits [1] err [2..] misc */
     /* staging for the host-pointer ABI */
@@ -84,6 +85,15 @@ void* dc_get_stream(void) { return (void*)G.st; }
 void dc_set_abs_error_bound(double bound) { absErrBound = bound; absErrorBound_binary = -100; }
 double dc_get_abs_error_bound(void) { return absErrBound; }
 long long dc_decode_chunk_bits_value(void) { return dc_decode_chunk_bits(); }
+
+/* diagnostic: copy the decoder phase stamps ([tile][16] s_memrealtime, 100 MHz) to the host */
+int dc_debug_stamps(unsigned long long* host, long long n) {
+    if (!G.D.dbg) return DC_ERR_ARG;
+    if (n > 4096 * 16) n = 4096 * 16;
+    HIPCHK(hipStreamSynchronize(G.st));
+    HIPCHK(hipMemcpy(host, G.D.dbg, (size_t)n * 8, hipMemcpyDeviceToHost));
+    return DC_OK;
+}
 
 int dc_init(int device) {
     if (G.inited) return DC_OK;
@@ -257,14 +267,14 @@ static int dec_ensure(long long max_chunks) {
     G.dec_pool = NULL;
     long long C = max_chunks + 4096;
     long long GR = (C + dc_decode_group() - 1) / dc_decode_group() + 1;
-    size_t off = 0, sz[15];
+    size_t off = 0, sz[20];
     sz[0] = 256;                          /* plan */
     sz[1] = (size_t)C;                    /* p_exit */
     sz[2] = (size_t)C * 2;                /* p_cnt */
     sz[3] = (size_t)C * 4;                /* p_mask */
     sz[4] = (size_t)C * 32 * 4;           /* map */
     sz[5] = (size_t)GR * 32 * 4;          /* fullmap */
-    sz[6] = (size_t)GR * 32 * 8;          /* gran */
+    sz[6] = (size_t)GR * 34 * 8;          /* gran */
     sz[7] = (size_t)C;                    /* entry */
     sz[8] = (size_t)C * 8;                /* tokoff */
     sz[9] = (size_t)C * 2;                /* pend */
@@ -273,13 +283,18 @@ static int dec_ensure(long long max_chunks) {
     sz[12] = 64;                          /* ctr */
     sz[13] = (size_t)C * 4;               /* known */
     sz[14] = (size_t)C * 8;               /* exitmask */
+    sz[15] = (size_t)GR * 6 * 8;          /* hist */
+    sz[16] = (size_t)C * 4;               /* cmeta */
+    sz[17] = (size_t)GR * 32 * 4;         /* tmap */
+    sz[18] = (size_t)GR;                  /* tentry */
+    sz[19] = (size_t)GR * 8;              /* tbase */
     size_t tot = 0;
-    for (int i = 0; i < 15; i++) tot += (sz[i] + 255) & ~(size_t)255;
+    for (int i = 0; i < 20; i++) tot += (sz[i] + 255) & ~(size_t)255;
     HIPCHK(hipMalloc(&G.dec_pool, tot));
     HIPCHK(hipMemsetAsync(G.dec_pool, 0, tot, G.st));
     char* b = (char*)G.dec_pool;
-    void* ptr[15];
-    for (int i = 0; i < 15; i++) { ptr[i] = b + off; off += (sz[i] + 255) & ~(size_t)255; }
+    void* ptr[20];
+    for (int i = 0; i < 20; i++) { ptr[i] = b + off; off += (sz[i] + 255) & ~(size_t)255; }
     G.D.plan = (Plan*)ptr[0];
     G.D.p_exit = (uint8_t*)ptr[1];
     G.D.p_cnt = (uint16_t*)ptr[2];
@@ -287,6 +302,11 @@ static int dec_ensure(long long max_chunks) {
     G.D.map = (uint32_t*)ptr[4];
     G.D.known = (uint32_t*)ptr[13];
     G.D.exitmask = (uint32_t*)ptr[14];
+    G.D.hist = (uint64_t*)ptr[15];
+    G.D.cmeta = (uint32_t*)ptr[16];
+    G.D.tmap = (uint32_t*)ptr[17];
+    G.D.tentry = (uint8_t*)ptr[18];
+    G.D.tbase = (unsigned long long*)ptr[19];
     G.D.fullmap = (uint32_t*)ptr[5];
     G.D.gran = (uint64_t*)ptr[6];
     G.D.entry = (uint8_t*)ptr[7];
@@ -297,6 +317,11 @@ static int dec_ensure(long long max_chunks) {
     G.D.ctr = (unsigned*)ptr[12];
     G.dec_cap_chunks = C;
     G.dec_epoch = 1;
+    G.D.dbg = NULL;
+    if (getenv("DC_DEBUG_STAMPS")) {
+        HIPCHK(hipMalloc((void**)&G.D.dbg, 4096 * 16 * 8));
+        HIPCHK(hipMemset(G.D.dbg, 0, 4096 * 16 * 8));
+    }
     return DC_OK;
 }
 
@@ -319,14 +344,15 @@ int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsig
     if (rc) return rc;
     if (++G.dec_epoch >= (1u << 22)) {
         long long GR = (G.dec_cap_chunks + dc_decode_group() - 1) / dc_decode_group() + 1;
-        HIPCHK(hipMemsetAsync(G.D.gran, 0, (size_t)GR * 32 * 8, G.st));
+        HIPCHK(hipMemsetAsync(G.D.gran, 0, (size_t)GR * 34 * 8, G.st));
+        HIPCHK(hipMemsetAsync(G.D.hist, 0, (size_t)GR * 6 * 8, G.st));
         G.dec_epoch = 1;
     }
     Params P;
     make_params(&P, ct, type, mask17);
-    if (dc_launch_decode((const uint8_t*)d_stream, nbytes >= 0 ? NULL : d_nbits,
-                         nbytes >= 0 ? (unsigned long long)nbytes * 8ull : 0ull, max_chunks, &P, &G.D,
-                         (float*)d_out, num, G.dec_epoch, DEC_ROUNDS, DEC_FIX_ITERS, G.st))
+    if (dc_launch_decode_fast((const uint8_t*)d_stream, nbytes >= 0 ? NULL : d_nbits,
+                              nbytes >= 0 ? (unsigned long long)nbytes * 8ull : 0ull, max_chunks, &P, &G.D,
+                              (float*)d_out, num, G.dec_epoch, G.st))
         return seterr(DC_ERR_HIP, "decode launch failed: %s", hipGetErrorString(hipGetLastError()));
     G.dec_pending = 1;
     G.dec_P = P;
@@ -339,8 +365,10 @@ int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsig
 
 static int read_dec_err(unsigned* err) {
     HIPCHK(hipMemcpyAsync(&G.h_scratch[2], G.D.err, 4, hipMemcpyDeviceToHost, G.st));
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[3], G.D.plan, 8, hipMemcpyDeviceToHost, G.st));
     HIPCHK(hipStreamSynchronize(G.st));
     *err = (unsigned)(G.h_scratch[2] & 0xFFFFFFFFu);
+    G.dec_nbits = G.h_scratch[3];
     return DC_OK;
 }
 
@@ -351,14 +379,25 @@ int dc_decode_finish(void) {
     rc = read_dec_err(&err);
     if (rc) return rc;
     if (!err) { G.dec_pending = 0; return DC_OK; }
-    if ((err & 8u) && !(err & 16u) && G.dec_pending) {
+    if ((err & (8u | 64u)) && !(err & 16u) && G.dec_pending) {
+        /* outside the fast path's assumptions: exact multi-kernel path (closure rounds, then
+         * complete entry maps for every chunk if an entry is still unresolved) */
         HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
         if (++G.dec_epoch >= (1u << 22)) G.dec_epoch = 1;
-        if (dc_launch_decode_more(G.dec_s, G.dec_max_chunks, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.dec_epoch,
-                                  DEC_FIX_ITERS, G.st))
+        if (dc_launch_decode(G.dec_s, NULL, G.dec_nbits, G.dec_max_chunks, &G.dec_P, &G.D, G.dec_out, G.dec_num,
+                             G.dec_epoch, DEC_ROUNDS, DEC_FIX_ITERS, G.st))
             return seterr(DC_ERR_HIP, "decode launch failed");
         rc = read_dec_err(&err);
         if (rc) return rc;
+        if ((err & 8u) && !(err & 16u)) {
+            HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
+            if (++G.dec_epoch >= (1u << 22)) G.dec_epoch = 1;
+            if (dc_launch_decode_more(G.dec_s, G.dec_max_chunks, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.dec_epoch,
+                                      DEC_FIX_ITERS, G.st))
+                return seterr(DC_ERR_HIP, "decode launch failed");
+            rc = read_dec_err(&err);
+            if (rc) return rc;
+        }
     }
     if ((err & 32u) && !(err & (8u | 16u)) && G.dec_pending) {
         HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));

@@ -36,13 +36,19 @@ typedef struct DecBufs { /* decoder metadata, sized for the maximum chunk count 
     uint32_t* known;     /* [chunk] entries with a valid map[] word (besides P's own positions) */
     uint32_t* exitmask;  /* [chunk][2] exits of all known entries, by closure-round parity */
     uint32_t* fullmap;   /* [group][32]  exit<<26 | count */
-    uint64_t* gran;      /* [group][32]  look-back granules */
+    uint64_t* gran;      /* [group][33]  look-back granules (32 map entries + inclusive) */
+    uint64_t* hist;      /* [group][6]   decoder-history look-back granules (3 aggregate + 3 final) */
+    uint32_t* cmeta;     /* [chunk] standard count | std exit<<10 | extra entries<<16 | ok<<20 */
+    uint32_t* tmap;      /* [group][32] tile map: exit<<26 | token count */
+    uint8_t* tentry;     /* [group] true entry of the tile's first chunk */
+    unsigned long long* tbase;   /* [group] first token index of the tile */
     uint8_t* entry;
     unsigned long long* tokoff;
     uint16_t* pend;
     uint16_t* done;
-    unsigned* err;       /* 8 unknown entry, 16 spin timeout, 32 pending left */
-    unsigned* ctr;       /* [0] group ticket, [1] exit count */
+    unsigned* err;       /* 8 unknown entry, 16 spin timeout, 32 pending left, 64 closure overflow */
+    unsigned* ctr;       /* [0,1] resolve ticket/exit, [2,3] parse, [4,5] decode */
+    unsigned long long* dbg;   /* optional phase stamps (s_memrealtime) [tile][16], NULL = off */
 } DecBufs;
 
 #ifdef __cplusplus
@@ -66,6 +72,9 @@ int dc_launch_decode(const uint8_t* s, const unsigned long long* dev_nbits, unsi
 int dc_launch_decode_more(const uint8_t* s, long long max_chunks, const DC_NS Params* P,
                           const DC_NS DecBufs* D, float* out, long long num, uint32_t epoch,
                           int fix_iters, dc_hip_stream st);
+int dc_launch_decode_fast(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                          long long max_chunks, const DC_NS Params* P, const DC_NS DecBufs* D, float* out,
+                          long long num, uint32_t epoch, dc_hip_stream st);
 int dc_launch_fixup_serial(const uint8_t* s, const DC_NS Params* P, const DC_NS DecBufs* D, float* out,
                            long long num, dc_hip_stream st);
 long long dc_decode_chunk_bits(void);
