@@ -29,6 +29,9 @@ namespace dc {
 
 constexpr int LROW = 33;                       // padded LDS row (words) per chunk
 constexpr int LWORDS = (GROUP + 1) * LROW;     // + one row for the words after the tile
+constexpr int OV = 512;                        // overlap: P_c starts OV bits before its chunk
+constexpr int OVW = OV / 32;
+constexpr int PWORDS = LWORDS + OVW + OVW / 32;
 constexpr int KMAX = 6;                        // extra known entries per chunk (besides P_c's own)
 constexpr int RMAX = 12;                       // closure rounds inside a tile
 constexpr int CW = CHUNK_BITS / 32;            // words per chunk
@@ -65,34 +68,40 @@ struct Rd {
     }
 };
 
-// stage the tile's stream words [tw, tw + GROUP*CW + 4) into padded LDS rows (zeros past the end)
-__device__ __forceinline__ void stage_tile(uint32_t* L, const uint8_t* s, long long nbytes, long long tw) {
+// stage stream words [tw, tw + nw) into padded LDS rows (zeros outside the stream; tw may be < 0)
+__device__ __forceinline__ void stage_words(uint32_t* L, const uint8_t* s, long long nbytes, long long tw, int nw) {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(s);
     const long long nwfull = nbytes >> 2;
-    constexpr int NW = GROUP * CW;
-    if (tw + NW + 4 <= nwfull && ((reinterpret_cast<uintptr_t>(s) & 15u) == 0) && (tw & 3) == 0) {
+    if (tw >= 0 && tw + nw <= nwfull && ((reinterpret_cast<uintptr_t>(s) & 15u) == 0) && (tw & 3) == 0 && (nw & 3) == 0) {
         const uint4* w4 = reinterpret_cast<const uint4*>(w + tw);
-        uint4 r[NW / 4 / GROUP];
+        const int n4 = nw >> 2;
+        constexpr int QF = CW * GROUP / 4 / GROUP;           // full rounds of GROUP uint4
+        uint4 r[QF + 1];
 #pragma unroll
-        for (int q = 0; q < NW / 4 / GROUP; q++) r[q] = w4[threadIdx.x + q * GROUP];
-        uint32_t tail = 0;
-        if (threadIdx.x < 4) tail = w[tw + NW + threadIdx.x];
-#pragma unroll
-        for (int q = 0; q < NW / 4 / GROUP; q++) {
-            const int i = 4 * (threadIdx.x + q * GROUP);
-            uint32_t* d = L + i + (i >> 5);
-            d[0] = __builtin_bswap32(r[q].x);
-            d[1] = __builtin_bswap32(r[q].y);
-            d[2] = __builtin_bswap32(r[q].z);
-            d[3] = __builtin_bswap32(r[q].w);
+        for (int q = 0; q <= QF; q++) {
+            const int i = threadIdx.x + q * GROUP;
+            if (q < QF || i < n4) r[q] = w4[i];
         }
-        if (threadIdx.x < 4) L[NW + GROUP + threadIdx.x] = __builtin_bswap32(tail);
+#pragma unroll
+        for (int q = 0; q <= QF; q++) {
+            const int i4 = threadIdx.x + q * GROUP;
+            if (q < QF || i4 < n4) {
+                const int i = 4 * i4;
+                uint32_t* d = L + i + (i >> 5);
+                d[0] = __builtin_bswap32(r[q].x);
+                d[1] = __builtin_bswap32(r[q].y);
+                d[2] = __builtin_bswap32(r[q].z);
+                d[3] = __builtin_bswap32(r[q].w);
+            }
+        }
         return;
     }
-    for (int i = threadIdx.x; i < NW + 4; i += blockDim.x) {
+    for (int i = threadIdx.x; i < nw; i += blockDim.x) {
         const long long gw = tw + i;
         uint32_t v = 0;
-        if (gw < nwfull) {
+        if (gw < 0) {
+            v = 0;
+        } else if (gw < nwfull) {
             v = __builtin_bswap32(w[gw]);
         } else if (4 * gw < nbytes) {
             for (int k = 0; k < 4; k++) {
@@ -104,8 +113,14 @@ __device__ __forceinline__ void stage_tile(uint32_t* L, const uint8_t* s, long l
     }
 }
 
-// walk entry e of chunk c (tile-relative bits [cs, cend)) alongside P_c; the reader that is behind
-// steps.  Returns the exit relative to the next chunk and the number of tokens starting in the chunk.
+// the tile's words [tw, tw + GROUP*CW + 4)
+__device__ __forceinline__ void stage_tile(uint32_t* L, const uint8_t* s, long long nbytes, long long tw) {
+    stage_words(L, s, nbytes, tw, GROUP * CW + 4);
+}
+
+// walk entry e of chunk c (LDS bits [cs, cend)) alongside P_c (whose first boundary in the chunk is
+// pmask's lowest bit); the reader that is behind steps.  Returns the exit relative to the next chunk
+// and the number of tokens starting in the chunk.
 template <int CT>
 __device__ __forceinline__ void walk_lds(const uint32_t* L, const Params& P, int cs, int cend, int e,
                                          uint32_t pmask, int pexit, int pcnt, int* out_exit, int* out_cnt) {
@@ -116,7 +131,7 @@ __device__ __forceinline__ void walk_lds(const uint32_t* L, const Params& P, int
     }
     Rd A, B;
     A.init(L, cs + e);
-    B.init(L, cs);
+    B.init(L, cs + (pmask ? __ffs(pmask) - 1 : 32));
     int ca = 0, cb = 0;
     bool merged = false;
     while (A.pos < cend) {
@@ -134,12 +149,11 @@ __device__ __forceinline__ void walk_lds(const uint32_t* L, const Params& P, int
 
 // ------------------------------------------------------------------------------------------------
 struct ParseShared {
-    uint32_t L[LWORDS];
+    uint32_t L[PWORDS];
     uint32_t ke[GROUP * KMAX];                 // entry<<16 | exit<<10 | cnt
     uint32_t em[2][GROUP];                     // exits of all known entries, by round parity
     uint32_t pm[GROUP];
     uint32_t pre[GROUP + 1];                   // exclusive prefix of the standard counts
-    uint32_t fm[32];                           // complete map of chunk 0: exit<<10 | cnt
     uint64_t bad[GROUP / 64];
     uint16_t n[GROUP], stdcnt[GROUP];
     uint8_t x[GROUP], nk[GROUP], stdexit[GROUP];
@@ -174,22 +188,25 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
     for (long long t = blockIdx.x; t < pl.ngroups; t += gridDim.x) {
         const long long tbit = t * (long long)GROUP * CHUNK_BITS;
         STAMP(0);
-        stage_tile(S.L, s, pl.nbytes, tbit >> 5);
+        // LDS bit OV = the tile's first stream bit; the OV bits before it let P_0 synchronise
+        stage_words(S.L, s, pl.nbytes, (tbit >> 5) - OVW, GROUP * CW + OVW + 4);
         const long long gc = t * GROUP + c;
         const long long rem = (long long)pl.nbits - tbit;
         const int nact = (int)min((long long)GROUP, (rem + CHUNK_BITS - 1) / CHUNK_BITS);
         const bool act = c < nact;
-        const int cs = c * CHUNK_BITS;
-        const int cend = (int)min((long long)(cs + CHUNK_BITS), rem);
+        const int cs = OV + c * CHUNK_BITS;
+        const int cend = OV + (int)min((long long)(c * CHUNK_BITS + CHUNK_BITS), rem);
         __syncthreads();
         STAMP(1);
 
-        // ---- round 1: P_c from the chunk's first bit
+        // ---- round 1: P_c from OV bits before the chunk (from bit 0 for the stream's first chunk);
+        // self-synchronisation makes P_c the true path inside the chunk in almost every case
         uint32_t pm = 0;
         int n = 0, x = 0;
         if (act) {
             Rd r;
-            r.init(S.L, cs);
+            r.init(S.L, gc == 0 ? cs : cs - OV);
+            while (r.pos < cs) r.step(S.L, token_len_bf<CT>(r.peek(), P));
             while (r.pos < cend) {
                 const int rel = r.pos - cs;
                 pm |= rel < 32 ? (1u << rel) : 0u;
@@ -203,15 +220,9 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
         __syncthreads();
         STAMP(2);
 
-        // ---- round 2: chunk 0's complete map (lanes 224..255) and P_{c-1}'s exit into chunk c
+        // ---- round 2: P_{c-1}'s exit into chunk c, where P_c has no boundary there (rare)
         uint32_t em = 1u << x;
         int nk = 0;
-        if (c >= GROUP - 32) {
-            const int e = c - (GROUP - 32);
-            int ex, cn;
-            walk_lds<CT>(S.L, P, 0, (int)min((long long)CHUNK_BITS, rem), e, S.pm[0], S.x[0], S.n[0], &ex, &cn);
-            S.fm[e] = ((uint32_t)ex << 10) | (uint32_t)cn;
-        }
         if (act && c > 0) {
             const int e = S.x[c - 1];
             if (!((pm >> e) & 1u)) {
@@ -223,8 +234,6 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
             }
         }
         S.nk[c] = (uint8_t)nk;
-        __syncthreads();
-        if (c == 0) for (int e = 0; e < 32; e++) em |= 1u << (S.fm[e] >> 10);
         S.em[0][c] = em;
         __syncthreads();
         STAMP(3);
@@ -282,11 +291,11 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
         if (c == GROUP - 1) S.pre[GROUP] = wpre + inc;
         __syncthreads();
 
-        // ---- tile map (lane = entry of chunk 0): follow the chain, hopping over standard runs
-        if (c < 32) {
-            const uint32_t f = S.fm[c];
-            int e = (int)(f >> 10), cc = 1;
-            unsigned long long cnt = f & 1023;
+        // ---- tile record: every tile entry that is a boundary of P_0 continues as P_0 and leaves
+        // chunk 0 at x_0; from there follow the chain, hopping over standard runs
+        if (c == 0) {
+            int e = S.x[0], cc = 1;
+            unsigned long long cnt = 0;
             bool good = true;
             while (cc < nact) {
                 if (e == S.x[cc - 1]) {
@@ -304,8 +313,9 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
                     cc++;
                 }
             }
-            D.tmap[t * 32 + c] = good ? (((uint32_t)e << 26) | (uint32_t)(cnt & 0x3FFFFFFu)) : ((uint32_t)UNKE << 26);
-            D.fullmap[t * 32 + c] = ((f >> 10) << 26) | (f & 1023);
+            D.tmap[t * 4 + 0] = S.pm[0];
+            D.tmap[t * 4 + 1] = (uint32_t)S.n[0] | ((uint32_t)S.x[0] << 16) | ((uint32_t)(good ? e : UNKE) << 24);
+            D.tmap[t * 4 + 2] = (uint32_t)cnt;
         }
         // ---- chunk records for the decode kernel
         if (act) {
@@ -321,45 +331,55 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
 }
 
 // ------------------------------------------------------------------------------------------------
-// chain the tiles: entry_t = exit of tile t-1 at entry_{t-1}; base_t = exclusive prefix of counts
-__global__ __launch_bounds__(1024) void tile_scan_kernel(DecBufs D) {
+// chain the tiles.  Tile t's entry is tile t-1's exit, which is the same for every entry of tile
+// t-1 that is a boundary of its P_0 -- so all entries follow in parallel.  An entry that is not a P_0
+// boundary (P_0 had not synchronised by the tile start: rare) walks chunk 0 from global memory until
+// it merges with P_0; if it does not merge inside the chunk the exact path takes over.
+template <int CT>
+__device__ int walk_chunk0(const uint8_t* s, long long nbytes, const Params& P, long long cs, long long cend, int e,
+                           uint32_t pm0, int n0, int* cnt) {
+    BitReader A, B;
+    A.init(s, nbytes, cs + e);
+    B.init(s, nbytes, cs + (pm0 ? __ffs(pm0) - 1 : 32));
+    int ca = 0, cb = 0;
+    while (A.pos < cend) {
+        if (A.pos == B.pos) { *cnt = ca + n0 - cb; return 1; }
+        const bool sa = A.pos < B.pos || B.pos >= cend;
+        const uint32_t tk = sa ? A.peek() : B.peek();
+        const int len = token_len<CT>(tk, P);
+        if (sa) { A.skip(len); ca++; } else { B.skip(len); cb++; }
+    }
+    *cnt = ca;
+    return 0;
+}
+
+template <int CT>
+__global__ __launch_bounds__(1024) void tile_scan_kernel(const uint8_t* __restrict__ s, Params P, DecBufs D) {
     __shared__ unsigned long long part[1024];
-    __shared__ int anyunk;
     const Plan pl = *D.plan;
     const long long nt = pl.ngroups;
     const int tid = threadIdx.x;
-    if (tid == 0) anyunk = 0;
-    __syncthreads();
-    for (long long t = tid; t < nt; t += 1024) {
-        int e = 0;
-        if (t > 0) {
-            const uint32_t* m = D.tmap + (t - 1) * 32;
-            const uint32_t x0 = m[0] >> 26;
-            bool cst = true;
-            for (int k = 1; k < 32; k++) cst &= (m[k] >> 26) == x0;
-            e = (cst && x0 != UNKE) ? (int)x0 : UNKE;
-            if (e == UNKE) anyunk = 1;
-        }
-        D.tentry[t] = (uint8_t)e;
-    }
-    __syncthreads();
-    if (anyunk && tid == 0) {                       // rare: varying-exit tiles, chain serially
-        for (long long t = 1; t < nt; t++) {
-            if (D.tentry[t] != UNKE) continue;
-            const int pe = D.tentry[t - 1];
-            const uint32_t v = pe == UNKE ? ((uint32_t)UNKE << 26) : D.tmap[(t - 1) * 32 + pe];
-            D.tentry[t] = (uint8_t)(v >> 26);
-        }
-    }
-    __syncthreads();
     const long long per = (nt + 1023) / 1024;
     const long long t0 = tid * per, t1 = min(nt, t0 + per);
     unsigned long long sum = 0;
     for (long long t = t0; t < t1; t++) {
-        const int e = D.tentry[t];
-        const uint32_t v = e == UNKE ? ((uint32_t)UNKE << 26) : D.tmap[t * 32 + e];
-        if (e == UNKE || ((v >> 26) == UNKE && t + 1 < nt)) atomicOr(D.err, 8u);
-        sum += e == UNKE ? 0 : (v & 0x3FFFFFFu);
+        int e = 0;
+        if (t > 0) e = (int)(D.tmap[(t - 1) * 4 + 1] >> 24);
+        const uint32_t pm0 = D.tmap[t * 4 + 0], r1 = D.tmap[t * 4 + 1];
+        const int n0 = (int)(r1 & 0xFFFF);
+        int c0 = 0;
+        bool good = e != UNKE;
+        if (good && ((pm0 >> e) & 1u)) {
+            c0 = n0 - __popc(pm0 & ((1u << e) - 1u));
+        } else if (good) {
+            const long long cs = t * (long long)GROUP * CHUNK_BITS;
+            const long long cend = min((long long)pl.nbits, cs + CHUNK_BITS);
+            const bool merged = walk_chunk0<CT>(s, pl.nbytes, P, cs, cend, e, pm0, n0, &c0);
+            good = merged || cend >= (long long)pl.nbits;   // unmerged only if chunk 0 ends the stream
+        }
+        if (!good || ((r1 >> 24) == UNKE && t + 1 < nt)) { atomicOr(D.err, 8u); e = UNKE; c0 = 0; }
+        D.tentry[t] = (uint32_t)e | ((uint32_t)c0 << 8);
+        sum += (unsigned long long)c0 + (e == UNKE ? 0u : D.tmap[t * 4 + 2]);
     }
     part[tid] = sum;
     __syncthreads();
@@ -372,8 +392,8 @@ __global__ __launch_bounds__(1024) void tile_scan_kernel(DecBufs D) {
     unsigned long long run = part[tid] - sum;
     for (long long t = t0; t < t1; t++) {
         D.tbase[t] = run;
-        const int e = D.tentry[t];
-        run += e == UNKE ? 0 : (D.tmap[t * 32 + e] & 0x3FFFFFFu);
+        const uint32_t te = D.tentry[t];
+        run += (te >> 8) + ((te & 0xFF) == UNKE ? 0u : D.tmap[t * 4 + 2]);
     }
 }
 
@@ -411,10 +431,9 @@ struct DecodeShared {
             uint32_t pre[GROUP + 1];
             uint16_t stdcnt[GROUP], devcnt[GROUP];
             uint8_t x[GROUP], stdexit[GROUP], dev[GROUP];
-            uint32_t fm[32];
             uint64_t bad[GROUP / 64];
             uint32_t wsum[GROUP / 64];
-            int ein;
+            int ein, c0;
             unsigned long long base;
         } r;
         struct {                                   // carry scan
@@ -466,7 +485,10 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
         const bool act = c < nact;
         const int cs = c * CHUNK_BITS;
         const int cend = (int)min((long long)(cs + CHUNK_BITS), rem);
-        if (c == 0) { S.need = 0; S.cplx = 0; S.u.r.ein = D.tentry[t]; S.u.r.base = D.tbase[t]; }
+        if (c == 0) {
+            const uint32_t te = D.tentry[t];
+            S.need = 0; S.cplx = 0; S.u.r.ein = (int)(te & 0xFF); S.u.r.c0 = (int)(te >> 8); S.u.r.base = D.tbase[t];
+        }
         // ---- chunk records -> LDS; standard counts prefix; failure mask
         const uint32_t cm = act ? D.cmeta[gc] : 0u;
         const int scnt = (int)(cm & 1023);
@@ -475,7 +497,6 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
         S.u.r.stdcnt[c] = (uint16_t)scnt;
         S.u.r.stdexit[c] = (uint8_t)((cm >> 10) & 63);
         S.u.r.dev[c] = 0xFF;
-        if (c < 32) S.u.r.fm[c] = D.fullmap[t * 32 + c];
         const unsigned long long bm = __ballot(!ok);
         if (lane == 0) S.u.r.bad[wid] = bm;
         __syncthreads();
@@ -483,8 +504,7 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
         if (c == 0) {
             int e = S.u.r.ein;
             if (e != UNKE) {
-                const uint32_t f = S.u.r.fm[e];
-                e = (int)(f >> 26);
+                e = S.u.r.x[0];                            // chunk 0 ends on P_0 (tile_scan checked)
                 int cc = 1;
                 while (cc < nact) {
                     if (e == S.u.r.x[cc - 1]) {
@@ -507,7 +527,7 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
         const int ein = S.u.r.ein;
         int e = ein, tc = 0;
         if (ein != UNKE) {
-            if (c == 0) tc = (int)(S.u.r.fm[ein] & 0x3FFFFFFu);
+            if (c == 0) tc = S.u.r.c0;
             else if (S.u.r.dev[c] != 0xFF) { e = S.u.r.dev[c]; tc = S.u.r.devcnt[c]; }
             else { e = S.u.r.x[c - 1]; tc = scnt; }
         }
@@ -533,6 +553,7 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
         float f1 = -1.0f, f2 = -1.0f, f3 = -1.0f;
         int k1 = first ? 0 : 1, k2 = first ? 0 : 2, k3 = first ? 0 : 3;
         int pend = 0;
+        bool sent = false;
         if (act && e != UNKE) {
             OutBuf ob;
             ob.valid = 0; ob.base = -4;
@@ -550,6 +571,8 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
                 const int kind = code == 0 ? 0 : (code == 1 ? k1 : (code == 2 ? ((k1 | k2) ? 4 : 0) : ((k1 | k2 | k3) ? 4 : 0)));
                 if (kind == 0) { if (idx < (unsigned long long)num) ob.put(out, (long long)idx, v); }
                 else pend = j + 1;
+                // history sentinel (-1.0f) or a prediction before the stream's history is full: exact path
+                sent |= (kind == 0 && __float_as_uint(v) == 0xBF800000u) || (first && j < 3 && code != 0);
                 f3 = f2; k3 = k2; f2 = f1; k2 = k1; f1 = v; k1 = kind;
                 r.step(S.L, len);
                 j++;
@@ -557,6 +580,8 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
             }
             ob.flush(out);
         }
+        if (sent) atomicOr(D.err, 128u);
+        sent = false;
         if (!act || e == UNKE) { k1 = 1; k2 = 2; k3 = 3; }
         __syncthreads();                                   // resolution arrays are dead from here
         S.u.k.kd[0][0][c] = (uint8_t)k1; S.u.k.kd[0][1][c] = (uint8_t)k2; S.u.k.kd[0][2][c] = (uint8_t)k3;
@@ -659,11 +684,13 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
                 const uint32_t pat = token_pattern_bf<CT>(tk, len, P, &code);
                 const float v = code == 0 ? __uint_as_float(pat) : predict_value(code, g1, g2, g3);
                 if (k0 + jj < (unsigned long long)num) out[k0 + jj] = v;
+                sent |= __float_as_uint(v) == 0xBF800000u;
                 g3 = g2; g2 = g1; g1 = v;
                 r.step(S.L, len);
             }
         }
         if (act) { D.pend[gc] = (uint16_t)min(pend, 65535); D.done[gc] = pend ? 1 : 0; }
+        if (sent) atomicOr(D.err, 128u);
         __syncthreads();
         STAMP(11);
     }
@@ -703,7 +730,7 @@ extern "C" int dc_launch_decode_fast(const uint8_t* s, const unsigned long long*
     hipLaunchKernelGGL(plan_kernel_fast, dim3(1), dim3(1), 0, st, D->plan, dev_nbits, host_nbits, max_chunks);
     const int gparse = (int)std::min<long long>(max_groups > 0 ? max_groups : 1, 256 * 8);
     DC_DISPATCH_F(P->ct, parse_kernel, dim3(gparse), dim3(GROUP), 0, st, s, *P, *D);
-    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, st, *D);
+    DC_DISPATCH_F(P->ct, tile_scan_kernel, dim3(1), dim3(1024), 0, st, s, *P, *D);
     const int gdec = (int)std::min<long long>(max_groups > 0 ? max_groups : 1, 256 * 3);
     DC_DISPATCH_F(P->ct, decode_kernel_fast, dim3(gdec), dim3(GROUP), 0, st, s, *P, *D, out, num, epoch);
     return hipGetLastError() == hipSuccess ? 0 : -1;

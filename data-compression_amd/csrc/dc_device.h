@@ -67,7 +67,7 @@ __device__ __forceinline__ void make_token(float x, float b1, float b2, float b3
 // Decoder: token length from the next 32 stream bits (MSB-aligned).  At most 10 bits decide it.
 template <int CT>
 __device__ __forceinline__ int token_len(uint32_t t, const Params& P) {
-    if (CT == 6) return 9 + mbits(P.B, t >> 23);
+    if (CT == 6) return 9 + mbits(P.B, (t >> 23) & 0xFFu);
     if (t >> 31) return 3;
     if (CT == 11) return 32;
     if (CT == 7) {
@@ -158,10 +158,28 @@ __device__ __forceinline__ uint32_t token_pattern_bf(uint32_t t, int len, const 
     return c3 ? 0u : u;
 }
 
+// NaN results follow x86 SSE (the reference's host): the first NaN operand in evaluation order,
+// quieted; a NaN made from non-NaN operands (inf - inf) is the x86 default NaN 0xFFC00000.  Only
+// streams decoded outside the codec's domain ever reach this (an encoder never predicts with NaNs).
+__device__ __noinline__ float x86_nan(float b1, float b2, float b3, bool use3) {
+    const uint32_t q = 0x00400000u;
+    if (b1 != b1) return __uint_as_float(__float_as_uint(b1) | q);
+    if (b2 != b2) return __uint_as_float(__float_as_uint(b2) | q);
+    if (use3 && b3 != b3) return __uint_as_float(__float_as_uint(b3) | q);
+    return __uint_as_float(0xFFC00000u);
+}
+__device__ __forceinline__ float predict2(float b1, float b2) {
+    const float v = __fsub_rn(__fmul_rn(2.0f, b1), b2);
+    return v != v ? x86_nan(b1, b2, 0.0f, false) : v;
+}
+__device__ __forceinline__ float predict3(float b1, float b2, float b3) {
+    const float v = __fadd_rn(__fsub_rn(__fmul_rn(3.0f, b1), __fmul_rn(3.0f, b2)), b3);
+    return v != v ? x86_nan(b1, b2, b3, true) : v;
+}
 __device__ __forceinline__ float predict_value(int code, float b1, float b2, float b3) {
     if (code == 1) return b1;
-    if (code == 2) return __fsub_rn(__fmul_rn(2.0f, b1), b2);
-    return __fadd_rn(__fsub_rn(__fmul_rn(3.0f, b1), __fmul_rn(3.0f, b2)), b3);
+    if (code == 2) return predict2(b1, b2);
+    return predict3(b1, b2, b3);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -286,7 +286,7 @@ static int dec_ensure(long long max_chunks) {
     sz[15] = (size_t)GR * 6 * 8;          /* hist */
     sz[16] = (size_t)C * 4;               /* cmeta */
     sz[17] = (size_t)GR * 32 * 4;         /* tmap */
-    sz[18] = (size_t)GR;                  /* tentry */
+    sz[18] = (size_t)GR * 4;              /* tentry */
     sz[19] = (size_t)GR * 8;              /* tbase */
     size_t tot = 0;
     for (int i = 0; i < 20; i++) tot += (sz[i] + 255) & ~(size_t)255;
@@ -305,7 +305,7 @@ static int dec_ensure(long long max_chunks) {
     G.D.hist = (uint64_t*)ptr[15];
     G.D.cmeta = (uint32_t*)ptr[16];
     G.D.tmap = (uint32_t*)ptr[17];
-    G.D.tentry = (uint8_t*)ptr[18];
+    G.D.tentry = (uint32_t*)ptr[18];
     G.D.tbase = (unsigned long long*)ptr[19];
     G.D.fullmap = (uint32_t*)ptr[5];
     G.D.gran = (uint64_t*)ptr[6];
@@ -379,7 +379,7 @@ int dc_decode_finish(void) {
     rc = read_dec_err(&err);
     if (rc) return rc;
     if (!err) { G.dec_pending = 0; return DC_OK; }
-    if ((err & (8u | 64u)) && !(err & 16u) && G.dec_pending) {
+    if ((err & (8u | 64u)) && !(err & (16u | 128u)) && G.dec_pending) {
         /* outside the fast path's assumptions: exact multi-kernel path (closure rounds, then
          * complete entry maps for every chunk if an entry is still unresolved) */
         HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
@@ -399,9 +399,23 @@ int dc_decode_finish(void) {
             if (rc) return rc;
         }
     }
-    if ((err & 32u) && !(err & (8u | 16u)) && G.dec_pending) {
+    if ((err & 32u) && !(err & (8u | 16u | 128u)) && G.dec_pending) {
         HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
         if (dc_launch_fixup_serial(G.dec_s, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.st))
+            return seterr(DC_ERR_HIP, "decode launch failed");
+        rc = read_dec_err(&err);
+        if (rc) return rc;
+    }
+    if (!err && G.dec_pending) {            /* a slow path wrote values: check for the history sentinel */
+        if (dc_launch_find_sentinel(G.dec_out, G.dec_num, G.D.err, G.st))
+            return seterr(DC_ERR_HIP, "decode launch failed");
+        rc = read_dec_err(&err);
+        if (rc) return rc;
+    }
+    if ((err & 128u) && !(err & 16u) && G.dec_pending) {
+        /* -1.0f history sentinel in the stream: exact sequential decode (reference semantics) */
+        HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
+        if (dc_launch_decode_serial(G.dec_s, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.st))
             return seterr(DC_ERR_HIP, "decode launch failed");
         rc = read_dec_err(&err);
         if (rc) return rc;

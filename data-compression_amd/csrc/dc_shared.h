@@ -39,8 +39,8 @@ typedef struct DecBufs { /* decoder metadata, sized for the maximum chunk count 
     uint64_t* gran;      /* [group][33]  look-back granules (32 map entries + inclusive) */
     uint64_t* hist;      /* [group][6]   decoder-history look-back granules (3 aggregate + 3 final) */
     uint32_t* cmeta;     /* [chunk] standard count | std exit<<10 | extra entries<<16 | ok<<20 */
-    uint32_t* tmap;      /* [group][32] tile map: exit<<26 | token count */
-    uint8_t* tentry;     /* [group] true entry of the tile's first chunk */
+    uint32_t* tmap;      /* [group][4]  tile record: P_0 mask, n_0 | x_0<<16 | tile exit<<24, rest count */
+    uint32_t* tentry;    /* [group] true entry of the tile's first chunk | its token count << 8 */
     unsigned long long* tbase;   /* [group] first token index of the tile */
     uint8_t* entry;
     unsigned long long* tokoff;
@@ -75,6 +75,9 @@ int dc_launch_decode_more(const uint8_t* s, long long max_chunks, const DC_NS Pa
 int dc_launch_decode_fast(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
                           long long max_chunks, const DC_NS Params* P, const DC_NS DecBufs* D, float* out,
                           long long num, uint32_t epoch, dc_hip_stream st);
+int dc_launch_decode_serial(const uint8_t* s, const DC_NS Params* P, const DC_NS DecBufs* D, float* out,
+                            long long num, dc_hip_stream st);
+int dc_launch_find_sentinel(const float* out, long long num, unsigned* err, dc_hip_stream st);
 int dc_launch_fixup_serial(const uint8_t* s, const DC_NS Params* P, const DC_NS DecBufs* D, float* out,
                            long long num, dc_hip_stream st);
 long long dc_decode_chunk_bits(void);

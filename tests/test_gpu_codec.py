@@ -170,3 +170,26 @@ def test_negative_one_rejected(dc):
     import ctypes
     s, nb, pos = dc.compress(5, x)       # the ABI reports the error and leaves the stream untouched
     assert nb == 0
+
+
+@pytest.mark.parametrize("bound", [1e-3, 1e-6])
+@pytest.mark.parametrize("ct", CTS)
+def test_signed_inputs(dc, oracle, bound, ct):
+    """The ABI does not require toSmallDataset: negative values put a 1 sign bit into raw tokens
+    (and misaligned speculative parses read arbitrary sign bits)."""
+    dc.set_bound(bound)
+    rs = np.random.RandomState(7)
+    x = (rs.randn(400000) * 3).astype(np.float32)
+    x[x == -1.0] = 0.5
+    x[1000:1300] = x[1000]
+    t, m17 = oracle.type_mask(np.abs(x))
+    s, nb, pos = dc.compress(ct, x, t, m17)
+    so, nbo, poso = oracle.compress(ct, x, bound, t, m17)
+    assert nb == nbo and pos == poso and np.array_equal(s, so)
+    out = dc.decompress(ct, s, x.size, t, m17)
+    spec, got = oracle.decompress(ct, s, x.size, bound, t, m17)
+    if ct == 6:
+        assert got == x.size
+    # CT5/7/11: a sign bit parses as a 3-bit code, so the stream decodes to other values (and may end
+    # early); the reference decoder's output is still the contract
+    assert np.array_equal(out[:got].view(np.uint32), spec[:got].view(np.uint32))
