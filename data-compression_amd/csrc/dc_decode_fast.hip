@@ -155,9 +155,10 @@ struct ParseShared {
     uint32_t pm[GROUP];
     uint32_t pre[GROUP + 1];                   // exclusive prefix of the standard counts
     uint64_t bad[GROUP / 64];
-    uint16_t n[GROUP], stdcnt[GROUP];
-    uint8_t x[GROUP], nk[GROUP], stdexit[GROUP];
+    uint16_t n[GROUP], stdcnt[GROUP], devcnt[GROUP];
+    uint8_t x[GROUP], nk[GROUP], stdexit[GROUP], dev[GROUP];
     uint32_t wsum[GROUP / 64];
+    int texit;
 };
 
 __device__ __forceinline__ int next_bad(const uint64_t* bad, int c, int nact) {
@@ -291,31 +292,53 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
         if (c == GROUP - 1) S.pre[GROUP] = wpre + inc;
         __syncthreads();
 
-        // ---- tile record: every tile entry that is a boundary of P_0 continues as P_0 and leaves
-        // chunk 0 at x_0; from there follow the chain, hopping over standard runs
+        // ---- tile chain: every tile entry that is a boundary of P_0 continues as P_0 and leaves chunk 0
+        // at x_0; from there one lane follows the chain, hopping over standard runs and recording the
+        // chunks where it deviates from them
+        S.dev[c] = 0xFF;
+        __syncthreads();
         if (c == 0) {
             int e = S.x[0], cc = 1;
-            unsigned long long cnt = 0;
             bool good = true;
             while (cc < nact) {
                 if (e == S.x[cc - 1]) {
                     const int fb = next_bad(S.bad, cc, nact);
-                    cnt += S.pre[fb] - S.pre[cc];
                     if (fb >= nact) { e = S.x[nact - 1]; break; }
-                    cnt += S.stdcnt[fb];
                     e = S.stdexit[fb];
                     cc = fb + 1;
                 } else {
                     int ex, cn;
                     if (!lookup_entry(S, cc, e, &ex, &cn)) { good = false; break; }
-                    cnt += (unsigned long long)cn;
+                    S.dev[cc] = (uint8_t)e;
+                    S.devcnt[cc] = (uint16_t)cn;
                     e = ex;
                     cc++;
                 }
             }
+            S.texit = good ? e : UNKE;
+        }
+        __syncthreads();
+        // chain entry and token count of every chunk (chunk 0's depend on the tile entry: tile_fix)
+        const bool dv = S.dev[c] != 0xFF;
+        const int centry = c == 0 ? 0 : (dv ? S.dev[c] : S.x[c - 1]);
+        const uint32_t ccnt = (c == 0 || !act) ? 0u : (dv ? S.devcnt[c] : (uint32_t)scnt);
+        uint32_t inc2 = ccnt;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t tv = __shfl_up(inc2, d, 64);
+            if (lane >= d) inc2 += tv;
+        }
+        if (lane == 63) S.wsum[wid] = inc2;
+        __syncthreads();
+        uint32_t wp2 = 0;
+        for (int w = 0; w < wid; w++) wp2 += S.wsum[w];
+        if (act) {
+            D.entry[gc] = (uint8_t)centry;
+            D.tokoff[gc] = wp2 + inc2 - ccnt;                 // tile-relative, chunks 1..c-1
+        }
+        if (c == GROUP - 1) {
             D.tmap[t * 4 + 0] = S.pm[0];
-            D.tmap[t * 4 + 1] = (uint32_t)S.n[0] | ((uint32_t)S.x[0] << 16) | ((uint32_t)(good ? e : UNKE) << 24);
-            D.tmap[t * 4 + 2] = (uint32_t)cnt;
+            D.tmap[t * 4 + 1] = (uint32_t)S.n[0] | ((uint32_t)S.x[0] << 16) | ((uint32_t)S.texit << 24);
+            D.tmap[t * 4 + 2] = wp2 + inc2;                   // tokens of chunks 1..nact-1
         }
         // ---- chunk records for the decode kernel
         if (act) {
@@ -330,57 +353,123 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
     }
 }
 
-// ------------------------------------------------------------------------------------------------
-// chain the tiles.  Tile t's entry is tile t-1's exit, which is the same for every entry of tile
-// t-1 that is a boundary of its P_0 -- so all entries follow in parallel.  An entry that is not a P_0
-// boundary (P_0 had not synchronised by the tile start: rare) walks chunk 0 from global memory until
-// it merges with P_0; if it does not merge inside the chunk the exact path takes over.
-template <int CT>
-__device__ int walk_chunk0(const uint8_t* s, long long nbytes, const Params& P, long long cs, long long cend, int e,
-                           uint32_t pm0, int n0, int* cnt) {
-    BitReader A, B;
-    A.init(s, nbytes, cs + e);
-    B.init(s, nbytes, cs + (pm0 ? __ffs(pm0) - 1 : 32));
-    int ca = 0, cb = 0;
-    while (A.pos < cend) {
-        if (A.pos == B.pos) { *cnt = ca + n0 - cb; return 1; }
-        const bool sa = A.pos < B.pos || B.pos >= cend;
-        const uint32_t tk = sa ? A.peek() : B.peek();
-        const int len = token_len<CT>(tk, P);
-        if (sa) { A.skip(len); ca++; } else { B.skip(len); cb++; }
+// map of chunk gc at entry e from the parse kernel's global records
+__device__ __forceinline__ bool lookup_global(const DecBufs& D, long long gc, int e, int* ex, int* cn) {
+    const uint32_t pm = D.p_mask[gc];
+    if ((pm >> e) & 1u) { *ex = D.p_exit[gc]; *cn = D.p_cnt[gc] - __popc(pm & ((1u << e) - 1u)); return true; }
+    const int nk = (int)((D.cmeta[gc] >> 16) & 15);
+    for (int k = 0; k < nk; k++) {
+        const uint32_t v = D.map[gc * 32 + k];
+        if ((int)(v >> 16) == e) { *ex = (int)((v >> 10) & 63); *cn = (int)(v & 1023); return true; }
     }
-    *cnt = ca;
-    return 0;
+    return false;
 }
 
+// ------------------------------------------------------------------------------------------------
+// tile_fix: tile t's entry E is tile t-1's exit, which is the same for every entry of tile t-1 that
+// is a boundary of its P_0 -- so every tile's entry is known at once.  When E is not a boundary of
+// tile t's own P_0 (P_0 had not synchronised by the tile start: a few % of tiles), one wave stages the
+// tile's first chunks and walks from E, chunk by chunk, until it joins the tile chain; the walked
+// chunks get their entries and offsets overridden.  One wave per tile.
+constexpr int FIXW = 8;                                   // chunks a fix-up walk may cover
+struct FixShared {
+    uint32_t L[4][FIXW * LROW + 8];
+};
+
 template <int CT>
-__global__ __launch_bounds__(1024) void tile_scan_kernel(const uint8_t* __restrict__ s, Params P, DecBufs D) {
+__global__ __launch_bounds__(256) void tile_fix_kernel(const uint8_t* __restrict__ s, Params P, DecBufs D) {
+    __shared__ FixShared S;
+    const Plan pl = *D.plan;
+    const long long nt = pl.ngroups;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const long long t = (long long)blockIdx.x * 4 + wv;
+    if (t >= nt) return;
+    const int E = t == 0 ? 0 : (int)(D.tmap[(t - 1) * 4 + 1] >> 24);
+    const uint32_t pm0 = D.tmap[t * 4 + 0], r1 = D.tmap[t * 4 + 1];
+    const int n0 = (int)(r1 & 0xFFFF), x0 = (int)((r1 >> 16) & 0xFF), X = (int)(r1 >> 24);
+    const long long tbit = t * (long long)GROUP * CHUNK_BITS;
+    const long long rem = (long long)pl.nbits - tbit;
+    const int nact = (int)min((long long)GROUP, (rem + CHUNK_BITS - 1) / CHUNK_BITS);
+    if (E == UNKE || (X == UNKE && t + 1 < nt)) {
+        if (lane == 0) { atomicOr(D.err, 8u); D.tentry[t] = UNKE; D.tmap[t * 4 + 3] = 0; }
+        return;
+    }
+    if ((pm0 >> E) & 1u) {
+        if (lane == 0) {
+            D.tentry[t] = (uint32_t)E | ((uint32_t)(n0 - __popc(pm0 & ((1u << E) - 1u))) << 6);
+            D.tmap[t * 4 + 3] = 0;
+        }
+        return;
+    }
+    // rare: stage the first FIXW chunks of the tile (wave-local LDS), walk from E
+    uint32_t* L = S.L[wv];
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(s);
+    const long long nwfull = pl.nbytes >> 2;
+    for (int i = lane; i < FIXW * CW + 4; i += 64) {
+        const long long gw = (tbit >> 5) + i;
+        uint32_t v = 0;
+        if (gw < nwfull) v = __builtin_bswap32(w[gw]);
+        else if (4 * gw < pl.nbytes)
+            for (int k = 0; k < 4; k++) { const long long bi = 4 * gw + k; v = (v << 8) | (bi < pl.nbytes ? (uint32_t)s[bi] : 0u); }
+        L[i + (i >> 5)] = v;
+    }
+    __builtin_amdgcn_s_waitcnt(0);                      // the wave's own LDS stores land in order
+    __builtin_amdgcn_wave_barrier();
+    if (lane != 0) return;
+    const int cend0 = (int)min((long long)CHUNK_BITS, rem);
+    int ex, c0;
+    walk_lds<CT>(L, P, 0, cend0, E, pm0, x0, n0, &ex, &c0);
+    const long long g0 = t * GROUP;
+    int k = 1;
+    uint32_t acc = 0;
+    int kjoin = nact;
+    long long delta = 0;
+    bool ok = true;
+    while (k < nact) {
+        if (ex == (int)D.entry[g0 + k]) {                          // joined the tile chain
+            kjoin = k;
+            delta = (long long)acc - (long long)D.tokoff[g0 + k];
+            break;
+        }
+        if (k >= FIXW) { ok = false; break; }
+        const long long gk = g0 + k;
+        int nx, cn;
+        if (!lookup_global(D, gk, ex, &nx, &cn)) {
+            const int cs = k * CHUNK_BITS;
+            const int ce = (int)min((long long)(cs + CHUNK_BITS), rem);
+            walk_lds<CT>(L, P, cs, ce, ex, D.p_mask[gk], D.p_exit[gk], D.p_cnt[gk], &nx, &cn);
+        }
+        D.entry[gk] = (uint8_t)ex;
+        D.tokoff[gk] = acc;
+        acc += (uint32_t)cn;
+        ex = nx;
+        k++;
+    }
+    if (k == nact) {                                               // walked to the tile end
+        kjoin = nact;
+        delta = (long long)acc - (long long)D.tmap[t * 4 + 2];
+        if (ex != X && t + 1 < nt) ok = false;                       // the next tile's entry would change
+    }
+    if (!ok) { atomicOr(D.err, 8u); D.tentry[t] = UNKE; D.tmap[t * 4 + 3] = 0; return; }
+    D.tentry[t] = (uint32_t)E | ((uint32_t)c0 << 6) | ((uint32_t)kjoin << 16);
+    D.tmap[t * 4 + 3] = (uint32_t)(int)delta;
+}
+
+// tile_scan: first token index of every tile (one workgroup, block scan of the tile counts)
+__global__ __launch_bounds__(1024) void tile_scan_kernel(DecBufs D) {
     __shared__ unsigned long long part[1024];
     const Plan pl = *D.plan;
     const long long nt = pl.ngroups;
     const int tid = threadIdx.x;
     const long long per = (nt + 1023) / 1024;
     const long long t0 = tid * per, t1 = min(nt, t0 + per);
+    auto count = [&](long long t) -> unsigned long long {
+        const uint32_t te = D.tentry[t];
+        if ((te & 63) == UNKE) return 0ull;
+        return (unsigned long long)((te >> 6) & 1023) + (unsigned long long)((long long)D.tmap[t * 4 + 2] + (int)D.tmap[t * 4 + 3]);
+    };
     unsigned long long sum = 0;
-    for (long long t = t0; t < t1; t++) {
-        int e = 0;
-        if (t > 0) e = (int)(D.tmap[(t - 1) * 4 + 1] >> 24);
-        const uint32_t pm0 = D.tmap[t * 4 + 0], r1 = D.tmap[t * 4 + 1];
-        const int n0 = (int)(r1 & 0xFFFF);
-        int c0 = 0;
-        bool good = e != UNKE;
-        if (good && ((pm0 >> e) & 1u)) {
-            c0 = n0 - __popc(pm0 & ((1u << e) - 1u));
-        } else if (good) {
-            const long long cs = t * (long long)GROUP * CHUNK_BITS;
-            const long long cend = min((long long)pl.nbits, cs + CHUNK_BITS);
-            const bool merged = walk_chunk0<CT>(s, pl.nbytes, P, cs, cend, e, pm0, n0, &c0);
-            good = merged || cend >= (long long)pl.nbits;   // unmerged only if chunk 0 ends the stream
-        }
-        if (!good || ((r1 >> 24) == UNKE && t + 1 < nt)) { atomicOr(D.err, 8u); e = UNKE; c0 = 0; }
-        D.tentry[t] = (uint32_t)e | ((uint32_t)c0 << 8);
-        sum += (unsigned long long)c0 + (e == UNKE ? 0u : D.tmap[t * 4 + 2]);
-    }
+    for (long long t = t0; t < t1; t++) sum += count(t);
     part[tid] = sum;
     __syncthreads();
     for (int d = 1; d < 1024; d <<= 1) {           // inclusive Hillis-Steele over 1024 partial sums
@@ -392,8 +481,7 @@ __global__ __launch_bounds__(1024) void tile_scan_kernel(const uint8_t* __restri
     unsigned long long run = part[tid] - sum;
     for (long long t = t0; t < t1; t++) {
         D.tbase[t] = run;
-        const uint32_t te = D.tentry[t];
-        run += (te >> 8) + ((te & 0xFF) == UNKE ? 0u : D.tmap[t * 4 + 2]);
+        run += count(t);
     }
 }
 
@@ -427,15 +515,6 @@ struct OutBuf {
 struct DecodeShared {
     uint32_t L[LWORDS];
     union {
-        struct {                                   // entry resolution
-            uint32_t pre[GROUP + 1];
-            uint16_t stdcnt[GROUP], devcnt[GROUP];
-            uint8_t x[GROUP], stdexit[GROUP], dev[GROUP];
-            uint64_t bad[GROUP / 64];
-            uint32_t wsum[GROUP / 64];
-            int ein, c0;
-            unsigned long long base;
-        } r;
         struct {                                   // carry scan
             uint8_t kd[2][3][GROUP];
             float fv[2][3][GROUP];
@@ -453,24 +532,12 @@ __device__ __forceinline__ int hflag(uint64_t v, uint32_t epoch) {
     return (((v >> 40) & 0x3FFFFFu) == (epoch & 0x3FFFFFu)) ? (int)(v >> 62) : 0;
 }
 
-// map of chunk gc at entry e from the parse kernel's global records
-__device__ __forceinline__ bool lookup_global(const DecBufs& D, long long gc, int e, int* ex, int* cn) {
-    const uint32_t pm = D.p_mask[gc];
-    if ((pm >> e) & 1u) { *ex = D.p_exit[gc]; *cn = D.p_cnt[gc] - __popc(pm & ((1u << e) - 1u)); return true; }
-    const int nk = (int)((D.cmeta[gc] >> 16) & 15);
-    for (int k = 0; k < nk; k++) {
-        const uint32_t v = D.map[gc * 32 + k];
-        if ((int)(v >> 16) == e) { *ex = (int)((v >> 10) & 63); *cn = (int)(v & 1023); return true; }
-    }
-    return false;
-}
-
 template <int CT>
 __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __restrict__ s, Params P, DecBufs D,
                                                             float* __restrict__ out, long long num, uint32_t epoch) {
     __shared__ DecodeShared S;
     const Plan pl = *D.plan;
-    const int c = threadIdx.x, lane = c & 63, wid = c >> 6;
+    const int c = threadIdx.x;
     while (true) {
         if (c == 0) S.tile = (long long)atomicAdd(&D.ctr[4], 1u);
         __syncthreads();
@@ -485,66 +552,26 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
         const bool act = c < nact;
         const int cs = c * CHUNK_BITS;
         const int cend = (int)min((long long)(cs + CHUNK_BITS), rem);
-        if (c == 0) {
-            const uint32_t te = D.tentry[t];
-            S.need = 0; S.cplx = 0; S.u.r.ein = (int)(te & 0xFF); S.u.r.c0 = (int)(te >> 8); S.u.r.base = D.tbase[t];
-        }
-        // ---- chunk records -> LDS; standard counts prefix; failure mask
-        const uint32_t cm = act ? D.cmeta[gc] : 0u;
-        const int scnt = (int)(cm & 1023);
-        const bool ok = !act || c == 0 || ((cm >> 20) & 1u);
-        S.u.r.x[c] = act ? D.p_exit[gc] : 0;
-        S.u.r.stdcnt[c] = (uint16_t)scnt;
-        S.u.r.stdexit[c] = (uint8_t)((cm >> 10) & 63);
-        S.u.r.dev[c] = 0xFF;
-        const unsigned long long bm = __ballot(!ok);
-        if (lane == 0) S.u.r.bad[wid] = bm;
-        __syncthreads();
-        // ---- true chain through the tile (one lane, hopping over standard runs)
-        if (c == 0) {
-            int e = S.u.r.ein;
-            if (e != UNKE) {
-                e = S.u.r.x[0];                            // chunk 0 ends on P_0 (tile_scan checked)
-                int cc = 1;
-                while (cc < nact) {
-                    if (e == S.u.r.x[cc - 1]) {
-                        const int fb = next_bad(S.u.r.bad, cc, nact);
-                        if (fb >= nact) break;
-                        e = S.u.r.stdexit[fb];
-                        cc = fb + 1;
-                    } else {
-                        int ex, cn;
-                        if (!lookup_global(D, t * GROUP + cc, e, &ex, &cn)) { atomicOr(D.err, 8u); S.u.r.ein = UNKE; break; }
-                        S.u.r.dev[cc] = (uint8_t)e;
-                        S.u.r.devcnt[cc] = (uint16_t)cn;
-                        e = ex;
-                        cc++;
-                    }
-                }
+        if (c == 0) { S.need = 0; S.cplx = 0; }
+        // ---- entry and first token index of every chunk (parse kernel chain + tile_fix overrides)
+        const uint32_t te = D.tentry[t];
+        const int ein = (int)(te & 63), c0 = (int)((te >> 6) & 1023), kjoin = (int)(te >> 16);
+        int e = UNKE;
+        unsigned long long k0 = 0;
+        if (act && ein != UNKE) {
+            const unsigned long long base = D.tbase[t];
+            if (c == 0) {
+                e = ein;
+                k0 = base;
+            } else {
+                e = D.entry[gc];
+                const long long rel = (long long)D.tokoff[gc] + (c >= kjoin ? (long long)(int)D.tmap[t * 4 + 3] : 0ll);
+                k0 = base + (unsigned long long)(c0 + rel);
             }
+            D.entry[gc] = (uint8_t)e;
+            D.tokoff[gc] = k0;
         }
-        __syncthreads();
-        const int ein = S.u.r.ein;
-        int e = ein, tc = 0;
-        if (ein != UNKE) {
-            if (c == 0) tc = S.u.r.c0;
-            else if (S.u.r.dev[c] != 0xFF) { e = S.u.r.dev[c]; tc = S.u.r.devcnt[c]; }
-            else { e = S.u.r.x[c - 1]; tc = scnt; }
-        }
-        if (!act) tc = 0;
-        uint32_t inc2 = (uint32_t)tc;
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t tv = __shfl_up(inc2, d, 64);
-            if (lane >= d) inc2 += tv;
-        }
-        if (lane == 63) S.u.r.wsum[wid] = inc2;
-        __syncthreads();
-        uint32_t wp2 = 0;
-        for (int w = 0; w < wid; w++) wp2 += S.u.r.wsum[w];
-        const unsigned long long k0 = S.u.r.base + wp2 + inc2 - (uint32_t)tc;
-        if (act) { D.entry[gc] = (uint8_t)(ein == UNKE ? UNKE : e); D.tokoff[gc] = k0; }
-        if (act && ein == UNKE) atomicOr(D.err, 8u);
-        if (ein == UNKE) e = UNKE;
+        if (act && ein == UNKE) { D.entry[gc] = UNKE; atomicOr(D.err, 8u); }
         __syncthreads();
         STAMP(9);
 
@@ -730,7 +757,9 @@ extern "C" int dc_launch_decode_fast(const uint8_t* s, const unsigned long long*
     hipLaunchKernelGGL(plan_kernel_fast, dim3(1), dim3(1), 0, st, D->plan, dev_nbits, host_nbits, max_chunks);
     const int gparse = (int)std::min<long long>(max_groups > 0 ? max_groups : 1, 256 * 8);
     DC_DISPATCH_F(P->ct, parse_kernel, dim3(gparse), dim3(GROUP), 0, st, s, *P, *D);
-    DC_DISPATCH_F(P->ct, tile_scan_kernel, dim3(1), dim3(1024), 0, st, s, *P, *D);
+    DC_DISPATCH_F(P->ct, tile_fix_kernel, dim3((unsigned)((max_groups + 3) / 4 > 0 ? (max_groups + 3) / 4 : 1)), dim3(256), 0, st,
+                  s, *P, *D);
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, st, *D);
     const int gdec = (int)std::min<long long>(max_groups > 0 ? max_groups : 1, 256 * 3);
     DC_DISPATCH_F(P->ct, decode_kernel_fast, dim3(gdec), dim3(GROUP), 0, st, s, *P, *D, out, num, epoch);
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -379,6 +379,7 @@ int dc_decode_finish(void) {
     rc = read_dec_err(&err);
     if (rc) return rc;
     if (!err) { G.dec_pending = 0; return DC_OK; }
+    if (getenv("DC_DEBUG_ERR")) fprintf(stderr, "[dcamd] fast decode status 0x%x\n", err);
     if ((err & (8u | 64u)) && !(err & (16u | 128u)) && G.dec_pending) {
         /* outside the fast path's assumptions: exact multi-kernel path (closure rounds, then
          * complete entry maps for every chunk if an entry is still unresolved) */
