@@ -63,6 +63,49 @@ __device__ __forceinline__ void make_token(float x, float b1, float b2, float b3
     val = top; len = 9 + m;
 }
 
+// Branch-free form of make_token (selects only; same tokens).  For a CT7 masked token the exponent
+// equals the mask's, so its mantissa bit count is the uniform P.mm.
+template <int CT>
+__device__ __forceinline__ void make_token_bf(float x, float b1, float b2, float b3, bool predict, const Params& P,
+                                              uint32_t& val, int& len) {
+    const uint32_t u = __float_as_uint(x);
+    const int m = mbits(P.B, (u >> 23) & 0xFFu);
+    uint32_t v = CT == 11 ? u : (u >> (23 - m));
+    int l = CT == 11 ? 32 : 9 + m;
+    if (CT == 7) {
+        const bool msk = (u >> 23) == (P.mask17 >> 8);
+        const bool f1 = ((u >> 15) & 0xFFu) != (P.mask17 & 0xFFu);
+        const uint32_t head = ((1u << P.type) - 1u) << 1;
+        const int tl0 = P.mm0, tl1 = P.mm;
+        const uint32_t v0 = (head << tl0) | (v & ((1u << tl0) - 1u));
+        const uint32_t v1 = ((head | 1u) << tl1) | (v & ((1u << tl1) - 1u));
+        const uint32_t vm = f1 ? v1 : v0;
+        const int lm = P.type + 2 + (f1 ? tl1 : tl0);
+        v = msk ? vm : v;
+        l = msk ? lm : l;
+    }
+    if (CT != 6) {
+        const float p2 = __fsub_rn(__fmul_rn(2.0f, b1), b2);
+        const float p3 = __fadd_rn(__fsub_rn(__fmul_rn(3.0f, b1), __fmul_rn(3.0f, b2)), b3);
+        const float d1 = fabsf(__fsub_rn(b1, x));
+        const float d2 = fabsf(__fsub_rn(p2, x));
+        const float d3 = fabsf(__fsub_rn(p3, x));
+        const bool c2 = d2 < d1;
+        float dmin = c2 ? d2 : d1;
+        uint32_t code = c2 ? 6u : 5u;
+        const bool c3 = d3 < dmin;
+        dmin = c3 ? d3 : dmin;
+        code = c3 ? 7u : code;
+        const bool pr = predict && dmin <= P.thr_le;
+        const bool z = fabsf(x) <= P.thr_lt;
+        v = pr ? code : v;
+        v = z ? 4u : v;
+        l = (pr || z) ? 3 : l;
+    }
+    val = v;
+    len = l;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Decoder: token length from the next 32 stream bits (MSB-aligned).  At most 10 bits decide it.
 template <int CT>

@@ -1,31 +1,33 @@
-// dc_encode.hip -- single-pass bit-wise encoder for gfx950 (CT 5/6/7/11).
+// dc_encode.hip -- bit-wise encoder for gfx950 (CT 5/6/7/11).
 //
 // Replaces the per-element serial loop of myCompress_bitwise (impl/dataCompression.c:3310-3444),
 // myCompress_bitwise_np (:2645-2654), myCompress_bitwise_mask (:2030-2141) and
 // myCompress_bitwise_op (:577-696), whose cost is one add_bit_to_bytes call (+ realloc) per output
 // bit (:5456-5489).
 //
-// One workgroup = one tile of TPB*K consecutive floats.  The encoder history is the ORIGINAL input
-// (:2095-2097), so every token is a pure function of x[i-3..i]: each lane builds its K tokens from
-// registers, the workgroup scans the token lengths, and a decoupled look-back over per-tile
-// descriptors (64-bit granules: flag | epoch | bit count) gives the tile's global bit offset G.
-// Word ownership makes the stream race-free without atomics on HBM or a zero pass: a tile writes
-// every 32-bit word whose first bit lies in [G, G+T) and completes the last one with the first
-// <= 31 bits of the following elements (recomputed locally, <= 11 tokens).  Bits are assembled
-// MSB-first in LDS with ds_or and leave as byte-swapped dwords (stream byte 0 = MSB of word 0).
+// The encoder history is the ORIGINAL input (:2095-2097), so every token is a pure function of
+// x[i-3..i].  Three launches, no inter-workgroup waiting:
+//   encode_count_kernel : per tile of ENC_TILE floats, the total token bit length
+//   encode_scan_kernel  : exclusive scan of the tile lengths -> every tile's global bit offset G
+//   encode_write_kernel : tokens again, packed MSB-first into LDS at offset G mod 32 (lane-local
+//                         accumulation, ds_or only on the words two lanes share), then the tile
+//                         writes every 32-bit word whose first bit lies in [G, G+T) as byte-swapped
+//                         dwords, completing its last word with the first <= 31 bits of the
+//                         following elements (recomputed locally, <= 11 tokens).
+// The write kernel walks the tiles in reverse so the input the count kernel read last is still in
+// the 256 MiB Infinity Cache when it is read again.
 #include "dc_device.h"
+#include <algorithm>
 
 namespace dc {
 
-constexpr int ENC_TPB = 256;
-constexpr int ENC_K = 16;                       // floats per lane (4 x dwordx4)
-constexpr int ENC_TILE = ENC_TPB * ENC_K;       // 4096 floats per tile
+constexpr int ENC_TILE = 4096;                  // floats per tile (one offset per tile)
+constexpr int ENC_TPB = 256;                    // write kernel: 4 waves per tile
+constexpr int ENC_K = ENC_TILE / ENC_TPB;       // 16 consecutive floats per lane
+constexpr int ENC_Q = ENC_TILE / 4 / ENC_TPB;   // coalesced float4 loads per lane
+constexpr int CNT_Q = ENC_TILE / 4 / 64;        // count kernel: one wave per tile, 16 float4 per lane
 constexpr int ENC_LDS_WORDS = ENC_TILE + 48;    // 32 bits/elem max + offset + head slack
-
-// descriptor granule: [63:62] flag (1 aggregate, 2 inclusive) | [61:38] epoch | [37:0] bits
-__device__ __forceinline__ uint64_t enc_pack(uint64_t flag, uint32_t epoch, uint64_t v) {
-    return (flag << 62) | ((uint64_t)(epoch & 0xFFFFFFu) << 38) | (v & ((1ull << 38) - 1));
-}
+constexpr int STG_WORDS = ENC_TILE + ENC_TILE / 16 + 8;   // staged floats, one pad word per 16
 
 __device__ __forceinline__ void lds_place(uint32_t* s, uint32_t off, uint32_t val, int len) {
     const uint32_t w = off >> 5, b = off & 31u;
@@ -38,59 +40,190 @@ __device__ __forceinline__ void lds_place(uint32_t* s, uint32_t off, uint32_t va
     }
 }
 
+__device__ __forceinline__ float halo_x(const float* __restrict__ x, long long idx0, long long e) {
+    // element e - (its history) when it precedes the array: unused by make_token (predict = false)
+    return (idx0 + e >= 0 && e >= -3) ? x[e] : 0.0f;
+}
+
+template <int CT, bool FULL>
+__device__ __forceinline__ void count_tokens(const float4* f, float h1, float h2, float h3, long long tb, long long n,
+                                             long long idx0, const Params& P, uint32_t& sum, bool& neg1) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int q = 0; q < CNT_Q; q++) {
+        const float p1 = __shfl_up(f[q].w, 1, 64), p2 = __shfl_up(f[q].z, 1, 64), p3 = __shfl_up(f[q].y, 1, 64);
+        const float b1 = lane ? p1 : h1, b2 = lane ? p2 : h2, b3 = lane ? p3 : h3;
+        h1 = __shfl(f[q].w, 63, 64); h2 = __shfl(f[q].z, 63, 64); h3 = __shfl(f[q].y, 63, 64);
+        const long long e = tb + 4 * (lane + 64 * q);
+        const float xs[7] = {b3, b2, b1, f[q].x, f[q].y, f[q].z, f[q].w};
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            uint32_t val;
+            int len;
+            make_token_bf<CT>(xs[3 + r], xs[2 + r], xs[1 + r], xs[r], FULL || idx0 + e + r >= 3, P, val, len);
+            const bool in = FULL || e + r < n;
+            sum += in ? (uint32_t)len : 0u;
+            neg1 |= in && (xs[3 + r] == -1.0f);
+        }
+    }
+}
+
+// count kernel: one wave per tile; lane i holds float4 number i + 64q (q < CNT_Q), so every load
+// instruction reads 1 KiB contiguous.  The history of a float4 is the previous float4: lane i-1's
+// (same q) or, for lane 0, lane 63's of q-1.
 template <int CT>
-__global__ __launch_bounds__(ENC_TPB) void encode_kernel(
+__global__ __launch_bounds__(256) void encode_count_kernel(const float* __restrict__ x, long long n, long long idx0,
+                                                           Params P, uint32_t* __restrict__ tbits, long long ntiles,
+                                                           unsigned* __restrict__ err) {
+    const int lane = threadIdx.x & 63;
+    for (long long tile = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); tile < ntiles; tile += (long long)gridDim.x * 4) {
+    const long long tb = tile * ENC_TILE;
+    float4 f[CNT_Q];
+    if (tb + ENC_TILE <= n) {
+        const float4* p4 = reinterpret_cast<const float4*>(x + tb);
+#pragma unroll
+        for (int q = 0; q < CNT_Q; q++) f[q] = p4[lane + 64 * q];
+    } else {
+#pragma unroll
+        for (int q = 0; q < CNT_Q; q++) {
+            const long long e = tb + 4 * (lane + 64 * q);
+            f[q].x = e < n ? x[e] : 0.0f; f[q].y = e + 1 < n ? x[e + 1] : 0.0f;
+            f[q].z = e + 2 < n ? x[e + 2] : 0.0f; f[q].w = e + 3 < n ? x[e + 3] : 0.0f;
+        }
+    }
+    const bool full = tb + ENC_TILE <= n && idx0 + tb >= 3;         // no bounds / history checks
+    float h1 = lane == 0 ? halo_x(x, idx0, tb - 1) : 0.0f;          // q = 0 history of lane 0
+    float h2 = lane == 0 ? halo_x(x, idx0, tb - 2) : 0.0f;
+    float h3 = lane == 0 ? halo_x(x, idx0, tb - 3) : 0.0f;
+    uint32_t sum = 0;
+    bool neg1 = false;
+    if (full) count_tokens<CT, true>(f, h1, h2, h3, tb, n, idx0, P, sum, neg1);
+    else count_tokens<CT, false>(f, h1, h2, h3, tb, n, idx0, P, sum, neg1);
+    if (CT != 6 && __any(neg1) && lane == 0) atomicOr(err, 1u);    // -1.0f is the reference's sentinel
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
+    if (lane == 0) tbits[tile] = sum;
+    }
+}
+
+// exclusive scan of the 32-bit tile lengths (one workgroup, staged through LDS in chunks of SCAN_CH
+// tiles with coalesced loads); toff[t] = tile t's global bit offset
+constexpr int SCAN_CH = 16384;
+__global__ __launch_bounds__(1024) void encode_scan_kernel(const uint32_t* __restrict__ tbits, uint64_t* __restrict__ toff,
+                                                           long long ntiles, int start_bit,
+                                                           unsigned long long* __restrict__ total_bits) {
+    __shared__ uint32_t cnt[SCAN_CH];
+    __shared__ unsigned long long part[1024];
+    __shared__ unsigned long long carry;
+    const int tid = threadIdx.x;
+    if (tid == 0) carry = (unsigned long long)start_bit;
+    constexpr int PER = SCAN_CH / 1024;
+    for (long long c0 = 0; c0 < ntiles; c0 += SCAN_CH) {
+        const int m = (int)min((long long)SCAN_CH, ntiles - c0);
+        for (int i = tid; i < SCAN_CH; i += 1024) cnt[i] = i < m ? tbits[c0 + i] : 0u;
+        __syncthreads();
+        unsigned long long sum = 0;
+#pragma unroll
+        for (int k = 0; k < PER; k++) sum += cnt[tid * PER + k];
+        part[tid] = sum;
+        __syncthreads();
+        for (int d = 1; d < 1024; d <<= 1) {
+            const unsigned long long v = tid >= d ? part[tid - d] : 0ull;
+            __syncthreads();
+            part[tid] += v;
+            __syncthreads();
+        }
+        unsigned long long run = carry + part[tid] - sum;
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const int i = tid * PER + k;
+            const unsigned long long b = cnt[i];
+            if (i < m) toff[c0 + i] = run;
+            run += b;
+        }
+        __syncthreads();
+        if (tid == 1023) carry += part[1023];
+        __syncthreads();
+    }
+    if (tid == 0) *total_bits = carry;
+}
+
+template <int CT>
+__global__ __launch_bounds__(ENC_TPB) void encode_write_kernel(
     const float* __restrict__ x, long long n, long long idx0, Params P, uint32_t* __restrict__ out,
-    uint64_t* __restrict__ desc, unsigned* __restrict__ tile_ctr, unsigned ntiles, uint32_t epoch,
-    int start_bit, unsigned long long* __restrict__ total_bits, unsigned* __restrict__ err) {
-    __shared__ uint32_t s_bits[ENC_LDS_WORDS];
+    const uint64_t* __restrict__ toff, unsigned ntiles, unsigned long long* __restrict__ dbg) {
+    __shared__ uint32_t s_bits[STG_WORDS > ENC_LDS_WORDS ? STG_WORDS : ENC_LDS_WORDS];   // staging, then bits
     __shared__ uint32_t s_wsum[ENC_TPB / 64];
-    __shared__ unsigned s_tile;
-    __shared__ unsigned long long s_G;
     __shared__ uint32_t s_head_val[12];
     __shared__ int s_head_len[12];
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    if (tid == 0) s_tile = atomicInc(tile_ctr, ntiles - 1);       // dynamic id: predecessors run
-    for (int i = tid; i < ENC_LDS_WORDS; i += ENC_TPB) s_bits[i] = 0u;
-    __syncthreads();
-    const unsigned tile = s_tile;
+    for (unsigned k = blockIdx.x; k < ntiles; k += gridDim.x) {
+    const unsigned tile = ntiles - 1 - k;
+#define ESTAMP(ph) do { if (dbg && tid == 0 && tile < 8192) dbg[tile * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+    ESTAMP(0);
     const long long tbase = (long long)tile * ENC_TILE;
     const long long base = tbase + (long long)tid * ENC_K;
-
-    // ---- load K floats + 3-float halo (history = original inputs)
-    float v[ENC_K + 4];
-    if (base + ENC_K <= n) {
-        const float4* p4 = reinterpret_cast<const float4*>(x + base);
+    const unsigned long long G = toff[tile];
+    const bool full = tbase + ENC_TILE <= n && idx0 + tbase >= 3;
+    // ---- coalesced float4 loads -> LDS (one pad word per 16 floats), then 16 consecutive per lane
+    {
+        float4 f[ENC_Q];
+        if (tbase + ENC_TILE <= n) {
+            const float4* p4 = reinterpret_cast<const float4*>(x + tbase);
 #pragma unroll
-        for (int q = 0; q < ENC_K / 4; q++) {
-            const float4 t = p4[q];
-            v[4 + 4 * q] = t.x; v[5 + 4 * q] = t.y; v[6 + 4 * q] = t.z; v[7 + 4 * q] = t.w;
+            for (int q = 0; q < ENC_Q; q++) f[q] = p4[tid + ENC_TPB * q];
+        } else {
+#pragma unroll
+            for (int q = 0; q < ENC_Q; q++) {
+                const long long e = tbase + 4 * (tid + ENC_TPB * q);
+                f[q].x = e < n ? x[e] : 0.0f; f[q].y = e + 1 < n ? x[e + 1] : 0.0f;
+                f[q].z = e + 2 < n ? x[e + 2] : 0.0f; f[q].w = e + 3 < n ? x[e + 3] : 0.0f;
+            }
         }
-    } else {
 #pragma unroll
-        for (int j = 0; j < ENC_K; j++) v[4 + j] = (base + j < n) ? x[base + j] : 0.0f;
+        for (int q = 0; q < ENC_Q; q++) {
+            const int e = 4 * (tid + ENC_TPB * q);
+            float* d = reinterpret_cast<float*>(s_bits) + 8 + e + (e >> 4);
+            d[0] = f[q].x; d[1] = f[q].y; d[2] = f[q].z; d[3] = f[q].w;
+        }
+        if (tid < 3) reinterpret_cast<float*>(s_bits)[5 + tid] = halo_x(x, idx0, tbase - 3 + tid);
     }
-    const long long gbase = idx0 + base;                          // global element index
+    __syncthreads();
+    float v[ENC_K + 4];
 #pragma unroll
-    for (int j = 1; j <= 3; j++) v[4 - j] = (gbase - j >= 0 && base - j > -4) ? x[base - j] : 0.0f;
+    for (int j = 1; j < ENC_K + 4; j++) {
+        const int e = tid * ENC_K + j - 4;                           // tile-relative element (>= -3)
+        v[j] = reinterpret_cast<const float*>(s_bits)[e < 0 ? 8 + e : 8 + e + (e >> 4)];
+    }
+    __syncthreads();
+    for (int i = tid; i < ENC_LDS_WORDS; i += ENC_TPB) s_bits[i] = 0u;
 
     // ---- tokens
     uint32_t tv[ENC_K];
-    int tl[ENC_K];
-    uint32_t mysum = 0;
-    bool neg1 = false;
+    uint32_t tlp[ENC_K / 4];                                         // token lengths, 4 per register
 #pragma unroll
-    for (int j = 0; j < ENC_K; j++) {
-        if (base + j < n) {
-            make_token<CT>(v[4 + j], v[3 + j], v[2 + j], v[1 + j], gbase + j >= 3, P, tv[j], tl[j]);
-            neg1 |= (v[4 + j] == -1.0f);
-        } else {
-            tv[j] = 0u; tl[j] = 0;
+    for (int q = 0; q < ENC_K / 4; q++) tlp[q] = 0u;
+    uint32_t mysum = 0;
+    if (full) {
+#pragma unroll
+        for (int j = 0; j < ENC_K; j++) {
+            int len;
+            make_token_bf<CT>(v[4 + j], v[3 + j], v[2 + j], v[1 + j], true, P, tv[j], len);
+            tlp[j >> 2] |= (uint32_t)len << (8 * (j & 3));
+            mysum += (uint32_t)len;
         }
-        mysum += (uint32_t)tl[j];
+    } else {
+#pragma unroll
+        for (int j = 0; j < ENC_K; j++) {
+            int len;
+            make_token_bf<CT>(v[4 + j], v[3 + j], v[2 + j], v[1 + j], idx0 + base + j >= 3, P, tv[j], len);
+            len = base + j < n ? len : 0;
+            tlp[j >> 2] |= (uint32_t)len << (8 * (j & 3));
+            mysum += (uint32_t)len;
+        }
     }
-    if (CT != 6 && neg1) atomicOr(err, 1u);                      // -1.0f is the reference's sentinel
+    ESTAMP(1);
 
     // ---- workgroup exclusive scan of bit lengths
     uint32_t inc = mysum;
@@ -102,16 +235,12 @@ __global__ __launch_bounds__(ENC_TPB) void encode_kernel(
     if (lane == 63) s_wsum[wid] = inc;
 
     // ---- head: first <= 31 bits of the elements after this tile (completes our last word)
-    const long long nb = tbase + ENC_TILE;                         // first element of next tile
+    const long long nb = tbase + ENC_TILE;
     if (wid == 1 && lane < 12) {
         uint32_t hv = 0u; int hl = 0;
         const long long e = nb + lane;
-        if (lane < 11 && e < n) {
-            const long long ge = idx0 + e;
-            const float xe = x[e];
-            const float e1 = x[e - 1], e2 = x[e - 2], e3 = x[e - 3];
-            make_token<CT>(xe, e1, e2, e3, ge >= 3, P, hv, hl);
-        }
+        if (lane < 11 && e < n)
+            make_token<CT>(x[e], x[e - 1], x[e - 2], x[e - 3], idx0 + e >= 3, P, hv, hl);
         s_head_val[lane] = hv;
         s_head_len[lane] = hl;
     }
@@ -122,68 +251,37 @@ __global__ __launch_bounds__(ENC_TPB) void encode_kernel(
         if (w < wid) wpre += s_wsum[w];
         T += s_wsum[w];
     }
-    const uint32_t excl = wpre + inc - mysum;
-
-    // ---- decoupled look-back for the tile's global bit offset
-    if (wid == 0) {
-        unsigned long long G = 0;
-        if (tile == 0) {
-            if (lane == 0) st_relaxed(&desc[0], enc_pack(2, epoch, (uint64_t)start_bit + T));
-            G = (unsigned long long)start_bit;
-        } else {
-            if (lane == 0) st_relaxed(&desc[tile], enc_pack(1, epoch, T));
-            long long look = (long long)tile - 1;
-            unsigned long long acc = 0;
-            while (true) {
-                const long long pred = look - lane;
-                uint64_t d = 0;
-                int flag = 2;
-                uint64_t val = 0;
-                if (pred >= 0) {
-                    unsigned spins = 0;
-                    do {
-                        d = ld_relaxed(&desc[pred]);
-                        flag = (((d >> 38) & 0xFFFFFFu) == (epoch & 0xFFFFFFu)) ? (int)(d >> 62) : 0;
-                        if (flag == 0) __builtin_amdgcn_s_sleep(1);
-                    } while (flag == 0 && ++spins < (1u << 26));
-                    val = d & ((1ull << 38) - 1);
-                    if (flag == 0) { atomicOr(err, 2u); flag = 2; val = 0; }   // bounded spin
-                }
-                const unsigned long long incl_mask = __ballot(flag == 2);
-                if (incl_mask) {
-                    const int k = __ffsll((long long)incl_mask) - 1;       // most recent inclusive
-                    uint64_t part = (lane <= k) ? val : 0;
-#pragma unroll
-                    for (int d2 = 32; d2 >= 1; d2 >>= 1) part += __shfl_xor(part, d2, 64);
-                    acc += part;
-                    break;
-                }
-                uint64_t part = val;
-#pragma unroll
-                for (int d2 = 32; d2 >= 1; d2 >>= 1) part += __shfl_xor(part, d2, 64);
-                acc += part;
-                look -= 64;
-            }
-            G = acc;
-            if (lane == 0) st_relaxed(&desc[tile], enc_pack(2, epoch, G + T));
-        }
-        if (lane == 0) {
-            s_G = G;
-            if (tile == ntiles - 1) *total_bits = G + T;
-        }
-    }
-    __syncthreads();
-    const unsigned long long G = s_G;
     const uint32_t boff = (uint32_t)(G & 31ull);
     const long long wb = (long long)(G >> 5);
+    ESTAMP(2);
 
-    // ---- assemble MSB-first in LDS
-    uint32_t off = boff + excl;
+    // ---- lane-local MSB-first packing: full words are plain LDS stores, the first and last word
+    // of the lane's bit range (shared with the neighbouring lanes) are ds_or
+    {
+        const uint32_t off = boff + wpre + inc - mysum;
+        uint32_t w = off >> 5;
+        int nin = (int)(off & 31u);                                   // bits already in the current word
+        bool shared = nin != 0;
+        uint64_t acc = 0;
 #pragma unroll
-    for (int j = 0; j < ENC_K; j++) {
-        if (tl[j]) lds_place(s_bits, off, tv[j], tl[j]);
-        off += (uint32_t)tl[j];
+        for (int j = 0; j < ENC_K; j++) {
+            const int len = (int)((tlp[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+            if (len) {
+                acc |= (uint64_t)tv[j] << (64 - nin - len);
+                nin += len;
+                if (nin >= 32) {
+                    const uint32_t word = (uint32_t)(acc >> 32);
+                    if (shared) atomicOr(&s_bits[w], word); else s_bits[w] = word;
+                    shared = false;
+                    acc <<= 32;
+                    nin -= 32;
+                    w++;
+                }
+            }
+        }
+        if (nin > 0) atomicOr(&s_bits[w], (uint32_t)(acc >> 32));
     }
+    __syncthreads();
     if (tid == 0) {
         uint32_t ho = boff + T;
         for (int j = 0; j < 11 && s_head_len[j]; j++) {
@@ -193,31 +291,48 @@ __global__ __launch_bounds__(ENC_TPB) void encode_kernel(
         }
     }
     __syncthreads();
+    ESTAMP(3);
 
     // ---- write owned words: first bit in [G, G+T) (tile 0 also owns the start_bit prefix word)
     const unsigned long long Gend = G + T;
     long long w0 = (long long)((G + 31) >> 5);
     if (tile == 0) w0 = 0;
     const long long w1 = (long long)((Gend + 31) >> 5);
-    for (long long w = w0 + tid; w < w1; w += ENC_TPB)
-        out[w] = __builtin_bswap32(s_bits[w - wb]);
+    for (long long w = w0 + tid; w < w1; w += ENC_TPB) out[w] = __builtin_bswap32(s_bits[w - wb]);
+    ESTAMP(4);
+    ESTAMP(5);
+    __syncthreads();                                                 // s_bits is restaged next tile
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
+#define DC_ENC_DISPATCH(KER, ...)                                                                  \
+    switch (P->ct) {                                                                               \
+        case 5: hipLaunchKernelGGL(KER<5>, __VA_ARGS__); break;                                    \
+        case 6: hipLaunchKernelGGL(KER<6>, __VA_ARGS__); break;                                    \
+        case 7: hipLaunchKernelGGL(KER<7>, __VA_ARGS__); break;                                    \
+        case 11: hipLaunchKernelGGL(KER<11>, __VA_ARGS__); break;                                  \
+        default: return -2;                                                                        \
+    }
+
 extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, const Params* P,
                                 uint32_t* out, uint64_t* desc, unsigned* tile_ctr, uint32_t epoch,
                                 int start_bit, unsigned long long* total_bits, unsigned* err,
-                                hipStream_t stream) {
+                                unsigned long long* dbg, hipStream_t stream) {
+    (void)tile_ctr;
+    (void)epoch;
     if (n <= 0) return 0;
     const unsigned ntiles = (unsigned)((n + ENC_TILE - 1) / ENC_TILE);
-    dim3 grid(ntiles), block(ENC_TPB);
-    switch (P->ct) {
-        case 5: hipLaunchKernelGGL(encode_kernel<5>, grid, block, 0, stream, x, n, idx0, *P, out, desc, tile_ctr, ntiles, epoch, start_bit, total_bits, err); break;
-        case 6: hipLaunchKernelGGL(encode_kernel<6>, grid, block, 0, stream, x, n, idx0, *P, out, desc, tile_ctr, ntiles, epoch, start_bit, total_bits, err); break;
-        case 7: hipLaunchKernelGGL(encode_kernel<7>, grid, block, 0, stream, x, n, idx0, *P, out, desc, tile_ctr, ntiles, epoch, start_bit, total_bits, err); break;
-        case 11: hipLaunchKernelGGL(encode_kernel<11>, grid, block, 0, stream, x, n, idx0, *P, out, desc, tile_ctr, ntiles, epoch, start_bit, total_bits, err); break;
-        default: return -2;
-    }
+    uint32_t* tbits = reinterpret_cast<uint32_t*>(desc + ntiles);     // desc holds 2 * ntiles words
+    // one wave (count) / one workgroup (write) per tile: measured faster than persistent grids here
+    const unsigned gc = (ntiles + 3) / 4;
+    const unsigned gw = ntiles;
+    DC_ENC_DISPATCH(encode_count_kernel, dim3(gc), dim3(256), 0, stream, x, n, idx0, *P, tbits,
+                    (long long)ntiles, err);
+    hipLaunchKernelGGL(encode_scan_kernel, dim3(1), dim3(1024), 0, stream, tbits, desc, (long long)ntiles, start_bit,
+                       total_bits);
+    DC_ENC_DISPATCH(encode_write_kernel, dim3(gw), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, desc, ntiles,
+                    dbg);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -34,6 +34,7 @@ typedef struct {
     /* encoder */
     uint64_t* enc_desc;
     long long enc_desc_cap;
+    unsigned long long* enc_dbg;   /* DC_DEBUG_STAMPS: [tile][8] encoder phase stamps */
     unsigned* enc_ctr;
     unsigned long long* d_total;
     unsigned* d_enc_err;
@@ -92,6 +93,14 @@ int dc_debug_stamps(unsigned long long* host, long long n) {
     if (n > 4096 * 16) n = 4096 * 16;
     HIPCHK(hipStreamSynchronize(G.st));
     HIPCHK(hipMemcpy(host, G.D.dbg, (size_t)n * 8, hipMemcpyDeviceToHost));
+    return DC_OK;
+}
+
+int dc_debug_enc_stamps(unsigned long long* host, long long n) {
+    if (!G.enc_dbg) return DC_ERR_ARG;
+    if (n > 8192 * 8) n = 8192 * 8;
+    HIPCHK(hipStreamSynchronize(G.st));
+    HIPCHK(hipMemcpy(host, G.enc_dbg, (size_t)n * 8, hipMemcpyDeviceToHost));
     return DC_OK;
 }
 
@@ -216,9 +225,9 @@ int dc_encode_device(int ct, const void* d_x, long long n, long long idx0, int t
     Params P;
     make_params(&P, ct, type, mask17);
     long long ntiles = dc_encode_tile_count(n);
-    if (ntiles > G.enc_desc_cap) {
+    if (2 * ntiles + 8 > G.enc_desc_cap) {
         if (G.enc_desc) HIPCHK(hipFree(G.enc_desc));
-        long long cap = ntiles + 1024;
+        long long cap = 2 * ntiles + 1024;
         HIPCHK(hipMalloc((void**)&G.enc_desc, cap * sizeof(uint64_t)));
         HIPCHK(hipMemsetAsync(G.enc_desc, 0, cap * sizeof(uint64_t), G.st));
         G.enc_desc_cap = cap;
@@ -235,8 +244,12 @@ int dc_encode_device(int ct, const void* d_x, long long n, long long idx0, int t
         if (tot != G.d_total) HIPCHK(hipMemcpyAsync(G.d_total, &v, sizeof v, hipMemcpyHostToDevice, G.st));
         return DC_OK;
     }
+    if (getenv("DC_DEBUG_STAMPS") && !G.enc_dbg) {
+        HIPCHK(hipMalloc((void**)&G.enc_dbg, 8192 * 8 * 8));
+        HIPCHK(hipMemset(G.enc_dbg, 0, 8192 * 8 * 8));
+    }
     if (dc_launch_encode((const float*)d_x, n, idx0, &P, (uint32_t*)d_out, G.enc_desc, G.enc_ctr, G.enc_epoch,
-                         start_bit, tot, G.d_enc_err, G.st))
+                         start_bit, tot, G.d_enc_err, G.enc_dbg, G.st))
         return seterr(DC_ERR_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (tot != G.d_total) HIPCHK(hipMemcpyAsync(G.d_total, tot, 8, hipMemcpyDeviceToDevice, G.st));
     return DC_OK;
