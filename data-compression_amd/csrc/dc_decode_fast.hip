@@ -29,7 +29,7 @@ namespace dc {
 
 constexpr int LROW = 33;                       // padded LDS row (words) per chunk
 constexpr int LWORDS = (GROUP + 1) * LROW;     // + one row for the words after the tile
-constexpr int OV = 512;                        // overlap: P_c starts OV bits before its chunk
+constexpr int OV = 1024;                       // overlap: P_c starts OV bits before its chunk
 constexpr int OVW = OV / 32;
 constexpr int PWORDS = LWORDS + OVW + OVW / 32;
 constexpr int KMAX = 6;                        // extra known entries per chunk (besides P_c's own)
@@ -588,12 +588,13 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
             r.init(S.L, cs + e);
             unsigned long long idx = k0;
             int j = 0;
-            while (r.pos < cend) {
+            // phase A: history still (partly) symbolic, or the stream's first three tokens
+            while (r.pos < cend && ((k1 | k2 | k3) != 0 || (first && j < 3))) {
                 const uint32_t tk = r.peek();
                 const int len = token_len_bf<CT>(tk, P);
                 int code;
                 const uint32_t pat = token_pattern_bf<CT>(tk, len, P, &code);
-                const float p2 = predict_value(2, f1, f2, f3), p3 = predict_value(3, f1, f2, f3);
+                const float p2 = predict2(f1, f2), p3 = predict3(f1, f2, f3);
                 const float v = code == 0 ? __uint_as_float(pat) : (code == 1 ? f1 : (code == 2 ? p2 : p3));
                 const int kind = code == 0 ? 0 : (code == 1 ? k1 : (code == 2 ? ((k1 | k2) ? 4 : 0) : ((k1 | k2 | k3) ? 4 : 0)));
                 if (kind == 0) { if (idx < (unsigned long long)num) ob.put(out, (long long)idx, v); }
@@ -603,6 +604,23 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
                 f3 = f2; k3 = k2; f2 = f1; k2 = k1; f1 = v; k1 = kind;
                 r.step(S.L, len);
                 j++;
+                idx++;
+            }
+            // phase B: concrete history (kinds stay 0 from here on)
+            while (r.pos < cend) {
+                const uint32_t tk = r.peek();
+                const int len = token_len_bf<CT>(tk, P);
+                int code;
+                const uint32_t pat = token_pattern_bf<CT>(tk, len, P, &code);
+                float v = code == 0 ? __uint_as_float(pat) : f1;
+                if (__builtin_expect(__any(code >= 2), 0)) {                 // predictions: wave-uniform branch
+                    const float p2 = predict2(f1, f2), p3 = predict3(f1, f2, f3);
+                    v = code == 2 ? p2 : (code == 3 ? p3 : v);
+                }
+                if (idx < (unsigned long long)num) ob.put(out, (long long)idx, v);
+                sent |= __float_as_uint(v) == 0xBF800000u;
+                f3 = f2; f2 = f1; f1 = v;
+                r.step(S.L, len);
                 idx++;
             }
             ob.flush(out);
