@@ -487,34 +487,46 @@ __global__ __launch_bounds__(1024) void tile_scan_kernel(DecBufs D) {
 
 // ------------------------------------------------------------------------------------------------
 // decode.  kinds: 0 concrete, 1..3 = the chunk's (tile's) incoming b1..b3, 4 derived (serial)
-struct OutBuf {
-    float v0, v1, v2, v3;
-    uint32_t valid;
-    long long base;
-    __device__ __forceinline__ void flush(float* out) {
-        if (!valid) return;
-        if (valid == 0xFu) {
-            *reinterpret_cast<float4*>(out + base) = make_float4(v0, v1, v2, v3);
-        } else {
-            if (valid & 1u) out[base] = v0;
-            if (valid & 2u) out[base + 1] = v1;
-            if (valid & 4u) out[base + 2] = v2;
-            if (valid & 8u) out[base + 3] = v3;
-        }
-        valid = 0;
+// Output ring: every lane keeps its last RING decoded values in LDS at slot (idx + a0) & (RING-1),
+// where a0 aligns the slots to 64-byte sectors of `out`.  Complete sectors leave as four 16-byte
+// stores issued back to back (HBM sees whole sectors instead of scattered partial lines); the values
+// before the chunk's first and after its last sector boundary leave as plain dword stores.
+constexpr int RING = 32;
+constexpr int SECT = 16;
+
+__device__ __forceinline__ void store_sector(const float* ring, float* out, long long s0, int a0, long long num);
+
+// at a flush point: the head (values before the first sector boundary) once it is complete, then the
+// complete sector (at most one is pending: a lane adds <= SECT values between flush points)
+__device__ __forceinline__ void flush_ring(const float* ring, float* out, long long k0, long long& fl, long long idx,
+                                           bool& hdone, int a0, long long num) {
+    if (!hdone && idx >= fl) {
+        for (long long ii = k0; ii < fl; ii++)
+            if (ii < num) out[ii] = ring[(ii + a0) & (RING - 1)];
+        hdone = true;
     }
-    __device__ __forceinline__ void put(float* out, long long idx, float v) {
-        const long long g = idx & ~3ll;
-        if (g != base) { flush(out); base = g; }
-        const int i = (int)(idx & 3);
-        v0 = i == 0 ? v : v0; v1 = i == 1 ? v : v1; v2 = i == 2 ? v : v2; v3 = i == 3 ? v : v3;
-        valid |= 1u << i;
+    if (fl + SECT <= idx) {
+        store_sector(ring, out, fl, a0, num);
+        fl += SECT;
     }
-};
+}
+
+__device__ __forceinline__ void store_sector(const float* ring, float* out, long long s0, int a0, long long num) {
+    const int sl = (int)((s0 + a0) & (RING - 1));
+    if (s0 + SECT <= num) {
+        const float4* r4 = reinterpret_cast<const float4*>(ring + sl);
+        float4* o4 = reinterpret_cast<float4*>(out + s0);
+#pragma unroll
+        for (int q = 0; q < SECT / 4; q++) o4[q] = r4[q];
+    } else {
+        for (int i = 0; i < SECT && s0 + i < num; i++) out[s0 + i] = ring[sl + i];
+    }
+}
 
 struct DecodeShared {
     uint32_t L[LWORDS];
     union {
+        float ring[GROUP * RING];                  // decode pass output rings
         struct {                                   // carry scan
             uint8_t kd[2][3][GROUP];
             float fv[2][3][GROUP];
@@ -581,13 +593,16 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
         int k1 = first ? 0 : 1, k2 = first ? 0 : 2, k3 = first ? 0 : 3;
         int pend = 0;
         bool sent = false;
-        if (act && e != UNKE) {
-            OutBuf ob;
-            ob.valid = 0; ob.base = -4;
+        const int a0 = (int)((reinterpret_cast<uintptr_t>(out) >> 2) & (SECT - 1));
+        float* ring = S.u.ring + c * RING;
+        long long fl = 0, idx = (long long)k0;                      // next sector to store; next index
+        bool hdone = false;                                          // head (partial first sector) stored
+        const bool dec = act && e != UNKE;
+        if (dec) {
+            fl = (((long long)k0 + a0 + SECT - 1) & ~(long long)(SECT - 1)) - a0;
             Rd r;
             r.init(S.L, cs + e);
-            unsigned long long idx = k0;
-            int j = 0;
+            int j = 0, it = 0;
             // phase A: history still (partly) symbolic, or the stream's first three tokens
             while (r.pos < cend && ((k1 | k2 | k3) != 0 || (first && j < 3))) {
                 const uint32_t tk = r.peek();
@@ -597,15 +612,21 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
                 const float p2 = predict2(f1, f2), p3 = predict3(f1, f2, f3);
                 const float v = code == 0 ? __uint_as_float(pat) : (code == 1 ? f1 : (code == 2 ? p2 : p3));
                 const int kind = code == 0 ? 0 : (code == 1 ? k1 : (code == 2 ? ((k1 | k2) ? 4 : 0) : ((k1 | k2 | k3) ? 4 : 0)));
-                if (kind == 0) { if (idx < (unsigned long long)num) ob.put(out, (long long)idx, v); }
-                else pend = j + 1;
+                if (kind != 0) pend = j + 1;                         // re-decoded by the fix-up
                 // history sentinel (-1.0f) or a prediction before the stream's history is full: exact path
                 sent |= (kind == 0 && __float_as_uint(v) == 0xBF800000u) || (first && j < 3 && code != 0);
+                ring[(idx + a0) & (RING - 1)] = v;
                 f3 = f2; k3 = k2; f2 = f1; k2 = k1; f1 = v; k1 = kind;
                 r.step(S.L, len);
                 j++;
                 idx++;
+                if (++it == SECT) {                                  // uniform among the active lanes
+                    it = 0;
+                    flush_ring(ring, out, (long long)k0, fl, idx, hdone, a0, num);
+                }
             }
+            flush_ring(ring, out, (long long)k0, fl, idx, hdone, a0, num);
+            it = 0;
             // phase B: concrete history (kinds stay 0 from here on)
             while (r.pos < cend) {
                 const uint32_t tk = r.peek();
@@ -617,13 +638,20 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
                     const float p2 = predict2(f1, f2), p3 = predict3(f1, f2, f3);
                     v = code == 2 ? p2 : (code == 3 ? p3 : v);
                 }
-                if (idx < (unsigned long long)num) ob.put(out, (long long)idx, v);
+                ring[(idx + a0) & (RING - 1)] = v;
                 sent |= __float_as_uint(v) == 0xBF800000u;
                 f3 = f2; f2 = f1; f1 = v;
                 r.step(S.L, len);
                 idx++;
+                if (++it == SECT) {
+                    it = 0;
+                    flush_ring(ring, out, (long long)k0, fl, idx, hdone, a0, num);
+                }
             }
-            ob.flush(out);
+            flush_ring(ring, out, (long long)k0, fl, idx, hdone, a0, num);
+            const long long t0 = hdone ? fl : (long long)k0;         // tail, or a chunk inside one sector
+            for (long long ii = t0; ii < idx; ii++)
+                if (ii < num) out[ii] = ring[(ii + a0) & (RING - 1)];
         }
         if (sent) atomicOr(D.err, 128u);
         sent = false;
