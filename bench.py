@@ -153,8 +153,10 @@ def main():
     nbits = L.encode_result()
     nbytes = (nbits + 7) // 8
 
-    # ---- timed region: barrier + sync on both sides, max over ranks
+    # ---- timed region: barrier + sync on both sides, max over ranks.  Per-kernel HIP events are
+    # recorded by the library on its own stream (dc_timing_enable), one event set per step.
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    L.L.dc_timing_enable(args.steps)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -175,6 +177,22 @@ def main():
         wall = float(w[0])
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    import ctypes
+    kms = np.zeros((args.steps, 6), np.float32)
+    for k in range(args.steps):
+        buf = (ctypes.c_float * 6)()
+        if L.L.dc_timing_read(k, buf) == 0:
+            kms[k] = np.frombuffer(buf, np.float32)
+    L.L.dc_timing_enable(0)
+    kavg = kms.mean(axis=0)
+    kernels = {   # name: (avg ms, algorithmic bytes per launch)
+        f"encode_count_kernel<{ct}>": (float(kavg[0]), 4.0 * n),
+        "encode_scan_kernel": (float(kavg[1]), 0.0),
+        f"encode_write_kernel<{ct}>": (float(kavg[2]), 4.0 * n + nbytes),
+        f"parse_kernel<{ct}>": (float(kavg[3]), float(nbytes)),
+        "tile_fix_kernel+tile_scan_kernel": (float(kavg[4]), 0.0),
+        f"decode_kernel_fast<{ct}>": (float(kavg[5]), nbytes + 4.0 * n),
+    }
 
     ok = None
     if args.check and rank == 0:
@@ -187,21 +205,17 @@ def main():
 
     ms_per_step = wall / args.steps * 1e3
     value = world * 4.0 * n / (wall / args.steps) / 1e9
-    # dominant kernel: the one-launch encoder vs the decoder chain (event-timed on the library stream)
-    enc_bytes = 4.0 * n + nbytes
-    dec_bytes = nbytes + 4.0 * n
-    if enc_ms >= dec_ms:
-        dom = {"kernel": "encode_kernel<7>", "ms": enc_ms, "bytes": enc_bytes}
-    else:
-        dom = {"kernel": "decode chain (7 kernels)", "ms": dec_ms, "bytes": dec_bytes}
-    achieved = dom["bytes"] / (dom["ms"] * 1e-3) / 1e9
+    # dominant kernel: the longest launch of the step (HIP events on the library stream)
+    dname = max(kernels, key=lambda k: kernels[k][0])
+    dom = {"kernel": dname, "ms": kernels[dname][0], "bytes": kernels[dname][1]}
+    achieved = dom["bytes"] / (dom["ms"] * 1e-3) / 1e9 if dom["ms"] > 0 else 0.0
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if os.path.exists(pmc):
         try:
             pj = json.load(open(pmc))
             if pj.get("n") == n and pj.get("ct") == ct:
-                traffic = pj.get("traffic_bytes_per_launch", {}).get(dom["kernel"])
+                traffic = pj.get("hbm_bytes_per_launch", {}).get(dname)
         except Exception:
             traffic = None
     res = {
@@ -225,6 +239,7 @@ def main():
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
                      "algorithmic_bytes_per_launch": int(dom["bytes"]), "avg_launch_ms": round(dom["ms"], 4)},
+        "kernels_ms": {k: round(v[0], 4) for k, v in kernels.items()},
         "phases_ms": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4), "med_dataset_serial_s": round(t_med, 4)},
         "pipeline_roofline_frac": round((8.0 * n + 2 * nbytes) / ((enc_ms + dec_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
     }

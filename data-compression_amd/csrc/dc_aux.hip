@@ -11,6 +11,7 @@
 //    positions of the set data bits (powers of two skipped) + overall parity.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "dc_shared.h"
 
 namespace dc {
@@ -310,6 +311,48 @@ extern "C" int dc_launch_ham_syndrome(const uint8_t* s, long long nbytes, unsign
     if (g < 1) g = 1;
     hipLaunchKernelGGL(ham_syndrome_kernel, dim3((unsigned)g), dim3(256), 0, st, s, nbytes, d_syn_ones, d_syn_ones + 1);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Per-kernel timing hooks (bench.py's roofline): when enabled, the launchers record HIP events on
+// their stream between kernels; event set s holds marks 0..3 (encode: start, count, scan, write) and
+// 4..7 (decode: start, parse, tile fix + scan, decode).
+static hipEvent_t* g_events = nullptr;
+static int g_nsets = 0, g_set = 0;
+
+extern "C" void dc_mark_phase(int k, hipStream_t st) {
+    if (!g_events || g_set >= g_nsets) return;
+    (void)hipEventRecord(g_events[g_set * 8 + k], st);
+}
+extern "C" void dc_mark_next_set(void) {
+    if (g_events && g_set < g_nsets) g_set++;
+}
+extern "C" int dc_timing_enable(int nsets) {
+    if (g_events) {
+        for (int i = 0; i < g_nsets * 8; i++) (void)hipEventDestroy(g_events[i]);
+        free(g_events);
+        g_events = nullptr;
+    }
+    g_nsets = 0;
+    g_set = 0;
+    if (nsets <= 0) return 0;
+    g_events = (hipEvent_t*)calloc((size_t)nsets * 8, sizeof(hipEvent_t));
+    if (!g_events) return -1;
+    for (int i = 0; i < nsets * 8; i++)
+        if (hipEventCreate(&g_events[i]) != hipSuccess) return -1;
+    g_nsets = nsets;
+    return 0;
+}
+/* ms[0..5] = encode count, encode scan, encode write, decode parse, decode tile fix+scan, decode */
+extern "C" int dc_timing_read(int set, float* ms) {
+    if (!g_events || set < 0 || set >= g_nsets) return -1;
+    hipEvent_t* e = g_events + set * 8;
+    const int a[6] = {0, 1, 2, 4, 5, 6};
+    for (int i = 0; i < 6; i++) {
+        if (hipEventSynchronize(e[a[i] + 1]) != hipSuccess) return -1;
+        if (hipEventElapsedTime(&ms[i], e[a[i]], e[a[i] + 1]) != hipSuccess) ms[i] = -1.0f;
+    }
+    return 0;
 }
 
 }  // namespace dc

@@ -802,12 +802,17 @@ extern "C" int dc_launch_decode_fast(const uint8_t* s, const unsigned long long*
     const long long max_groups = (max_chunks + GROUP - 1) / GROUP;
     hipLaunchKernelGGL(plan_kernel_fast, dim3(1), dim3(1), 0, st, D->plan, dev_nbits, host_nbits, max_chunks);
     const int gparse = (int)std::min<long long>(max_groups > 0 ? max_groups : 1, 256 * 8);
+    dc_mark_phase(4, st);
     DC_DISPATCH_F(P->ct, parse_kernel, dim3(gparse), dim3(GROUP), 0, st, s, *P, *D);
+    dc_mark_phase(5, st);
     DC_DISPATCH_F(P->ct, tile_fix_kernel, dim3((unsigned)((max_groups + 3) / 4 > 0 ? (max_groups + 3) / 4 : 1)), dim3(256), 0, st,
                   s, *P, *D);
     hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, st, *D);
     const int gdec = (int)std::min<long long>(max_groups > 0 ? max_groups : 1, 256 * 3);
+    dc_mark_phase(6, st);
     DC_DISPATCH_F(P->ct, decode_kernel_fast, dim3(gdec), dim3(GROUP), 0, st, s, *P, *D, out, num, epoch);
+    dc_mark_phase(7, st);
+    dc_mark_next_set();
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

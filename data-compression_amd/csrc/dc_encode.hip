@@ -324,15 +324,19 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
     if (n <= 0) return 0;
     const unsigned ntiles = (unsigned)((n + ENC_TILE - 1) / ENC_TILE);
     uint32_t* tbits = reinterpret_cast<uint32_t*>(desc + ntiles);     // desc holds 2 * ntiles words
+    dc_mark_phase(0, stream);
     // one wave (count) / one workgroup (write) per tile: measured faster than persistent grids here
     const unsigned gc = (ntiles + 3) / 4;
     const unsigned gw = ntiles;
     DC_ENC_DISPATCH(encode_count_kernel, dim3(gc), dim3(256), 0, stream, x, n, idx0, *P, tbits,
                     (long long)ntiles, err);
+    dc_mark_phase(1, stream);
     hipLaunchKernelGGL(encode_scan_kernel, dim3(1), dim3(1024), 0, stream, tbits, desc, (long long)ntiles, start_bit,
                        total_bits);
+    dc_mark_phase(2, stream);
     DC_ENC_DISPATCH(encode_write_kernel, dim3(gw), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, desc, ntiles,
                     dbg);
+    dc_mark_phase(3, stream);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

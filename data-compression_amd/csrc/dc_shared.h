@@ -81,6 +81,10 @@ int dc_launch_find_sentinel(const float* out, long long num, unsigned* err, dc_h
 int dc_launch_fixup_serial(const uint8_t* s, const DC_NS Params* P, const DC_NS DecBufs* D, float* out,
                            long long num, dc_hip_stream st);
 long long dc_decode_chunk_bits(void);
+void dc_mark_phase(int k, dc_hip_stream st);
+void dc_mark_next_set(void);
+int dc_timing_enable(int nsets);
+int dc_timing_read(int set, float* ms);
 long long dc_decode_group(void);
 
 int dc_launch_to_small(const float* x, long long n, float* y, float* part_v, long long* part_i, float* d_min,

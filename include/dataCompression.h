@@ -1,0 +1,103 @@
+/*
+ * dataCompression.h -- drop-in C ABI of libdcamd for the float bit-wise codec path of
+ * smallcat9603/data-compression (impl/dataCompression.h / impl/dataCompression.c).
+ *
+ * Every declaration below has the reference's name, argument order, argument meaning and ownership
+ * rules; the line numbers cite the reference declaration (impl/dataCompression.h) and definition
+ * (impl/dataCompression.c) it replaces.  The compute runs on an MI355X (gfx950) behind these
+ * host-pointer entry points; the device-pointer API is in dc_gpu.h.
+ *
+ * Ownership (as in the reference): *data_bits is realloc()ed by the callee (pass NULL, bytes = 0,
+ * pos = 8 for a new stream; a non-empty stream is appended to); returned float* / *data_small /
+ * hamming check strings are malloc()ed host memory owned by the caller.
+ * Errors: the reference printf()s and exit()s on malformed streams (c:2503, :1775, :3162); this
+ * library prints the reason to stderr (also dc_last_error(), dc_gpu.h) and returns instead: a failed
+ * compress leaves *data_bits / *bytes / *pos untouched, a failed decompress returns its malloc()ed
+ * buffer with unspecified contents.  There is no CPU fallback: a missing gfx950 device is such an
+ * error.
+ * absErrorBound: the reference bakes the bound in at compile time (#define absErrorBound, :3).  The
+ * library is built with -DDC_ABS_ERROR_BOUND=<value> (default 1e-3, the bench configuration) and
+ * exports the reference's globals absErrBound / absErrorBound_binary (impl/dataCompression.c:21-22);
+ * dc_set_abs_error_bound() (dc_gpu.h) changes it at run time.
+ */
+#ifndef DC_DATACOMPRESSION_H
+#define DC_DATACOMPRESSION_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+extern double absErrBound;            /* impl/dataCompression.c:21 */
+extern int absErrorBound_binary;      /* impl/dataCompression.c:22 */
+
+/* ---- CT5: zero / 3-predictor / raw tokens ------------------------------------------------------ */
+/* h:90  c:3310-3444 */
+void myCompress_bitwise(float data[], int num, unsigned char** data_bits, int* bytes, int* pos);
+/* h:86  c:2922-3135 */
+float* myDecompress_bitwise(unsigned char* data_bits, int bytes, int num);
+
+/* ---- CT6: raw tokens only (no prediction) ------------------------------------------------------ */
+/* h:77  c:2645-2654 */
+void myCompress_bitwise_np(float data[], int num, unsigned char** data_bits, int* bytes, int* pos);
+/* h:74  c:2459-2609 */
+float* myDecompress_bitwise_np(unsigned char* data_bits, int bytes, int num);
+
+/* ---- CT11: 3-bit codes or verbatim 32-bit floats ----------------------------------------------- */
+/* h:81  c:577-696 */
+void myCompress_bitwise_op(float data[], int num, unsigned char** data_bits, int* bytes, int* pos);
+/* h:82  c:698-797 */
+float* myDecompress_bitwise_op(unsigned char* data_bits, int bytes, int num);
+
+/* ---- CT7 (and the CT9 payload): bitmask-based tokens; mask = 17 '0'/'1' chars (sign, exponent,
+ *      8 mantissa bits of the dataset mean), type from med_dataset_float ------------------------- */
+/* h:70  c:2030-2141 */
+void myCompress_bitwise_mask(float data[], int num, unsigned char** data_bits, int* bytes, int* pos, int type,
+                             char mask[1 + 8 + 8]);
+/* h:67  c:1703-1898 */
+float* myDecompress_bitwise_mask(unsigned char* data_bits, int bytes, int num, int type, char mask[1 + 8 + 8]);
+
+/* ---- pre-passes ---------------------------------------------------------------------------------- */
+/* h:96  c:3543-3562: *data_small = data - min (new malloc array), returns min */
+float toSmallDataset_float(float data[], float** data_small, int num);
+/* h:99  c:3593-3620: left-to-right float mean; *type from the maximum */
+float med_dataset_float(float* data, int num, int* type);
+
+/* ---- integrity (CT8/CT9: CRC-32, CT10: Hamming SECDED per block) --------------------------------- */
+/* h:143 c:5524-5534 (zlib crc32) */
+uint32_t do_crc32(unsigned char* data_bits, int bytes);
+/* h:146 c:5581 */
+int hmLength(int k);
+/* h:153 c:5740-5748: *c = r+1 '0'/'1' chars (check bits + overall parity) */
+void hamming_encode(unsigned char* bits, char** c, int bytes, int* r);
+/* h:154 c:5750-5779: 0 ok, 1 two-bit error (resend), 2 parity-bit flip, 3 single bit corrected */
+int hamming_decode(unsigned char* bits, char* c, int bytes, int r);
+/* h:158 c:5868 */
+int block_size(int data_bytes);
+/* h:157 c:5858 */
+void bit_flip(unsigned char* bits, int bytes);
+/* h:144 c:5536 */
+uint64_t get_random_int(uint64_t from, uint64_t to);
+
+/* ---- helpers the callers link against ------------------------------------------------------------ */
+/* h:141 c:5512 */
+int to_absErrorBound_binary(double absErrBound);
+/* h:117 c:5220 */
+void getFloatBin(float f, char bin[]);
+/* h:125 c:5244 */
+void floattostr(float* f, char* str);
+/* h:126 c:5256 */
+void doubletostr(double* d, char* str);
+/* h:127 c:5267 */
+float strtofloat(char* str);
+/* h:128 c:5279 */
+double strtodbl(char* str);
+/* h:138 c:5456 */
+void add_bit_to_bytes(unsigned char** data_bits, int* bytes, int* pos, int flag);
+/* h:139 c:5492 */
+void bit_set(unsigned char* p_data, unsigned char position, int flag);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
