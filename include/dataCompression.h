@@ -16,7 +16,7 @@
  * buffer with unspecified contents.  There is no CPU fallback: a missing gfx950 device is such an
  * error.
  * absErrorBound: the reference bakes the bound in at compile time (#define absErrorBound, :3).  The
- * library is built with -DDC_ABS_ERROR_BOUND=<value> (default 1e-3, the bench configuration) and
+ * library is built with -DDC_ABS_ERROR_BOUND=<value> (default 1e-6, the reference header's value) and
  * exports the reference's globals absErrBound / absErrorBound_binary (impl/dataCompression.c:21-22);
  * dc_set_abs_error_bound() (dc_gpu.h) changes it at run time.
  */
