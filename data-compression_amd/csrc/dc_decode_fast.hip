@@ -27,19 +27,19 @@
 
 namespace dc {
 
-constexpr int LROW = 33;                       // padded LDS row (words) per chunk
-constexpr int LWORDS = (GROUP + 1) * LROW;     // + one row for the words after the tile
+constexpr int LROW = 32;                       // LDS words per chunk
+constexpr int LWORDS = GROUP * LROW + 8;       // + the words after the tile
 constexpr int OV = 1024;                       // overlap: P_c starts OV bits before its chunk
 constexpr int OVW = OV / 32;
-constexpr int PWORDS = LWORDS + OVW + OVW / 32;
-constexpr int KMAX = 6;                        // extra known entries per chunk (besides P_c's own)
+constexpr int PWORDS = LWORDS + OVW;
+constexpr int KMAX = 2;                        // extra known entries per chunk (besides P_c's own)
 constexpr int RMAX = 12;                       // closure rounds inside a tile
 constexpr int CW = CHUNK_BITS / 32;            // words per chunk
 constexpr int UNKE = 63;
 
 #define STAMP(ph) do { if (D.dbg && threadIdx.x == 0 && t < 4096) D.dbg[t * 16 + (ph)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
-__device__ __forceinline__ uint32_t ldw(const uint32_t* L, int w) { return L[w + (w >> 5)]; }
+__device__ __forceinline__ uint32_t ldw(const uint32_t* L, int w) { return L[w]; }
 
 // branch-free MSB-first reader: w0:w1 hold the next 64 bits from bit sh of w0, w2 the next word,
 // pf the word after it (loaded one step ahead so its LDS latency is off the critical path)
@@ -87,7 +87,7 @@ __device__ __forceinline__ void stage_words(uint32_t* L, const uint8_t* s, long 
             const int i4 = threadIdx.x + q * GROUP;
             if (q < QF || i4 < n4) {
                 const int i = 4 * i4;
-                uint32_t* d = L + i + (i >> 5);
+                uint32_t* d = L + i;
                 d[0] = __builtin_bswap32(r[q].x);
                 d[1] = __builtin_bswap32(r[q].y);
                 d[2] = __builtin_bswap32(r[q].z);
@@ -109,7 +109,7 @@ __device__ __forceinline__ void stage_words(uint32_t* L, const uint8_t* s, long 
                 v = (v << 8) | (bi < nbytes ? (uint32_t)s[bi] : 0u);
             }
         }
-        L[i + (i >> 5)] = v;
+        L[i] = v;
     }
 }
 
@@ -153,9 +153,8 @@ struct ParseShared {
     uint32_t ke[GROUP * KMAX];                 // entry<<16 | exit<<10 | cnt
     uint32_t em[2][GROUP];                     // exits of all known entries, by round parity
     uint32_t pm[GROUP];
-    uint32_t pre[GROUP + 1];                   // exclusive prefix of the standard counts
     uint64_t bad[GROUP / 64];
-    uint16_t n[GROUP], stdcnt[GROUP], devcnt[GROUP];
+    uint16_t n[GROUP], devcnt[GROUP];
     uint8_t x[GROUP], nk[GROUP], stdexit[GROUP], dev[GROUP];
     uint32_t wsum[GROUP / 64];
     int texit;
@@ -275,21 +274,9 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
             if (lookup_entry(S, c, S.x[c - 1], &ex, &cn)) { scnt = cn; sex = ex; ok = (ex == x); }
             else atomicOr(D.err, 8u);
         }
-        S.stdcnt[c] = (uint16_t)scnt;
         S.stdexit[c] = (uint8_t)sex;
         const unsigned long long bm = __ballot(!ok);
         if (lane == 0) S.bad[wid] = bm;
-        uint32_t inc = (uint32_t)scnt;
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t tv = __shfl_up(inc, d, 64);
-            if (lane >= d) inc += tv;
-        }
-        if (lane == 63) S.wsum[wid] = inc;
-        __syncthreads();
-        uint32_t wpre = 0;
-        for (int w = 0; w < wid; w++) wpre += S.wsum[w];
-        S.pre[c] = wpre + inc - (uint32_t)scnt;
-        if (c == GROUP - 1) S.pre[GROUP] = wpre + inc;
         __syncthreads();
 
         // ---- tile chain: every tile entry that is a boundary of P_0 continues as P_0 and leaves chunk 0
@@ -411,7 +398,7 @@ __global__ __launch_bounds__(256) void tile_fix_kernel(const uint8_t* __restrict
         if (gw < nwfull) v = __builtin_bswap32(w[gw]);
         else if (4 * gw < pl.nbytes)
             for (int k = 0; k < 4; k++) { const long long bi = 4 * gw + k; v = (v << 8) | (bi < pl.nbytes ? (uint32_t)s[bi] : 0u); }
-        L[i + (i >> 5)] = v;
+        L[i] = v;
     }
     __builtin_amdgcn_s_waitcnt(0);                      // the wave's own LDS stores land in order
     __builtin_amdgcn_wave_barrier();
