@@ -478,8 +478,8 @@ __global__ __launch_bounds__(1024) void tile_scan_kernel(DecBufs D) {
 // where a0 aligns the slots to 64-byte sectors of `out`.  Complete sectors leave as four 16-byte
 // stores issued back to back (HBM sees whole sectors instead of scattered partial lines); the values
 // before the chunk's first and after its last sector boundary leave as plain dword stores.
-constexpr int RING = 32;
-constexpr int SECT = 16;
+constexpr int RING = 16;
+constexpr int SECT = 8;
 
 __device__ __forceinline__ void store_sector(const float* ring, float* out, long long s0, int a0, long long num);
 
