@@ -158,44 +158,42 @@ __device__ __forceinline__ uint32_t token_pattern(uint32_t t, int len, const Par
 }
 
 
-// Branch-free token length (selects only; every lane of a wave follows the same instruction stream).
+// Branch-free token length from the next 32 stream bits, with the uniform constants of Params:
+// c3 tokens (leading 1) are 3 bits; CT7 masked tokens ('0' + type ones) type+2+{mm0|mm}; raw tokens
+// 9 + clamp(B + E - 127, 0, 23) = clamp(E + B - 118, 9, 32); CT11 verbatim 32.
 template <int CT>
 __device__ __forceinline__ int token_len_bf(uint32_t t, const Params& P) {
-    const int raw = 9 + mbits(P.B, (t >> 23) & 0xFFu);
-    if (CT == 6) return raw;
-    int len = raw;
+    const int E = (int)((t >> 23) & 0xFFu);
+    int len = min(max(E + P.rawadd, 9), 32);
     if (CT == 11) len = 32;
     if (CT == 7) {
-        const uint32_t ones = (1u << P.type) - 1u;
-        const bool msk = ((t >> (31 - P.type)) & ones) == ones;
-        const int ml = (((t >> (30 - P.type)) & 1u) ? P.mm : P.mm0) + P.type + 2;
-        len = msk ? ml : raw;
+        const bool msk = (t & P.hm) == P.hm;
+        const int lm = P.lm0 + (((t >> P.fsh) & 1u) ? P.dlm : 0);
+        len = msk ? lm : len;
     }
-    return (t >> 31) ? 3 : len;
+    if (CT != 6) len = ((int)t < 0) ? 3 : len;
+    return len;
 }
 
-// Branch-free non-predicted value pattern and predictor code (0 = none/'100', 1..3 = 101/110/111).
+// Branch-free value pattern of a non-predicted token and its predictor code (0 = none/'100',
+// 1..3 = 101/110/111).  Raw: top len bits + midpoint bit (decompress_bitwise_float :3166-3184),
+// y = 0xFFFFFFFF >> len (0 for len 32); CT7 masked (:1939-2010) from the precomputed c/k constants.
 template <int CT>
 __device__ __forceinline__ uint32_t token_pattern_bf(uint32_t t, int len, const Params& P, int* code) {
-    const bool c3 = (CT != 6) && (t >> 31);
+    const bool c3 = (CT != 6) && ((int)t < 0);
     *code = c3 ? (int)((t >> 29) & 3u) : 0;
     uint32_t u;
     if (CT == 11) {
         u = t;
     } else {
-        const uint32_t keep = len >= 32 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> len);
-        u = (t & keep) | (len < 32 ? (1u << (31 - len)) : 0u);                 // raw + midpoint
+        const uint32_t y = (uint32_t)(0xFFFFFFFFull >> len);
+        u = (t & ~y) | (y & ~(y >> 1));
         if (CT == 7) {
-            const uint32_t ones = (1u << P.type) - 1u;
-            const bool msk = ((t >> (31 - P.type)) & ones) == ones;
-            const uint32_t rest = t << (P.type + 2);
-            const bool fl = (t >> (30 - P.type)) & 1u;
-            const int tl0 = P.mm0, tl1 = P.mm;                                   // uniform
-            const uint32_t tail0 = tl0 > 0 ? (rest >> (32 - tl0)) : 0u;
-            const uint32_t tail1 = tl1 > 0 ? (rest >> (32 - tl1)) : 0u;
-            const uint32_t u0 = (P.mask17 << 15) | (tl0 > 0 ? tail0 << (15 - tl0) : 0u) | (tl0 < 15 ? 1u << (14 - tl0) : 0u);
-            const uint32_t u1 = ((P.mask17 >> 8) << 23) | (tl1 > 0 ? tail1 << (23 - tl1) : 0u) | (tl1 < 23 ? 1u << (22 - tl1) : 0u);
-            u = msk ? (fl ? u1 : u0) : u;
+            const bool msk = (t & P.hm) == P.hm;
+            const uint32_t rest = t << P.rs;
+            const uint32_t u0 = P.c0 | ((rest >> 17) & P.k0);
+            const uint32_t u1 = P.c1 | ((rest >> 9) & P.k1);
+            u = msk ? (((t >> P.fsh) & 1u) ? u1 : u0) : u;
         }
     }
     return c3 ? 0u : u;

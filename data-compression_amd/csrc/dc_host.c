@@ -207,6 +207,17 @@ static void make_params(Params* P, int ct, int type, uint32_t mask17) {
     int m = P->B + (int)((P->mask17 >> 8) & 0xFF) - 127;
     P->mm = m > 23 ? 23 : (m < 0 ? 0 : m);
     P->mm0 = P->mm > 8 ? P->mm - 8 : 0;
+    P->rawadd = P->B - 118;
+    P->hm = type > 0 ? (((1u << type) - 1u) << (31 - type)) : 0u;
+    P->fsh = 30 - type;
+    P->rs = type + 2;
+    P->lm0 = type + 2 + P->mm0;
+    P->dlm = P->mm - P->mm0;
+    const int tl0 = P->mm0, tl1 = P->mm;
+    P->c0 = (P->mask17 << 15) | (tl0 < 15 ? 1u << (14 - tl0) : 0u);
+    P->k0 = tl0 > 0 ? (((1u << tl0) - 1u) << (15 - tl0)) : 0u;
+    P->c1 = ((P->mask17 >> 8) << 23) | (tl1 < 23 ? 1u << (22 - tl1) : 0u);
+    P->k1 = tl1 > 0 ? (((1u << tl1) - 1u) << (23 - tl1)) : 0u;
 }
 
 static int valid_ct(int ct) { return ct == 5 || ct == 6 || ct == 7 || ct == 11; }

@@ -18,6 +18,14 @@ typedef struct Params {  /* per-call codec parameters, computed on the host */
     uint32_t mask17;     /* CT7 mask: top 17 bits of the mean's pattern (pingpong.c:202-206) */
     int mm;              /* m(mask exponent) */
     int mm0;             /* max(mm - 8, 0) */
+    /* derived decode constants (token length / value without branches, dc_device.h) */
+    int rawadd;          /* B - 118: raw length = clamp(E + rawadd, 9, 32) */
+    uint32_t hm;         /* CT7: the type leading-one bits after the first bit of a masked token */
+    int fsh;             /* CT7: shift of the masked token's flag bit (30 - type) */
+    int lm0, dlm;        /* CT7: masked length flag 0 = lm0, flag 1 = lm0 + dlm */
+    int rs;              /* CT7: type + 2 (head length) */
+    uint32_t c0, k0;     /* CT7 flag 0 value = c0 | ((t << rs) >> 17 & k0) */
+    uint32_t c1, k1;     /* CT7 flag 1 value = c1 | ((t << rs) >> 9 & k1) */
 } Params;
 
 typedef struct Plan {    /* device-resident sizes of the stream being decoded */
