@@ -27,7 +27,8 @@
 
 namespace dc {
 
-constexpr int LROW = 32;                       // LDS words per chunk
+constexpr int LROW = 32;                       // LDS words per chunk (unpadded: measured faster than a
+                                               // 33-word row, the lanes drift apart within a few tokens)
 constexpr int LWORDS = GROUP * LROW + 8;       // + the words after the tile
 constexpr int OV = 1024;                       // overlap: P_c starts OV bits before its chunk
 constexpr int OVW = OV / 32;
@@ -151,7 +152,7 @@ __device__ __forceinline__ void walk_lds(const uint32_t* L, const Params& P, int
 struct ParseShared {
     uint32_t L[PWORDS];
     uint32_t ke[GROUP * KMAX];                 // entry<<16 | exit<<10 | cnt
-    uint32_t em[2][GROUP];                     // exits of all known entries, by round parity
+    uint8_t nkr[2][GROUP];                     // known-entry count of every chunk, by round parity
     uint32_t pm[GROUP];
     uint64_t bad[GROUP / 64];
     uint16_t n[GROUP], devcnt[GROUP];
@@ -206,7 +207,14 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
         if (act) {
             Rd r;
             r.init(S.L, gc == 0 ? cs : cs - OV);
-            while (r.pos < cs) r.step(S.L, token_len_bf<CT>(r.peek(), P));
+            const unsigned long long q0 = D.dbg ? __builtin_amdgcn_s_memtime() : 0;
+            int nst = 0;
+            while (r.pos < cs) { r.step(S.L, token_len_bf<CT>(r.peek(), P)); nst++; }
+            if (D.dbg && t < 4096 && (c & 63) == 0) {                 // per-wave cycles and steps (diagnostic)
+                int mx = nst;
+                for (int d = 32; d >= 1; d >>= 1) mx = max(mx, __shfl_xor(mx, d, 64));
+                D.dbg[t * 16 + 12 + (c >> 6)] = ((__builtin_amdgcn_s_memtime() - q0) << 16) | (unsigned)mx;
+            }
             while (r.pos < cend) {
                 const int rel = r.pos - cs;
                 pm |= rel < 32 ? (1u << rel) : 0u;
@@ -221,7 +229,6 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
         STAMP(2);
 
         // ---- round 2: P_{c-1}'s exit into chunk c, where P_c has no boundary there (rare)
-        uint32_t em = 1u << x;
         int nk = 0;
         if (act && c > 0) {
             const int e = S.x[c - 1];
@@ -230,11 +237,10 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
                 walk_lds<CT>(S.L, P, cs, cend, e, pm, x, n, &ex, &cn);
                 S.ke[c * KMAX] = ((uint32_t)e << 16) | ((uint32_t)ex << 10) | (uint32_t)cn;
                 nk = 1;
-                em |= 1u << ex;
             }
         }
         S.nk[c] = (uint8_t)nk;
-        S.em[0][c] = em;
+        S.nkr[0][c] = (uint8_t)nk;
         __syncthreads();
         STAMP(3);
 
@@ -246,7 +252,11 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
             if (act && c > 0) {
                 uint32_t known = pm;
                 for (int k = 0; k < nk; k++) known |= 1u << (S.ke[c * KMAX + k] >> 16);
-                uint32_t need = S.em[pp][c - 1] & ~known;
+                // exits of the predecessor's entries known at the end of the previous round
+                uint32_t emp = 1u << S.x[c - 1];
+                const int nkp = S.nkr[pp][c - 1];
+                for (int k = 0; k < nkp; k++) emp |= 1u << ((S.ke[(c - 1) * KMAX + k] >> 10) & 63u);
+                uint32_t need = emp & ~known;
                 while (need) {
                     const int e = __ffs(need) - 1;
                     need &= need - 1;
@@ -255,11 +265,10 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
                     walk_lds<CT>(S.L, P, cs, cend, e, pm, x, n, &ex, &cn);
                     S.ke[c * KMAX + nk] = ((uint32_t)e << 16) | ((uint32_t)ex << 10) | (uint32_t)cn;
                     nk++;
-                    em |= 1u << ex;
-                    added = 1;
+                        added = 1;
                 }
             }
-            S.em[rp][c] = em;
+            S.nkr[rp][c] = (uint8_t)nk;
             S.nk[c] = (uint8_t)nk;
             if (!__syncthreads_or(added)) break;
         }

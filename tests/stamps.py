@@ -31,5 +31,10 @@ for i, nm in enumerate(names):
 dd = np.diff(a[:, 8:12], axis=1) * 10.0 / 1000.0
 for i, nm in enumerate(["stage+resolve", "decode pass1", "carry+fixup"]):
     print(f"decode {nm:13s} mean {dd[:, i].mean():8.2f} us  p50 {np.median(dd[:, i]):8.2f}  max {dd[:, i].max():8.2f}")
+w = a[:, 12:16]
+cyc, stp = (w >> 16).astype(np.float64), (w & 0xFFFF).astype(np.float64)
+ok = stp > 0
+print("pre-loop cycles/wave-step mean %.1f  (steps/wave mean %.1f, cycles/wave mean %.0f)" %
+      ((cyc[ok] / stp[ok]).mean(), stp[ok].mean(), cyc[ok].mean()))
 t0 = a[:, 0].min()
 print("parse span us", (a[:, 7].max() - t0) / 100.0, " decode start->end us", (a[:, 11].max() - a[:, 8].min()) / 100.0)
