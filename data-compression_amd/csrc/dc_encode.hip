@@ -25,7 +25,7 @@ constexpr int ENC_TILE = 4096;                  // floats per tile (one offset p
 constexpr int ENC_TPB = 256;                    // write kernel: 4 waves per tile
 constexpr int ENC_K = ENC_TILE / ENC_TPB;       // 16 consecutive floats per lane
 constexpr int ENC_Q = ENC_TILE / 4 / ENC_TPB;   // coalesced float4 loads per lane
-constexpr int CNT_Q = ENC_TILE / 4 / 64;        // count kernel: one wave per tile, 16 float4 per lane
+constexpr int CNT_Q = ENC_TILE / 4 / 128;       // count kernel: one wave per half tile, 8 float4 per lane
 constexpr int ENC_LDS_WORDS = ENC_TILE + 48;    // 32 bits/elem max + offset + head slack
 constexpr int STG_WORDS = ENC_TILE + ENC_TILE / 16 + 8;   // staged floats, one pad word per 16
 
@@ -76,10 +76,11 @@ __global__ __launch_bounds__(256) void encode_count_kernel(const float* __restri
                                                            Params P, uint32_t* __restrict__ tbits, long long ntiles,
                                                            unsigned* __restrict__ err) {
     const int lane = threadIdx.x & 63;
-    for (long long tile = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); tile < ntiles; tile += (long long)gridDim.x * 4) {
-    const long long tb = tile * ENC_TILE;
+    constexpr int HALF = ENC_TILE / 2;
+    for (long long h = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); h < 2 * ntiles; h += (long long)gridDim.x * 4) {
+    const long long tb = h * HALF;                                   // one wave per half tile
     float4 f[CNT_Q];
-    if (tb + ENC_TILE <= n) {
+    if (tb + HALF <= n) {
         const float4* p4 = reinterpret_cast<const float4*>(x + tb);
 #pragma unroll
         for (int q = 0; q < CNT_Q; q++) f[q] = p4[lane + 64 * q];
@@ -91,7 +92,7 @@ __global__ __launch_bounds__(256) void encode_count_kernel(const float* __restri
             f[q].z = e + 2 < n ? x[e + 2] : 0.0f; f[q].w = e + 3 < n ? x[e + 3] : 0.0f;
         }
     }
-    const bool full = tb + ENC_TILE <= n && idx0 + tb >= 3;         // no bounds / history checks
+    const bool full = tb + HALF <= n && idx0 + tb >= 3;             // no bounds / history checks
     float h1 = lane == 0 ? halo_x(x, idx0, tb - 1) : 0.0f;          // q = 0 history of lane 0
     float h2 = lane == 0 ? halo_x(x, idx0, tb - 2) : 0.0f;
     float h3 = lane == 0 ? halo_x(x, idx0, tb - 3) : 0.0f;
@@ -102,7 +103,7 @@ __global__ __launch_bounds__(256) void encode_count_kernel(const float* __restri
     if (CT != 6 && __any(neg1) && lane == 0) atomicOr(err, 1u);    // -1.0f is the reference's sentinel
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
-    if (lane == 0) tbits[tile] = sum;
+    if (lane == 0) tbits[h] = sum;                                   // half-tile bit count
     }
 }
 
@@ -120,7 +121,7 @@ __global__ __launch_bounds__(1024) void encode_scan_kernel(const uint32_t* __res
     constexpr int PER = SCAN_CH / 1024;
     for (long long c0 = 0; c0 < ntiles; c0 += SCAN_CH) {
         const int m = (int)min((long long)SCAN_CH, ntiles - c0);
-        for (int i = tid; i < SCAN_CH; i += 1024) cnt[i] = i < m ? tbits[c0 + i] : 0u;
+        for (int i = tid; i < SCAN_CH; i += 1024) cnt[i] = i < m ? tbits[2 * (c0 + i)] + tbits[2 * (c0 + i) + 1] : 0u;
         __syncthreads();
         unsigned long long sum = 0;
 #pragma unroll
@@ -148,6 +149,22 @@ __global__ __launch_bounds__(1024) void encode_scan_kernel(const uint32_t* __res
     if (tid == 0) *total_bits = carry;
 }
 
+// a tile's floats as coalesced float4s: thread tid holds float4 number tid + ENC_TPB*q
+__device__ __forceinline__ void load_tile4(const float* __restrict__ x, long long n, long long tbase, int tid, float4* f) {
+    if (tbase + ENC_TILE <= n) {
+        const float4* p4 = reinterpret_cast<const float4*>(x + tbase);
+#pragma unroll
+        for (int q = 0; q < ENC_Q; q++) f[q] = p4[tid + ENC_TPB * q];
+    } else {
+#pragma unroll
+        for (int q = 0; q < ENC_Q; q++) {
+            const long long e = tbase + 4 * (tid + ENC_TPB * q);
+            f[q].x = e < n ? x[e] : 0.0f; f[q].y = e + 1 < n ? x[e + 1] : 0.0f;
+            f[q].z = e + 2 < n ? x[e + 2] : 0.0f; f[q].w = e + 3 < n ? x[e + 3] : 0.0f;
+        }
+    }
+}
+
 template <int CT>
 __global__ __launch_bounds__(ENC_TPB) void encode_write_kernel(
     const float* __restrict__ x, long long n, long long idx0, Params P, uint32_t* __restrict__ out,
@@ -166,21 +183,17 @@ __global__ __launch_bounds__(ENC_TPB) void encode_write_kernel(
     const long long base = tbase + (long long)tid * ENC_K;
     const unsigned long long G = toff[tile];
     const bool full = tbase + ENC_TILE <= n && idx0 + tbase >= 3;
+    // the first elements of the next tile (for the head tokens) are loaded now, used after the tokens
+    float h0 = 0.0f, h1 = 0.0f, h2 = 0.0f, h3 = 0.0f;
+    const bool hin = wid == 1 && lane < 11 && tbase + ENC_TILE + lane < n;
+    if (hin) {
+        const long long e = tbase + ENC_TILE + lane;
+        h0 = x[e]; h1 = x[e - 1]; h2 = x[e - 2]; h3 = x[e - 3];
+    }
     // ---- coalesced float4 loads -> LDS (one pad word per 16 floats), then 16 consecutive per lane
     {
         float4 f[ENC_Q];
-        if (tbase + ENC_TILE <= n) {
-            const float4* p4 = reinterpret_cast<const float4*>(x + tbase);
-#pragma unroll
-            for (int q = 0; q < ENC_Q; q++) f[q] = p4[tid + ENC_TPB * q];
-        } else {
-#pragma unroll
-            for (int q = 0; q < ENC_Q; q++) {
-                const long long e = tbase + 4 * (tid + ENC_TPB * q);
-                f[q].x = e < n ? x[e] : 0.0f; f[q].y = e + 1 < n ? x[e + 1] : 0.0f;
-                f[q].z = e + 2 < n ? x[e + 2] : 0.0f; f[q].w = e + 3 < n ? x[e + 3] : 0.0f;
-            }
-        }
+        load_tile4(x, n, tbase, tid, f);
 #pragma unroll
         for (int q = 0; q < ENC_Q; q++) {
             const int e = 4 * (tid + ENC_TPB * q);
@@ -235,12 +248,9 @@ __global__ __launch_bounds__(ENC_TPB) void encode_write_kernel(
     if (lane == 63) s_wsum[wid] = inc;
 
     // ---- head: first <= 31 bits of the elements after this tile (completes our last word)
-    const long long nb = tbase + ENC_TILE;
     if (wid == 1 && lane < 12) {
         uint32_t hv = 0u; int hl = 0;
-        const long long e = nb + lane;
-        if (lane < 11 && e < n)
-            make_token<CT>(x[e], x[e - 1], x[e - 2], x[e - 3], idx0 + e >= 3, P, hv, hl);
+        if (lane < 11 && hin) make_token<CT>(h0, h1, h2, h3, idx0 + tbase + ENC_TILE + lane >= 3, P, hv, hl);
         s_head_val[lane] = hv;
         s_head_len[lane] = hl;
     }
@@ -315,6 +325,21 @@ __global__ __launch_bounds__(ENC_TPB) void encode_write_kernel(
         default: return -2;                                                                        \
     }
 
+// persistent write kernel: as many workgroups as are resident at once
+static unsigned write_grid(int ct) {
+    static unsigned cache[12];
+    const int ci = (ct > 0 && ct < 12) ? ct : 0;
+    if (cache[ci]) return cache[ci];
+    int dev = 0, ncu = 256, per = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const void* f = ct == 5 ? (const void*)encode_write_kernel<5> : ct == 6 ? (const void*)encode_write_kernel<6>
+                  : ct == 7 ? (const void*)encode_write_kernel<7> : (const void*)encode_write_kernel<11>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, ENC_TPB, 0) != hipSuccess || per < 1) per = 1;
+    cache[ci] = (unsigned)(per * ncu);
+    return cache[ci];
+}
+
 extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, const Params* P,
                                 uint32_t* out, uint64_t* desc, unsigned* tile_ctr, uint32_t epoch,
                                 int start_bit, unsigned long long* total_bits, unsigned* err,
@@ -326,8 +351,8 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
     uint32_t* tbits = reinterpret_cast<uint32_t*>(desc + ntiles);     // desc holds 2 * ntiles words
     dc_mark_phase(0, stream);
     // one wave (count) / one workgroup (write) per tile: measured faster than persistent grids here
-    const unsigned gc = (ntiles + 3) / 4;
-    const unsigned gw = ntiles;
+    const unsigned gc = (2 * ntiles + 3) / 4;
+    const unsigned gw = std::min<unsigned>(ntiles, write_grid(P->ct));
     DC_ENC_DISPATCH(encode_count_kernel, dim3(gc), dim3(256), 0, stream, x, n, idx0, *P, tbits,
                     (long long)ntiles, err);
     dc_mark_phase(1, stream);

@@ -25,3 +25,6 @@ t0 = a[:, 0].min()
 print("tiles", len(a), "span us", (a[:, 5].max() - t0) / 100.0)
 order = np.argsort(a[:, 0])
 print("start times of tiles 0,1000,2000,..:", [round((a[i, 0] - t0) / 100.0, 1) for i in range(0, len(a), 1000)])
+dur = (a[:, 5] - a[:, 0]) / 100.0
+span = (a[:, 5].max() - a[:, 0].min()) / 100.0
+print("tile duration mean %.2f us; implied concurrent tiles %.0f" % (dur.mean(), len(a) * dur.mean() / span))
