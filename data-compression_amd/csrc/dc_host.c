@@ -62,6 +62,12 @@ typedef struct {
     int* d_i;                        /* [0] type */
     uint32_t* d_crctab; uint32_t* d_x2n; uint32_t* d_crcparts; long long crcparts_cap; uint32_t* d_crc;
     unsigned long long* d_ham;
+    /* CT1 byte-wise codec */
+    void* c1_scr; size_t c1_scr_cap;
+    void* c1_in; size_t c1_in_cap;
+    void* c1_codes; size_t c1_codes_cap;
+    void* c1_pos; size_t c1_pos_cap;
+    void* c1_out; size_t c1_out_cap;
     char msg[512];
 } dc_ctx;
 
@@ -788,4 +794,130 @@ void add_bit_to_bytes(unsigned char** data_bits, int* bytes, int* pos, int flag)
     bit_set(&(*data_bits)[*bytes - 1], (unsigned char)*pos, flag);
     (*pos)--;
     if (*pos == 0) *pos = 8;
+}
+
+/* ============================================================================================
+ * CT1 byte-wise codec: myCompress (impl/dataCompression.c:3980-4118), myDecompress (:3943-3977)
+ * ========================================================================================== */
+static int c1_scratch(long long n, uint32_t** traw, unsigned long long** rawoff, uint8_t** carr) {
+    const long long nt = dc_ct1_tiles(n > 0 ? n : 1);
+    const size_t need = (size_t)nt * 4 + 16 + (size_t)(nt + 1) * 8 + (size_t)n + 64;
+    int rc = grow(&G.c1_scr, &G.c1_scr_cap, need);
+    if (rc) return rc;
+    char* p = (char*)G.c1_scr;
+    *rawoff = (unsigned long long*)p;                    /* 8-byte aligned first */
+    *traw = (uint32_t*)(p + (size_t)(nt + 1) * 8);
+    *carr = (uint8_t*)(p + (size_t)(nt + 1) * 8 + (size_t)nt * 4 + 16);
+    return DC_OK;
+}
+
+int dc_ct1_encode_device(const void* d_x, long long n, void* d_raw, void* d_codes, void* d_pos1, long long* nraw_out) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (n < 0) return seterr(DC_ERR_ARG, "n < 0");
+    if (n == 0) { if (nraw_out) *nraw_out = 0; return DC_OK; }
+    uint32_t* traw; unsigned long long* rawoff; uint8_t* carr;
+    if ((rc = c1_scratch(n, &traw, &rawoff, &carr))) return rc;
+    HIPCHK(hipMemsetAsync(G.d_enc_err, 0, 4, G.st));
+    if (dc_launch_ct1_encode((const float*)d_x, n, thr_le(absErrBound), traw, rawoff, (float*)d_raw, (char*)d_codes,
+                             (int*)d_pos1, G.d_enc_err, G.st))
+        return seterr(DC_ERR_HIP, "ct1 encode launch failed");
+    const long long nt = dc_ct1_tiles(n);
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[0], rawoff + nt, 8, hipMemcpyDeviceToHost, G.st));
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[1], G.d_enc_err, 4, hipMemcpyDeviceToHost, G.st));
+    HIPCHK(hipStreamSynchronize(G.st));
+    if (G.h_scratch[1] & 1u) return seterr(DC_ERR_INPUT, "input contains -1.0f (the reference's history sentinel)");
+    if (nraw_out) *nraw_out = (long long)G.h_scratch[0];
+    return DC_OK;
+}
+
+int dc_ct1_decode_device(const void* d_raw, long long nraw, const void* d_codes, const void* d_pos1, long long ncodes,
+                         long long num, void* d_out) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (num <= 0) return DC_OK;
+    uint32_t* traw; unsigned long long* rawoff; uint8_t* carr;
+    if ((rc = c1_scratch(num, &traw, &rawoff, &carr))) return rc;
+    HIPCHK(hipMemsetAsync(G.d_enc_err, 0, 4, G.st));
+    if (dc_launch_ct1_decode((const float*)d_raw, nraw, (const char*)d_codes, (const int*)d_pos1, ncodes, num, carr, traw,
+                             rawoff, (float*)d_out, G.d_enc_err, G.st))
+        return seterr(DC_ERR_HIP, "ct1 decode launch failed");
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[1], G.d_enc_err, 4, hipMemcpyDeviceToHost, G.st));
+    HIPCHK(hipStreamSynchronize(G.st));
+    if (G.h_scratch[1] & 4u) return seterr(DC_ERR_STREAM, "ct1 codes out of range or raw array too short");
+    return DC_OK;
+}
+
+/* h:120 c:3980-4118.  *array_float / *array_char / *array_char_displacement are realloc()ed to the
+ * raw and code counts (left untouched when a count is 0, as the reference does); returns the raw count. */
+int myCompress(float data[], float** array_float, char** array_char, int** array_char_displacement, int num) {
+    const char* fn = "myCompress";
+    int rc = ensure_init();
+    if (rc) { abi_fail(fn, rc); return 0; }
+    if (num <= 0) return 0;
+    const size_t n = (size_t)num;
+    if ((rc = grow(&G.c1_in, &G.c1_in_cap, n * 4 + 64)) || (rc = grow(&G.c1_out, &G.c1_out_cap, n * 4 + 64)) ||
+        (rc = grow(&G.c1_codes, &G.c1_codes_cap, n + 64)) || (rc = grow(&G.c1_pos, &G.c1_pos_cap, n * 4 + 64))) {
+        abi_fail(fn, rc); return 0;
+    }
+    if (hipMemcpyAsync(G.c1_in, data, n * 4, hipMemcpyHostToDevice, G.st) != hipSuccess) {
+        abi_fail(fn, seterr(DC_ERR_HIP, "H2D copy failed")); return 0;
+    }
+    long long nraw = 0;
+    if ((rc = dc_ct1_encode_device(G.c1_in, num, G.c1_out, G.c1_codes, G.c1_pos, &nraw))) { abi_fail(fn, rc); return 0; }
+    const long long nc = num - nraw;
+    if (nraw > 0) {
+        float* a = (float*)realloc(*array_float, sizeof(float) * (size_t)nraw);
+        if (!a) { abi_fail(fn, seterr(DC_ERR_ARG, "realloc failed")); return 0; }
+        *array_float = a;
+        if (hipMemcpy(a, G.c1_out, sizeof(float) * (size_t)nraw, hipMemcpyDeviceToHost) != hipSuccess) {
+            abi_fail(fn, seterr(DC_ERR_HIP, "D2H copy failed")); return 0;
+        }
+    }
+    if (nc > 0) {
+        char* c = (char*)realloc(*array_char, (size_t)nc);
+        int* p = (int*)realloc(*array_char_displacement, sizeof(int) * (size_t)nc);
+        if (!c || !p) { abi_fail(fn, seterr(DC_ERR_ARG, "realloc failed")); return 0; }
+        *array_char = c;
+        *array_char_displacement = p;
+        if (hipMemcpy(c, G.c1_codes, (size_t)nc, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(p, G.c1_pos, sizeof(int) * (size_t)nc, hipMemcpyDeviceToHost) != hipSuccess) {
+            abi_fail(fn, seterr(DC_ERR_HIP, "D2H copy failed")); return 0;
+        }
+    }
+    return (int)nraw;
+}
+
+/* h:121 c:3943-3977.  The reference does not pass the code count: it consumes displacement entries
+ * while they name a later position (reading one entry past the last code).  The same rule gives the
+ * count here: entries are taken while they increase and stay within [1, num]. */
+float* myDecompress(float array_float[], char array_char[], int array_char_displacement[], int num) {
+    const char* fn = "myDecompress";
+    float* out = (float*)malloc(sizeof(float) * (size_t)(num > 0 ? num : 1));
+    int rc = ensure_init();
+    if (rc) { abi_fail(fn, rc); return out; }
+    if (num <= 0) return out;
+    long long nc = 0;
+    if (array_char_displacement) {
+        int prev = 0;
+        while (nc < num && array_char_displacement[nc] > prev && array_char_displacement[nc] <= num) {
+            prev = array_char_displacement[nc];
+            nc++;
+        }
+    }
+    const long long nraw = num - nc;
+    const size_t n = (size_t)num;
+    if ((rc = grow(&G.c1_in, &G.c1_in_cap, n * 4 + 64)) || (rc = grow(&G.c1_out, &G.c1_out_cap, n * 4 + 64)) ||
+        (rc = grow(&G.c1_codes, &G.c1_codes_cap, n + 64)) || (rc = grow(&G.c1_pos, &G.c1_pos_cap, n * 4 + 64))) {
+        abi_fail(fn, rc); return out;
+    }
+    if ((nraw > 0 && hipMemcpyAsync(G.c1_in, array_float, sizeof(float) * (size_t)nraw, hipMemcpyHostToDevice, G.st) != hipSuccess) ||
+        (nc > 0 && hipMemcpyAsync(G.c1_codes, array_char, (size_t)nc, hipMemcpyHostToDevice, G.st) != hipSuccess) ||
+        (nc > 0 && hipMemcpyAsync(G.c1_pos, array_char_displacement, sizeof(int) * (size_t)nc, hipMemcpyHostToDevice, G.st) != hipSuccess)) {
+        abi_fail(fn, seterr(DC_ERR_HIP, "H2D copy failed")); return out;
+    }
+    if ((rc = dc_ct1_decode_device(G.c1_in, nraw, G.c1_codes, G.c1_pos, nc, num, G.c1_out))) abi_fail(fn, rc);
+    if (hipMemcpy(out, G.c1_out, sizeof(float) * n, hipMemcpyDeviceToHost) != hipSuccess)
+        abi_fail(fn, seterr(DC_ERR_HIP, "D2H copy failed"));
+    return out;
 }

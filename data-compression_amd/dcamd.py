@@ -26,13 +26,13 @@ ABI_SYMBOLS = [
     "myDecompress_bitwise", "myDecompress_bitwise_np", "myDecompress_bitwise_op", "myDecompress_bitwise_mask",
     "toSmallDataset_float", "med_dataset_float", "do_crc32", "hmLength", "hamming_encode", "hamming_decode",
     "bit_flip", "block_size", "get_random_int", "floattostr", "strtofloat", "doubletostr", "strtodbl",
-    "getFloatBin", "to_absErrorBound_binary", "add_bit_to_bytes", "bit_set",
+    "getFloatBin", "to_absErrorBound_binary", "add_bit_to_bytes", "bit_set", "myCompress", "myDecompress",
 ]
 EXT_SYMBOLS = [
     "dc_init", "dc_last_error", "dc_get_stream", "dc_synchronize", "dc_set_abs_error_bound",
     "dc_get_abs_error_bound", "dc_stream_capacity", "dc_encode_device", "dc_encode_result",
     "dc_decode_device", "dc_decode_finish", "dc_to_small_device", "dc_med_device", "dc_crc32_device",
-    "dc_decode_chunk_bits_value",
+    "dc_decode_chunk_bits_value", "dc_ct1_encode_device", "dc_ct1_decode_device",
 ]
 
 
@@ -87,6 +87,10 @@ class Lib:
         L.hamming_decode.argtypes = [_u8p, C.c_char_p, C.c_int, C.c_int]
         L.hmLength.argtypes = [C.c_int]
         L.block_size.argtypes = [C.c_int]
+        L.myCompress.argtypes = [_f32p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_int]
+        L.myCompress.restype = C.c_int
+        L.myDecompress.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.myDecompress.restype = vp
 
     # ---- state
     def init(self, device=0):
@@ -140,6 +144,32 @@ class Lib:
         else:
             fn = {5: self.L.myDecompress_bitwise, 6: self.L.myDecompress_bitwise_np, 11: self.L.myDecompress_bitwise_op}
             p = fn[ct](sarg, s.size, num)
+        out = np.frombuffer(C.string_at(p, 4 * num), np.float32).copy() if num else np.zeros(0, np.float32)
+        _libc.free(p)
+        return out
+
+    # ---- CT1 byte-wise codec (myCompress / myDecompress)
+    def ct1_compress(self, x):
+        x = np.ascontiguousarray(x, np.float32)
+        pf, pc, pp = C.c_void_p(None), C.c_void_p(None), C.c_void_p(None)
+        nf = self.L.myCompress(x if x.size else np.zeros(1, np.float32), C.byref(pf), C.byref(pc), C.byref(pp), x.size)
+        nc = x.size - nf
+        raw = np.frombuffer(C.string_at(pf.value, 4 * nf), np.float32).copy() if nf else np.zeros(0, np.float32)
+        codes = C.string_at(pc.value, nc) if nc else b""
+        pos = np.frombuffer(C.string_at(pp.value, 4 * nc), np.int32).copy() if nc else np.zeros(0, np.int32)
+        for q in (pf, pc, pp):
+            if q.value:
+                _libc.free(q)
+        return raw, codes, pos
+
+    def ct1_decompress(self, raw, codes, pos, num):
+        raw = np.ascontiguousarray(raw, np.float32)
+        pos = np.ascontiguousarray(pos, np.int32)
+        # the reference reads one displacement entry past the last code: give it a terminator
+        posx = np.concatenate([pos, np.zeros(1, np.int32)])
+        cb = C.create_string_buffer(bytes(codes), len(codes) + 1)
+        p = self.L.myDecompress(raw.ctypes.data if raw.size else None, C.cast(cb, C.c_void_p),
+                                posx.ctypes.data, num)
         out = np.frombuffer(C.string_at(p, 4 * num), np.float32).copy() if num else np.zeros(0, np.float32)
         _libc.free(p)
         return out

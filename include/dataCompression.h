@@ -57,6 +57,12 @@ void myCompress_bitwise_mask(float data[], int num, unsigned char** data_bits, i
 /* h:67  c:1703-1898 */
 float* myDecompress_bitwise_mask(unsigned char* data_bits, int bytes, int num, int type, char mask[1 + 8 + 8]);
 
+/* ---- CT1: byte-wise 4-predictor split into raw floats + ('a'..'d', 1-based position) codes ----- */
+/* h:120 c:3980-4118: *array_float, *array_char, *array_char_displacement realloc()ed; returns the raw count */
+int myCompress(float data[], float** array_float, char** array_char, int** array_char_displacement, int num);
+/* h:121 c:3943-3977 */
+float* myDecompress(float array_float[], char array_char[], int array_char_displacement[], int num);
+
 /* ---- pre-passes ---------------------------------------------------------------------------------- */
 /* h:96  c:3543-3562: *data_small = data - min (new malloc array), returns min */
 float toSmallDataset_float(float data[], float** data_small, int num);

@@ -63,6 +63,12 @@ int dc_med_device(const void* d_x, long long n, float* mean_out, int* type_out);
 /* zlib-compatible CRC-32 of a device byte range. */
 int dc_crc32_device(const void* d_s, long long nbytes, uint32_t* crc_out);
 
+/* CT1 byte-wise codec on device buffers: d_raw (n floats), d_codes (n chars), d_pos1 (n ints) must
+ * hold the worst case; *nraw_out = raw count (codes = n - raw).  Synchronous. */
+int dc_ct1_encode_device(const void* d_x, long long n, void* d_raw, void* d_codes, void* d_pos1, long long* nraw_out);
+int dc_ct1_decode_device(const void* d_raw, long long nraw, const void* d_codes, const void* d_pos1, long long ncodes,
+                         long long num, void* d_out);
+
 /* Decoder/encoder geometry (for tests and bench). */
 long long dc_decode_chunk_bits_value(void);
 

@@ -193,3 +193,32 @@ def test_signed_inputs(dc, oracle, bound, ct):
     # CT5/7/11: a sign bit parses as a 3-bit code, so the stream decodes to other values (and may end
     # early); the reference decoder's output is still the contract
     assert np.array_equal(out[:got].view(np.uint32), spec[:got].view(np.uint32))
+
+
+@pytest.mark.parametrize("bound", BOUNDS)
+@pytest.mark.parametrize("case", CASES)
+def test_ct1_golden(dc, oracle, bound, case):
+    """CT1 byte-wise codec (myCompress :3980 / myDecompress :3943) vs the compiled reference's arrays."""
+    g = golden(bound)
+    dc.set_bound(bound)
+    x = g[f"{case}/input"]
+    raw, codes, pos = dc.ct1_compress(x)
+    assert np.array_equal(raw.view(np.uint32), g[f"{case}/ct1/raw"].view(np.uint32))
+    assert codes == g[f"{case}/ct1/codes"].tobytes()
+    assert np.array_equal(pos, g[f"{case}/ct1/pos"])
+    out = dc.ct1_decompress(raw, codes, pos, x.size)
+    ref = oracle.bytewise_decompress(raw, codes, pos, x.size)
+    assert np.array_equal(out.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("kind,n", [("u10", 1 << 20), ("ramp", 300000), ("himeno", 1 << 18), ("mixed", 500000),
+                                    ("eq", 100000)])
+def test_ct1_roundtrip(dc, oracle, kind, n):
+    dc.set_bound(1e-3)
+    x = _inputs(oracle, kind, n)
+    raw, codes, pos = dc.ct1_compress(x)
+    r2, c2, p2 = oracle.bytewise_compress(x, 1e-3)
+    assert np.array_equal(raw.view(np.uint32), r2.view(np.uint32)) and codes == c2 and np.array_equal(pos, p2)
+    out = dc.ct1_decompress(raw, codes, pos, n)
+    ref = oracle.bytewise_decompress(raw, codes, pos, n)
+    assert np.array_equal(out.view(np.uint32), ref.view(np.uint32))
