@@ -365,6 +365,18 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// count + scan only: total bits (start_bit + stream bits) of an encode, nothing written
+extern "C" int dc_launch_encode_bits(const float* x, long long n, long long idx0, const Params* P, uint64_t* desc,
+                                     unsigned long long* total_bits, unsigned* err, hipStream_t stream) {
+    if (n <= 0) return 0;
+    const unsigned ntiles = (unsigned)((n + ENC_TILE - 1) / ENC_TILE);
+    uint32_t* tbits = reinterpret_cast<uint32_t*>(desc + ntiles);
+    const unsigned gc = (2 * ntiles + 3) / 4;
+    DC_ENC_DISPATCH(encode_count_kernel, dim3(gc), dim3(256), 0, stream, x, n, idx0, *P, tbits, (long long)ntiles, err);
+    hipLaunchKernelGGL(encode_scan_kernel, dim3(1), dim3(1024), 0, stream, tbits, desc, (long long)ntiles, 0, total_bits);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" long long dc_encode_tile_count(long long n) { return (n + ENC_TILE - 1) / ENC_TILE; }
 
 }  // namespace dc

@@ -272,6 +272,36 @@ int dc_encode_device(int ct, const void* d_x, long long n, long long idx0, int t
     return DC_OK;
 }
 
+/* bits an encode of these n floats would produce (no stream written); synchronous */
+int dc_encode_bits_device(int ct, const void* d_x, long long n, long long idx0, int type, uint32_t mask17,
+                          unsigned long long* bits_out) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (!valid_ct(ct)) return seterr(DC_ERR_ARG, "unsupported CT %d", ct);
+    if (n < 0) return seterr(DC_ERR_ARG, "n < 0");
+    if (ct == 7 && (type < 1 || type > 7)) return seterr(DC_ERR_ARG, "CT7 type %d outside 1..7", type);
+    if ((uintptr_t)d_x & 15u) return seterr(DC_ERR_ARG, "misaligned device buffer");
+    if (n == 0) { *bits_out = 0; return DC_OK; }
+    Params P;
+    make_params(&P, ct, type, mask17);
+    const long long ntiles = dc_encode_tile_count(n);
+    if (2 * ntiles + 8 > G.enc_desc_cap) {
+        if (G.enc_desc) HIPCHK(hipFree(G.enc_desc));
+        const long long cap = 2 * ntiles + 1024;
+        HIPCHK(hipMalloc((void**)&G.enc_desc, cap * sizeof(uint64_t)));
+        G.enc_desc_cap = cap;
+    }
+    HIPCHK(hipMemsetAsync(G.d_enc_err, 0, 4, G.st));
+    if (dc_launch_encode_bits((const float*)d_x, n, idx0, &P, G.enc_desc, G.d_total, G.d_enc_err, G.st))
+        return seterr(DC_ERR_HIP, "encode launch failed");
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[0], G.d_total, 8, hipMemcpyDeviceToHost, G.st));
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[1], G.d_enc_err, 4, hipMemcpyDeviceToHost, G.st));
+    HIPCHK(hipStreamSynchronize(G.st));
+    if (G.h_scratch[1] & 1u) return seterr(DC_ERR_INPUT, "input contains -1.0f (the reference's history sentinel)");
+    *bits_out = G.h_scratch[0];
+    return DC_OK;
+}
+
 int dc_encode_result(unsigned long long* total_bits) {
     int rc = ensure_init();
     if (rc) return rc;

@@ -32,7 +32,7 @@ EXT_SYMBOLS = [
     "dc_init", "dc_last_error", "dc_get_stream", "dc_synchronize", "dc_set_abs_error_bound",
     "dc_get_abs_error_bound", "dc_stream_capacity", "dc_encode_device", "dc_encode_result",
     "dc_decode_device", "dc_decode_finish", "dc_to_small_device", "dc_med_device", "dc_crc32_device",
-    "dc_decode_chunk_bits_value", "dc_ct1_encode_device", "dc_ct1_decode_device",
+    "dc_decode_chunk_bits_value", "dc_ct1_encode_device", "dc_ct1_decode_device", "dc_encode_bits_device",
 ]
 
 
@@ -63,6 +63,7 @@ class Lib:
         L.dc_stream_capacity.restype = C.c_size_t
         L.dc_encode_device.argtypes = [C.c_int, vp, ll, ll, C.c_int, u32, C.c_int, vp, vp]
         L.dc_encode_result.argtypes = [C.POINTER(C.c_ulonglong)]
+        L.dc_encode_bits_device.argtypes = [C.c_int, vp, ll, ll, C.c_int, u32, C.POINTER(C.c_ulonglong)]
         L.dc_decode_device.argtypes = [C.c_int, vp, ll, vp, ll, ll, C.c_int, u32, vp]
         L.dc_to_small_device.argtypes = [vp, ll, vp, C.POINTER(C.c_float)]
         L.dc_med_device.argtypes = [vp, ll, C.POINTER(C.c_float), C.POINTER(C.c_int)]
@@ -215,6 +216,11 @@ class Lib:
         self.check(self.L.dc_encode_device(ct, x_ptr, n, idx0, type_, mask17, start_bit, out_ptr, total_ptr),
                    "dc_encode_device")
 
+    def encode_bits(self, ct, x_ptr, n, idx0=0, type_=0, mask17=0):
+        v = C.c_ulonglong(0)
+        self.check(self.L.dc_encode_bits_device(ct, x_ptr, n, idx0, type_, mask17, C.byref(v)), "dc_encode_bits_device")
+        return v.value
+
     def encode_result(self):
         v = C.c_ulonglong(0)
         self.check(self.L.dc_encode_result(C.byref(v)), "dc_encode_result")
@@ -239,6 +245,47 @@ class Lib:
         v = C.c_uint32(0)
         self.check(self.L.dc_crc32_device(s_ptr, nbytes, C.byref(v)), "dc_crc32_device")
         return v.value
+
+
+# ---- multi-GPU: one process per GPU, contiguous shards -------------------------
+def shard_offsets(bits_per_rank):
+    """Exclusive scan of the per-rank stream bit counts -> global start bit of every shard."""
+    out, acc = [], 0
+    for b in bits_per_rank:
+        out.append(acc)
+        acc += int(b)
+    return out, acc
+
+
+def gather_stream(local, start_bit, local_bits, group=None):
+    """All-gather per-rank shard streams into the single global stream (every rank gets it).
+
+    local: uint8 torch tensor holding this rank's shard, encoded with start_bit = (global start bit
+    mod 8) so its first byte's high bits are zero; local_bits = start_bit + the shard's bits.  The
+    shards are placed at their global byte offsets and the byte two shards share is OR-ed: the
+    result is byte-identical to encoding the whole array in one stream.  Works with
+    gloo (CPU tensors) and RCCL (device tensors)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    dev = local.device
+    meta = torch.tensor([int(local_bits) - int(start_bit), int(start_bit)], dtype=torch.int64, device=dev)
+    metas = [torch.zeros_like(meta) for _ in range(world)]
+    dist.all_gather(metas, meta, group=group)
+    bits = [int(m[0]) for m in metas]
+    starts, total = shard_offsets(bits)
+    nbytes = [(int(m[1]) + b + 7) // 8 for m, b in zip(metas, bits)]
+    pad = max(nbytes) if nbytes else 0
+    buf = torch.zeros(pad, dtype=torch.uint8, device=dev)
+    buf[: local.numel()] = local[:pad]
+    parts = [torch.zeros_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    out = torch.zeros((total + 7) // 8, dtype=torch.uint8, device=dev)
+    for g in range(world):
+        b0, nb = starts[g] // 8, nbytes[g]
+        if nb:
+            out[b0:b0 + nb] |= parts[g][:nb]
+    return out, total
 
 
 def gen_u10(n, seed=42, offset=0):

@@ -45,6 +45,10 @@ size_t dc_stream_capacity(long long n);
  * *d_total_bits (device, may be NULL) receives start_bit + bits written. */
 int dc_encode_device(int ct, const void* d_x, long long n, long long idx0, int type, uint32_t mask17,
                      int start_bit, void* d_out, unsigned long long* d_total_bits);
+/* Stream bits an encode of these n floats would produce, without writing a stream (count + scan
+ * kernels only; synchronous).  The multi-GPU path uses it to place shards before encoding them. */
+int dc_encode_bits_device(int ct, const void* d_x, long long n, long long idx0, int type, uint32_t mask17,
+                          unsigned long long* bits_out);
 /* Wait for the last encode and return start_bit + bits written (host value). */
 int dc_encode_result(unsigned long long* total_bits);
 

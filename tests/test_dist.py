@@ -1,0 +1,83 @@
+"""Multi-process (gloo, world_size 2, CPU) tests of the sharded path: per-rank shard streams are
+stitched into the single-stream bytes by an all-gather (dcamd.gather_stream), as the RCCL path does
+on GPUs.  Shard streams come from the oracle (test infrastructure): the first k tokens of a stream
+depend only on x[:k] (encoder history = original inputs), so a shard's bits are the global stream's
+bits between the two shard boundaries."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "data-compression_amd"))
+
+
+def _bits_of(nbytes, pos):
+    return nbytes * 8 if pos == 8 else (nbytes - 1) * 8 + (8 - pos)
+
+
+def _extract(stream, b0, b1):
+    """bits [b0, b1) of stream, re-packed so that they start at bit b0 % 8 of byte 0."""
+    bits = np.unpackbits(stream)
+    lead = b0 % 8
+    sub = np.concatenate([np.zeros(lead, np.uint8), bits[b0:b1]])
+    return np.packbits(sub)
+
+
+def _worker(rank, world, port, ct, n, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import dcamd
+        from pyoracle import Oracle
+        O = Oracle()
+        x = O.gen_u10(n)
+        _, xs = O.to_small(x)
+        t, m17 = O.type_mask(xs)
+        s, nb, pos = O.compress(ct, xs, 1e-3, t, m17)
+        cut = [n * r // world for r in range(world + 1)]
+        offs = []
+        for c in cut:
+            if c == 0:
+                offs.append(0)
+            else:
+                _, nbc, posc = O.compress(ct, xs[:c], 1e-3, t, m17)
+                offs.append(_bits_of(nbc, posc))
+        b0, b1 = offs[rank], offs[rank + 1]
+        local = torch.from_numpy(_extract(s, b0, b1))
+        out, total = dcamd.gather_stream(local, b0 % 8, b0 % 8 + (b1 - b0))
+        q.put((rank, total == _bits_of(nb, pos), bool(np.array_equal(out.numpy(), s))))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+@pytest.mark.parametrize("ct,n", [(7, 20001), (6, 4099), (5, 777)])
+def test_gather_stream_world2(ct, n):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, ct, n, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] and r[2] for r in res), res
+
+
+def test_shard_offsets():
+    import dcamd
+    assert dcamd.shard_offsets([5, 0, 7]) == ([0, 5, 5], 12)

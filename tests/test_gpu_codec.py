@@ -222,3 +222,37 @@ def test_ct1_roundtrip(dc, oracle, kind, n):
     out = dc.ct1_decompress(raw, codes, pos, n)
     ref = oracle.bytewise_decompress(raw, codes, pos, n)
     assert np.array_equal(out.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("ct", CTS)
+def test_shard_encode_with_start_bit(dc, oracle, ct):
+    """Multi-GPU building blocks on one device: a shard's bit count (count kernels only), then the
+    shard encoded at start_bit = global offset mod 8 with its predictor halo, equals the global
+    stream's bits of that shard."""
+    import torch
+    dc.set_bound(1e-3)
+    n = 300000
+    x = oracle.gen_u10(n)
+    _, xs = oracle.to_small(x)
+    t, m17 = oracle.type_mask(xs)
+    s, nb, pos = oracle.compress(ct, xs, 1e-3, t, m17)
+    cut = 123457
+    _, nbc, posc = oracle.compress(ct, xs[:cut], 1e-3, t, m17)
+    b0 = nbc * 8 if posc == 8 else (nbc - 1) * 8 + (8 - posc)
+    total = nb * 8 if pos == 8 else (nb - 1) * 8 + (8 - pos)
+    pad = (4 - cut % 4) % 4                                        # 16-byte aligned shard start
+    dx2 = torch.from_numpy(np.concatenate([np.zeros(pad, np.float32), xs])).cuda()
+    shard = dx2[pad + cut:]
+    assert shard.data_ptr() % 16 == 0
+    bits1 = dc.encode_bits(ct, shard.data_ptr(), n - cut, idx0=cut, type_=t, mask17=m17)
+    assert bits1 == total - b0
+    cap = dc.stream_capacity(n - cut)
+    out = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    dc.encode_device(ct, shard.data_ptr(), n - cut, out.data_ptr(), idx0=cut, type_=t, mask17=m17, start_bit=b0 % 8)
+    tb = dc.encode_result()
+    assert tb == b0 % 8 + bits1
+    got = out[: (tb + 7) // 8].cpu().numpy()
+    bits = np.unpackbits(s)[b0:total]
+    want = np.packbits(np.concatenate([np.zeros(b0 % 8, np.uint8), bits]))
+    assert np.array_equal(got, want)
