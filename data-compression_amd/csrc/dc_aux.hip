@@ -120,6 +120,137 @@ __global__ __launch_bounds__(256) void med_kernel(const float* __restrict__ x, l
     }
 }
 
+// ---------------------------------------------------------------- exact parallel mean
+// med_dataset_float (:3593-3620) sums left to right in float.  While the running sum s stays in one
+// binade [2^e, 2^(e+1)) its ulp u is fixed and fl(s + x) = s + u*r(x), with r = x/u rounded to an
+// integer (ties to even on s/u, i.e. on the parity of k = s/u).  So a run of elements is a 2-state
+// transducer: start parity -> (added units, end parity).  One workgroup walks the array in LDS
+// chunks: each thread folds its elements for both start parities, a block scan composes the
+// threads, and the chunk is applied at once unless the sum would leave the binade (or an element is
+// negative / not finite / too large), in which case lane 0 adds the elements around that point one
+// at a time, exactly like the reference.  Below 2^20 the sum is always added one element at a time.
+constexpr int MX_CH = 8192;                                // floats staged per chunk
+constexpr int MX_T = 1024;
+
+__global__ __launch_bounds__(MX_T) void med_exact_kernel(const float* __restrict__ x, long long n,
+                                                         float* __restrict__ out_mean, int* __restrict__ out_type) {
+    __shared__ float buf[MX_CH];
+    __shared__ int fd[2][2][MX_T];                          // [buffer][start parity] units added
+    __shared__ unsigned char fe[2][2][MX_T];                // [buffer][start parity] end parity
+    __shared__ int fbad[2][MX_T];                           // first thread (inclusive scan of "cannot")
+    __shared__ float s_sum;
+    __shared__ int s_start;
+    __shared__ float smax[MX_T];
+    const int tid = threadIdx.x;
+    float mx = x[0];
+    if (tid == 0) s_sum = 0.0f;
+    for (long long c0 = 0; c0 < n; c0 += MX_CH) {
+        const int m = (int)min((long long)MX_CH, n - c0);
+        for (int i = tid; i < m; i += MX_T) { const float v = x[c0 + i]; buf[i] = v; mx = v > mx ? v : mx; }
+        if (tid == 0) s_start = 0;
+        __syncthreads();
+        while (true) {
+            if (tid == 0) {                                 // small sums: exact serial adds
+                float sv = s_sum;
+                int st = s_start;
+                while (st < m && !(sv >= 1048576.0f && sv < 3.0e38f)) sv = __fadd_rn(sv, buf[st++]);
+                s_sum = sv;
+                s_start = st;
+            }
+            __syncthreads();
+            const int st = s_start;
+            if (st >= m) break;
+            const float sv = s_sum;
+            const uint32_t sb = __float_as_uint(sv);
+            const int E = (int)((sb >> 23) & 0xFFu);       // s in [2^(E-127), 2^(E-126)), u = 2^(E-150)
+            const int k0 = (int)((sb & 0x7FFFFFu) | 0x800000u);
+            const float scale = __uint_as_float((uint32_t)(277 - E) << 23);   // 2^(150-E) = 1/u
+            const float lim = __uint_as_float((uint32_t)(E + 1) << 23);       // 2^(E-126)
+            // this thread's contiguous share of [st, m)
+            const int len = m - st, per = (len + MX_T - 1) / MX_T;
+            const int b = st + tid * per, e = min(m, b + per);
+            int d0 = 0, d1 = 0, p0 = 0, p1 = 1;
+            bool bad = false;
+            for (int i = b; i < e; i++) {
+                const float v = buf[i];
+                bad |= !(v >= 0.0f) || !(v < lim);          // negative, NaN, inf or >= the binade
+                const float q = __fmul_rn(v, scale);        // exact: power-of-two scaling
+                const float fq = floorf(q);
+                const float fr = __fsub_rn(q, fq);
+                const int fl = (int)fq;
+                const int up = fr > 0.5f ? 1 : 0, tie = fr == 0.5f ? 1 : 0;
+                const int r0 = fl + up + (tie & ((p0 + fl) & 1));
+                const int r1 = fl + up + (tie & ((p1 + fl) & 1));
+                d0 += r0; d1 += r1;
+                p0 = (p0 + r0) & 1; p1 = (p1 + r1) & 1;
+                bad |= (d0 > (1 << 24)) || (d1 > (1 << 24));
+            }
+            int cur = 0;
+            fd[0][0][tid] = d0; fd[0][1][tid] = d1; fe[0][0][tid] = (unsigned char)p0; fe[0][1][tid] = (unsigned char)p1;
+            fbad[0][tid] = bad ? tid : MX_T;
+            __syncthreads();
+            for (int dd = 1; dd < MX_T; dd <<= 1) {         // inclusive scan: F_t = f_t o ... o f_0
+                int a0 = fd[cur][0][tid], a1 = fd[cur][1][tid];
+                int q0 = fe[cur][0][tid], q1 = fe[cur][1][tid];
+                int bb = fbad[cur][tid];
+                if (tid >= dd) {
+                    const int b0 = fd[cur][0][tid - dd], b1 = fd[cur][1][tid - dd];
+                    const int e0 = fe[cur][0][tid - dd], e1 = fe[cur][1][tid - dd];
+                    // earlier part (tid-dd) first: start parity p -> its end parity feeds ours
+                    const int na0 = b0 + (e0 ? a1 : a0), na1 = b1 + (e1 ? a1 : a0);
+                    const int nq0 = e0 ? q1 : q0, nq1 = e1 ? q1 : q0;
+                    a0 = na0; a1 = na1; q0 = nq0; q1 = nq1;
+                    bb = min(bb, fbad[cur][tid - dd]);
+                }
+                fd[cur ^ 1][0][tid] = a0; fd[cur ^ 1][1][tid] = a1;
+                fe[cur ^ 1][0][tid] = (unsigned char)q0; fe[cur ^ 1][1][tid] = (unsigned char)q1;
+                fbad[cur ^ 1][tid] = bb;
+                cur ^= 1;
+                __syncthreads();
+            }
+            // first thread whose inclusive sum leaves the binade (k >= 2^24) or that saw a bad element
+            const int par = k0 & 1;
+            const int kend = k0 + fd[cur][par][tid];
+            const bool leave = kend >= (1 << 24) || fbad[cur][tid] <= tid;
+            const int first = __syncthreads_or(leave) ? 0 : -1;
+            __shared__ int s_first;
+            if (tid == 0) s_first = MX_T;
+            __syncthreads();
+            if (first == 0 && leave) atomicMin(&s_first, tid);
+            __syncthreads();
+            const int f = s_first;
+            if (tid == 0) {
+                if (f >= MX_T) {                            // whole remainder applied at once
+                    s_sum = __fmul_rn((float)(k0 + fd[cur][par][MX_T - 1]), __uint_as_float((uint32_t)(E - 23) << 23));
+                    s_start = m;
+                } else {                                    // apply threads < f, then f's elements serially
+                    const int kf = f == 0 ? k0 : k0 + fd[cur][par][f - 1];
+                    float sv2 = __fmul_rn((float)kf, __uint_as_float((uint32_t)(E - 23) << 23));
+                    const int bf = st + f * per, ef = min(m, bf + per);
+                    for (int i = bf; i < ef; i++) sv2 = __fadd_rn(sv2, buf[i]);
+                    s_sum = sv2;
+                    s_start = ef;
+                }
+            }
+            __syncthreads();
+        }
+        __syncthreads();
+    }
+    smax[tid] = mx;
+    __syncthreads();
+    if (tid == 0) {
+        float mm = smax[0];
+        for (int i = 1; i < MX_T; i++) if (smax[i] > mm) mm = smax[i];
+        int type = 0, add = 0;                               // :3605-3614
+        for (int i = 7; i > 0; i--) {
+            add += 1 << i;
+            if ((double)mm < ldexp(1.0, add - 127)) { type = 8 - i; break; }
+        }
+        *out_type = type;
+        *out_mean = __fdiv_rn(s_sum, (float)n);
+    }
+}
+
 // ---------------------------------------------------------------- CRC-32 (zlib)
 constexpr uint32_t CRC_POLY = 0xEDB88320u;
 constexpr int CRC_RUN = 64;                               // bytes per lane
@@ -286,7 +417,7 @@ extern "C" int dc_launch_to_small(const float* x, long long n, float* y, float* 
 
 extern "C" int dc_launch_med(const float* x, long long n, float* d_mean, int* d_type, hipStream_t st) {
     if (n <= 0) return 0;
-    hipLaunchKernelGGL(med_kernel, dim3(1), dim3(256), 0, st, x, n, d_mean, d_type);
+    hipLaunchKernelGGL(med_exact_kernel, dim3(1), dim3(MX_T), 0, st, x, n, d_mean, d_type);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

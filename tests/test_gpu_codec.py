@@ -256,3 +256,27 @@ def test_shard_encode_with_start_bit(dc, oracle, ct):
     bits = np.unpackbits(s)[b0:total]
     want = np.packbits(np.concatenate([np.zeros(b0 % 8, np.uint8), bits]))
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("kind,n", [("u10", 1 << 24), ("u10", 1 << 20), ("ramp", 1 << 21), ("unit", 3000001),
+                                    ("himeno", 1 << 18), ("signed", 1 << 20), ("nan", 100000), ("tiny", 1 << 20)])
+def test_med_exact_parallel(dc, oracle, kind, n):
+    """med_dataset_float's left-to-right float sum, computed by the binade-transducer scan, must equal
+    the serial sum bit for bit (mean and type)."""
+    import torch
+    rs = np.random.RandomState(n % 1000)
+    if kind == "signed":
+        x = (rs.randn(n) * 3).astype(np.float32)
+    elif kind == "nan":
+        x = oracle.gen_u10(n)
+        x[n // 2] = np.nan
+    elif kind == "tiny":
+        x = (rs.rand(n) * 1e-30).astype(np.float32)
+    else:
+        x = _inputs(oracle, kind, n)
+    d = torch.from_numpy(x).cuda()
+    torch.cuda.synchronize()
+    mean, t = dc.med_device(d.data_ptr(), n)
+    om, ot = oracle.med(x)
+    assert np.array_equal(np.float32(mean).view(np.uint32), np.float32(om).view(np.uint32)), (mean, om)
+    assert t == ot
