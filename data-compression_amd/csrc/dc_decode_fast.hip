@@ -42,30 +42,32 @@ constexpr int UNKE = 63;
 
 __device__ __forceinline__ uint32_t ldw(const uint32_t* L, int w) { return L[w]; }
 
-// branch-free MSB-first reader: w0:w1 hold the next 64 bits from bit sh of w0, w2 the next word,
-// pf the word after it (loaded one step ahead so its LDS latency is off the critical path)
+// branch-free MSB-first reader: w0:w1 hold the next 64 bits from bit sh of w0, w2 the next word.
+// Every step is fetch() (issues the LDS read of the word after w2, at the top of the step) ... step()
+// (shifts it in).  The read is not loop-carried, so the compiler needs no back-edge copy of an
+// in-flight register -- with a loop-carried prefetch it placed an lgkmcnt(0) wait on every step.
 struct Rd {
-    uint32_t w0, w1, w2, pf;
-    int sh, wi, pos;
+    uint32_t a, b, c, nx;                      // the 64-bit window (a:b) is read from bit 32 - s of a
+    int s, wi, pos;                            // s in [0, 31]; wi = LDS index of a; pos = stream bit
     __device__ __forceinline__ void init(const uint32_t* L, int p) {
-        wi = p >> 5;
-        w0 = ldw(L, wi); w1 = ldw(L, wi + 1); w2 = ldw(L, wi + 2); pf = ldw(L, wi + 3);
-        sh = p & 31;
+        wi = (p - 1) >> 5;                     // a word boundary is bit 32 of a (s = 0), never bit 0
+        s = 32 * (wi + 1) - p;
+        a = ldw(L, max(wi, 0)); b = ldw(L, wi + 1); c = ldw(L, wi + 2);
         pos = p;
     }
+    __device__ __forceinline__ void fetch(const uint32_t* L) { nx = ldw(L, wi + 3); }
     __device__ __forceinline__ uint32_t peek() const {
-        return (uint32_t)(((((uint64_t)w0) << 32) | (uint64_t)w1) << sh >> 32);
+        return __builtin_amdgcn_alignbit(a, b, (uint32_t)s);           // ((a:b) >> s), low word
     }
-    __device__ __forceinline__ void step(const uint32_t* L, int len) {
-        sh += len;
+    __device__ __forceinline__ void step(int len) {
+        uint32_t d;
+        const bool adv = __builtin_usub_overflow((uint32_t)s, (uint32_t)len, &d);   // borrow = next word
+        s = (int)(d & 31u);
         pos += len;
-        const bool adv = sh >= 32;
-        w0 = adv ? w1 : w0;
-        w1 = adv ? w2 : w1;
-        w2 = adv ? pf : w2;
+        a = adv ? b : a;
+        b = adv ? c : b;
+        c = adv ? nx : c;
         wi += adv ? 1 : 0;
-        sh -= adv ? 32 : 0;
-        pf = ldw(L, wi + 3);
     }
 };
 
@@ -138,9 +140,10 @@ __device__ __forceinline__ void walk_lds(const uint32_t* L, const Params& P, int
     while (A.pos < cend) {
         if (A.pos == B.pos) { merged = true; break; }
         const bool sa = A.pos < B.pos || B.pos >= cend;
+        const uint32_t nx = ldw(L, (sa ? A.wi : B.wi) + 3);
         const uint32_t tk = sa ? A.peek() : B.peek();
         const int len = token_len_bf<CT>(tk, P);
-        if (sa) { A.step(L, len); ca++; } else { B.step(L, len); cb++; }
+        if (sa) { A.nx = nx; A.step(len); ca++; } else { B.nx = nx; B.step(len); cb++; }
     }
     if (merged) { *out_exit = pexit; *out_cnt = ca + pcnt - cb; return; }
     const int x = A.pos - (cs + CHUNK_BITS);
@@ -208,17 +211,19 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
             Rd r;
             r.init(S.L, gc == 0 ? cs : cs - OV);
             const unsigned long long q0 = D.dbg ? __builtin_amdgcn_s_memtime() : 0;
-            int nst = 0;
-            while (r.pos < cs) { r.step(S.L, token_len_bf<CT>(r.peek(), P)); nst++; }
-            if (D.dbg && t < 4096 && (c & 63) == 0) {                 // per-wave cycles and steps (diagnostic)
-                int mx = nst;
-                for (int d = 32; d >= 1; d >>= 1) mx = max(mx, __shfl_xor(mx, d, 64));
-                D.dbg[t * 16 + 12 + (c >> 6)] = ((__builtin_amdgcn_s_memtime() - q0) << 16) | (unsigned)mx;
+            while (r.pos < cs) { r.fetch(S.L); r.step(token_len_bf<CT>(r.peek(), P)); }
+            if (D.dbg && t < 4096 && (c & 63) == 0)                  // per-wave cycles (diagnostic)
+                D.dbg[t * 16 + 12 + (c >> 6)] = (__builtin_amdgcn_s_memtime() - q0) << 16;
+            const int pend = min(cs + 32, cend);                      // boundaries in the first word
+            while (r.pos < pend) {
+                r.fetch(S.L);
+                pm |= 1u << (r.pos - cs);
+                r.step(token_len_bf<CT>(r.peek(), P));
+                n++;
             }
             while (r.pos < cend) {
-                const int rel = r.pos - cs;
-                pm |= rel < 32 ? (1u << rel) : 0u;
-                r.step(S.L, token_len_bf<CT>(r.peek(), P));
+                r.fetch(S.L);
+                r.step(token_len_bf<CT>(r.peek(), P));
                 n++;
             }
             const int xx = r.pos - (cs + CHUNK_BITS);
@@ -601,6 +606,7 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
             int j = 0, it = 0;
             // phase A: history still (partly) symbolic, or the stream's first three tokens
             while (r.pos < cend && ((k1 | k2 | k3) != 0 || (first && j < 3))) {
+                r.fetch(S.L);
                 const uint32_t tk = r.peek();
                 const int len = token_len_bf<CT>(tk, P);
                 int code;
@@ -613,7 +619,7 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
                 sent |= (kind == 0 && __float_as_uint(v) == 0xBF800000u) || (first && j < 3 && code != 0);
                 ring[(idx + a0) & (RING - 1)] = v;
                 f3 = f2; k3 = k2; f2 = f1; k2 = k1; f1 = v; k1 = kind;
-                r.step(S.L, len);
+                r.step(len);
                 j++;
                 idx++;
                 if (++it == SECT) {                                  // uniform among the active lanes
@@ -625,6 +631,7 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
             it = 0;
             // phase B: concrete history (kinds stay 0 from here on)
             while (r.pos < cend) {
+                r.fetch(S.L);
                 const uint32_t tk = r.peek();
                 const int len = token_len_bf<CT>(tk, P);
                 int code;
@@ -637,7 +644,7 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
                 ring[(idx + a0) & (RING - 1)] = v;
                 sent |= __float_as_uint(v) == 0xBF800000u;
                 f3 = f2; f2 = f1; f1 = v;
-                r.step(S.L, len);
+                r.step(len);
                 idx++;
                 if (++it == SECT) {
                     it = 0;
@@ -747,6 +754,7 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
             Rd r;
             r.init(S.L, cs + e);
             for (int jj = 0; jj < pend; jj++) {
+                r.fetch(S.L);
                 const uint32_t tk = r.peek();
                 const int len = token_len_bf<CT>(tk, P);
                 int code;
@@ -755,7 +763,7 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
                 if (k0 + jj < (unsigned long long)num) out[k0 + jj] = v;
                 sent |= __float_as_uint(v) == 0xBF800000u;
                 g3 = g2; g2 = g1; g1 = v;
-                r.step(S.L, len);
+                r.step(len);
             }
         }
         if (act) { D.pend[gc] = (uint16_t)min(pend, 65535); D.done[gc] = pend ? 1 : 0; }

@@ -106,6 +106,30 @@ __device__ __forceinline__ void make_token_bf(float x, float b1, float b2, float
     len = l;
 }
 
+// Encoder: token LENGTH only (count pass).  Same decision as make_token_bf: the predicted code is
+// the first strict minimum of (d1, d2, d3), so "some prediction within threshold" is
+// min(d1, d2, d3) <= thr_le, where a NaN d1 keeps dmin = NaN (never predicts) and NaN d2 / d3 are
+// skipped -- exactly IEEE minNum's treatment of the second and third operands.
+template <int CT>
+__device__ __forceinline__ int token_len_enc(float x, float b1, float b2, float b3, bool predict, const Params& P) {
+    const uint32_t u = __float_as_uint(x);
+    int l = CT == 11 ? 32 : min(max((int)((u >> 23) & 0xFFu) + P.rawadd, 9), 32);
+    if (CT == 7) {
+        const bool msk = (u >> 23) == (P.mask17 >> 8);
+        const bool f1 = ((u >> 15) & 0xFFu) != (P.mask17 & 0xFFu);
+        l = msk ? P.lm0 + (f1 ? P.dlm : 0) : l;
+    }
+    if (CT != 6) {
+        const float p2 = __fsub_rn(__fmul_rn(2.0f, b1), b2);
+        const float p3 = __fadd_rn(__fsub_rn(__fmul_rn(3.0f, b1), __fmul_rn(3.0f, b2)), b3);
+        const float d1 = fabsf(__fsub_rn(b1, x));
+        const float dmin = fminf(fminf(d1, fabsf(__fsub_rn(p2, x))), fabsf(__fsub_rn(p3, x)));
+        const bool pr = predict && d1 == d1 && dmin <= P.thr_le;
+        l = (pr || fabsf(x) <= P.thr_lt) ? 3 : l;
+    }
+    return l;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Decoder: token length from the next 32 stream bits (MSB-aligned).  At most 10 bits decide it.
 template <int CT>
@@ -168,7 +192,7 @@ __device__ __forceinline__ int token_len_bf(uint32_t t, const Params& P) {
     if (CT == 11) len = 32;
     if (CT == 7) {
         const bool msk = (t & P.hm) == P.hm;
-        const int lm = P.lm0 + (((t >> P.fsh) & 1u) ? P.dlm : 0);
+        const int lm = (int)__umul24(__builtin_amdgcn_ubfe(t, (uint32_t)P.fsh, 1u), (uint32_t)P.dlm) + P.lm0;
         len = msk ? lm : len;
     }
     if (CT != 6) len = ((int)t < 0) ? 3 : len;

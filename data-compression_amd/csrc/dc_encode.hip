@@ -18,6 +18,7 @@
 // the 256 MiB Infinity Cache when it is read again.
 #include "dc_device.h"
 #include <algorithm>
+#include <stdlib.h>
 
 namespace dc {
 
@@ -25,7 +26,9 @@ constexpr int ENC_TILE = 4096;                  // floats per tile (one offset p
 constexpr int ENC_TPB = 256;                    // write kernel: 4 waves per tile
 constexpr int ENC_K = ENC_TILE / ENC_TPB;       // 16 consecutive floats per lane
 constexpr int ENC_Q = ENC_TILE / 4 / ENC_TPB;   // coalesced float4 loads per lane
-constexpr int CNT_Q = ENC_TILE / 4 / 128;       // count kernel: one wave per half tile, 8 float4 per lane
+constexpr int CNT_Q = 4;                        // count kernel: one wave per tile part, CNT_Q float4 per lane
+constexpr int CNT_SUB = 256 * CNT_Q;            // floats per count wave
+constexpr int CNT_PARTS = ENC_TILE / CNT_SUB;   // count parts per tile (tbits entries)
 constexpr int ENC_LDS_WORDS = ENC_TILE + 48;    // 32 bits/elem max + offset + head slack
 constexpr int STG_WORDS = ENC_TILE + ENC_TILE / 16 + 8;   // staged floats, one pad word per 16
 
@@ -45,65 +48,102 @@ __device__ __forceinline__ float halo_x(const float* __restrict__ x, long long i
     return (idx0 + e >= 0 && e >= -3) ? x[e] : 0.0f;
 }
 
-template <int CT, bool FULL>
-__device__ __forceinline__ void count_tokens(const float4* f, float h1, float h2, float h3, long long tb, long long n,
-                                             long long idx0, const Params& P, uint32_t& sum, bool& neg1) {
+// lane i gets v of lane i-1, lane 0 gets first (DPP wave_shr:1, a GFX9-family wavefront shift)
+__device__ __forceinline__ float wave_shr1(float v, float first) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(first), __float_as_int(v), 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float lane63(float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63)); }
+
+// lengths of the CNT_Q float4s of one count part, every element predicted (history h1..h3 for
+// lane 0's first element)
+template <int CT>
+__device__ __forceinline__ void count_tokens(const float4* f, float h1, float h2, float h3, const Params& P,
+                                             uint32_t& sum, bool& neg1) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int q = 0; q < CNT_Q; q++) {
-        const float p1 = __shfl_up(f[q].w, 1, 64), p2 = __shfl_up(f[q].z, 1, 64), p3 = __shfl_up(f[q].y, 1, 64);
-        const float b1 = lane ? p1 : h1, b2 = lane ? p2 : h2, b3 = lane ? p3 : h3;
-        h1 = __shfl(f[q].w, 63, 64); h2 = __shfl(f[q].z, 63, 64); h3 = __shfl(f[q].y, 63, 64);
-        const long long e = tb + 4 * (lane + 64 * q);
+        const float b1 = wave_shr1(f[q].w, h1), b2 = wave_shr1(f[q].z, h2), b3 = wave_shr1(f[q].y, h3);
+        h1 = lane63(f[q].w); h2 = lane63(f[q].z); h3 = lane63(f[q].y);
         const float xs[7] = {b3, b2, b1, f[q].x, f[q].y, f[q].z, f[q].w};
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-            uint32_t val;
-            int len;
-            make_token_bf<CT>(xs[3 + r], xs[2 + r], xs[1 + r], xs[r], FULL || idx0 + e + r >= 3, P, val, len);
-            const bool in = FULL || e + r < n;
-            sum += in ? (uint32_t)len : 0u;
-            neg1 |= in && (xs[3 + r] == -1.0f);
+            sum += (uint32_t)token_len_enc<CT>(xs[3 + r], xs[2 + r], xs[1 + r], xs[r], true, P);
+            neg1 |= xs[3 + r] == -1.0f;
         }
     }
 }
 
-// count kernel: one wave per tile; lane i holds float4 number i + 64q (q < CNT_Q), so every load
-// instruction reads 1 KiB contiguous.  The history of a float4 is the previous float4: lane i-1's
-// (same q) or, for lane 0, lane 63's of q-1.
+// count kernel: one wave per tile part; lane i holds float4 number i + 64q (q < CNT_Q), so every
+// load instruction reads 1 KiB contiguous.  The history of a float4 is the previous float4: lane
+// i-1's (same q) or, for lane 0, lane 63's of q-1.  One code path for every part: elements past n
+// are loaded as 0.0f (a 3-bit zero token each, subtracted afterwards) and the <= 3 elements before
+// global index 3 (no prediction, impl/dataCompression.c:1146) are corrected by lane 0.
+// one count part's floats (whole float4s; past n -> 0.0f) and its three history floats
+__device__ __forceinline__ void load_part(const float* __restrict__ x, long long n, long long idx0, long long tb,
+                                          int lane, float4* f, float* hist) {
+    const float4* p4 = reinterpret_cast<const float4*>(x + tb);
+    if (tb + CNT_SUB <= n) {
+#pragma unroll
+        for (int q = 0; q < CNT_Q; q++) f[q] = p4[lane + 64 * q];
+    } else {                                                         // whole float4s only
+        const int rem = (int)(n - tb);
+#pragma unroll
+        for (int q = 0; q < CNT_Q; q++) f[q] = 4 * (lane + 64 * q) + 4 <= rem ? p4[lane + 64 * q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 1; k <= 3; k++) hist[k - 1] = halo_x(x, idx0, tb - k);   // wave-uniform (scalar) loads
+}
+
 template <int CT>
 __global__ __launch_bounds__(256) void encode_count_kernel(const float* __restrict__ x, long long n, long long idx0,
                                                            Params P, uint32_t* __restrict__ tbits, long long ntiles,
                                                            unsigned* __restrict__ err) {
     const int lane = threadIdx.x & 63;
-    constexpr int HALF = ENC_TILE / 2;
-    for (long long h = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); h < 2 * ntiles; h += (long long)gridDim.x * 4) {
-    const long long tb = h * HALF;                                   // one wave per half tile
+    const long long np = CNT_PARTS * ntiles, stride = (long long)gridDim.x * 4;
+    long long h = (long long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float4 f[CNT_Q];
-    if (tb + HALF <= n) {
-        const float4* p4 = reinterpret_cast<const float4*>(x + tb);
-#pragma unroll
-        for (int q = 0; q < CNT_Q; q++) f[q] = p4[lane + 64 * q];
-    } else {
-#pragma unroll
-        for (int q = 0; q < CNT_Q; q++) {
-            const long long e = tb + 4 * (lane + 64 * q);
-            f[q].x = e < n ? x[e] : 0.0f; f[q].y = e + 1 < n ? x[e + 1] : 0.0f;
-            f[q].z = e + 2 < n ? x[e + 2] : 0.0f; f[q].w = e + 3 < n ? x[e + 3] : 0.0f;
-        }
-    }
-    const bool full = tb + HALF <= n && idx0 + tb >= 3;             // no bounds / history checks
-    float h1 = lane == 0 ? halo_x(x, idx0, tb - 1) : 0.0f;          // q = 0 history of lane 0
-    float h2 = lane == 0 ? halo_x(x, idx0, tb - 2) : 0.0f;
-    float h3 = lane == 0 ? halo_x(x, idx0, tb - 3) : 0.0f;
+    float hist[3];
+    if (h < np) load_part(x, n, idx0, h * CNT_SUB, lane, f, hist);
+    for (; h < np; h += stride) {                                    // persistent: next part prefetched
+    const long long tb = h * CNT_SUB;                                // one wave per tile part
+    float4 g[CNT_Q];
+    float ghist[3];
+    if (h + stride < np) load_part(x, n, idx0, (h + stride) * CNT_SUB, lane, g, ghist);
+    const float h1 = hist[0], h2 = hist[1], h3 = hist[2];
     uint32_t sum = 0;
     bool neg1 = false;
-    if (full) count_tokens<CT, true>(f, h1, h2, h3, tb, n, idx0, P, sum, neg1);
-    else count_tokens<CT, false>(f, h1, h2, h3, tb, n, idx0, P, sum, neg1);
-    if (CT != 6 && __any(neg1) && lane == 0) atomicOr(err, 1u);    // -1.0f is the reference's sentinel
+    count_tokens<CT>(f, h1, h2, h3, P, sum, neg1);
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
-    if (lane == 0) tbits[h] = sum;                                   // half-tile bit count
+    if (lane == 0) {
+        int vend = CNT_SUB;                                          // elements the vector pass saw
+        if (tb + CNT_SUB > n) {                                      // the 0.0f padding's tokens
+            const int rem = (int)max(n - tb, 0ll);                   // 0: a part past the end
+            vend = rem & ~3;
+            sum -= (uint32_t)token_len_enc<CT>(0.0f, 0.0f, 0.0f, 0.0f, true, P) * (uint32_t)(CNT_SUB - vend);
+            for (int j = vend; j < rem; j++) {                       // the straddling float4
+                const long long e = tb + j;
+                const float v = x[e];
+                neg1 |= v == -1.0f;
+                sum += (uint32_t)token_len_enc<CT>(v, halo_x(x, idx0, e - 1), halo_x(x, idx0, e - 2),
+                                                   halo_x(x, idx0, e - 3), idx0 + e >= 3, P);
+            }
+        }
+        if (CT != 6) {                                               // unpredicted head elements
+            for (int j = 0; j < 3 && j < vend && idx0 + tb + j < 3; j++) {
+                const long long e = tb + j;
+                const float v = x[e], b1 = halo_x(x, idx0, e - 1), b2 = halo_x(x, idx0, e - 2),
+                            b3 = halo_x(x, idx0, e - 3);
+                sum += (uint32_t)(token_len_enc<CT>(v, b1, b2, b3, false, P) - token_len_enc<CT>(v, b1, b2, b3, true, P));
+            }
+        }
+    }
+    if (CT != 6 && __any(neg1) && lane == 0) atomicOr(err, 1u);    // -1.0f is the reference's sentinel
+    if (lane == 0) tbits[h] = sum;                                   // tile-part bit count
+#pragma unroll
+    for (int q = 0; q < CNT_Q; q++) f[q] = g[q];
+#pragma unroll
+    for (int k = 0; k < 3; k++) hist[k] = ghist[k];
     }
 }
 
@@ -121,7 +161,14 @@ __global__ __launch_bounds__(1024) void encode_scan_kernel(const uint32_t* __res
     constexpr int PER = SCAN_CH / 1024;
     for (long long c0 = 0; c0 < ntiles; c0 += SCAN_CH) {
         const int m = (int)min((long long)SCAN_CH, ntiles - c0);
-        for (int i = tid; i < SCAN_CH; i += 1024) cnt[i] = i < m ? tbits[2 * (c0 + i)] + tbits[2 * (c0 + i) + 1] : 0u;
+        for (int i = tid; i < SCAN_CH; i += 1024) {
+            uint32_t c = 0;
+            if (i < m) {
+#pragma unroll
+                for (int k = 0; k < CNT_PARTS; k++) c += tbits[CNT_PARTS * (c0 + i) + k];
+            }
+            cnt[i] = c;
+        }
         __syncthreads();
         unsigned long long sum = 0;
 #pragma unroll
@@ -340,6 +387,20 @@ static unsigned write_grid(int ct) {
     return cache[ci];
 }
 
+static unsigned count_grid(int ct) {
+    static unsigned cache[12];
+    const int ci = (ct > 0 && ct < 12) ? ct : 0;
+    if (cache[ci]) return cache[ci];
+    int dev = 0, ncu = 256, per = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const void* f = ct == 5 ? (const void*)encode_count_kernel<5> : ct == 6 ? (const void*)encode_count_kernel<6>
+                  : ct == 7 ? (const void*)encode_count_kernel<7> : (const void*)encode_count_kernel<11>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, 256, 0) != hipSuccess || per < 1) per = 1;
+    cache[ci] = (unsigned)(per * ncu);
+    return cache[ci];
+}
+
 extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, const Params* P,
                                 uint32_t* out, uint64_t* desc, unsigned* tile_ctr, uint32_t epoch,
                                 int start_bit, unsigned long long* total_bits, unsigned* err,
@@ -348,10 +409,10 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
     (void)epoch;
     if (n <= 0) return 0;
     const unsigned ntiles = (unsigned)((n + ENC_TILE - 1) / ENC_TILE);
-    uint32_t* tbits = reinterpret_cast<uint32_t*>(desc + ntiles);     // desc holds 2 * ntiles words
+    uint32_t* tbits = reinterpret_cast<uint32_t*>(desc + ntiles);     // desc: dc_encode_desc_words(n)
     dc_mark_phase(0, stream);
     // one wave (count) / one workgroup (write) per tile: measured faster than persistent grids here
-    const unsigned gc = (2 * ntiles + 3) / 4;
+    const unsigned gc = getenv("DC_CNT_NP") ? (CNT_PARTS * ntiles + 3) / 4 : std::min<unsigned>((CNT_PARTS * ntiles + 3) / 4, count_grid(P->ct));
     const unsigned gw = std::min<unsigned>(ntiles, write_grid(P->ct));
     DC_ENC_DISPATCH(encode_count_kernel, dim3(gc), dim3(256), 0, stream, x, n, idx0, *P, tbits,
                     (long long)ntiles, err);
@@ -371,12 +432,18 @@ extern "C" int dc_launch_encode_bits(const float* x, long long n, long long idx0
     if (n <= 0) return 0;
     const unsigned ntiles = (unsigned)((n + ENC_TILE - 1) / ENC_TILE);
     uint32_t* tbits = reinterpret_cast<uint32_t*>(desc + ntiles);
-    const unsigned gc = (2 * ntiles + 3) / 4;
+    const unsigned gc = std::min<unsigned>((CNT_PARTS * ntiles + 3) / 4, count_grid(P->ct));
     DC_ENC_DISPATCH(encode_count_kernel, dim3(gc), dim3(256), 0, stream, x, n, idx0, *P, tbits, (long long)ntiles, err);
     hipLaunchKernelGGL(encode_scan_kernel, dim3(1), dim3(1024), 0, stream, tbits, desc, (long long)ntiles, 0, total_bits);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 extern "C" long long dc_encode_tile_count(long long n) { return (n + ENC_TILE - 1) / ENC_TILE; }
+
+// u64 words of the encode descriptor buffer: tile offsets + 32-bit tile-part counts
+extern "C" long long dc_encode_desc_words(long long n) {
+    const long long nt = dc_encode_tile_count(n);
+    return nt + (CNT_PARTS * nt + 1) / 2;
+}
 
 }  // namespace dc

@@ -241,10 +241,9 @@ int dc_encode_device(int ct, const void* d_x, long long n, long long idx0, int t
     if (((uintptr_t)d_x & 15u) || ((uintptr_t)d_out & 3u)) return seterr(DC_ERR_ARG, "misaligned device buffer");
     Params P;
     make_params(&P, ct, type, mask17);
-    long long ntiles = dc_encode_tile_count(n);
-    if (2 * ntiles + 8 > G.enc_desc_cap) {
+    if (dc_encode_desc_words(n) + 8 > G.enc_desc_cap) {
         if (G.enc_desc) HIPCHK(hipFree(G.enc_desc));
-        long long cap = 2 * ntiles + 1024;
+        long long cap = dc_encode_desc_words(n) + 1024;
         HIPCHK(hipMalloc((void**)&G.enc_desc, cap * sizeof(uint64_t)));
         HIPCHK(hipMemsetAsync(G.enc_desc, 0, cap * sizeof(uint64_t), G.st));
         G.enc_desc_cap = cap;
@@ -284,10 +283,9 @@ int dc_encode_bits_device(int ct, const void* d_x, long long n, long long idx0, 
     if (n == 0) { *bits_out = 0; return DC_OK; }
     Params P;
     make_params(&P, ct, type, mask17);
-    const long long ntiles = dc_encode_tile_count(n);
-    if (2 * ntiles + 8 > G.enc_desc_cap) {
+    if (dc_encode_desc_words(n) + 8 > G.enc_desc_cap) {
         if (G.enc_desc) HIPCHK(hipFree(G.enc_desc));
-        const long long cap = 2 * ntiles + 1024;
+        const long long cap = dc_encode_desc_words(n) + 1024;
         HIPCHK(hipMalloc((void**)&G.enc_desc, cap * sizeof(uint64_t)));
         G.enc_desc_cap = cap;
     }
