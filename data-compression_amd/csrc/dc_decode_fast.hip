@@ -30,7 +30,10 @@ namespace dc {
 constexpr int LROW = 32;                       // LDS words per chunk (unpadded: measured faster than a
                                                // 33-word row, the lanes drift apart within a few tokens)
 constexpr int LWORDS = GROUP * LROW + 8;       // + the words after the tile
-constexpr int OV = 1024;                       // overlap: P_c starts OV bits before its chunk
+#ifndef DC_OV
+#define DC_OV 1024
+#endif
+constexpr int OV = DC_OV;                       // overlap: P_c starts OV bits before its chunk
 constexpr int OVW = OV / 32;
 constexpr int PWORDS = LWORDS + OVW;
 constexpr int KMAX = 2;                        // extra known entries per chunk (besides P_c's own)
@@ -492,8 +495,14 @@ __global__ __launch_bounds__(1024) void tile_scan_kernel(DecBufs D) {
 // where a0 aligns the slots to 64-byte sectors of `out`.  Complete sectors leave as four 16-byte
 // stores issued back to back (HBM sees whole sectors instead of scattered partial lines); the values
 // before the chunk's first and after its last sector boundary leave as plain dword stores.
-constexpr int RING = 16;
-constexpr int SECT = 8;
+#ifndef DC_RING
+#define DC_RING 16
+#endif
+constexpr int RING = DC_RING;
+#ifndef DC_SECT
+#define DC_SECT 8
+#endif
+constexpr int SECT = DC_SECT;
 
 __device__ __forceinline__ void store_sector(const float* ring, float* out, long long s0, int a0, long long num);
 

@@ -64,25 +64,22 @@ __device__ __forceinline__ void make_token(float x, float b1, float b2, float b3
 }
 
 // Branch-free form of make_token (selects only; same tokens).  For a CT7 masked token the exponent
-// equals the mask's, so its mantissa bit count is the uniform P.mm.
+// equals the mask's, so its mantissa bit count is the uniform P.mm and its value is a bit-select of
+// the raw top bits with uniform constants.  The predicted code is the first strict minimum of
+// (d1, d2, d3); "some prediction within threshold" is min(d1, d2, d3) <= thr_le with a NaN d1
+// never predicting (token_len_enc below has the argument).
 template <int CT>
 __device__ __forceinline__ void make_token_bf(float x, float b1, float b2, float b3, bool predict, const Params& P,
                                               uint32_t& val, int& len) {
     const uint32_t u = __float_as_uint(x);
-    const int m = mbits(P.B, (u >> 23) & 0xFFu);
-    uint32_t v = CT == 11 ? u : (u >> (23 - m));
-    int l = CT == 11 ? 32 : 9 + m;
+    int l = CT == 11 ? 32 : min(max((int)((u >> 23) & 0xFFu) + P.rawadd, 9), 32);   // 9 + m
+    uint32_t v = CT == 11 ? u : (u >> (32 - l));                                     // top 9 + m bits
     if (CT == 7) {
         const bool msk = (u >> 23) == (P.mask17 >> 8);
         const bool f1 = ((u >> 15) & 0xFFu) != (P.mask17 & 0xFFu);
-        const uint32_t head = ((1u << P.type) - 1u) << 1;
-        const int tl0 = P.mm0, tl1 = P.mm;
-        const uint32_t v0 = (head << tl0) | (v & ((1u << tl0) - 1u));
-        const uint32_t v1 = ((head | 1u) << tl1) | (v & ((1u << tl1) - 1u));
-        const uint32_t vm = f1 ? v1 : v0;
-        const int lm = P.type + 2 + (f1 ? tl1 : tl0);
+        const uint32_t vm = f1 ? ((v & P.em1) | P.eh1) : ((v & P.em0) | P.eh0);
+        l = msk ? P.lm0 + (f1 ? P.dlm : 0) : l;
         v = msk ? vm : v;
-        l = msk ? lm : l;
     }
     if (CT != 6) {
         const float p2 = __fsub_rn(__fmul_rn(2.0f, b1), b2);
@@ -90,17 +87,14 @@ __device__ __forceinline__ void make_token_bf(float x, float b1, float b2, float
         const float d1 = fabsf(__fsub_rn(b1, x));
         const float d2 = fabsf(__fsub_rn(p2, x));
         const float d3 = fabsf(__fsub_rn(p3, x));
-        const bool c2 = d2 < d1;
-        float dmin = c2 ? d2 : d1;
-        uint32_t code = c2 ? 6u : 5u;
-        const bool c3 = d3 < dmin;
-        dmin = c3 ? d3 : dmin;
-        code = c3 ? 7u : code;
-        const bool pr = predict && dmin <= P.thr_le;
+        const float d12 = fminf(d1, d2);
+        const bool c2 = d2 < d1, c3 = d3 < d12;
+        const uint32_t code = c3 ? 7u : (c2 ? 6u : 5u);
+        const bool pr = predict && d1 == d1 && fminf(d12, d3) <= P.thr_le;
         const bool z = fabsf(x) <= P.thr_lt;
-        v = pr ? code : v;
-        v = z ? 4u : v;
-        l = (pr || z) ? 3 : l;
+        const bool s3 = pr || z;
+        v = s3 ? (z ? 4u : code) : v;
+        l = s3 ? 3 : l;
     }
     val = v;
     len = l;
@@ -205,19 +199,20 @@ __device__ __forceinline__ int token_len_bf(uint32_t t, const Params& P) {
 template <int CT>
 __device__ __forceinline__ uint32_t token_pattern_bf(uint32_t t, int len, const Params& P, int* code) {
     const bool c3 = (CT != 6) && ((int)t < 0);
-    *code = c3 ? (int)((t >> 29) & 3u) : 0;
+    *code = c3 ? (int)__builtin_amdgcn_ubfe(t, 29u, 2u) : 0;
     uint32_t u;
     if (CT == 11) {
         u = t;
     } else {
-        const uint32_t y = (uint32_t)(0xFFFFFFFFull >> len);
+        const uint32_t y = 0x7FFFFFFFu >> (uint32_t)(len - 1);         // 0xFFFFFFFF >> len, len in [3, 32]
         u = (t & ~y) | (y & ~(y >> 1));
-        if (CT == 7) {
-            const bool msk = (t & P.hm) == P.hm;
-            const uint32_t rest = t << P.rs;
-            const uint32_t u0 = P.c0 | ((rest >> 17) & P.k0);
-            const uint32_t u1 = P.c1 | ((rest >> 9) & P.k1);
-            u = msk ? (((t >> P.fsh) & 1u) ? u1 : u0) : u;
+        if (CT == 7) {                                                // bit selects, no divergent branch
+            const uint32_t u0 = P.c0 | ((t >> P.s0) & P.k0);
+            const uint32_t u1 = P.c1 | ((t >> P.s1) & P.k1);
+            const uint32_t mf = (uint32_t)__builtin_amdgcn_sbfe((int)t, (uint32_t)P.fsh, 1u);   // flag: all ones
+            const uint32_t mm = (t & P.hm) == P.hm ? 0xFFFFFFFFu : 0u;
+            const uint32_t um = (u1 & mf) | (u0 & ~mf);
+            u = (um & mm) | (u & ~mm);
         }
     }
     return c3 ? 0u : u;

@@ -9,8 +9,8 @@
 // x[i-3..i].  Three launches, no inter-workgroup waiting:
 //   encode_count_kernel : per tile of ENC_TILE floats, the total token bit length
 //   encode_scan_kernel  : exclusive scan of the tile lengths -> every tile's global bit offset G
-//   encode_write_kernel : tokens again, packed MSB-first into LDS at offset G mod 32 (lane-local
-//                         accumulation, ds_or only on the words two lanes share), then the tile
+//   encode_write_kernel : tokens again, ORed MSB-first into a zeroed LDS bit buffer at offset
+//                         G mod 32 + their prefix (one 64-bit shift, two ds_or each), then the tile
 //                         writes every 32-bit word whose first bit lies in [G, G+T) as byte-swapped
 //                         dwords, completing its last word with the first <= 31 bits of the
 //                         following elements (recomputed locally, <= 11 tokens).
@@ -26,7 +26,10 @@ constexpr int ENC_TILE = 4096;                  // floats per tile (one offset p
 constexpr int ENC_TPB = 256;                    // write kernel: 4 waves per tile
 constexpr int ENC_K = ENC_TILE / ENC_TPB;       // 16 consecutive floats per lane
 constexpr int ENC_Q = ENC_TILE / 4 / ENC_TPB;   // coalesced float4 loads per lane
-constexpr int CNT_Q = 4;                        // count kernel: one wave per tile part, CNT_Q float4 per lane
+#ifndef DC_CNT_Q
+#define DC_CNT_Q 4
+#endif
+constexpr int CNT_Q = DC_CNT_Q;                 // count kernel: one wave per tile part, CNT_Q float4 per lane
 constexpr int CNT_SUB = 256 * CNT_Q;            // floats per count wave
 constexpr int CNT_PARTS = ENC_TILE / CNT_SUB;   // count parts per tile (tbits entries)
 constexpr int ENC_LDS_WORDS = ENC_TILE + 48;    // 32 bits/elem max + offset + head slack
@@ -59,7 +62,6 @@ __device__ __forceinline__ float lane63(float v) { return __int_as_float(__built
 template <int CT>
 __device__ __forceinline__ void count_tokens(const float4* f, float h1, float h2, float h3, const Params& P,
                                              uint32_t& sum, bool& neg1) {
-    const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int q = 0; q < CNT_Q; q++) {
         const float b1 = wave_shr1(f[q].w, h1), b2 = wave_shr1(f[q].z, h2), b3 = wave_shr1(f[q].y, h3);
@@ -94,25 +96,15 @@ __device__ __forceinline__ void load_part(const float* __restrict__ x, long long
     for (int k = 1; k <= 3; k++) hist[k - 1] = halo_x(x, idx0, tb - k);   // wave-uniform (scalar) loads
 }
 
+// bit count of one tile part from its loaded floats; lane 0 corrects the padding and head elements
 template <int CT>
-__global__ __launch_bounds__(256) void encode_count_kernel(const float* __restrict__ x, long long n, long long idx0,
-                                                           Params P, uint32_t* __restrict__ tbits, long long ntiles,
-                                                           unsigned* __restrict__ err) {
-    const int lane = threadIdx.x & 63;
-    const long long np = CNT_PARTS * ntiles, stride = (long long)gridDim.x * 4;
-    long long h = (long long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    float4 f[CNT_Q];
-    float hist[3];
-    if (h < np) load_part(x, n, idx0, h * CNT_SUB, lane, f, hist);
-    for (; h < np; h += stride) {                                    // persistent: next part prefetched
-    const long long tb = h * CNT_SUB;                                // one wave per tile part
-    float4 g[CNT_Q];
-    float ghist[3];
-    if (h + stride < np) load_part(x, n, idx0, (h + stride) * CNT_SUB, lane, g, ghist);
-    const float h1 = hist[0], h2 = hist[1], h3 = hist[2];
+__device__ __forceinline__ void count_part(const float* __restrict__ x, long long n, long long idx0, const Params& P,
+                                           long long h, const float4* f, const float* hist, int lane,
+                                           uint32_t* psum, unsigned* __restrict__ err) {
+    const long long tb = h * CNT_SUB;
     uint32_t sum = 0;
     bool neg1 = false;
-    count_tokens<CT>(f, h1, h2, h3, P, sum, neg1);
+    count_tokens<CT>(f, hist[0], hist[1], hist[2], P, sum, neg1);
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
     if (lane == 0) {
@@ -139,59 +131,99 @@ __global__ __launch_bounds__(256) void encode_count_kernel(const float* __restri
         }
     }
     if (CT != 6 && __any(neg1) && lane == 0) atomicOr(err, 1u);    // -1.0f is the reference's sentinel
-    if (lane == 0) tbits[h] = sum;                                   // tile-part bit count
-#pragma unroll
-    for (int q = 0; q < CNT_Q; q++) f[q] = g[q];
-#pragma unroll
-    for (int k = 0; k < 3; k++) hist[k] = ghist[k];
-    }
+    if (lane == 0) *psum = sum;                                      // tile-part bit count
 }
 
-// exclusive scan of the 32-bit tile lengths (one workgroup, staged through LDS in chunks of SCAN_CH
-// tiles with coalesced loads); toff[t] = tile t's global bit offset
-constexpr int SCAN_CH = 16384;
-__global__ __launch_bounds__(1024) void encode_scan_kernel(const uint32_t* __restrict__ tbits, uint64_t* __restrict__ toff,
+// one workgroup per tile (its four waves = the tile's four parts); tcnt[tile] = the tile's bits
+template <int CT>
+__global__ __launch_bounds__(256) void encode_count_kernel(const float* __restrict__ x, long long n, long long idx0,
+                                                           Params P, uint32_t* __restrict__ tcnt, long long ntiles,
+                                                           unsigned* __restrict__ err) {
+    static_assert(CNT_PARTS == 4, "one workgroup of four waves per tile");
+    __shared__ uint32_t wsum[4];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const long long h = (long long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(wid);
+    float4 f[CNT_Q];
+    float hist[3];
+    load_part(x, n, idx0, h * CNT_SUB, lane, f, hist);
+    count_part<CT>(x, n, idx0, P, h, f, hist, lane, wsum + wid, err);
+    __syncthreads();
+    if (threadIdx.x == 0) tcnt[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    (void)ntiles;
+}
+
+// exclusive scan of the tile bit counts (one workgroup): coalesced, all-at-once loads of SCAN_T
+// counts per thread into LDS (one pad word per 16), then each thread scans SCAN_T consecutive tiles;
+// toff[t] = tile t's global bit offset
+constexpr int SCAN_T = 16;
+constexpr int SCAN_CH = 1024 * SCAN_T;
+__global__ __launch_bounds__(1024) void encode_scan_kernel(const uint32_t* __restrict__ tcnt, uint64_t* __restrict__ toff,
                                                            long long ntiles, int start_bit,
                                                            unsigned long long* __restrict__ total_bits) {
-    __shared__ uint32_t cnt[SCAN_CH];
-    __shared__ unsigned long long part[1024];
-    __shared__ unsigned long long carry;
-    const int tid = threadIdx.x;
-    if (tid == 0) carry = (unsigned long long)start_bit;
-    constexpr int PER = SCAN_CH / 1024;
+    __shared__ uint32_t cnt[SCAN_CH + SCAN_CH / 16];           // also the u64 offsets of half the tiles
+    __shared__ unsigned long long wtot[1024 / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    unsigned long long carry = (unsigned long long)start_bit;
     for (long long c0 = 0; c0 < ntiles; c0 += SCAN_CH) {
-        const int m = (int)min((long long)SCAN_CH, ntiles - c0);
-        for (int i = tid; i < SCAN_CH; i += 1024) {
-            uint32_t c = 0;
-            if (i < m) {
+        uint32_t v[SCAN_T];
 #pragma unroll
-                for (int k = 0; k < CNT_PARTS; k++) c += tbits[CNT_PARTS * (c0 + i) + k];
-            }
-            cnt[i] = c;
+        for (int k = 0; k < SCAN_T; k++) {
+            const long long t = c0 + k * 1024 + tid;
+            v[k] = t < ntiles ? tcnt[t] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < SCAN_T; k++) {
+            const int i = k * 1024 + tid;
+            cnt[i + (i >> 4)] = v[k];
         }
         __syncthreads();
+        uint32_t c[SCAN_T];
         unsigned long long sum = 0;
 #pragma unroll
-        for (int k = 0; k < PER; k++) sum += cnt[tid * PER + k];
-        part[tid] = sum;
-        __syncthreads();
-        for (int d = 1; d < 1024; d <<= 1) {
-            const unsigned long long v = tid >= d ? part[tid - d] : 0ull;
-            __syncthreads();
-            part[tid] += v;
-            __syncthreads();
+        for (int i = 0; i < SCAN_T; i++) {
+            c[i] = cnt[tid * (SCAN_T + 1) + i];
+            sum += c[i];
         }
-        unsigned long long run = carry + part[tid] - sum;
+        unsigned long long inc = sum;
 #pragma unroll
-        for (int k = 0; k < PER; k++) {
-            const int i = tid * PER + k;
-            const unsigned long long b = cnt[i];
-            if (i < m) toff[c0 + i] = run;
-            run += b;
+        for (int d = 1; d < 64; d <<= 1) {
+            const unsigned long long u = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += u;
         }
+        if (lane == 63) wtot[wid] = inc;
         __syncthreads();
-        if (tid == 1023) carry += part[1023];
-        __syncthreads();
+        unsigned long long wpre = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < 1024 / 64; w++) {
+            const unsigned long long u = wtot[w];
+            wpre += w < wid ? u : 0ull;
+            tot += u;
+        }
+        unsigned long long run = carry + wpre + inc - sum;
+        // offsets leave through LDS so the global stores are coalesced: half the tiles per pass
+        unsigned long long* o = reinterpret_cast<unsigned long long*>(cnt);
+        const int m = (int)min((long long)SCAN_CH, ntiles - c0);
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+            __syncthreads();                                         // cnt (then o) is free
+            if ((tid >> 9) == half) {
+                const int b = (tid & 511) * (SCAN_T + 1);
+#pragma unroll
+                for (int i = 0; i < SCAN_T; i++) {
+                    o[b + i] = run;
+                    run += c[i];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < SCAN_CH / 2 / 1024; k++) {
+                const int j = k * 1024 + tid;                        // tile within the half
+                const int jj = half * (SCAN_CH / 2) + j;
+                if (jj < m) toff[c0 + jj] = o[(j >> 4) * (SCAN_T + 1) + (j & 15)];
+            }
+        }
+        carry += tot;
+        __syncthreads();                                             // cnt / wtot are rewritten
     }
     if (tid == 0) *total_bits = carry;
 }
@@ -279,6 +311,7 @@ __global__ __launch_bounds__(ENC_TPB) void encode_write_kernel(
             int len;
             make_token_bf<CT>(v[4 + j], v[3 + j], v[2 + j], v[1 + j], idx0 + base + j >= 3, P, tv[j], len);
             len = base + j < n ? len : 0;
+            tv[j] = len ? tv[j] : 0u;
             tlp[j >> 2] |= (uint32_t)len << (8 * (j & 3));
             mysum += (uint32_t)len;
         }
@@ -312,31 +345,19 @@ __global__ __launch_bounds__(ENC_TPB) void encode_write_kernel(
     const long long wb = (long long)(G >> 5);
     ESTAMP(2);
 
-    // ---- lane-local MSB-first packing: full words are plain LDS stores, the first and last word
-    // of the lane's bit range (shared with the neighbouring lanes) are ds_or
+    // ---- MSB-first packing: the LDS bit buffer is zeroed, so every token is ORed in at its bit
+    // offset (measured faster than lane-local word assembly with divergent stores)
     {
-        const uint32_t off = boff + wpre + inc - mysum;
-        uint32_t w = off >> 5;
-        int nin = (int)(off & 31u);                                   // bits already in the current word
-        bool shared = nin != 0;
-        uint64_t acc = 0;
+        uint32_t off = boff + wpre + inc - mysum;
 #pragma unroll
         for (int j = 0; j < ENC_K; j++) {
             const int len = (int)((tlp[j >> 2] >> (8 * (j & 3))) & 0xFFu);
-            if (len) {
-                acc |= (uint64_t)tv[j] << (64 - nin - len);
-                nin += len;
-                if (nin >= 32) {
-                    const uint32_t word = (uint32_t)(acc >> 32);
-                    if (shared) atomicOr(&s_bits[w], word); else s_bits[w] = word;
-                    shared = false;
-                    acc <<= 32;
-                    nin -= 32;
-                    w++;
-                }
-            }
+            const uint64_t v = (uint64_t)tv[j] << ((64 - (int)(off & 31u) - len) & 63);   // len 0: tv = 0
+            uint32_t* d = s_bits + (off >> 5);
+            atomicOr(d, (uint32_t)(v >> 32));
+            atomicOr(d + 1, (uint32_t)v);
+            off += (uint32_t)len;
         }
-        if (nin > 0) atomicOr(&s_bits[w], (uint32_t)(acc >> 32));
     }
     __syncthreads();
     if (tid == 0) {
@@ -387,20 +408,6 @@ static unsigned write_grid(int ct) {
     return cache[ci];
 }
 
-static unsigned count_grid(int ct) {
-    static unsigned cache[12];
-    const int ci = (ct > 0 && ct < 12) ? ct : 0;
-    if (cache[ci]) return cache[ci];
-    int dev = 0, ncu = 256, per = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    const void* f = ct == 5 ? (const void*)encode_count_kernel<5> : ct == 6 ? (const void*)encode_count_kernel<6>
-                  : ct == 7 ? (const void*)encode_count_kernel<7> : (const void*)encode_count_kernel<11>;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, 256, 0) != hipSuccess || per < 1) per = 1;
-    cache[ci] = (unsigned)(per * ncu);
-    return cache[ci];
-}
-
 extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, const Params* P,
                                 uint32_t* out, uint64_t* desc, unsigned* tile_ctr, uint32_t epoch,
                                 int start_bit, unsigned long long* total_bits, unsigned* err,
@@ -409,10 +416,10 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
     (void)epoch;
     if (n <= 0) return 0;
     const unsigned ntiles = (unsigned)((n + ENC_TILE - 1) / ENC_TILE);
-    uint32_t* tbits = reinterpret_cast<uint32_t*>(desc + ntiles);     // desc: dc_encode_desc_words(n)
+    uint32_t* tbits = reinterpret_cast<uint32_t*>(desc + ntiles);     // tile counts; desc: dc_encode_desc_words(n)
     dc_mark_phase(0, stream);
-    // one wave (count) / one workgroup (write) per tile: measured faster than persistent grids here
-    const unsigned gc = getenv("DC_CNT_NP") ? (CNT_PARTS * ntiles + 3) / 4 : std::min<unsigned>((CNT_PARTS * ntiles + 3) / 4, count_grid(P->ct));
+    // count: one workgroup per tile (a persistent count grid with prefetch measured slower)
+    const unsigned gc = ntiles;                                    // count: one workgroup per tile
     const unsigned gw = std::min<unsigned>(ntiles, write_grid(P->ct));
     DC_ENC_DISPATCH(encode_count_kernel, dim3(gc), dim3(256), 0, stream, x, n, idx0, *P, tbits,
                     (long long)ntiles, err);
@@ -432,7 +439,7 @@ extern "C" int dc_launch_encode_bits(const float* x, long long n, long long idx0
     if (n <= 0) return 0;
     const unsigned ntiles = (unsigned)((n + ENC_TILE - 1) / ENC_TILE);
     uint32_t* tbits = reinterpret_cast<uint32_t*>(desc + ntiles);
-    const unsigned gc = std::min<unsigned>((CNT_PARTS * ntiles + 3) / 4, count_grid(P->ct));
+    const unsigned gc = ntiles;
     DC_ENC_DISPATCH(encode_count_kernel, dim3(gc), dim3(256), 0, stream, x, n, idx0, *P, tbits, (long long)ntiles, err);
     hipLaunchKernelGGL(encode_scan_kernel, dim3(1), dim3(1024), 0, stream, tbits, desc, (long long)ntiles, 0, total_bits);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -443,7 +450,7 @@ extern "C" long long dc_encode_tile_count(long long n) { return (n + ENC_TILE - 
 // u64 words of the encode descriptor buffer: tile offsets + 32-bit tile-part counts
 extern "C" long long dc_encode_desc_words(long long n) {
     const long long nt = dc_encode_tile_count(n);
-    return nt + (CNT_PARTS * nt + 1) / 2;
+    return nt + (nt + 1) / 2;
 }
 
 }  // namespace dc

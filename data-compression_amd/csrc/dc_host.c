@@ -217,6 +217,8 @@ static void make_params(Params* P, int ct, int type, uint32_t mask17) {
     P->hm = type > 0 ? (((1u << type) - 1u) << (31 - type)) : 0u;
     P->fsh = 30 - type;
     P->rs = type + 2;
+    P->s0 = 17 - P->rs;
+    P->s1 = 9 - P->rs;
     P->lm0 = type + 2 + P->mm0;
     P->dlm = P->mm - P->mm0;
     const int tl0 = P->mm0, tl1 = P->mm;
@@ -224,6 +226,13 @@ static void make_params(Params* P, int ct, int type, uint32_t mask17) {
     P->k0 = tl0 > 0 ? (((1u << tl0) - 1u) << (15 - tl0)) : 0u;
     P->c1 = ((P->mask17 >> 8) << 23) | (tl1 < 23 ? 1u << (22 - tl1) : 0u);
     P->k1 = tl1 > 0 ? (((1u << tl1) - 1u) << (23 - tl1)) : 0u;
+    {   /* masked token = head ones(type), flag, then the low tl bits of the raw top bits */
+        const uint32_t head = type > 0 ? ((1u << type) - 1u) << 1 : 0u;
+        P->em0 = (1u << tl0) - 1u;
+        P->eh0 = head << tl0;
+        P->em1 = tl1 >= 32 ? 0xFFFFFFFFu : (1u << tl1) - 1u;
+        P->eh1 = (head | 1u) << tl1;
+    }
 }
 
 static int valid_ct(int ct) { return ct == 5 || ct == 6 || ct == 7 || ct == 11; }

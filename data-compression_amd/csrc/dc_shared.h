@@ -26,6 +26,9 @@ typedef struct Params {  /* per-call codec parameters, computed on the host */
     int rs;              /* CT7: type + 2 (head length) */
     uint32_t c0, k0;     /* CT7 flag 0 value = c0 | ((t << rs) >> 17 & k0) */
     uint32_t c1, k1;     /* CT7 flag 1 value = c1 | ((t << rs) >> 9 & k1) */
+    int s0, s1;          /* CT7: the same as c0 | ((t >> s0) & k0), c1 | ((t >> s1) & k1): 17 - rs, 9 - rs */
+    uint32_t em0, eh0;   /* CT7 encoder, flag 0 token = (v & em0) | eh0 (v = top 9+mm bits of the float) */
+    uint32_t em1, eh1;   /* CT7 encoder, flag 1 token = (v & em1) | eh1 */
 } Params;
 
 typedef struct Plan {    /* device-resident sizes of the stream being decoded */

@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "lib", "libdcamd.so")
+LIB = os.environ.get("DCAMD_LIB") or os.path.join(HERE, "lib", "libdcamd.so")   # override: A/B experiments
 
 _f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
 _u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")

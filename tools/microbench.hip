@@ -40,6 +40,28 @@ __global__ void clk_kernel(unsigned long long* out, int iters) {
     if (a == 12345.0f) out[2] = 1;
 }
 
+// VALU issue rate: 8 independent chains of 32-bit integer ops (add / xor / bfe / select / alignbit)
+__global__ void valu_kernel(unsigned* out, int iters) {
+    unsigned a[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) a[k] = threadIdx.x * (k + 3);
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            unsigned v = a[k];
+            v = v + 0x9E3779B9u;
+            v = v ^ (v >> 7);
+            v = __builtin_amdgcn_alignbit(v, a[(k + 1) & 7], 5u);
+            v = (v & 1u) ? v + 3u : v ^ 0x55u;
+            a[k] = v;
+        }
+    }
+    unsigned r = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) r ^= a[k];
+    if (r == 0x12345678u) out[0] = r;
+}
+
 extern "C" int mb_run(int which, const void* x, void* y, long long nbytes, int grid, int block, int iters, float* ms,
                       unsigned long long* clk) {
     hipEvent_t e0, e1;
@@ -51,6 +73,7 @@ extern "C" int mb_run(int which, const void* x, void* y, long long nbytes, int g
             if (which == 0) hipLaunchKernelGGL(rd_kernel, dim3(grid), dim3(block), 0, 0, (const float4*)x, n4, (float*)y);
             if (which == 1) hipLaunchKernelGGL(rd16_kernel, dim3(grid), dim3(block), 0, 0, (const float4*)x, n4, (float*)y);
             if (which == 2) hipLaunchKernelGGL(cp_kernel, dim3(grid), dim3(block), 0, 0, (const float4*)x, (float4*)y, n4);
+            if (which == 4) hipLaunchKernelGGL(valu_kernel, dim3(grid), dim3(block), 0, 0, (unsigned*)y, (int)nbytes);
             if (which == 3) hipLaunchKernelGGL(clk_kernel, dim3(grid), dim3(block), 0, 0, (unsigned long long*)y, (int)nbytes);
         }
         (void)hipEventRecord(e1, 0);

@@ -18,3 +18,12 @@ for which, name in [(0, "read"), (1, "read16"), (2, "copy")]:
 for grid in [256, 2048]:
     L.mb_run(3, x.data_ptr(), y.data_ptr(), 200000, grid, 256, 1, ctypes.byref(ms), clk)
     print(f"clock grid {grid}: {clk[0] / (clk[1] * 10e-9) / 1e9:.3f} GHz (memtime/memrealtime)")
+
+# VALU issue rate: W waves per SIMD (blocks of 256 = one wave per SIMD), 8 chains x 6 ops x iters
+if len(sys.argv) > 1 and sys.argv[1] == "valu":
+    iters = 20000
+    for W in (1, 2, 3, 4, 6, 8):
+        L.mb_run(4, x.data_ptr(), y.data_ptr(), iters, 256 * W, 256, 3, ctypes.byref(ms), clk)
+        waves = 256 * W * 4
+        instr = waves * iters * 72.0          # 72 VALU per iteration (checked in the .s)
+        print(f"valu W={W}: {ms.value*1e3:9.1f} us  {instr / 1024 / (ms.value * 1e-3) / 1e9:6.3f} G wave-instr/s per SIMD")
