@@ -503,6 +503,7 @@ constexpr int RING = DC_RING;
 #define DC_SECT 8
 #endif
 constexpr int SECT = DC_SECT;
+static_assert(SECT == 2 || SECT % 4 == 0, "sectors of 2 or 4k floats");
 
 __device__ __forceinline__ void store_sector(const float* ring, float* out, long long s0, int a0, long long num);
 
@@ -524,10 +525,14 @@ __device__ __forceinline__ void flush_ring(const float* ring, float* out, long l
 __device__ __forceinline__ void store_sector(const float* ring, float* out, long long s0, int a0, long long num) {
     const int sl = (int)((s0 + a0) & (RING - 1));
     if (s0 + SECT <= num) {
-        const float4* r4 = reinterpret_cast<const float4*>(ring + sl);
-        float4* o4 = reinterpret_cast<float4*>(out + s0);
+        if constexpr (SECT % 4 == 0) {
+            const float4* r4 = reinterpret_cast<const float4*>(ring + sl);
+            float4* o4 = reinterpret_cast<float4*>(out + s0);
 #pragma unroll
-        for (int q = 0; q < SECT / 4; q++) o4[q] = r4[q];
+            for (int q = 0; q < SECT / 4; q++) o4[q] = r4[q];
+        } else {
+            *reinterpret_cast<float2*>(out + s0) = *reinterpret_cast<const float2*>(ring + sl);
+        }
     } else {
         for (int i = 0; i < SECT && s0 + i < num; i++) out[s0 + i] = ring[sl + i];
     }
@@ -537,9 +542,9 @@ struct DecodeShared {
     uint32_t L[LWORDS];
     union {
         float ring[GROUP * RING];                  // decode pass output rings
-        struct {                                   // carry scan
-            uint8_t kd[2][3][GROUP];
-            float fv[2][3][GROUP];
+        struct {                                   // carry scan (in place, two barriers a step)
+            uint8_t kd[3][GROUP];
+            float fv[3][GROUP];
         } k;
     } u;
     float tin[3];
@@ -669,32 +674,37 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
         sent = false;
         if (!act || e == UNKE) { k1 = 1; k2 = 2; k3 = 3; }
         __syncthreads();                                   // resolution arrays are dead from here
-        S.u.k.kd[0][0][c] = (uint8_t)k1; S.u.k.kd[0][1][c] = (uint8_t)k2; S.u.k.kd[0][2][c] = (uint8_t)k3;
-        S.u.k.fv[0][0][c] = f1; S.u.k.fv[0][1][c] = f2; S.u.k.fv[0][2][c] = f3;
+        S.u.k.kd[0][c] = (uint8_t)k1; S.u.k.kd[1][c] = (uint8_t)k2; S.u.k.kd[2][c] = (uint8_t)k3;
+        S.u.k.fv[0][c] = f1; S.u.k.fv[1][c] = f2; S.u.k.fv[2][c] = f3;
         __syncthreads();
         STAMP(10);
         // ---- inclusive scan of carry functions: F_c = f_c o ... o f_0
-        int cur = 0;
         for (int d = 1; d < GROUP; d <<= 1) {
+            int kk[3];
+            float vv[3];
+#pragma unroll
             for (int i = 0; i < 3; i++) {
-                const int k0i = S.u.k.kd[cur][i][c];
-                int kk = k0i;
-                float vv = S.u.k.fv[cur][i][c];
+                const int k0i = S.u.k.kd[i][c];
+                kk[i] = k0i;
+                vv[i] = S.u.k.fv[i][c];
                 if (c >= d && k0i >= 1 && k0i <= 3) {
-                    kk = S.u.k.kd[cur][k0i - 1][c - d];
-                    vv = S.u.k.fv[cur][k0i - 1][c - d];
+                    kk[i] = S.u.k.kd[k0i - 1][c - d];
+                    vv[i] = S.u.k.fv[k0i - 1][c - d];
                 }
-                S.u.k.kd[cur ^ 1][i][c] = (uint8_t)kk;
-                S.u.k.fv[cur ^ 1][i][c] = vv;
             }
-            cur ^= 1;
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                S.u.k.kd[i][c] = (uint8_t)kk[i];
+                S.u.k.fv[i][c] = vv[i];
+            }
             __syncthreads();
         }
         int ik[3];
         float iv[3];
         for (int i = 0; i < 3; i++) {
-            ik[i] = c == 0 ? i + 1 : S.u.k.kd[cur][i][c - 1];
-            iv[i] = c == 0 ? 0.0f : S.u.k.fv[cur][i][c - 1];
+            ik[i] = c == 0 ? i + 1 : S.u.k.kd[i][c - 1];
+            iv[i] = c == 0 ? 0.0f : S.u.k.fv[i][c - 1];
         }
         if (pend > 0) {
             bool needs = false, cx = false;
@@ -702,13 +712,13 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
             if (needs) S.need = 1;
             if (cx) S.cplx = 1;
         }
-        const int tk0 = S.u.k.kd[cur][0][GROUP - 1], tk1 = S.u.k.kd[cur][1][GROUP - 1], tk2 = S.u.k.kd[cur][2][GROUP - 1];
+        const int tk0 = S.u.k.kd[0][GROUP - 1], tk1 = S.u.k.kd[1][GROUP - 1], tk2 = S.u.k.kd[2][GROUP - 1];
         if (c == 0) {
             for (int i = 0; i < 3; i++)
-                st_relaxed(&D.hist[t * 6 + i], hpack(1, epoch, S.u.k.kd[cur][i][GROUP - 1], S.u.k.fv[cur][i][GROUP - 1]));
+                st_relaxed(&D.hist[t * 6 + i], hpack(1, epoch, S.u.k.kd[i][GROUP - 1], S.u.k.fv[i][GROUP - 1]));
             if (tk0 == 0 && tk1 == 0 && tk2 == 0)
                 for (int i = 0; i < 3; i++)
-                    st_relaxed(&D.hist[t * 6 + 3 + i], hpack(2, epoch, 0, S.u.k.fv[cur][i][GROUP - 1]));
+                    st_relaxed(&D.hist[t * 6 + 3 + i], hpack(2, epoch, 0, S.u.k.fv[i][GROUP - 1]));
             if (tk0 == 4 || tk1 == 4 || tk2 == 4) S.cplx = 1;
         }
         __syncthreads();
@@ -753,7 +763,7 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
             const int kk[3] = {tk0, tk1, tk2};
             for (int i = 0; i < 3; i++)
                 st_relaxed(&D.hist[t * 6 + 3 + i],
-                           hpack(2, epoch, 0, kk[i] == 0 ? S.u.k.fv[cur][i][GROUP - 1] : S.tin[kk[i] - 1]));
+                           hpack(2, epoch, 0, kk[i] == 0 ? S.u.k.fv[i][GROUP - 1] : S.tin[kk[i] - 1]));
         }
         // ---- fix-up: re-decode the pending prefix with concrete history
         if (act && pend > 0) {
@@ -809,6 +819,21 @@ __global__ void plan_kernel_fast(Plan* plan, const unsigned long long* dev_nbits
     *plan = p;
 }
 
+// resident decode workgroups (persistent grid; tiles are claimed from an atomic counter in order)
+static int decode_grid(int ct) {
+    static int cache[12];
+    const int ci = (ct > 0 && ct < 12) ? ct : 0;
+    if (cache[ci]) return cache[ci];
+    int dev = 0, ncu = 256, per = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const void* f = ct == 5 ? (const void*)decode_kernel_fast<5> : ct == 6 ? (const void*)decode_kernel_fast<6>
+                  : ct == 7 ? (const void*)decode_kernel_fast<7> : (const void*)decode_kernel_fast<11>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, GROUP, 0) != hipSuccess || per < 1) per = 1;
+    cache[ci] = per * ncu;
+    return cache[ci];
+}
+
 extern "C" int dc_launch_decode_fast(const uint8_t* s, const unsigned long long* dev_nbits,
                                      unsigned long long host_nbits, long long max_chunks, const Params* P,
                                      const DecBufs* D, float* out, long long num, uint32_t epoch, hipStream_t st) {
@@ -821,7 +846,7 @@ extern "C" int dc_launch_decode_fast(const uint8_t* s, const unsigned long long*
     DC_DISPATCH_F(P->ct, tile_fix_kernel, dim3((unsigned)((max_groups + 3) / 4 > 0 ? (max_groups + 3) / 4 : 1)), dim3(256), 0, st,
                   s, *P, *D);
     hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, st, *D);
-    const int gdec = (int)std::min<long long>(max_groups > 0 ? max_groups : 1, 256 * 3);
+    const int gdec = (int)std::min<long long>(max_groups > 0 ? max_groups : 1, decode_grid(P->ct));
     dc_mark_phase(6, st);
     DC_DISPATCH_F(P->ct, decode_kernel_fast, dim3(gdec), dim3(GROUP), 0, st, s, *P, *D, out, num, epoch);
     dc_mark_phase(7, st);
