@@ -27,15 +27,22 @@
 
 namespace dc {
 
-constexpr int LROW = 32;                       // LDS words per chunk (unpadded: measured faster than a
-                                               // 33-word row, the lanes drift apart within a few tokens)
-constexpr int LWORDS = GROUP * LROW + 8;       // + the words after the tile
+constexpr int LROW = 32;                       // stream words per chunk
+// LDS rows are padded to 33 words (stream word w sits at w + w/32): ds_read_b32 banks are
+// (address/4) mod 32 per 32-lane half, and the lanes of a wave walk their chunks at nearly the same
+// word offset, so unpadded rows put a whole half-wave on one or two banks (SQ_LDS_BANK_CONFLICT
+// was ~ half of the LDS cycles); padded, lane c's word w is on bank (c + w) mod 32.
+#ifndef DC_PAD
+#define DC_PAD 1
+#endif
+__host__ __device__ constexpr int padw(int n) { return DC_PAD ? n + (n >> 5) + 1 : n; }
+constexpr int LWORDS = padw(GROUP * LROW + 8);  // + the words after the tile
 #ifndef DC_OV
 #define DC_OV 1024
 #endif
 constexpr int OV = DC_OV;                       // overlap: P_c starts OV bits before its chunk
 constexpr int OVW = OV / 32;
-constexpr int PWORDS = LWORDS + OVW;
+constexpr int PWORDS = padw(GROUP * LROW + 8 + OVW);
 constexpr int KMAX = 2;                        // extra known entries per chunk (besides P_c's own)
 constexpr int RMAX = 12;                       // closure rounds inside a tile
 constexpr int CW = CHUNK_BITS / 32;            // words per chunk
@@ -43,7 +50,8 @@ constexpr int UNKE = 63;
 
 #define STAMP(ph) do { if (D.dbg && threadIdx.x == 0 && t < 4096) D.dbg[t * 16 + (ph)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
-__device__ __forceinline__ uint32_t ldw(const uint32_t* L, int w) { return L[w]; }
+__device__ __forceinline__ int lidx(int w) { return DC_PAD ? w + (w >> 5) : w; }
+__device__ __forceinline__ uint32_t ldw(const uint32_t* L, int w) { return L[lidx(w)]; }
 
 // branch-free MSB-first reader: w0:w1 hold the next 64 bits from bit sh of w0, w2 the next word.
 // Every step is fetch() (issues the LDS read of the word after w2, at the top of the step) ... step()
@@ -93,7 +101,7 @@ __device__ __forceinline__ void stage_words(uint32_t* L, const uint8_t* s, long 
             const int i4 = threadIdx.x + q * GROUP;
             if (q < QF || i4 < n4) {
                 const int i = 4 * i4;
-                uint32_t* d = L + i;
+                uint32_t* d = L + lidx(i);
                 d[0] = __builtin_bswap32(r[q].x);
                 d[1] = __builtin_bswap32(r[q].y);
                 d[2] = __builtin_bswap32(r[q].z);
@@ -115,7 +123,7 @@ __device__ __forceinline__ void stage_words(uint32_t* L, const uint8_t* s, long 
                 v = (v << 8) | (bi < nbytes ? (uint32_t)s[bi] : 0u);
             }
         }
-        L[i] = v;
+        L[lidx(i)] = v;
     }
 }
 
@@ -127,8 +135,7 @@ __device__ __forceinline__ void stage_tile(uint32_t* L, const uint8_t* s, long l
 // walk entry e of chunk c (LDS bits [cs, cend)) alongside P_c (whose first boundary in the chunk is
 // pmask's lowest bit); the reader that is behind steps.  Returns the exit relative to the next chunk
 // and the number of tokens starting in the chunk.
-template <int CT>
-__device__ __forceinline__ void walk_lds(const uint32_t* L, const Params& P, int cs, int cend, int e,
+__device__ __forceinline__ void walk_lds(const uint32_t* L, const uint8_t* tl, int cs, int cend, int e,
                                          uint32_t pmask, int pexit, int pcnt, int* out_exit, int* out_cnt) {
     if ((pmask >> e) & 1u) {
         *out_exit = pexit;
@@ -145,7 +152,7 @@ __device__ __forceinline__ void walk_lds(const uint32_t* L, const Params& P, int
         const bool sa = A.pos < B.pos || B.pos >= cend;
         const uint32_t nx = ldw(L, (sa ? A.wi : B.wi) + 3);
         const uint32_t tk = sa ? A.peek() : B.peek();
-        const int len = token_len_bf<CT>(tk, P);
+        const int len = tl[tk >> 23];
         if (sa) { A.nx = nx; A.step(len); ca++; } else { B.nx = nx; B.step(len); cb++; }
     }
     if (merged) { *out_exit = pexit; *out_cnt = ca + pcnt - cb; return; }
@@ -157,6 +164,7 @@ __device__ __forceinline__ void walk_lds(const uint32_t* L, const Params& P, int
 // ------------------------------------------------------------------------------------------------
 struct ParseShared {
     uint32_t L[PWORDS];
+    uint8_t tl[512];                           // token length by the first 9 bits (build_lut_len)
     uint32_t ke[GROUP * KMAX];                 // entry<<16 | exit<<10 | cnt
     uint8_t nkr[2][GROUP];                     // known-entry count of every chunk, by round parity
     uint32_t pm[GROUP];
@@ -192,6 +200,7 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
     __shared__ ParseShared S;
     const Plan pl = *D.plan;
     const int c = threadIdx.x, lane = c & 63, wid = c >> 6;
+    build_lut_len<CT>(S.tl, P, c, GROUP);                             // visible after the first barrier
     for (long long t = blockIdx.x; t < pl.ngroups; t += gridDim.x) {
         const long long tbit = t * (long long)GROUP * CHUNK_BITS;
         STAMP(0);
@@ -214,19 +223,19 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
             Rd r;
             r.init(S.L, gc == 0 ? cs : cs - OV);
             const unsigned long long q0 = D.dbg ? __builtin_amdgcn_s_memtime() : 0;
-            while (r.pos < cs) { r.fetch(S.L); r.step(token_len_bf<CT>(r.peek(), P)); }
+            while (r.pos < cs) { r.fetch(S.L); r.step(S.tl[r.peek() >> 23]); }
             if (D.dbg && t < 4096 && (c & 63) == 0)                  // per-wave cycles (diagnostic)
                 D.dbg[t * 16 + 12 + (c >> 6)] = (__builtin_amdgcn_s_memtime() - q0) << 16;
             const int pend = min(cs + 32, cend);                      // boundaries in the first word
             while (r.pos < pend) {
                 r.fetch(S.L);
                 pm |= 1u << (r.pos - cs);
-                r.step(token_len_bf<CT>(r.peek(), P));
+                r.step(S.tl[r.peek() >> 23]);
                 n++;
             }
             while (r.pos < cend) {
                 r.fetch(S.L);
-                r.step(token_len_bf<CT>(r.peek(), P));
+                r.step(S.tl[r.peek() >> 23]);
                 n++;
             }
             const int xx = r.pos - (cs + CHUNK_BITS);
@@ -242,7 +251,7 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
             const int e = S.x[c - 1];
             if (!((pm >> e) & 1u)) {
                 int ex, cn;
-                walk_lds<CT>(S.L, P, cs, cend, e, pm, x, n, &ex, &cn);
+                walk_lds(S.L, S.tl, cs, cend, e, pm, x, n, &ex, &cn);
                 S.ke[c * KMAX] = ((uint32_t)e << 16) | ((uint32_t)ex << 10) | (uint32_t)cn;
                 nk = 1;
             }
@@ -270,7 +279,7 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
                     need &= need - 1;
                     if (nk >= KMAX) { atomicOr(D.err, 64u); break; }
                     int ex, cn;
-                    walk_lds<CT>(S.L, P, cs, cend, e, pm, x, n, &ex, &cn);
+                    walk_lds(S.L, S.tl, cs, cend, e, pm, x, n, &ex, &cn);
                     S.ke[c * KMAX + nk] = ((uint32_t)e << 16) | ((uint32_t)ex << 10) | (uint32_t)cn;
                     nk++;
                         added = 1;
@@ -377,7 +386,8 @@ __device__ __forceinline__ bool lookup_global(const DecBufs& D, long long gc, in
 // chunks get their entries and offsets overridden.  One wave per tile.
 constexpr int FIXW = 8;                                   // chunks a fix-up walk may cover
 struct FixShared {
-    uint32_t L[4][FIXW * LROW + 8];
+    uint32_t L[4][padw(FIXW * LROW + 8)];
+    uint8_t tl[512];
 };
 
 template <int CT>
@@ -387,6 +397,8 @@ __global__ __launch_bounds__(256) void tile_fix_kernel(const uint8_t* __restrict
     const long long nt = pl.ngroups;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const long long t = (long long)blockIdx.x * 4 + wv;
+    build_lut_len<CT>(S.tl, P, threadIdx.x, 256);
+    __syncthreads();
     if (t >= nt) return;
     const int E = t == 0 ? 0 : (int)(D.tmap[(t - 1) * 4 + 1] >> 24);
     const uint32_t pm0 = D.tmap[t * 4 + 0], r1 = D.tmap[t * 4 + 1];
@@ -415,14 +427,14 @@ __global__ __launch_bounds__(256) void tile_fix_kernel(const uint8_t* __restrict
         if (gw < nwfull) v = __builtin_bswap32(w[gw]);
         else if (4 * gw < pl.nbytes)
             for (int k = 0; k < 4; k++) { const long long bi = 4 * gw + k; v = (v << 8) | (bi < pl.nbytes ? (uint32_t)s[bi] : 0u); }
-        L[i] = v;
+        L[lidx(i)] = v;
     }
     __builtin_amdgcn_s_waitcnt(0);                      // the wave's own LDS stores land in order
     __builtin_amdgcn_wave_barrier();
     if (lane != 0) return;
     const int cend0 = (int)min((long long)CHUNK_BITS, rem);
     int ex, c0;
-    walk_lds<CT>(L, P, 0, cend0, E, pm0, x0, n0, &ex, &c0);
+    walk_lds(L, S.tl, 0, cend0, E, pm0, x0, n0, &ex, &c0);
     const long long g0 = t * GROUP;
     int k = 1;
     uint32_t acc = 0;
@@ -441,7 +453,7 @@ __global__ __launch_bounds__(256) void tile_fix_kernel(const uint8_t* __restrict
         if (!lookup_global(D, gk, ex, &nx, &cn)) {
             const int cs = k * CHUNK_BITS;
             const int ce = (int)min((long long)(cs + CHUNK_BITS), rem);
-            walk_lds<CT>(L, P, cs, ce, ex, D.p_mask[gk], D.p_exit[gk], D.p_cnt[gk], &nx, &cn);
+            walk_lds(L, S.tl, cs, ce, ex, D.p_mask[gk], D.p_exit[gk], D.p_cnt[gk], &nx, &cn);
         }
         D.entry[gk] = (uint8_t)ex;
         D.tokoff[gk] = acc;
@@ -487,6 +499,8 @@ __global__ __launch_bounds__(1024) void tile_scan_kernel(DecBufs D) {
         D.tbase[t] = run;
         run += count(t);
     }
+    if (t1 == nt && t0 < t1) D.tbase[nt] = run;             // total: the last tile's end
+    if (nt == 0 && tid == 0) D.tbase[0] = 0;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -505,41 +519,46 @@ constexpr int RING = DC_RING;
 constexpr int SECT = DC_SECT;
 static_assert(SECT == 2 || SECT % 4 == 0, "sectors of 2 or 4k floats");
 
-__device__ __forceinline__ void store_sector(const float* ring, float* out, long long s0, int a0, long long num);
-
-// at a flush point: the head (values before the first sector boundary) once it is complete, then the
-// complete sector (at most one is pending: a lane adds <= SECT values between flush points)
-__device__ __forceinline__ void flush_ring(const float* ring, float* out, long long k0, long long& fl, long long idx,
-                                           bool& hdone, int a0, long long num) {
-    if (!hdone && idx >= fl) {
-        for (long long ii = k0; ii < fl; ii++)
-            if (ii < num) out[ii] = ring[(ii + a0) & (RING - 1)];
-        hdone = true;
-    }
-    if (fl + SECT <= idx) {
-        store_sector(ring, out, fl, a0, num);
-        fl += SECT;
-    }
-}
-
-__device__ __forceinline__ void store_sector(const float* ring, float* out, long long s0, int a0, long long num) {
-    const int sl = (int)((s0 + a0) & (RING - 1));
-    if (s0 + SECT <= num) {
+// Indices are relative to the chunk's first output index k0 (32-bit): token j sits in ring slot
+// (j + r0) & (RING - 1) with r0 = (k0 + a0) & (RING - 1); sectors start at j = h + SECT*i, h = the
+// values before the first sector boundary; lim = num - k0 bounds every store.
+__device__ __forceinline__ void store_sector(const float* ring, float* outk, int s0, int r0, int lim) {
+#ifdef DC_NOSTORE
+    if (lim >= 0) return;
+#endif
+    const int sl = (s0 + r0) & (RING - 1);
+    if (s0 + SECT <= lim) {
         if constexpr (SECT % 4 == 0) {
             const float4* r4 = reinterpret_cast<const float4*>(ring + sl);
-            float4* o4 = reinterpret_cast<float4*>(out + s0);
+            float4* o4 = reinterpret_cast<float4*>(outk + s0);
 #pragma unroll
             for (int q = 0; q < SECT / 4; q++) o4[q] = r4[q];
         } else {
-            *reinterpret_cast<float2*>(out + s0) = *reinterpret_cast<const float2*>(ring + sl);
+            *reinterpret_cast<float2*>(outk + s0) = *reinterpret_cast<const float2*>(ring + sl);
         }
     } else {
-        for (int i = 0; i < SECT && s0 + i < num; i++) out[s0 + i] = ring[sl + i];
+        for (int i = 0; i < SECT && s0 + i < lim; i++) outk[s0 + i] = ring[sl + i];
+    }
+}
+
+// at a flush point (j values decoded): the head (values before the first sector boundary) once it
+// is complete, then the complete sector (at most one is pending: a lane adds <= SECT values between
+// flush points)
+__device__ __forceinline__ void flush_ring(const float* ring, float* outk, int r0, int& fl, int j, bool& hdone, int lim) {
+    if (!hdone && j >= fl) {
+        for (int ii = 0; ii < fl; ii++)
+            if (ii < lim) outk[ii] = ring[(ii + r0) & (RING - 1)];
+        hdone = true;
+    }
+    if (fl + SECT <= j) {
+        store_sector(ring, outk, fl, r0, lim);
+        fl += SECT;
     }
 }
 
 struct DecodeShared {
     uint32_t L[LWORDS];
+    TokLut T;                                      // token length / pattern tables (build_lut)
     union {
         float ring[GROUP * RING];                  // decode pass output rings
         struct {                                   // carry scan (in place, two barriers a step)
@@ -565,6 +584,7 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
     __shared__ DecodeShared S;
     const Plan pl = *D.plan;
     const int c = threadIdx.x;
+    build_lut<CT>(S.T, P, c, GROUP);                                  // visible after the first barrier
     while (true) {
         if (c == 0) S.tile = (long long)atomicAdd(&D.ctr[4], 1u);
         __syncthreads();
@@ -610,11 +630,15 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
         bool sent = false;
         const int a0 = (int)((reinterpret_cast<uintptr_t>(out) >> 2) & (SECT - 1));
         float* ring = S.u.ring + c * RING;
-        long long fl = 0, idx = (long long)k0;                      // next sector to store; next index
-        bool hdone = false;                                          // head (partial first sector) stored
         const bool dec = act && e != UNKE;
+        float* outk = out + (long long)k0;
         if (dec) {
-            fl = (((long long)k0 + a0 + SECT - 1) & ~(long long)(SECT - 1)) - a0;
+            const long long k0l = (long long)k0;
+            const int r0 = (int)((k0l + a0) & (RING - 1));
+            int fl = (int)((SECT - ((k0l + a0) & (SECT - 1))) & (SECT - 1));   // first sector start
+            bool hdone = false;                                      // head (partial first sector) stored
+            const long long liml = num - k0l;
+            const int lim = liml > 0x7FFFFFFFll ? 0x7FFFFFFF : (int)max(liml, 0ll);
             Rd r;
             r.init(S.L, cs + e);
             int j = 0, it = 0;
@@ -622,53 +646,62 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
             while (r.pos < cend && ((k1 | k2 | k3) != 0 || (first && j < 3))) {
                 r.fetch(S.L);
                 const uint32_t tk = r.peek();
-                const int len = token_len_bf<CT>(tk, P);
-                int code;
-                const uint32_t pat = token_pattern_bf<CT>(tk, len, P, &code);
+                const uint32_t meta = S.T.meta[tk >> 23];
+                uint32_t pat = lut_pattern(S.T, tk, meta);
+                int code = 0;
+                if (CT != 6) {
+                    const bool c3 = (int)tk < 0;
+                    code = c3 ? (int)__builtin_amdgcn_ubfe(tk, 29u, 2u) : 0;
+                    pat = c3 ? 0u : pat;
+                }
                 const float p2 = predict2(f1, f2), p3 = predict3(f1, f2, f3);
                 const float v = code == 0 ? __uint_as_float(pat) : (code == 1 ? f1 : (code == 2 ? p2 : p3));
                 const int kind = code == 0 ? 0 : (code == 1 ? k1 : (code == 2 ? ((k1 | k2) ? 4 : 0) : ((k1 | k2 | k3) ? 4 : 0)));
                 if (kind != 0) pend = j + 1;                         // re-decoded by the fix-up
                 // history sentinel (-1.0f) or a prediction before the stream's history is full: exact path
                 sent |= (kind == 0 && __float_as_uint(v) == 0xBF800000u) || (first && j < 3 && code != 0);
-                ring[(idx + a0) & (RING - 1)] = v;
+                ring[(j + r0) & (RING - 1)] = v;
                 f3 = f2; k3 = k2; f2 = f1; k2 = k1; f1 = v; k1 = kind;
-                r.step(len);
+                r.step((int)(meta >> 8));
                 j++;
-                idx++;
                 if (++it == SECT) {                                  // uniform among the active lanes
                     it = 0;
-                    flush_ring(ring, out, (long long)k0, fl, idx, hdone, a0, num);
+                    flush_ring(ring, outk, r0, fl, j, hdone, lim);
                 }
             }
-            flush_ring(ring, out, (long long)k0, fl, idx, hdone, a0, num);
+            flush_ring(ring, outk, r0, fl, j, hdone, lim);
             it = 0;
             // phase B: concrete history (kinds stay 0 from here on)
             while (r.pos < cend) {
                 r.fetch(S.L);
                 const uint32_t tk = r.peek();
-                const int len = token_len_bf<CT>(tk, P);
-                int code;
-                const uint32_t pat = token_pattern_bf<CT>(tk, len, P, &code);
-                float v = code == 0 ? __uint_as_float(pat) : f1;
-                if (__builtin_expect(__any(code >= 2), 0)) {                 // predictions: wave-uniform branch
-                    const float p2 = predict2(f1, f2), p3 = predict3(f1, f2, f3);
-                    v = code == 2 ? p2 : (code == 3 ? p3 : v);
+                const uint32_t meta = S.T.meta[tk >> 23];
+                const uint32_t pat = lut_pattern(S.T, tk, meta);
+                float v;
+                if (CT == 6) {
+                    v = __uint_as_float(pat);
+                } else {
+                    const uint32_t cc = __builtin_amdgcn_ubfe(tk, 29u, 3u);    // 4..7 = '100'..'111'
+                    v = cc < 4u ? __uint_as_float(pat) : (cc == 5u ? f1 : 0.0f);
+                    if (__builtin_expect(__any(cc >= 6u), 0)) {              // predictions: wave-uniform branch
+                        const float p2 = predict2(f1, f2), p3 = predict3(f1, f2, f3);
+                        v = cc == 6u ? p2 : (cc == 7u ? p3 : v);
+                    }
                 }
-                ring[(idx + a0) & (RING - 1)] = v;
+                ring[(j + r0) & (RING - 1)] = v;
                 sent |= __float_as_uint(v) == 0xBF800000u;
                 f3 = f2; f2 = f1; f1 = v;
-                r.step(len);
-                idx++;
+                r.step((int)(meta >> 8));
+                j++;
                 if (++it == SECT) {
                     it = 0;
-                    flush_ring(ring, out, (long long)k0, fl, idx, hdone, a0, num);
+                    flush_ring(ring, outk, r0, fl, j, hdone, lim);
                 }
             }
-            flush_ring(ring, out, (long long)k0, fl, idx, hdone, a0, num);
-            const long long t0 = hdone ? fl : (long long)k0;         // tail, or a chunk inside one sector
-            for (long long ii = t0; ii < idx; ii++)
-                if (ii < num) out[ii] = ring[(ii + a0) & (RING - 1)];
+            flush_ring(ring, outk, r0, fl, j, hdone, lim);
+            const int t0 = hdone ? fl : 0;                           // tail, or a chunk inside one sector
+            for (int ii = t0; ii < j; ii++)
+                if (ii < lim) outk[ii] = ring[(ii + r0) & (RING - 1)];
         }
         if (sent) atomicOr(D.err, 128u);
         sent = false;
@@ -775,11 +808,17 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
             for (int jj = 0; jj < pend; jj++) {
                 r.fetch(S.L);
                 const uint32_t tk = r.peek();
-                const int len = token_len_bf<CT>(tk, P);
-                int code;
-                const uint32_t pat = token_pattern_bf<CT>(tk, len, P, &code);
+                const uint32_t meta = S.T.meta[tk >> 23];
+                const int len = (int)(meta >> 8);
+                uint32_t pat = lut_pattern(S.T, tk, meta);
+                int code = 0;
+                if (CT != 6) {
+                    const bool c3 = (int)tk < 0;
+                    code = c3 ? (int)__builtin_amdgcn_ubfe(tk, 29u, 2u) : 0;
+                    pat = c3 ? 0u : pat;
+                }
                 const float v = code == 0 ? __uint_as_float(pat) : predict_value(code, g1, g2, g3);
-                if (k0 + jj < (unsigned long long)num) out[k0 + jj] = v;
+                if (k0 + jj < (unsigned long long)num) outk[jj] = v;
                 sent |= __float_as_uint(v) == 0xBF800000u;
                 g3 = g2; g2 = g1; g1 = v;
                 r.step(len);

@@ -218,6 +218,63 @@ __device__ __forceinline__ uint32_t token_pattern_bf(uint32_t t, int len, const 
     return c3 ? 0u : u;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Token tables.  Everything a token's length and (non-predicted) value pattern depend on lies in its
+// first 9 bits: the c3 bit, the 8 exponent bits, and for CT7 (type <= 7, enforced by the host) the
+// type head ones and the flag bit, which end at bit 30 - type >= 23.  Per-call LDS tables indexed by
+// t >> 23 therefore replace the selects of token_len_bf / token_pattern_bf:
+//   meta[t >> 23]          = sh | len << 8          (len 3..32; sh = the masked-token shift, 0 for raw)
+//   kv[(t >> 23) & 255]    = {keep, add}: pattern = ((t >> sh) & keep) | add for every non-c3 token
+// (a c3 token's pattern is 0 / a prediction, selected by the caller; CT6 has no c3 tokens and its
+// sign bit passes through `keep`, so bit 31 is not needed to index kv).
+struct TokLut {
+    uint16_t meta[512];
+    uint2 kv[256];
+};
+
+template <int CT>
+__device__ __forceinline__ void build_lut_len(uint8_t* tl, const Params& P, int tid, int nthr) {
+    for (int i = tid; i < 512; i += nthr) tl[i] = (uint8_t)token_len_bf<CT>((uint32_t)i << 23, P);
+}
+
+template <int CT>
+__device__ __forceinline__ void build_lut_meta(uint16_t* meta, const Params& P, int tid, int nthr) {
+    for (int i = tid; i < 512; i += nthr) {
+        const uint32_t t = (uint32_t)i << 23;
+        const int len = token_len_bf<CT>(t, P);
+        int sh = 0;
+        if (CT == 7 && (int)t >= 0 && (t & P.hm) == P.hm) sh = ((t >> P.fsh) & 1u) ? P.s1 : P.s0;
+        meta[i] = (uint16_t)(sh | (len << 8));
+    }
+}
+
+template <int CT>
+__device__ __forceinline__ void build_lut(TokLut& T, const Params& P, int tid, int nthr) {
+    build_lut_meta<CT>(T.meta, P, tid, nthr);
+    for (int i = tid; i < 256; i += nthr) {
+        const uint32_t t = (uint32_t)i << 23;                  // bit 31 clear: never a c3 token
+        uint32_t keep, add;
+        if (CT == 11) {
+            keep = 0xFFFFFFFFu; add = 0u;
+        } else {
+            const int len = token_len_bf<6>(t, P);             // raw length 9 + m(E)
+            const uint32_t y = len >= 32 ? 0u : 0xFFFFFFFFu >> len;
+            keep = ~y; add = y & ~(y >> 1);
+            if (CT == 7 && (t & P.hm) == P.hm) {
+                const bool f1 = (t >> P.fsh) & 1u;
+                keep = f1 ? P.k1 : P.k0;
+                add = f1 ? P.c1 : P.c0;
+            }
+        }
+        T.kv[i] = make_uint2(keep, add);
+    }
+}
+
+__device__ __forceinline__ uint32_t lut_pattern(const TokLut& T, uint32_t t, uint32_t meta) {
+    const uint2 kv = T.kv[(t >> 23) & 255u];
+    return ((t >> (meta & 31u)) & kv.x) | kv.y;
+}
+
 // NaN results follow x86 SSE (the reference's host): the first NaN operand in evaluation order,
 // quieted; a NaN made from non-NaN operands (inf - inf) is the x86 default NaN 0xFFC00000.  Only
 // streams decoded outside the codec's domain ever reach this (an encoder never predicts with NaNs).
