@@ -671,33 +671,42 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
             }
             flush_ring(ring, outk, r0, fl, j, hdone, lim);
             it = 0;
-            // phase B: concrete history (kinds stay 0 from here on)
-            while (r.pos < cend) {
-                r.fetch(S.L);
-                const uint32_t tk = r.peek();
-                const uint32_t meta = S.T.meta[tk >> 23];
-                const uint32_t pat = lut_pattern(S.T, tk, meta);
-                float v;
-                if (CT == 6) {
-                    v = __uint_as_float(pat);
-                } else {
-                    const uint32_t cc = __builtin_amdgcn_ubfe(tk, 29u, 3u);    // 4..7 = '100'..'111'
-                    v = cc < 4u ? __uint_as_float(pat) : (cc == 5u ? f1 : 0.0f);
-                    if (__builtin_expect(__any(cc >= 6u), 0)) {              // predictions: wave-uniform branch
-                        const float p2 = predict2(f1, f2), p3 = predict3(f1, f2, f3);
-                        v = cc == 6u ? p2 : (cc == 7u ? p3 : v);
+            // phase B: concrete history (kinds stay 0 from here on).  Runs in uniform blocks of SECT
+            // steps with per-lane predication (a finished lane steps by 0 and keeps its history), so
+            // the only branches are the block loop, the flush and the rare prediction branch.  Only
+            // '110'/'111' predictions can make the -1.0f sentinel here unless chk_all (CT6 or a
+            // negative mask with 23 kept mantissa bits: patterns without a midpoint bit).
+            const bool chk_all = (CT == 6 && P.B >= 23) || (CT == 7 && (P.mask17 >> 16) != 0u && P.mm == 23);
+            int sentv = 0;
+            while (__any(r.pos < cend)) {
+#pragma unroll
+                for (int u = 0; u < SECT; u++) {
+                    r.fetch(S.L);
+                    const uint32_t tk = r.peek();
+                    const uint32_t meta = S.T.meta[tk >> 23];
+                    const uint32_t pat = lut_pattern(S.T, tk, meta);
+                    const bool on = r.pos < cend;
+                    float v;
+                    if (CT == 6) {
+                        v = __uint_as_float(pat);
+                    } else {
+                        const uint32_t cc = __builtin_amdgcn_ubfe(tk, 29u, 3u);    // 4..7 = '100'..'111'
+                        v = cc < 4u ? __uint_as_float(pat) : (cc == 5u ? f1 : 0.0f);
+                        if (__builtin_expect(__any(on && cc >= 6u), 0)) {       // predictions: wave-uniform branch
+                            const float p2 = predict2(f1, f2), p3 = predict3(f1, f2, f3);
+                            v = cc == 6u ? p2 : (cc == 7u ? p3 : v);
+                            sentv |= (on && cc >= 6u && __float_as_uint(v) == 0xBF800000u) ? 1 : 0;
+                        }
                     }
+                    if (chk_all) sentv |= (on && __float_as_uint(v) == 0xBF800000u) ? 1 : 0;
+                    ring[(j + r0) & (RING - 1)] = v;
+                    f3 = on ? f2 : f3; f2 = on ? f1 : f2; f1 = on ? v : f1;
+                    r.step(on ? (int)(meta >> 8) : 0);
+                    j += on ? 1 : 0;
                 }
-                ring[(j + r0) & (RING - 1)] = v;
-                sent |= __float_as_uint(v) == 0xBF800000u;
-                f3 = f2; f2 = f1; f1 = v;
-                r.step((int)(meta >> 8));
-                j++;
-                if (++it == SECT) {
-                    it = 0;
-                    flush_ring(ring, outk, r0, fl, j, hdone, lim);
-                }
+                flush_ring(ring, outk, r0, fl, j, hdone, lim);
             }
+            sent |= sentv != 0;
             flush_ring(ring, outk, r0, fl, j, hdone, lim);
             const int t0 = hdone ? fl : 0;                           // tail, or a chunk inside one sector
             for (int ii = t0; ii < j; ii++)
