@@ -112,6 +112,11 @@ int dc_debug_enc_stamps(unsigned long long* host, long long n) {
 
 int dc_init(int device) {
     if (G.inited) return DC_OK;
+    {   /* run-time override of the compile-time bound, so an unchanged app binary can run at another
+         * bound (the reference recompiles after impl/set-parameter.sh edits the header) */
+        const char* eb = getenv("DC_ABS_ERROR_BOUND");
+        if (eb && *eb && atof(eb) > 0.0) dc_set_abs_error_bound(atof(eb));
+    }
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return seterr(DC_ERR_NOGPU, "no HIP device visible");
     if (device < 0 || device >= n) return seterr(DC_ERR_ARG, "device %d out of range", device);
@@ -777,6 +782,84 @@ void bit_flip(unsigned char* bits, int bytes) {                  /* :5858-5865, 
 }
 
 uint64_t get_random_int(uint64_t from, uint64_t to) { return (uint64_t)rand() % (to - from + 1) + from; }
+
+/* ---- Himeno plane extraction and binary file helpers (link closure of the float apps) ----------- */
+#ifndef MIMAX
+#define MIMAX 129                                                /* impl/param.h:7-9 */
+#endif
+#ifndef MJMAX
+#define MJMAX 129
+#endif
+#ifndef MKMAX
+#define MKMAX 131
+#endif
+
+/* transform_3d_array_to_1d_array (:3741-3775) for an explicit [mi][mj][mk] extent */
+float* dc_transform_3d_array_to_1d_array(const float* data, int mi, int mj, int mk, int ijk, int v, int imax,
+                                         int jmax, int kmax) {
+    int A, B;
+    if (ijk == 1) { A = jmax; B = kmax; }
+    else if (ijk == 2) { A = imax; B = kmax; }
+    else if (ijk == 3) { A = imax; B = jmax; }
+    else { seterr(DC_ERR_ARG, "transform_3d_array_to_1d_array: ijk %d", ijk); return NULL; }
+    float* o = (float*)malloc(sizeof(float) * (size_t)(A > 0 ? A : 1) * (size_t)(B > 0 ? B : 1));
+    if (!o) return NULL;
+    (void)mi;
+    size_t n = 0;
+    for (int a = 0; a < A; a++)
+        for (int b = 0; b < B; b++) {
+            size_t i, j, k;
+            if (ijk == 1) { i = (size_t)v; j = (size_t)a; k = (size_t)b; }
+            else if (ijk == 2) { i = (size_t)a; j = (size_t)v; k = (size_t)b; }
+            else { i = (size_t)a; j = (size_t)b; k = (size_t)v; }
+            o[n++] = data[(i * (size_t)mj + j) * (size_t)mk + k];
+        }
+    return o;
+}
+
+float* transform_3d_array_to_1d_array(float data[MIMAX][MJMAX][MKMAX], int ijk, int v, int imax, int jmax, int kmax) {
+    return dc_transform_3d_array_to_1d_array(&data[0][0][0], MIMAX, MJMAX, MKMAX, ijk, v, imax, jmax, kmax);
+}
+
+/* :5290-5339 (the reference reports success / failure on stdout) */
+static void write_binary(const char* file, const void* data, size_t sz, int count) {
+    FILE* fp = fopen(file, "wb");
+    if (!fp) { printf("failed to open %s\n", file); return; }
+    fwrite(data, sz, (size_t)count, fp);
+    fclose(fp);
+    printf("saved %s\n", file);
+}
+void writetobinary_float(const char* file, float* data, int count) { write_binary(file, data, sizeof(float), count); }
+void writetobinary_char(const char* file, unsigned char* data, int count) { write_binary(file, data, 1, count); }
+
+/* :5383-5410: the whole file; the reference exit(0)s when it cannot be opened, this returns NULL */
+unsigned char* readfrombinary_char(const char* file, int* bytes_sz) {
+    FILE* fp = fopen(file, "rb");
+    if (!fp) { printf("failed to open %s\n", file); seterr(DC_ERR_ARG, "cannot open %s", file); return NULL; }
+    fseek(fp, 0, SEEK_END);
+    long sz = ftell(fp);
+    fseek(fp, 0, SEEK_SET);
+    unsigned char* arr = (unsigned char*)malloc(sz > 0 ? (size_t)sz : 1);
+    size_t got = arr ? fread(arr, 1, (size_t)(sz > 0 ? sz : 0), fp) : 0;
+    fclose(fp);
+    *bytes_sz = (int)got;
+    return arr;
+}
+
+/* :5412-5432 */
+float* readfrombinary_writetotxt_float(const char* binaryfile, const char* txtfile, int count) {
+    FILE* fp = fopen(binaryfile, "rb");
+    if (!fp) { seterr(DC_ERR_ARG, "cannot open %s", binaryfile); return NULL; }
+    float* arr = (float*)malloc(sizeof(float) * (size_t)(count > 0 ? count : 1));
+    size_t got = arr ? fread(arr, sizeof(float), (size_t)(count > 0 ? count : 0), fp) : 0;
+    fclose(fp);
+    (void)got;
+    fp = fopen(txtfile, "w");
+    if (!fp) { seterr(DC_ERR_ARG, "cannot open %s", txtfile); return arr; }
+    for (int i = 0; i < count; i++) fprintf(fp, "%f\n", arr[i]);
+    fclose(fp);
+    return arr;
+}
 
 void floattostr(float* a, char* str) {                           /* :5244-5252 */
     uint32_t c;

@@ -28,6 +28,42 @@
 extern "C" {
 #endif
 
+/* ---- application configuration macros of the reference header (impl/dataCompression.h:4-41): the
+ *      apps (pingpong.c, himenoBMTxps.c) read them; each can be overridden with -D.  absErrorBound
+ *      must equal the bound libdcamd was built with (make BOUND=...). ------------------------------ */
+#ifndef BER
+#define BER 1e-6
+#endif
+#ifndef absErrorBound
+#define absErrorBound 0.000001
+#endif
+#ifndef byte_or_bit
+#define byte_or_bit 2
+#endif
+#ifndef filename
+#define filename "dataset/testfloat_8_8_128"
+#endif
+#ifndef suffix
+#define suffix ".txt"
+#endif
+#ifndef output_suffix
+#define output_suffix "_output_"
+#endif
+#ifndef clusters
+#define clusters 100
+#endif
+#define bin_suffix ".dat"
+#define sz_suffix ".sz"
+#define zs_suffix ".zs"
+#define out_suffix ".out"
+#define sz_comp_cmd_prefix "./sz -z -f -c sz.config -M ABS -A "
+#define sz_comp_cmd_prefix_double "./sz -z -d -c sz.config -M ABS -A "
+#define sz_comp_cmd_suffix1 " -i "
+#define sz_comp_cmd_suffix2 ".dat -1 "
+#define sz_decomp_cmd_prefix "./sz -x -f -s "
+#define sz_decomp_cmd_prefix_double "./sz -x -d -s "
+#define sz_decomp_cmd_suffix ".dat.zs -1 "
+
 extern double absErrBound;            /* impl/dataCompression.c:21 */
 extern int absErrorBound_binary;      /* impl/dataCompression.c:22 */
 
@@ -102,6 +138,33 @@ double strtodbl(char* str);
 void add_bit_to_bytes(unsigned char** data_bits, int* bytes, int* pos, int flag);
 /* h:139 c:5492 */
 void bit_set(unsigned char* p_data, unsigned char position, int flag);
+
+/* ---- Himeno halo plane extraction and binary file helpers (link closure of pingpong/himenoBMTxps) -
+ * The 3-D array extent comes from the app's param.h (MIMAX/MJMAX/MKMAX, impl/param.h:7-9), which the
+ * reference compiles into dataCompression.c together with the app; libdcamd is built with the same
+ * values (make ... PARAM="-DMIMAX=.. -DMJMAX=.. -DMKMAX=..", default the reference param.h 129/129/131).
+ * dc_transform_3d_array_to_1d_array takes the extent explicitly for callers with another param.h. */
+#ifndef MIMAX
+#define MIMAX 129
+#endif
+#ifndef MJMAX
+#define MJMAX 129
+#endif
+#ifndef MKMAX
+#define MKMAX 131
+#endif
+/* h:124 c:3741-3775: plane ijk (1: i=v, 2: j=v, 3: k=v) of data as a new malloc()ed array, row-major */
+float* transform_3d_array_to_1d_array(float data[MIMAX][MJMAX][MKMAX], int ijk, int v, int imax, int jmax, int kmax);
+float* dc_transform_3d_array_to_1d_array(const float* data, int mi, int mj, int mk, int ijk, int v, int imax,
+                                         int jmax, int kmax);
+/* h:129 c:5290 */
+void writetobinary_float(const char* file, float* data, int count);
+/* h:131 c:5324 */
+void writetobinary_char(const char* file, unsigned char* data, int count);
+/* h:134 c:5383: whole file, *bytes_sz = its size */
+unsigned char* readfrombinary_char(const char* file, int* bytes_sz);
+/* h:135 c:5412: count floats from binaryfile, also written to txtfile as "%f\n" */
+float* readfrombinary_writetotxt_float(const char* binaryfile, const char* txtfile, int count);
 
 #ifdef __cplusplus
 }
