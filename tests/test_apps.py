@@ -6,7 +6,13 @@ container only) into oracle/_ref/apps/: `<app>_ref` with the reference codec com
 with this repo's include/dataCompression.h and -ldcamd.  The binaries travel to the GPU box with the
 tree; the reference sources do not.  On the GPU box both pingpong builds run the same input and must
 print the same compression ratio and the same round-trip error (`gosa`) for every deterministic CT
-(5/6/7/11; 8/9/10 flip random bits seeded by time(), 1 is the byte-wise codec)."""
+(1/5/6/7/11; 8/9/10 flip random bits seeded by time()).
+
+himenoBMTxps is link-checked only: with impl/param.h's two z-ranks each rank "receives" a halo from
+MPI_PROC_NULL at the physical boundary, decompresses a 0-byte stream and copies the never-written
+result (plus an uninitialised min) into p (impl/himenoBMTxps.c:644-706), so even the reference build
+prints a different Gosa on every run (inf, 2.8e20, 3.4e7 in three runs here) -- no fixed output to
+compare against."""
 import os
 import re
 import shutil
@@ -63,7 +69,7 @@ def _metrics(out):
 @pytest.mark.gpu
 @pytest.mark.skipif(not (os.path.isfile(_app("pingpong_dcamd")) and os.path.isfile(MPIRUN)),
                     reason="oracle/_ref/apps not built (run oracle/build_apps.sh where /root/reference exists)")
-@pytest.mark.parametrize("ct", [5, 6, 7, 11])
+@pytest.mark.parametrize("ct", [1, 5, 6, 7, 11])
 def test_pingpong_dcamd_matches_reference(ct, tmp_path):
     import sys
     sys.path.insert(0, os.path.join(ROOT, "data-compression_amd"))
@@ -77,6 +83,7 @@ def test_pingpong_dcamd_matches_reference(ct, tmp_path):
     out_gpu = _run_pingpong(_app("pingpong_dcamd"), ct, path, env)
     rr, gr = _metrics(out_ref)
     rg, gg = _metrics(out_gpu)
-    assert rr, out_ref[-1500:]
+    assert (rr or ct == 1) and gr, out_ref[-1500:]     # CT1 prints no bit-wise rate line
     assert rr == rg, (out_ref[-1500:], out_gpu[-1500:])
     assert gr == gg, (out_ref[-1500:], out_gpu[-1500:])
+
