@@ -36,6 +36,9 @@ def parse():
     ap.add_argument("--cpu-log2n", type=int, default=22, help="cpu_baseline sample size (2^k floats)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify the round trip against the oracle")
+    ap.add_argument("--ber", type=float, default=0.0,
+                    help="CT9 flow (BASELINE configs[4]): CRC-32 of the CT7 stream, floor(bits*BER) real bit flips on "
+                         "the received copy, CRC check, resend, decode -- all inside the timed step")
     return ap.parse_args()
 
 
@@ -147,11 +150,52 @@ def main():
         if ev:
             ev[2].record(ext)
 
-    for _ in range(args.warmup):
+    for _ in range(max(args.warmup, 1)):
         step()
     L.decode_finish()
     nbits = L.encode_result()
     nbytes = (nbits + 7) // 8
+
+    # ---- CT9 flow (--ber): sender CRC, channel copy with floor(bits*BER) flipped bits, receiver CRC
+    # check (one host round trip, as the MPI receiver's compare), resend of the clean stream, decode
+    # of the received copy.  The stream length is the warm-up's (same input every step).
+    resends = [0]
+    if args.ber > 0:
+        rcv = torch.empty(cap, dtype=torch.uint8, device=dev)
+        d_crc = torch.zeros(2, dtype=torch.int32, device=dev)
+        nflip = int(nbits * args.ber)
+        seed = [1]
+
+        def step(ev=None):                                   # noqa: F811 -- the CT9 variant of the step
+            if ev:
+                ev[0].record(ext)
+            L.encode_device(ct, xs.data_ptr(), n, stream.data_ptr(), idx0=idx0, type_=typ, mask17=mask17,
+                            total_ptr=d_nbits.data_ptr())
+            L.crc32_device_async(stream.data_ptr(), nbytes, d_crc.data_ptr())
+            with torch.cuda.stream(ext):
+                rcv[:nbytes].copy_(stream[:nbytes])
+            L.flip_bits_device(rcv.data_ptr(), nbits, nflip, seed[0])
+            seed[0] += nflip
+            L.crc32_device_async(rcv.data_ptr(), nbytes, d_crc.data_ptr() + 4)
+            L.synchronize()
+            c = d_crc.cpu().numpy()
+            while c[0] != c[1]:                               # damaged: resend and check again
+                resends[0] += 1
+                with torch.cuda.stream(ext):
+                    rcv[:nbytes].copy_(stream[:nbytes])
+                L.crc32_device_async(rcv.data_ptr(), nbytes, d_crc.data_ptr() + 4)
+                L.synchronize()
+                c = d_crc.cpu().numpy()
+            if ev:
+                ev[1].record(ext)
+            L.decode_device(ct, rcv.data_ptr(), nbytes, n, out.data_ptr(), type_=typ, mask17=mask17, max_bytes=cap)
+            if ev:
+                ev[2].record(ext)
+
+        for _ in range(args.warmup):
+            step()
+        L.decode_finish()
+        resends[0] = 0
 
     # ---- timed region: barrier + sync on both sides, max over ranks.  Per-kernel HIP events are
     # recorded by the library on its own stream (dc_timing_enable), one event set per step.
@@ -245,6 +289,14 @@ def main():
     }
     if ok is not None:
         res["check_vs_oracle"] = ok
+    if args.ber > 0:
+        res["metric"] = "GB/s (input float bytes) CT=9 flow: CT7 encode + CRC-32 + BER bit flips + CRC check + resend + decode"
+        res["config"]["workload"] = (f"CT9 (CT7 stream + CRC-32) at BER={args.ber:g} with real bit flips, "
+                                     f"{args.input.upper()} 2^{args.log2n} float32 per GPU, absErrorBound={args.bound:g}")
+        res["config"]["ber"] = args.ber
+        res["config"]["flips_per_step"] = int(nbits * args.ber)
+        res["config"]["resends"] = resends[0]
+        res["config"]["detected_all"] = resends[0] == args.steps
     if rank == 0 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(ct, args.bound, 1 << args.cpu_log2n, args.input)
     if rank == 0:

@@ -434,6 +434,33 @@ extern "C" int dc_launch_crc32(const uint8_t* s, long long nbytes, const uint32_
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// BER fault injection for the CT8/CT9 flow: flip `count` stream bits at the
+// positions splitmix64(seed + i) mod nbits, MSB-first within each byte like bit_flip (:5858-5865).
+// The reference's own pingpong CT9 path only *simulates* a CRC failure (impl/pingpong.c:421-430);
+// this flips real bits so the receiver's CRC check has something to detect.
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(256) void flip_bits_kernel(uint8_t* s, unsigned long long nbits, long long count,
+                                                        unsigned long long seed) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= count || nbits == 0) return;
+    const unsigned long long p = splitmix64(seed + (unsigned long long)i) % nbits;
+    const unsigned long long byte = p >> 3;
+    uint32_t* w = reinterpret_cast<uint32_t*>(s + (byte & ~3ull));
+    atomicXor(w, (uint32_t)(0x80u >> (p & 7)) << (8 * (byte & 3)));
+}
+
+extern "C" int dc_launch_flip_bits(uint8_t* s, unsigned long long nbits, long long count, unsigned long long seed,
+                                   hipStream_t st) {
+    if (count <= 0) return 0;
+    hipLaunchKernelGGL(flip_bits_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st, s, nbits, count, seed);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int dc_launch_ham_syndrome(const uint8_t* s, long long nbytes, unsigned long long* d_syn_ones,
                                       hipStream_t st) {
     (void)hipMemsetAsync(d_syn_ones, 0, 16, st);

@@ -531,23 +531,44 @@ int dc_med_device(const void* d_x, long long n, float* mean_out, int* type_out) 
     return DC_OK;
 }
 
+int dc_flip_bits_device(void* d_s, unsigned long long nbits, long long count, unsigned long long seed) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if ((uintptr_t)d_s & 3u) return seterr(DC_ERR_ARG, "stream must be 4-byte aligned");
+    if (dc_launch_flip_bits((uint8_t*)d_s, nbits, count, seed, G.st)) return seterr(DC_ERR_HIP, "flip launch failed");
+    return DC_OK;
+}
+
+static int crc_into(const void* d_s, long long nbytes, uint32_t* d_out);
+
+int dc_crc32_device_async(const void* d_s, long long nbytes, uint32_t* d_crc) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    return crc_into(d_s, nbytes, d_crc);
+}
+
 int dc_crc32_device(const void* d_s, long long nbytes, uint32_t* crc_out) {
     int rc = ensure_init();
     if (rc) return rc;
-    long long parts = dc_crc_parts(nbytes) + 1;
-    if (parts > G.crcparts_cap) {
-        if (G.d_crcparts) HIPCHK(hipFree(G.d_crcparts));
-        HIPCHK(hipMalloc((void**)&G.d_crcparts, parts * 4 + 1024));
-        G.crcparts_cap = parts;
-    }
-    if (dc_launch_crc32((const uint8_t*)d_s, nbytes, G.d_crctab, G.d_x2n, G.d_crcparts, 0u, G.d_crc, G.st))
-        return seterr(DC_ERR_HIP, "crc launch failed");
+    if ((rc = crc_into(d_s, nbytes, G.d_crc))) return rc;
     if (crc_out) {
         uint32_t h;
         HIPCHK(hipMemcpyAsync(&h, G.d_crc, 4, hipMemcpyDeviceToHost, G.st));
         HIPCHK(hipStreamSynchronize(G.st));
         *crc_out = h;
     }
+    return DC_OK;
+}
+
+static int crc_into(const void* d_s, long long nbytes, uint32_t* d_out) {
+    long long parts = dc_crc_parts(nbytes) + 1;
+    if (parts > G.crcparts_cap) {
+        if (G.d_crcparts) HIPCHK(hipFree(G.d_crcparts));
+        HIPCHK(hipMalloc((void**)&G.d_crcparts, parts * 4 + 1024));
+        G.crcparts_cap = parts;
+    }
+    if (dc_launch_crc32((const uint8_t*)d_s, nbytes, G.d_crctab, G.d_x2n, G.d_crcparts, 0u, d_out, G.st))
+        return seterr(DC_ERR_HIP, "crc launch failed");
     return DC_OK;
 }
 

@@ -33,6 +33,7 @@ EXT_SYMBOLS = [
     "dc_get_abs_error_bound", "dc_stream_capacity", "dc_encode_device", "dc_encode_result",
     "dc_decode_device", "dc_decode_finish", "dc_to_small_device", "dc_med_device", "dc_crc32_device",
     "dc_decode_chunk_bits_value", "dc_ct1_encode_device", "dc_ct1_decode_device", "dc_encode_bits_device",
+    "dc_crc32_device_async", "dc_flip_bits_device",
 ]
 
 
@@ -245,6 +246,27 @@ class Lib:
         v = C.c_uint32(0)
         self.check(self.L.dc_crc32_device(s_ptr, nbytes, C.byref(v)), "dc_crc32_device")
         return v.value
+
+    def crc32_device_async(self, s_ptr, nbytes, d_crc_ptr):
+        self.check(self.L.dc_crc32_device_async(C.c_void_p(s_ptr), C.c_longlong(nbytes), C.c_void_p(d_crc_ptr)),
+                   "dc_crc32_device_async")
+
+    def flip_bits_device(self, s_ptr, nbits, count, seed):
+        self.check(self.L.dc_flip_bits_device(C.c_void_p(s_ptr), C.c_ulonglong(nbits), C.c_longlong(count),
+                                              C.c_ulonglong(seed)), "dc_flip_bits_device")
+
+
+def flip_positions(nbits, count, seed):
+    """Host restatement of dc_flip_bits_device's positions (splitmix64(seed + i) mod nbits)."""
+    M = (1 << 64) - 1
+    out = []
+    for i in range(count):
+        z = (seed + i + 0x9E3779B97F4A7C15) & M
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        z ^= z >> 31
+        out.append(z % nbits)
+    return out
 
 
 # ---- multi-GPU: one process per GPU, contiguous shards (DESIGN.md section 7) -------------------------

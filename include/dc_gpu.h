@@ -66,6 +66,12 @@ int dc_to_small_device(const void* d_x, long long n, void* d_out, float* min_out
 int dc_med_device(const void* d_x, long long n, float* mean_out, int* type_out);
 /* zlib-compatible CRC-32 of a device byte range. */
 int dc_crc32_device(const void* d_s, long long nbytes, uint32_t* crc_out);
+/* The same, asynchronous on the library stream, result to device memory d_crc (one uint32). */
+int dc_crc32_device_async(const void* d_s, long long nbytes, uint32_t* d_crc);
+/* BER fault injection (CT8/CT9 flow): flip `count` bits of the stream at positions
+ * splitmix64(seed + i) mod nbits (MSB-first in each byte, as bit_flip).  The stream buffer must be
+ * 4-byte aligned and padded to whole words.  Asynchronous. */
+int dc_flip_bits_device(void* d_s, unsigned long long nbits, long long count, unsigned long long seed);
 
 /* CT1 byte-wise codec on device buffers: d_raw (n floats), d_codes (n chars), d_pos1 (n ints) must
  * hold the worst case; *nraw_out = raw count (codes = n - raw).  Synchronous. */

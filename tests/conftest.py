@@ -43,7 +43,13 @@ def gpu_available():
 
 @pytest.fixture(scope="session")
 def dc():
-    """libdcamd on cuda:0 -- must load and initialise on the GPU box (no fallback)."""
+    """libdcamd on cuda:0 -- must load and initialise on the GPU box (no fallback).  torch's HIP
+    runtime is brought up first (tests hand torch device buffers to the library), as bench.py does."""
+    try:
+        import torch
+        torch.zeros(1, device="cuda")
+    except ImportError:
+        pass
     import dcamd
     L = dcamd.Lib()
     L.init(0)

@@ -280,3 +280,58 @@ def test_med_exact_parallel(dc, oracle, kind, n):
     om, ot = oracle.med(x)
     assert np.array_equal(np.float32(mean).view(np.uint32), np.float32(om).view(np.uint32)), (mean, om)
     assert t == ot
+
+
+@pytest.mark.parametrize("ber", [1e-6, 1e-4])
+def test_ct9_ber_flow(dc, oracle, ber):
+    """CT9 (bitmask + CRC) with real bit flips: the sender's CRC-32 of the CT7
+    stream, floor(bits*BER) flipped bits on the received copy (positions of dcamd.flip_positions),
+    the receiver's CRC detects the damage, the retransmitted clean stream passes and decodes exactly
+    like the oracle.  CRC-32 pinned to zlib (= the reference's do_crc32)."""
+    import zlib
+    import torch
+    import dcamd
+    dc.set_bound(1e-3)
+    n = 1 << 20
+    x = oracle.gen_u10(n)
+    _, xs = oracle.to_small(x)
+    t, m17 = oracle.type_mask(xs)
+    dx = torch.from_numpy(xs).cuda()
+    cap = dc.stream_capacity(n)
+    snd = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    rcv = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    crc = torch.zeros(2, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    dc.encode_device(7, dx.data_ptr(), n, snd.data_ptr(), type_=t, mask17=m17)
+    nbits = dc.encode_result()
+    nb = (nbits + 7) // 8
+    dc.crc32_device_async(snd.data_ptr(), nb, crc.data_ptr())
+    dc.synchronize()
+    rcv.copy_(snd)
+    torch.cuda.synchronize()
+    nflip = int(nbits * ber)
+    assert nflip > 0
+    dc.flip_bits_device(rcv.data_ptr(), nbits, nflip, 12345)
+    dc.crc32_device_async(rcv.data_ptr(), nb, crc.data_ptr() + 4)
+    dc.synchronize()
+    clean = snd[:nb].cpu().numpy()
+    got = rcv[:nb].cpu().numpy()
+    want = np.unpackbits(clean)
+    for p in dcamd.flip_positions(nbits, nflip, 12345):
+        want[p] ^= 1
+    assert np.array_equal(got, np.packbits(want))
+    c = crc.cpu().numpy().view(np.uint32)
+    assert c[0] == zlib.crc32(clean.tobytes())
+    assert c[1] == zlib.crc32(got.tobytes())
+    assert c[0] != c[1]                                     # damage detected -> resend
+    rcv.copy_(snd)
+    torch.cuda.synchronize()
+    dc.crc32_device_async(rcv.data_ptr(), nb, crc.data_ptr() + 4)
+    dc.synchronize()
+    c = crc.cpu().numpy().view(np.uint32)
+    assert c[0] == c[1]
+    out = torch.empty(n, dtype=torch.float32, device="cuda")
+    dc.decode_device(7, rcv.data_ptr(), nb, n, out.data_ptr(), type_=t, mask17=m17)
+    dc.decode_finish()
+    ref, _ = oracle.decompress(7, clean, n, 1e-3, t, m17)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
