@@ -253,7 +253,7 @@ __global__ __launch_bounds__(MX_T) void med_exact_kernel(const float* __restrict
 
 // ---------------------------------------------------------------- CRC-32 (zlib)
 constexpr uint32_t CRC_POLY = 0xEDB88320u;
-constexpr int CRC_RUN = 64;                               // bytes per lane
+constexpr int CRC_RUN = 128;                              // bytes per lane (8 x 16-byte loads)
 constexpr int CRC_BLK = CRC_RUN * 256;                    // bytes per workgroup
 
 __device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {     // a*b mod P (reflected)
@@ -277,42 +277,60 @@ __device__ __forceinline__ uint32_t xpow8n(unsigned long long n, const uint32_t*
     return p;
 }
 
+// Raw CRC (init 0, no final xor) of every CRC_BLK block.  Each lane takes a 128-byte run with
+// 16-byte loads and slicing-by-4 tables in LDS (T_k = table of a byte followed by k zero bytes, built
+// on the host from zlib's byte table); CRC is linear over GF(2), so the block value is the XOR of
+// every run's CRC times x^(8 * bytes after it) -- for full blocks a per-lane host constant
+// kpow[j] = x^(8 * CRC_RUN * j), so the combine is one carry-less multiply and an XOR reduction.
 __global__ __launch_bounds__(256) void crc_blocks_kernel(const uint8_t* __restrict__ s, long long nbytes,
                                                          const uint32_t* __restrict__ tab_g,
+                                                         const uint32_t* __restrict__ kpow_g,
                                                          const uint32_t* __restrict__ x2n_g,
                                                          uint32_t* __restrict__ part) {
-    __shared__ uint32_t tab[256];
+    __shared__ uint32_t tab[4][256];
     __shared__ uint32_t x2n[32];
-    __shared__ uint32_t red[256];
-    tab[threadIdx.x] = tab_g[threadIdx.x];
-    if (threadIdx.x < 32) x2n[threadIdx.x] = x2n_g[threadIdx.x];
+    __shared__ uint32_t red[4];
+    const int t = threadIdx.x;
+    for (int k = 0; k < 4; k++) tab[k][t] = tab_g[k * 256 + t];
+    if (t < 32) x2n[t] = x2n_g[t];
+    const uint32_t kfull = kpow_g[255 - t];
     __syncthreads();
+    const bool al = (reinterpret_cast<uintptr_t>(s) & 15u) == 0;
     const long long nblk = (nbytes + CRC_BLK - 1) / CRC_BLK;
     for (long long b = blockIdx.x; b < nblk; b += gridDim.x) {
-        const long long st = b * CRC_BLK + (long long)threadIdx.x * CRC_RUN;
+        const long long st = b * CRC_BLK + (long long)t * CRC_RUN;
         uint32_t r = 0;
-        for (int i = 0; i < CRC_RUN; i++) {               // raw CRC (init 0) of this lane's run
-            const long long p = st + i;
-            if (p < nbytes) r = tab[(r ^ s[p]) & 0xFFu] ^ (r >> 8);
-        }
-        red[threadIdx.x] = r;
-        __syncthreads();
-        for (int w = 1; w < 256; w <<= 1) {               // combine neighbours: left shifted by right's length
-            uint32_t v = 0;
-            const int t = threadIdx.x;
-            const bool act = (t % (2 * w)) == 0;
-            if (act) {
-                const long long rs = b * CRC_BLK + (long long)(t + w) * CRC_RUN;
-                long long rlen = (long long)w * CRC_RUN;
-                if (rs >= nbytes) rlen = 0;
-                else if (rs + rlen > nbytes) rlen = nbytes - rs;
-                v = (rlen ? multmodp(xpow8n((unsigned long long)rlen, x2n), red[t]) : red[t]) ^ red[t + w];
+        if (al && st + CRC_RUN <= nbytes) {
+            const uint4* p4 = reinterpret_cast<const uint4*>(s + st);
+            uint4 q[CRC_RUN / 16];
+#pragma unroll
+            for (int i = 0; i < CRC_RUN / 16; i++) q[i] = p4[i];
+#pragma unroll
+            for (int i = 0; i < CRC_RUN / 16; i++) {
+                const uint32_t w[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const uint32_t c = r ^ w[j];
+                    r = tab[3][c & 0xFFu] ^ tab[2][(c >> 8) & 0xFFu] ^ tab[1][(c >> 16) & 0xFFu] ^ tab[0][c >> 24];
+                }
             }
-            __syncthreads();
-            if (act) red[t] = v;
-            __syncthreads();
+        } else {
+            for (long long p = st; p < st + CRC_RUN && p < nbytes; p++) r = tab[0][(r ^ s[p]) & 0xFFu] ^ (r >> 8);
         }
-        if (threadIdx.x == 0) part[b] = red[0];
+        const long long blen = min((long long)CRC_BLK, nbytes - b * CRC_BLK);
+        uint32_t v;
+        if (blen == CRC_BLK) {
+            v = multmodp(kfull, r);
+        } else {                                          // the last, partial block
+            const long long end = min(st + CRC_RUN, nbytes);
+            const long long after = b * CRC_BLK + blen - max(end, st);
+            v = (r && after > 0) ? multmodp(xpow8n((unsigned long long)after, x2n), r) : r;
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) v ^= __shfl_xor(v, d, 64);
+        if ((t & 63) == 0) red[t >> 6] = v;
+        __syncthreads();
+        if (t == 0) part[b] = red[0] ^ red[1] ^ red[2] ^ red[3];
         __syncthreads();
     }
 }
@@ -422,13 +440,15 @@ extern "C" int dc_launch_med(const float* x, long long n, float* d_mean, int* d_
 }
 
 extern "C" long long dc_crc_parts(long long nbytes) { return (nbytes + CRC_BLK - 1) / CRC_BLK; }
+extern "C" int dc_crc_run_bytes(void) { return CRC_RUN; }
 
 extern "C" int dc_launch_crc32(const uint8_t* s, long long nbytes, const uint32_t* d_tab, const uint32_t* d_x2n,
                                uint32_t* d_parts, uint32_t init, uint32_t* d_out, hipStream_t st) {
     long long nblk = dc_crc_parts(nbytes);
-    if (nbytes > 0) {
+    if (nbytes > 0) {                                     // d_tab: 4 slicing tables, then kpow[256]
         long long g = nblk > 4096 ? 4096 : nblk;
-        hipLaunchKernelGGL(crc_blocks_kernel, dim3((unsigned)g), dim3(256), 0, st, s, nbytes, d_tab, d_x2n, d_parts);
+        hipLaunchKernelGGL(crc_blocks_kernel, dim3((unsigned)g), dim3(256), 0, st, s, nbytes, d_tab, d_tab + 1024,
+                           d_x2n, d_parts);
     }
     hipLaunchKernelGGL(crc_final_kernel, dim3(1), dim3(256), 0, st, d_parts, nbytes, d_x2n, init, d_out);
     return hipGetLastError() == hipSuccess ? 0 : -1;

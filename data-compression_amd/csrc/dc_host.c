@@ -110,6 +110,27 @@ int dc_debug_enc_stamps(unsigned long long* host, long long n) {
     return DC_OK;
 }
 
+/* carry-less a*b mod P (reflected CRC-32) and x^(8n) mod P, as zlib's crc32_combine */
+static uint32_t h_multmodp(uint32_t a, uint32_t b) {
+    uint32_t m = 1u << 31, p = 0;
+    for (int i = 0; i < 32; i++) {
+        if (a & m) p ^= b;
+        m >>= 1;
+        b = (b & 1u) ? (b >> 1) ^ 0xEDB88320u : b >> 1;
+    }
+    return p;
+}
+static uint32_t h_xpow8n(unsigned long long n, const uint32_t* x2n) {
+    uint32_t p = 1u << 31;                          /* x^0 */
+    int k = 3;
+    while (n) {
+        if (n & 1) p = h_multmodp(x2n[k & 31], p);
+        n >>= 1;
+        k++;
+    }
+    return p;
+}
+
 int dc_init(int device) {
     if (G.inited) return DC_OK;
     {   /* run-time override of the compile-time bound, so an unchanged app binary can run at another
@@ -139,23 +160,22 @@ int dc_init(int device) {
     HIPCHK(hipMalloc((void**)&G.d_i, 64));
     HIPCHK(hipMalloc((void**)&G.d_crc, 64));
     HIPCHK(hipMalloc((void**)&G.d_ham, 64));
-    /* CRC tables: byte table and x^(2^k) mod P (reflected), zlib's construction */
-    uint32_t tab[256], x2n[32];
+    /* CRC tables: zlib's byte table T0, slicing tables T1..T3 (a byte followed by k zero bytes),
+     * x^(2^k) mod P (reflected) and kpow[j] = x^(8 * run * j) mod P for the block combine */
+    uint32_t tab[4 * 256 + 256], x2n[32];
     for (uint32_t i = 0; i < 256; i++) {
         uint32_t c = i;
         for (int k = 0; k < 8; k++) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
         tab[i] = c;
     }
+    for (int k = 1; k < 4; k++)
+        for (int i = 0; i < 256; i++) tab[k * 256 + i] = (tab[(k - 1) * 256 + i] >> 8) ^ tab[tab[(k - 1) * 256 + i] & 0xFFu];
     uint32_t p = 1u << 30;                          /* x^1 */
     x2n[0] = p;
-    for (int k = 1; k < 32; k++) {
-        uint32_t a = p, b = p, m = 1u << 31, r = 0;
-        for (int i = 0; i < 32; i++) {
-            if (a & m) r ^= b;
-            m >>= 1;
-            b = (b & 1u) ? (b >> 1) ^ 0xEDB88320u : b >> 1;
-        }
-        x2n[k] = p = r;
+    for (int k = 1; k < 32; k++) x2n[k] = p = h_multmodp(p, p);
+    {
+        const unsigned long long run = (unsigned long long)dc_crc_run_bytes();
+        for (int j = 0; j < 256; j++) tab[1024 + j] = h_xpow8n(run * (unsigned long long)j, x2n);
     }
     HIPCHK(hipMalloc((void**)&G.d_crctab, sizeof tab));
     HIPCHK(hipMalloc((void**)&G.d_x2n, sizeof x2n));

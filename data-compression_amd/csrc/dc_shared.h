@@ -111,6 +111,7 @@ int dc_launch_to_small(const float* x, long long n, float* y, float* part_v, lon
                        dc_hip_stream st);
 int dc_launch_med(const float* x, long long n, float* d_mean, int* d_type, dc_hip_stream st);
 long long dc_crc_parts(long long nbytes);
+int dc_crc_run_bytes(void);
 int dc_launch_crc32(const uint8_t* s, long long nbytes, const uint32_t* d_tab, const uint32_t* d_x2n,
                     uint32_t* d_parts, uint32_t init, uint32_t* d_out, dc_hip_stream st);
 int dc_launch_flip_bits(uint8_t* s, unsigned long long nbits, long long count, unsigned long long seed,
