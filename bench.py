@@ -237,6 +237,10 @@ def main():
         "tile_fix_kernel+tile_scan_kernel": (float(kavg[4]), 0.0),
         f"decode_kernel_fast<{ct}>": (float(kavg[5]), nbytes + 4.0 * n),
     }
+    if kavg[0] < 1e-3 and kavg[1] < 1e-3:             # single-pass encoder: one fused launch
+        kernels.pop(f"encode_count_kernel<{ct}>")
+        kernels.pop("encode_scan_kernel")
+        kernels[f"encode_fused_kernel<{ct}>"] = kernels.pop(f"encode_write_kernel<{ct}>")
 
     ok = None
     if args.check and rank == 0:

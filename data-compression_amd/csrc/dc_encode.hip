@@ -384,6 +384,232 @@ __global__ __launch_bounds__(ENC_TPB) void encode_write_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------
+// Single-pass encoder: encode_write_kernel's tile work with the tile offset from a decoupled
+// look-back instead of the count + scan launches.  A tile publishes its bit count as soon as its
+// workgroup scan is done (flag status 1), packs its tokens into LDS at a tile-relative offset (bit 0
+// of buffer word 1; word 0 stays zero), and only then looks back: wave 0 reads the flags of the 64
+// preceding tiles at once, adds the counts up to the nearest inclusive prefix (status 2) and moves
+// 64 tiles further back if there is none.  Tiles are claimed in increasing order from an atomic
+// counter, so every predecessor is running or done (no deadlock).  The tile publishes its inclusive
+// prefix, then stores its owned words shifted into place with v_alignbit (G mod 32).
+// flags[t] = status << 62 | (epoch mod 2^22) << 40 | value (40 bits)
+__device__ __forceinline__ uint64_t eflag(uint64_t st, uint32_t epoch, unsigned long long v) {
+    return (st << 62) | ((uint64_t)(epoch & 0x3FFFFFu) << 40) | (v & 0xFFFFFFFFFFull);
+}
+
+constexpr int FBUF = (STG_WORDS > ENC_LDS_WORDS ? STG_WORDS : ENC_LDS_WORDS) + 1;
+
+// tile work up to the packed bits: stage, tokens, workgroup scan, head tokens, publish the count
+// (flag status 1, tile 0: inclusive), pack at the tile-relative offset into buf (buf[0] = 0).
+// Returns the tile's bit count T.
+template <int CT>
+__device__ __forceinline__ uint32_t fused_compute(const float* __restrict__ x, long long n, long long idx0, const Params& P,
+                                                  uint64_t* __restrict__ flags, uint32_t epoch, int start_bit,
+                                                  unsigned tile, uint32_t* buf, uint32_t* s_wsum, uint32_t* s_head_val,
+                                                  int* s_head_len, bool& neg1) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const long long tbase = (long long)tile * ENC_TILE;
+    const long long base = tbase + (long long)tid * ENC_K;
+    const bool full = tbase + ENC_TILE <= n && idx0 + tbase >= 3;
+    float h0 = 0.0f, h1 = 0.0f, h2 = 0.0f, h3 = 0.0f;
+    const bool hin = wid == 1 && lane < 11 && tbase + ENC_TILE + lane < n;
+    if (hin) {
+        const long long e = tbase + ENC_TILE + lane;
+        h0 = x[e]; h1 = x[e - 1]; h2 = x[e - 2]; h3 = x[e - 3];
+    }
+    {
+        float4 f[ENC_Q];
+        load_tile4(x, n, tbase, tid, f);
+#pragma unroll
+        for (int q = 0; q < ENC_Q; q++) {
+            const int e = 4 * (tid + ENC_TPB * q);
+            float* d = reinterpret_cast<float*>(buf) + 8 + e + (e >> 4);
+            d[0] = f[q].x; d[1] = f[q].y; d[2] = f[q].z; d[3] = f[q].w;
+        }
+        if (tid < 3) reinterpret_cast<float*>(buf)[5 + tid] = halo_x(x, idx0, tbase - 3 + tid);
+    }
+    __syncthreads();
+    float v[ENC_K + 4];
+#pragma unroll
+    for (int j = 1; j < ENC_K + 4; j++) {
+        const int e = tid * ENC_K + j - 4;
+        v[j] = reinterpret_cast<const float*>(buf)[e < 0 ? 8 + e : 8 + e + (e >> 4)];
+    }
+    __syncthreads();
+    for (int i = tid; i < FBUF; i += ENC_TPB) buf[i] = 0u;
+
+    uint32_t tv[ENC_K];
+    uint32_t tlp[ENC_K / 4];
+#pragma unroll
+    for (int q = 0; q < ENC_K / 4; q++) tlp[q] = 0u;
+    uint32_t mysum = 0;
+    if (full) {
+#pragma unroll
+        for (int j = 0; j < ENC_K; j++) {
+            int len;
+            make_token_bf<CT>(v[4 + j], v[3 + j], v[2 + j], v[1 + j], true, P, tv[j], len);
+            tlp[j >> 2] |= (uint32_t)len << (8 * (j & 3));
+            mysum += (uint32_t)len;
+            neg1 |= v[4 + j] == -1.0f;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < ENC_K; j++) {
+            int len;
+            make_token_bf<CT>(v[4 + j], v[3 + j], v[2 + j], v[1 + j], idx0 + base + j >= 3, P, tv[j], len);
+            len = base + j < n ? len : 0;
+            tv[j] = len ? tv[j] : 0u;
+            tlp[j >> 2] |= (uint32_t)len << (8 * (j & 3));
+            mysum += (uint32_t)len;
+            neg1 |= base + j < n && v[4 + j] == -1.0f;
+        }
+    }
+    uint32_t inc = mysum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += t;
+    }
+    if (lane == 63) s_wsum[wid] = inc;
+    if (wid == 1 && lane < 12) {
+        uint32_t hv = 0u; int hl = 0;
+        if (lane < 11 && hin) make_token<CT>(h0, h1, h2, h3, idx0 + tbase + ENC_TILE + lane >= 3, P, hv, hl);
+        s_head_val[lane] = hv;
+        s_head_len[lane] = hl;
+    }
+    __syncthreads();
+    uint32_t wpre = 0, T = 0;
+#pragma unroll
+    for (int w = 0; w < ENC_TPB / 64; w++) {
+        if (w < wid) wpre += s_wsum[w];
+        T += s_wsum[w];
+    }
+    if (tid == 0)                                                    // publish the count early
+        st_relaxed(&flags[tile], tile == 0 ? eflag(2, epoch, (unsigned long long)start_bit + T) : eflag(1, epoch, T));
+    uint32_t* bb = buf + 1;                                          // tile bit 0 = MSB of buf[1]
+    {
+        uint32_t off = wpre + inc - mysum;
+#pragma unroll
+        for (int j = 0; j < ENC_K; j++) {
+            const int len = (int)((tlp[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+            const uint64_t vv = (uint64_t)tv[j] << ((64 - (int)(off & 31u) - len) & 63);
+            uint32_t* d = bb + (off >> 5);
+            atomicOr(d, (uint32_t)(vv >> 32));
+            atomicOr(d + 1, (uint32_t)vv);
+            off += (uint32_t)len;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t ho = T;
+        for (int j = 0; j < 11 && s_head_len[j]; j++) {
+            if (ho - T >= 32u) break;
+            lds_place(bb, ho, s_head_val[j], s_head_len[j]);
+            ho += (uint32_t)s_head_len[j];
+        }
+    }
+    __syncthreads();
+    return T;
+}
+
+// look-back for the tile's exclusive prefix G (wave 0), publish the inclusive prefix, store the owned
+// words of buf shifted into place
+__device__ __forceinline__ void fused_finish(uint32_t* __restrict__ out, uint64_t* __restrict__ flags, uint32_t epoch,
+                                             int start_bit, unsigned tile, unsigned ntiles, uint32_t T, const uint32_t* buf,
+                                             unsigned long long* __restrict__ total_bits, unsigned* __restrict__ err,
+                                             unsigned long long* s_G) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (wid == 0) {
+        unsigned long long G = (unsigned long long)start_bit;
+        if (tile > 0) {
+            unsigned long long acc = 0;
+            long long k = (long long)tile - 1;
+            unsigned spins = 0;
+            while (true) {
+                const long long q = k - lane;
+                const uint64_t fv = q >= 0 ? ld_relaxed(&flags[q]) : eflag(2, epoch, 0);
+                const bool mine = ((fv >> 40) & 0x3FFFFFu) == (epoch & 0x3FFFFFu);
+                const int stt = mine ? (int)(fv >> 62) : 0;
+                const unsigned long long incl = __ballot(stt == 2);
+                const int fi = incl ? __ffsll((long long)incl) - 1 : 64;
+                const unsigned long long need = fi == 64 ? ~0ull : ((2ull << fi) - 1ull);
+                if (__ballot(stt == 0) & need) {                     // a predecessor has not published yet
+                    if (++spins > (1u << 22)) { if (lane == 0) atomicOr(err, 4u); break; }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                unsigned long long val = (lane <= fi) ? (fv & 0xFFFFFFFFFFull) : 0ull;
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) val += __shfl_xor(val, d, 64);
+                acc += val;
+                if (fi < 64) break;
+                k -= 64;
+            }
+            G = acc;
+        }
+        if (lane == 0) {
+            *s_G = G;
+            if (tile > 0) st_relaxed(&flags[tile], eflag(2, epoch, G + T));
+            if (tile == ntiles - 1) *total_bits = G + T;
+        }
+    }
+    __syncthreads();
+    const unsigned long long G = *s_G;
+    const int sh = (int)(G & 31ull);
+    const long long wb = (long long)(G >> 5);
+    long long w0 = (long long)((G + 31) >> 5);
+    if (tile == 0) w0 = 0;
+    const long long w1 = (long long)((G + T + 31) >> 5);
+    for (long long w = w0 + tid; w < w1; w += ENC_TPB) {
+        const long long i = w - wb;
+        const uint32_t val = sh ? __builtin_amdgcn_alignbit(buf[i], buf[i + 1], (uint32_t)sh) : buf[i + 1];
+        out[w] = __builtin_bswap32(val);
+    }
+}
+
+// Tiles are software-pipelined: the workgroup computes and packs tile t+1 into its second buffer
+// before it looks back for tile t, so the look-back latency overlaps the next tile's work.
+template <int CT>
+__global__ __launch_bounds__(ENC_TPB) void encode_fused_kernel(
+    const float* __restrict__ x, long long n, long long idx0, Params P, uint32_t* __restrict__ out,
+    uint64_t* __restrict__ flags, unsigned* __restrict__ ctr, uint32_t epoch, int start_bit, unsigned ntiles,
+    unsigned long long* __restrict__ total_bits, unsigned* __restrict__ err) {
+    __shared__ uint32_t s_buf[2][FBUF];
+    __shared__ uint32_t s_wsum[ENC_TPB / 64];
+    __shared__ uint32_t s_head_val[12];
+    __shared__ int s_head_len[12];
+    __shared__ unsigned s_tile;
+    __shared__ unsigned long long s_G;
+    const int tid = threadIdx.x, lane = tid & 63;
+    bool neg1 = false;
+    if (tid == 0) s_tile = atomicAdd(&ctr[0], 1u);
+    __syncthreads();
+    unsigned cur = s_tile;
+    int cb = 0;
+    uint32_t Tcur = 0;
+    if (cur < ntiles) Tcur = fused_compute<CT>(x, n, idx0, P, flags, epoch, start_bit, cur, s_buf[0], s_wsum, s_head_val,
+                                               s_head_len, neg1);
+    while (cur < ntiles) {
+        __syncthreads();
+        if (tid == 0) s_tile = atomicAdd(&ctr[0], 1u);
+        __syncthreads();
+        const unsigned nxt = s_tile;
+        uint32_t Tn = 0;
+        if (nxt < ntiles) Tn = fused_compute<CT>(x, n, idx0, P, flags, epoch, start_bit, nxt, s_buf[cb ^ 1], s_wsum,
+                                                 s_head_val, s_head_len, neg1);
+        fused_finish(out, flags, epoch, start_bit, cur, ntiles, Tcur, s_buf[cb], total_bits, err, &s_G);
+        cur = nxt;
+        Tcur = Tn;
+        cb ^= 1;
+    }
+    if (CT != 6 && __any(neg1) && lane == 0) atomicOr(err, 1u);      // -1.0f is the reference's sentinel
+    if (tid == 0) {
+        __threadfence();
+        if (atomicAdd(&ctr[1], 1u) == gridDim.x - 1) { atomicExch(&ctr[0], 0u); atomicExch(&ctr[1], 0u); }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 #define DC_ENC_DISPATCH(KER, ...)                                                                  \
     switch (P->ct) {                                                                               \
         case 5: hipLaunchKernelGGL(KER<5>, __VA_ARGS__); break;                                    \
@@ -408,14 +634,41 @@ static unsigned write_grid(int ct) {
     return cache[ci];
 }
 
+static unsigned fused_grid(int ct) {
+    static unsigned cache[12];
+    const int ci = (ct > 0 && ct < 12) ? ct : 0;
+    if (cache[ci]) return cache[ci];
+    int dev = 0, ncu = 256, per = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const void* f = ct == 5 ? (const void*)encode_fused_kernel<5> : ct == 6 ? (const void*)encode_fused_kernel<6>
+                  : ct == 7 ? (const void*)encode_fused_kernel<7> : (const void*)encode_fused_kernel<11>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, ENC_TPB, 0) != hipSuccess || per < 1) per = 1;
+    cache[ci] = (unsigned)(per * ncu);
+    return cache[ci];
+}
+
 extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, const Params* P,
                                 uint32_t* out, uint64_t* desc, unsigned* tile_ctr, uint32_t epoch,
                                 int start_bit, unsigned long long* total_bits, unsigned* err,
                                 unsigned long long* dbg, hipStream_t stream) {
-    (void)tile_ctr;
-    (void)epoch;
     if (n <= 0) return 0;
     const unsigned ntiles = (unsigned)((n + ENC_TILE - 1) / ENC_TILE);
+    // single pass (decoupled look-back, software-pipelined tiles): measured 284 us against 257 us for
+    // count + scan + write at 2^26 U10 (the write kernel re-reads its tiles from the Infinity Cache
+    // and hides their latency across 65536 count workgroups); kept as an option, DC_ENC_FUSED=1
+    static int fused = -1;
+    if (fused < 0) fused = getenv("DC_ENC_FUSED") ? 1 : 0;
+    if (fused && !dbg) {
+        const unsigned gf = std::min<unsigned>(ntiles, fused_grid(P->ct));
+        dc_mark_phase(0, stream);
+        dc_mark_phase(1, stream);
+        dc_mark_phase(2, stream);
+        DC_ENC_DISPATCH(encode_fused_kernel, dim3(gf), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, desc, tile_ctr,
+                        epoch, start_bit, ntiles, total_bits, err);
+        dc_mark_phase(3, stream);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     uint32_t* tbits = reinterpret_cast<uint32_t*>(desc + ntiles);     // tile counts; desc: dc_encode_desc_words(n)
     dc_mark_phase(0, stream);
     // count: one workgroup per tile (a persistent count grid with prefetch measured slower)

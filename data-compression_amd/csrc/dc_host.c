@@ -283,7 +283,7 @@ int dc_encode_device(int ct, const void* d_x, long long n, long long idx0, int t
         G.enc_desc_cap = cap;
         G.enc_epoch = 1;
     }
-    if (++G.enc_epoch >= (1u << 24)) {
+    if (++G.enc_epoch >= (1u << 22)) {          /* flags carry 22 epoch bits */
         HIPCHK(hipMemsetAsync(G.enc_desc, 0, G.enc_desc_cap * sizeof(uint64_t), G.st));
         G.enc_epoch = 1;
     }
