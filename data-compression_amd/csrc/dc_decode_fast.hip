@@ -43,6 +43,14 @@ constexpr int LWORDS = padw(GROUP * LROW + 8);  // + the words after the tile
 constexpr int OV = DC_OV;                       // overlap: P_c starts OV bits before its chunk
 constexpr int OVW = OV / 32;
 constexpr int PWORDS = padw(GROUP * LROW + 8 + OVW);
+#ifndef DC_PARSE_LUT
+#define DC_PARSE_LUT 1
+#endif
+#if DC_PARSE_LUT
+#define PLEN(t) ((int)S.tl[(t) >> 23])
+#else
+#define PLEN(t) token_len_bf<CT>((t), P)
+#endif
 constexpr int KMAX = 2;                        // extra known entries per chunk (besides P_c's own)
 constexpr int RMAX = 12;                       // closure rounds inside a tile
 constexpr int CW = CHUNK_BITS / 32;            // words per chunk
@@ -223,19 +231,19 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
             Rd r;
             r.init(S.L, gc == 0 ? cs : cs - OV);
             const unsigned long long q0 = D.dbg ? __builtin_amdgcn_s_memtime() : 0;
-            while (r.pos < cs) { r.fetch(S.L); r.step(S.tl[r.peek() >> 23]); }
+            while (r.pos < cs) { r.fetch(S.L); r.step(PLEN(r.peek())); }
             if (D.dbg && t < 4096 && (c & 63) == 0)                  // per-wave cycles (diagnostic)
                 D.dbg[t * 16 + 12 + (c >> 6)] = (__builtin_amdgcn_s_memtime() - q0) << 16;
             const int pend = min(cs + 32, cend);                      // boundaries in the first word
             while (r.pos < pend) {
                 r.fetch(S.L);
                 pm |= 1u << (r.pos - cs);
-                r.step(S.tl[r.peek() >> 23]);
+                r.step(PLEN(r.peek()));
                 n++;
             }
             while (r.pos < cend) {
                 r.fetch(S.L);
-                r.step(S.tl[r.peek() >> 23]);
+                r.step(PLEN(r.peek()));
                 n++;
             }
             const int xx = r.pos - (cs + CHUNK_BITS);
