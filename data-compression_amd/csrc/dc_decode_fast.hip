@@ -564,6 +564,43 @@ __device__ __forceinline__ void flush_ring(const float* ring, float* outk, int r
     }
 }
 
+// Phase-B flushes with the global stores one flush behind the LDS reads: the sector read at flush k
+// sits in registers and leaves at flush k+1, so no flush waits on its own LDS read.
+struct PendSector {
+    float4 a, b;
+    int s0;
+    bool have;
+};
+__device__ __forceinline__ void pend_store(PendSector& p, float* outk, int lim) {
+    if (!p.have) return;
+    if (p.s0 + SECT <= lim) {
+        float4* o4 = reinterpret_cast<float4*>(outk + p.s0);
+        o4[0] = p.a;
+        o4[1] = p.b;
+    } else {
+        const float v[8] = {p.a.x, p.a.y, p.a.z, p.a.w, p.b.x, p.b.y, p.b.z, p.b.w};
+        for (int i = 0; i < SECT && p.s0 + i < lim; i++) outk[p.s0 + i] = v[i];
+    }
+    p.have = false;
+}
+__device__ __forceinline__ void flush_ring_deferred(const float* ring, float* outk, int r0, int& fl, int j, bool& hdone,
+                                                    int lim, PendSector& p) {
+    if (!hdone && j >= fl) {
+        for (int ii = 0; ii < fl; ii++)
+            if (ii < lim) outk[ii] = ring[(ii + r0) & (RING - 1)];
+        hdone = true;
+    }
+    if (fl + SECT <= j) {
+        pend_store(p, outk, lim);
+        const float4* r4 = reinterpret_cast<const float4*>(ring + ((fl + r0) & (RING - 1)));
+        p.a = r4[0];
+        p.b = r4[1];
+        p.s0 = fl;
+        p.have = true;
+        fl += SECT;
+    }
+}
+
 struct DecodeShared {
     uint32_t L[LWORDS];
     TokLut T;                                      // token length / pattern tables (build_lut)
@@ -686,6 +723,9 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
             // negative mask with 23 kept mantissa bits: patterns without a midpoint bit).
             const bool chk_all = (CT == 6 && P.B >= 23) || (CT == 7 && (P.mask17 >> 16) != 0u && P.mm == 23);
             int sentv = 0;
+            PendSector ps;
+            ps.have = false;
+            ps.s0 = 0;
             while (__any(r.pos < cend)) {
 #pragma unroll
                 for (int u = 0; u < SECT; u++) {
@@ -712,8 +752,9 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
                     r.step(on ? (int)(meta >> 8) : 0);
                     j += on ? 1 : 0;
                 }
-                flush_ring(ring, outk, r0, fl, j, hdone, lim);
+                flush_ring_deferred(ring, outk, r0, fl, j, hdone, lim, ps);
             }
+            pend_store(ps, outk, lim);
             sent |= sentv != 0;
             flush_ring(ring, outk, r0, fl, j, hdone, lim);
             const int t0 = hdone ? fl : 0;                           // tail, or a chunk inside one sector
