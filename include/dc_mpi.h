@@ -1,0 +1,38 @@
+/*
+ * dc_mpi.h -- float MPI send/recv wrappers of libdcamd_mpi.so (data-compression_amd/csrc/dc_mpi.c).
+ *
+ * Float counterparts of the reference's MPI_Send_bitwise_double / MPI_Recv_bitwise_double
+ * (impl/dataCompression.h:57-62, impl/dataCompression.c:226-353): same argument list, one MPI_CHAR
+ * message framed [int bytes][float min][stream] (CT7: [int bytes][float min][int type][char mask[17]]
+ * [stream]); the receiver decodes into buf and adds min back.  The codec runs on the MI355X.
+ * Include after <mpi.h>.
+ */
+#ifndef DC_MPI_H
+#define DC_MPI_H
+#include <mpi.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* CT5: zero / 3-predictor / raw tokens (myCompress_bitwise) */
+int MPI_Send_bitwise_float(const void* buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm);
+int MPI_Recv_bitwise_float(void* buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
+                           MPI_Status* status);
+/* CT6: raw tokens only (myCompress_bitwise_np) */
+int MPI_Send_bitwise_float_np(const void* buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm);
+int MPI_Recv_bitwise_float_np(void* buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
+                              MPI_Status* status);
+/* CT11: 3-bit codes or verbatim floats (myCompress_bitwise_op) */
+int MPI_Send_bitwise_float_op(const void* buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm);
+int MPI_Recv_bitwise_float_op(void* buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
+                              MPI_Status* status);
+/* CT7: bitmask tokens, type / mask from med_dataset_float of the shifted data (impl/pingpong.c:198-206) */
+int MPI_Send_bitwise_float_mask(const void* buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm);
+int MPI_Recv_bitwise_float_mask(void* buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
+                                MPI_Status* status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
