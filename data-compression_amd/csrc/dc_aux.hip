@@ -454,6 +454,33 @@ extern "C" int dc_launch_crc32(const uint8_t* s, long long nbytes, const uint32_
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// Shard stream: bits [start_bit, start_bit + 8*nout) of s as nout bytes starting at bit 0 (MSB first),
+// so a shard of a global stream decodes like a stream of its own (dc_decode_shard_device).
+__global__ __launch_bounds__(256) void bit_shift_copy_kernel(const uint8_t* __restrict__ s, long long sbytes,
+                                                             unsigned long long start_bit, unsigned long long nbits,
+                                                             uint8_t* __restrict__ d, long long nout) {
+    const long long b0 = (long long)(start_bit >> 3);
+    const int sh = (int)(start_bit & 7);
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nout; i += (long long)gridDim.x * 256) {
+        const long long a = b0 + i;
+        const uint32_t hi = a < sbytes ? s[a] : 0u, lo = a + 1 < sbytes ? s[a + 1] : 0u;
+        uint32_t v = (((hi << 8 | lo) << sh) >> 8) & 0xFFu;
+        const long long rem = (long long)nbits - 8 * i;                  // bits after the shard are zero
+        if (rem <= 0) v = 0;
+        else if (rem < 8) v &= (0xFFu << (8 - rem)) & 0xFFu;
+        d[i] = (uint8_t)v;
+    }
+}
+
+extern "C" int dc_launch_bit_shift_copy(const uint8_t* s, long long sbytes, unsigned long long start_bit,
+                                        unsigned long long nbits, uint8_t* d, long long nout, hipStream_t st) {
+    if (nout <= 0) return 0;
+    long long g = (nout + 255) / 256;
+    if (g > 8192) g = 8192;
+    hipLaunchKernelGGL(bit_shift_copy_kernel, dim3((unsigned)g), dim3(256), 0, st, s, sbytes, start_bit, nbits, d, nout);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // BER fault injection for the CT8/CT9 flow: flip `count` stream bits at the
 // positions splitmix64(seed + i) mod nbits, MSB-first within each byte like bit_flip (:5858-5865).
 // The reference's own pingpong CT9 path only *simulates* a CRC failure (impl/pingpong.c:421-430);

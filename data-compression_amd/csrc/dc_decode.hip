@@ -368,12 +368,12 @@ __global__ __launch_bounds__(256) void decode_kernel(const uint8_t* __restrict__
 // 6. re-decode pending prefixes whose three preceding values are final
 template <int CT>
 __device__ bool fix_chunk(const uint8_t* s, const Params& P, const DecBufs& D, const Plan& pl, long long c,
-                          float* out, long long num, int it, bool serial) {
+                          float* out, long long num, int it, bool serial, const float* hin = nullptr) {
     const unsigned long long k0 = D.tokoff[c];
     float h[3];
     for (int q = 0; q < 3; q++) {
         const long long idx = (long long)k0 - 1 - q;
-        if (idx < 0) { h[q] = -1.0f; continue; }
+        if (idx < 0) { h[q] = hin ? hin[-1 - idx] : -1.0f; continue; }   // before a shard: its incoming b1..b3
         if (idx >= num) { h[q] = 0.0f; continue; }
         long long d = c - 1;
         while (d > 0 && (long long)D.tokoff[d] > idx) d--;
@@ -422,6 +422,20 @@ __global__ void fixup_serial_kernel(const uint8_t* __restrict__ s, Params P, Dec
     for (long long c = 0; c < pl.nchunks; c++) {
         if (D.pend[c] == 0 || D.done[c] != 0 || D.entry[c] == UNK) continue;
         fix_chunk<CT>(s, P, D, pl, c, out, num, 0x7FFF, true);
+        D.done[c] = 0x7FFF;
+    }
+}
+
+// a shard's deferred prefixes (dc_decode_shard_fix): chunks [0, nc) in order, the values before the
+// shard from hin (b1, b2, b3)
+template <int CT>
+__global__ void shard_fix_kernel(const uint8_t* __restrict__ s, Params P, DecBufs D, float* __restrict__ out,
+                                 long long num, long long nc, const float* __restrict__ hin) {
+    const Plan pl = *D.plan;
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    for (long long c = 0; c < pl.nchunks && c < nc; c++) {
+        if (D.pend[c] == 0 || D.done[c] != 0 || D.entry[c] == UNK) continue;
+        fix_chunk<CT>(s, P, D, pl, c, out, num, 0x7FFF, true, hin);
         D.done[c] = 0x7FFF;
     }
 }
@@ -476,6 +490,12 @@ extern "C" int dc_launch_decode_more(const uint8_t* s, long long max_chunks, con
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+extern "C" int dc_launch_shard_fix(const uint8_t* s, const Params* P, const DecBufs* D, float* out, long long num,
+                                   long long nchunks, const float* hin, hipStream_t st) {
+    DC_DISPATCH(P->ct, shard_fix_kernel, dim3(1), dim3(64), 0, st, s, *P, *D, out, num, nchunks, hin);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int dc_launch_fixup_serial(const uint8_t* s, const Params* P, const DecBufs* D, float* out,
                                       long long num, hipStream_t st) {
     DC_DISPATCH(P->ct, fixup_serial_kernel, dim3(1), dim3(64), 0, st, s, *P, *D, out, num);
@@ -496,6 +516,7 @@ __global__ void decode_serial_kernel(const uint8_t* s, Params P, DecBufs D, floa
     BitReader r;
     r.init(s, pl.nbytes, 0);
     float b1 = -1.0f, b2 = -1.0f, b3 = -1.0f;
+    if (D.shard == 2 && D.hin) { b1 = D.hin[0]; b2 = D.hin[1]; b3 = D.hin[2]; }   // a shard's incoming values
     long long n = 0;
     while (n < num && r.pos < nbits) {
         const uint32_t tk = r.peek();

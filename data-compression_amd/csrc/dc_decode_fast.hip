@@ -612,7 +612,7 @@ struct DecodeShared {
         } k;
     } u;
     float tin[3];
-    int need, cplx;
+    int need, cplx, defer;
     long long tile;
 };
 
@@ -644,7 +644,7 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
         const bool act = c < nact;
         const int cs = c * CHUNK_BITS;
         const int cend = (int)min((long long)(cs + CHUNK_BITS), rem);
-        if (c == 0) { S.need = 0; S.cplx = 0; }
+        if (c == 0) { S.need = 0; S.cplx = 0; S.defer = 0; }
         // ---- entry and first token index of every chunk (parse kernel chain + tile_fix overrides)
         const uint32_t te = D.tentry[t];
         const int ein = (int)(te & 63), c0 = (int)((te >> 6) & 1023), kjoin = (int)(te >> 16);
@@ -668,7 +668,7 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
         STAMP(9);
 
         // ---- pass 1: decode from the true entry; concrete values are stored immediately
-        const bool first = (gc == 0);
+        const bool first = (gc == 0) && D.shard == 0;    // a shard's first chunk has symbolic history
         float f1 = -1.0f, f2 = -1.0f, f3 = -1.0f;
         int k1 = first ? 0 : 1, k2 = first ? 0 : 2, k3 = first ? 0 : 3;
         int pend = 0;
@@ -846,18 +846,28 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
                 if (++spins > (1u << 24)) { bad = true; atomicOr(D.err, 16u); break; }
                 __builtin_amdgcn_s_sleep(1);
             }
+            if (k < 0 && !bad) {                             // before the stream: a shard's incoming values
+                if (D.shard == 2) val = D.hin[j];
+                else if (D.shard == 1) S.defer = 1;
+            }
             if (bad) atomicOr(D.err, 32u);
             S.tin[c] = val;
         }
         __syncthreads();
+        const bool defer = need && S.defer;                  // incoming values unknown yet (shard, mode 1)
         if (need && c == 0 && !(tk0 == 0 && tk1 == 0 && tk2 == 0)) {
             const int kk[3] = {tk0, tk1, tk2};
             for (int i = 0; i < 3; i++)
                 st_relaxed(&D.hist[t * 6 + 3 + i],
-                           hpack(2, epoch, 0, kk[i] == 0 ? S.u.k.fv[i][GROUP - 1] : S.tin[kk[i] - 1]));
+                           defer ? hpack(2, epoch, 4, 0.0f)
+                                 : hpack(2, epoch, 0, kk[i] == 0 ? S.u.k.fv[i][GROUP - 1] : S.tin[kk[i] - 1]));
         }
+        // deferred: prefixes that depend on the shard's incoming values wait for dc_decode_shard_fix
+        const bool dchunk = defer && act && pend > 0 &&
+                            ((ik[0] >= 1 && ik[0] <= 3) || (ik[1] >= 1 && ik[1] <= 3) || (ik[2] >= 1 && ik[2] <= 3));
+        if (dchunk) atomicOr(D.err, 256u);
         // ---- fix-up: re-decode the pending prefix with concrete history
-        if (act && pend > 0) {
+        if (act && pend > 0 && !dchunk) {
             float g1 = ik[0] == 0 ? iv[0] : S.tin[ik[0] - 1];
             float g2 = ik[1] == 0 ? iv[1] : S.tin[ik[1] - 1];
             float g3 = ik[2] == 0 ? iv[2] : S.tin[ik[2] - 1];
@@ -882,7 +892,7 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
                 r.step(len);
             }
         }
-        if (act) { D.pend[gc] = (uint16_t)min(pend, 65535); D.done[gc] = pend ? 1 : 0; }
+        if (act) { D.pend[gc] = (uint16_t)min(pend, 65535); D.done[gc] = (pend && !dchunk) ? 1 : 0; }
         if (sent) atomicOr(D.err, 128u);
         __syncthreads();
         STAMP(11);

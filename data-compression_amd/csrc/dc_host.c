@@ -51,6 +51,10 @@ typedef struct {
     float* dec_out;
     long long dec_num;
     unsigned long long dec_nbits;
+    int dec_shard;                   /* shard mode of the pending decode (DecBufs.shard) */
+    const float* dec_hin;            /* its incoming values (shard mode 2) */
+    int shard_deferred;              /* 1: tile-0 prefixes wait for dc_decode_shard_fix, 2: later tiles too */
+    void* shard_buf; size_t shard_cap;
     /* pinned host scratch */
     unsigned long long* h_scratch;   /* [0] total bits [1] err [2..] misc */
     /* staging for the host-pointer ABI */
@@ -447,6 +451,7 @@ int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsig
                               (float*)d_out, num, G.dec_epoch, G.st))
         return seterr(DC_ERR_HIP, "decode launch failed: %s", hipGetErrorString(hipGetLastError()));
     G.dec_pending = 1;
+    G.dec_shard = G.D.shard;
     G.dec_P = P;
     G.dec_s = (const uint8_t*)d_stream;
     G.dec_max_chunks = max_chunks;
@@ -470,8 +475,28 @@ int dc_decode_finish(void) {
     unsigned err = 0;
     rc = read_dec_err(&err);
     if (rc) return rc;
+    G.shard_deferred = 0;
+    if (G.dec_shard == 1 && (err & (256u | 32u))) {  /* shard prefixes waiting for their incoming values */
+        G.shard_deferred = (err & 32u) ? 2 : 1;
+        err &= ~(256u | 32u);
+        HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
+    }
     if (!err) { G.dec_pending = 0; return DC_OK; }
     if (getenv("DC_DEBUG_ERR")) fprintf(stderr, "[dcamd] fast decode status 0x%x\n", err);
+    if (G.dec_shard && (err & (8u | 64u | 128u | 16u))) {
+        /* a shard outside the fast path (e.g. a locally periodic stream): exact sequential decode of the
+         * shard from its incoming values -- now, or in dc_decode_shard_fix when they come later */
+        HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
+        G.dec_pending = 0;
+        if (G.dec_shard == 1) { G.shard_deferred = 3; return DC_OK; }
+        DecBufs D = G.D;
+        D.shard = 2;
+        D.hin = G.dec_hin;
+        if (dc_launch_decode_serial(G.dec_s, &G.dec_P, &D, G.dec_out, G.dec_num, G.st))
+            return seterr(DC_ERR_HIP, "decode launch failed");
+        HIPCHK(hipStreamSynchronize(G.st));
+        return DC_OK;
+    }
     if ((err & (8u | 64u)) && !(err & (16u | 128u)) && G.dec_pending) {
         /* outside the fast path's assumptions: exact multi-kernel path (closure rounds, then
          * complete entry maps for every chunk if an entry is still unresolved) */
@@ -494,7 +519,10 @@ int dc_decode_finish(void) {
     }
     if ((err & 32u) && !(err & (8u | 16u | 128u)) && G.dec_pending) {
         HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
-        if (dc_launch_fixup_serial(G.dec_s, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.st))
+        if (G.dec_shard == 2) {                      /* a shard with known incoming values */
+            if (dc_launch_shard_fix(G.dec_s, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.dec_max_chunks, G.dec_hin, G.st))
+                return seterr(DC_ERR_HIP, "decode launch failed");
+        } else if (dc_launch_fixup_serial(G.dec_s, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.st))
             return seterr(DC_ERR_HIP, "decode launch failed");
         rc = read_dec_err(&err);
         if (rc) return rc;
@@ -517,6 +545,47 @@ int dc_decode_finish(void) {
     HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
     if (err) return seterr(DC_ERR_STREAM, "decoder status 0x%x (8: unresolved entry, 16: look-back timeout, "
                                           "32: prediction chain)", err);
+    return DC_OK;
+}
+
+/* ---- shards of one global stream: decode tokens [start_bit, start_bit + nbits) ------ */
+int dc_decode_shard_device(int ct, const void* d_stream, long long stream_bytes, unsigned long long start_bit,
+                           unsigned long long nbits, long long num, int type, uint32_t mask17, const float* d_hin,
+                           void* d_out) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    const long long nb = (long long)((nbits + 7) / 8);
+    if (grow(&G.shard_buf, &G.shard_cap, (size_t)nb + 64)) return DC_ERR_HIP;
+    if (dc_launch_bit_shift_copy((const uint8_t*)d_stream, stream_bytes, start_bit, nbits, (uint8_t*)G.shard_buf, nb + 8,
+                                 G.st))
+        return seterr(DC_ERR_HIP, "shard copy launch failed");
+    G.D.shard = d_hin ? 2 : 1;
+    G.D.hin = d_hin;
+    rc = dc_decode_device(ct, G.shard_buf, nb, NULL, nb, num, type, mask17, d_out);
+    G.dec_shard = G.D.shard;
+    G.dec_hin = d_hin;
+    G.D.shard = 0;
+    G.D.hin = NULL;
+    return rc;
+}
+
+int dc_decode_shard_fix(const float* d_hin) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (!G.shard_deferred) return DC_OK;
+    DecBufs D = G.D;
+    D.shard = 2;
+    D.hin = d_hin;
+    if (G.shard_deferred == 3) {                    /* exact sequential decode of the whole shard */
+        if (dc_launch_decode_serial(G.dec_s, &G.dec_P, &D, G.dec_out, G.dec_num, G.st))
+            return seterr(DC_ERR_HIP, "shard fix launch failed");
+    } else {
+        const long long nc = G.shard_deferred == 2 ? G.dec_max_chunks : dc_decode_group();
+        if (dc_launch_shard_fix(G.dec_s, &G.dec_P, &D, G.dec_out, G.dec_num, nc, d_hin, G.st))
+            return seterr(DC_ERR_HIP, "shard fix launch failed");
+    }
+    G.shard_deferred = 0;
+    HIPCHK(hipStreamSynchronize(G.st));
     return DC_OK;
 }
 

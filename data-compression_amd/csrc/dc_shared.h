@@ -60,6 +60,9 @@ typedef struct DecBufs { /* decoder metadata, sized for the maximum chunk count 
     unsigned* err;       /* 8 unknown entry, 16 spin timeout, 32 pending left, 64 closure overflow */
     unsigned* ctr;       /* [0,1] resolve ticket/exit, [2,3] parse, [4,5] decode */
     unsigned long long* dbg;   /* optional phase stamps (s_memrealtime) [tile][16], NULL = off */
+    int shard;           /* 0: the stream starts the data; 1: a shard, the three values before it come
+                            later (dc_decode_shard_fix); 2: a shard with those values in hin */
+    const float* hin;    /* [3] b1, b2, b3 before the shard (device), shard == 2 */
 } DecBufs;
 
 #ifdef __cplusplus
@@ -114,6 +117,10 @@ long long dc_crc_parts(long long nbytes);
 int dc_crc_run_bytes(void);
 int dc_launch_crc32(const uint8_t* s, long long nbytes, const uint32_t* d_tab, const uint32_t* d_x2n,
                     uint32_t* d_parts, uint32_t init, uint32_t* d_out, dc_hip_stream st);
+int dc_launch_bit_shift_copy(const uint8_t* s, long long sbytes, unsigned long long start_bit, unsigned long long nbits,
+                             uint8_t* d, long long nout, dc_hip_stream st);
+int dc_launch_shard_fix(const uint8_t* s, const DC_NS Params* P, const DC_NS DecBufs* D, float* out, long long num,
+                        long long nchunks, const float* hin, dc_hip_stream st);
 int dc_launch_flip_bits(uint8_t* s, unsigned long long nbits, long long count, unsigned long long seed,
                         dc_hip_stream st);
 int dc_launch_ham_syndrome(const uint8_t* s, long long nbytes, unsigned long long* d_syn_ones, dc_hip_stream st);

@@ -33,7 +33,7 @@ EXT_SYMBOLS = [
     "dc_get_abs_error_bound", "dc_stream_capacity", "dc_encode_device", "dc_encode_result",
     "dc_decode_device", "dc_decode_finish", "dc_to_small_device", "dc_med_device", "dc_crc32_device",
     "dc_decode_chunk_bits_value", "dc_ct1_encode_device", "dc_ct1_decode_device", "dc_encode_bits_device",
-    "dc_crc32_device_async", "dc_flip_bits_device",
+    "dc_crc32_device_async", "dc_flip_bits_device", "dc_decode_shard_device", "dc_decode_shard_fix",
 ]
 
 
@@ -66,6 +66,8 @@ class Lib:
         L.dc_encode_result.argtypes = [C.POINTER(C.c_ulonglong)]
         L.dc_encode_bits_device.argtypes = [C.c_int, vp, ll, ll, C.c_int, u32, C.POINTER(C.c_ulonglong)]
         L.dc_decode_device.argtypes = [C.c_int, vp, ll, vp, ll, ll, C.c_int, u32, vp]
+        L.dc_decode_shard_device.argtypes = [C.c_int, vp, ll, C.c_ulonglong, C.c_ulonglong, ll, C.c_int, u32, vp, vp]
+        L.dc_decode_shard_fix.argtypes = [vp]
         L.dc_to_small_device.argtypes = [vp, ll, vp, C.POINTER(C.c_float)]
         L.dc_med_device.argtypes = [vp, ll, C.POINTER(C.c_float), C.POINTER(C.c_int)]
         L.dc_crc32_device.argtypes = [vp, ll, C.POINTER(C.c_uint32)]
@@ -230,6 +232,15 @@ class Lib:
     def decode_device(self, ct, s_ptr, nbytes, num, out_ptr, type_=0, mask17=0, d_nbits=None, max_bytes=None):
         self.check(self.L.dc_decode_device(ct, s_ptr, nbytes, d_nbits, max_bytes if max_bytes is not None else nbytes,
                                            num, type_, mask17, out_ptr), "dc_decode_device")
+
+    def decode_shard_device(self, ct, s_ptr, stream_bytes, start_bit, nbits, num, out_ptr, type_=0, mask17=0,
+                            hin_ptr=None):
+        """Decode the shard at bits [start_bit, start_bit + nbits) of a device stream (dc_gpu.h)."""
+        self.check(self.L.dc_decode_shard_device(ct, s_ptr, stream_bytes, start_bit, nbits, num, type_, mask17, hin_ptr,
+                                                 out_ptr), "dc_decode_shard_device")
+
+    def decode_shard_fix(self, hin_ptr):
+        self.check(self.L.dc_decode_shard_fix(hin_ptr), "dc_decode_shard_fix")
 
     def decode_finish(self):
         self.check(self.L.dc_decode_finish(), "dc_decode_finish")

@@ -61,6 +61,17 @@ int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsig
  * serial prediction chains).  Returns DC_OK or DC_ERR_STREAM. */
 int dc_decode_finish(void);
 
+/* Shards of one global stream (multi-GPU decode): decode num values from the
+ * tokens at bits [start_bit, start_bit + nbits) of d_stream (stream_bytes long; start_bit must be a
+ * token boundary -- the shard offsets of the encode).  d_hin = the three values before the shard
+ * (b1 = x[-1], b2 = x[-2], b3 = x[-3], device floats), or NULL when they are not known yet: values
+ * that depend on them are then left for dc_decode_shard_fix (after dc_decode_finish).  Shards that
+ * need the exact slow paths report DC_ERR_STREAM (decode the whole stream instead). */
+int dc_decode_shard_device(int ct, const void* d_stream, long long stream_bytes, unsigned long long start_bit,
+                           unsigned long long nbits, long long num, int type, uint32_t mask17, const float* d_hin,
+                           void* d_out);
+int dc_decode_shard_fix(const float* d_hin);
+
 /* Pre-passes on device data: toSmallDataset_float and med_dataset_float (exact). */
 int dc_to_small_device(const void* d_x, long long n, void* d_out, float* min_out);
 int dc_med_device(const void* d_x, long long n, float* mean_out, int* type_out);

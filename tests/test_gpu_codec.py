@@ -335,3 +335,36 @@ def test_ct9_ber_flow(dc, oracle, ber):
     dc.decode_finish()
     ref, _ = oracle.decompress(7, clean, n, 1e-3, t, m17)
     assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("ct", CTS)
+@pytest.mark.parametrize("kind", ["u10", "ramp", "mixed"])
+@pytest.mark.parametrize("mode", ["known", "deferred"])
+def test_shard_decode(dc, oracle, ct, kind, mode):
+    """Multi-GPU decode building block: a shard of one global stream, from its start bit,
+    decodes exactly like that part of the whole stream -- with the three values before it given up
+    front ("known"), or supplied afterwards to re-decode the prefix that depends on them
+    ("deferred": the 12-byte exchange of the multi-GPU flow)."""
+    import torch
+    dc.set_bound(1e-3)
+    n = 300000
+    x = _inputs(oracle, kind, n)
+    _, xs = oracle.to_small(x)
+    t, m17 = oracle.type_mask(xs)
+    s, nb, pos = oracle.compress(ct, xs, 1e-3, t, m17)
+    ref, _ = oracle.decompress(ct, s, n, 1e-3, t, m17)
+    total = nb * 8 if pos == 8 else (nb - 1) * 8 + (8 - pos)
+    for cut in (123457, 3, 262144 + 5):
+        _, nbc, posc = oracle.compress(ct, xs[:cut], 1e-3, t, m17)
+        b0 = nbc * 8 if posc == 8 else (nbc - 1) * 8 + (8 - posc)
+        ds = torch.from_numpy(np.concatenate([s, np.zeros(64, np.uint8)])).cuda()
+        out = torch.full((n - cut,), -7.0, dtype=torch.float32, device="cuda")
+        hin = torch.from_numpy(ref[cut - 3:cut][::-1].copy()).cuda()          # b1, b2, b3
+        torch.cuda.synchronize()
+        dc.decode_shard_device(ct, ds.data_ptr(), nb, b0, total - b0, n - cut, out.data_ptr(), type_=t, mask17=m17,
+                               hin_ptr=hin.data_ptr() if mode == "known" else None)
+        dc.decode_finish()
+        if mode == "deferred":
+            dc.decode_shard_fix(hin.data_ptr())
+        got = out.cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), ref[cut:].view(np.uint32)), (cut, np.flatnonzero(got != ref[cut:])[:10])
