@@ -584,8 +584,7 @@ int dc_decode_shard_fix(const float* d_hin) {
         if (dc_launch_shard_fix(G.dec_s, &G.dec_P, &D, G.dec_out, G.dec_num, nc, d_hin, G.st))
             return seterr(DC_ERR_HIP, "shard fix launch failed");
     }
-    G.shard_deferred = 0;
-    HIPCHK(hipStreamSynchronize(G.st));
+    HIPCHK(hipStreamSynchronize(G.st));             /* re-runnable with other values until the next decode */
     return DC_OK;
 }
 

@@ -321,6 +321,67 @@ def gather_stream(local, start_bit, local_bits, group=None):
     return out, total
 
 
+def exchange_history(last3, group=None):
+    """The 12-byte exchange of the sharded decode: every rank contributes the last three
+    values of its shard (x[-1], x[-2], x[-3], a float32 tensor of 3) and receives the previous rank's,
+    i.e. its own shard's incoming history b1, b2, b3 (rank 0 gets None)."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    parts = [torch_like_zeros(last3) for _ in range(world)]
+    dist.all_gather(parts, last3.contiguous(), group=group)
+    return parts[rank - 1] if rank > 0 else None
+
+
+def torch_like_zeros(t):
+    import torch
+    return torch.zeros_like(t)
+
+
+def settle_history(tail3, fix, group=None):
+    """Run the exchange until no shard's last values change: fix(hin) re-decodes this rank's prefix that
+    depends on its incoming values and returns its (possibly updated) last three values.  One round
+    unless a prediction chain spans a whole shard, at most world_size rounds."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    last3 = tail3()
+    for _ in range(world):
+        hin = exchange_history(last3, group)
+        changed = torch.zeros(1, dtype=torch.int32, device=last3.device)
+        if hin is not None:
+            new3 = fix(hin)
+            changed[0] = int(not torch.equal(new3, last3))
+            last3 = new3
+        dist.all_reduce(changed, op=dist.ReduceOp.MAX, group=group)
+        if int(changed[0]) == 0:
+            break
+    return last3
+
+
+def decode_sharded(L, ct, stream, stream_bytes, start_bit, nbits, num, out, type_=0, mask17=0, group=None):
+    """Decode this rank's shard of one global stream on its GPU: rank 0 decodes
+    the stream start; the others decode from their start bit with deferred incoming values; then the
+    12-byte exchange and the prefix fix-up.  stream / out are device tensors, start_bit / nbits come
+    from the encode's shard offsets (shard_offsets), num >= 3."""
+    import torch.distributed as dist
+    if dist.get_rank(group) == 0:
+        L.decode_device(ct, stream.data_ptr(), (int(nbits) + 7) // 8, num, out.data_ptr(), type_, mask17)
+    else:
+        L.decode_shard_device(ct, stream.data_ptr(), stream_bytes, start_bit, nbits, num, out.data_ptr(), type_, mask17)
+    L.decode_finish()
+
+    def tail3():
+        return out[num - 3:num].flip(0).contiguous()
+
+    def fix(hin):
+        L.decode_shard_fix(hin.data_ptr())
+        return tail3()
+
+    settle_history(tail3, fix, group)
+    return out
+
+
 def gen_u10(n, seed=42, offset=0):
     """Synthetic U10 input: counter-based splitmix64 -> uniform [0,10) float32."""
     i = np.arange(offset, offset + n, dtype=np.uint64) + np.uint64(1)

@@ -81,3 +81,42 @@ def test_gather_stream_world2(ct, n):
 def test_shard_offsets():
     import dcamd
     assert dcamd.shard_offsets([5, 0, 7]) == ([0, 5, 5], 12)
+
+
+def _settle_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import dcamd
+        # every shard is one prediction chain: its last values are its incoming values + 1, so rank r
+        # ends at r only after the exchange has run r rounds
+        state = {"last": torch.zeros(3) if rank == 0 else torch.full((3,), -1.0)}
+
+        def tail3():
+            return state["last"].clone()
+
+        def fix(hin):
+            state["last"] = hin + 1.0
+            return tail3()
+
+        out = dcamd.settle_history(tail3, fix)
+        q.put((rank, out.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_settle_history_world3():
+    """The sharded decode's 12-byte exchange converges even when prediction chains span whole shards."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_settle_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    for r in range(world):
+        assert res[r] == [float(r)] * 3, res
