@@ -481,6 +481,49 @@ extern "C" int dc_launch_bit_shift_copy(const uint8_t* s, long long sbytes, unsi
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// Himeno halo planes: the plane ijk = 1/2/3 at index v of a [mi][mj][mk] float array in
+// the order of transform_3d_array_to_1d_array (impl/dataCompression.c:3741-3775), gathered into a
+// contiguous array; and the decoded plane + min scattered back (impl/himenoBMTxps.c:699-706).
+__device__ __forceinline__ long long plane_index(long long a, long long b, int ijk, int v, int mj, int mk) {
+    long long i, j, k;
+    if (ijk == 1) { i = v; j = a; k = b; }
+    else if (ijk == 2) { i = a; j = v; k = b; }
+    else { i = a; j = b; k = v; }
+    return (i * mj + j) * mk + k;
+}
+__global__ __launch_bounds__(256) void plane_gather_kernel(const float* __restrict__ p, int mj, int mk, int ijk, int v,
+                                                           int A, int B, float* __restrict__ out) {
+    const long long n = (long long)A * B;
+    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long long)gridDim.x * 256)
+        out[e] = p[plane_index(e / B, e % B, ijk, v, mj, mk)];
+}
+__global__ __launch_bounds__(256) void plane_scatter_kernel(const float* __restrict__ x, const float* __restrict__ d_min,
+                                                            float* __restrict__ p, int mj, int mk, int ijk, int v, int A,
+                                                            int B) {
+    const long long n = (long long)A * B;
+    const float mn = *d_min;
+    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long long)gridDim.x * 256)
+        p[plane_index(e / B, e % B, ijk, v, mj, mk)] = __fadd_rn(x[e], mn);
+}
+extern "C" int dc_launch_plane_gather(const float* p, int mj, int mk, int ijk, int v, int A, int B, float* out,
+                                      hipStream_t st) {
+    const long long n = (long long)A * B;
+    if (n <= 0) return 0;
+    long long g = (n + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(plane_gather_kernel, dim3((unsigned)g), dim3(256), 0, st, p, mj, mk, ijk, v, A, B, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+extern "C" int dc_launch_plane_scatter(const float* x, const float* d_min, float* p, int mj, int mk, int ijk, int v,
+                                       int A, int B, hipStream_t st) {
+    const long long n = (long long)A * B;
+    if (n <= 0) return 0;
+    long long g = (n + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(plane_scatter_kernel, dim3((unsigned)g), dim3(256), 0, st, x, d_min, p, mj, mk, ijk, v, A, B);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // BER fault injection for the CT8/CT9 flow: flip `count` stream bits at the
 // positions splitmix64(seed + i) mod nbits, MSB-first within each byte like bit_flip (:5858-5865).
 // The reference's own pingpong CT9 path only *simulates* a CRC failure (impl/pingpong.c:421-430);

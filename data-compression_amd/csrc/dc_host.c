@@ -55,6 +55,8 @@ typedef struct {
     const float* dec_hin;            /* its incoming values (shard mode 2) */
     int shard_deferred;              /* 1: tile-0 prefixes wait for dc_decode_shard_fix, 2: later tiles too */
     void* shard_buf; size_t shard_cap;
+    void* halo_a; size_t halo_a_cap;
+    void* halo_b; size_t halo_b_cap;
     /* pinned host scratch */
     unsigned long long* h_scratch;   /* [0] total bits [1] err [2..] misc */
     /* staging for the host-pointer ABI */
@@ -585,6 +587,64 @@ int dc_decode_shard_fix(const float* d_hin) {
             return seterr(DC_ERR_HIP, "shard fix launch failed");
     }
     HIPCHK(hipStreamSynchronize(G.st));             /* re-runnable with other values until the next decode */
+    return DC_OK;
+}
+
+/* ---- Himeno halo planes on the device (impl/himenoBMTxps.c:483-706) ------------- */
+static int plane_dims(int ijk, int imax, int jmax, int kmax, int* A, int* B) {
+    if (ijk == 1) { *A = jmax; *B = kmax; }
+    else if (ijk == 2) { *A = imax; *B = kmax; }
+    else if (ijk == 3) { *A = imax; *B = jmax; }
+    else return seterr(DC_ERR_ARG, "ijk %d outside 1..3", ijk);
+    return DC_OK;
+}
+
+int dc_halo_encode_device(int ct, const void* d_p, int mi, int mj, int mk, int ijk, int v, int imax, int jmax,
+                          int kmax, int type, uint32_t mask17, void* d_stream, unsigned long long* d_bits,
+                          float* d_min, int* type_out, uint32_t* mask17_out) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    int A = 0, B = 0;
+    if ((rc = plane_dims(ijk, imax, jmax, kmax, &A, &B))) return rc;
+    if (v < 0 || (ijk == 1 && v >= mi) || (ijk == 2 && v >= mj) || (ijk == 3 && v >= mk) || A > (ijk == 1 ? mj : mi) ||
+        B > (ijk == 3 ? mj : mk))
+        return seterr(DC_ERR_ARG, "plane outside the %dx%dx%d array", mi, mj, mk);
+    const long long n = (long long)A * B;
+    if (n <= 0) return seterr(DC_ERR_ARG, "empty plane");
+    if (grow(&G.halo_a, &G.halo_a_cap, (size_t)n * 4 + 64) || grow(&G.halo_b, &G.halo_b_cap, (size_t)n * 4 + 64))
+        return DC_ERR_HIP;
+    if (dc_launch_plane_gather((const float*)d_p, mj, mk, ijk, v, A, B, (float*)G.halo_a, G.st))
+        return seterr(DC_ERR_HIP, "plane gather launch failed");
+    if (dc_launch_to_small((const float*)G.halo_a, n, (float*)G.halo_b, G.part_v, G.part_i, &G.d_f[0], G.st))
+        return seterr(DC_ERR_HIP, "to_small launch failed");
+    if (d_min) HIPCHK(hipMemcpyAsync(d_min, &G.d_f[0], 4, hipMemcpyDeviceToDevice, G.st));
+    if (ct == 7 && type <= 0) {                     /* mask of this plane, as himenoBMTxps.c:483-500 */
+        float mean;
+        if ((rc = dc_med_device(G.halo_b, n, &mean, &type))) return rc;
+        uint32_t u;
+        memcpy(&u, &mean, 4);
+        mask17 = u >> 15;
+    }
+    if (type_out) *type_out = type;
+    if (mask17_out) *mask17_out = mask17;
+    return dc_encode_device(ct, G.halo_b, n, 0, type, mask17, 0, d_stream, d_bits);
+}
+
+int dc_halo_decode_device(int ct, const void* d_stream, long long nbytes, const unsigned long long* d_bits, int type,
+                          uint32_t mask17, const float* d_min, void* d_p, int mi, int mj, int mk, int ijk, int v,
+                          int imax, int jmax, int kmax) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    int A = 0, B = 0;
+    if ((rc = plane_dims(ijk, imax, jmax, kmax, &A, &B))) return rc;
+    (void)mi;
+    const long long n = (long long)A * B;
+    if (grow(&G.halo_a, &G.halo_a_cap, (size_t)n * 4 + 64)) return DC_ERR_HIP;
+    const long long cap = nbytes >= 0 ? nbytes : (long long)dc_stream_capacity(n);
+    if ((rc = dc_decode_device(ct, d_stream, nbytes, d_bits, cap, n, type, mask17, G.halo_a))) return rc;
+    if ((rc = dc_decode_finish())) return rc;
+    if (dc_launch_plane_scatter((const float*)G.halo_a, d_min, (float*)d_p, mj, mk, ijk, v, A, B, G.st))
+        return seterr(DC_ERR_HIP, "plane scatter launch failed");
     return DC_OK;
 }
 

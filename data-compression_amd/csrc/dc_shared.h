@@ -121,6 +121,9 @@ int dc_launch_bit_shift_copy(const uint8_t* s, long long sbytes, unsigned long l
                              uint8_t* d, long long nout, dc_hip_stream st);
 int dc_launch_shard_fix(const uint8_t* s, const DC_NS Params* P, const DC_NS DecBufs* D, float* out, long long num,
                         long long nchunks, const float* hin, dc_hip_stream st);
+int dc_launch_plane_gather(const float* p, int mj, int mk, int ijk, int v, int A, int B, float* out, dc_hip_stream st);
+int dc_launch_plane_scatter(const float* x, const float* d_min, float* p, int mj, int mk, int ijk, int v, int A, int B,
+                            dc_hip_stream st);
 int dc_launch_flip_bits(uint8_t* s, unsigned long long nbits, long long count, unsigned long long seed,
                         dc_hip_stream st);
 int dc_launch_ham_syndrome(const uint8_t* s, long long nbytes, unsigned long long* d_syn_ones, dc_hip_stream st);

@@ -34,6 +34,7 @@ EXT_SYMBOLS = [
     "dc_decode_device", "dc_decode_finish", "dc_to_small_device", "dc_med_device", "dc_crc32_device",
     "dc_decode_chunk_bits_value", "dc_ct1_encode_device", "dc_ct1_decode_device", "dc_encode_bits_device",
     "dc_crc32_device_async", "dc_flip_bits_device", "dc_decode_shard_device", "dc_decode_shard_fix",
+    "dc_halo_encode_device", "dc_halo_decode_device",
 ]
 
 
@@ -238,6 +239,19 @@ class Lib:
         """Decode the shard at bits [start_bit, start_bit + nbits) of a device stream (dc_gpu.h)."""
         self.check(self.L.dc_decode_shard_device(ct, s_ptr, stream_bytes, start_bit, nbits, num, type_, mask17, hin_ptr,
                                                  out_ptr), "dc_decode_shard_device")
+
+    def halo_encode_device(self, ct, p_ptr, dims, ijk, v, ext, stream_ptr, bits_ptr, min_ptr, type_=0, mask17=0):
+        """Fused Himeno halo-plane encode (dc_gpu.h); dims = (mi, mj, mk), ext = (imax, jmax, kmax)."""
+        t, m = C.c_int(0), C.c_uint32(0)
+        self.check(self.L.dc_halo_encode_device(ct, C.c_void_p(p_ptr), *dims, ijk, v, *ext, type_, C.c_uint32(mask17),
+                                                C.c_void_p(stream_ptr), C.c_void_p(bits_ptr), C.c_void_p(min_ptr),
+                                                C.byref(t), C.byref(m)), "dc_halo_encode_device")
+        return t.value, m.value
+
+    def halo_decode_device(self, ct, stream_ptr, nbytes, bits_ptr, type_, mask17, min_ptr, p_ptr, dims, ijk, v, ext):
+        self.check(self.L.dc_halo_decode_device(ct, C.c_void_p(stream_ptr), C.c_longlong(nbytes), C.c_void_p(bits_ptr),
+                                                type_, C.c_uint32(mask17), C.c_void_p(min_ptr), C.c_void_p(p_ptr), *dims,
+                                                ijk, v, *ext), "dc_halo_decode_device")
 
     def decode_shard_fix(self, hin_ptr):
         self.check(self.L.dc_decode_shard_fix(hin_ptr), "dc_decode_shard_fix")

@@ -72,6 +72,18 @@ int dc_decode_shard_device(int ct, const void* d_stream, long long stream_bytes,
                            void* d_out);
 int dc_decode_shard_fix(const float* d_hin);
 
+/* Himeno halo planes on device-resident p[mi][mj][mk] (the fused form of transform_3d_array_to_1d_array +
+ * toSmallDataset_float + compress, impl/himenoBMTxps.c:483-706): encode the plane ijk (1: i = v,
+ * 2: j = v, 3: k = v) of extent imax x jmax x kmax; *d_min (device) gets the plane minimum.  CT7 with
+ * type <= 0 derives type / mask from the plane (med_dataset_float, synchronous) and returns them in
+ * *type_out / *mask17_out.  Decode: stream -> plane values + *d_min written back into p's plane. */
+int dc_halo_encode_device(int ct, const void* d_p, int mi, int mj, int mk, int ijk, int v, int imax, int jmax,
+                          int kmax, int type, uint32_t mask17, void* d_stream, unsigned long long* d_bits,
+                          float* d_min, int* type_out, uint32_t* mask17_out);
+int dc_halo_decode_device(int ct, const void* d_stream, long long nbytes, const unsigned long long* d_bits, int type,
+                          uint32_t mask17, const float* d_min, void* d_p, int mi, int mj, int mk, int ijk, int v,
+                          int imax, int jmax, int kmax);
+
 /* Pre-passes on device data: toSmallDataset_float and med_dataset_float (exact). */
 int dc_to_small_device(const void* d_x, long long n, void* d_out, float* min_out);
 int dc_med_device(const void* d_x, long long n, float* mean_out, int* type_out);

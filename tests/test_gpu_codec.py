@@ -368,3 +368,49 @@ def test_shard_decode(dc, oracle, ct, kind, mode):
             dc.decode_shard_fix(hin.data_ptr())
         got = out.cpu().numpy()
         assert np.array_equal(got.view(np.uint32), ref[cut:].view(np.uint32)), (cut, np.flatnonzero(got != ref[cut:])[:10])
+
+
+@pytest.mark.parametrize("ct", CTS)
+@pytest.mark.parametrize("ijk,v", [(3, 1), (3, 128), (1, 1), (2, 64)])
+def test_halo_plane_device(dc, oracle, ct, ijk, v):
+    """Fused Himeno halo path: the plane of a device-resident p[129][129][131]
+    (impl/param.h) gathered in transform_3d_array_to_1d_array order, toSmallDataset_float'ed and
+    encoded on the GPU equals the oracle stream of the host-side plane; the decode writes plane + min
+    back into p exactly as impl/himenoBMTxps.c:699-706."""
+    import torch
+    dc.set_bound(1e-3)
+    mi, mj, mk = 129, 129, 131
+    imax, jmax, kmax = 128, 128, 130
+    ii = np.arange(mi, dtype=np.float32)[:, None, None]
+    rs = np.random.RandomState(ijk * 1000 + v)
+    p = (ii * ii / np.float32((imax - 1) * (imax - 1)) + np.zeros((mi, mj, mk), np.float32)).astype(np.float32)
+    p += (rs.rand(mi, mj, mk).astype(np.float32) * np.float32(0.01))
+    A, B = {1: (jmax, kmax), 2: (imax, kmax), 3: (imax, jmax)}[ijk]
+    a, b = np.meshgrid(np.arange(A), np.arange(B), indexing="ij")
+    idx = {1: (v, a, b), 2: (a, v, b), 3: (a, b, v)}[ijk]
+    plane = p[idx].reshape(-1).copy()
+    mn, xs = oracle.to_small(plane)
+    t, m17 = oracle.type_mask(xs)
+    s, nb, pos = oracle.compress(ct, xs, 1e-3, t, m17)
+    dp = torch.from_numpy(p).cuda()
+    n = A * B
+    st = torch.zeros(dc.stream_capacity(n), dtype=torch.uint8, device="cuda")
+    bits = torch.zeros(1, dtype=torch.int64, device="cuda")
+    dmin = torch.zeros(1, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    ty, mk17 = dc.halo_encode_device(ct, dp.data_ptr(), (mi, mj, mk), ijk, v, (imax, jmax, kmax), st.data_ptr(),
+                                     bits.data_ptr(), dmin.data_ptr(), type_=0, mask17=0)
+    if ct == 7:
+        assert (ty, mk17) == (t, m17)
+    tb = dc.encode_result()
+    assert (tb + 7) // 8 == nb
+    assert np.array_equal(st[:nb].cpu().numpy(), s)
+    assert np.float32(dmin.cpu().numpy()[0]) == np.float32(mn)
+    q = torch.zeros_like(dp)
+    dc.halo_decode_device(ct, st.data_ptr(), nb, 0, ty, mk17, dmin.data_ptr(), q.data_ptr(), (mi, mj, mk), ijk, v,
+                          (imax, jmax, kmax))
+    dc.synchronize()
+    dec, _ = oracle.decompress(ct, s, n, 1e-3, t, m17)
+    want = (dec + np.float32(mn)).astype(np.float32)
+    got = q.cpu().numpy()[idx].reshape(-1)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
