@@ -36,6 +36,9 @@ def parse():
     ap.add_argument("--cpu-log2n", type=int, default=22, help="cpu_baseline sample size (2^k floats)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify the round trip against the oracle")
+    ap.add_argument("--halo", action="store_true",
+                    help="BASELINE configs[3]: Himeno L-size z-halo planes (256x256 of p[257][257][k]) per rank, "
+                         "fused device halo encode + decode, CT from --ct (config: 5)")
     ap.add_argument("--ber", type=float, default=0.0,
                     help="CT9 flow (BASELINE configs[4]): CRC-32 of the CT7 stream, floor(bits*BER) real bit flips on "
                          "the received copy, CRC check, resend, decode -- all inside the timed step")
@@ -80,8 +83,84 @@ def cpu_baseline(ct, bound, n, kind):
                       + (" (compiled reference)" if kind_s == "reference" else " restatement (oracle)")}
 
 
+def halo_bench(args):
+    """Himeno halo exchange payload (impl/himenoBMTxps.c:644-706): every Jacobi iteration each rank
+    compresses its two z-halo planes (k = 1 and k = kmax - 2 of p[257][257][kk], 65,536 floats each)
+    and decompresses the two it receives.  Here a step = encode + decode of both planes on this
+    rank's GPU through the fused device path (no MPI; the planes are independent streams)."""
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    import dcamd
+    L = dcamd.Lib()
+    L.init(local)
+    L.set_bound(args.bound)
+    mi, mj, mk = 257, 257, 8                       # L-size i/j extent; a thin z slab per rank
+    imax, jmax, kmax = 256, 256, 7
+    ii = torch.arange(mi, dtype=torch.float32, device=dev).view(mi, 1, 1)
+    p = (ii * ii / float((imax - 1) * (imax - 1))).expand(mi, mj, mk).contiguous()     # initmt (it = 0)
+    q = torch.zeros_like(p)
+    n = imax * jmax
+    cap = L.stream_capacity(n)
+    st = [torch.zeros(cap, dtype=torch.uint8, device=dev) for _ in range(2)]
+    bits = torch.zeros(2, dtype=torch.int64, device=dev)
+    mins = torch.zeros(2, dtype=torch.float32, device=dev)
+    ct = args.ct if args.ct != 7 else 5
+    planes = [1, kmax - 2]
+
+    def step():
+        for h, v in enumerate(planes):
+            L.halo_encode_device(ct, p.data_ptr(), (mi, mj, mk), 3, v, (imax, jmax, kmax), st[h].data_ptr(),
+                                 bits.data_ptr() + 8 * h, mins.data_ptr() + 4 * h)
+        for h, v in enumerate(planes):
+            L.halo_decode_device(ct, st[h].data_ptr(), -1, bits.data_ptr() + 8 * h, 0, 0, mins.data_ptr() + 4 * h,
+                                 q.data_ptr(), (mi, mj, mk), 3, v, (imax, jmax, kmax))
+
+    for _ in range(max(args.warmup, 1)):
+        step()
+    L.synchronize()
+    nbytes = [(int(b) + 7) // 8 for b in bits.cpu()]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    L.synchronize()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    if dist is not None:
+        w = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        wall = float(w[0])
+    res = {"metric": f"GB/s (halo plane float bytes) compress+decompress, Himeno L z-halos, CT={ct} "
+                     f"absErrorBound={args.bound:g}",
+           "value": round(world * 2 * 4.0 * n / (wall / args.steps) / 1e9, 4), "unit": "GB/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+           "data": "synthetic Himeno initmt pressure field (p = i^2/(imax-1)^2, it = 0)",
+           "config": {"workload": "Himeno L-size z-halo planes, 2 x 256x256 floats per rank per step, fused device "
+                                  "plane gather + toSmallDataset + encode, decode + min scatter", "ct": ct,
+                      "plane_floats": n, "stream_bytes": nbytes, "ratio": round(4.0 * n / max(nbytes[0], 1), 3),
+                      "parallelism": f"dp{world}"}}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.halo:
+        return halo_bench(args)
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
