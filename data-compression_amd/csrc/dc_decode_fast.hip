@@ -51,7 +51,10 @@ constexpr int PWORDS = padw(GROUP * LROW + 8 + OVW);
 #else
 #define PLEN(t) token_len_bf<CT>((t), P)
 #endif
-constexpr int KMAX = 2;                        // extra known entries per chunk (besides P_c's own)
+#ifndef DC_KMAX
+#define DC_KMAX 3                               // 3: the three phases of a period-3 run ('101' chains)
+#endif
+constexpr int KMAX = DC_KMAX;                        // extra known entries per chunk (besides P_c's own)
 constexpr int RMAX = 12;                       // closure rounds inside a tile
 constexpr int CW = CHUNK_BITS / 32;            // words per chunk
 constexpr int UNKE = 63;
@@ -174,10 +177,13 @@ struct ParseShared {
     uint32_t L[PWORDS];
     uint8_t tl[512];                           // token length by the first 9 bits (build_lut_len)
     uint32_t ke[GROUP * KMAX];                 // entry<<16 | exit<<10 | cnt
-    uint8_t nkr[2][GROUP];                     // known-entry count of every chunk, by round parity
+    union {                                    // closure rounds, then the tile chain
+        uint8_t nkr[2][GROUP];                 // known-entry count of every chunk, by round parity
+        uint16_t devcnt[GROUP];
+    };
     uint32_t pm[GROUP];
     uint64_t bad[GROUP / 64];
-    uint16_t n[GROUP], devcnt[GROUP];
+    uint16_t n[GROUP];
     uint8_t x[GROUP], nk[GROUP], stdexit[GROUP], dev[GROUP];
     uint32_t wsum[GROUP / 64];
     int texit;
