@@ -91,12 +91,13 @@ def halo_bench(args):
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        # RCCL over xGMI; DC_BENCH_BACKEND=gloo rehearses the multi-rank path with several ranks per GPU
+        dist.init_process_group(os.environ.get("DC_BENCH_BACKEND", "nccl"))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     import dcamd
@@ -164,12 +165,13 @@ def main():
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        # RCCL over xGMI; DC_BENCH_BACKEND=gloo rehearses the multi-rank path with several ranks per GPU
+        dist.init_process_group(os.environ.get("DC_BENCH_BACKEND", "nccl"))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
