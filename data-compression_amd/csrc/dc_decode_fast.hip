@@ -643,8 +643,14 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
         if (t >= pl.ngroups) break;
         const long long tbit = t * (long long)GROUP * CHUNK_BITS;
         STAMP(8);
-        stage_tile(S.L, s, pl.nbytes, tbit >> 5);
         const long long gc = t * GROUP + c;
+        // the tile's chain records are loaded before the stream is staged (one memory round trip)
+        const uint32_t te = D.tentry[t];
+        const unsigned long long base = D.tbase[t];
+        const int tmx = (int)D.tmap[t * 4 + 3];
+        const int e_rec = D.entry[gc];
+        const unsigned long long off_rec = D.tokoff[gc];
+        stage_tile(S.L, s, pl.nbytes, tbit >> 5);
         const long long rem = (long long)pl.nbits - tbit;
         const int nact = (int)min((long long)GROUP, (rem + CHUNK_BITS - 1) / CHUNK_BITS);
         const bool act = c < nact;
@@ -652,18 +658,16 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
         const int cend = (int)min((long long)(cs + CHUNK_BITS), rem);
         if (c == 0) { S.need = 0; S.cplx = 0; S.defer = 0; }
         // ---- entry and first token index of every chunk (parse kernel chain + tile_fix overrides)
-        const uint32_t te = D.tentry[t];
         const int ein = (int)(te & 63), c0 = (int)((te >> 6) & 1023), kjoin = (int)(te >> 16);
         int e = UNKE;
         unsigned long long k0 = 0;
         if (act && ein != UNKE) {
-            const unsigned long long base = D.tbase[t];
             if (c == 0) {
                 e = ein;
                 k0 = base;
             } else {
-                e = D.entry[gc];
-                const long long rel = (long long)D.tokoff[gc] + (c >= kjoin ? (long long)(int)D.tmap[t * 4 + 3] : 0ll);
+                e = e_rec;
+                const long long rel = (long long)off_rec + (c >= kjoin ? (long long)tmx : 0ll);
                 k0 = base + (unsigned long long)(c0 + rel);
             }
             D.entry[gc] = (uint8_t)e;
