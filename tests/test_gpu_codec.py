@@ -414,3 +414,29 @@ def test_halo_plane_device(dc, oracle, ct, ijk, v):
     want = (dec + np.float32(mn)).astype(np.float32)
     got = q.cpu().numpy()[idx].reshape(-1)
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def test_fused_encoder_option():
+    """The optional single-pass encoder (DC_ENC_FUSED=1, decoupled look-back) writes the same stream as
+    the default count + scan + write encoder (checked in a child process: the switch is read once)."""
+    import subprocess
+    import sys
+    import os
+    code = r'''
+import sys, numpy as np, torch
+sys.path.insert(0, "data-compression_amd"); sys.path.insert(0, "oracle")
+import dcamd
+from pyoracle import Oracle
+torch.zeros(1, device="cuda")
+L = dcamd.Lib(); L.init(0); L.set_bound(1e-3); O = Oracle()
+for n, ct in ((1 << 20, 7), (300001, 5), (4099, 6), (70000, 11)):
+    x = O.gen_u10(n); _, xs = O.to_small(x); t, m = O.type_mask(xs)
+    s, nb, pos = O.compress(ct, xs, 1e-3, t, m)
+    g, nbg, posg = L.compress(ct, xs, t, m)
+    assert nbg == nb and posg == pos and np.array_equal(g, s), (n, ct)
+print("FUSED_OK")
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, DC_ENC_FUSED="1"))
+    assert "FUSED_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
