@@ -51,6 +51,9 @@ constexpr int PWORDS = padw(GROUP * LROW + 8 + OVW);
 #else
 #define PLEN(t) token_len_bf<CT>((t), P)
 #endif
+#ifndef DC_DEC_NT
+#define DC_DEC_NT 1                              // decode stages the stream with nontemporal loads (its last read)
+#endif
 #ifndef DC_KMAX
 #define DC_KMAX 3                               // 3: the three phases of a period-3 run ('101' chains)
 #endif
@@ -94,7 +97,8 @@ struct Rd {
 };
 
 // stage stream words [tw, tw + nw) into padded LDS rows (zeros outside the stream; tw may be < 0)
-__device__ __forceinline__ void stage_words(uint32_t* L, const uint8_t* s, long long nbytes, long long tw, int nw) {
+__device__ __forceinline__ void stage_words(uint32_t* L, const uint8_t* s, long long nbytes, long long tw, int nw,
+                                            bool nt = false) {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(s);
     const long long nwfull = nbytes >> 2;
     if (tw >= 0 && tw + nw <= nwfull && ((reinterpret_cast<uintptr_t>(s) & 15u) == 0) && (tw & 3) == 0 && (nw & 3) == 0) {
@@ -105,7 +109,15 @@ __device__ __forceinline__ void stage_words(uint32_t* L, const uint8_t* s, long 
 #pragma unroll
         for (int q = 0; q <= QF; q++) {
             const int i = threadIdx.x + q * GROUP;
-            if (q < QF || i < n4) r[q] = w4[i];
+            if (q < QF || i < n4) {
+                if (nt) {
+                    typedef unsigned u4v __attribute__((ext_vector_type(4)));
+                    const u4v w = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(w4 + i));
+                    r[q] = make_uint4(w.x, w.y, w.z, w.w);
+                } else {
+                    r[q] = w4[i];
+                }
+            }
         }
 #pragma unroll
         for (int q = 0; q <= QF; q++) {
@@ -140,7 +152,7 @@ __device__ __forceinline__ void stage_words(uint32_t* L, const uint8_t* s, long 
 
 // the tile's words [tw, tw + GROUP*CW + 4)
 __device__ __forceinline__ void stage_tile(uint32_t* L, const uint8_t* s, long long nbytes, long long tw) {
-    stage_words(L, s, nbytes, tw, GROUP * CW + 4);
+    stage_words(L, s, nbytes, tw, GROUP * CW + 4, DC_DEC_NT);        // the decode is the stream's last reader
 }
 
 // walk entry e of chunk c (LDS bits [cs, cend)) alongside P_c (whose first boundary in the chunk is

@@ -29,6 +29,12 @@ constexpr int ENC_Q = ENC_TILE / 4 / ENC_TPB;   // coalesced float4 loads per la
 #ifndef DC_CNT_Q
 #define DC_CNT_Q 4
 #endif
+#ifndef DC_WR_NT
+#define DC_WR_NT 0
+#endif
+#ifndef DC_CNT_NT
+#define DC_CNT_NT 1                     // the count pass streams x past the caches: measured count 85 -> 57 us
+#endif
 constexpr int CNT_Q = DC_CNT_Q;                 // count kernel: one wave per tile part, CNT_Q float4 per lane
 constexpr int CNT_SUB = 256 * CNT_Q;            // floats per count wave
 constexpr int CNT_PARTS = ENC_TILE / CNT_SUB;   // count parts per tile (tbits entries)
@@ -86,7 +92,15 @@ __device__ __forceinline__ void load_part(const float* __restrict__ x, long long
     const float4* p4 = reinterpret_cast<const float4*>(x + tb);
     if (tb + CNT_SUB <= n) {
 #pragma unroll
-        for (int q = 0; q < CNT_Q; q++) f[q] = p4[lane + 64 * q];
+        for (int q = 0; q < CNT_Q; q++) {
+#if DC_CNT_NT
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            const f4v w = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p4 + lane + 64 * q));
+            f[q] = make_float4(w.x, w.y, w.z, w.w);
+#else
+            f[q] = p4[lane + 64 * q];
+#endif
+        }
     } else {                                                         // whole float4s only
         const int rem = (int)(n - tb);
 #pragma unroll
@@ -233,7 +247,15 @@ __device__ __forceinline__ void load_tile4(const float* __restrict__ x, long lon
     if (tbase + ENC_TILE <= n) {
         const float4* p4 = reinterpret_cast<const float4*>(x + tbase);
 #pragma unroll
-        for (int q = 0; q < ENC_Q; q++) f[q] = p4[tid + ENC_TPB * q];
+        for (int q = 0; q < ENC_Q; q++) {
+#if DC_WR_NT
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            const f4v w = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p4 + tid + ENC_TPB * q));
+            f[q] = make_float4(w.x, w.y, w.z, w.w);
+#else
+            f[q] = p4[tid + ENC_TPB * q];
+#endif
+        }
     } else {
 #pragma unroll
         for (int q = 0; q < ENC_Q; q++) {
