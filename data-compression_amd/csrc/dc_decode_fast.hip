@@ -221,10 +221,28 @@ __device__ __forceinline__ bool lookup_entry(const ParseShared& S, int c, int e,
     return false;
 }
 
+__device__ __forceinline__ Plan make_plan(const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                                          long long max_chunks) {
+    const unsigned long long nbits = dev_nbits ? *dev_nbits : host_nbits;
+    Plan p;
+    p.nbits = nbits;
+    p.nbytes = (long long)((nbits + 7) >> 3);
+    long long nc = (long long)((nbits + CHUNK_BITS - 1) / CHUNK_BITS);
+    if (nc > max_chunks) nc = max_chunks;
+    p.nchunks = nc;
+    p.ngroups = (nc + GROUP - 1) / GROUP;
+    return p;
+}
+
+// the parse also derives the plan (sizes from the bit length, on the device so encode -> decode needs no
+// host round trip) and publishes it for the later kernels
 template <int CT>
-__global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict__ s, Params P, DecBufs D) {
+__global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict__ s, Params P, DecBufs D,
+                                                    const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                                                    long long max_chunks) {
     __shared__ ParseShared S;
-    const Plan pl = *D.plan;
+    const Plan pl = make_plan(dev_nbits, host_nbits, max_chunks);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *D.plan = pl;
     const int c = threadIdx.x, lane = c & 63, wid = c >> 6;
     build_lut_len<CT>(S.tl, P, c, GROUP);                             // visible after the first barrier
     for (long long t = blockIdx.x; t < pl.ngroups; t += gridDim.x) {
@@ -935,19 +953,6 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
         default: return -2;                                                                          \
     }
 
-__global__ void plan_kernel_fast(Plan* plan, const unsigned long long* dev_nbits, unsigned long long host_nbits,
-                                 long long max_chunks) {
-    const unsigned long long nbits = dev_nbits ? *dev_nbits : host_nbits;
-    Plan p;
-    p.nbits = nbits;
-    p.nbytes = (long long)((nbits + 7) >> 3);
-    long long nc = (long long)((nbits + CHUNK_BITS - 1) / CHUNK_BITS);
-    if (nc > max_chunks) nc = max_chunks;
-    p.nchunks = nc;
-    p.ngroups = (nc + GROUP - 1) / GROUP;
-    *plan = p;
-}
-
 // resident decode workgroups (persistent grid; tiles are claimed from an atomic counter in order)
 static int decode_grid(int ct) {
     static int cache[12];
@@ -967,10 +972,9 @@ extern "C" int dc_launch_decode_fast(const uint8_t* s, const unsigned long long*
                                      unsigned long long host_nbits, long long max_chunks, const Params* P,
                                      const DecBufs* D, float* out, long long num, uint32_t epoch, hipStream_t st) {
     const long long max_groups = (max_chunks + GROUP - 1) / GROUP;
-    hipLaunchKernelGGL(plan_kernel_fast, dim3(1), dim3(1), 0, st, D->plan, dev_nbits, host_nbits, max_chunks);
     const int gparse = (int)std::min<long long>(max_groups > 0 ? max_groups : 1, 256 * 8);
     dc_mark_phase(4, st);
-    DC_DISPATCH_F(P->ct, parse_kernel, dim3(gparse), dim3(GROUP), 0, st, s, *P, *D);
+    DC_DISPATCH_F(P->ct, parse_kernel, dim3(gparse), dim3(GROUP), 0, st, s, *P, *D, dev_nbits, host_nbits, max_chunks);
     dc_mark_phase(5, st);
     DC_DISPATCH_F(P->ct, tile_fix_kernel, dim3((unsigned)((max_groups + 3) / 4 > 0 ? (max_groups + 3) / 4 : 1)), dim3(256), 0, st,
                   s, *P, *D);
