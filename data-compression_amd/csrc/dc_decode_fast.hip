@@ -517,10 +517,10 @@ __global__ __launch_bounds__(256) void tile_fix_kernel(const uint8_t* __restrict
 
 // tile_scan: first token index of every tile (one workgroup, block scan of the tile counts)
 __global__ __launch_bounds__(1024) void tile_scan_kernel(DecBufs D) {
-    __shared__ unsigned long long part[1024];
+    __shared__ unsigned long long wtot[16];
     const Plan pl = *D.plan;
     const long long nt = pl.ngroups;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const long long per = (nt + 1023) / 1024;
     const long long t0 = tid * per, t1 = min(nt, t0 + per);
     auto count = [&](long long t) -> unsigned long long {
@@ -530,15 +530,19 @@ __global__ __launch_bounds__(1024) void tile_scan_kernel(DecBufs D) {
     };
     unsigned long long sum = 0;
     for (long long t = t0; t < t1; t++) sum += count(t);
-    part[tid] = sum;
-    __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {           // inclusive Hillis-Steele over 1024 partial sums
-        const unsigned long long v = tid >= d ? part[tid - d] : 0ull;
-        __syncthreads();
-        part[tid] += v;
-        __syncthreads();
+    unsigned long long inc = sum;                    // wave scan, then the 16 wave totals
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long u = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += u;
     }
-    unsigned long long run = part[tid] - sum;
+    if (lane == 63) wtot[wid] = inc;
+    __syncthreads();
+    unsigned long long wpre = 0;
+#pragma unroll
+    for (int w = 0; w < 16; w++) wpre += w < wid ? wtot[w] : 0ull;
+    unsigned long long part_tid = wpre + inc;
+    unsigned long long run = part_tid - sum;
     for (long long t = t0; t < t1; t++) {
         D.tbase[t] = run;
         run += count(t);
