@@ -65,7 +65,11 @@ constexpr int UNKE = 63;
 #define STAMP(ph) do { if (D.dbg && threadIdx.x == 0 && t < 4096) D.dbg[t * 16 + (ph)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
 __device__ __forceinline__ int lidx(int w) { return DC_PAD ? w + (w >> 5) : w; }
-__device__ __forceinline__ uint32_t ldw(const uint32_t* L, int w) { return L[lidx(w)]; }
+__device__ __forceinline__ uint32_t ldw(const uint32_t* L, int w) {
+    // byte offset (w + w / 32) * 4: one v_add_lshl_u32 after the shift
+    const uint32_t off = ((uint32_t)lidx(w)) << 2;
+    return *(const uint32_t*)((const char*)L + off);
+}
 
 // branch-free MSB-first reader: w0:w1 hold the next 64 bits from bit sh of w0, w2 the next word.
 // Every step is fetch() (issues the LDS read of the word after w2, at the top of the step) ... step()
@@ -73,14 +77,15 @@ __device__ __forceinline__ uint32_t ldw(const uint32_t* L, int w) { return L[lid
 // in-flight register -- with a loop-carried prefetch it placed an lgkmcnt(0) wait on every step.
 struct Rd {
     uint32_t a, b, c, nx;                      // the 64-bit window (a:b) is read from bit 32 - s of a
-    int s, wi, pos;                            // s in [0, 31]; wi = LDS index of a; pos = stream bit
+    int s, w3, pos;                            // s in [0, 31]; w3 = word index of the next fetch; pos = stream bit
     __device__ __forceinline__ void init(const uint32_t* L, int p) {
-        wi = (p - 1) >> 5;                     // a word boundary is bit 32 of a (s = 0), never bit 0
+        const int wi = (p - 1) >> 5;           // a word boundary is bit 32 of a (s = 0), never bit 0
         s = 32 * (wi + 1) - p;
         a = ldw(L, max(wi, 0)); b = ldw(L, wi + 1); c = ldw(L, wi + 2);
+        w3 = wi + 3;
         pos = p;
     }
-    __device__ __forceinline__ void fetch(const uint32_t* L) { nx = ldw(L, wi + 3); }
+    __device__ __forceinline__ void fetch(const uint32_t* L) { nx = ldw(L, w3); }
     __device__ __forceinline__ uint32_t peek() const {
         return __builtin_amdgcn_alignbit(a, b, (uint32_t)s);           // ((a:b) >> s), low word
     }
@@ -92,7 +97,7 @@ struct Rd {
         a = adv ? b : a;
         b = adv ? c : b;
         c = adv ? nx : c;
-        wi += adv ? 1 : 0;
+        w3 += adv ? 1 : 0;
     }
 };
 
@@ -173,7 +178,7 @@ __device__ __forceinline__ void walk_lds(const uint32_t* L, const uint8_t* tl, i
     while (A.pos < cend) {
         if (A.pos == B.pos) { merged = true; break; }
         const bool sa = A.pos < B.pos || B.pos >= cend;
-        const uint32_t nx = ldw(L, (sa ? A.wi : B.wi) + 3);
+        const uint32_t nx = ldw(L, sa ? A.w3 : B.w3);
         const uint32_t tk = sa ? A.peek() : B.peek();
         const int len = tl[tk >> 23];
         if (sa) { A.nx = nx; A.step(len); ca++; } else { B.nx = nx; B.step(len); cb++; }
