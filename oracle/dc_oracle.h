@@ -73,6 +73,19 @@ int orc_hamming_decode(unsigned char* bits, char* c, long bytes, int r, long* er
 /* block_size (:5868-5879) for a given BER */
 int orc_block_size(int data_bytes, double ber);
 
+/* ---- double codecs (dc_oracle64.c): myCompress_bitwise_double :3189 (ct 5), _np :2633 (6),
+ * _mask :1590 (7), _op :355 (11); grammar decoder of myDecompress_bitwise_double :2656 / _np :2286 /
+ * _mask :1199 / _op :476.  mask20 = the top 20 bits of the mean's pattern (char mask[1+11+8]). */
+int orc64_mbits(int B, int E);
+double orc64_to_small(const double* data, long n, double* out);   /* toSmallDataset_double :3522 */
+double orc64_med(const double* data, long n, int* type);          /* med_dataset_double :3564 */
+uint32_t orc64_mask20(double mean);
+void orc64_compress(int ct, const double* data, long num, double bound, int type, uint32_t mask20,
+                    unsigned char** bits, int* bytes, int* pos);
+long orc64_decompress_spec(int ct, const unsigned char* bits, long bytes, long num, double bound,
+                           int type, uint32_t mask20, double* out);
+void orc64_gen_u10(double* out, long n, uint64_t seed, long offset);
+
 /* Synthetic inputs: U10 counter-based splitmix64, HIMENO-L plane. */
 void orc_gen_u10(float* out, long n, uint64_t seed, long offset);
 void orc_gen_himeno_plane(float* out, int imax, int jmax);

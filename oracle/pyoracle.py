@@ -19,6 +19,7 @@ REFDIR = os.path.join(HERE, "_ref")
 _f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
 _u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
 _i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
 _libc = C.CDLL(None)
 _libc.free.argtypes = [C.c_void_p]
 _libc.malloc.argtypes = [C.c_size_t]
@@ -70,6 +71,19 @@ class Oracle:
         L.orc_block_size.argtypes = [C.c_int, C.c_double]
         L.orc_gen_u10.argtypes = [_f32p, C.c_long, C.c_uint64, C.c_long]
         L.orc_gen_himeno_plane.argtypes = [_f32p, C.c_int, C.c_int]
+        # double codecs (dc_oracle64.c)
+        L.orc64_to_small.argtypes = [_f64p, C.c_long, _f64p]
+        L.orc64_to_small.restype = C.c_double
+        L.orc64_med.argtypes = [_f64p, C.c_long, C.POINTER(C.c_int)]
+        L.orc64_med.restype = C.c_double
+        L.orc64_mask20.argtypes = [C.c_double]
+        L.orc64_mask20.restype = C.c_uint32
+        L.orc64_compress.argtypes = [C.c_int, _f64p, C.c_long, C.c_double, C.c_int, C.c_uint32,
+                                     C.POINTER(C.c_void_p), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.orc64_decompress_spec.argtypes = [C.c_int, _u8p, C.c_long, C.c_long, C.c_double, C.c_int,
+                                            C.c_uint32, _f64p]
+        L.orc64_decompress_spec.restype = C.c_long
+        L.orc64_gen_u10.argtypes = [_f64p, C.c_long, C.c_uint64, C.c_long]
 
     # -- helpers
     def bound_binary(self, b):
@@ -171,6 +185,50 @@ class Oracle:
         self.L.orc_gen_u10(out, n, seed, offset)
         return out
 
+    # -- double codecs
+    def to_small64(self, x):
+        x = np.ascontiguousarray(x, np.float64)
+        out = np.empty_like(x)
+        mn = self.L.orc64_to_small(x, x.size, out)
+        return np.float64(mn), out
+
+    def med64(self, x):
+        x = np.ascontiguousarray(x, np.float64)
+        t = C.c_int(0)
+        mean = self.L.orc64_med(x, x.size, C.byref(t))
+        return np.float64(mean), t.value
+
+    def mask20(self, mean):
+        return int(self.L.orc64_mask20(float(mean)))
+
+    def compress64(self, ct, x, bound, type_=0, mask20=0, prefix=None, prefix_pos=8):
+        x = np.ascontiguousarray(x, np.float64)
+        p = C.c_void_p(None)
+        nbytes = C.c_int(0)
+        pos = C.c_int(8)
+        if prefix is not None and len(prefix):
+            buf = _libc.malloc(len(prefix))
+            C.memmove(buf, bytes(prefix), len(prefix))
+            p = C.c_void_p(buf)
+            nbytes.value = len(prefix)
+            pos.value = prefix_pos
+        self.L.orc64_compress(ct, x, x.size, bound, type_, mask20, C.byref(p), C.byref(nbytes), C.byref(pos))
+        out = np.frombuffer(C.string_at(p.value, nbytes.value), np.uint8).copy() if nbytes.value else np.zeros(0, np.uint8)
+        _libc.free(p)
+        return out, nbytes.value, pos.value
+
+    def decompress64(self, ct, s, num, bound, type_=0, mask20=0):
+        s = np.ascontiguousarray(s, np.uint8)
+        out = np.zeros(num, np.float64)
+        n = self.L.orc64_decompress_spec(ct, s if s.size else np.zeros(1, np.uint8), s.size, num, bound,
+                                         type_, mask20, out)
+        return out, n
+
+    def gen_u10_64(self, n, seed=42, offset=0):
+        out = np.empty(n, np.float64)
+        self.L.orc64_gen_u10(out, n, seed, offset)
+        return out
+
     def gen_himeno_plane(self, imax=256, jmax=256):
         out = np.empty(imax * jmax, np.float32)
         self.L.orc_gen_himeno_plane(out, imax, jmax)
@@ -222,6 +280,19 @@ class RefLib:
         L.myCompress.argtypes = [_f32p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_int]
         L.myDecompress.argtypes = [_f32p, C.c_char_p, _i32p, C.c_int]
         L.myDecompress.restype = C.c_void_p
+        dp = [_f64p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        for nm in ("myCompress_bitwise_double", "myCompress_bitwise_double_np", "myCompress_bitwise_double_op"):
+            getattr(L, nm).argtypes = dp
+        L.myCompress_bitwise_double_mask.argtypes = dp + [C.c_int, C.c_char_p]
+        for nm in ("myDecompress_bitwise_double", "myDecompress_bitwise_double_np", "myDecompress_bitwise_double_op"):
+            getattr(L, nm).argtypes = [_u8p, C.c_int, C.c_int]
+            getattr(L, nm).restype = C.c_void_p
+        L.myDecompress_bitwise_double_mask.argtypes = [_u8p, C.c_int, C.c_int, C.c_int, C.c_char_p]
+        L.myDecompress_bitwise_double_mask.restype = C.c_void_p
+        L.toSmallDataset_double.argtypes = [_f64p, C.POINTER(C.c_void_p), C.c_int]
+        L.toSmallDataset_double.restype = C.c_double
+        L.med_dataset_double.argtypes = [_f64p, C.c_int, C.POINTER(C.c_int)]
+        L.med_dataset_double.restype = C.c_double
 
     @staticmethod
     def mask_chars(mask17):
@@ -262,6 +333,46 @@ class RefLib:
         out = np.frombuffer(C.string_at(p, 4 * num), np.float32).copy()
         _libc.free(p)
         return out
+
+    @staticmethod
+    def mask_chars20(mask20):
+        return "".join("1" if (mask20 >> (19 - i)) & 1 else "0" for i in range(20)).encode()
+
+    _D = {5: "", 6: "_np", 11: "_op", 7: "_mask"}
+
+    def compress64(self, ct, x, type_=0, mask20=0):
+        x = np.ascontiguousarray(x, np.float64)
+        p = C.c_void_p(None)
+        nb = C.c_int(0)
+        pos = C.c_int(8)
+        args = (x, x.size, C.byref(p), C.byref(nb), C.byref(pos))
+        f = getattr(self.L, "myCompress_bitwise_double" + self._D[ct])
+        f(*args, type_, self.mask_chars20(mask20)) if ct == 7 else f(*args)
+        out = np.frombuffer(C.string_at(p.value, nb.value), np.uint8).copy() if nb.value else np.zeros(0, np.uint8)
+        _libc.free(p)
+        return out, nb.value, pos.value
+
+    def decompress64(self, ct, s, num, type_=0, mask20=0):
+        s = np.ascontiguousarray(s, np.uint8)
+        f = getattr(self.L, "myDecompress_bitwise_double" + self._D[ct])
+        p = f(s, s.size, num, type_, self.mask_chars20(mask20)) if ct == 7 else f(s, s.size, num)
+        out = np.frombuffer(C.string_at(p, 8 * num), np.float64).copy()
+        _libc.free(p)
+        return out
+
+    def to_small64(self, x):
+        x = np.ascontiguousarray(x, np.float64)
+        p = C.c_void_p(None)
+        mn = self.L.toSmallDataset_double(x, C.byref(p), x.size)
+        out = np.frombuffer(C.string_at(p.value, 8 * x.size), np.float64).copy()
+        _libc.free(p)
+        return np.float64(mn), out
+
+    def med64(self, x):
+        x = np.ascontiguousarray(x, np.float64)
+        t = C.c_int(0)
+        mean = self.L.med_dataset_double(x, x.size, C.byref(t))
+        return np.float64(mean), t.value
 
     def to_small(self, x):
         x = np.ascontiguousarray(x, np.float32)

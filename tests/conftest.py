@@ -54,3 +54,15 @@ def dc():
     L = dcamd.Lib()
     L.init(0)
     return L
+
+
+CASES64 = ["testdouble", "u10_16k", "eq16k", "unit32k", "q2", "ramp20k", "mixed", "edge"]
+_golden64_cache = {}
+
+
+def golden64(bound):
+    """Double-codec fixtures of tests/golden/make_golden64.py (compiled reference outputs)."""
+    if bound not in _golden64_cache:
+        with np.load(os.path.join(GOLDEN, "golden64_%g.npz" % bound), allow_pickle=False) as z:
+            _golden64_cache[bound] = {k: z[k] for k in z.files}
+    return _golden64_cache[bound]
