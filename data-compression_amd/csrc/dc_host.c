@@ -94,6 +94,7 @@ static int seterr(int code, const char* fmt, ...) {
     } while (0)
 
 const char* dc_last_error(void) { return G.msg; }
+int dc_set_error(int code, const char* msg) { return seterr(code, "%s", msg); }
 void* dc_get_stream(void) { return (void*)G.st; }
 void dc_set_abs_error_bound(double bound) { absErrBound = bound; absErrorBound_binary = -100; }
 double dc_get_abs_error_bound(void) { return absErrBound; }

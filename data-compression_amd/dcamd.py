@@ -15,6 +15,7 @@ LIB = os.environ.get("DCAMD_LIB") or os.path.join(HERE, "lib", "libdcamd.so")   
 
 _f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
 _u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
 _libc = C.CDLL(None)
 _libc.free.argtypes = [C.c_void_p]
 _libc.malloc.argtypes = [C.c_size_t]
@@ -27,6 +28,10 @@ ABI_SYMBOLS = [
     "toSmallDataset_float", "med_dataset_float", "do_crc32", "hmLength", "hamming_encode", "hamming_decode",
     "bit_flip", "block_size", "get_random_int", "floattostr", "strtofloat", "doubletostr", "strtodbl",
     "getFloatBin", "to_absErrorBound_binary", "add_bit_to_bytes", "bit_set", "myCompress", "myDecompress",
+    "myCompress_bitwise_double", "myCompress_bitwise_double_np", "myCompress_bitwise_double_op",
+    "myCompress_bitwise_double_mask", "myDecompress_bitwise_double", "myDecompress_bitwise_double_np",
+    "myDecompress_bitwise_double_op", "myDecompress_bitwise_double_mask", "toSmallDataset_double",
+    "med_dataset_double",
 ]
 EXT_SYMBOLS = [
     "dc_init", "dc_last_error", "dc_get_stream", "dc_synchronize", "dc_set_abs_error_bound",
@@ -35,6 +40,8 @@ EXT_SYMBOLS = [
     "dc_decode_chunk_bits_value", "dc_ct1_encode_device", "dc_ct1_decode_device", "dc_encode_bits_device",
     "dc_crc32_device_async", "dc_flip_bits_device", "dc_decode_shard_device", "dc_decode_shard_fix",
     "dc_halo_encode_device", "dc_halo_decode_device",
+    "dc64_stream_capacity", "dc64_encode_device", "dc64_encode_result", "dc64_decode_device", "dc64_decode_finish",
+    "dc64_last_decode_flags", "dc64_to_small_device", "dc64_med_device",
 ]
 
 
@@ -96,6 +103,28 @@ class Lib:
         L.myCompress.restype = C.c_int
         L.myDecompress.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         L.myDecompress.restype = vp
+        # double codecs
+        dp = [_f64p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        for nm in ("myCompress_bitwise_double", "myCompress_bitwise_double_np", "myCompress_bitwise_double_op"):
+            getattr(L, nm).argtypes = dp
+        L.myCompress_bitwise_double_mask.argtypes = dp + [C.c_int, C.c_char_p]
+        for nm in ("myDecompress_bitwise_double", "myDecompress_bitwise_double_np", "myDecompress_bitwise_double_op"):
+            getattr(L, nm).argtypes = [_u8p, C.c_int, C.c_int]
+            getattr(L, nm).restype = vp
+        L.myDecompress_bitwise_double_mask.argtypes = [_u8p, C.c_int, C.c_int, C.c_int, C.c_char_p]
+        L.myDecompress_bitwise_double_mask.restype = vp
+        L.toSmallDataset_double.argtypes = [_f64p, C.POINTER(C.c_void_p), C.c_int]
+        L.toSmallDataset_double.restype = C.c_double
+        L.med_dataset_double.argtypes = [_f64p, C.c_int, C.POINTER(C.c_int)]
+        L.med_dataset_double.restype = C.c_double
+        L.dc64_stream_capacity.argtypes = [ll]
+        L.dc64_stream_capacity.restype = C.c_size_t
+        L.dc64_encode_device.argtypes = [C.c_int, vp, ll, C.c_int, u32, C.c_int, vp, vp]
+        L.dc64_encode_result.argtypes = [C.POINTER(C.c_ulonglong)]
+        L.dc64_decode_device.argtypes = [C.c_int, vp, ll, vp, ll, ll, C.c_int, u32, vp]
+        L.dc64_last_decode_flags.restype = C.c_uint
+        L.dc64_to_small_device.argtypes = [vp, ll, vp, C.POINTER(C.c_double)]
+        L.dc64_med_device.argtypes = [vp, ll, C.POINTER(C.c_double), C.POINTER(C.c_int)]
 
     # ---- state
     def init(self, device=0):
@@ -152,6 +181,72 @@ class Lib:
         out = np.frombuffer(C.string_at(p, 4 * num), np.float32).copy() if num else np.zeros(0, np.float32)
         _libc.free(p)
         return out
+
+    # ---- double codecs (myCompress_bitwise_double* / myDecompress_bitwise_double*)
+    _D = {5: "", 6: "_np", 11: "_op", 7: "_mask"}
+
+    @staticmethod
+    def mask_chars20(mask20):
+        return "".join("1" if (mask20 >> (19 - i)) & 1 else "0" for i in range(20)).encode()
+
+    def compress64(self, ct, x, type_=0, mask20=0, prefix=None, prefix_pos=8):
+        x = np.ascontiguousarray(x, np.float64)
+        p = C.c_void_p(None)
+        nb = C.c_int(0)
+        pos = C.c_int(8)
+        if prefix is not None and len(prefix):
+            buf = _libc.malloc(len(prefix))
+            C.memmove(buf, bytes(prefix), len(prefix))
+            p = C.c_void_p(buf)
+            nb.value = len(prefix)
+            pos.value = prefix_pos
+        args = (x if x.size else np.zeros(1, np.float64), x.size, C.byref(p), C.byref(nb), C.byref(pos))
+        f = getattr(self.L, "myCompress_bitwise_double" + self._D[ct])
+        f(*args, type_, self.mask_chars20(mask20)) if ct == 7 else f(*args)
+        out = np.frombuffer(C.string_at(p.value, nb.value), np.uint8).copy() if nb.value else np.zeros(0, np.uint8)
+        if p.value:
+            _libc.free(p)
+        return out, nb.value, pos.value
+
+    def decompress64(self, ct, s, num, type_=0, mask20=0):
+        s = np.ascontiguousarray(s, np.uint8)
+        sarg = s if s.size else np.zeros(1, np.uint8)
+        f = getattr(self.L, "myDecompress_bitwise_double" + self._D[ct])
+        p = f(sarg, s.size, num, type_, self.mask_chars20(mask20)) if ct == 7 else f(sarg, s.size, num)
+        out = np.frombuffer(C.string_at(p, 8 * num), np.float64).copy() if num else np.zeros(0, np.float64)
+        _libc.free(p)
+        return out
+
+    def to_small64(self, x):
+        x = np.ascontiguousarray(x, np.float64)
+        p = C.c_void_p(None)
+        mn = self.L.toSmallDataset_double(x, C.byref(p), x.size)
+        out = np.frombuffer(C.string_at(p.value, 8 * x.size), np.float64).copy()
+        _libc.free(p)
+        return np.float64(mn), out
+
+    def med64(self, x):
+        x = np.ascontiguousarray(x, np.float64)
+        t = C.c_int(0)
+        mean = self.L.med_dataset_double(x, x.size, C.byref(t))
+        return np.float64(mean), t.value
+
+    def encode64_device(self, ct, x_ptr, n, out_ptr, type_=0, mask20=0, start_bit=0, total_ptr=None):
+        self.check(self.L.dc64_encode_device(ct, x_ptr, n, type_, mask20, start_bit, out_ptr, total_ptr),
+                   "dc64_encode_device")
+
+    def encode64_result(self):
+        v = C.c_ulonglong(0)
+        self.check(self.L.dc64_encode_result(C.byref(v)), "dc64_encode_result")
+        return v.value
+
+    def decode64_device(self, ct, s_ptr, nbytes, num, out_ptr, type_=0, mask20=0, d_nbits=None, max_bytes=None):
+        self.check(self.L.dc64_decode_device(ct, s_ptr, nbytes, d_nbits, max_bytes if max_bytes is not None else nbytes,
+                                             num, type_, mask20, out_ptr), "dc64_decode_device")
+
+    def decode64_finish(self):
+        self.check(self.L.dc64_decode_finish(), "dc64_decode_finish")
+        return int(self.L.dc64_last_decode_flags())
 
     # ---- CT1 byte-wise codec (myCompress / myDecompress)
     def ct1_compress(self, x):

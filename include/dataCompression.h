@@ -99,6 +99,29 @@ int myCompress(float data[], float** array_float, char** array_char, int** array
 /* h:121 c:3943-3977 */
 float* myDecompress(float array_float[], char array_char[], int array_char_displacement[], int num);
 
+/* ---- double bit-wise codecs (k-means / mm / lu payloads), same shapes as the float ones --------- */
+/* h:89  c:3189-3308 */
+void myCompress_bitwise_double(double data[], int num, unsigned char** data_bits, int* bytes, int* pos);
+/* h:76  c:2633-2643 */
+void myCompress_bitwise_double_np(double data[], int num, unsigned char** data_bits, int* bytes, int* pos);
+/* h:79  c:355-475 */
+void myCompress_bitwise_double_op(double data[], int num, unsigned char** data_bits, int* bytes, int* pos);
+/* h:66  c:1590-1701: mask = the first 1+11+8 chars of doubletostr(mean) */
+void myCompress_bitwise_double_mask(double data[], int num, unsigned char** data_bits, int* bytes, int* pos, int type,
+                                    char mask[1 + 11 + 8]);
+/* h:84  c:2656-2869 */
+double* myDecompress_bitwise_double(unsigned char* data_bits, int bytes, int num);
+/* h:72  c:2286-2457 */
+double* myDecompress_bitwise_double_np(unsigned char* data_bits, int bytes, int num);
+/* h:80  c:476-575 */
+double* myDecompress_bitwise_double_op(unsigned char* data_bits, int bytes, int num);
+/* h:63  c:1199-1394 */
+double* myDecompress_bitwise_double_mask(unsigned char* data_bits, int bytes, int num, int type, char mask[1 + 11 + 8]);
+/* h:95  c:3522-3541 */
+double toSmallDataset_double(double data[], double** data_small, int num);
+/* h:98  c:3564-3590: left-to-right double mean; *type from the maximum */
+double med_dataset_double(double* data, int num, int* type);
+
 /* ---- pre-passes ---------------------------------------------------------------------------------- */
 /* h:96  c:3543-3562: *data_small = data - min (new malloc array), returns min */
 float toSmallDataset_float(float data[], float** data_small, int num);

@@ -102,6 +102,24 @@ int dc_ct1_encode_device(const void* d_x, long long n, void* d_raw, void* d_code
 int dc_ct1_decode_device(const void* d_raw, long long nraw, const void* d_codes, const void* d_pos1, long long ncodes,
                          long long num, void* d_out);
 
+/* ---- double codecs (CT 5/6/7/11 of myCompress_bitwise_double*, impl/dataCompression.c:355-3308) ---
+ * mask20 = the top 20 bits of the mean's pattern (char mask[1+11+8]).  d_out of the encoder needs
+ * dc64_stream_capacity(n) bytes, 4-byte aligned; start_bit 0..7 leaves that many zero bits first
+ * (the host ABI ORs the bits of a partially filled last byte there).  Asynchronous on the library
+ * stream; *d_total_bits (device, optional) receives the bit count. */
+size_t dc64_stream_capacity(long long n);
+int dc64_encode_device(int ct, const void* d_x, long long n, int type, uint32_t mask20, int start_bit, void* d_out,
+                       unsigned long long* d_total_bits);
+int dc64_encode_result(unsigned long long* total_bits);                   /* sync + bits of the last encode */
+/* Decode num doubles from a device stream of nbytes bytes (or *d_nbits bits when d_nbits is given;
+ * max_bytes bounds the scratch).  Asynchronous; dc64_decode_finish() waits and reports a short stream. */
+int dc64_decode_device(int ct, const void* d_stream, long long nbytes, const unsigned long long* d_nbits,
+                       long long max_bytes, long long num, int type, uint32_t mask20, void* d_out);
+int dc64_decode_finish(void);
+unsigned dc64_last_decode_flags(void);            /* after finish: 1 = the exact serial decoder ran */
+int dc64_to_small_device(const void* d_x, long long n, void* d_out, double* min_out);   /* synchronous */
+int dc64_med_device(const void* d_x, long long n, double* mean_out, int* type_out);     /* synchronous */
+
 /* Decoder/encoder geometry (for tests and bench). */
 long long dc_decode_chunk_bits_value(void);
 
