@@ -55,9 +55,24 @@ __device__ __forceinline__ double u2d(uint64_t u) { return __longlong_as_double(
 __device__ __forceinline__ int mbits(int B, int E) { return min(max(B + E - 1023, 0), 52); }
 __device__ __forceinline__ uint32_t bswap(uint32_t v) { return __builtin_bswap32(v); }
 
-__device__ __forceinline__ double pred2(double b1, double b2) { return __dsub_rn(__dmul_rn(2.0, b1), b2); }
+// NaN results follow x86 SSE2 as gcc orders the operations (the reference's host): 2*b1 - b2 returns
+// the first NaN of b1, b2 (quieted); 3*b1 - 3*b2 + b3 is evaluated as b3 + (3*b1 - 3*b2), so a NaN b3
+// wins; a NaN made from non-NaN operands (inf - inf) is the x86 default NaN 0xFFF8000000000000.
+// Only streams decoded outside the codec's domain reach this (an encoder never predicts with NaNs).
+__device__ __noinline__ double x86_nan(double b1, double b2, double b3, bool use3) {
+    const uint64_t q = 0x0008000000000000ull;
+    if (use3 && b3 != b3) return u2d(d2u(b3) | q);
+    if (b1 != b1) return u2d(d2u(b1) | q);
+    if (b2 != b2) return u2d(d2u(b2) | q);
+    return u2d(0xFFF8000000000000ull);
+}
+__device__ __forceinline__ double pred2(double b1, double b2) {
+    const double v = __dsub_rn(__dmul_rn(2.0, b1), b2);
+    return v != v ? x86_nan(b1, b2, 0.0, false) : v;
+}
 __device__ __forceinline__ double pred3(double b1, double b2, double b3) {
-    return __dadd_rn(__dsub_rn(__dmul_rn(3.0, b1), __dmul_rn(3.0, b2)), b3);
+    const double v = __dadd_rn(__dsub_rn(__dmul_rn(3.0, b1), __dmul_rn(3.0, b2)), b3);
+    return v != v ? x86_nan(b1, b2, b3, true) : v;
 }
 
 // ---------------------------------------------------------------------------------------------- encoder

@@ -84,3 +84,4 @@ def test_append64(oracle, bound, ct):
     assert nb1 == g[f"append/ct{ct}/first_bytes"] and p1 == g[f"append/ct{ct}/first_pos"]
     s2, nb2, p2 = oracle.compress64(ct, xs[333:], bound, prefix=s1, prefix_pos=p1)
     assert np.array_equal(s2, g[f"append/ct{ct}/stream"]) and p2 == g[f"append/ct{ct}/pos"]
+
