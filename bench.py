@@ -39,6 +39,9 @@ def parse():
     ap.add_argument("--halo", action="store_true",
                     help="BASELINE configs[3]: Himeno L-size z-halo planes (256x256 of p[257][257][k]) per rank, "
                          "fused device halo encode + decode, CT from --ct (config: 5)")
+    ap.add_argument("--f64", action="store_true",
+                    help="the double codecs (myCompress/myDecompress_bitwise_double*, k-means/mm/lu payloads): "
+                         "compress+decompress of 2^log2n U10 doubles per GPU, CT from --ct")
     ap.add_argument("--ber", type=float, default=0.0,
                     help="CT9 flow (BASELINE configs[4]): CRC-32 of the CT7 stream, floor(bits*BER) real bit flips on "
                          "the received copy, CRC check, resend, decode -- all inside the timed step")
@@ -158,10 +161,131 @@ def halo_bench(args):
         dist.destroy_process_group()
 
 
+def f64_bench(args):
+    """Double codecs (dc_f64.hip): a step = dc64_encode_device + dc64_decode_device of the rank's block of
+    2^log2n U10 doubles already in HBM; toSmallDataset_double / med_dataset_double run once before."""
+    import ctypes
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group(os.environ.get("DC_BENCH_BACKEND", "nccl"))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    import dcamd
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    L = dcamd.Lib()
+    L.init(local)
+    L.set_bound(args.bound)
+    n = 1 << args.log2n
+    ct = args.ct
+    from pyoracle import Oracle
+    O = Oracle()
+    x = torch.from_numpy(O.gen_u10_64(n, 42, rank * n)).to(dev)
+    xs = torch.empty_like(x)
+    mn = ctypes.c_double(0)
+    L.check(L.L.dc64_to_small_device(ctypes.c_void_p(x.data_ptr()), n, ctypes.c_void_p(xs.data_ptr()), ctypes.byref(mn)),
+            "dc64_to_small_device")
+    mean, typ = ctypes.c_double(0), ctypes.c_int(0)
+    t_med0 = time.perf_counter()
+    L.check(L.L.dc64_med_device(ctypes.c_void_p(xs.data_ptr()), n, ctypes.byref(mean), ctypes.byref(typ)), "dc64_med_device")
+    t_med = time.perf_counter() - t_med0
+    typ = typ.value
+    mask20 = int(np.array([mean.value], np.float64).view(np.uint64)[0] >> 44)
+    cap = int(L.L.dc64_stream_capacity(n))
+    stream = torch.empty(cap, dtype=torch.uint8, device=dev)
+    out = torch.empty(n, dtype=torch.float64, device=dev)
+    d_nbits = torch.zeros(1, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    ext = torch.cuda.ExternalStream(L.L.dc_get_stream())
+
+    def step(ev=None):
+        if ev:
+            ev[0].record(ext)
+        L.encode64_device(ct, xs.data_ptr(), n, stream.data_ptr(), typ, mask20, total_ptr=d_nbits.data_ptr())
+        if ev:
+            ev[1].record(ext)
+        L.decode64_device(ct, stream.data_ptr(), -1, n, out.data_ptr(), typ, mask20, d_nbits=d_nbits.data_ptr(),
+                          max_bytes=cap)
+        if ev:
+            ev[2].record(ext)
+
+    for _ in range(max(args.warmup, 1)):
+        step()
+    flags = L.decode64_finish()
+    nbytes = (L.encode64_result() + 7) // 8
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    L.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    L.synchronize()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    flags |= L.decode64_finish()
+    if dist is not None:
+        w = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        wall = float(w[0])
+    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    ok = None
+    if args.check and rank == 0:
+        s_h = stream[:nbytes].cpu().numpy()
+        so, nbo, _ = O.compress64(ct, xs.cpu().numpy(), args.bound, typ, mask20)
+        ref, _ = O.decompress64(ct, so, n, args.bound, typ, mask20)
+        ok = bool(nbo == nbytes and np.array_equal(s_h, so) and
+                  np.array_equal(out.cpu().numpy().view(np.uint64), ref.view(np.uint64)))
+    res = {"metric": f"GB/s (input double bytes) compress+decompress, double CT={ct} absErrorBound={args.bound:g}",
+           "value": round(world * 8.0 * n / (wall / args.steps) / 1e9, 3), "unit": "GB/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+           "data": "synthetic U10 doubles (counter-based splitmix64, 53-bit uniform [0,10), seed 42), generated per rank",
+           "config": {"workload": f"double CT{ct} bit-wise compress+decompress, U10 2^{args.log2n} float64 per GPU, "
+                                  f"absErrorBound={args.bound:g}", "doubles_per_gpu": n, "ct": ct,
+                      "stream_bytes": int(nbytes), "ratio": round(8.0 * n / nbytes, 4), "type": typ,
+                      "mask20": f"{mask20:05x}", "parallelism": f"dp{world}", "exact_fallback": bool(flags & 1)},
+           "phases_ms": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4), "med_dataset_double_s": round(t_med, 4)}}
+    if ok is not None:
+        res["check_vs_oracle"] = ok
+    if rank == 0 and not args.no_cpu:
+        R = None
+        try:
+            from pyoracle import RefLib
+            R = RefLib(args.bound)
+        except (FileNotFoundError, OSError):
+            pass
+        m = 1 << args.cpu_log2n
+        xh = np.ascontiguousarray(xs[:m].cpu().numpy())
+        t0 = time.perf_counter()
+        s, nb, _ = R.compress64(ct, xh, typ, mask20) if R else O.compress64(ct, xh, args.bound, typ, mask20)
+        t1 = time.perf_counter()
+        R.decompress64(ct, s, m, typ, mask20) if R else O.decompress64(ct, s, m, args.bound, typ, mask20)
+        t2 = time.perf_counter()
+        res["cpu_baseline"] = {"value": round(8.0 * m / (t2 - t0) / 1e9, 6), "unit": "GB/s", "cores": 1,
+                               "kind": "reference" if R else "port",
+                               "sample": f"U10 2^{args.cpu_log2n} doubles CT{ct}: compress {t1 - t0:.3f} s + decompress "
+                                         f"{t2 - t1:.3f} s, single-threaded impl/dataCompression.c"
+                                         + (" (compiled reference)" if R else " restatement (oracle)")}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     if args.halo:
         return halo_bench(args)
+    if args.f64:
+        return f64_bench(args)
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
