@@ -362,56 +362,86 @@ __device__ __forceinline__ double tok_value(uint64_t win, int len, const P64& P)
     return u2d((win & ~((1ull << (64 - len)) - 1ull)) | (1ull << (63 - len)));
 }
 
-// chunk maps: map[c][e] = exit | count << 8 for every entry e of chunk c (one lane per chunk)
+// A workgroup of 64 lanes handles 64 consecutive chunks: their stream words (plus the 8 that follow,
+// for walks past the last chunk) are staged in LDS, one pad word per 64 so that lanes walking their
+// chunks at about the same offset hit different banks.
+constexpr int GW = 64 * MAPW + 8;
+constexpr int SW = GW + GW / 64 + 2;
+constexpr int MB = 512;                     // P0 boundaries kept for the first MB bits of a chunk
+__device__ __forceinline__ int sidx(int w) { return w + (w >> 6); }
+__device__ __forceinline__ uint64_t peekS(const uint32_t* S, uint32_t q) {
+    const int w = (int)(q >> 5), s = (int)(q & 31);
+    const uint64_t a = ((uint64_t)S[sidx(w)] << 32) | S[sidx(w + 1)];
+    return s ? (a << s) | ((uint64_t)S[sidx(w + 2)] >> (32 - s)) : a;
+}
+__device__ __forceinline__ void stage_group(uint32_t* S, const uint32_t* __restrict__ W, long long w0, long long wlim) {
+    for (int i = threadIdx.x; i < GW; i += blockDim.x) {
+        const long long w = w0 + i;
+        S[sidx(i)] = w < wlim ? W[w] : 0u;
+    }
+}
+
+// chunk maps, entry-major: map[e * mstride + c] = exit | count << 8 for every entry e of chunk c.  One
+// lane per chunk parses P0 from the chunk's bit 0 (boundaries of its first MB bits kept); every other
+// entry walks until it lands on a P0 boundary (then it shares P0's remaining tokens and exit) or
+// leaves the chunk.
 template <int CT>
 __global__ __launch_bounds__(64) void dec_map(const uint32_t* __restrict__ W, const Plan64* __restrict__ pl, P64 P,
-                                              uint32_t* __restrict__ map) {
-    __shared__ uint32_t M[64 * (MAPW + 1)];
-    const long long c = blockIdx.x * 64ll + threadIdx.x;
-    if (c >= pl->nchunks) return;
-    const unsigned long long nb = pl->nbits;
-    uint32_t* mk = M + threadIdx.x * (MAPW + 1);
-    for (int i = 0; i < MAPW; i++) mk[i] = 0u;
-    const unsigned long long cs = (unsigned long long)c * CB, ce = cs + CB;
-    unsigned long long p = cs;
-    uint32_t cnt0 = 0;
+                                              uint32_t* __restrict__ map, long long mstride) {
+    __shared__ uint32_t S[SW];
+    __shared__ uint32_t M[64 * (MB / 32 + 1)];
+    const long long g0 = blockIdx.x * 64ll;
+    const long long nc = pl->nchunks;
+    if (g0 >= nc) return;
+    stage_group(S, W, g0 * MAPW, pl->nwords + 4);
+    const long long c = g0 + threadIdx.x;
+    uint32_t* mk = M + threadIdx.x * (MB / 32 + 1);
+#pragma unroll
+    for (int i = 0; i < MB / 32; i++) mk[i] = 0u;
+    __syncthreads();
+    if (c >= nc) return;
+    const long long avail = (long long)pl->nbits - g0 * CB;            // stream bits from the group start
+    const uint32_t lim = (uint32_t)std::min(avail, (long long)(64 * CB + 64));
+    const uint32_t cs = threadIdx.x * CB, ce = cs + CB;
+    uint32_t p = cs, cnt0 = 0;
     while (p < ce) {
-        const int l = tok_len<CT>(peek(W, p), P);
-        if (p + (unsigned long long)l > nb) { p = ce; break; }     // the stream's last (padding) bits
-        const uint32_t r = (uint32_t)(p - cs);
-        mk[r >> 5] |= 1u << (r & 31);
+        const int l = tok_len<CT>(peekS(S, p), P);
+        if (p + (uint32_t)l > lim) { p = ce; break; }                  // the stream's last (padding) bits
+        const uint32_t r = p - cs;
+        if (r < MB) mk[r >> 5] |= 1u << (r & 31);
         cnt0++;
-        p += (unsigned long long)l;
+        p += (uint32_t)l;
     }
-    const uint32_t exit0 = (uint32_t)(p - ce);
-    uint32_t* mo = map + c * 64;
-    mo[0] = exit0 | (cnt0 << 8);
+    const uint32_t exit0 = p - ce;
+    map[c] = exit0 | (cnt0 << 8);
     for (int e = 1; e < 64; e++) {
         uint32_t q = (uint32_t)e, cnt = 0, ex = 0;
         while (true) {
             if (q >= CB) { ex = q - CB; break; }
-            if (cs + q >= nb) { ex = 0; break; }
-            if ((mk[q >> 5] >> (q & 31)) & 1u) {                   // joined P0: its remaining tokens
+            if (cs + q >= lim) { ex = 0; break; }
+            if (q < MB && ((mk[q >> 5] >> (q & 31)) & 1u)) {            // joined P0: its remaining tokens
                 uint32_t before = __popc(mk[q >> 5] & ((1u << (q & 31)) - 1u));
                 for (uint32_t i = 0; i < (q >> 5); i++) before += __popc(mk[i]);
                 cnt += cnt0 - before;
                 ex = exit0;
                 break;
             }
-            const int l = tok_len<CT>(peek(W, cs + q), P);
-            if (cs + q + (unsigned long long)l > nb) { ex = 0; break; }
+            const int l = tok_len<CT>(peekS(S, cs + q), P);
+            if (cs + q + (uint32_t)l > lim) { ex = 0; break; }
             cnt++;
             q += (uint32_t)l;
         }
-        mo[e] = ex | (cnt << 8);
+        map[(long long)e * mstride + c] = ex | (cnt << 8);
     }
 }
 
 // compose FAN consecutive node maps (level l-1) into one map (level l); one lane per entry
+// (level-1 input = the entry-major chunk maps: node i entry e at in[e * nin_max + i])
 template <typename T>
 __global__ __launch_bounds__(64) void dec_compose(const T* __restrict__ in, long long nin_max,
                                                   const Plan64* __restrict__ pl, long long div,
                                                   unsigned long long* __restrict__ outm) {
+    const bool emaj = sizeof(T) == 4;
     const long long g = blockIdx.x;
     const long long nin = (pl->nchunks + div - 1) / div;         // nodes at the input level
     if (g * FAN >= nin) return;
@@ -419,12 +449,11 @@ __global__ __launch_bounds__(64) void dec_compose(const T* __restrict__ in, long
     unsigned long long cnt = 0;
     const long long end = std::min(nin, (g + 1) * FAN);
     for (long long i = g * FAN; i < end; i++) {
-        const unsigned long long m = (unsigned long long)in[i * 64 + e];
+        const unsigned long long m = (unsigned long long)(emaj ? in[(long long)e * nin_max + i] : in[i * 64 + e]);
         e = (int)(m & 63ull);
         cnt += m >> 8;
     }
     outm[g * 64 + threadIdx.x] = (unsigned long long)e | (cnt << 8);
-    (void)nin_max;
 }
 
 // assign entry / first token of the FAN children of every node (one thread per node)
@@ -432,7 +461,8 @@ template <typename T>
 __global__ void dec_descend(const T* __restrict__ cmap, const Plan64* __restrict__ pl, long long div_child,
                             const uint8_t* __restrict__ pent, const unsigned long long* __restrict__ pbase,
                             uint8_t* __restrict__ cent, unsigned long long* __restrict__ cbase, long long npar_max,
-                            int root) {
+                            int root, long long mstride) {
+    const bool emaj = sizeof(T) == 4;           // chunk maps are entry-major
     const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     const long long nchild = (pl->nchunks + div_child - 1) / div_child;
     if (g >= npar_max || g * FAN >= nchild) return;
@@ -442,7 +472,7 @@ __global__ void dec_descend(const T* __restrict__ cmap, const Plan64* __restrict
     for (long long i = g * FAN; i < end; i++) {
         cent[i] = (uint8_t)e;
         cbase[i] = k;
-        const unsigned long long m = (unsigned long long)cmap[i * 64 + e];
+        const unsigned long long m = (unsigned long long)(emaj ? cmap[(long long)e * mstride + i] : cmap[i * 64 + e]);
         e = (int)(m & 63ull);
         k += m >> 8;
     }
@@ -450,15 +480,22 @@ __global__ void dec_descend(const T* __restrict__ cmap, const Plan64* __restrict
 
 // decode every chunk from its true entry; history kinds: 0 concrete, 1..3 incoming b1..b3, 4 derived
 template <int CT>
-__global__ __launch_bounds__(256) void dec_chunks(const uint32_t* __restrict__ W, const Plan64* __restrict__ pl, P64 P,
-                                                  const uint8_t* __restrict__ cent,
-                                                  const unsigned long long* __restrict__ cbase, double* __restrict__ out,
-                                                  long long num, uint16_t* __restrict__ pend, uint8_t* __restrict__ thru,
-                                                  unsigned* __restrict__ err) {
-    const long long c = blockIdx.x * 256ll + threadIdx.x;
+__global__ __launch_bounds__(64) void dec_chunks(const uint32_t* __restrict__ W, const Plan64* __restrict__ pl, P64 P,
+                                                 const uint8_t* __restrict__ cent,
+                                                 const unsigned long long* __restrict__ cbase, double* __restrict__ out,
+                                                 long long num, uint16_t* __restrict__ pend, uint8_t* __restrict__ thru,
+                                                 unsigned* __restrict__ err) {
+    __shared__ uint32_t S[SW];
+    const long long g0 = blockIdx.x * 64ll;
+    if (g0 >= pl->nchunks) return;
+    stage_group(S, W, g0 * MAPW, pl->nwords + 4);
+    __syncthreads();
+    const long long c = g0 + threadIdx.x;
     if (c >= pl->nchunks) return;
-    const unsigned long long nb = pl->nbits, cs = (unsigned long long)c * CB, ce = cs + CB;
-    unsigned long long p = cs + cent[c];
+    const long long avail = (long long)pl->nbits - g0 * CB;
+    const uint32_t nb = (uint32_t)std::min(avail, (long long)(64 * CB + 64));
+    const uint32_t cs = threadIdx.x * CB, ce = cs + CB;
+    uint32_t p = cs + cent[c];
     const long long k0 = (long long)cbase[c];
     double f1 = -1.0, f2 = -1.0, f3 = -1.0;
     int q1 = c ? 1 : 0, q2 = c ? 2 : 0, q3 = c ? 3 : 0;
@@ -466,9 +503,9 @@ __global__ __launch_bounds__(256) void dec_chunks(const uint32_t* __restrict__ W
     bool bad = false;
     long long j = 0;
     while (p < ce && k0 + j < num) {
-        const uint64_t win = peek(W, p);
+        const uint64_t win = peekS(S, p);
         const int l = tok_len<CT>(win, P);
-        if (p + (unsigned long long)l > nb) break;
+        if (p + (uint32_t)l > nb) break;
         double v;
         int q = 0;
         if (CT != 6 && (win >> 63)) {
@@ -487,7 +524,7 @@ __global__ __launch_bounds__(256) void dec_chunks(const uint32_t* __restrict__ W
             bad |= d2u(v) == 0xBFF0000000000000ull;                        // the -1.0 history sentinel
         }
         f3 = f2; q3 = q2; f2 = f1; q2 = q1; f1 = v; q1 = q;
-        p += (unsigned long long)l;
+        p += (uint32_t)l;
         j++;
     }
     pend[c] = (uint16_t)pd;
@@ -526,7 +563,8 @@ __global__ __launch_bounds__(256) void dec_fix(const uint32_t* __restrict__ W, c
                                                double* __restrict__ out, const uint16_t* __restrict__ pend,
                                                const uint8_t* __restrict__ thru, unsigned* __restrict__ err) {
     const long long c = blockIdx.x * 256ll + threadIdx.x;
-    if (c <= 0 || c >= pl->nchunks || pend[c] == 0 || thru[c - 1]) return;
+    if (c <= 0 || c >= pl->nchunks || pend[c] == 0) return;
+    if (thru[c - 1]) { atomicAdd(err + 1, 1u); return; }             // left to the ordered pass
     const long long k0 = (long long)cbase[c];
     if (k0 < 3) { atomicOr(err, ERR_SERIAL); return; }
     if (redecode_prefix<CT>(W, P, (unsigned long long)c * CB + cent[c], pend[c], out, k0)) atomicOr(err, ERR_SERIAL);
@@ -540,6 +578,7 @@ __global__ __launch_bounds__(64) void dec_fix_serial(const uint32_t* __restrict_
                                                      const uint16_t* __restrict__ pend, const uint8_t* __restrict__ thru,
                                                      unsigned* __restrict__ err) {
     const long long nc = pl->nchunks;
+    if (err[1] == 0) return;                                         // no chain crosses a whole chunk
     for (long long b = 1; b < nc; b += 64) {
         const long long c = b + threadIdx.x;
         const bool need = c < nc && pend[c] != 0 && thru[c - 1];
@@ -854,12 +893,12 @@ extern "C" int dc64_decode_device(int ct, const void* d_stream, long long nbytes
     uint16_t* pend = (uint16_t*)(base + Lo.off_pend);
     uint8_t* thru = (uint8_t*)(base + Lo.off_thru);
     double* out = (double*)d_out;
-    H64(hipMemsetAsync(C64.d_err, 0, 4, st));
+    H64(hipMemsetAsync(C64.d_err, 0, 8, st));
     hipLaunchKernelGGL(dec_plan, dim3(1), dim3(1), 0, st, C64.plan, d_nbits, (unsigned long long)nbytes * 8ull, max_chunks,
                        C64.d_err);
     hipLaunchKernelGGL(dec_stage, dim3((unsigned)std::min<long long>((max_words + 255) / 256, 4096)), dim3(256), 0, st,
                        (const uint8_t*)d_stream, C64.plan, W, max_words + 8);
-    DISPATCH64(ct, dec_map, dim3((unsigned)((max_chunks + 63) / 64)), dim3(64), 0, st, W, C64.plan, P, map);
+    DISPATCH64(ct, dec_map, dim3((unsigned)((max_chunks + 63) / 64)), dim3(64), 0, st, W, C64.plan, P, map, max_chunks);
     // compose upwards: level l nodes cover FAN^l chunks
     long long div = 1;
     for (int l = 1; l <= Lo.nlev; l++) {
@@ -882,16 +921,16 @@ extern "C" int dc64_decode_device(int ct, const void* d_stream, long long nbytes
         const unsigned g = (unsigned)((Lo.nnode[l] + 63) / 64);
         if (l == 1)
             hipLaunchKernelGGL(dec_descend<uint32_t>, dim3(g), dim3(64), 0, st, map, C64.plan, div, pent, pbase, cent,
-                               cbase, Lo.nnode[l], l == Lo.nlev ? 1 : 0);
+                               cbase, Lo.nnode[l], l == Lo.nlev ? 1 : 0, max_chunks);
         else
             hipLaunchKernelGGL(dec_descend<unsigned long long>, dim3(g), dim3(64), 0, st,
                                (const unsigned long long*)(base + Lo.off_lmap[l - 1]), C64.plan, div, pent, pbase, cent,
-                               cbase, Lo.nnode[l], l == Lo.nlev ? 1 : 0);
+                               cbase, Lo.nnode[l], l == Lo.nlev ? 1 : 0, max_chunks);
     }
     const uint8_t* cent = (const uint8_t*)(base + Lo.off_ent[0]);
     const unsigned long long* cbase = (const unsigned long long*)(base + Lo.off_base[0]);
     const unsigned gc = (unsigned)((max_chunks + 255) / 256);
-    DISPATCH64(ct, dec_chunks, dim3(gc), dim3(256), 0, st, W, C64.plan, P, cent, cbase, out, num, pend, thru, C64.d_err);
+    DISPATCH64(ct, dec_chunks, dim3((unsigned)((max_chunks + 63) / 64)), dim3(64), 0, st, W, C64.plan, P, cent, cbase, out, num, pend, thru, C64.d_err);
     DISPATCH64(ct, dec_fix, dim3(gc), dim3(256), 0, st, W, C64.plan, P, cent, cbase, out, pend, thru, C64.d_err);
     DISPATCH64(ct, dec_fix_serial, dim3(1), dim3(64), 0, st, W, C64.plan, P, cent, cbase, out, pend, thru, C64.d_err);
     H64(hipMemsetAsync(C64.d_total + 1, 0xFF, 8, st));
