@@ -436,6 +436,142 @@ __global__ __launch_bounds__(64) void dec_map(const uint32_t* __restrict__ W, co
 }
 
 // compose FAN consecutive node maps (level l-1) into one map (level l); one lane per entry
+// ---- fast path: speculative entries.  Lane c pre-walks the previous chunk from its bit 0 (any start
+// synchronises with the true token boundaries with high probability within one chunk of random data)
+// and so arrives at chunk c with a speculative entry se[c]; it then walks chunk c: exit sx[c], tokens
+// sn[c].  The entries are right when every link holds: sx[c-1] == se[c] (chunk 0 starts at bit 0).
+constexpr int OVB = CB;                     // pre-walk overlap (bits)
+constexpr int OVW = OVB / 32;
+constexpr int GWS = OVW + 64 * MAPW + 8;
+constexpr int SWS = GWS + GWS / 64 + 2;
+
+template <int CT>
+__global__ __launch_bounds__(64) void dec_spec(const uint32_t* __restrict__ W, const Plan64* __restrict__ pl, P64 P,
+                                               uint8_t* __restrict__ se, uint8_t* __restrict__ sx,
+                                               uint16_t* __restrict__ sn) {
+    __shared__ uint32_t S[SWS];
+    const long long g0 = blockIdx.x * 64ll;
+    const long long nc = pl->nchunks;
+    if (g0 >= nc) return;
+    const long long w0 = g0 * MAPW - OVW, wlim = pl->nwords + 4;
+    for (int i = threadIdx.x; i < GWS; i += 64) {
+        const long long w = w0 + i;
+        S[sidx(i)] = (w >= 0 && w < wlim) ? W[w] : 0u;
+    }
+    __syncthreads();
+    const long long c = g0 + threadIdx.x;
+    if (c >= nc) return;
+    const long long avail = (long long)pl->nbits - (g0 * CB - OVB);         // stream bits from S's origin
+    const uint32_t lim = (uint32_t)std::min(avail, (long long)(OVB + 64 * CB + 64));
+    const uint32_t cs = OVB + threadIdx.x * CB, ce = cs + CB;
+    uint32_t p = c == 0 ? cs : cs - OVB;
+    while (p < cs) p += (uint32_t)tok_len<CT>(peekS(S, p), P);
+    const uint32_t e = p - cs;
+    uint32_t n = 0;
+    while (p < ce) {
+        const int l = tok_len<CT>(peekS(S, p), P);
+        if (p + (uint32_t)l > lim) { p = ce; break; }
+        n++;
+        p += (uint32_t)l;
+    }
+    se[c] = (uint8_t)e;
+    sx[c] = (uint8_t)(p - ce);
+    sn[c] = (uint16_t)n;
+}
+
+// broken links: bad[c] = sx[c-1] != se[c]; ctr[0] counts them
+__global__ __launch_bounds__(256) void dec_links(const Plan64* __restrict__ pl, const uint8_t* __restrict__ se,
+                                                 const uint8_t* __restrict__ sx, uint8_t* __restrict__ bad,
+                                                 unsigned* __restrict__ ctr) {
+    const long long c = blockIdx.x * 256ll + threadIdx.x;
+    if (c >= pl->nchunks) return;
+    const bool b = c > 0 && sx[c - 1] != se[c];
+    bad[c] = b ? 1 : 0;
+    if (b) atomicAdd(ctr, 1u);
+}
+
+// one repair round: a chunk with a broken link whose predecessor's link holds takes the predecessor's
+// exit as its entry and walks again (chains of broken links advance one chunk per round)
+template <int CT>
+__global__ __launch_bounds__(256) void dec_relink(const uint32_t* __restrict__ W, const Plan64* __restrict__ pl, P64 P,
+                                                  uint8_t* __restrict__ se, uint8_t* __restrict__ sx,
+                                                  uint16_t* __restrict__ sn, const uint8_t* __restrict__ bad,
+                                                  const unsigned* __restrict__ ctr) {
+    if (*ctr == 0) return;
+    const long long c = blockIdx.x * 256ll + threadIdx.x;
+    if (c <= 0 || c >= pl->nchunks || !bad[c] || bad[c - 1]) return;
+    const unsigned long long nb = pl->nbits, cs = (unsigned long long)c * CB, ce = cs + CB;
+    const int t = sx[c - 1];
+    unsigned long long p = cs + (unsigned long long)t;
+    uint32_t n = 0;
+    while (p < ce) {
+        const int l = tok_len<CT>(peek(W, p), P);
+        if (p + (unsigned long long)l > nb) { p = ce; break; }
+        n++;
+        p += (unsigned long long)l;
+    }
+    se[c] = (uint8_t)t;
+    sx[c] = (uint8_t)(p - ce);
+    sn[c] = (uint16_t)n;
+}
+
+// exclusive scan of the chunk token counts -> first token index of every chunk (3 launches)
+__global__ __launch_bounds__(1024) void cnt_scan_part(const Plan64* __restrict__ pl, const uint16_t* __restrict__ sn,
+                                                      unsigned long long* __restrict__ base,
+                                                      unsigned long long* __restrict__ psum) {
+    __shared__ unsigned long long ws[16];
+    const long long c = blockIdx.x * 1024ll + threadIdx.x;
+    if (blockIdx.x * 1024ll >= pl->nchunks) return;
+    const unsigned long long v = c < pl->nchunks ? sn[c] : 0ull;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    unsigned long long s = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long o = __shfl_up(s, d, 64);
+        if (lane >= d) s += o;
+    }
+    if (lane == 63) ws[wv] = s;
+    __syncthreads();
+    unsigned long long pre = 0, tot = 0;
+    for (int i = 0; i < 16; i++) { if (i < wv) pre += ws[i]; tot += ws[i]; }
+    if (c < pl->nchunks) base[c] = pre + s - v;
+    if (threadIdx.x == 0) psum[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(1024) void cnt_scan_top(const Plan64* __restrict__ pl, unsigned long long* __restrict__ psum) {
+    __shared__ unsigned long long ws[16];
+    __shared__ unsigned long long carry;
+    const long long nb = (pl->nchunks + 1023) / 1024;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (long long b = 0; b < nb; b += 1024) {
+        const long long i = b + threadIdx.x;
+        const unsigned long long v = i < nb ? psum[i] : 0ull;
+        unsigned long long s = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const unsigned long long o = __shfl_up(s, d, 64);
+            if (lane >= d) s += o;
+        }
+        if (lane == 63) ws[wv] = s;
+        __syncthreads();
+        unsigned long long pre = 0;
+        for (int k = 0; k < wv; k++) pre += ws[k];
+        const unsigned long long off = carry + pre + s - v;
+        if (i < nb) psum[i] = off;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry = off + v;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(1024) void cnt_scan_add(const Plan64* __restrict__ pl, const unsigned long long* __restrict__ psum,
+                                                     unsigned long long* __restrict__ base) {
+    const long long c = blockIdx.x * 1024ll + threadIdx.x;
+    if (c < pl->nchunks) base[c] += psum[blockIdx.x];
+}
+
 // (level-1 input = the entry-major chunk maps: node i entry e at in[e * nin_max + i])
 template <typename T>
 __global__ __launch_bounds__(64) void dec_compose(const T* __restrict__ in, long long nin_max,
@@ -738,7 +874,8 @@ struct Ctx64 {
     unsigned long long* h = nullptr;        // pinned: [0] total bits [1] err [2] ndec
     // pre-passes
     double* pv = nullptr; long long* pi = nullptr; double* d_f = nullptr; int* d_i = nullptr;
-    int dec_pending = 0, dec_ct = 0;
+    int dec_pending = 0, dec_ct = 0, map_fallback = 0;
+    unsigned* ctr = nullptr;
     long long dec_num = 0;
 };
 Ctx64 C64;
@@ -762,6 +899,7 @@ int ensure64(hipStream_t* st) {
         H64(hipMalloc((void**)&C64.pi, 1024 * sizeof(long long)));
         H64(hipMalloc((void**)&C64.d_f, 64));
         H64(hipMalloc((void**)&C64.d_i, 64));
+        H64(hipMalloc((void**)&C64.ctr, 64));
     }
     return DC_OK;
 }
@@ -840,7 +978,7 @@ namespace {
 struct DecLayout {
     int nlev;                       // levels above the chunks (the last one has a single node)
     long long nnode[8];             // max nodes per level (0 = chunks)
-    size_t off_w, off_map, off_lmap[8], off_ent[8], off_base[8], off_pend, off_thru, total;
+    size_t off_w, off_map, off_lmap[8], off_ent[8], off_base[8], off_sx, off_sn, off_bad, off_psum, off_pend, off_thru, total;
 };
 DecLayout layout(long long max_words, long long max_chunks) {
     DecLayout Lo{};
@@ -860,6 +998,10 @@ DecLayout layout(long long max_words, long long max_chunks) {
         if (l == 7) break;
     }
     Lo.nlev = l;
+    Lo.off_sx = take((size_t)max_chunks);
+    Lo.off_sn = take((size_t)max_chunks * 2);
+    Lo.off_bad = take((size_t)max_chunks);
+    Lo.off_psum = take((size_t)((max_chunks + 1023) / 1024 + 1) * 8);
     Lo.off_pend = take((size_t)max_chunks * 2);
     Lo.off_thru = take((size_t)max_chunks);
     Lo.total = o;
@@ -898,6 +1040,30 @@ extern "C" int dc64_decode_device(int ct, const void* d_stream, long long nbytes
                        C64.d_err);
     hipLaunchKernelGGL(dec_stage, dim3((unsigned)std::min<long long>((max_words + 255) / 256, 4096)), dim3(256), 0, st,
                        (const uint8_t*)d_stream, C64.plan, W, max_words + 8);
+    uint8_t* se = (uint8_t*)(base + Lo.off_ent[0]);
+    uint8_t* sx = (uint8_t*)(base + Lo.off_sx);
+    uint16_t* sn = (uint16_t*)(base + Lo.off_sn);
+    uint8_t* bad = (uint8_t*)(base + Lo.off_bad);
+    unsigned long long* cb0 = (unsigned long long*)(base + Lo.off_base[0]);
+    const unsigned g64 = (unsigned)((max_chunks + 63) / 64), g256 = (unsigned)((max_chunks + 255) / 256);
+    const unsigned g1k = (unsigned)((max_chunks + 1023) / 1024);
+    constexpr int ROUNDS = 4;
+    H64(hipMemsetAsync(C64.ctr, 0, sizeof(unsigned) * (ROUNDS + 1), st));
+    DISPATCH64(ct, dec_spec, dim3(g64), dim3(64), 0, st, W, C64.plan, P, se, sx, sn);
+    for (int r = 0; r <= ROUNDS; r++) {
+        hipLaunchKernelGGL(dec_links, dim3(g256), dim3(256), 0, st, C64.plan, se, sx, bad, C64.ctr + r);
+        if (r < ROUNDS) DISPATCH64(ct, dec_relink, dim3(g256), dim3(256), 0, st, W, C64.plan, P, se, sx, sn, bad, C64.ctr + r);
+    }
+    H64(hipMemcpyAsync(C64.h + 6, C64.ctr + ROUNDS, 4, hipMemcpyDeviceToHost, st));
+    H64(hipStreamSynchronize(st));
+    const unsigned broken = (unsigned)C64.h[6];
+    C64.map_fallback = broken != 0;
+    if (!broken) {
+        unsigned long long* psum = (unsigned long long*)(base + Lo.off_psum);
+        hipLaunchKernelGGL(cnt_scan_part, dim3(g1k), dim3(1024), 0, st, C64.plan, sn, cb0, psum);
+        hipLaunchKernelGGL(cnt_scan_top, dim3(1), dim3(1024), 0, st, C64.plan, psum);
+        hipLaunchKernelGGL(cnt_scan_add, dim3(g1k), dim3(1024), 0, st, C64.plan, psum, cb0);
+    } else {
     DISPATCH64(ct, dec_map, dim3((unsigned)((max_chunks + 63) / 64)), dim3(64), 0, st, W, C64.plan, P, map, max_chunks);
     // compose upwards: level l nodes cover FAN^l chunks
     long long div = 1;
@@ -926,6 +1092,7 @@ extern "C" int dc64_decode_device(int ct, const void* d_stream, long long nbytes
             hipLaunchKernelGGL(dec_descend<unsigned long long>, dim3(g), dim3(64), 0, st,
                                (const unsigned long long*)(base + Lo.off_lmap[l - 1]), C64.plan, div, pent, pbase, cent,
                                cbase, Lo.nnode[l], l == Lo.nlev ? 1 : 0, max_chunks);
+    }
     }
     const uint8_t* cent = (const uint8_t*)(base + Lo.off_ent[0]);
     const unsigned long long* cbase = (const unsigned long long*)(base + Lo.off_base[0]);
@@ -958,7 +1125,10 @@ extern "C" int dc64_decode_finish(void) {
     return DC_OK;
 }
 
-extern "C" unsigned dc64_last_decode_flags(void) { return C64.h ? (unsigned)C64.h[1] : 0u; }
+// bit 0: the exact serial decoder ran; bit 1: speculative entries failed, the chunk-map path ran
+extern "C" unsigned dc64_last_decode_flags(void) {
+    return (C64.h ? ((unsigned)C64.h[1] & ERR_SERIAL) : 0u) | (C64.map_fallback ? 2u : 0u);
+}
 
 extern "C" int dc64_to_small_device(const void* d_x, long long n, void* d_out, double* min_out) {
     hipStream_t st;

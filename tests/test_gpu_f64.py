@@ -173,3 +173,18 @@ def test_device_api64_chained(dc, oracle):
     ref, _ = oracle.decompress64(7, so, n, bound, t, m20)
     assert np.array_equal(out.cpu().numpy().view(np.uint64), ref.view(np.uint64))
     assert flags == 0                        # the parallel path decoded it (no exact serial fallback)
+
+
+def test_decode64_paths(dc, oracle):
+    """Random data decodes on the speculative-entry path; a constant input (a periodic '100' stream whose
+    misaligned parses never resynchronise) takes the chunk-map path -- both bit-exact."""
+    bound = 1e-3
+    dc.set_bound(bound)
+    for x, want in ((oracle.gen_u10_64(1 << 19), 0), (np.full(1 << 19, 0.123456789), 2)):
+        mn, xs = oracle.to_small64(x)
+        s, nb, pos = dc.compress64(5, xs)
+        d = dc.decompress64(5, s, xs.size)
+        flags = int(dc.L.dc64_last_decode_flags())
+        ref, _ = oracle.decompress64(5, s, xs.size, bound)
+        assert np.array_equal(d.view(np.uint64), ref.view(np.uint64))
+        assert flags & 2 == want, flags
