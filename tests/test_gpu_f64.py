@@ -175,16 +175,24 @@ def test_device_api64_chained(dc, oracle):
     assert flags == 0                        # the parallel path decoded it (no exact serial fallback)
 
 
-def test_decode64_paths(dc, oracle):
-    """Random data decodes on the speculative-entry path; a constant input (a periodic '100' stream whose
-    misaligned parses never resynchronise) takes the chunk-map path -- both bit-exact."""
+def test_decode64_paths(dc, oracle, monkeypatch):
+    """Random data decodes on the speculative-entry path (flags 0); the chunk-map path (forced with
+    DC64_FORCE_MAP=1, taken by itself when link repair does not converge) decodes the same streams --
+    U10, a constant input (periodic '100' stream) and '101' runs -- bit-exactly."""
     bound = 1e-3
     dc.set_bound(bound)
-    for x, want in ((oracle.gen_u10_64(1 << 19), 0), (np.full(1 << 19, 0.123456789), 2)):
-        mn, xs = oracle.to_small64(x)
-        s, nb, pos = dc.compress64(5, xs)
-        d = dc.decompress64(5, s, xs.size)
-        flags = int(dc.L.dc64_last_decode_flags())
-        ref, _ = oracle.decompress64(5, s, xs.size, bound)
-        assert np.array_equal(d.view(np.uint64), ref.view(np.uint64))
-        assert flags & 2 == want, flags
+    rs = np.random.RandomState(8)
+    cases = [oracle.gen_u10_64(1 << 19), np.full(1 << 19, 0.123456789), np.repeat(rs.rand(1 << 10) * 7.0, 512)]
+    for force in ("0", "1"):
+        monkeypatch.setenv("DC64_FORCE_MAP", force)
+        for i, x in enumerate(cases):
+            mn, xs = oracle.to_small64(x)
+            s, nb, pos = dc.compress64(5, xs)
+            d = dc.decompress64(5, s, xs.size)
+            flags = int(dc.L.dc64_last_decode_flags())
+            ref, _ = oracle.decompress64(5, s, xs.size, bound)
+            assert np.array_equal(d.view(np.uint64), ref.view(np.uint64)), (force, i)
+            if force == "1":
+                assert flags & 2, flags
+            elif i == 0:
+                assert flags == 0, flags
