@@ -492,24 +492,39 @@ __global__ __launch_bounds__(256) void dec_links(const Plan64* __restrict__ pl, 
 }
 
 // one repair round: a chunk with a broken link whose predecessor's link holds takes the predecessor's
-// exit as its entry and walks again (chains of broken links advance one chunk per round)
+// exit as its entry and walks again (chains of broken links advance one chunk per round).  64 chunks
+// per workgroup, their words staged in LDS like dec_spec.
 template <int CT>
-__global__ __launch_bounds__(256) void dec_relink(const uint32_t* __restrict__ W, const Plan64* __restrict__ pl, P64 P,
-                                                  uint8_t* __restrict__ se, uint8_t* __restrict__ sx,
-                                                  uint16_t* __restrict__ sn, const uint8_t* __restrict__ bad,
-                                                  const unsigned* __restrict__ ctr) {
+__global__ __launch_bounds__(64) void dec_relink(const uint32_t* __restrict__ W, const Plan64* __restrict__ pl, P64 P,
+                                                 uint8_t* __restrict__ se, uint8_t* __restrict__ sx,
+                                                 uint16_t* __restrict__ sn, const uint8_t* __restrict__ bad,
+                                                 const unsigned* __restrict__ ctr) {
+    __shared__ uint32_t S[SW];
+    __shared__ int any;
     if (*ctr == 0) return;
-    const long long c = blockIdx.x * 256ll + threadIdx.x;
-    if (c <= 0 || c >= pl->nchunks || !bad[c] || bad[c - 1]) return;
-    const unsigned long long nb = pl->nbits, cs = (unsigned long long)c * CB, ce = cs + CB;
+    const long long g0 = blockIdx.x * 64ll;
+    const long long nc = pl->nchunks;
+    if (g0 >= nc) return;
+    const long long c = g0 + threadIdx.x;
+    const bool mine = c > 0 && c < nc && bad[c] && !bad[c - 1];
+    if (threadIdx.x == 0) any = 0;
+    __syncthreads();
+    if (mine) any = 1;
+    __syncthreads();
+    if (!any) return;
+    stage_group(S, W, g0 * MAPW, pl->nwords + 4);
+    __syncthreads();
+    if (!mine) return;
+    const long long avail = (long long)pl->nbits - g0 * CB;
+    const uint32_t lim = (uint32_t)std::min(avail, (long long)(64 * CB + 64));
+    const uint32_t cs = threadIdx.x * CB, ce = cs + CB;
     const int t = sx[c - 1];
-    unsigned long long p = cs + (unsigned long long)t;
-    uint32_t n = 0;
+    uint32_t p = cs + (uint32_t)t, n = 0;
     while (p < ce) {
-        const int l = tok_len<CT>(peek(W, p), P);
-        if (p + (unsigned long long)l > nb) { p = ce; break; }
+        const int l = tok_len<CT>(peekS(S, p), P);
+        if (p + (uint32_t)l > lim) { p = ce; break; }
         n++;
-        p += (unsigned long long)l;
+        p += (uint32_t)l;
     }
     se[c] = (uint8_t)t;
     sx[c] = (uint8_t)(p - ce);
@@ -876,6 +891,7 @@ struct Ctx64 {
     // pre-passes
     double* pv = nullptr; long long* pi = nullptr; double* d_f = nullptr; int* d_i = nullptr;
     int dec_pending = 0, dec_ct = 0, map_fallback = 0;
+    long long dbg_words = 0, dbg_chunks = 0;
     unsigned* ctr = nullptr;
     long long dec_num = 0;
 };
@@ -979,7 +995,7 @@ namespace {
 struct DecLayout {
     int nlev;                       // levels above the chunks (the last one has a single node)
     long long nnode[8];             // max nodes per level (0 = chunks)
-    size_t off_w, off_map, off_lmap[8], off_ent[8], off_base[8], off_sx, off_sn, off_bad, off_psum, off_pend, off_thru, total;
+    size_t off_w, off_map, off_lmap[8], off_ent[8], off_base[8], off_sx, off_sn, off_bad, off_rl, off_psum, off_pend, off_thru, total;
 };
 DecLayout layout(long long max_words, long long max_chunks) {
     DecLayout Lo{};
@@ -1002,6 +1018,7 @@ DecLayout layout(long long max_words, long long max_chunks) {
     Lo.off_sx = take((size_t)max_chunks);
     Lo.off_sn = take((size_t)max_chunks * 2);
     Lo.off_bad = take((size_t)max_chunks);
+    Lo.off_rl = take((size_t)max_chunks);
     Lo.off_psum = take((size_t)((max_chunks + 1023) / 1024 + 1) * 8);
     Lo.off_pend = take((size_t)max_chunks * 2);
     Lo.off_thru = take((size_t)max_chunks);
@@ -1024,6 +1041,8 @@ extern "C" int dc64_decode_device(int ct, const void* d_stream, long long nbytes
     const long long max_chunks = (max_bytes * 8 + CB - 1) / CB;
     if (max_chunks > (1ll << 36)) return dc_set_error(DC_ERR_ARG, "stream too large");
     const DecLayout Lo = layout(max_words, max_chunks);
+    C64.dbg_words = max_words;
+    C64.dbg_chunks = max_chunks;
     if (Lo.total > C64.pool_cap) {
         if (C64.pool) (void)hipFree(C64.pool);
         C64.pool = nullptr; C64.pool_cap = 0;
@@ -1053,7 +1072,7 @@ extern "C" int dc64_decode_device(int ct, const void* d_stream, long long nbytes
     DISPATCH64(ct, dec_spec, dim3(g64), dim3(64), 0, st, W, C64.plan, P, se, sx, sn);
     for (int r = 0; r <= ROUNDS; r++) {
         hipLaunchKernelGGL(dec_links, dim3(g256), dim3(256), 0, st, C64.plan, se, sx, bad, C64.ctr + r);
-        if (r < ROUNDS) DISPATCH64(ct, dec_relink, dim3(g256), dim3(256), 0, st, W, C64.plan, P, se, sx, sn, bad, C64.ctr + r);
+        if (r < ROUNDS) DISPATCH64(ct, dec_relink, dim3(g64), dim3(64), 0, st, W, C64.plan, P, se, sx, sn, bad, C64.ctr + r);
     }
     H64(hipMemcpyAsync(C64.h + 6, C64.ctr + ROUNDS, 4, hipMemcpyDeviceToHost, st));
     H64(hipStreamSynchronize(st));
@@ -1125,6 +1144,27 @@ extern "C" int dc64_decode_finish(void) {
     if ((err & ERR_SERIAL) && C64.h[2] != ~0ull && (long long)C64.h[2] < C64.dec_num)
         return dc_set_error(DC_ERR_STREAM, "double decode: stream holds fewer tokens than num");
     return DC_OK;
+}
+
+// debug: the last decode's chunk records (entry, exit, count, first token) -> host arrays
+extern "C" long long dc64_debug_chunks(uint8_t* e, uint8_t* x, uint16_t* n, unsigned long long* b, long long cap) {
+    hipStream_t st;
+    if (ensure64(&st)) return -1;
+    Plan64 pl;
+    if (hipMemcpy(&pl, C64.plan, sizeof pl, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    const long long nc = std::min(pl.nchunks, cap < 0 ? -cap : cap);
+    const DecLayout Lo = layout(C64.dbg_words, C64.dbg_chunks);
+    char* base = (char*)C64.pool;
+    (void)hipMemcpy(e, base + Lo.off_ent[0], nc, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(x, base + Lo.off_sx, nc, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(n, base + Lo.off_sn, nc * 2, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(b, base + Lo.off_base[0], nc * 8, hipMemcpyDeviceToHost);
+    if (cap < 0) (void)hipMemcpy(e, base + Lo.off_rl, nc, hipMemcpyDeviceToHost);
+    return nc;
+}
+
+extern "C" int dc64_debug_ctr(unsigned* out) {
+    return hipMemcpy(out, C64.ctr, 5 * sizeof(unsigned), hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 
 // bit 0: the exact serial decoder ran; bit 1: speculative entries failed, the chunk-map path ran

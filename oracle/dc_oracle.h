@@ -85,6 +85,8 @@ void orc64_compress(int ct, const double* data, long num, double bound, int type
 long orc64_decompress_spec(int ct, const unsigned char* bits, long bytes, long num, double bound,
                            int type, uint32_t mask20, double* out);
 void orc64_gen_u10(double* out, long n, uint64_t seed, long offset);
+long orc64_chunk_records(int ct, const unsigned char* s, long bytes, long num, double bound, int type,
+                         uint32_t mask20, long cb, unsigned char* ent, unsigned char* ex, unsigned short* cnt);
 
 /* Synthetic inputs: U10 counter-based splitmix64, HIMENO-L plane. */
 void orc_gen_u10(float* out, long n, uint64_t seed, long offset);

@@ -231,3 +231,32 @@ void orc64_gen_u10(double* out, long n, uint64_t seed, long offset) {
         out[i] = (double)(z >> 11) * 0x1p-53 * 10.0;
     }
 }
+
+/* Test helper: the true token boundaries of a double stream cut into chunks of cb bits -- for every
+ * chunk the entry offset of its first token, the tokens starting in it and its exit into the next. */
+long orc64_chunk_records(int ct, const unsigned char* s, long bytes, long num, double bound, int type,
+                         uint32_t mask20, long cb, unsigned char* ent, unsigned char* ex, unsigned short* cnt) {
+    const int B = orc_bound_binary(bound);
+    const long nbits = bytes * 8;
+    const int mm = orc64_mbits(B, (int)((mask20 >> 8) & 0x7FF));
+    const long nc = (nbits + cb - 1) / cb;
+    for (long c = 0; c < nc; c++) { ent[c] = 0; ex[c] = 0; cnt[c] = 0; }
+    long p = 0, n = 0;
+    int started = -1;
+    while (n < num && p < nbits) {
+        int len;
+        if (ct != 6 && get_bit(s, p)) len = 3;
+        else if (ct == 11) len = 64;
+        else if (ct == 7 && get_bits(s, nbits, p + 1, type) == (1ull << type) - 1ull)
+            len = type + 2 + (get_bits(s, nbits, p + 1 + type, 1) ? mm : (mm > 8 ? mm - 8 : 0));
+        else len = 12 + orc64_mbits(B, (int)get_bits(s, nbits, p + 1, 11));
+        if (p + len > nbits) break;
+        const long c = p / cb;
+        if (c != started) { ent[c] = (unsigned char)(p - c * cb); started = (int)c; }
+        cnt[c]++;
+        if ((p + len) / cb != c && c + 1 < nc) ex[c] = (unsigned char)(p + len - (c + 1) * cb);
+        p += len;
+        n++;
+    }
+    return nc;
+}
