@@ -9,7 +9,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "dc_shared.h"
 #include "../../include/dc_gpu.h"
+
+int dc_set_error(int code, const char* msg);
 
 /* device staging buffers of this file */
 static void* g_a; static size_t g_a_cap;
@@ -137,4 +140,124 @@ double med_dataset_double(double* data, int num, int* type) {
         (rc = dc64_med_device(g_a, num, &mean, type)))
         fail("med_dataset_double", rc ? rc : DC_ERR_HIP);
     return mean;
+}
+
+/* ---- CT1 byte-wise codec for doubles (myCompress_double :3815-3941 / myDecompress_double :3778-3813) */
+static void* c_scr; static size_t c_scr_cap;
+static void* c_codes; static size_t c_codes_cap;
+static void* c_pos; static size_t c_pos_cap;
+static unsigned* c_err;
+
+static int c1_setup(long long n, uint32_t** traw, unsigned long long** rawoff, uint8_t** carr) {
+    const long long nt = dc_ct1_tiles(n > 0 ? n : 1);
+    const size_t need = (size_t)(nt + 1) * 8 + (size_t)nt * 4 + 16 + (size_t)n + 64;
+    if (grow(&c_scr, &c_scr_cap, need)) return DC_ERR_HIP;
+    if (!c_err && hipMalloc((void**)&c_err, 64) != hipSuccess) return DC_ERR_HIP;
+    char* p = (char*)c_scr;
+    *rawoff = (unsigned long long*)p;
+    *traw = (uint32_t*)(p + (size_t)(nt + 1) * 8);
+    *carr = (uint8_t*)(p + (size_t)(nt + 1) * 8 + (size_t)nt * 4 + 16);
+    return DC_OK;
+}
+
+/* h:122 c:3815-3941: *array_double / *array_char / *array_char_displacement realloc()ed to the raw and
+ * code counts (untouched when a count is 0, as the reference); returns the raw count */
+int myCompress_double(double data[], double** array_double, char** array_char, int** array_char_displacement, int num) {
+    const char* fn = "myCompress_double";
+    int rc = dc_init(0);
+    if (rc) { fail(fn, rc); return 0; }
+    if (num <= 0) return 0;
+    const size_t n = (size_t)num;
+    const hipStream_t st = (hipStream_t)dc_get_stream();
+    uint32_t* traw; unsigned long long* rawoff; uint8_t* carr;
+    if ((rc = grow(&g_a, &g_a_cap, n * 8 + 64)) || (rc = grow(&g_b, &g_b_cap, n * 8 + 64)) ||
+        (rc = grow(&c_codes, &c_codes_cap, n + 64)) || (rc = grow(&c_pos, &c_pos_cap, n * 4 + 64)) ||
+        (rc = c1_setup(num, &traw, &rawoff, &carr))) { fail(fn, rc); return 0; }
+    unsigned long long h[2] = {0, 0};
+    const long long nt = dc_ct1_tiles(num);
+    if (hipMemcpyAsync(g_a, data, n * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemsetAsync(c_err, 0, 4, st) != hipSuccess ||
+        dc_launch_ct1_encode64((const double*)g_a, num, dc_get_abs_error_bound(), traw, rawoff, (double*)g_b,
+                               (char*)c_codes, (int*)c_pos, c_err, st) ||
+        hipMemcpyAsync(&h[0], rawoff + nt, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(&h[1], c_err, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) { fail(fn, DC_ERR_HIP); return 0; }
+    if (h[1] & 1u) { fail(fn, dc_set_error(DC_ERR_INPUT, "input contains -1.0 (the reference's history sentinel)")); return 0; }
+    const long long nraw = (long long)h[0], nc = num - nraw;
+    if (nraw > 0) {
+        double* a = (double*)realloc(*array_double, sizeof(double) * (size_t)nraw);
+        if (!a) { fail(fn, DC_ERR_ARG); return 0; }
+        *array_double = a;
+        if (hipMemcpy(a, g_b, sizeof(double) * (size_t)nraw, hipMemcpyDeviceToHost) != hipSuccess) { fail(fn, DC_ERR_HIP); return 0; }
+    }
+    if (nc > 0) {
+        char* c = (char*)realloc(*array_char, (size_t)nc);
+        int* p = (int*)realloc(*array_char_displacement, sizeof(int) * (size_t)nc);
+        if (!c || !p) { fail(fn, DC_ERR_ARG); return 0; }
+        *array_char = c;
+        *array_char_displacement = p;
+        if (hipMemcpy(c, c_codes, (size_t)nc, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(p, c_pos, sizeof(int) * (size_t)nc, hipMemcpyDeviceToHost) != hipSuccess) { fail(fn, DC_ERR_HIP); return 0; }
+    }
+    return (int)nraw;
+}
+
+/* h:123 c:3778-3813; the code count is taken as in myDecompress (dc_host.c): entries while they increase
+ * and stay within [1, num] */
+double* myDecompress_double(double array_double[], char array_char[], int array_char_displacement[], int num) {
+    const char* fn = "myDecompress_double";
+    double* out = (double*)malloc(sizeof(double) * (size_t)(num > 0 ? num : 1));
+    int rc = dc_init(0);
+    if (rc) { fail(fn, rc); return out; }
+    if (num <= 0) return out;
+    long long nc = 0;
+    if (array_char_displacement) {
+        int prev = 0;
+        while (nc < num && array_char_displacement[nc] > prev && array_char_displacement[nc] <= num) {
+            prev = array_char_displacement[nc];
+            nc++;
+        }
+    }
+    const long long nraw = num - nc;
+    const size_t n = (size_t)num;
+    const hipStream_t st = (hipStream_t)dc_get_stream();
+    uint32_t* traw; unsigned long long* rawoff; uint8_t* carr;
+    if ((rc = grow(&g_a, &g_a_cap, n * 8 + 64)) || (rc = grow(&g_b, &g_b_cap, n * 8 + 64)) ||
+        (rc = grow(&c_codes, &c_codes_cap, n + 64)) || (rc = grow(&c_pos, &c_pos_cap, n * 4 + 64)) ||
+        (rc = c1_setup(num, &traw, &rawoff, &carr))) { fail(fn, rc); return out; }
+    unsigned h = 0;
+    if ((nraw > 0 && hipMemcpyAsync(g_a, array_double, sizeof(double) * (size_t)nraw, hipMemcpyHostToDevice, st) != hipSuccess) ||
+        (nc > 0 && hipMemcpyAsync(c_codes, array_char, (size_t)nc, hipMemcpyHostToDevice, st) != hipSuccess) ||
+        (nc > 0 && hipMemcpyAsync(c_pos, array_char_displacement, sizeof(int) * (size_t)nc, hipMemcpyHostToDevice, st) != hipSuccess) ||
+        hipMemsetAsync(c_err, 0, 4, st) != hipSuccess ||
+        dc_launch_ct1_decode64((const double*)g_a, nraw, (const char*)c_codes, (const int*)c_pos, nc, num, carr, traw,
+                               rawoff, (double*)g_b, c_err, st) ||
+        hipMemcpyAsync(&h, c_err, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) { fail(fn, DC_ERR_HIP); return out; }
+    if (h & 4u) fail(fn, dc_set_error(DC_ERR_STREAM, "ct1 codes out of range or raw array too short"));
+    if (hipMemcpy(out, g_b, sizeof(double) * n, hipMemcpyDeviceToHost) != hipSuccess) fail(fn, DC_ERR_HIP);
+    return out;
+}
+
+/* ---- double file helpers of the k-means / mm / lu link closure */
+void writetobinary_double(const char* file, double* data, int count) {          /* :5307-5322 */
+    FILE* fp = fopen(file, "wb");
+    if (!fp) { printf("failed to open %s\n", file); return; }
+    fwrite(data, sizeof(double), (size_t)(count > 0 ? count : 0), fp);
+    fclose(fp);
+    printf("saved %s\n", file);
+}
+
+double* readfrombinary_writetotxt_double(const char* binaryfile, const char* txtfile, int count) {   /* :5434-5454 */
+    FILE* fp = fopen(binaryfile, "rb");
+    if (!fp) { dc_set_error(DC_ERR_ARG, "cannot open the binary file"); return NULL; }
+    double* arr = (double*)malloc(sizeof(double) * (size_t)(count > 0 ? count : 1));
+    size_t got = arr ? fread(arr, sizeof(double), (size_t)(count > 0 ? count : 0), fp) : 0;
+    fclose(fp);
+    (void)got;
+    fp = fopen(txtfile, "w");
+    if (!fp) { dc_set_error(DC_ERR_ARG, "cannot open the text file"); return arr; }
+    for (int i = 0; i < count; i++) fprintf(fp, "%lf\n", arr[i]);
+    fclose(fp);
+    return arr;
 }

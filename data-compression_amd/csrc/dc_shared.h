@@ -100,6 +100,11 @@ int dc_launch_ct1_encode(const float* x, long long n, float thr_le, uint32_t* tr
 int dc_launch_ct1_decode(const float* raw, long long nraw, const char* codes, const int* pos1, long long ncodes,
                          long long num, uint8_t* carr, uint32_t* traw, unsigned long long* rawoff, float* out,
                          unsigned* err, dc_hip_stream st);
+int dc_launch_ct1_encode64(const double* x, long long n, double bound, uint32_t* traw, unsigned long long* rawoff,
+                           double* raw, char* codes, int* pos1, unsigned* err, dc_hip_stream st);
+int dc_launch_ct1_decode64(const double* raw, long long nraw, const char* codes, const int* pos1, long long ncodes,
+                           long long num, uint8_t* carr, uint32_t* traw, unsigned long long* rawoff, double* out,
+                           unsigned* err, dc_hip_stream st);
 int dc_launch_find_sentinel(const float* out, long long num, unsigned* err, dc_hip_stream st);
 int dc_launch_fixup_serial(const uint8_t* s, const DC_NS Params* P, const DC_NS DecBufs* D, float* out,
                            long long num, dc_hip_stream st);

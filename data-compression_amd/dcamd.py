@@ -31,7 +31,8 @@ ABI_SYMBOLS = [
     "myCompress_bitwise_double", "myCompress_bitwise_double_np", "myCompress_bitwise_double_op",
     "myCompress_bitwise_double_mask", "myDecompress_bitwise_double", "myDecompress_bitwise_double_np",
     "myDecompress_bitwise_double_op", "myDecompress_bitwise_double_mask", "toSmallDataset_double",
-    "med_dataset_double",
+    "med_dataset_double", "myCompress_double", "myDecompress_double", "writetobinary_double",
+    "readfrombinary_writetotxt_double",
 ]
 EXT_SYMBOLS = [
     "dc_init", "dc_last_error", "dc_get_stream", "dc_synchronize", "dc_set_abs_error_bound",
@@ -117,6 +118,11 @@ class Lib:
         L.toSmallDataset_double.restype = C.c_double
         L.med_dataset_double.argtypes = [_f64p, C.c_int, C.POINTER(C.c_int)]
         L.med_dataset_double.restype = C.c_double
+        L.myCompress_double.argtypes = [_f64p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                        C.c_int]
+        L.myCompress_double.restype = C.c_int
+        L.myDecompress_double.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.myDecompress_double.restype = vp
         L.dc64_stream_capacity.argtypes = [ll]
         L.dc64_stream_capacity.restype = C.c_size_t
         L.dc64_encode_device.argtypes = [C.c_int, vp, ll, C.c_int, u32, C.c_int, vp, vp]
@@ -230,6 +236,31 @@ class Lib:
         t = C.c_int(0)
         mean = self.L.med_dataset_double(x, x.size, C.byref(t))
         return np.float64(mean), t.value
+
+    def ct1_compress64(self, x):
+        x = np.ascontiguousarray(x, np.float64)
+        pf, pc, pp = C.c_void_p(None), C.c_void_p(None), C.c_void_p(None)
+        nf = self.L.myCompress_double(x if x.size else np.zeros(1, np.float64), C.byref(pf), C.byref(pc), C.byref(pp),
+                                      x.size)
+        nc = x.size - nf
+        raw = np.frombuffer(C.string_at(pf.value, 8 * nf), np.float64).copy() if nf else np.zeros(0, np.float64)
+        codes = C.string_at(pc.value, nc) if nc else b""
+        pos = np.frombuffer(C.string_at(pp.value, 4 * nc), np.int32).copy() if nc else np.zeros(0, np.int32)
+        for q in (pf, pc, pp):
+            if q.value:
+                _libc.free(q)
+        return raw, codes, pos
+
+    def ct1_decompress64(self, raw, codes, pos, num):
+        raw = np.ascontiguousarray(raw, np.float64)
+        pos = np.ascontiguousarray(pos, np.int32)
+        posx = np.concatenate([pos, np.zeros(1, np.int32)])   # terminator, as ct1_decompress
+        cb = C.create_string_buffer(bytes(codes), len(codes) + 1)
+        p = self.L.myDecompress_double(raw.ctypes.data if raw.size else None, C.cast(cb, C.c_void_p), posx.ctypes.data,
+                                       num)
+        out = np.frombuffer(C.string_at(p, 8 * num), np.float64).copy() if num else np.zeros(0, np.float64)
+        _libc.free(p)
+        return out
 
     def encode64_device(self, ct, x_ptr, n, out_ptr, type_=0, mask20=0, start_bit=0, total_ptr=None):
         self.check(self.L.dc64_encode_device(ct, x_ptr, n, type_, mask20, start_bit, out_ptr, total_ptr),

@@ -122,6 +122,15 @@ double toSmallDataset_double(double data[], double** data_small, int num);
 /* h:98  c:3564-3590: left-to-right double mean; *type from the maximum */
 double med_dataset_double(double* data, int num, int* type);
 
+/* h:122 c:3815-3941: CT1 byte-wise for doubles */
+int myCompress_double(double data[], double** array_double, char** array_char, int** array_char_displacement, int num);
+/* h:123 c:3778-3813 */
+double* myDecompress_double(double array_double[], char array_char[], int array_char_displacement[], int num);
+/* h:130 c:5307 */
+void writetobinary_double(const char* file, double* data, int count);
+/* h:136 c:5434: count doubles from binaryfile, also written to txtfile as "%lf\n" */
+double* readfrombinary_writetotxt_double(const char* binaryfile, const char* txtfile, int count);
+
 /* ---- pre-passes ---------------------------------------------------------------------------------- */
 /* h:96  c:3543-3562: *data_small = data - min (new malloc array), returns min */
 float toSmallDataset_float(float data[], float** data_small, int num);
@@ -191,5 +200,9 @@ float* readfrombinary_writetotxt_float(const char* binaryfile, const char* txtfi
 
 #ifdef __cplusplus
 }
+#endif
+/* the MPI wrappers of libdcamd_mpi.so (the reference header declares them after mpi.h, h:43-61) */
+#if defined(MPI_VERSION)
+#include "dc_mpi.h"
 #endif
 #endif

@@ -32,6 +32,38 @@ int MPI_Send_bitwise_float_mask(const void* buf, int count, MPI_Datatype datatyp
 int MPI_Recv_bitwise_float_mask(void* buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
                                 MPI_Status* status);
 
+/* ---- the reference's double wrappers (impl/dataCompression.h:43-61, dataCompression.c:24-353, :800-1197),
+ * same signatures; framing [int bytes][double min][stream]; _cn: the first len doubles compressed, the rest raw
+ * (csrc/dc_mpi64.c) */
+int MPI_Send_bitwise_double(const void* buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm);
+int MPI_Recv_bitwise_double(void* buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
+                            MPI_Status* status);
+int MPI_Send_bitwise_double_np(const void* buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm);
+int MPI_Recv_bitwise_double_np(void* buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
+                               MPI_Status* status);
+int MPI_Send_bitwise_double_op(const void* buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm);
+int MPI_Recv_bitwise_double_op(void* buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
+                               MPI_Status* status);
+int MPI_Send_bitwise_double_cn(const void* buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                               int len);
+int MPI_Recv_bitwise_double_cn(void* buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
+                               MPI_Status* status, int len);
+int MPI_Send_bitwise_double_np_cn(const void* buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                                  int len);
+int MPI_Recv_bitwise_double_np_cn(void* buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
+                                  MPI_Status* status, int len);
+int MPI_Send_bitwise_double_op_cn(const void* buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                                  int len);
+int MPI_Recv_bitwise_double_op_cn(void* buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
+                                  MPI_Status* status, int len);
+/* CT8 (CRC-32), CT9 (bitmask + CRC-32), CT10 (CRC-32 + Hamming): broadcast from root, resend on failure */
+void MPI_Bcast_bitwise_crc(double* buffer, int count, int root, int rank, int procs, float* compress_ratio,
+                           double* gosa, int* resend);
+void MPI_Bcast_bitwise_mask_crc(double* buffer, int count, int root, int rank, int procs, float* compress_ratio,
+                                double* gosa, int* resend);
+void MPI_Bcast_bitwise_crc_hamming(double* buffer, int count, int root, int rank, int procs, float* compress_ratio,
+                                   double* gosa, int* resend);
+
 #ifdef __cplusplus
 }
 #endif

@@ -29,3 +29,14 @@ for app in pingpong himenoBMTxps; do
       -I"$REF/impl" "$REF/impl/$app.c" -o "$OUT/${app}_dcamd" -L"$LIB" -ldcamd -Wl,-rpath,"$LIB" "$STDCXX" -lm
   echo "build_apps: built $OUT/${app}_ref $OUT/${app}_dcamd"
 done
+# the double apps: k-means / mm / lu use the double codecs and the MPI_Bcast_bitwise_* wrappers
+# (libdcamd_mpi.so); their reference build needs the reference param.h next to the app
+for app in k-means mm lu; do
+  [ -f "$REF/impl/$app.c" ] || continue
+  MPICH_CC=gcc "$MPI/bin/mpicc" -O3 -ffp-contract=off -w -iquote "$gen" -I- -I"$gen" -I"$REF/impl" \
+      "$REF/impl/$app.c" "$REF/impl/dataCompression.c" -o "$OUT/${app}_ref" -lz -lm || { echo "build_apps: $app (reference build) failed"; continue; }
+  MPICH_CC=gcc "$MPI/bin/mpicc" -O3 -w -DabsErrorBound="$BOUND" -iquote "$REPO/include" -I- -I"$REPO/include" \
+      -I"$REF/impl" "$REF/impl/$app.c" -o "$OUT/${app}_dcamd" -L"$LIB" -ldcamd_mpi -ldcamd -Wl,-rpath,"$LIB" "$STDCXX" -lm \
+      || { echo "build_apps: $app (libdcamd build) failed"; continue; }
+  echo "build_apps: built $OUT/${app}_ref $OUT/${app}_dcamd"
+done

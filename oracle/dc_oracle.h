@@ -85,6 +85,8 @@ void orc64_compress(int ct, const double* data, long num, double bound, int type
 long orc64_decompress_spec(int ct, const unsigned char* bits, long bytes, long num, double bound,
                            int type, uint32_t mask20, double* out);
 void orc64_gen_u10(double* out, long n, uint64_t seed, long offset);
+int orc64_bytewise_compress(const double* data, int num, double bound, double* raw, char* codes, int* pos1);
+void orc64_bytewise_decompress(const double* raw, const char* codes, const int* pos1, int ncodes, int num, double* out);
 long orc64_chunk_records(int ct, const unsigned char* s, long bytes, long num, double bound, int type,
                          uint32_t mask20, long cb, unsigned char* ent, unsigned char* ex, unsigned short* cnt);
 

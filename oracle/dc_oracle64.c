@@ -260,3 +260,47 @@ long orc64_chunk_records(int ct, const unsigned char* s, long bytes, long num, d
     }
     return nc;
 }
+
+/* ------------------------------------------------------------------ CT1 byte-wise for doubles */
+int orc64_bytewise_compress(const double* data, int num, double bound, double* raw, char* codes, int* pos1) {
+    double b1 = -1, b2 = -1, b3 = -1, b4 = -1;              /* myCompress_double :3815-3941 */
+    int nf = 0, nc = 0;
+    for (int n = 0; n < num; n++) {
+        double x = data[n];
+        if (b4 == -1 || b3 == -1 || b2 == -1 || b1 == -1) {
+            raw[nf++] = x;
+            if (b4 == -1) b4 = x;
+            else if (b3 == -1) b3 = x;
+            else if (b2 == -1) b2 = x;
+            else if (b1 == -1) b1 = x;
+            continue;
+        }
+        double p1 = b1, p2 = 2 * b1 - b2, p3 = 3 * b1 - 3 * b2 + b3, p4 = 4 * b1 - 6 * b2 + 4 * b3 - b4;
+        double d1 = fabs(p1 - x), d2 = fabs(p2 - x), d3 = fabs(p3 - x), d4 = fabs(p4 - x);
+        double dmin = d1; char t = 'a';
+        if (d2 < dmin) { dmin = d2; t = 'b'; }
+        if (d3 < dmin) { dmin = d3; t = 'c'; }
+        if (d4 < dmin) { dmin = d4; t = 'd'; }
+        b4 = b3; b3 = b2; b2 = b1; b1 = x;
+        if (dmin <= bound) { codes[nc] = t; nc++; pos1[nc - 1] = nf + nc; }
+        else raw[nf++] = x;
+    }
+    return nf;
+}
+
+void orc64_bytewise_decompress(const double* raw, const char* codes, const int* pos1, int ncodes, int num,
+                               double* out) {                /* myDecompress_double :3778-3813 */
+    int fp = 0, cp = 0;
+    for (int i = 0; i < num; i++) {
+        if (cp < ncodes && pos1[cp] - 1 == i) {
+            char t = codes[cp];
+            if (t == 'a') out[i] = out[i - 1];
+            else if (t == 'b') out[i] = 2 * out[i - 1] - out[i - 2];
+            else if (t == 'c') out[i] = 3 * out[i - 1] - 3 * out[i - 2] + out[i - 3];
+            else if (t == 'd') out[i] = 4 * out[i - 1] - 6 * out[i - 2] + 4 * out[i - 3] - out[i - 4];
+            cp++;
+        } else {
+            out[i] = raw[fp++];
+        }
+    }
+}

@@ -84,6 +84,8 @@ class Oracle:
                                             C.c_uint32, _f64p]
         L.orc64_decompress_spec.restype = C.c_long
         L.orc64_gen_u10.argtypes = [_f64p, C.c_long, C.c_uint64, C.c_long]
+        L.orc64_bytewise_compress.argtypes = [_f64p, C.c_int, C.c_double, _f64p, C.c_char_p, _i32p]
+        L.orc64_bytewise_decompress.argtypes = [_f64p, C.c_char_p, _i32p, C.c_int, C.c_int, _f64p]
 
     # -- helpers
     def bound_binary(self, b):
@@ -224,6 +226,22 @@ class Oracle:
                                          type_, mask20, out)
         return out, n
 
+    def bytewise_compress64(self, x, bound):
+        x = np.ascontiguousarray(x, np.float64)
+        raw = np.zeros(max(x.size, 1), np.float64)
+        codes = C.create_string_buffer(max(x.size, 1))
+        pos = np.zeros(max(x.size, 1), np.int32)
+        nf = self.L.orc64_bytewise_compress(x, x.size, bound, raw, codes, pos)
+        nc = x.size - nf
+        return raw[:nf].copy(), codes.raw[:nc], pos[:nc].copy()
+
+    def bytewise_decompress64(self, raw, codes, pos, num):
+        raw = np.ascontiguousarray(raw, np.float64) if len(raw) else np.zeros(1, np.float64)
+        pos = np.ascontiguousarray(pos, np.int32) if len(pos) else np.zeros(1, np.int32)
+        out = np.zeros(num, np.float64)
+        self.L.orc64_bytewise_decompress(raw, codes or b"\0", pos, len(codes), num, out)
+        return out
+
     def gen_u10_64(self, n, seed=42, offset=0):
         out = np.empty(n, np.float64)
         self.L.orc64_gen_u10(out, n, seed, offset)
@@ -289,6 +307,7 @@ class RefLib:
             getattr(L, nm).restype = C.c_void_p
         L.myDecompress_bitwise_double_mask.argtypes = [_u8p, C.c_int, C.c_int, C.c_int, C.c_char_p]
         L.myDecompress_bitwise_double_mask.restype = C.c_void_p
+        L.myCompress_double.argtypes = [_f64p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_int]
         L.toSmallDataset_double.argtypes = [_f64p, C.POINTER(C.c_void_p), C.c_int]
         L.toSmallDataset_double.restype = C.c_double
         L.med_dataset_double.argtypes = [_f64p, C.c_int, C.POINTER(C.c_int)]
@@ -359,6 +378,18 @@ class RefLib:
         out = np.frombuffer(C.string_at(p, 8 * num), np.float64).copy()
         _libc.free(p)
         return out
+
+    def bytewise64(self, x):
+        x = np.ascontiguousarray(x, np.float64)
+        pf, pc, pp = C.c_void_p(None), C.c_void_p(None), C.c_void_p(None)
+        nf = self.L.myCompress_double(x, C.byref(pf), C.byref(pc), C.byref(pp), x.size)
+        nc = x.size - nf
+        raw = np.frombuffer(C.string_at(pf.value, 8 * nf), np.float64).copy() if nf else np.zeros(0, np.float64)
+        codes = C.string_at(pc.value, nc) if nc else b""
+        pos = np.frombuffer(C.string_at(pp.value, 4 * nc), np.int32).copy() if nc else np.zeros(0, np.int32)
+        for q in (pf, pc, pp):
+            _libc.free(q)
+        return raw, codes, pos
 
     def to_small64(self, x):
         x = np.ascontiguousarray(x, np.float64)

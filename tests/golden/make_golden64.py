@@ -9,7 +9,8 @@ Outputs (data only -- inputs and the reference's outputs, no reference source):
                         myCompress_bitwise_double{,_np,_mask,_op} (impl/dataCompression.c:3189,
                         :2633, :1590, :355), bytes, pos, type, mask20, the reference decoder's output
                         (run in a child process: on quirk streams it corrupts its heap) and whether
-                        it is self-consistent (equal to the grammar decoder); append-mode streams.
+                        it is self-consistent (equal to the grammar decoder); CT1 arrays of
+                        myCompress_double (:3815); append-mode streams.
   kat64_*               the reference tree's double KATs, copied verbatim: the binary inputs (.bi),
                         the streams (.bc: CT6 / CT11 at absErrorBound 1e-6) and the decoded text.
 """
@@ -91,6 +92,10 @@ def main():
                 if dec is not None:
                     rec[key + "/ref_decoded"] = dec
                 print(f"{bound:g} {name:10s} ct{ct:2d} bytes={nb:7d} pos={pos} type={t} consistent={ok}")
+            raw, codes, p1 = R.bytewise64(x)                   # CT1: myCompress_double (:3815)
+            rec[f"{name}/ct1/raw"] = raw
+            rec[f"{name}/ct1/codes"] = np.frombuffer(codes, np.uint8).copy()
+            rec[f"{name}/ct1/pos"] = p1
         x = ins["edge"]
         mn, xs = R.to_small64(x)
         import ctypes as C

@@ -36,19 +36,21 @@ def test_apps_link_unchanged():
     """pingpong and himenoBMTxps compile and link against include/ + libdcamd with no source change."""
     subprocess.check_call([os.path.join(ROOT, "oracle", "build_apps.sh")], stdout=subprocess.DEVNULL,
                           stderr=subprocess.DEVNULL)
-    for app in ("pingpong", "himenoBMTxps"):
+    for app in ("pingpong", "himenoBMTxps", "k-means", "mm", "lu"):
         exe = _app(app + "_dcamd")
         assert os.path.isfile(exe), exe
         undef = subprocess.run(["nm", "-u", exe], capture_output=True, text=True, check=True).stdout
         # every codec symbol the app needs comes from libdcamd, none from a reference object
-        lib = subprocess.run(["nm", "-D", "--defined-only",
-                              os.path.join(ROOT, "data-compression_amd", "lib", "libdcamd.so")],
-                             capture_output=True, text=True, check=True).stdout
-        exported = {ln.split()[-1] for ln in lib.splitlines() if ln.strip()}
+        exported = set()
+        for so in ("libdcamd.so", "libdcamd_mpi.so"):
+            lib = subprocess.run(["nm", "-D", "--defined-only",
+                                  os.path.join(ROOT, "data-compression_amd", "lib", so)],
+                                 capture_output=True, text=True, check=True).stdout
+            exported |= {ln.split()[-1] for ln in lib.splitlines() if ln.strip()}
         for sym in re.findall(r"\bU (\S+)", undef):
             s = sym.split("@")[0]
-            if re.match(r"(my|toSmall|med_|do_crc|hamming|bit_flip|block_size|floattostr|get_random|transform_|"
-                        r"readfrombinary|writetobinary)", s):
+            if re.match(r"(my|toSmall|med_|do_crc|hamming|bit_flip|block_size|floattostr|doubletostr|get_random|"
+                        r"transform_|readfrombinary|writetobinary|MPI_Bcast_bitwise|MPI_Send_bitwise|MPI_Recv_bitwise)", s):
                 assert s in exported, s
 
 
@@ -87,3 +89,26 @@ def test_pingpong_dcamd_matches_reference(ct, tmp_path):
     assert rr == rg, (out_ref[-1500:], out_gpu[-1500:])
     assert gr == gg, (out_ref[-1500:], out_gpu[-1500:])
 
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not (os.path.isfile(_app("k-means_dcamd")) and os.path.isfile(MPIRUN)),
+                    reason="oracle/_ref/apps not built (run oracle/build_apps.sh where /root/reference exists)")
+@pytest.mark.parametrize("ct", [5, 6, 7, 8, 9])
+def test_kmeans_dcamd_matches_reference(ct, tmp_path):
+    """impl/k-means.c unchanged: 1000 iterations broadcasting 100 cluster centres (x and y) per iteration
+    through the double codecs (CT5/6/7) and MPI_Bcast_bitwise_crc / _mask_crc (CT8/9), on
+    impl/dataset/testfloat_8_8_128.txt.  Both builds print the same mean error (gosa) and compression
+    ratio (CT8/9 resend counts are random, seeded by time(), as in the reference)."""
+    ds = tmp_path / "dataset"
+    ds.mkdir()
+    shutil.copyfile(os.path.join(ROOT, "tests", "golden", "kat_testfloat_8_8_128.txt"), ds / "testfloat_8_8_128.txt")
+    env = dict(os.environ, DC_ABS_ERROR_BOUND="0.001", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    outs = []
+    for exe in (_app("k-means_ref"), _app("k-means_dcamd")):
+        r = subprocess.run([MPIRUN, "-np", "2", exe, str(ct)], capture_output=True, text=True, timeout=300, env=env,
+                           cwd=str(tmp_path))
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        outs.append((re.findall(r"gosa = ([0-9.eE+-]+)", r.stdout), re.findall(r"compress ratio = ([0-9.eE+-]+)", r.stdout)))
+    assert outs[0][0] and outs[0][1], outs
+    assert outs[0] == outs[1], outs

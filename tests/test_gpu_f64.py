@@ -196,3 +196,31 @@ def test_decode64_paths(dc, oracle, monkeypatch):
                 assert flags & 2, flags
             elif i == 0:
                 assert flags == 0, flags
+
+
+@pytest.mark.parametrize("bound", BOUNDS)
+@pytest.mark.parametrize("case", CASES64)
+def test_ct1_double_gpu(dc, oracle, bound, case):
+    """myCompress_double / myDecompress_double on the GPU: arrays equal the compiled reference's
+    (golden), the decode equals the oracle's bit for bit."""
+    g = golden64(bound)
+    dc.set_bound(bound)
+    x = g[f"{case}/input"]
+    raw, codes, pos = dc.ct1_compress64(x)
+    assert np.array_equal(raw.view(np.uint64), g[f"{case}/ct1/raw"].view(np.uint64))
+    assert codes == g[f"{case}/ct1/codes"].tobytes() and np.array_equal(pos, g[f"{case}/ct1/pos"])
+    d = dc.ct1_decompress64(raw, codes, pos, x.size)
+    ref = oracle.bytewise_decompress64(raw, codes, pos, x.size)
+    assert np.array_equal(d.view(np.uint64), ref.view(np.uint64))
+
+
+def test_ct1_double_large(dc, oracle):
+    bound = 1e-3
+    dc.set_bound(bound)
+    rs = np.random.RandomState(4)
+    x = np.concatenate([oracle.gen_u10_64(1 << 18), np.arange(1 << 17) * 0.25, np.repeat(rs.rand(256), 512)])
+    raw, codes, pos = dc.ct1_compress64(x)
+    r2, c2, p2 = oracle.bytewise_compress64(x, bound)
+    assert np.array_equal(raw.view(np.uint64), r2.view(np.uint64)) and codes == c2 and np.array_equal(pos, p2)
+    d = dc.ct1_decompress64(raw, codes, pos, x.size)
+    assert np.array_equal(d.view(np.uint64), oracle.bytewise_decompress64(raw, codes, pos, x.size).view(np.uint64))

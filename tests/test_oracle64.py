@@ -85,3 +85,19 @@ def test_append64(oracle, bound, ct):
     s2, nb2, p2 = oracle.compress64(ct, xs[333:], bound, prefix=s1, prefix_pos=p1)
     assert np.array_equal(s2, g[f"append/ct{ct}/stream"]) and p2 == g[f"append/ct{ct}/pos"]
 
+
+
+@pytest.mark.parametrize("bound", BOUNDS)
+@pytest.mark.parametrize("case", CASES64)
+def test_ct1_double_oracle(oracle, bound, case):
+    """myCompress_double (:3815) arrays of the oracle equal the compiled reference's; the decoder
+    restores raws exactly and rebuilds codes from the decoded history."""
+    g = golden64(bound)
+    x = g[f"{case}/input"]
+    raw, codes, pos = oracle.bytewise_compress64(x, bound)
+    assert np.array_equal(raw.view(np.uint64), g[f"{case}/ct1/raw"].view(np.uint64))
+    assert codes == g[f"{case}/ct1/codes"].tobytes() and np.array_equal(pos, g[f"{case}/ct1/pos"])
+    d = oracle.bytewise_decompress64(raw, codes, pos, x.size)
+    israw = np.ones(x.size, bool)
+    israw[pos - 1] = False
+    assert np.array_equal(d[israw].view(np.uint64), x[israw].view(np.uint64))
