@@ -186,6 +186,73 @@ __global__ __launch_bounds__(1024) void enc_scan(const uint32_t* __restrict__ tb
     }
 }
 
+// the same scan in three launches for many tiles: block scans (1024 tiles each), a scan of the block
+// sums, then offsets + start bit, zeroing of every tile's first word and the stream's last word
+__global__ __launch_bounds__(1024) void enc_scan_part(const uint32_t* __restrict__ tbits, long long ntiles,
+                                                      unsigned long long* __restrict__ toff,
+                                                      unsigned long long* __restrict__ psum) {
+    __shared__ unsigned long long ws[16];
+    const long long t = blockIdx.x * 1024ll + threadIdx.x;
+    const unsigned long long v = t < ntiles ? tbits[t] : 0ull;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    unsigned long long s = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long o = __shfl_up(s, d, 64);
+        if (lane >= d) s += o;
+    }
+    if (lane == 63) ws[wv] = s;
+    __syncthreads();
+    unsigned long long pre = 0, tot = 0;
+    for (int i = 0; i < 16; i++) { if (i < wv) pre += ws[i]; tot += ws[i]; }
+    if (t < ntiles) toff[t] = pre + s - v;
+    if (threadIdx.x == 0) psum[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(1024) void scan_top(unsigned long long* __restrict__ psum, long long nb) {
+    __shared__ unsigned long long ws[16];
+    __shared__ unsigned long long carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (long long b = 0; b <= nb; b += 1024) {                  // psum[nb] = the total
+        const long long i = b + threadIdx.x;
+        const unsigned long long v = i < nb ? psum[i] : 0ull;
+        unsigned long long s = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const unsigned long long o = __shfl_up(s, d, 64);
+            if (lane >= d) s += o;
+        }
+        if (lane == 63) ws[wv] = s;
+        __syncthreads();
+        unsigned long long pre = 0;
+        for (int k = 0; k < wv; k++) pre += ws[k];
+        const unsigned long long off = carry + pre + s - v;
+        if (i <= nb) psum[i] = off;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry = off + v;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(1024) void enc_scan_add(long long ntiles, int start_bit, const unsigned long long* __restrict__ psum,
+                                                     unsigned long long* __restrict__ toff, uint32_t* __restrict__ out,
+                                                     unsigned long long* __restrict__ total) {
+    const long long t = blockIdx.x * 1024ll + threadIdx.x;
+    if (t < ntiles) {
+        const unsigned long long off = toff[t] + psum[blockIdx.x] + (unsigned long long)start_bit;
+        toff[t] = off;
+        out[off >> 5] = 0u;
+    }
+    if (t == 0) {
+        const long long nb = (ntiles + 1023) / 1024;
+        const unsigned long long end = psum[nb] + (unsigned long long)start_bit;
+        if (end > (unsigned long long)start_bit) out[(end - 1) >> 5] = 0u;
+        *total = end - (unsigned long long)start_bit;
+    }
+}
+
 __device__ __forceinline__ void lds_or(uint32_t* L, uint32_t off, uint64_t val, int len) {   // len 1..64
     const uint32_t w = off >> 5, b = off & 31u;
     const int end = (int)b + len;                                     // 1..95
@@ -441,7 +508,10 @@ __global__ __launch_bounds__(64) void dec_map(const uint32_t* __restrict__ W, co
 // synchronises with the true token boundaries with high probability within one chunk of random data)
 // and so arrives at chunk c with a speculative entry se[c]; it then walks chunk c: exit sx[c], tokens
 // sn[c].  The entries are right when every link holds: sx[c-1] == se[c] (chunk 0 starts at bit 0).
-constexpr int OVB = CB;                     // pre-walk overlap (bits)
+#ifndef DC64_OVB
+#define DC64_OVB 2048
+#endif
+constexpr int OVB = DC64_OVB;                // pre-walk overlap (bits)
 constexpr int OVW = OVB / 32;
 constexpr int GWS = OVW + 64 * MAPW + 8;
 constexpr int SWS = GWS + GWS / 64 + 2;
@@ -882,7 +952,8 @@ extern "C" int dc_set_error(int code, const char* msg);
 namespace {
 struct Ctx64 {
     // encoder
-    uint32_t* tbits = nullptr; unsigned long long* toff = nullptr; long long enc_cap = 0;
+    uint32_t* tbits = nullptr; unsigned long long* toff = nullptr; unsigned long long* psum = nullptr;
+    long long enc_cap = 0;
     unsigned long long* d_total = nullptr; unsigned* d_err = nullptr;
     // decoder
     void* pool = nullptr; size_t pool_cap = 0;
@@ -966,13 +1037,22 @@ extern "C" int dc64_encode_device(int ct, const void* d_x, long long n, int type
         if (C64.tbits) { (void)hipFree(C64.tbits); (void)hipFree(C64.toff); }
         H64(hipMalloc((void**)&C64.tbits, (size_t)nt * 4));
         H64(hipMalloc((void**)&C64.toff, (size_t)nt * 8));
+        if (C64.psum) (void)hipFree(C64.psum);
+        H64(hipMalloc((void**)&C64.psum, (size_t)((nt + 1023) / 1024 + 2) * 8));
         C64.enc_cap = nt;
     }
     const double* x = (const double*)d_x;
     uint32_t* out = (uint32_t*)d_out;
     H64(hipMemsetAsync(C64.d_err, 0, 4, st));
     DISPATCH64(ct, enc_count, dim3((unsigned)nt), dim3(ETPB), 0, st, x, n, P, C64.tbits, C64.d_err);
-    hipLaunchKernelGGL(enc_scan, dim3(1), dim3(1024), 0, st, C64.tbits, nt, start_bit, C64.toff, out, tot);
+    if (nt <= 4096) {
+        hipLaunchKernelGGL(enc_scan, dim3(1), dim3(1024), 0, st, C64.tbits, nt, start_bit, C64.toff, out, tot);
+    } else {
+        const long long nb = (nt + 1023) / 1024;
+        hipLaunchKernelGGL(enc_scan_part, dim3((unsigned)nb), dim3(1024), 0, st, C64.tbits, nt, C64.toff, C64.psum);
+        hipLaunchKernelGGL(scan_top, dim3(1), dim3(1024), 0, st, C64.psum, nb);
+        hipLaunchKernelGGL(enc_scan_add, dim3((unsigned)nb), dim3(1024), 0, st, nt, start_bit, C64.psum, C64.toff, out, tot);
+    }
     DISPATCH64(ct, enc_write, dim3((unsigned)nt), dim3(ETPB), 0, st, x, n, P, C64.toff, out);
     DISPATCH64(ct, enc_serial, dim3(1), dim3(64), 0, st, x, n, P, start_bit, (uint8_t*)d_out, tot, C64.d_err);
     if (tot != C64.d_total) H64(hipMemcpyAsync(C64.d_total, tot, 8, hipMemcpyDeviceToDevice, st));
