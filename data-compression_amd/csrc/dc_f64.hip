@@ -724,6 +724,15 @@ __global__ __launch_bounds__(64) void dec_chunks(const uint32_t* __restrict__ W,
     int pd = 0;
     bool bad = false;
     long long j = 0;
+    // outputs leave as whole 32-byte sectors (4 doubles, two 16-byte stores) from a 4-register buffer;
+    // pending values are written too (dec_fix rewrites them) -- the partial head / tail sectors, shared
+    // with the neighbouring chunks, element by element
+    const bool al = (reinterpret_cast<uintptr_t>(out) & 31) == 0;
+    double r0 = 0.0, r1 = 0.0, r2 = 0.0, r3 = 0.0;
+    auto put = [&](long long i) {
+        const int sl = (int)(i & 3);
+        out[i] = sl == 0 ? r0 : sl == 1 ? r1 : sl == 2 ? r2 : r3;
+    };
     while (p < ce && k0 + j < num) {
         const uint64_t win = peekS(S, p);
         const int l = tok_len<CT>(win, P);
@@ -741,13 +750,31 @@ __global__ __launch_bounds__(64) void dec_chunks(const uint32_t* __restrict__ W,
             v = tok_value<CT>(win, l, P);
         }
         if (q) pd = (int)j + 1;
-        else {
-            out[k0 + j] = v;
-            bad |= d2u(v) == 0xBFF0000000000000ull;                        // the -1.0 history sentinel
+        else bad |= d2u(v) == 0xBFF0000000000000ull;                       // the -1.0 history sentinel
+        const long long g = k0 + j;
+        if (al) {
+            const int sl = (int)(g & 3);
+            r0 = sl == 0 ? v : r0; r1 = sl == 1 ? v : r1; r2 = sl == 2 ? v : r2; r3 = sl == 3 ? v : r3;
+            if (sl == 3) {
+                if (g - 3 >= k0) {
+                    double2* o2 = reinterpret_cast<double2*>(out + (g - 3));
+                    o2[0] = make_double2(r0, r1);
+                    o2[1] = make_double2(r2, r3);
+                } else {
+                    for (long long i = k0; i <= g; i++) put(i);
+                }
+            }
+        } else if (!q) {
+            out[g] = v;
         }
         f3 = f2; q3 = q2; f2 = f1; q2 = q1; f1 = v; q1 = q;
         p += (uint32_t)l;
         j++;
+    }
+    if (al && j > 0) {                                                     // the partial last sector
+        const long long gl = k0 + j - 1;
+        if ((gl & 3) != 3)
+            for (long long i = std::max(k0, gl & ~3ll); i <= gl; i++) put(i);
     }
     pend[c] = (uint16_t)pd;
     thru[c] = (uint8_t)((q1 | q2 | q3) ? 1 : 0);
