@@ -12,7 +12,7 @@ def load(d, counter):
     for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] == counter:
-                name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("dc::", "")
+                name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("dc::", "").replace("dc64::", "")
                 vals[name].append(float(r["Counter_Value"]) * 1024.0)
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
