@@ -550,55 +550,56 @@ __global__ __launch_bounds__(64) void dec_spec(const uint32_t* __restrict__ W, c
     sn[c] = (uint16_t)n;
 }
 
-// broken links: bad[c] = sx[c-1] != se[c]; ctr[0] counts them
+// broken links: bad[c] = sx[c-1] != se[c]; *ctr counts them, list[] holds them (any order)
 __global__ __launch_bounds__(256) void dec_links(const Plan64* __restrict__ pl, const uint8_t* __restrict__ se,
                                                  const uint8_t* __restrict__ sx, uint8_t* __restrict__ bad,
-                                                 unsigned* __restrict__ ctr) {
+                                                 unsigned* __restrict__ ctr, unsigned* __restrict__ list) {
     const long long c = blockIdx.x * 256ll + threadIdx.x;
     if (c >= pl->nchunks) return;
     const bool b = c > 0 && sx[c - 1] != se[c];
     bad[c] = b ? 1 : 0;
-    if (b) atomicAdd(ctr, 1u);
+    if (b) list[atomicAdd(ctr, 1u)] = (unsigned)c;
 }
 
 // one repair round: a chunk with a broken link whose predecessor's link holds takes the predecessor's
-// exit as its entry and walks again (chains of broken links advance one chunk per round).  64 chunks
-// per workgroup, their words staged in LDS like dec_spec.
+// exit as its entry and walks again (chains of broken links advance one chunk per round).  One
+// workgroup per listed chunk: its words are staged in LDS, lane 0 walks.
 template <int CT>
 __global__ __launch_bounds__(64) void dec_relink(const uint32_t* __restrict__ W, const Plan64* __restrict__ pl, P64 P,
                                                  uint8_t* __restrict__ se, uint8_t* __restrict__ sx,
                                                  uint16_t* __restrict__ sn, const uint8_t* __restrict__ bad,
-                                                 const unsigned* __restrict__ ctr) {
-    __shared__ uint32_t S[SW];
-    __shared__ int any;
-    if (*ctr == 0) return;
-    const long long g0 = blockIdx.x * 64ll;
-    const long long nc = pl->nchunks;
-    if (g0 >= nc) return;
-    const long long c = g0 + threadIdx.x;
-    const bool mine = c > 0 && c < nc && bad[c] && !bad[c - 1];
-    if (threadIdx.x == 0) any = 0;
-    __syncthreads();
-    if (mine) any = 1;
-    __syncthreads();
-    if (!any) return;
-    stage_group(S, W, g0 * MAPW, pl->nwords + 4);
-    __syncthreads();
-    if (!mine) return;
-    const long long avail = (long long)pl->nbits - g0 * CB;
-    const uint32_t lim = (uint32_t)std::min(avail, (long long)(64 * CB + 64));
-    const uint32_t cs = threadIdx.x * CB, ce = cs + CB;
-    const int t = sx[c - 1];
-    uint32_t p = cs + (uint32_t)t, n = 0;
-    while (p < ce) {
-        const int l = tok_len<CT>(peekS(S, p), P);
-        if (p + (uint32_t)l > lim) { p = ce; break; }
-        n++;
-        p += (uint32_t)l;
+                                                 const unsigned* __restrict__ ctr, const unsigned* __restrict__ list) {
+    __shared__ uint32_t S[MAPW + 8];
+    const unsigned nl = *ctr;
+    const long long wlim = pl->nwords + 4;
+    for (unsigned i = blockIdx.x; i < nl; i += gridDim.x) {
+        const long long c = list[i];
+        if (c <= 0 || c >= pl->nchunks || !bad[c] || bad[c - 1]) continue;     // uniform in the workgroup
+        __syncthreads();
+        for (int k = threadIdx.x; k < MAPW + 8; k += 64) {
+            const long long w = c * MAPW + k;
+            S[k] = w < wlim ? W[w] : 0u;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const long long avail = (long long)pl->nbits - c * CB;
+            const uint32_t lim = (uint32_t)std::min(avail, (long long)(CB + 64));
+            const int t = sx[c - 1];
+            uint32_t p = (uint32_t)t, n = 0;
+            while (p < (uint32_t)CB) {
+                const uint32_t w = p >> 5, sh = p & 31;
+                const uint64_t a = ((uint64_t)S[w] << 32) | S[w + 1];
+                const uint64_t win = sh ? (a << sh) | ((uint64_t)S[w + 2] >> (32 - sh)) : a;
+                const int l = tok_len<CT>(win, P);
+                if (p + (uint32_t)l > lim) { p = CB; break; }
+                n++;
+                p += (uint32_t)l;
+            }
+            se[c] = (uint8_t)t;
+            sx[c] = (uint8_t)(p - CB);
+            sn[c] = (uint16_t)n;
+        }
     }
-    se[c] = (uint8_t)t;
-    sx[c] = (uint8_t)(p - ce);
-    sn[c] = (uint16_t)n;
 }
 
 // exclusive scan of the chunk token counts -> first token index of every chunk (3 launches)
@@ -1102,7 +1103,7 @@ namespace {
 struct DecLayout {
     int nlev;                       // levels above the chunks (the last one has a single node)
     long long nnode[8];             // max nodes per level (0 = chunks)
-    size_t off_w, off_map, off_lmap[8], off_ent[8], off_base[8], off_sx, off_sn, off_bad, off_rl, off_psum, off_pend, off_thru, total;
+    size_t off_w, off_map, off_lmap[8], off_ent[8], off_base[8], off_sx, off_sn, off_bad, off_list, off_psum, off_pend, off_thru, total;
 };
 DecLayout layout(long long max_words, long long max_chunks) {
     DecLayout Lo{};
@@ -1125,7 +1126,7 @@ DecLayout layout(long long max_words, long long max_chunks) {
     Lo.off_sx = take((size_t)max_chunks);
     Lo.off_sn = take((size_t)max_chunks * 2);
     Lo.off_bad = take((size_t)max_chunks);
-    Lo.off_rl = take((size_t)max_chunks);
+    Lo.off_list = take((size_t)max_chunks * 4);
     Lo.off_psum = take((size_t)((max_chunks + 1023) / 1024 + 1) * 8);
     Lo.off_pend = take((size_t)max_chunks * 2);
     Lo.off_thru = take((size_t)max_chunks);
@@ -1171,6 +1172,7 @@ extern "C" int dc64_decode_device(int ct, const void* d_stream, long long nbytes
     uint8_t* sx = (uint8_t*)(base + Lo.off_sx);
     uint16_t* sn = (uint16_t*)(base + Lo.off_sn);
     uint8_t* bad = (uint8_t*)(base + Lo.off_bad);
+    unsigned* list = (unsigned*)(base + Lo.off_list);
     unsigned long long* cb0 = (unsigned long long*)(base + Lo.off_base[0]);
     const unsigned g64 = (unsigned)((max_chunks + 63) / 64), g256 = (unsigned)((max_chunks + 255) / 256);
     const unsigned g1k = (unsigned)((max_chunks + 1023) / 1024);
@@ -1178,8 +1180,9 @@ extern "C" int dc64_decode_device(int ct, const void* d_stream, long long nbytes
     H64(hipMemsetAsync(C64.ctr, 0, sizeof(unsigned) * (ROUNDS + 1), st));
     DISPATCH64(ct, dec_spec, dim3(g64), dim3(64), 0, st, W, C64.plan, P, se, sx, sn);
     for (int r = 0; r <= ROUNDS; r++) {
-        hipLaunchKernelGGL(dec_links, dim3(g256), dim3(256), 0, st, C64.plan, se, sx, bad, C64.ctr + r);
-        if (r < ROUNDS) DISPATCH64(ct, dec_relink, dim3(g64), dim3(64), 0, st, W, C64.plan, P, se, sx, sn, bad, C64.ctr + r);
+        hipLaunchKernelGGL(dec_links, dim3(g256), dim3(256), 0, st, C64.plan, se, sx, bad, C64.ctr + r, list);
+        if (r < ROUNDS) DISPATCH64(ct, dec_relink, dim3(1024), dim3(64), 0, st, W, C64.plan, P, se, sx, sn, bad, C64.ctr + r,
+                                   list);
     }
     H64(hipMemcpyAsync(C64.h + 6, C64.ctr + ROUNDS, 4, hipMemcpyDeviceToHost, st));
     H64(hipStreamSynchronize(st));
@@ -1259,14 +1262,13 @@ extern "C" long long dc64_debug_chunks(uint8_t* e, uint8_t* x, uint16_t* n, unsi
     if (ensure64(&st)) return -1;
     Plan64 pl;
     if (hipMemcpy(&pl, C64.plan, sizeof pl, hipMemcpyDeviceToHost) != hipSuccess) return -1;
-    const long long nc = std::min(pl.nchunks, cap < 0 ? -cap : cap);
+    const long long nc = std::min(pl.nchunks, cap);
     const DecLayout Lo = layout(C64.dbg_words, C64.dbg_chunks);
     char* base = (char*)C64.pool;
     (void)hipMemcpy(e, base + Lo.off_ent[0], nc, hipMemcpyDeviceToHost);
     (void)hipMemcpy(x, base + Lo.off_sx, nc, hipMemcpyDeviceToHost);
     (void)hipMemcpy(n, base + Lo.off_sn, nc * 2, hipMemcpyDeviceToHost);
     (void)hipMemcpy(b, base + Lo.off_base[0], nc * 8, hipMemcpyDeviceToHost);
-    if (cap < 0) (void)hipMemcpy(e, base + Lo.off_rl, nc, hipMemcpyDeviceToHost);
     return nc;
 }
 
