@@ -511,7 +511,10 @@ __global__ __launch_bounds__(64) void dec_map(const uint32_t* __restrict__ W, co
 #ifndef DC64_OVB
 #define DC64_OVB 2048
 #endif
-constexpr int OVB = DC64_OVB;                // pre-walk overlap (bits)
+constexpr int OVB = DC64_OVB;
+#ifndef DC64_RING
+#define DC64_RING 0                              // 1: 64-byte output sectors through a padded LDS ring
+#endif                // pre-walk overlap (bits)
 constexpr int OVW = OVB / 32;
 constexpr int GWS = OVW + 64 * MAPW + 8;
 constexpr int SWS = GWS + GWS / 64 + 2;
@@ -709,6 +712,9 @@ __global__ __launch_bounds__(64) void dec_chunks(const uint32_t* __restrict__ W,
                                                  long long num, uint16_t* __restrict__ pend, uint8_t* __restrict__ thru,
                                                  unsigned* __restrict__ err) {
     __shared__ uint32_t S[SW];
+#if DC64_RING
+    __shared__ double RING[64 * 17];
+#endif
     const long long g0 = blockIdx.x * 64ll;
     if (g0 >= pl->nchunks) return;
     stage_group(S, W, g0 * MAPW, pl->nwords + 4);
@@ -720,6 +726,9 @@ __global__ __launch_bounds__(64) void dec_chunks(const uint32_t* __restrict__ W,
     const uint32_t cs = threadIdx.x * CB, ce = cs + CB;
     uint32_t p = cs + cent[c];
     const long long k0 = (long long)cbase[c];
+#if DC64_RING
+    double* ring = RING + threadIdx.x * 17;               // 16 doubles + 1 pad (2-way LDS conflicts)
+#endif
     double f1 = -1.0, f2 = -1.0, f3 = -1.0;
     int q1 = c ? 1 : 0, q2 = c ? 2 : 0, q3 = c ? 3 : 0;
     int pd = 0;
@@ -753,6 +762,25 @@ __global__ __launch_bounds__(64) void dec_chunks(const uint32_t* __restrict__ W,
         if (q) pd = (int)j + 1;
         else bad |= d2u(v) == 0xBFF0000000000000ull;                       // the -1.0 history sentinel
         const long long g = k0 + j;
+#if DC64_RING
+        if (al) {
+            ring[g & 15] = v;
+            if ((g & 7) == 7) {
+                if (g - 7 >= k0) {
+                    const int b = (int)((g - 7) & 15);
+                    double2* o2 = reinterpret_cast<double2*>(out + (g - 7));
+                    o2[0] = make_double2(ring[b], ring[b + 1]);
+                    o2[1] = make_double2(ring[b + 2], ring[b + 3]);
+                    o2[2] = make_double2(ring[b + 4], ring[b + 5]);
+                    o2[3] = make_double2(ring[b + 6], ring[b + 7]);
+                } else {
+                    for (long long i = k0; i <= g; i++) out[i] = ring[i & 15];
+                }
+            }
+        } else if (!q) {
+            out[g] = v;
+        }
+#else
         if (al) {
             const int sl = (int)(g & 3);
             r0 = sl == 0 ? v : r0; r1 = sl == 1 ? v : r1; r2 = sl == 2 ? v : r2; r3 = sl == 3 ? v : r3;
@@ -768,14 +796,20 @@ __global__ __launch_bounds__(64) void dec_chunks(const uint32_t* __restrict__ W,
         } else if (!q) {
             out[g] = v;
         }
+#endif
         f3 = f2; q3 = q2; f2 = f1; q2 = q1; f1 = v; q1 = q;
         p += (uint32_t)l;
         j++;
     }
     if (al && j > 0) {                                                     // the partial last sector
         const long long gl = k0 + j - 1;
+#if DC64_RING
+        if ((gl & 7) != 7)
+            for (long long i = std::max(k0, gl & ~7ll); i <= gl; i++) out[i] = ring[i & 15];
+#else
         if ((gl & 3) != 3)
             for (long long i = std::max(k0, gl & ~3ll); i <= gl; i++) put(i);
+#endif
     }
     pend[c] = (uint16_t)pd;
     thru[c] = (uint8_t)((q1 | q2 | q3) ? 1 : 0);
