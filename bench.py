@@ -253,6 +253,13 @@ def f64_bench(args):
                       "stream_bytes": int(nbytes), "ratio": round(8.0 * n / nbytes, 4), "type": typ,
                       "mask20": f"{mask20:05x}", "parallelism": f"dp{world}", "exact_fallback": bool(flags & 1)},
            "phases_ms": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4), "med_dataset_double_s": round(t_med, 4)}}
+    # roofline of the dominant phase (decode: stream in, doubles out), HIP events on the library stream
+    dbytes = float(nbytes) + 8.0 * n
+    dach = dbytes / (dec_ms * 1e-3) / 1e9 if dec_ms > 0 else 0.0
+    res["roofline"] = {"bound": "hbm", "kernel": "double decode (all launches of dc64_decode_device)",
+                       "achieved": round(dach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": round(dach / HBM_PEAK_GBS, 4), "traffic": None,
+                       "algorithmic_bytes_per_launch": int(dbytes), "avg_launch_ms": round(dec_ms, 4)}
     if ok is not None:
         res["check_vs_oracle"] = ok
     if rank == 0 and not args.no_cpu:
