@@ -31,6 +31,7 @@ int absErrorBound_binary = -100;
 typedef struct {
     int inited, device;
     hipStream_t st;
+    hipStream_t enc_st;              /* encoder stream (dc_set_encode_stream), NULL = st */
     /* encoder */
     uint64_t* enc_desc;
     long long enc_desc_cap;
@@ -94,6 +95,16 @@ static int seterr(int code, const char* fmt, ...) {
     } while (0)
 
 const char* dc_last_error(void) { return G.msg; }
+#define ENC_ST (G.enc_st ? G.enc_st : G.st)
+static int ensure_init(void);
+/* encoder launches go to this HIP stream (NULL: the library stream), so a caller can overlap the
+ * encode of one buffer with the decode of another; the caller orders dependent work with events */
+int dc_set_encode_stream(void* stream) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    G.enc_st = (hipStream_t)stream;
+    return DC_OK;
+}
 int dc_set_error(int code, const char* msg) { return seterr(code, "%s", msg); }
 void* dc_get_stream(void) { return (void*)G.st; }
 void dc_set_abs_error_bound(double bound) { absErrBound = bound; absErrorBound_binary = -100; }
@@ -200,6 +211,7 @@ int dc_synchronize(void) {
     int rc = ensure_init();
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(G.st));
+    if (G.enc_st) HIPCHK(hipStreamSynchronize(G.enc_st));
     return DC_OK;
 }
 
@@ -286,19 +298,19 @@ int dc_encode_device(int ct, const void* d_x, long long n, long long idx0, int t
         if (G.enc_desc) HIPCHK(hipFree(G.enc_desc));
         long long cap = dc_encode_desc_words(n) + 1024;
         HIPCHK(hipMalloc((void**)&G.enc_desc, cap * sizeof(uint64_t)));
-        HIPCHK(hipMemsetAsync(G.enc_desc, 0, cap * sizeof(uint64_t), G.st));
+        HIPCHK(hipMemsetAsync(G.enc_desc, 0, cap * sizeof(uint64_t), ENC_ST));
         G.enc_desc_cap = cap;
         G.enc_epoch = 1;
     }
     if (++G.enc_epoch >= (1u << 22)) {          /* flags carry 22 epoch bits */
-        HIPCHK(hipMemsetAsync(G.enc_desc, 0, G.enc_desc_cap * sizeof(uint64_t), G.st));
+        HIPCHK(hipMemsetAsync(G.enc_desc, 0, G.enc_desc_cap * sizeof(uint64_t), ENC_ST));
         G.enc_epoch = 1;
     }
     unsigned long long* tot = d_total_bits ? d_total_bits : G.d_total;
     if (n == 0) {
         unsigned long long v = (unsigned long long)start_bit;
-        HIPCHK(hipMemcpyAsync(tot, &v, sizeof v, hipMemcpyHostToDevice, G.st));
-        if (tot != G.d_total) HIPCHK(hipMemcpyAsync(G.d_total, &v, sizeof v, hipMemcpyHostToDevice, G.st));
+        HIPCHK(hipMemcpyAsync(tot, &v, sizeof v, hipMemcpyHostToDevice, ENC_ST));
+        if (tot != G.d_total) HIPCHK(hipMemcpyAsync(G.d_total, &v, sizeof v, hipMemcpyHostToDevice, ENC_ST));
         return DC_OK;
     }
     if (getenv("DC_DEBUG_STAMPS") && !G.enc_dbg) {
@@ -306,9 +318,9 @@ int dc_encode_device(int ct, const void* d_x, long long n, long long idx0, int t
         HIPCHK(hipMemset(G.enc_dbg, 0, 8192 * 8 * 8));
     }
     if (dc_launch_encode((const float*)d_x, n, idx0, &P, (uint32_t*)d_out, G.enc_desc, G.enc_ctr, G.enc_epoch,
-                         start_bit, tot, G.d_enc_err, G.enc_dbg, G.st))
+                         start_bit, tot, G.d_enc_err, G.enc_dbg, ENC_ST))
         return seterr(DC_ERR_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
-    if (tot != G.d_total) HIPCHK(hipMemcpyAsync(G.d_total, tot, 8, hipMemcpyDeviceToDevice, G.st));
+    if (tot != G.d_total) HIPCHK(hipMemcpyAsync(G.d_total, tot, 8, hipMemcpyDeviceToDevice, ENC_ST));
     return DC_OK;
 }
 
@@ -330,12 +342,12 @@ int dc_encode_bits_device(int ct, const void* d_x, long long n, long long idx0, 
         HIPCHK(hipMalloc((void**)&G.enc_desc, cap * sizeof(uint64_t)));
         G.enc_desc_cap = cap;
     }
-    HIPCHK(hipMemsetAsync(G.d_enc_err, 0, 4, G.st));
-    if (dc_launch_encode_bits((const float*)d_x, n, idx0, &P, G.enc_desc, G.d_total, G.d_enc_err, G.st))
+    HIPCHK(hipMemsetAsync(G.d_enc_err, 0, 4, ENC_ST));
+    if (dc_launch_encode_bits((const float*)d_x, n, idx0, &P, G.enc_desc, G.d_total, G.d_enc_err, ENC_ST))
         return seterr(DC_ERR_HIP, "encode launch failed");
-    HIPCHK(hipMemcpyAsync(&G.h_scratch[0], G.d_total, 8, hipMemcpyDeviceToHost, G.st));
-    HIPCHK(hipMemcpyAsync(&G.h_scratch[1], G.d_enc_err, 4, hipMemcpyDeviceToHost, G.st));
-    HIPCHK(hipStreamSynchronize(G.st));
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[0], G.d_total, 8, hipMemcpyDeviceToHost, ENC_ST));
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[1], G.d_enc_err, 4, hipMemcpyDeviceToHost, ENC_ST));
+    HIPCHK(hipStreamSynchronize(ENC_ST));
     if (G.h_scratch[1] & 1u) return seterr(DC_ERR_INPUT, "input contains -1.0f (the reference's history sentinel)");
     *bits_out = G.h_scratch[0];
     return DC_OK;
@@ -344,12 +356,12 @@ int dc_encode_bits_device(int ct, const void* d_x, long long n, long long idx0, 
 int dc_encode_result(unsigned long long* total_bits) {
     int rc = ensure_init();
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(&G.h_scratch[0], G.d_total, 8, hipMemcpyDeviceToHost, G.st));
-    HIPCHK(hipMemcpyAsync(&G.h_scratch[1], G.d_enc_err, 4, hipMemcpyDeviceToHost, G.st));
-    HIPCHK(hipStreamSynchronize(G.st));
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[0], G.d_total, 8, hipMemcpyDeviceToHost, ENC_ST));
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[1], G.d_enc_err, 4, hipMemcpyDeviceToHost, ENC_ST));
+    HIPCHK(hipStreamSynchronize(ENC_ST));
     unsigned err = (unsigned)(G.h_scratch[1] & 0xFFFFFFFFu);
     if (err) {
-        HIPCHK(hipMemsetAsync(G.d_enc_err, 0, 4, G.st));
+        HIPCHK(hipMemsetAsync(G.d_enc_err, 0, 4, ENC_ST));
         if (err & 1u)
             return seterr(DC_ERR_INPUT, "input contains -1.0f, the reference encoder's empty-history sentinel "
                                         "(impl/dataCompression.c:2032); CT5/7/11 inputs must be >= 0 (toSmallDataset_float)");

@@ -31,6 +31,7 @@ int dc_init(int device);                       /* optional; first call of any en
 const char* dc_last_error(void);
 void* dc_get_stream(void);                     /* hipStream_t all library work is ordered on */
 int dc_synchronize(void);
+int dc_set_encode_stream(void* stream);        /* encoder launches on this hipStream_t (NULL: dc_get_stream()) */
 void dc_set_abs_error_bound(double bound);     /* runtime absErrorBound (default: header macro) */
 double dc_get_abs_error_bound(void);
 
