@@ -42,7 +42,7 @@ EXT_SYMBOLS = [
     "dc_crc32_device_async", "dc_flip_bits_device", "dc_decode_shard_device", "dc_decode_shard_fix",
     "dc_halo_encode_device", "dc_halo_decode_device",
     "dc64_stream_capacity", "dc64_encode_device", "dc64_encode_result", "dc64_decode_device", "dc64_decode_finish",
-    "dc64_last_decode_flags", "dc64_to_small_device", "dc64_med_device",
+    "dc64_last_decode_flags", "dc64_to_small_device", "dc64_med_device", "dc_set_encode_stream",
 ]
 
 
