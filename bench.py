@@ -419,7 +419,6 @@ def main():
     # ---- timed region: barrier + sync on both sides, max over ranks.  Per-kernel HIP events are
     # recorded by the library on its own stream (dc_timing_enable), one event set per step.
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    pipelined = False                                  # the timed steps run back to back
     if args.ber <= 0:
         # two stream buffers; the encoder on its own stream: enc(k+1) || dec(k).  dec(k) waits for
         # enc(k); enc(k+2) (same buffer as k) waits for dec(k).
@@ -447,27 +446,14 @@ def main():
                             d_nbits=nb2[b].data_ptr(), max_bytes=cap)
             dec_done[k].record(ext)
 
-        dec_end = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-        # warm the pipelined path (both buffers, both streams)
-        torch.cuda.synchronize()
-        L.synchronize()
     L.L.dc_timing_enable(args.steps)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     L.synchronize()
     t0 = time.perf_counter()
-    if pipelined:
-        L.check(L.L.dc_set_encode_stream(ctypes.c_void_p(es.cuda_stream)), "dc_set_encode_stream")
-        enc(0)
-        for k in range(args.steps):
-            if k + 1 < args.steps:
-                enc(k + 1)
-            dec(k)
-            dec_end[k].record(ext)
-    else:
-        for k in range(args.steps):
-            step(evs[k])
+    for k in range(args.steps):
+        step(evs[k])
     L.synchronize()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -481,11 +467,7 @@ def main():
         dist.all_reduce(w, op=dist.ReduceOp.MAX)
         wall = float(w[0])
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    if pipelined:
-        dec_ms = float(np.mean([evs[k][2].elapsed_time(dec_end[k]) for k in range(args.steps)]))
-        L.L.dc_set_encode_stream(None)
-    else:
-        dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     import ctypes
     kms = np.zeros((args.steps, 6), np.float32)
     for k in range(args.steps):
@@ -494,7 +476,7 @@ def main():
             kms[k] = np.frombuffer(buf, np.float32)
     L.L.dc_timing_enable(0)
     kavg = kms.mean(axis=0)
-    if not pipelined and args.ber <= 0 and not args.no_pipelined:
+    if args.ber <= 0 and not args.no_pipelined:
         # the same K steps pipelined (encode k+1 || decode k), reported beside the serial value
         L.synchronize()
         torch.cuda.synchronize()
@@ -583,10 +565,6 @@ def main():
     }
     if pipe is not None:
         res["pipelined"] = pipe
-    if pipelined:
-        res["config"]["pipelining"] = ("encode of step k+1 on its own HIP stream overlaps the decode of step k "
-                                       "(two stream buffers); every step encodes and decodes the whole block; "
-                                       "kernel times are measured while the two overlap")
     if ok is not None:
         res["check_vs_oracle"] = ok
     if args.ber > 0:
