@@ -120,24 +120,44 @@ __device__ __forceinline__ void token_at(const double* __restrict__ x, long long
     make_token<CT>(v, b1, b2, b3, pred, P, val, len);
 }
 
+// the tokens of the 4 consecutive elements e0..e0+3 from one load of x[e0-3 .. e0+3]
+template <int CT>
+__device__ __forceinline__ void tokens4(const double* __restrict__ x, long long n, long long e0, const P64& P,
+                                        uint64_t* val, int* len, bool* neg1) {
+    double w[7];
+    if (e0 >= 3 && e0 + 4 <= n) {
+#pragma unroll
+        for (int i = 0; i < 7; i++) w[i] = x[e0 - 3 + i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 7; i++) {
+            const long long e = e0 - 3 + i;
+            w[i] = (e >= 0 && e < n) ? x[e] : 0.0;
+        }
+    }
+    bool m1 = false;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        val[k] = 0; len[k] = 0;
+        if (e0 + k < n) {
+            make_token<CT>(w[3 + k], w[2 + k], w[1 + k], w[k], e0 + k >= 3, P, val[k], len[k]);
+            m1 |= w[3 + k] == -1.0;
+        }
+    }
+    *neg1 = m1;
+}
+
 template <int CT>
 __global__ __launch_bounds__(ETPB) void enc_count(const double* __restrict__ x, long long n, P64 P,
                                                  uint32_t* __restrict__ tbits, unsigned* __restrict__ err) {
     __shared__ uint32_t part[ETPB / 64];
     const long long t = blockIdx.x;
     const long long e0 = t * ETILE + 4 * threadIdx.x;
-    uint32_t sum = 0;
+    uint64_t vv[4];
+    int ll[4];
     bool neg1 = false;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const long long e = e0 + k;
-        if (e < n) {
-            uint64_t v; int l;
-            token_at<CT>(x, e, P, v, l);
-            sum += (uint32_t)l;
-            neg1 |= x[e] == -1.0;
-        }
-    }
+    tokens4<CT>(x, n, e0, P, vv, ll, &neg1);
+    uint32_t sum = (uint32_t)(ll[0] + ll[1] + ll[2] + ll[3]);
     if (neg1) atomicOr(err, ERR_SERIAL);
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
@@ -276,13 +296,9 @@ __global__ __launch_bounds__(ETPB) void enc_write(const double* __restrict__ x, 
     const long long e0 = t * ETILE + 4 * threadIdx.x;
     uint64_t val[4];
     int len[4];
-    uint32_t sum = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        len[k] = 0; val[k] = 0;
-        if (e0 + k < n) token_at<CT>(x, e0 + k, P, val[k], len[k]);
-        sum += (uint32_t)len[k];
-    }
+    bool neg1;                                        // (reported by the count pass)
+    tokens4<CT>(x, n, e0, P, val, len, &neg1);
+    const uint32_t sum = (uint32_t)(len[0] + len[1] + len[2] + len[3]);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t s = sum;
 #pragma unroll
