@@ -975,6 +975,8 @@ static int decode_grid(int ct) {
                   : ct == 7 ? (const void*)decode_kernel_fast<7> : (const void*)decode_kernel_fast<11>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, GROUP, 0) != hipSuccess || per < 1) per = 1;
     cache[ci] = per * ncu;
+    const char* e = getenv("DC_DECODE_GRID");                 // experiment override
+    if (e && atoi(e) > 0) cache[ci] = atoi(e);
     return cache[ci];
 }
 
