@@ -132,8 +132,11 @@ __global__ __launch_bounds__(256) void med_kernel(const float* __restrict__ x, l
 constexpr int MX_CH = 8192;                                // floats staged per chunk
 constexpr int MX_T = 1024;
 
-__global__ __launch_bounds__(MX_T) void med_exact_kernel(const float* __restrict__ x, long long n,
-                                                         float* __restrict__ out_mean, int* __restrict__ out_type) {
+// s_init: the running sum before x[0] (0 for the whole array; a multi-GPU shard continues its
+// predecessor's sum); out_sum / out_max (optional) receive the raw sum and max.
+__global__ __launch_bounds__(MX_T) void med_exact_kernel(const float* __restrict__ x, long long n, float s_init,
+                                                         float* __restrict__ out_mean, int* __restrict__ out_type,
+                                                         float* __restrict__ out_sum, float* __restrict__ out_max) {
     __shared__ float buf[MX_CH];
     __shared__ int fd[2][2][MX_T];                          // [buffer][start parity] units added
     __shared__ unsigned char fe[2][2][MX_T];                // [buffer][start parity] end parity
@@ -143,13 +146,24 @@ __global__ __launch_bounds__(MX_T) void med_exact_kernel(const float* __restrict
     __shared__ float smax[MX_T];
     const int tid = threadIdx.x;
     float mx = x[0];
-    if (tid == 0) s_sum = 0.0f;
+    if (tid == 0) s_sum = s_init;
     for (long long c0 = 0; c0 < n; c0 += MX_CH) {
         const int m = (int)min((long long)MX_CH, n - c0);
         for (int i = tid; i < m; i += MX_T) { const float v = x[c0 + i]; buf[i] = v; mx = v > mx ? v : mx; }
         if (tid == 0) s_start = 0;
         __syncthreads();
         while (true) {
+            if (s_sum == 0.0f) {                            // fl(0 + 0) = 0: skip a zero run in parallel
+                __shared__ int s_nz;
+                if (tid == 0) s_nz = m;
+                __syncthreads();
+                const int st0 = s_start;
+                for (int i = st0 + tid; i < m; i += MX_T)
+                    if (__float_as_uint(buf[i]) != 0u) { atomicMin(&s_nz, i); break; }
+                __syncthreads();
+                if (tid == 0) s_start = s_nz;
+                __syncthreads();
+            }
             if (tid == 0) {                                 // small sums: exact serial adds
                 float sv = s_sum;
                 int st = s_start;
@@ -248,6 +262,8 @@ __global__ __launch_bounds__(MX_T) void med_exact_kernel(const float* __restrict
         }
         *out_type = type;
         *out_mean = __fdiv_rn(s_sum, (float)n);
+        if (out_sum) *out_sum = s_sum;
+        if (out_max) *out_max = mm;
     }
 }
 
@@ -435,7 +451,16 @@ extern "C" int dc_launch_to_small(const float* x, long long n, float* y, float* 
 
 extern "C" int dc_launch_med(const float* x, long long n, float* d_mean, int* d_type, hipStream_t st) {
     if (n <= 0) return 0;
-    hipLaunchKernelGGL(med_exact_kernel, dim3(1), dim3(MX_T), 0, st, x, n, d_mean, d_type);
+    hipLaunchKernelGGL(med_exact_kernel, dim3(1), dim3(MX_T), 0, st, x, n, 0.0f, d_mean, d_type, (float*)nullptr,
+                       (float*)nullptr);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// the running float sum of med_dataset_float continued from s_init over x[0..n) (+ the max of x)
+extern "C" int dc_launch_med_sum(const float* x, long long n, float s_init, float* d_sum, float* d_max, float* d_mean,
+                                 int* d_type, hipStream_t st) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(med_exact_kernel, dim3(1), dim3(MX_T), 0, st, x, n, s_init, d_mean, d_type, d_sum, d_max);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -205,6 +205,9 @@ struct ParseShared {
     uint8_t x[GROUP], nk[GROUP], stdexit[GROUP], dev[GROUP];
     uint32_t wsum[GROUP / 64];
     int texit;
+#ifdef DC_PARSE_PAD
+    uint32_t occpad[DC_PARSE_PAD / 4];          // occupancy experiment: extra LDS per workgroup
+#endif
 };
 
 __device__ __forceinline__ int next_bad(const uint64_t* bad, int c, int nact) {
@@ -660,6 +663,9 @@ struct DecodeShared {
     float tin[3];
     int need, cplx, defer;
     long long tile;
+#ifdef DC_DEC_PAD
+    uint32_t occpad[DC_DEC_PAD / 4];            // occupancy experiment: extra LDS per workgroup
+#endif
 };
 
 __device__ __forceinline__ uint64_t hpack(uint64_t flag, uint32_t epoch, uint32_t kind, float v) {

@@ -32,6 +32,10 @@ typedef struct {
     int inited, device;
     hipStream_t st;
     hipStream_t enc_st;              /* encoder stream (dc_set_encode_stream), NULL = st */
+    hipEvent_t ev_enc;               /* orders an encode on enc_st after the work queued on st */
+    hipEvent_t ev_lib;               /* orders an internal encode on st after the work queued on enc_st */
+    hipStream_t last_enc_st;         /* stream of the last encode (dc_encode_result waits on it) */
+    int abi_rc;                      /* status of the last reference-ABI call (dc_abi_status) */
     /* encoder */
     uint64_t* enc_desc;
     long long enc_desc_cap;
@@ -46,6 +50,7 @@ typedef struct {
     long long dec_cap_chunks;
     uint32_t dec_epoch;
     int dec_pending;
+    int dec_queued;                  /* decodes issued since the last finish */
     Params dec_P;
     const uint8_t* dec_s;
     long long dec_max_chunks;
@@ -103,8 +108,11 @@ int dc_set_encode_stream(void* stream) {
     int rc = ensure_init();
     if (rc) return rc;
     G.enc_st = (hipStream_t)stream;
+    if (G.enc_st == G.st) G.enc_st = NULL;
     return DC_OK;
 }
+int dc_abi_status(void) { return G.abi_rc; }
+void dc_abi_set_status(int rc) { G.abi_rc = rc; }      /* the double ABI (dc_host64.c) reports through it too */
 int dc_set_error(int code, const char* msg) { return seterr(code, "%s", msg); }
 void* dc_get_stream(void) { return (void*)G.st; }
 void dc_set_abs_error_bound(double bound) { absErrBound = bound; absErrorBound_binary = -100; }
@@ -166,6 +174,8 @@ int dc_init(int device) {
         return seterr(DC_ERR_NOGPU, "device %d is %s, libdcamd is built for gfx950", device, prop.gcnArchName);
     G.device = device;
     HIPCHK(hipStreamCreateWithFlags(&G.st, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&G.ev_enc, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&G.ev_lib, hipEventDisableTiming));
     HIPCHK(hipHostMalloc((void**)&G.h_scratch, 64 * sizeof(unsigned long long), 0));
     HIPCHK(hipMalloc((void**)&G.enc_ctr, 64));
     HIPCHK(hipMemset(G.enc_ctr, 0, 64));
@@ -284,10 +294,33 @@ static int valid_ct(int ct) { return ct == 5 || ct == 6 || ct == 7 || ct == 11; 
 size_t dc_stream_capacity(long long n) { return (size_t)((n * 32 + 7 + 31) / 32) * 4 + 64; }
 
 /* ------------------------------------------------------------------------------------------ */
+static int encode_on(hipStream_t st, int ct, const void* d_x, long long n, long long idx0, int type, uint32_t mask17,
+                     int start_bit, void* d_out, unsigned long long* d_total_bits);
+
+/* public entry: on the encode stream (dc_set_encode_stream) after the work queued on the library stream */
 int dc_encode_device(int ct, const void* d_x, long long n, long long idx0, int type, uint32_t mask17,
                      int start_bit, void* d_out, unsigned long long* d_total_bits) {
     int rc = ensure_init();
     if (rc) return rc;
+    if (G.enc_st) {
+        HIPCHK(hipEventRecord(G.ev_enc, G.st));
+        HIPCHK(hipStreamWaitEvent(G.enc_st, G.ev_enc, 0));
+    }
+    return encode_on(ENC_ST, ct, d_x, n, idx0, type, mask17, start_bit, d_out, d_total_bits);
+}
+
+/* internal callers (host ABI, halo path): always on the library stream */
+static int encode_lib(int ct, const void* d_x, long long n, long long idx0, int type, uint32_t mask17, int start_bit,
+                      void* d_out, unsigned long long* d_total_bits) {
+    if (G.enc_st) {                       /* the encoder scratch is shared with encodes on the encode stream */
+        HIPCHK(hipEventRecord(G.ev_lib, G.enc_st));
+        HIPCHK(hipStreamWaitEvent(G.st, G.ev_lib, 0));
+    }
+    return encode_on(G.st, ct, d_x, n, idx0, type, mask17, start_bit, d_out, d_total_bits);
+}
+
+static int encode_on(hipStream_t st, int ct, const void* d_x, long long n, long long idx0, int type, uint32_t mask17,
+                     int start_bit, void* d_out, unsigned long long* d_total_bits) {
     if (!valid_ct(ct)) return seterr(DC_ERR_ARG, "unsupported CT %d", ct);
     if (start_bit < 0 || start_bit > 7 || n < 0) return seterr(DC_ERR_ARG, "bad start_bit/n");
     if (ct == 7 && (type < 1 || type > 7)) return seterr(DC_ERR_ARG, "CT7 type %d outside 1..7", type);
@@ -298,19 +331,20 @@ int dc_encode_device(int ct, const void* d_x, long long n, long long idx0, int t
         if (G.enc_desc) HIPCHK(hipFree(G.enc_desc));
         long long cap = dc_encode_desc_words(n) + 1024;
         HIPCHK(hipMalloc((void**)&G.enc_desc, cap * sizeof(uint64_t)));
-        HIPCHK(hipMemsetAsync(G.enc_desc, 0, cap * sizeof(uint64_t), ENC_ST));
+        HIPCHK(hipMemsetAsync(G.enc_desc, 0, cap * sizeof(uint64_t), st));
         G.enc_desc_cap = cap;
         G.enc_epoch = 1;
     }
     if (++G.enc_epoch >= (1u << 22)) {          /* flags carry 22 epoch bits */
-        HIPCHK(hipMemsetAsync(G.enc_desc, 0, G.enc_desc_cap * sizeof(uint64_t), ENC_ST));
+        HIPCHK(hipMemsetAsync(G.enc_desc, 0, G.enc_desc_cap * sizeof(uint64_t), st));
         G.enc_epoch = 1;
     }
     unsigned long long* tot = d_total_bits ? d_total_bits : G.d_total;
+    G.last_enc_st = st;
     if (n == 0) {
         unsigned long long v = (unsigned long long)start_bit;
-        HIPCHK(hipMemcpyAsync(tot, &v, sizeof v, hipMemcpyHostToDevice, ENC_ST));
-        if (tot != G.d_total) HIPCHK(hipMemcpyAsync(G.d_total, &v, sizeof v, hipMemcpyHostToDevice, ENC_ST));
+        HIPCHK(hipMemcpyAsync(tot, &v, sizeof v, hipMemcpyHostToDevice, st));
+        if (tot != G.d_total) HIPCHK(hipMemcpyAsync(G.d_total, &v, sizeof v, hipMemcpyHostToDevice, st));
         return DC_OK;
     }
     if (getenv("DC_DEBUG_STAMPS") && !G.enc_dbg) {
@@ -318,9 +352,9 @@ int dc_encode_device(int ct, const void* d_x, long long n, long long idx0, int t
         HIPCHK(hipMemset(G.enc_dbg, 0, 8192 * 8 * 8));
     }
     if (dc_launch_encode((const float*)d_x, n, idx0, &P, (uint32_t*)d_out, G.enc_desc, G.enc_ctr, G.enc_epoch,
-                         start_bit, tot, G.d_enc_err, G.enc_dbg, ENC_ST))
+                         start_bit, tot, G.d_enc_err, G.enc_dbg, st))
         return seterr(DC_ERR_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
-    if (tot != G.d_total) HIPCHK(hipMemcpyAsync(G.d_total, tot, 8, hipMemcpyDeviceToDevice, ENC_ST));
+    if (tot != G.d_total) HIPCHK(hipMemcpyAsync(G.d_total, tot, 8, hipMemcpyDeviceToDevice, st));
     return DC_OK;
 }
 
@@ -336,6 +370,10 @@ int dc_encode_bits_device(int ct, const void* d_x, long long n, long long idx0, 
     if (n == 0) { *bits_out = 0; return DC_OK; }
     Params P;
     make_params(&P, ct, type, mask17);
+    if (G.enc_st) {
+        HIPCHK(hipEventRecord(G.ev_enc, G.st));
+        HIPCHK(hipStreamWaitEvent(G.enc_st, G.ev_enc, 0));
+    }
     if (dc_encode_desc_words(n) + 8 > G.enc_desc_cap) {
         if (G.enc_desc) HIPCHK(hipFree(G.enc_desc));
         const long long cap = dc_encode_desc_words(n) + 1024;
@@ -356,12 +394,13 @@ int dc_encode_bits_device(int ct, const void* d_x, long long n, long long idx0, 
 int dc_encode_result(unsigned long long* total_bits) {
     int rc = ensure_init();
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(&G.h_scratch[0], G.d_total, 8, hipMemcpyDeviceToHost, ENC_ST));
-    HIPCHK(hipMemcpyAsync(&G.h_scratch[1], G.d_enc_err, 4, hipMemcpyDeviceToHost, ENC_ST));
-    HIPCHK(hipStreamSynchronize(ENC_ST));
+    hipStream_t st = G.last_enc_st ? G.last_enc_st : G.st;
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[0], G.d_total, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[1], G.d_enc_err, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
     unsigned err = (unsigned)(G.h_scratch[1] & 0xFFFFFFFFu);
     if (err) {
-        HIPCHK(hipMemsetAsync(G.d_enc_err, 0, 4, ENC_ST));
+        HIPCHK(hipMemsetAsync(G.d_enc_err, 0, 4, st));
         if (err & 1u)
             return seterr(DC_ERR_INPUT, "input contains -1.0f, the reference encoder's empty-history sentinel "
                                         "(impl/dataCompression.c:2032); CT5/7/11 inputs must be >= 0 (toSmallDataset_float)");
@@ -436,6 +475,18 @@ static int dec_ensure(long long max_chunks) {
     return DC_OK;
 }
 
+/* next decoder epoch; look-back flags carry 22 epoch bits, so on a wrap the flag arrays are cleared
+ * (a stale flag of an old epoch must never read as published) */
+static int dec_next_epoch(void) {
+    if (++G.dec_epoch >= (1u << 22)) {
+        const long long GR = (G.dec_cap_chunks + dc_decode_group() - 1) / dc_decode_group() + 1;
+        HIPCHK(hipMemsetAsync(G.D.gran, 0, (size_t)GR * 34 * 8, G.st));
+        HIPCHK(hipMemsetAsync(G.D.hist, 0, (size_t)GR * 6 * 8, G.st));
+        G.dec_epoch = 1;
+    }
+    return DC_OK;
+}
+
 #define DEC_ROUNDS 3
 #define DEC_FIX_ITERS 3
 
@@ -453,12 +504,7 @@ int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsig
     if (max_chunks < 1) max_chunks = 1;
     rc = dec_ensure(max_chunks);
     if (rc) return rc;
-    if (++G.dec_epoch >= (1u << 22)) {
-        long long GR = (G.dec_cap_chunks + dc_decode_group() - 1) / dc_decode_group() + 1;
-        HIPCHK(hipMemsetAsync(G.D.gran, 0, (size_t)GR * 34 * 8, G.st));
-        HIPCHK(hipMemsetAsync(G.D.hist, 0, (size_t)GR * 6 * 8, G.st));
-        G.dec_epoch = 1;
-    }
+    if ((rc = dec_next_epoch())) return rc;
     Params P;
     make_params(&P, ct, type, mask17);
     if (dc_launch_decode_fast((const uint8_t*)d_stream, nbytes >= 0 ? NULL : d_nbits,
@@ -466,6 +512,7 @@ int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsig
                               (float*)d_out, num, G.dec_epoch, G.st))
         return seterr(DC_ERR_HIP, "decode launch failed: %s", hipGetErrorString(hipGetLastError()));
     G.dec_pending = 1;
+    G.dec_queued++;
     G.dec_shard = G.D.shard;
     G.dec_P = P;
     G.dec_s = (const uint8_t*)d_stream;
@@ -484,13 +531,32 @@ static int read_dec_err(unsigned* err) {
     return DC_OK;
 }
 
+int dc_decode_status(unsigned* status_out) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    unsigned err = 0;
+    if ((rc = read_dec_err(&err))) return rc;
+    if (status_out) *status_out = err;
+    return DC_OK;
+}
+
 int dc_decode_finish(void) {
     int rc = ensure_init();
     if (rc) return rc;
     unsigned err = 0;
     rc = read_dec_err(&err);
     if (rc) return rc;
+    const int queued = G.dec_queued;
+    G.dec_queued = 0;
     G.shard_deferred = 0;
+    if (err && queued > 1 && !G.dec_shard) {
+        /* the status words are OR-ed over every decode since the last finish: only the last one's
+         * arguments are kept, so an earlier decode that left the fast path cannot be completed */
+        G.dec_pending = 0;
+        HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
+        return seterr(DC_ERR_STREAM, "decoder status 0x%x over %d queued decodes: an earlier decode left the fast "
+                                     "path and was not completed (call dc_decode_finish after each decode)", err, queued);
+    }
     if (G.dec_shard == 1 && (err & (256u | 32u))) {  /* shard prefixes waiting for their incoming values */
         G.shard_deferred = (err & 32u) ? 2 : 1;
         err &= ~(256u | 32u);
@@ -516,7 +582,7 @@ int dc_decode_finish(void) {
         /* outside the fast path's assumptions: exact multi-kernel path (closure rounds, then
          * complete entry maps for every chunk if an entry is still unresolved) */
         HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
-        if (++G.dec_epoch >= (1u << 22)) G.dec_epoch = 1;
+        if ((rc = dec_next_epoch())) return rc;
         if (dc_launch_decode(G.dec_s, NULL, G.dec_nbits, G.dec_max_chunks, &G.dec_P, &G.D, G.dec_out, G.dec_num,
                              G.dec_epoch, DEC_ROUNDS, DEC_FIX_ITERS, G.st))
             return seterr(DC_ERR_HIP, "decode launch failed");
@@ -524,7 +590,7 @@ int dc_decode_finish(void) {
         if (rc) return rc;
         if ((err & 8u) && !(err & 16u)) {
             HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
-            if (++G.dec_epoch >= (1u << 22)) G.dec_epoch = 1;
+            if ((rc = dec_next_epoch())) return rc;
             if (dc_launch_decode_more(G.dec_s, G.dec_max_chunks, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.dec_epoch,
                                       DEC_FIX_ITERS, G.st))
                 return seterr(DC_ERR_HIP, "decode launch failed");
@@ -640,7 +706,7 @@ int dc_halo_encode_device(int ct, const void* d_p, int mi, int mj, int mk, int i
     }
     if (type_out) *type_out = type;
     if (mask17_out) *mask17_out = mask17;
-    return dc_encode_device(ct, G.halo_b, n, 0, type, mask17, 0, d_stream, d_bits);
+    return encode_lib(ct, G.halo_b, n, 0, type, mask17, 0, d_stream, d_bits);
 }
 
 int dc_halo_decode_device(int ct, const void* d_stream, long long nbytes, const unsigned long long* d_bits, int type,
@@ -690,6 +756,32 @@ int dc_med_device(const void* d_x, long long n, float* mean_out, int* type_out) 
     if (mean_out) *mean_out = m;
     if (type_out) *type_out = t;
     return DC_OK;
+}
+
+/* multi-GPU med_dataset_float: the exact running float sum of x[0..n) continued from s_init (the sum
+ * the previous shards ended with) and the max of x; synchronous */
+int dc_med_sum_device(const void* d_x, long long n, float s_init, float* sum_out, float* max_out) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (n <= 0) return seterr(DC_ERR_ARG, "empty input");
+    if (dc_launch_med_sum((const float*)d_x, n, s_init, &G.d_f[2], &G.d_f[3], &G.d_f[1], &G.d_i[0], G.st))
+        return seterr(DC_ERR_HIP, "med launch failed");
+    float h[2];
+    HIPCHK(hipMemcpyAsync(h, &G.d_f[2], 8, hipMemcpyDeviceToHost, G.st));
+    HIPCHK(hipStreamSynchronize(G.st));
+    if (sum_out) *sum_out = h[0];
+    if (max_out) *max_out = h[1];
+    return DC_OK;
+}
+
+/* type of med_dataset_float from a (global) max (impl/dataCompression.c:3605-3614) */
+int dc_type_from_max(float mx) {
+    int add = 0;
+    for (int i = 7; i > 0; i--) {
+        add += 1 << i;
+        if ((double)mx < ldexp(1.0, add - 127)) return 8 - i;
+    }
+    return 0;
 }
 
 int dc_flip_bits_device(void* d_s, unsigned long long nbits, long long count, unsigned long long seed) {
@@ -743,6 +835,7 @@ static uint32_t mask_from_chars(const char* mask) {
 }
 
 static void abi_fail(const char* fn, int rc) {
+    G.abi_rc = rc;
     fprintf(stderr, "libdcamd: %s failed (%d): %s\n", fn, rc, G.msg);
 }
 
@@ -750,6 +843,7 @@ static void abi_fail(const char* fn, int rc) {
 static int abi_compress(const char* fn, int ct, const float* data, int num, unsigned char** data_bits, int* bytes,
                         int* pos, int type, uint32_t mask17) {
     int rc = ensure_init();
+    G.abi_rc = DC_OK;
     if (rc) { abi_fail(fn, rc); return rc; }
     if (num <= 0) return DC_OK;
     const long long used = (long long)(*bytes) * 8 - (*pos == 8 ? 0 : *pos);
@@ -762,7 +856,7 @@ static int abi_compress(const char* fn, int ct, const float* data, int num, unsi
         rc = seterr(DC_ERR_HIP, "H2D copy failed"); abi_fail(fn, rc); return rc;
     }
     unsigned long long tb = 0;
-    if ((rc = dc_encode_device(ct, G.d_a, num, 0, type, mask17, sb, G.d_b, NULL)) || (rc = dc_encode_result(&tb))) {
+    if ((rc = encode_lib(ct, G.d_a, num, 0, type, mask17, sb, G.d_b, NULL)) || (rc = dc_encode_result(&tb))) {
         abi_fail(fn, rc); return rc;
     }
     const long long nb_new = (long long)((tb + 7) >> 3);
@@ -783,21 +877,26 @@ static int abi_compress(const char* fn, int ct, const float* data, int num, unsi
 
 static float* abi_decompress(const char* fn, int ct, const unsigned char* data_bits, int bytes, int num, int type,
                              uint32_t mask17) {
-    float* out = (float*)malloc(sizeof(float) * (size_t)(num > 0 ? num : 1));
+    /* on an error the result is all zeros (never stale device data) and dc_abi_status() reports it */
+    const size_t osz = sizeof(float) * (size_t)(num > 0 ? num : 1);
+    float* out = (float*)malloc(osz);
     int rc = ensure_init();
-    if (rc) { abi_fail(fn, rc); return out; }
-    if (num <= 0 || bytes <= 0) return out;
+    G.abi_rc = DC_OK;
+    if (rc) { abi_fail(fn, rc); if (out) memset(out, 0, osz); return out; }
+    if (!out) { abi_fail(fn, seterr(DC_ERR_ARG, "malloc of %zu bytes failed", osz)); return out; }
+    if (num <= 0 || bytes <= 0) { memset(out, 0, osz); return out; }
     if ((rc = grow(&G.d_a, &G.d_a_cap, (size_t)bytes + 64)) || (rc = grow(&G.d_b, &G.d_b_cap, (size_t)num * 4 + 64))) {
-        abi_fail(fn, rc); return out;
+        abi_fail(fn, rc); memset(out, 0, osz); return out;
     }
     if (hipMemcpyAsync(G.d_a, data_bits, (size_t)bytes, hipMemcpyHostToDevice, G.st) != hipSuccess) {
-        abi_fail(fn, seterr(DC_ERR_HIP, "H2D copy failed")); return out;
+        abi_fail(fn, seterr(DC_ERR_HIP, "H2D copy failed")); memset(out, 0, osz); return out;
     }
     if ((rc = dc_decode_device(ct, G.d_a, bytes, NULL, bytes, num, type, mask17, G.d_b)) || (rc = dc_decode_finish())) {
-        abi_fail(fn, rc);
+        abi_fail(fn, rc); memset(out, 0, osz); return out;
     }
-    if (hipMemcpy(out, G.d_b, (size_t)num * 4, hipMemcpyDeviceToHost) != hipSuccess)
-        abi_fail(fn, seterr(DC_ERR_HIP, "D2H copy failed"));
+    if (hipMemcpy(out, G.d_b, (size_t)num * 4, hipMemcpyDeviceToHost) != hipSuccess) {
+        abi_fail(fn, seterr(DC_ERR_HIP, "D2H copy failed")); memset(out, 0, osz);
+    }
     return out;
 }
 

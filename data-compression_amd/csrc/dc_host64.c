@@ -13,6 +13,7 @@
 #include "../../include/dc_gpu.h"
 
 int dc_set_error(int code, const char* msg);
+void dc_abi_set_status(int rc);
 
 /* device staging buffers of this file */
 static void* g_a; static size_t g_a_cap;
@@ -27,7 +28,10 @@ static int grow(void** p, size_t* cap, size_t need) {
     return DC_OK;
 }
 
-static void fail(const char* fn, int rc) { fprintf(stderr, "libdcamd: %s failed (%d): %s\n", fn, rc, dc_last_error()); }
+static void fail(const char* fn, int rc) {
+    dc_abi_set_status(rc);
+    fprintf(stderr, "libdcamd: %s failed (%d): %s\n", fn, rc, dc_last_error());
+}
 
 static uint32_t mask20_from_chars(const char* mask) {
     uint32_t m = 0;
@@ -38,6 +42,7 @@ static uint32_t mask20_from_chars(const char* mask) {
 static int compress64(const char* fn, int ct, const double* data, int num, unsigned char** data_bits, int* bytes,
                       int* pos, int type, uint32_t mask20) {
     int rc = dc_init(0);
+    dc_abi_set_status(DC_OK);
     if (rc) { fail(fn, rc); return rc; }
     if (num <= 0) return DC_OK;
     const long long used = (long long)(*bytes) * 8 - (*pos == 8 ? 0 : *pos);
@@ -68,8 +73,13 @@ static int compress64(const char* fn, int ct, const double* data, int num, unsig
 
 static double* decompress64(const char* fn, int ct, const unsigned char* data_bits, int bytes, int num, int type,
                             uint32_t mask20) {
-    double* out = (double*)malloc(sizeof(double) * (size_t)(num > 0 ? num : 1));
+    /* on an error the result is all zeros and dc_abi_status() reports it */
+    const size_t osz = sizeof(double) * (size_t)(num > 0 ? num : 1);
+    double* out = (double*)malloc(osz);
     int rc = dc_init(0);
+    dc_abi_set_status(DC_OK);
+    if (!out) { fail(fn, DC_ERR_ARG); return out; }
+    memset(out, 0, osz);
     if (rc) { fail(fn, rc); return out; }
     if (num <= 0 || bytes <= 0) return out;
     const hipStream_t st = (hipStream_t)dc_get_stream();
@@ -77,9 +87,10 @@ static double* decompress64(const char* fn, int ct, const unsigned char* data_bi
         fail(fn, rc); return out;
     }
     if (hipMemcpyAsync(g_a, data_bits, (size_t)bytes, hipMemcpyHostToDevice, st) != hipSuccess) { fail(fn, DC_ERR_HIP); return out; }
-    if ((rc = dc64_decode_device(ct, g_a, bytes, NULL, bytes, num, type, mask20, g_b)) || (rc = dc64_decode_finish()))
-        fail(fn, rc);
-    if (hipMemcpy(out, g_b, (size_t)num * 8, hipMemcpyDeviceToHost) != hipSuccess) fail(fn, DC_ERR_HIP);
+    if ((rc = dc64_decode_device(ct, g_a, bytes, NULL, bytes, num, type, mask20, g_b)) || (rc = dc64_decode_finish())) {
+        fail(fn, rc); return out;
+    }
+    if (hipMemcpy(out, g_b, (size_t)num * 8, hipMemcpyDeviceToHost) != hipSuccess) { fail(fn, DC_ERR_HIP); memset(out, 0, osz); }
     return out;
 }
 

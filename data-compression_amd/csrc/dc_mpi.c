@@ -14,7 +14,7 @@
  * Differences from the double originals: the receiver stages the message in its own buffer instead
  * of receiving into `buf` (a stream larger than count floats cannot overflow it), and the sender frees
  * its temporaries.  Return value: the MPI_Send / MPI_Recv result, or MPI_ERR_OTHER when the codec
- * reports an error (dc_last_error()).
+ * reports an error (dc_abi_status() after the ABI call; dc_last_error() explains).
  */
 #include <mpi.h>
 #include <stdint.h>
@@ -46,7 +46,7 @@ static int send_ct(int ct, const float* buf, int count, int dest, int tag, MPI_C
         myCompress_bitwise_mask(small, count, &bits, &bytes, &pos, type, mask);
     }
     free(small);
-    if (count > 0 && !bits) return MPI_ERR_OTHER;
+    if ((count > 0 && !bits) || dc_abi_status() != DC_OK) { free(bits); return MPI_ERR_OTHER; }
     const int hdr = ct == 7 ? MHDR : HDR;
     unsigned char* msg = (unsigned char*)malloc((size_t)hdr + (size_t)bytes);
     if (!msg) { free(bits); return MPI_ERR_OTHER; }
@@ -94,6 +94,7 @@ static int recv_ct(int ct, float* buf, int count, int source, int tag, MPI_Comm 
     else dec = myDecompress_bitwise_mask(bits, bytes, count, type, mask);
     free(msg);
     if (!dec) return MPI_ERR_OTHER;
+    if (dc_abi_status() != DC_OK) { free(dec); return MPI_ERR_OTHER; }
     for (int i = 0; i < count; i++) buf[i] = dec[i] + mn;   /* impl/dataCompression.c:245-248 (double) */
     free(dec);
     return ret;

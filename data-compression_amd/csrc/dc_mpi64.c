@@ -26,6 +26,7 @@
 #include <time.h>
 
 #include "../../include/dataCompression.h"
+#include "../../include/dc_gpu.h"
 #include "../../include/dc_mpi.h"
 
 enum { HDR64 = (int)(sizeof(int) + sizeof(double)) };
@@ -44,7 +45,7 @@ static int compress_ct(int ct, const double* x, int n, unsigned char** bits, int
     else if (ct == 6) myCompress_bitwise_double_np(small, n, bits, bytes, &pos);
     else myCompress_bitwise_double_op(small, n, bits, bytes, &pos);
     free(small);
-    return (n > 0 && !*bits) ? -1 : 0;
+    return ((n > 0 && !*bits) || dc_abi_status() != DC_OK) ? -1 : 0;
 }
 
 static double* decompress_ct(int ct, unsigned char* bits, int bytes, int n) {
@@ -89,6 +90,7 @@ static int recv64(int ct, double* buf, int len, int source, int tag, MPI_Comm co
     double* dec = decompress_ct(ct, msg + HDR64, bytes, len);
     free(msg);
     if (!dec) return MPI_ERR_OTHER;
+    if (dc_abi_status() != DC_OK) { free(dec); return MPI_ERR_OTHER; }
     for (int i = 0; i < len; i++) buf[i] = dec[i] + mn;   /* :245-248 */
     free(dec);
     return ret;

@@ -43,6 +43,7 @@ EXT_SYMBOLS = [
     "dc_halo_encode_device", "dc_halo_decode_device",
     "dc64_stream_capacity", "dc64_encode_device", "dc64_encode_result", "dc64_decode_device", "dc64_decode_finish",
     "dc64_last_decode_flags", "dc64_to_small_device", "dc64_med_device", "dc_set_encode_stream",
+    "dc_decode_status", "dc_abi_status", "dc_med_sum_device", "dc_type_from_max",
 ]
 
 
@@ -79,6 +80,9 @@ class Lib:
         L.dc_decode_shard_fix.argtypes = [vp]
         L.dc_to_small_device.argtypes = [vp, ll, vp, C.POINTER(C.c_float)]
         L.dc_med_device.argtypes = [vp, ll, C.POINTER(C.c_float), C.POINTER(C.c_int)]
+        L.dc_med_sum_device.argtypes = [vp, ll, C.c_float, C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.dc_type_from_max.argtypes = [C.c_float]
+        L.dc_decode_status.argtypes = [C.POINTER(C.c_uint)]
         L.dc_crc32_device.argtypes = [vp, ll, C.POINTER(C.c_uint32)]
         L.dc_decode_chunk_bits_value.restype = ll
         pp = [_f32p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int), C.POINTER(C.c_int)]
@@ -385,6 +389,25 @@ class Lib:
     def decode_finish(self):
         self.check(self.L.dc_decode_finish(), "dc_decode_finish")
 
+    def decode_status(self):
+        """Fast-path status word OR-ed over every decode since the last finish (0: all on the fast path)."""
+        v = C.c_uint(0)
+        self.check(self.L.dc_decode_status(C.byref(v)), "dc_decode_status")
+        return v.value
+
+    def abi_status(self):
+        return int(self.L.dc_abi_status())
+
+    def med_sum_device(self, x_ptr, n, s_init=0.0):
+        """Exact running float sum of med_dataset_float continued from s_init, and the max (multi-GPU mean)."""
+        sm, mx = C.c_float(0), C.c_float(0)
+        self.check(self.L.dc_med_sum_device(C.c_void_p(x_ptr), n, C.c_float(s_init), C.byref(sm), C.byref(mx)),
+                   "dc_med_sum_device")
+        return np.float32(sm.value), np.float32(mx.value)
+
+    def type_from_max(self, mx):
+        return int(self.L.dc_type_from_max(C.c_float(float(mx))))
+
     def synchronize(self):
         self.check(self.L.dc_synchronize(), "dc_synchronize")
 
@@ -442,6 +465,9 @@ def gather_stream(local, start_bit, local_bits, group=None):
     import torch.distributed as dist
     world = dist.get_world_size(group)
     dev = local.device
+    if dev.type == "cuda" and dist.get_backend(group) == "gloo":    # gloo collectives on host copies
+        out, total = gather_stream(local.cpu(), start_bit, local_bits, group)
+        return out.to(dev), total
     meta = torch.tensor([int(local_bits) - int(start_bit), int(start_bit)], dtype=torch.int64, device=dev)
     metas = [torch.zeros_like(meta) for _ in range(world)]
     dist.all_gather(metas, meta, group=group)
@@ -459,6 +485,37 @@ def gather_stream(local, start_bit, local_bits, group=None):
         if nb:
             out[b0:b0 + nb] |= parts[g][:nb]
     return out, total
+
+
+def _bcast_scalar(v, src, dev, group=None, dtype=None):
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=dtype or torch.float32, device=dev)
+    dist.broadcast(t, src, group=group)
+    return t.cpu().numpy()[0]
+
+
+def global_med(L, xs_ptr, n, dev, group=None):
+    """med_dataset_float of the global array whose contiguous shard of n floats this rank holds (all
+    shards the same size): the exact left-to-right float sum is continued shard by shard (rank r starts
+    from the sum rank r-1 ended with, one broadcast per rank), the max is all-reduced.  Returns the
+    mean and type every rank agrees on -- those of the single-GPU med_dataset_float of the whole array."""
+    import numpy as _np
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    s = _np.float32(0.0)
+    mx = _np.float32(0.0)
+    for r in range(world):
+        if rank == r:
+            s, mx = L.med_sum_device(xs_ptr, n, s)
+        s = _np.float32(_bcast_scalar(float(s), r, dev, group))
+    m = torch.tensor([float(mx)], dtype=torch.float32, device=dev)
+    dist.all_reduce(m, op=dist.ReduceOp.MAX, group=group)
+    gmax = _np.float32(m.cpu().numpy()[0])
+    mean = _np.float32(s / _np.float32(world * n))
+    return mean, L.type_from_max(gmax)
 
 
 def exchange_history(last3, group=None):

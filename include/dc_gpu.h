@@ -31,7 +31,11 @@ int dc_init(int device);                       /* optional; first call of any en
 const char* dc_last_error(void);
 void* dc_get_stream(void);                     /* hipStream_t all library work is ordered on */
 int dc_synchronize(void);
-int dc_set_encode_stream(void* stream);        /* encoder launches on this hipStream_t (NULL: dc_get_stream()) */
+/* Encoder launches of dc_encode_device go to this hipStream_t (NULL: dc_get_stream()); each such encode
+ * first waits for the work already queued on dc_get_stream().  The caller orders a later decode of the
+ * stream (on dc_get_stream()) after the encode with its own event.  Internal callers (the host ABI, the
+ * halo path, the MPI wrappers) always encode on dc_get_stream(). */
+int dc_set_encode_stream(void* stream);
 void dc_set_abs_error_bound(double bound);     /* runtime absErrorBound (default: header macro) */
 double dc_get_abs_error_bound(void);
 
@@ -59,8 +63,16 @@ int dc_encode_result(unsigned long long* total_bits);
 int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsigned long long* d_nbits,
                      long long max_bytes, long long num, int type, uint32_t mask17, void* d_out);
 /* Wait, check the decoder's status words and complete rare slow paths (extra closure rounds,
- * serial prediction chains).  Returns DC_OK or DC_ERR_STREAM. */
+ * serial prediction chains) of the LAST decode.  Returns DC_OK or DC_ERR_STREAM.  Several decodes may
+ * be queued before one finish; if any of them left the fast path the status words say so, only the last
+ * one can be completed, and finish returns DC_ERR_STREAM ("an earlier decode was not completed"). */
 int dc_decode_finish(void);
+/* Wait and return the fast path's status word OR-ed over every decode since the last finish, without
+ * running any slow path (0: every queued decode completed on the fast path).  For benchmarks. */
+int dc_decode_status(unsigned* status_out);
+/* Status of the last reference-ABI call (myCompress_* / myDecompress_* / the MPI wrappers): DC_OK or
+ * the DC_ERR_* code it failed with (the ABI signatures have no error return). */
+int dc_abi_status(void);
 
 /* Shards of one global stream (multi-GPU decode): decode num values from the
  * tokens at bits [start_bit, start_bit + nbits) of d_stream (stream_bytes long; start_bit must be a
@@ -88,6 +100,11 @@ int dc_halo_decode_device(int ct, const void* d_stream, long long nbytes, const 
 /* Pre-passes on device data: toSmallDataset_float and med_dataset_float (exact). */
 int dc_to_small_device(const void* d_x, long long n, void* d_out, float* min_out);
 int dc_med_device(const void* d_x, long long n, float* mean_out, int* type_out);
+/* Multi-GPU med_dataset_float over contiguous shards: the exact left-to-right float sum of x[0..n)
+ * continued from s_init (0 on the first shard, else the sum the previous shard returned) and the max of
+ * x; the global mean is sum / (float)n_total and the type dc_type_from_max(global max).  Synchronous. */
+int dc_med_sum_device(const void* d_x, long long n, float s_init, float* sum_out, float* max_out);
+int dc_type_from_max(float mx);
 /* zlib-compatible CRC-32 of a device byte range. */
 int dc_crc32_device(const void* d_s, long long nbytes, uint32_t* crc_out);
 /* The same, asynchronous on the library stream, result to device memory d_crc (one uint32). */
