@@ -126,6 +126,43 @@ DC_PAIR64(, 5)
 DC_PAIR64(_np, 6)
 DC_PAIR64(_op, 11)
 
+/* MPI_Bcast_bitwise_double (:165-224): one broadcast of count*8+12 bytes, framing [int bytes][double min]
+ * [stream] (the stream never exceeds count*8 bytes: a CT5 token is at most 64 bits) */
+int MPI_Bcast_bitwise_double(void* buf, int count, MPI_Datatype datatype, int root, MPI_Comm comm) {
+    (void)datatype;
+    int myrank = 0;
+    MPI_Comm_rank(comm, &myrank);
+    const size_t tot = (size_t)HDR64 + (size_t)(count > 0 ? count : 0) * sizeof(double);
+    unsigned char* aux = (unsigned char*)calloc(tot > 0 ? tot : 1, 1);
+    if (!aux) return MPI_ERR_OTHER;
+    int fail = 0;
+    if (myrank == root) {
+        unsigned char* bits = NULL;
+        int bytes = 0;
+        double mn = 0;
+        fail = compress_ct(5, (const double*)buf, count, &bits, &bytes, &mn) || (size_t)HDR64 + (size_t)bytes > tot;
+        if (!fail) {
+            memcpy(aux, &bytes, sizeof(int));
+            memcpy(aux + sizeof(int), &mn, sizeof(double));
+            if (bytes) memcpy(aux + HDR64, bits, (size_t)bytes);
+        }
+        free(bits);
+    }
+    int ret = MPI_Bcast(aux, (int)tot, MPI_UNSIGNED_CHAR, root, comm);
+    if (ret == MPI_SUCCESS && myrank != root) {
+        int bytes = 0;
+        double mn = 0;
+        memcpy(&bytes, aux, sizeof(int));
+        memcpy(&mn, aux + sizeof(int), sizeof(double));
+        double* dec = (bytes >= 0 && (size_t)HDR64 + (size_t)bytes <= tot) ? decompress_ct(5, aux + HDR64, bytes, count) : NULL;
+        if (!dec || dc_abi_status() != DC_OK) ret = MPI_ERR_OTHER;
+        else for (int i = 0; i < count; i++) ((double*)buf)[i] = dec[i] + mn;   /* :213-216 */
+        free(dec);
+    }
+    free(aux);
+    return fail ? MPI_ERR_OTHER : ret;
+}
+
 /* ---- broadcasts with CRC-32 / Hamming (:800-1197) */
 enum { BC_CRC = 0, BC_MASK = 1, BC_HAM = 2 };
 

@@ -189,6 +189,61 @@ void bit_set(unsigned char* p_data, unsigned char position, int flag);
 float* transform_3d_array_to_1d_array(float data[MIMAX][MJMAX][MKMAX], int ijk, int v, int imax, int jmax, int kmax);
 float* dc_transform_3d_array_to_1d_array(const float* data, int mi, int mj, int mk, int ijk, int v, int imax,
                                          int jmax, int kmax);
+/* ---- single-token helpers the serial codecs are built from (host, dc_host_token.c) ---------------
+ * compress_*: append one element's raw (or CT7 masked) token to the caller's stream (add_bit_to_bytes
+ * semantics); decompress_*: value of one token given as a '0'/'1' string of bits_num chars, with the
+ * caller's history for the 3-bit codes.  The caller's string is never realloc()ed. */
+/* h:93  c:3479-3520 */
+void compress_bitwise_float(float real_value, unsigned char** data_bits, int* bytes, int* pos);
+/* h:69  c:2143-2284 */
+void compress_bitwise_float_mask(float real_value, unsigned char** data_bits, int* bytes, int* pos, int type,
+                                 char mask[1 + 8 + 8]);
+/* h:87  c:3137-3186 */
+float decompress_bitwise_float(char* bits, int bits_num, float before_value1, float before_value2, float before_value3);
+/* h:75  c:2611-2630 */
+float decompress_bitwise_float_np(char* bits, int bits_num);
+/* h:68  c:1900-2027 */
+float decompress_bitwise_float_mask(char* bits, int bits_num, float before_value1, float before_value2,
+                                    float before_value3, int type, char mask[1 + 8 + 8]);
+/* h:92  c:3446-3477 */
+void compress_bitwise_double(double real_value, unsigned char** data_bits, int* bytes, int* pos);
+/* h:65  c:1493-1588 */
+void compress_bitwise_double_mask(double real_value, unsigned char** data_bits, int* bytes, int* pos, int type,
+                                  char mask[1 + 11 + 8]);
+/* h:85  c:2871-2920 */
+double decompress_bitwise_double(char* bits, int bits_num, double before_value1, double before_value2,
+                                 double before_value3);
+/* h:73  c:2438-2457 */
+double decompress_bitwise_double_np(char* bits, int bits_num);
+/* h:64  c:1396-1491 */
+double decompress_bitwise_double_mask(char* bits, int bits_num, double before_value1, double before_value2,
+                                      double before_value3, int type, char mask[1 + 11 + 8]);
+/* h:118 c:5232 */
+void getDoubleBin(double num, char bin[]);
+
+/* ---- character-level Hamming SECDED (k data chars, r check chars + overall parity) ---------------- */
+/* h:147 c:5544 */
+void hamming_code(char* data, char* c, int k, int r);
+/* h:148 c:5595: v[i] = '1' where check bit i disagrees, v[r] the overall parity verdict */
+void hamming_verify(char* data, char* c, int k, int r, char* v);
+/* h:149 c:5631: *error_bit_pos += the syndrome (not initialised, as the reference); 0..3 as hamming_decode */
+int error_info(char* v, int r, int* error_bit_pos);
+/* h:150 c:5656 */
+void hamming_print(char* data, char* c, int k, int r);
+/* h:151 c:5678 */
+void hamming_rectify(char* data, char* c, int k, int r, int error_bit_pos);
+/* h:152 c:5712: 8 '0'/'1' chars per byte, MSB first */
+void cast_bits_to_char(unsigned char* bits, char* data, int bytes);
+/* h:155 c:5781 */
+void hamming_verify_bit(unsigned char* bits, char* c, int bytes, int r, char* v);
+/* h:156 c:5822 */
+void hamming_rectify_bit(unsigned char* bits, char* c, int bytes, int r, int error_bit_pos);
+
+/* h:132 c:5341 (NULL instead of exit(0) when the file cannot be opened) */
+float* readfrombinary_float(const char* file, int count);
+/* h:133 c:5362 */
+double* readfrombinary_double(const char* file, int count);
+
 /* h:129 c:5290 */
 void writetobinary_float(const char* file, float* data, int count);
 /* h:131 c:5324 */

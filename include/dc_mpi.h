@@ -57,6 +57,9 @@ int MPI_Send_bitwise_double_op_cn(const void* buf, int count, MPI_Datatype datat
 int MPI_Recv_bitwise_double_op_cn(void* buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
                                   MPI_Status* status, int len);
 /* CT8 (CRC-32), CT9 (bitmask + CRC-32), CT10 (CRC-32 + Hamming): broadcast from root, resend on failure */
+/* h:50 c:165-224: root compresses (CT5), every rank receives [int bytes][double min][stream] padded to
+ * count*8+12 bytes by one MPI_Bcast, non-roots decode and add min back into buf */
+int MPI_Bcast_bitwise_double(void* buf, int count, MPI_Datatype datatype, int root, MPI_Comm comm);
 void MPI_Bcast_bitwise_crc(double* buffer, int count, int root, int rank, int procs, float* compress_ratio,
                            double* gosa, int* resend);
 void MPI_Bcast_bitwise_mask_crc(double* buffer, int count, int root, int rank, int procs, float* compress_ratio,

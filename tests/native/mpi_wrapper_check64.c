@@ -102,6 +102,20 @@ int main(int argc, char** argv) {
             }
         }
     }
+    /* MPI_Bcast_bitwise_double (:165-224): CT5 from root 0 */
+    memcpy(y, x, sizeof(double) * (size_t)n);
+    if (rank != 0) memset(y, 0, sizeof(double) * (size_t)n);
+    {
+        const int rc = MPI_Bcast_bitwise_double(y, n, MPI_DOUBLE, 0, MPI_COMM_WORLD);
+        if (rank == 1) {
+            double* want = local_round_trip(5, x, n);
+            fails += (rc != MPI_SUCCESS) | report("bcast_double", 5, n, want, y, n);
+            free(want);
+        } else if (rank == 0 && (rc != MPI_SUCCESS || memcmp(x, y, sizeof(double) * (size_t)n) != 0)) {
+            printf("bcast_double root rc=%d (root buffer must stay unchanged)\n", rc);
+            fails++;
+        }
+    }
     /* broadcasts: CT8 (crc), CT9 (mask_crc), CT10 (crc_hamming) */
     for (int mode = 8; mode <= 10; mode++) {
         memcpy(y, x, sizeof(double) * (size_t)n);

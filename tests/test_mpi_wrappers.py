@@ -15,7 +15,7 @@ CHECK = os.path.join(LIB, "mpi_wrapper_check")
 MPIRUN = "/opt/conda/bin/mpirun"
 SYMS = [f"MPI_{d}_bitwise_float{s}" for d in ("Send", "Recv") for s in ("", "_np", "_op", "_mask")]
 SYMS += [f"MPI_{d}_bitwise_double{s}{c}" for d in ("Send", "Recv") for s in ("", "_np", "_op") for c in ("", "_cn")]
-SYMS += ["MPI_Bcast_bitwise_crc", "MPI_Bcast_bitwise_mask_crc", "MPI_Bcast_bitwise_crc_hamming"]
+SYMS += ["MPI_Bcast_bitwise_double", "MPI_Bcast_bitwise_crc", "MPI_Bcast_bitwise_mask_crc", "MPI_Bcast_bitwise_crc_hamming"]
 CHECK64 = os.path.join(LIB, "mpi_wrapper_check64")
 
 
@@ -46,9 +46,9 @@ def test_mpi_wrappers_round_trip(n):
 @pytest.mark.parametrize("n,ber", [(1 << 20, "0"), (1 << 20, "1e-6"), (4099, "0")])
 def test_mpi_double_wrappers(n, ber):
     """The reference's double wrappers (dc_mpi64.c): send/recv (+ _cn) equal the local round trip bit for
-    bit; the CRC / Hamming broadcasts deliver the clean decode to rank 1 -- with DC_BER=1e-6 through
+    bit; MPI_Bcast_bitwise_double and the CRC / Hamming broadcasts deliver the clean decode to rank 1 -- with DC_BER=1e-6 through
     simulated CRC failures and resends (CT8/9) and real bit flips + Hamming correction / resend (CT10)."""
     env = dict(os.environ, DC_ABS_ERROR_BOUND="0.001", HSA_ENABLE_IPC_MODE_LEGACY="0", DC_BER=ber)
     r = subprocess.run([MPIRUN, "-np", "2", CHECK64, str(n)], capture_output=True, text=True, timeout=200, env=env)
     ok = re.findall(r"MPI_WRAPPER64 (\w+) ct=(\d+) n=\d+ OK", r.stdout)
-    assert r.returncode == 0 and len(ok) == 9, r.stdout[-2000:] + r.stderr[-2000:]
+    assert r.returncode == 0 and len(ok) == 10, r.stdout[-2000:] + r.stderr[-2000:]
