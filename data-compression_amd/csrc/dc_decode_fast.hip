@@ -682,15 +682,8 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
     const Plan pl = *D.plan;
     const int c = threadIdx.x;
     build_lut<CT>(S.T, P, c, GROUP);                                  // visible after the first barrier
-    // tiles are claimed in increasing order from an atomic counter; the claim of the next tile is issued
-    // when the current one starts, so its round trip overlaps the tile's work instead of separating tiles
-    unsigned nxt = 0;
-    if (c == 0) nxt = atomicAdd(&D.ctr[4], 1u);
     while (true) {
-        if (c == 0) {
-            S.tile = (long long)nxt;
-            if ((long long)nxt < pl.ngroups) nxt = atomicAdd(&D.ctr[4], 1u);
-        }
+        if (c == 0) S.tile = (long long)atomicAdd(&D.ctr[4], 1u);
         __syncthreads();
         const long long t = S.tile;
         if (t >= pl.ngroups) break;
