@@ -122,139 +122,316 @@ __global__ __launch_bounds__(256) void med_kernel(const float* __restrict__ x, l
 
 // ---------------------------------------------------------------- exact parallel mean
 // med_dataset_float (:3593-3620) sums left to right in float.  While the running sum s stays in one
-// binade [2^e, 2^(e+1)) its ulp u is fixed and fl(s + x) = s + u*r(x), with r = x/u rounded to an
-// integer (ties to even on s/u, i.e. on the parity of k = s/u).  So a run of elements is a 2-state
-// transducer: start parity -> (added units, end parity).  One workgroup walks the array in LDS
-// chunks: each thread folds its elements for both start parities, a block scan composes the
-// threads, and the chunk is applied at once unless the sum would leave the binade (or an element is
-// negative / not finite / too large), in which case lane 0 adds the elements around that point one
-// at a time, exactly like the reference.  Below 2^20 the sum is always added one element at a time.
-constexpr int MX_CH = 8192;                                // floats staged per chunk
-constexpr int MX_T = 1024;
+// binade [2^(E-127), 2^(E-126)) its ulp u = 2^(E-150) is fixed and fl(s + x) = s + u*r(x), with r =
+// x/u rounded to an integer (ties to even on s/u, i.e. on the parity of k = s/u), as long as the sum
+// stays below the binade's top (k < 2^24) and 0 <= x < 2^(E-126).  So a chunk of MC elements is a
+// 2-state transducer for a given binade: start parity -> (units added, end parity).
+//   med_chunk_sum   : per chunk its double sum and max (all CUs)
+//   med_chunk_scan  : one workgroup: exclusive scan of the double chunk sums = an estimate of the
+//                     running sum at every chunk, whose binade E_est picks the chunk's window of
+//                     MW candidate binades [E_est - 4, E_est + 1] (the float sum stalls below the real
+//                     one, never far above it)
+//   med_chunk_trans : per chunk and candidate binade the transducer (all CUs; one pass over x)
+//   med_compose     : one workgroup: from s_init, blocks of 1024 chunks are composed with a block scan
+//                     while the running sum stays in its binade and each chunk has a valid transducer
+//                     for it; a chunk where the sum leaves the binade, or that holds an element the
+//                     transducer cannot take (negative, NaN, too large, the binade not in its window),
+//                     or a sum below SMIN, is added element by element by one lane, exactly like the
+//                     reference.  At 2^26 U10: about 25 such chunks (the binade crossings).
+constexpr int MC = 2048;                                   // elements per chunk
+constexpr int MW = 6;                                      // candidate binades per chunk
+constexpr int MC_T = 256;                                  // threads of the chunk kernels (8 elements each)
+constexpr int MC_PER = MC / MC_T;
+constexpr int MX_T = 1024;                                 // compose workgroup
+#define MED_SMIN 7.8886091e-31f                            // 2^-100: below it 1/u would overflow float
 
-// s_init: the running sum before x[0] (0 for the whole array; a multi-GPU shard continues its
-// predecessor's sum); out_sum / out_max (optional) receive the raw sum and max.
-__global__ __launch_bounds__(MX_T) void med_exact_kernel(const float* __restrict__ x, long long n, float s_init,
-                                                         float* __restrict__ out_mean, int* __restrict__ out_type,
-                                                         float* __restrict__ out_sum, float* __restrict__ out_max) {
-    __shared__ float buf[MX_CH];
-    __shared__ int fd[2][2][MX_T];                          // [buffer][start parity] units added
-    __shared__ unsigned char fe[2][2][MX_T];                // [buffer][start parity] end parity
-    __shared__ int fbad[2][MX_T];                           // first thread (inclusive scan of "cannot")
+struct MedScratch {
+    double* csum;                                          // [nch] chunk sums, then their exclusive scan
+    float* cmax;                                           // [nch] chunk max (NaN-skipping)
+    int* elo;                                              // [nch] first candidate binade
+    int2* T;                                               // [nch * MW] units added from parity 0 / 1
+    uint8_t* F;                                            // [nch * MW] end parity 0 | end parity 1 << 1 | bad << 2
+    uint8_t* Z;                                            // [nch] 1: every element is +0 / -0
+};
+
+extern "C" long long dc_med_scratch_bytes(long long n) {
+    const long long nch = (n + MC - 1) / MC;
+    return nch * (8 + 4 + 4 + MW * 8 + MW + 1) + 4 * 256;
+}
+
+__host__ __device__ inline MedScratch med_scratch(void* base, long long nch) {
+    MedScratch m;
+    char* b = (char*)base;
+    m.csum = (double*)b; b += nch * 8;
+    m.T = (int2*)b; b += nch * MW * 8;
+    m.cmax = (float*)b; b += nch * 4;
+    m.elo = (int*)b; b += nch * 4;
+    m.F = (uint8_t*)b; b += nch * MW;
+    m.Z = (uint8_t*)b;
+    return m;
+}
+
+__device__ __forceinline__ void load_chunk(const float* __restrict__ x, long long n, long long c, float* v) {
+    const long long e0 = c * MC + (long long)threadIdx.x * MC_PER;
+    if (e0 + MC_PER <= n && ((reinterpret_cast<uintptr_t>(x) & 15u) == 0)) {
+        const float4* p = reinterpret_cast<const float4*>(x + e0);
+        const float4 a = p[0], b = p[1];
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < MC_PER; i++) v[i] = e0 + i < n ? x[e0 + i] : 0.0f;
+    }
+}
+
+__global__ __launch_bounds__(MC_T) void med_chunk_sum_kernel(const float* __restrict__ x, long long n, MedScratch M) {
+    __shared__ double ws[MC_T / 64];
+    __shared__ float wm[MC_T / 64];
+    const long long c = blockIdx.x;
+    float v[MC_PER];
+    load_chunk(x, n, c, v);
+    const long long e0 = c * MC + (long long)threadIdx.x * MC_PER;
+    double sm = 0.0;
+    float mx = -INFINITY;
+    bool nz = false;
+#pragma unroll
+    for (int i = 0; i < MC_PER; i++)
+        if (e0 + i < n) {
+            sm += (double)v[i];
+            mx = v[i] > mx ? v[i] : mx;                          // NaNs never win (as the reference's >)
+            nz |= (__float_as_uint(v[i]) & 0x7FFFFFFFu) != 0u;
+        }
+    const bool anynz = __syncthreads_or(nz);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        sm += __shfl_xor(sm, d, 64);
+        const float o = __shfl_xor(mx, d, 64);
+        mx = o > mx ? o : mx;
+    }
+    if ((threadIdx.x & 63) == 0) { ws[threadIdx.x >> 6] = sm; wm[threadIdx.x >> 6] = mx; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        float m = -INFINITY;
+        for (int w = 0; w < MC_T / 64; w++) { t += ws[w]; m = wm[w] > m ? wm[w] : m; }
+        M.csum[c] = isfinite(t) ? t : 0.0;
+        M.cmax[c] = m;
+        M.Z[c] = anynz ? 0 : 1;
+    }
+}
+
+__global__ __launch_bounds__(1024) void med_chunk_scan_kernel(MedScratch M, long long nch, float s_init) {
+    __shared__ double wt[16];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const long long per = (nch + 1023) / 1024, c0 = tid * per, c1 = min(nch, c0 + per);
+    double sm = 0.0;
+    for (long long c = c0; c < c1; c++) sm += M.csum[c];
+    double inc = sm;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const double u = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += u;
+    }
+    if (lane == 63) wt[wid] = inc;
+    __syncthreads();
+    double run = (double)s_init + inc - sm;
+    for (int w = 0; w < wid; w++) run += wt[w];
+    for (long long c = c0; c < c1; c++) {
+        const float est = (float)fmin(fmax(run, 0.0), 3.0e38);
+        const int E = (int)((__float_as_uint(est) >> 23) & 0xFFu);
+        M.elo[c] = E - 4;
+        run += M.csum[c];
+    }
+}
+
+// transducer of one thread's elements for binade E (k's parity p in, units added / parity out)
+__device__ __forceinline__ void trans_elems(const float* v, int cnt, int E, int& d0, int& d1, int& p0, int& p1, bool& bad) {
+    const float scale = __uint_as_float((uint32_t)(277 - E) << 23);      // 2^(150-E) = 1/u
+    const float lim = __uint_as_float((uint32_t)(E + 1) << 23);          // 2^(E-126), the binade's top
+    d0 = 0; d1 = 0; p0 = 0; p1 = 1; bad = false;
+#pragma unroll
+    for (int i = 0; i < MC_PER; i++) {
+        if (i < cnt) {
+            bad |= !(v[i] >= 0.0f) || !(v[i] < lim);                 // negative, NaN, inf or >= the binade's top
+            const float q = __fmul_rn(v[i], scale);                  // exact: power-of-two scaling
+            const float fq = floorf(q);
+            const float fr = __fsub_rn(q, fq);
+            const int fl = (int)fq;
+            const int up = fr > 0.5f ? 1 : 0, tie = fr == 0.5f ? 1 : 0;
+            const int r0 = fl + up + (tie & ((p0 + fl) & 1));
+            const int r1 = fl + up + (tie & ((p1 + fl) & 1));
+            d0 = min(d0 + r0, 1 << 25); d1 = min(d1 + r1, 1 << 25); // >= 2^24 leaves the binade anyway
+            p0 = (p0 + r0) & 1; p1 = (p1 + r1) & 1;
+        }
+    }
+}
+
+// f then g (f earlier): start parity p -> f's units + g's units from f's end parity
+__device__ __forceinline__ void compose(int& a0, int& a1, int& q0, int& q1, int b0, int b1, int e0, int e1) {
+    // (a, q) = f, (b, e) = g  ->  f then g
+    const int n0 = min(a0 + (q0 ? b1 : b0), 1 << 25), n1 = min(a1 + (q1 ? b1 : b0), 1 << 25);
+    const int m0 = q0 ? e1 : e0, m1 = q1 ? e1 : e0;
+    a0 = n0; a1 = n1; q0 = m0; q1 = m1;
+}
+
+__global__ __launch_bounds__(MC_T) void med_chunk_trans_kernel(const float* __restrict__ x, long long n, MedScratch M) {
+    __shared__ int sd[MW][MC_T / 64][4];
+    const long long c = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    float v[MC_PER];
+    load_chunk(x, n, c, v);
+    const long long e0 = c * MC + (long long)tid * MC_PER;
+    const int cnt = (int)max(0ll, min((long long)MC_PER, n - e0));
+    const int elo = M.elo[c];
+#pragma unroll
+    for (int w = 0; w < MW; w++) {
+        const int E = elo + w;
+        int d0 = 0, d1 = 0, p0 = 0, p1 = 1;
+        bool bad = E < 24 || E > 253;                                 // 1/u or the binade top not a float
+        if (!bad) trans_elems(v, cnt, E, d0, d1, p0, p1, bad);
+        // ordered reduction over the wave: lane i absorbs lane i + d (its successor block)
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int b0 = __shfl_down(d0, d, 64), b1 = __shfl_down(d1, d, 64);
+            const int e0_ = __shfl_down(p0, d, 64), e1_ = __shfl_down(p1, d, 64);
+            const int bb = __shfl_down((int)bad, d, 64);
+            if ((lane & (2 * d - 1)) == 0 && lane + d < 64) {
+                compose(d0, d1, p0, p1, b0, b1, e0_, e1_);
+                bad |= bb != 0;
+            }
+        }
+        if (lane == 0) { sd[w][wid][0] = d0; sd[w][wid][1] = d1; sd[w][wid][2] = p0 | (p1 << 1); sd[w][wid][3] = bad; }
+    }
+    __syncthreads();
+    if (tid < MW) {
+        const int w = tid;
+        int a0 = sd[w][0][0], a1 = sd[w][0][1], q0 = sd[w][0][2] & 1, q1 = sd[w][0][2] >> 1;
+        bool bad = sd[w][0][3] != 0;
+        for (int k = 1; k < MC_T / 64; k++) {
+            compose(a0, a1, q0, q1, sd[w][k][0], sd[w][k][1], sd[w][k][2] & 1, sd[w][k][2] >> 1);
+            bad |= sd[w][k][3] != 0;
+        }
+        M.T[c * MW + w] = make_int2(a0, a1);
+        M.F[c * MW + w] = (uint8_t)(q0 | (q1 << 1) | (bad ? 4 : 0));
+    }
+}
+
+__global__ __launch_bounds__(MX_T) void med_compose_kernel(const float* __restrict__ x, long long n, float s_init,
+                                                           MedScratch M, float* __restrict__ out_mean,
+                                                           int* __restrict__ out_type, float* __restrict__ out_sum,
+                                                           float* __restrict__ out_max) {
+    __shared__ float buf[MC];
+    __shared__ int sa[2][2][MX_T];                          // [buffer][start parity] units
+    __shared__ unsigned char sq[2][2][MX_T];                // [buffer][start parity] end parity
+    __shared__ int sb[2][MX_T];                             // first invalid chunk (inclusive min)
     __shared__ float s_sum;
-    __shared__ int s_start;
+    __shared__ long long s_c;
+    __shared__ int s_first;
     __shared__ float smax[MX_T];
     const int tid = threadIdx.x;
-    float mx = x[0];
-    if (tid == 0) s_sum = s_init;
-    for (long long c0 = 0; c0 < n; c0 += MX_CH) {
-        const int m = (int)min((long long)MX_CH, n - c0);
-        for (int i = tid; i < m; i += MX_T) { const float v = x[c0 + i]; buf[i] = v; mx = v > mx ? v : mx; }
-        if (tid == 0) s_start = 0;
-        __syncthreads();
-        while (true) {
-            if (s_sum == 0.0f) {                            // fl(0 + 0) = 0: skip a zero run in parallel
-                __shared__ int s_nz;
-                if (tid == 0) s_nz = m;
-                __syncthreads();
-                const int st0 = s_start;
-                for (int i = st0 + tid; i < m; i += MX_T)
-                    if (__float_as_uint(buf[i]) != 0u) { atomicMin(&s_nz, i); break; }
-                __syncthreads();
-                if (tid == 0) s_start = s_nz;
-                __syncthreads();
-            }
-            if (tid == 0) {                                 // small sums: exact serial adds
-                float sv = s_sum;
-                int st = s_start;
-                while (st < m && !(sv >= 1048576.0f && sv < 3.0e38f)) sv = __fadd_rn(sv, buf[st++]);
-                s_sum = sv;
-                s_start = st;
-            }
+    const long long nch = (n + MC - 1) / MC;
+    if (tid == 0) { s_sum = s_init; s_c = 0; }
+    __syncthreads();
+    while (true) {
+        const long long c = s_c;
+        if (c >= nch) break;
+        const float sv = s_sum;
+        if (sv != sv) {                                     // NaN + anything stays NaN
+            if (tid == 0) s_c = nch;
             __syncthreads();
-            const int st = s_start;
-            if (st >= m) break;
-            const float sv = s_sum;
-            const uint32_t sb = __float_as_uint(sv);
-            const int E = (int)((sb >> 23) & 0xFFu);       // s in [2^(E-127), 2^(E-126)), u = 2^(E-150)
-            const int k0 = (int)((sb & 0x7FFFFFu) | 0x800000u);
-            const float scale = __uint_as_float((uint32_t)(277 - E) << 23);   // 2^(150-E) = 1/u
-            const float lim = __uint_as_float((uint32_t)(E + 1) << 23);       // 2^(E-126)
-            // this thread's contiguous share of [st, m)
-            const int len = m - st, per = (len + MX_T - 1) / MX_T;
-            const int b = st + tid * per, e = min(m, b + per);
-            int d0 = 0, d1 = 0, p0 = 0, p1 = 1;
-            bool bad = false;
-            for (int i = b; i < e; i++) {
-                const float v = buf[i];
-                bad |= !(v >= 0.0f) || !(v < lim);          // negative, NaN, inf or >= the binade
-                const float q = __fmul_rn(v, scale);        // exact: power-of-two scaling
-                const float fq = floorf(q);
-                const float fr = __fsub_rn(q, fq);
-                const int fl = (int)fq;
-                const int up = fr > 0.5f ? 1 : 0, tie = fr == 0.5f ? 1 : 0;
-                const int r0 = fl + up + (tie & ((p0 + fl) & 1));
-                const int r1 = fl + up + (tie & ((p1 + fl) & 1));
-                d0 += r0; d1 += r1;
-                p0 = (p0 + r0) & 1; p1 = (p1 + r1) & 1;
-                bad |= (d0 > (1 << 24)) || (d1 > (1 << 24));
+            break;
+        }
+        if (__float_as_uint(sv) == 0u) {                    // +0 + (+-0) = +0: skip runs of zero chunks
+            if (tid == 0) s_first = MX_T;
+            __syncthreads();
+            if (c + tid < nch && !M.Z[c + tid]) atomicMin(&s_first, tid);
+            __syncthreads();
+            const int f = s_first;
+            __syncthreads();
+            if (f > 0) {                                     // f zero chunks (or the rest of this block)
+                if (tid == 0) s_c = min(nch, c + (long long)f);
+                __syncthreads();
+                continue;
+            }
+        }
+        bool serial = true;
+        if (sv >= MED_SMIN && sv < 3.0e38f) {
+            const uint32_t sbits = __float_as_uint(sv);
+            const int E = (int)((sbits >> 23) & 0xFFu);
+            const int k0 = (int)((sbits & 0x7FFFFFu) | 0x800000u), par = k0 & 1;
+            const long long cc = c + tid;
+            const int cnt = (int)min((long long)MX_T, nch - c);
+            int a0 = 0, a1 = 0, q0 = 0, q1 = 1, fb = MX_T;
+            if (tid < cnt) {
+                const int w = E - M.elo[cc];
+                if (w >= 0 && w < MW) {
+                    const int2 tv = M.T[cc * MW + w];
+                    const int f = M.F[cc * MW + w];
+                    a0 = tv.x; a1 = tv.y; q0 = f & 1; q1 = (f >> 1) & 1;
+                    if (f & 4) fb = tid;
+                } else {
+                    fb = tid;
+                }
+            } else {
+                fb = tid;
             }
             int cur = 0;
-            fd[0][0][tid] = d0; fd[0][1][tid] = d1; fe[0][0][tid] = (unsigned char)p0; fe[0][1][tid] = (unsigned char)p1;
-            fbad[0][tid] = bad ? tid : MX_T;
+            sa[0][0][tid] = a0; sa[0][1][tid] = a1; sq[0][0][tid] = (unsigned char)q0; sq[0][1][tid] = (unsigned char)q1;
+            sb[0][tid] = fb;
             __syncthreads();
-            for (int dd = 1; dd < MX_T; dd <<= 1) {         // inclusive scan: F_t = f_t o ... o f_0
-                int a0 = fd[cur][0][tid], a1 = fd[cur][1][tid];
-                int q0 = fe[cur][0][tid], q1 = fe[cur][1][tid];
-                int bb = fbad[cur][tid];
+            for (int dd = 1; dd < MX_T; dd <<= 1) {          // inclusive scan: F_t = f_0 then ... then f_t
+                int b0 = sa[cur][0][tid], b1 = sa[cur][1][tid];
+                int e0 = sq[cur][0][tid], e1 = sq[cur][1][tid];
+                int bb = sb[cur][tid];
                 if (tid >= dd) {
-                    const int b0 = fd[cur][0][tid - dd], b1 = fd[cur][1][tid - dd];
-                    const int e0 = fe[cur][0][tid - dd], e1 = fe[cur][1][tid - dd];
-                    // earlier part (tid-dd) first: start parity p -> its end parity feeds ours
-                    const int na0 = b0 + (e0 ? a1 : a0), na1 = b1 + (e1 ? a1 : a0);
-                    const int nq0 = e0 ? q1 : q0, nq1 = e1 ? q1 : q0;
-                    a0 = na0; a1 = na1; q0 = nq0; q1 = nq1;
-                    bb = min(bb, fbad[cur][tid - dd]);
+                    int p0 = sa[cur][0][tid - dd], p1 = sa[cur][1][tid - dd];
+                    int r0 = sq[cur][0][tid - dd], r1 = sq[cur][1][tid - dd];
+                    compose(p0, p1, r0, r1, b0, b1, e0, e1);
+                    b0 = p0; b1 = p1; e0 = r0; e1 = r1;
+                    bb = min(bb, sb[cur][tid - dd]);
                 }
-                fd[cur ^ 1][0][tid] = a0; fd[cur ^ 1][1][tid] = a1;
-                fe[cur ^ 1][0][tid] = (unsigned char)q0; fe[cur ^ 1][1][tid] = (unsigned char)q1;
-                fbad[cur ^ 1][tid] = bb;
+                sa[cur ^ 1][0][tid] = b0; sa[cur ^ 1][1][tid] = b1;
+                sq[cur ^ 1][0][tid] = (unsigned char)e0; sq[cur ^ 1][1][tid] = (unsigned char)e1;
+                sb[cur ^ 1][tid] = bb;
                 cur ^= 1;
                 __syncthreads();
             }
-            // first thread whose inclusive sum leaves the binade (k >= 2^24) or that saw a bad element
-            const int par = k0 & 1;
-            const int kend = k0 + fd[cur][par][tid];
-            const bool leave = kend >= (1 << 24) || fbad[cur][tid] <= tid;
-            const int first = __syncthreads_or(leave) ? 0 : -1;
-            __shared__ int s_first;
+            const int kend = k0 + sa[cur][par][tid];
+            const bool leave = kend >= (1 << 24) || sb[cur][tid] <= tid;
             if (tid == 0) s_first = MX_T;
             __syncthreads();
-            if (first == 0 && leave) atomicMin(&s_first, tid);
+            if (leave) atomicMin(&s_first, tid);
             __syncthreads();
-            const int f = s_first;
+            const int f = min(s_first, cnt);
             if (tid == 0) {
-                if (f >= MX_T) {                            // whole remainder applied at once
-                    s_sum = __fmul_rn((float)(k0 + fd[cur][par][MX_T - 1]), __uint_as_float((uint32_t)(E - 23) << 23));
-                    s_start = m;
-                } else {                                    // apply threads < f, then f's elements serially
-                    const int kf = f == 0 ? k0 : k0 + fd[cur][par][f - 1];
-                    float sv2 = __fmul_rn((float)kf, __uint_as_float((uint32_t)(E - 23) << 23));
-                    const int bf = st + f * per, ef = min(m, bf + per);
-                    for (int i = bf; i < ef; i++) sv2 = __fadd_rn(sv2, buf[i]);
-                    s_sum = sv2;
-                    s_start = ef;
-                }
+                const int kf = f == 0 ? k0 : k0 + sa[cur][par][f - 1];
+                s_sum = __fmul_rn((float)kf, __uint_as_float((uint32_t)(E - 23) << 23));   // k * u, exact
+                s_c = c + f;
+            }
+            serial = f < cnt;                                 // chunk c + f is added element by element
+            __syncthreads();
+        }
+        if (serial) {
+            const long long cs = s_c;
+            const int m = (int)min((long long)MC, n - cs * MC);
+            for (int i = tid; i < m; i += MX_T) buf[i] = x[cs * MC + i];
+            __syncthreads();
+            if (tid == 0) {
+                float s2 = s_sum;
+                for (int i = 0; i < m; i++) s2 = __fadd_rn(s2, buf[i]);
+                s_sum = s2;
+                s_c = cs + 1;
             }
             __syncthreads();
         }
-        __syncthreads();
     }
+    // max: x[0] folded with every chunk's max (strict >, as the reference's loop)
+    float mx = -INFINITY;
+    for (long long c = tid; c < nch; c += MX_T) { const float v = M.cmax[c]; mx = v > mx ? v : mx; }
     smax[tid] = mx;
     __syncthreads();
     if (tid == 0) {
-        float mm = smax[0];
-        for (int i = 1; i < MX_T; i++) if (smax[i] > mm) mm = smax[i];
+        float mm = x[0];
+        for (int i = 0; i < MX_T; i++) if (smax[i] > mm) mm = smax[i];
         int type = 0, add = 0;                               // :3605-3614
         for (int i = 7; i > 0; i--) {
             add += 1 << i;
@@ -449,18 +626,17 @@ extern "C" int dc_launch_to_small(const float* x, long long n, float* y, float* 
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-extern "C" int dc_launch_med(const float* x, long long n, float* d_mean, int* d_type, hipStream_t st) {
+// med_dataset_float's running float sum of x[0..n) continued from s_init, its mean and type, and
+// (optional) the raw sum and max; scratch: dc_med_scratch_bytes(n) bytes of device memory
+extern "C" int dc_launch_med(const float* x, long long n, float s_init, void* scratch, float* d_mean, int* d_type,
+                             float* d_sum, float* d_max, hipStream_t st) {
     if (n <= 0) return 0;
-    hipLaunchKernelGGL(med_exact_kernel, dim3(1), dim3(MX_T), 0, st, x, n, 0.0f, d_mean, d_type, (float*)nullptr,
-                       (float*)nullptr);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-// the running float sum of med_dataset_float continued from s_init over x[0..n) (+ the max of x)
-extern "C" int dc_launch_med_sum(const float* x, long long n, float s_init, float* d_sum, float* d_max, float* d_mean,
-                                 int* d_type, hipStream_t st) {
-    if (n <= 0) return 0;
-    hipLaunchKernelGGL(med_exact_kernel, dim3(1), dim3(MX_T), 0, st, x, n, s_init, d_mean, d_type, d_sum, d_max);
+    const long long nch = (n + MC - 1) / MC;
+    const MedScratch M = med_scratch(scratch, nch);
+    hipLaunchKernelGGL(med_chunk_sum_kernel, dim3((unsigned)nch), dim3(MC_T), 0, st, x, n, M);
+    hipLaunchKernelGGL(med_chunk_scan_kernel, dim3(1), dim3(1024), 0, st, M, nch, s_init);
+    hipLaunchKernelGGL(med_chunk_trans_kernel, dim3((unsigned)nch), dim3(MC_T), 0, st, x, n, M);
+    hipLaunchKernelGGL(med_compose_kernel, dim3(1), dim3(MX_T), 0, st, x, n, s_init, M, d_mean, d_type, d_sum, d_max);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

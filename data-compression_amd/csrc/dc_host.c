@@ -71,6 +71,7 @@ typedef struct {
     /* aux */
     float* part_v; long long* part_i;
     float* d_f;                      /* [0] min [1] mean */
+    void* med_scr; size_t med_scr_cap;  /* exact mean: chunk transducers (dc_med_scratch_bytes) */
     int* d_i;                        /* [0] type */
     uint32_t* d_crctab; uint32_t* d_x2n; uint32_t* d_crcparts; long long crcparts_cap; uint32_t* d_crc;
     unsigned long long* d_ham;
@@ -747,7 +748,9 @@ int dc_med_device(const void* d_x, long long n, float* mean_out, int* type_out) 
     int rc = ensure_init();
     if (rc) return rc;
     if (n <= 0) return seterr(DC_ERR_ARG, "empty input");
-    if (dc_launch_med((const float*)d_x, n, &G.d_f[1], &G.d_i[0], G.st)) return seterr(DC_ERR_HIP, "med launch failed");
+    if (grow(&G.med_scr, &G.med_scr_cap, (size_t)dc_med_scratch_bytes(n))) return DC_ERR_HIP;
+    if (dc_launch_med((const float*)d_x, n, 0.0f, G.med_scr, &G.d_f[1], &G.d_i[0], NULL, NULL, G.st))
+        return seterr(DC_ERR_HIP, "med launch failed");
     float m;
     int t;
     HIPCHK(hipMemcpyAsync(&m, &G.d_f[1], 4, hipMemcpyDeviceToHost, G.st));
@@ -764,7 +767,8 @@ int dc_med_sum_device(const void* d_x, long long n, float s_init, float* sum_out
     int rc = ensure_init();
     if (rc) return rc;
     if (n <= 0) return seterr(DC_ERR_ARG, "empty input");
-    if (dc_launch_med_sum((const float*)d_x, n, s_init, &G.d_f[2], &G.d_f[3], &G.d_f[1], &G.d_i[0], G.st))
+    if (grow(&G.med_scr, &G.med_scr_cap, (size_t)dc_med_scratch_bytes(n))) return DC_ERR_HIP;
+    if (dc_launch_med((const float*)d_x, n, s_init, G.med_scr, &G.d_f[1], &G.d_i[0], &G.d_f[2], &G.d_f[3], G.st))
         return seterr(DC_ERR_HIP, "med launch failed");
     float h[2];
     HIPCHK(hipMemcpyAsync(h, &G.d_f[2], 8, hipMemcpyDeviceToHost, G.st));

@@ -117,9 +117,9 @@ long long dc_decode_group(void);
 
 int dc_launch_to_small(const float* x, long long n, float* y, float* part_v, long long* part_i, float* d_min,
                        dc_hip_stream st);
-int dc_launch_med(const float* x, long long n, float* d_mean, int* d_type, dc_hip_stream st);
-int dc_launch_med_sum(const float* x, long long n, float s_init, float* d_sum, float* d_max, float* d_mean, int* d_type,
-                      dc_hip_stream st);
+int dc_launch_med(const float* x, long long n, float s_init, void* scratch, float* d_mean, int* d_type, float* d_sum,
+                  float* d_max, dc_hip_stream st);
+long long dc_med_scratch_bytes(long long n);
 long long dc_crc_parts(long long nbytes);
 int dc_crc_run_bytes(void);
 int dc_launch_crc32(const uint8_t* s, long long nbytes, const uint32_t* d_tab, const uint32_t* d_x2n,

@@ -259,7 +259,9 @@ def test_shard_encode_with_start_bit(dc, oracle, ct):
 
 
 @pytest.mark.parametrize("kind,n", [("u10", 1 << 24), ("u10", 1 << 20), ("ramp", 1 << 21), ("unit", 3000001),
-                                    ("himeno", 1 << 18), ("signed", 1 << 20), ("nan", 100000), ("tiny", 1 << 20)])
+                                    ("himeno", 1 << 18), ("signed", 1 << 20), ("nan", 100000), ("tiny", 1 << 20),
+                                    ("zeros", 1 << 22), ("zeros_u10", (1 << 21) + 77), ("wide", 1 << 20),
+                                    ("u10", 1 << 26)])
 def test_med_exact_parallel(dc, oracle, kind, n):
     """med_dataset_float's left-to-right float sum, computed by the binade-transducer scan, must equal
     the serial sum bit for bit (mean and type)."""
@@ -272,6 +274,14 @@ def test_med_exact_parallel(dc, oracle, kind, n):
         x[n // 2] = np.nan
     elif kind == "tiny":
         x = (rs.rand(n) * 1e-30).astype(np.float32)
+    elif kind == "zeros":                      # the EQ input after toSmallDataset: zero chunks are skipped
+        x = np.zeros(n, np.float32)
+        x[::7919] = -0.0
+    elif kind == "zeros_u10":                  # a zero prefix, then values (the skip ends mid-block)
+        x = oracle.gen_u10(n)
+        x[: n // 3] = 0.0
+    elif kind == "wide":                       # exponents over ~60 binades: many serial chunks
+        x = (rs.rand(n) * np.exp2(rs.randint(-30, 30, n))).astype(np.float32)
     else:
         x = _inputs(oracle, kind, n)
     d = torch.from_numpy(x).cuda()
