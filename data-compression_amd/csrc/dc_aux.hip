@@ -138,80 +138,127 @@ __global__ __launch_bounds__(256) void med_kernel(const float* __restrict__ x, l
 //                     transducer cannot take (negative, NaN, too large, the binade not in its window),
 //                     or a sum below SMIN, is added element by element by one lane, exactly like the
 //                     reference.  At 2^26 U10: about 25 such chunks (the binade crossings).
+// The same kernels run med_dataset_double (:3564-3590) with u = 2^(E-1075) and k < 2^53 (MedFP<double>).
 constexpr int MC = 2048;                                   // elements per chunk
 constexpr int MW = 6;                                      // candidate binades per chunk
 constexpr int MC_T = 256;                                  // threads of the chunk kernels (8 elements each)
 constexpr int MC_PER = MC / MC_T;
 constexpr int MX_T = 1024;                                 // compose workgroup
-#define MED_SMIN 7.8886091e-31f                            // 2^-100: below it 1/u would overflow float
 
+// float / double: the running sum's binade E (biased exponent), k = s/u in [2^M, 2^(M+1)), u = 2^(E-bias-M)
+template <typename T> struct MedFP;
+template <> struct MedFP<float> {
+    typedef uint32_t U;
+    typedef int D;                                         // units added per chunk (saturated)
+    static constexpr int M = 23, BIAS = 127, EMIN = 24, EMAX = 253;
+    static constexpr D SAT = 1 << 25;
+    __device__ static U bits(float v) { return __float_as_uint(v); }
+    __device__ static float from(U b) { return __uint_as_float(b); }
+    __device__ static int expo(float v) { return (int)((bits(v) >> 23) & 0xFFu); }
+    __device__ static float pow2(int e) { return from((U)(e + BIAS) << M); }       // 2^e, e in the normal range
+    __device__ static float mul(float a, float b) { return __fmul_rn(a, b); }
+    __device__ static float sub(float a, float b) { return __fsub_rn(a, b); }
+    __device__ static float add(float a, float b) { return __fadd_rn(a, b); }
+    __device__ static float smin() { return pow2(-100); }                         // 1/u stays a float above it
+    __device__ static float smax() { return 3.0e38f; }
+    __device__ static float mean(float s, long long n) { return __fdiv_rn(s, (float)n); }
+    __device__ static int type(float mx) {                                        // :3605-3614
+        int add = 0;
+        for (int i = 7; i > 0; i--) { add += 1 << i; if ((double)mx < ldexp(1.0, add - 127)) return 8 - i; }
+        return 0;
+    }
+};
+template <> struct MedFP<double> {
+    typedef unsigned long long U;
+    typedef long long D;
+    static constexpr int M = 52, BIAS = 1023, EMIN = 53, EMAX = 2045;
+    static constexpr D SAT = 1ll << 54;
+    __device__ static U bits(double v) { return (U)__double_as_longlong(v); }
+    __device__ static double from(U b) { return __longlong_as_double((long long)b); }
+    __device__ static int expo(double v) { return (int)((bits(v) >> 52) & 0x7FFull); }
+    __device__ static double pow2(int e) { return from((U)(e + BIAS) << M); }
+    __device__ static double mul(double a, double b) { return __dmul_rn(a, b); }
+    __device__ static double sub(double a, double b) { return __dsub_rn(a, b); }
+    __device__ static double add(double a, double b) { return __dadd_rn(a, b); }
+    __device__ static double smin() { return pow2(-960); }
+    __device__ static double smax() { return 1.0e308; }
+    __device__ static double mean(double s, long long n) { return __ddiv_rn(s, (double)n); }
+    __device__ static int type(double mx) {                                       // :3576-3585
+        int add = 0;
+        for (int i = 10; i > 0; i--) { add += 1 << i; if (mx < ldexp(1.0, add - 1023)) return 11 - i; }
+        return 0;
+    }
+};
+
+template <typename T>
 struct MedScratch {
-    double* csum;                                          // [nch] chunk sums, then their exclusive scan
-    float* cmax;                                           // [nch] chunk max (NaN-skipping)
+    double* csum;                                          // [nch] chunk sums (an estimate only)
+    T* cmax;                                               // [nch] chunk max (NaN-skipping)
     int* elo;                                              // [nch] first candidate binade
-    int2* T;                                               // [nch * MW] units added from parity 0 / 1
+    typename MedFP<T>::D* Td;                              // [nch * MW * 2] units added from parity 0 / 1
     uint8_t* F;                                            // [nch * MW] end parity 0 | end parity 1 << 1 | bad << 2
     uint8_t* Z;                                            // [nch] 1: every element is +0 / -0
 };
 
-extern "C" long long dc_med_scratch_bytes(long long n) {
+template <typename T>
+__host__ __device__ inline long long med_scratch_bytes(long long n) {
     const long long nch = (n + MC - 1) / MC;
-    return nch * (8 + 4 + 4 + MW * 8 + MW + 1) + 4 * 256;
+    return nch * (8 + (long long)sizeof(T) + 4 + MW * 2 * (long long)sizeof(typename MedFP<T>::D) + MW + 1) + 1024;
 }
+extern "C" long long dc_med_scratch_bytes(long long n) { return med_scratch_bytes<float>(n); }
+extern "C" long long dc_med_scratch_bytes64(long long n) { return med_scratch_bytes<double>(n); }
 
-__host__ __device__ inline MedScratch med_scratch(void* base, long long nch) {
-    MedScratch m;
+template <typename T>
+__host__ __device__ inline MedScratch<T> med_scratch(void* base, long long nch) {
+    MedScratch<T> m;
     char* b = (char*)base;
     m.csum = (double*)b; b += nch * 8;
-    m.T = (int2*)b; b += nch * MW * 8;
-    m.cmax = (float*)b; b += nch * 4;
+    m.Td = (typename MedFP<T>::D*)b; b += nch * MW * 2 * (long long)sizeof(typename MedFP<T>::D);
+    m.cmax = (T*)b; b += nch * (long long)sizeof(T);
     m.elo = (int*)b; b += nch * 4;
     m.F = (uint8_t*)b; b += nch * MW;
     m.Z = (uint8_t*)b;
     return m;
 }
 
-__device__ __forceinline__ void load_chunk(const float* __restrict__ x, long long n, long long c, float* v) {
+template <typename T>
+__device__ __forceinline__ void load_chunk(const T* __restrict__ x, long long n, long long c, T* v) {
     const long long e0 = c * MC + (long long)threadIdx.x * MC_PER;
-    if (e0 + MC_PER <= n && ((reinterpret_cast<uintptr_t>(x) & 15u) == 0)) {
-        const float4* p = reinterpret_cast<const float4*>(x + e0);
-        const float4 a = p[0], b = p[1];
-        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-    } else {
 #pragma unroll
-        for (int i = 0; i < MC_PER; i++) v[i] = e0 + i < n ? x[e0 + i] : 0.0f;
-    }
+    for (int i = 0; i < MC_PER; i++) v[i] = e0 + i < n ? x[e0 + i] : (T)0;
 }
 
-__global__ __launch_bounds__(MC_T) void med_chunk_sum_kernel(const float* __restrict__ x, long long n, MedScratch M) {
+template <typename T>
+__global__ __launch_bounds__(MC_T) void med_chunk_sum_kernel(const T* __restrict__ x, long long n, MedScratch<T> M) {
+    typedef MedFP<T> FP;
     __shared__ double ws[MC_T / 64];
-    __shared__ float wm[MC_T / 64];
+    __shared__ T wm[MC_T / 64];
     const long long c = blockIdx.x;
-    float v[MC_PER];
+    T v[MC_PER];
     load_chunk(x, n, c, v);
     const long long e0 = c * MC + (long long)threadIdx.x * MC_PER;
     double sm = 0.0;
-    float mx = -INFINITY;
+    T mx = -INFINITY;
     bool nz = false;
 #pragma unroll
     for (int i = 0; i < MC_PER; i++)
         if (e0 + i < n) {
             sm += (double)v[i];
             mx = v[i] > mx ? v[i] : mx;                          // NaNs never win (as the reference's >)
-            nz |= (__float_as_uint(v[i]) & 0x7FFFFFFFu) != 0u;
+            nz |= (FP::bits(v[i]) << 1) != 0;
         }
     const bool anynz = __syncthreads_or(nz);
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
         sm += __shfl_xor(sm, d, 64);
-        const float o = __shfl_xor(mx, d, 64);
+        const T o = __shfl_xor(mx, d, 64);
         mx = o > mx ? o : mx;
     }
     if ((threadIdx.x & 63) == 0) { ws[threadIdx.x >> 6] = sm; wm[threadIdx.x >> 6] = mx; }
     __syncthreads();
     if (threadIdx.x == 0) {
         double t = 0.0;
-        float m = -INFINITY;
+        T m = -INFINITY;
         for (int w = 0; w < MC_T / 64; w++) { t += ws[w]; m = wm[w] > m ? wm[w] : m; }
         M.csum[c] = isfinite(t) ? t : 0.0;
         M.cmax[c] = m;
@@ -219,7 +266,11 @@ __global__ __launch_bounds__(MC_T) void med_chunk_sum_kernel(const float* __rest
     }
 }
 
-__global__ __launch_bounds__(1024) void med_chunk_scan_kernel(MedScratch M, long long nch, float s_init) {
+// exclusive scan of the chunk sums -> an estimate of the running sum at every chunk; its binade
+// E_est opens the chunk's window [E_est - 4, E_est + 1] (the float sum stalls below the real one)
+template <typename T>
+__global__ __launch_bounds__(1024) void med_chunk_scan_kernel(MedScratch<T> M, long long nch, T s_init) {
+    typedef MedFP<T> FP;
     __shared__ double wt[16];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const long long per = (nch + 1023) / 1024, c0 = tid * per, c1 = min(nch, c0 + per);
@@ -236,48 +287,55 @@ __global__ __launch_bounds__(1024) void med_chunk_scan_kernel(MedScratch M, long
     double run = (double)s_init + inc - sm;
     for (int w = 0; w < wid; w++) run += wt[w];
     for (long long c = c0; c < c1; c++) {
-        const float est = (float)fmin(fmax(run, 0.0), 3.0e38);
-        const int E = (int)((__float_as_uint(est) >> 23) & 0xFFu);
-        M.elo[c] = E - 4;
+        const T est = (T)fmin(fmax(run, 0.0), (double)FP::smax());
+        M.elo[c] = FP::expo(est) - 4;
         run += M.csum[c];
     }
 }
 
 // transducer of one thread's elements for binade E (k's parity p in, units added / parity out)
-__device__ __forceinline__ void trans_elems(const float* v, int cnt, int E, int& d0, int& d1, int& p0, int& p1, bool& bad) {
-    const float scale = __uint_as_float((uint32_t)(277 - E) << 23);      // 2^(150-E) = 1/u
-    const float lim = __uint_as_float((uint32_t)(E + 1) << 23);          // 2^(E-126), the binade's top
+template <typename T>
+__device__ __forceinline__ void trans_elems(const T* v, int cnt, int E, typename MedFP<T>::D& d0,
+                                            typename MedFP<T>::D& d1, int& p0, int& p1, bool& bad) {
+    typedef MedFP<T> FP;
+    typedef typename FP::D D;
+    const T scale = FP::pow2(FP::BIAS + FP::M - E);                 // 1/u
+    const T lim = FP::pow2(E + 1 - FP::BIAS);                       // the binade's top
     d0 = 0; d1 = 0; p0 = 0; p1 = 1; bad = false;
 #pragma unroll
     for (int i = 0; i < MC_PER; i++) {
         if (i < cnt) {
-            bad |= !(v[i] >= 0.0f) || !(v[i] < lim);                 // negative, NaN, inf or >= the binade's top
-            const float q = __fmul_rn(v[i], scale);                  // exact: power-of-two scaling
-            const float fq = floorf(q);
-            const float fr = __fsub_rn(q, fq);
-            const int fl = (int)fq;
-            const int up = fr > 0.5f ? 1 : 0, tie = fr == 0.5f ? 1 : 0;
-            const int r0 = fl + up + (tie & ((p0 + fl) & 1));
-            const int r1 = fl + up + (tie & ((p1 + fl) & 1));
-            d0 = min(d0 + r0, 1 << 25); d1 = min(d1 + r1, 1 << 25); // >= 2^24 leaves the binade anyway
-            p0 = (p0 + r0) & 1; p1 = (p1 + r1) & 1;
+            bad |= !(v[i] >= (T)0) || !(v[i] < lim);              // negative, NaN, inf or >= the binade's top
+            const T q = FP::mul(v[i], scale);                     // exact: power-of-two scaling
+            const T fq = floor(q);
+            const T fr = FP::sub(q, fq);
+            const D fl = (D)fq;
+            const int up = fr > (T)0.5 ? 1 : 0, tie = fr == (T)0.5 ? 1 : 0;
+            const D r0 = fl + up + (tie & (int)((p0 + fl) & 1));
+            const D r1 = fl + up + (tie & (int)((p1 + fl) & 1));
+            d0 = min(d0 + r0, FP::SAT); d1 = min(d1 + r1, FP::SAT);   // >= 2^(M+1) leaves the binade anyway
+            p0 = (int)((p0 + r0) & 1); p1 = (int)((p1 + r1) & 1);
         }
     }
 }
 
 // f then g (f earlier): start parity p -> f's units + g's units from f's end parity
-__device__ __forceinline__ void compose(int& a0, int& a1, int& q0, int& q1, int b0, int b1, int e0, int e1) {
-    // (a, q) = f, (b, e) = g  ->  f then g
-    const int n0 = min(a0 + (q0 ? b1 : b0), 1 << 25), n1 = min(a1 + (q1 ? b1 : b0), 1 << 25);
+template <typename D>
+__device__ __forceinline__ void compose(D& a0, D& a1, int& q0, int& q1, D b0, D b1, int e0, int e1, D sat) {
+    const D n0 = min(a0 + (q0 ? b1 : b0), sat), n1 = min(a1 + (q1 ? b1 : b0), sat);
     const int m0 = q0 ? e1 : e0, m1 = q1 ? e1 : e0;
     a0 = n0; a1 = n1; q0 = m0; q1 = m1;
 }
 
-__global__ __launch_bounds__(MC_T) void med_chunk_trans_kernel(const float* __restrict__ x, long long n, MedScratch M) {
-    __shared__ int sd[MW][MC_T / 64][4];
+template <typename T>
+__global__ __launch_bounds__(MC_T) void med_chunk_trans_kernel(const T* __restrict__ x, long long n, MedScratch<T> M) {
+    typedef MedFP<T> FP;
+    typedef typename FP::D D;
+    __shared__ D sd[MW][MC_T / 64][2];
+    __shared__ int sf[MW][MC_T / 64];
     const long long c = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    float v[MC_PER];
+    T v[MC_PER];
     load_chunk(x, n, c, v);
     const long long e0 = c * MC + (long long)tid * MC_PER;
     const int cnt = (int)max(0ll, min((long long)MC_PER, n - e0));
@@ -285,48 +343,54 @@ __global__ __launch_bounds__(MC_T) void med_chunk_trans_kernel(const float* __re
 #pragma unroll
     for (int w = 0; w < MW; w++) {
         const int E = elo + w;
-        int d0 = 0, d1 = 0, p0 = 0, p1 = 1;
-        bool bad = E < 24 || E > 253;                                 // 1/u or the binade top not a float
-        if (!bad) trans_elems(v, cnt, E, d0, d1, p0, p1, bad);
+        D d0 = 0, d1 = 0;
+        int p0 = 0, p1 = 1;
+        bool bad = E < FP::EMIN || E > FP::EMAX;                      // 1/u or the binade top not a number
+        if (!bad) trans_elems<T>(v, cnt, E, d0, d1, p0, p1, bad);
         // ordered reduction over the wave: lane i absorbs lane i + d (its successor block)
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
-            const int b0 = __shfl_down(d0, d, 64), b1 = __shfl_down(d1, d, 64);
-            const int e0_ = __shfl_down(p0, d, 64), e1_ = __shfl_down(p1, d, 64);
-            const int bb = __shfl_down((int)bad, d, 64);
-            if ((lane & (2 * d - 1)) == 0 && lane + d < 64) {
-                compose(d0, d1, p0, p1, b0, b1, e0_, e1_);
-                bad |= bb != 0;
+            const D b0 = __shfl_down(d0, d, 64), b1 = __shfl_down(d1, d, 64);
+            const int f = __shfl_down(p0 | (p1 << 1) | ((int)bad << 2), d, 64);
+            if ((lane & (2 * d - 1)) == 0) {
+                compose(d0, d1, p0, p1, b0, b1, f & 1, (f >> 1) & 1, FP::SAT);
+                bad |= (f & 4) != 0;
             }
         }
-        if (lane == 0) { sd[w][wid][0] = d0; sd[w][wid][1] = d1; sd[w][wid][2] = p0 | (p1 << 1); sd[w][wid][3] = bad; }
+        if (lane == 0) { sd[w][wid][0] = d0; sd[w][wid][1] = d1; sf[w][wid] = p0 | (p1 << 1) | ((int)bad << 2); }
     }
     __syncthreads();
     if (tid < MW) {
         const int w = tid;
-        int a0 = sd[w][0][0], a1 = sd[w][0][1], q0 = sd[w][0][2] & 1, q1 = sd[w][0][2] >> 1;
-        bool bad = sd[w][0][3] != 0;
+        D a0 = sd[w][0][0], a1 = sd[w][0][1];
+        int q0 = sf[w][0] & 1, q1 = (sf[w][0] >> 1) & 1;
+        bool bad = (sf[w][0] & 4) != 0;
         for (int k = 1; k < MC_T / 64; k++) {
-            compose(a0, a1, q0, q1, sd[w][k][0], sd[w][k][1], sd[w][k][2] & 1, sd[w][k][2] >> 1);
-            bad |= sd[w][k][3] != 0;
+            compose(a0, a1, q0, q1, sd[w][k][0], sd[w][k][1], sf[w][k] & 1, (sf[w][k] >> 1) & 1, FP::SAT);
+            bad |= (sf[w][k] & 4) != 0;
         }
-        M.T[c * MW + w] = make_int2(a0, a1);
+        M.Td[(c * MW + w) * 2] = a0;
+        M.Td[(c * MW + w) * 2 + 1] = a1;
         M.F[c * MW + w] = (uint8_t)(q0 | (q1 << 1) | (bad ? 4 : 0));
     }
 }
 
-__global__ __launch_bounds__(MX_T) void med_compose_kernel(const float* __restrict__ x, long long n, float s_init,
-                                                           MedScratch M, float* __restrict__ out_mean,
-                                                           int* __restrict__ out_type, float* __restrict__ out_sum,
-                                                           float* __restrict__ out_max) {
-    __shared__ float buf[MC];
-    __shared__ int sa[2][2][MX_T];                          // [buffer][start parity] units
+template <typename T>
+__global__ __launch_bounds__(MX_T) void med_compose_kernel(const T* __restrict__ x, long long n, T s_init,
+                                                           MedScratch<T> M, T* __restrict__ out_mean,
+                                                           int* __restrict__ out_type, T* __restrict__ out_sum,
+                                                           T* __restrict__ out_max) {
+    typedef MedFP<T> FP;
+    typedef typename FP::D D;
+    typedef typename FP::U U;
+    __shared__ T buf[MC];
+    __shared__ D sa[2][2][MX_T];                            // [buffer][start parity] units
     __shared__ unsigned char sq[2][2][MX_T];                // [buffer][start parity] end parity
     __shared__ int sb[2][MX_T];                             // first invalid chunk (inclusive min)
-    __shared__ float s_sum;
+    __shared__ T s_sum;
     __shared__ long long s_c;
     __shared__ int s_first;
-    __shared__ float smax[MX_T];
+    __shared__ T smx[MX_T / 64];
     const int tid = threadIdx.x;
     const long long nch = (n + MC - 1) / MC;
     if (tid == 0) { s_sum = s_init; s_c = 0; }
@@ -334,58 +398,53 @@ __global__ __launch_bounds__(MX_T) void med_compose_kernel(const float* __restri
     while (true) {
         const long long c = s_c;
         if (c >= nch) break;
-        const float sv = s_sum;
-        if (sv != sv) {                                     // NaN + anything stays NaN
-            if (tid == 0) s_c = nch;
-            __syncthreads();
-            break;
-        }
-        if (__float_as_uint(sv) == 0u) {                    // +0 + (+-0) = +0: skip runs of zero chunks
+        const T sv = s_sum;
+        if (sv != sv) break;                                // NaN + anything stays NaN
+        if (FP::bits(sv) == 0) {                            // +0 + (+-0) = +0: skip runs of zero chunks
             if (tid == 0) s_first = MX_T;
             __syncthreads();
             if (c + tid < nch && !M.Z[c + tid]) atomicMin(&s_first, tid);
             __syncthreads();
             const int f = s_first;
             __syncthreads();
-            if (f > 0) {                                     // f zero chunks (or the rest of this block)
+            if (f > 0) {
                 if (tid == 0) s_c = min(nch, c + (long long)f);
                 __syncthreads();
                 continue;
             }
         }
         bool serial = true;
-        if (sv >= MED_SMIN && sv < 3.0e38f) {
-            const uint32_t sbits = __float_as_uint(sv);
-            const int E = (int)((sbits >> 23) & 0xFFu);
-            const int k0 = (int)((sbits & 0x7FFFFFu) | 0x800000u), par = k0 & 1;
+        if (sv >= FP::smin() && sv < FP::smax()) {
+            const U sbits = FP::bits(sv);
+            const int E = FP::expo(sv);
+            const D k0 = (D)((sbits & ((U(1) << FP::M) - 1)) | (U(1) << FP::M));
+            const int par = (int)(k0 & 1);
             const long long cc = c + tid;
             const int cnt = (int)min((long long)MX_T, nch - c);
-            int a0 = 0, a1 = 0, q0 = 0, q1 = 1, fb = MX_T;
+            D a0 = 0, a1 = 0;
+            int q0 = 0, q1 = 1, fb = tid;
             if (tid < cnt) {
                 const int w = E - M.elo[cc];
                 if (w >= 0 && w < MW) {
-                    const int2 tv = M.T[cc * MW + w];
+                    a0 = M.Td[(cc * MW + w) * 2];
+                    a1 = M.Td[(cc * MW + w) * 2 + 1];
                     const int f = M.F[cc * MW + w];
-                    a0 = tv.x; a1 = tv.y; q0 = f & 1; q1 = (f >> 1) & 1;
-                    if (f & 4) fb = tid;
-                } else {
-                    fb = tid;
+                    q0 = f & 1; q1 = (f >> 1) & 1;
+                    fb = (f & 4) ? tid : MX_T;
                 }
-            } else {
-                fb = tid;
             }
             int cur = 0;
             sa[0][0][tid] = a0; sa[0][1][tid] = a1; sq[0][0][tid] = (unsigned char)q0; sq[0][1][tid] = (unsigned char)q1;
             sb[0][tid] = fb;
             __syncthreads();
             for (int dd = 1; dd < MX_T; dd <<= 1) {          // inclusive scan: F_t = f_0 then ... then f_t
-                int b0 = sa[cur][0][tid], b1 = sa[cur][1][tid];
+                D b0 = sa[cur][0][tid], b1 = sa[cur][1][tid];
                 int e0 = sq[cur][0][tid], e1 = sq[cur][1][tid];
                 int bb = sb[cur][tid];
                 if (tid >= dd) {
-                    int p0 = sa[cur][0][tid - dd], p1 = sa[cur][1][tid - dd];
+                    D p0 = sa[cur][0][tid - dd], p1 = sa[cur][1][tid - dd];
                     int r0 = sq[cur][0][tid - dd], r1 = sq[cur][1][tid - dd];
-                    compose(p0, p1, r0, r1, b0, b1, e0, e1);
+                    compose(p0, p1, r0, r1, b0, b1, e0, e1, FP::SAT);
                     b0 = p0; b1 = p1; e0 = r0; e1 = r1;
                     bb = min(bb, sb[cur][tid - dd]);
                 }
@@ -395,16 +454,16 @@ __global__ __launch_bounds__(MX_T) void med_compose_kernel(const float* __restri
                 cur ^= 1;
                 __syncthreads();
             }
-            const int kend = k0 + sa[cur][par][tid];
-            const bool leave = kend >= (1 << 24) || sb[cur][tid] <= tid;
+            const D kend = k0 + sa[cur][par][tid];
+            const bool leave = kend >= (D(1) << (FP::M + 1)) || sb[cur][tid] <= tid;
             if (tid == 0) s_first = MX_T;
             __syncthreads();
             if (leave) atomicMin(&s_first, tid);
             __syncthreads();
             const int f = min(s_first, cnt);
             if (tid == 0) {
-                const int kf = f == 0 ? k0 : k0 + sa[cur][par][f - 1];
-                s_sum = __fmul_rn((float)kf, __uint_as_float((uint32_t)(E - 23) << 23));   // k * u, exact
+                const D kf = f == 0 ? k0 : k0 + sa[cur][par][f - 1];
+                s_sum = FP::mul((T)kf, FP::pow2(E - FP::BIAS - FP::M));   // k * u, exact
                 s_c = c + f;
             }
             serial = f < cnt;                                 // chunk c + f is added element by element
@@ -416,8 +475,8 @@ __global__ __launch_bounds__(MX_T) void med_compose_kernel(const float* __restri
             for (int i = tid; i < m; i += MX_T) buf[i] = x[cs * MC + i];
             __syncthreads();
             if (tid == 0) {
-                float s2 = s_sum;
-                for (int i = 0; i < m; i++) s2 = __fadd_rn(s2, buf[i]);
+                T s2 = s_sum;
+                for (int i = 0; i < m; i++) s2 = FP::add(s2, buf[i]);
                 s_sum = s2;
                 s_c = cs + 1;
             }
@@ -425,23 +484,33 @@ __global__ __launch_bounds__(MX_T) void med_compose_kernel(const float* __restri
         }
     }
     // max: x[0] folded with every chunk's max (strict >, as the reference's loop)
-    float mx = -INFINITY;
-    for (long long c = tid; c < nch; c += MX_T) { const float v = M.cmax[c]; mx = v > mx ? v : mx; }
-    smax[tid] = mx;
+    T mx = -INFINITY;
+    for (long long c = tid; c < nch; c += MX_T) { const T v = M.cmax[c]; mx = v > mx ? v : mx; }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) { const T o = __shfl_xor(mx, d, 64); mx = o > mx ? o : mx; }
+    if ((tid & 63) == 0) smx[tid >> 6] = mx;
     __syncthreads();
     if (tid == 0) {
-        float mm = x[0];
-        for (int i = 0; i < MX_T; i++) if (smax[i] > mm) mm = smax[i];
-        int type = 0, add = 0;                               // :3605-3614
-        for (int i = 7; i > 0; i--) {
-            add += 1 << i;
-            if ((double)mm < ldexp(1.0, add - 127)) { type = 8 - i; break; }
-        }
-        *out_type = type;
-        *out_mean = __fdiv_rn(s_sum, (float)n);
+        T mm = x[0];
+        for (int i = 0; i < MX_T / 64; i++) if (smx[i] > mm) mm = smx[i];
+        *out_type = FP::type(mm);
+        *out_mean = FP::mean(s_sum, n);
         if (out_sum) *out_sum = s_sum;
         if (out_max) *out_max = mm;
     }
+}
+
+template <typename T>
+static int launch_med(const T* x, long long n, T s_init, void* scratch, T* d_mean, int* d_type, T* d_sum, T* d_max,
+                      hipStream_t st) {
+    if (n <= 0) return 0;
+    const long long nch = (n + MC - 1) / MC;
+    const MedScratch<T> M = med_scratch<T>(scratch, nch);
+    hipLaunchKernelGGL(med_chunk_sum_kernel<T>, dim3((unsigned)nch), dim3(MC_T), 0, st, x, n, M);
+    hipLaunchKernelGGL(med_chunk_scan_kernel<T>, dim3(1), dim3(1024), 0, st, M, nch, s_init);
+    hipLaunchKernelGGL(med_chunk_trans_kernel<T>, dim3((unsigned)nch), dim3(MC_T), 0, st, x, n, M);
+    hipLaunchKernelGGL(med_compose_kernel<T>, dim3(1), dim3(MX_T), 0, st, x, n, s_init, M, d_mean, d_type, d_sum, d_max);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // ---------------------------------------------------------------- CRC-32 (zlib)
@@ -630,14 +699,11 @@ extern "C" int dc_launch_to_small(const float* x, long long n, float* y, float* 
 // (optional) the raw sum and max; scratch: dc_med_scratch_bytes(n) bytes of device memory
 extern "C" int dc_launch_med(const float* x, long long n, float s_init, void* scratch, float* d_mean, int* d_type,
                              float* d_sum, float* d_max, hipStream_t st) {
-    if (n <= 0) return 0;
-    const long long nch = (n + MC - 1) / MC;
-    const MedScratch M = med_scratch(scratch, nch);
-    hipLaunchKernelGGL(med_chunk_sum_kernel, dim3((unsigned)nch), dim3(MC_T), 0, st, x, n, M);
-    hipLaunchKernelGGL(med_chunk_scan_kernel, dim3(1), dim3(1024), 0, st, M, nch, s_init);
-    hipLaunchKernelGGL(med_chunk_trans_kernel, dim3((unsigned)nch), dim3(MC_T), 0, st, x, n, M);
-    hipLaunchKernelGGL(med_compose_kernel, dim3(1), dim3(MX_T), 0, st, x, n, s_init, M, d_mean, d_type, d_sum, d_max);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    return launch_med<float>(x, n, s_init, scratch, d_mean, d_type, d_sum, d_max, st);
+}
+// med_dataset_double (:3564-3590): the same on doubles (scratch: dc_med_scratch_bytes64(n))
+extern "C" int dc_launch_med64(const double* x, long long n, void* scratch, double* d_mean, int* d_type, hipStream_t st) {
+    return launch_med<double>(x, n, 0.0, scratch, d_mean, d_type, (double*)nullptr, (double*)nullptr, st);
 }
 
 extern "C" long long dc_crc_parts(long long nbytes) { return (nbytes + CRC_BLK - 1) / CRC_BLK; }

@@ -976,50 +976,6 @@ __global__ void sub_min(const double* __restrict__ x, long long n, const double*
         y[i] = __dsub_rn(x[i], m);
 }
 
-// med_dataset_double: the sequential double sum (order-dependent, so one lane adds a staged block while
-// the workgroup loads the next), max, type from max (:3564-3590)
-__global__ __launch_bounds__(1024) void med_kernel(const double* __restrict__ x, long long n, double* __restrict__ dmean,
-                                                   int* __restrict__ dtype) {
-    __shared__ double buf[2][1024];
-    __shared__ double smax[16];
-    double total = 0.0, mx = x[0];
-    double lmax = x[0];
-    const int tid = threadIdx.x;
-    if (n > 0) buf[0][tid] = tid < n ? x[tid] : 0.0;
-    __syncthreads();
-    int cur = 0;
-    for (long long b = 0; b < n; b += 1024) {
-        const long long nxt = b + 1024 + tid;
-        if (nxt < n) buf[cur ^ 1][tid] = x[nxt];
-        if (b + tid < n) { const double v = buf[cur][tid]; if (v > lmax) lmax = v; }
-        if (tid == 0) {
-            const int lim = (int)std::min(1024ll, n - b);
-            for (int i = 0; i < lim; i++) total = __dadd_rn(total, buf[cur][i]);
-        }
-        __syncthreads();
-        cur ^= 1;
-    }
-    // max with the reference's rule (data[i] > max, starting from data[0]): NaN never wins
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const double o = __shfl_xor(lmax, d, 64);
-        if (o > lmax) lmax = o;
-    }
-    if ((tid & 63) == 0) smax[tid >> 6] = lmax;
-    __syncthreads();
-    if (tid == 0) {
-        mx = x[0];
-        for (int i = 0; i < 16; i++) if (smax[i] > mx) mx = smax[i];
-        int add = 0, type = 0;
-        for (int i = 10; i > 0; i--) {
-            add += 1 << i;
-            if (mx < ldexp(1.0, add - 1023)) { type = 11 - i; break; }
-        }
-        *dtype = type;
-        *dmean = total / (double)n;
-    }
-}
-
 }  // namespace dc64
 
 // ================================================================================================ host
@@ -1039,6 +995,7 @@ struct Ctx64 {
     unsigned long long* h = nullptr;        // pinned: [0] total bits [1] err [2] ndec
     // pre-passes
     double* pv = nullptr; long long* pi = nullptr; double* d_f = nullptr; int* d_i = nullptr;
+    void* med_scr = nullptr; size_t med_cap = 0;          // exact mean scratch (dc_med_scratch_bytes64)
     int dec_pending = 0, dec_ct = 0, map_fallback = 0;
     long long dbg_words = 0, dbg_chunks = 0;
     unsigned* ctr = nullptr;
@@ -1351,13 +1308,26 @@ extern "C" int dc64_to_small_device(const void* d_x, long long n, void* d_out, d
     return DC_OK;
 }
 
+extern "C" int dc_launch_med64(const double* x, long long n, void* scratch, double* d_mean, int* d_type, hipStream_t st);
+extern "C" long long dc_med_scratch_bytes64(long long n);
+
+// med_dataset_double (:3564-3590): the exact left-to-right double sum by the binade-transducer kernels of
+// dc_aux.hip (every CU; the binade crossings one lane at a time)
 extern "C" int dc64_med_device(const void* d_x, long long n, double* mean_out, int* type_out) {
     hipStream_t st;
     int rc = ensure64(&st);
     if (rc) return rc;
     if (n <= 0) return dc_set_error(DC_ERR_ARG, "dc64_med_device: n must be > 0");
-    hipLaunchKernelGGL(med_kernel, dim3(1), dim3(1024), 0, st, (const double*)d_x, n, C64.d_f + 1, C64.d_i);
-    H64(hipGetLastError());
+    const size_t need = (size_t)dc_med_scratch_bytes64(n);
+    if (C64.med_cap < need) {
+        if (C64.med_scr) H64(hipFree(C64.med_scr));
+        C64.med_scr = nullptr;
+        C64.med_cap = 0;
+        H64(hipMalloc(&C64.med_scr, need + need / 8));
+        C64.med_cap = need + need / 8;
+    }
+    if (dc_launch_med64((const double*)d_x, n, C64.med_scr, C64.d_f + 1, C64.d_i, st))
+        return dc_set_error(DC_ERR_HIP, "dc64_med_device: launch failed");
     H64(hipMemcpyAsync(C64.h + 4, C64.d_f + 1, 8, hipMemcpyDeviceToHost, st));
     H64(hipMemcpyAsync(C64.h + 5, C64.d_i, 4, hipMemcpyDeviceToHost, st));
     H64(hipStreamSynchronize(st));

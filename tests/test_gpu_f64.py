@@ -1,6 +1,7 @@
 """GPU parity of the DOUBLE codecs (dc_f64.hip through the reference C ABI
 myCompress_bitwise_double* / myDecompress_bitwise_double*, impl/dataCompression.c:355-3308) against the
 compiled reference's golden vectors, the reference's double KATs and the CPU oracle.  Bit-exact."""
+import ctypes as C
 import hashlib
 import os
 
@@ -224,3 +225,36 @@ def test_ct1_double_large(dc, oracle):
     assert np.array_equal(raw.view(np.uint64), r2.view(np.uint64)) and codes == c2 and np.array_equal(pos, p2)
     d = dc.ct1_decompress64(raw, codes, pos, x.size)
     assert np.array_equal(d.view(np.uint64), oracle.bytewise_decompress64(raw, codes, pos, x.size).view(np.uint64))
+
+
+@pytest.mark.parametrize("kind,n", [("u10", 1 << 24), ("u10", 1 << 26), ("ramp", 1 << 21), ("signed", 1 << 20),
+                                    ("nan", 100003), ("zeros", 1 << 22), ("wide", 1 << 20), ("tiny", 1 << 20)])
+def test_med64_exact_parallel(dc, oracle, kind, n):
+    """med_dataset_double's left-to-right double sum (impl/dataCompression.c:3564-3590) by the binade-
+    transducer kernels (dc_aux.hip) must equal the serial sum bit for bit (mean and type)."""
+    import torch
+    rs = np.random.RandomState(n % 997)
+    if kind == "u10":
+        x = oracle.gen_u10_64(n)
+    elif kind == "ramp":
+        x = np.arange(n, dtype=np.float64) * 0.0005
+    elif kind == "signed":
+        x = rs.randn(n) * 3
+    elif kind == "nan":
+        x = oracle.gen_u10_64(n)
+        x[n // 3] = np.nan
+    elif kind == "zeros":
+        x = np.zeros(n)
+        x[::7919] = -0.0
+    elif kind == "wide":
+        x = rs.rand(n) * np.exp2(rs.randint(-200, 200, n).astype(np.float64))
+    else:
+        x = rs.rand(n) * 1e-300
+    d = torch.from_numpy(np.ascontiguousarray(x, np.float64)).cuda()
+    torch.cuda.synchronize()
+    mean = C.c_double(0)
+    t = C.c_int(0)
+    dc.check(dc.L.dc64_med_device(C.c_void_p(d.data_ptr()), n, C.byref(mean), C.byref(t)), "dc64_med_device")
+    om, ot = oracle.med64(x)
+    assert np.array_equal(np.float64(mean.value).view(np.uint64), np.float64(om).view(np.uint64)), (mean.value, om)
+    assert t.value == ot
