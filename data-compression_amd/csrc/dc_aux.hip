@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <algorithm>
 #include "dc_shared.h"
 
 namespace dc {
@@ -28,16 +29,26 @@ __device__ __forceinline__ MinKey min_pick(MinKey a, MinKey b) {
     return a.i <= b.i ? a : b;                           // equal (incl. +0 == -0): first occurrence
 }
 
+// per-workgroup (min, first index) over x[1..n): float4 loads, grid-stride; min_pick is a total order
+// (value, then index), so the partials can be combined in any order
 __global__ __launch_bounds__(256) void min_partial_kernel(const float* __restrict__ x, long long n,
                                                           float* __restrict__ pv, long long* __restrict__ pi) {
     __shared__ float sv[256];
     __shared__ long long si[256];
     MinKey m = {__int_as_float(0x7fc00000), (long long)1 << 62};
-    for (long long i = 1 + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (long long)gridDim.x * blockDim.x) {
-        MinKey k = {x[i], i};
-        m = min_pick(m, k);
+    const long long n4 = ((reinterpret_cast<uintptr_t>(x) & 15u) == 0) ? (n >> 2) : 0;
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (long long)gridDim.x * blockDim.x) {
+        const float4 v = x4[q];
+        const long long i = 4 * q;
+        if (i > 0) m = min_pick(m, MinKey{v.x, i});          // element 0 is the reference's start value
+        m = min_pick(m, MinKey{v.y, i + 1});
+        m = min_pick(m, MinKey{v.z, i + 2});
+        m = min_pick(m, MinKey{v.w, i + 3});
     }
+    for (long long i = max(4 * n4, 1ll) + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        m = min_pick(m, MinKey{x[i], i});
     sv[threadIdx.x] = m.v; si[threadIdx.x] = m.i;
     __syncthreads();
     for (int s = 128; s > 0; s >>= 1) {
@@ -51,15 +62,30 @@ __global__ __launch_bounds__(256) void min_partial_kernel(const float* __restric
     if (threadIdx.x == 0) { pv[blockIdx.x] = sv[0]; pi[blockIdx.x] = si[0]; }
 }
 
-__global__ void min_final_kernel(const float* __restrict__ x, const float* __restrict__ pv,
-                                 const long long* __restrict__ pi, int nparts, float* __restrict__ out_min) {
-    if (threadIdx.x != 0) return;
+__global__ __launch_bounds__(256) void min_final_kernel(const float* __restrict__ x, const float* __restrict__ pv,
+                                                        const long long* __restrict__ pi, int nparts,
+                                                        float* __restrict__ out_min) {
+    __shared__ float sv[256];
+    __shared__ long long si[256];
     MinKey m = {__int_as_float(0x7fc00000), (long long)1 << 62};
-    for (int p = 0; p < nparts; p++) { MinKey k = {pv[p], pi[p]}; m = min_pick(m, k); }
-    const float x0 = x[0];
-    float r = x0;                                        // min = data[0]; later strictly smaller wins
-    if (!(m.v != m.v) && m.v < x0) r = m.v;
-    *out_min = r;
+    for (int p = threadIdx.x; p < nparts; p += 256) m = min_pick(m, MinKey{pv[p], pi[p]});
+    sv[threadIdx.x] = m.v; si[threadIdx.x] = m.i;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            MinKey a = {sv[threadIdx.x], si[threadIdx.x]}, b = {sv[threadIdx.x + s], si[threadIdx.x + s]};
+            const MinKey r = min_pick(a, b);
+            sv[threadIdx.x] = r.v; si[threadIdx.x] = r.i;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const float mv = sv[0];
+        const float x0 = x[0];
+        float r = x0;                                        // min = data[0]; later strictly smaller wins
+        if (!(mv != mv) && mv < x0) r = mv;
+        *out_min = r;
+    }
 }
 
 __global__ __launch_bounds__(256) void sub_min_kernel(const float* __restrict__ x, long long n,
@@ -683,9 +709,9 @@ __global__ __launch_bounds__(256) void ham_syndrome_kernel(const uint8_t* __rest
 extern "C" int dc_launch_to_small(const float* x, long long n, float* y, float* part_v, long long* part_i,
                                   float* d_min, hipStream_t st) {
     if (n <= 0) return 0;
-    const int nparts = 256;
+    const int nparts = (int)std::min<long long>(DC_MIN_PARTS, std::max<long long>(1, n / 4096));
     hipLaunchKernelGGL(min_partial_kernel, dim3(nparts), dim3(256), 0, st, x, n, part_v, part_i);
-    hipLaunchKernelGGL(min_final_kernel, dim3(1), dim3(64), 0, st, x, part_v, part_i, nparts, d_min);
+    hipLaunchKernelGGL(min_final_kernel, dim3(1), dim3(256), 0, st, x, part_v, part_i, nparts, d_min);
     if (y) {
         long long g = (n / 4 + 255) / 256;
         if (g > 2048) g = 2048;

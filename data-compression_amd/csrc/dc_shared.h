@@ -53,6 +53,7 @@ typedef struct DecBufs { /* decoder metadata, sized for the maximum chunk count 
     uint32_t* tmap;      /* [group][4]  tile record: P_0 mask, n_0 | x_0<<16 | tile exit<<24, rest count */
     uint32_t* tentry;    /* [group] true entry of the tile's first chunk | its token count << 8 */
     unsigned long long* tbase;   /* [group] first token index of the tile */
+    uint64_t* tflag;     /* [group] token-count look-back: status<<62 | epoch<<40 | tokens (1 aggregate, 2 inclusive) */
     uint8_t* entry;
     unsigned long long* tokoff;
     uint16_t* pend;
@@ -117,6 +118,7 @@ long long dc_decode_group(void);
 
 int dc_launch_to_small(const float* x, long long n, float* y, float* part_v, long long* part_i, float* d_min,
                        dc_hip_stream st);
+#define DC_MIN_PARTS 2048                /* toSmallDataset: per-workgroup minima combined by min_final */
 int dc_launch_med(const float* x, long long n, float s_init, void* scratch, float* d_mean, int* d_type, float* d_sum,
                   float* d_max, dc_hip_stream st);
 long long dc_med_scratch_bytes(long long n);
