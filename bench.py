@@ -402,6 +402,8 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
     ext = torch.cuda.ExternalStream(L.L.dc_get_stream())
     idx0 = C.rank * n
 
+    slow = [False]                # the stream needs the decoder's exact slow path: finish inside the step
+
     def step(ev=None):
         if ev:
             ev[0].record(ext)
@@ -411,6 +413,8 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
             ev[1].record(ext)
         L.decode_device(ct, stream.data_ptr(), -1, n, out.data_ptr(), type_=typ, mask17=mask17,
                         d_nbits=d_nbits.data_ptr(), max_bytes=cap)
+        if slow[0]:
+            L.decode_finish()                         # the exact slow path, timed (host-synchronised)
         if ev:
             ev[2].record(ext)
 
@@ -420,6 +424,7 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
         step()
         warm_status |= L.decode_status()
         L.decode_finish()                             # completes a slow path if one was needed
+    slow[0] = warm_status != 0
     nbits = L.encode_result()
     nbytes = (nbits + 7) // 8
 
@@ -495,7 +500,8 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
     L.L.dc_timing_enable(0)
     kavg = kms.mean(axis=0)
     res = {"nbits": int(nbits), "nbytes": int(nbytes), "wall": wall, "enc_ms": enc_ms, "dec_ms": dec_ms,
-           "kavg": kavg, "status": int(status), "warm_status": int(warm_status), "resends": resends[0]}
+           "kavg": kavg, "status": int(status | warm_status), "warm_status": int(warm_status), "resends": resends[0],
+           "slow_path_timed": slow[0]}
 
     if pipelined and ber <= 0:
         # the same K steps pipelined (encode k+1 || decode k, two stream buffers), reported beside value
@@ -593,6 +599,7 @@ def line_for(C, W, R, steps):
     return {"value": round(C.world * 4.0 * n / (ms * 1e-3) / 1e9, 3), "ms_per_step": round(ms, 4),
             "stream_bytes": int(nbytes), "ratio": round(4.0 * n / max(nbytes, 1), 4), "fast_path": R["status"] == 0,
             "decoder_status": R["status"],
+            "slow_path_in_timed_step": bool(R.get("slow_path_timed", False)),
             "dominant": {"kernel": dname, "avg_launch_ms": round(dms, 4), "achieved_GBs": round(ach, 1),
                          "frac": round(ach / HBM_PEAK_GBS, 4)},
             "step_roofline_frac": round(step_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -632,9 +639,10 @@ def main():
     R = run_codec(C, W, args.steps, args.warmup, pipelined=not args.no_pipelined, ber=args.ber, check=args.check)
     n, nbytes = W["n"], R["nbytes"]
     main_line = line_for(C, W, R, args.steps)
-    if R["status"] != 0:
+    if R["status"] != 0 and not R["slow_path_timed"]:
         # a timed step left the decoder's fast path: its exact slow path ran outside the timed region,
-        # so the time is not the codec's -- refuse to report it
+        # so the time is not the codec's -- refuse to report it (streams that need the slow path from the
+        # warm-up on run it inside every timed step and are reported with fast_path false)
         print(f"bench.py: decoder status 0x{R['status']:x} in the timed steps (slow path not timed)", file=sys.stderr)
         sys.exit(1)
     kernels = kernel_table(ct, n, nbytes, R["kavg"])
@@ -679,7 +687,8 @@ def main():
         "phases_ms": {"encode": round(R["enc_ms"], 4), "decode": round(R["dec_ms"], 4),
                       "med_dataset_s": round(W["t_med"], 4)},
         "pipeline_roofline_frac": round((8.0 * n + 2 * nbytes) / ((R["enc_ms"] + R["dec_ms"]) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-        "decoder_fast_path": True,
+        "decoder_fast_path": R["status"] == 0,
+        "slow_path_in_timed_step": bool(R["slow_path_timed"]),
     }
     if "pipelined" in R:
         res["pipelined"] = R["pipelined"]
