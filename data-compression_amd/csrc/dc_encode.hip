@@ -641,24 +641,14 @@ __global__ __launch_bounds__(ENC_TPB) void encode_fused_kernel(
         default: return -2;                                                                        \
     }
 
-// persistent write kernel: as many workgroups as are resident at once
-static unsigned write_grid(int ct) {
-    static unsigned cache[12];
-    const int ci = (ct > 0 && ct < 12) ? ct : 0;
-    if (cache[ci]) return cache[ci];
-    int dev = 0, ncu = 256, per = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    const void* f = ct == 5 ? (const void*)encode_write_kernel<5> : ct == 6 ? (const void*)encode_write_kernel<6>
-                  : ct == 7 ? (const void*)encode_write_kernel<7> : (const void*)encode_write_kernel<11>;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, ENC_TPB, 0) != hipSuccess || per < 1) per = 1;
-    cache[ci] = (unsigned)(per * ncu);
-    // one workgroup per tile measured best (write 165 -> 159 us against the resident-count grid, 2048 and
-    // 4096 in between); DC_WRITE_GRID overrides for sweeps
-    cache[ci] = 1u << 30;
-    const char* e = getenv("DC_WRITE_GRID");
-    if (e && atoi(e) > 0) cache[ci] = (unsigned)atoi(e);
-    return cache[ci];
+// write kernel grid: one workgroup per tile (measured best: write 165 -> 159 us against a resident-count
+// persistent grid, 2048 and 4096 in between); DC_WRITE_GRID overrides it for sweeps
+static unsigned write_grid() {
+    static unsigned g = [] {
+        const char* e = getenv("DC_WRITE_GRID");
+        return (e && atoi(e) > 0) ? (unsigned)atoi(e) : (1u << 30);
+    }();
+    return g;
 }
 
 static unsigned fused_grid(int ct) {
@@ -700,7 +690,7 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
     dc_mark_phase(0, stream);
     // count: one workgroup per tile (a persistent count grid with prefetch measured slower)
     const unsigned gc = ntiles;                                    // count: one workgroup per tile
-    const unsigned gw = std::min<unsigned>(ntiles, write_grid(P->ct));
+    const unsigned gw = std::min<unsigned>(ntiles, write_grid());
     DC_ENC_DISPATCH(encode_count_kernel, dim3(gc), dim3(256), 0, stream, x, n, idx0, *P, tbits,
                     (long long)ntiles, err);
     dc_mark_phase(1, stream);
