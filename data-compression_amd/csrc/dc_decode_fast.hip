@@ -823,10 +823,15 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
         __syncthreads();                                   // resolution arrays are dead from here
         S.u.k.kd[0][c] = (uint8_t)k1; S.u.k.kd[1][c] = (uint8_t)k2; S.u.k.kd[2][c] = (uint8_t)k3;
         S.u.k.fv[0][c] = f1; S.u.k.fv[1][c] = f2; S.u.k.fv[2][c] = f3;
-        __syncthreads();
+        // the scan only serves pending prefixes and a tile whose last chunk ends on symbolic history: when
+        // no chunk left a prefix pending and the last chunk's history is concrete, F_last is that history
+        const int lastc = nact - 1;
+        const bool anypend = __syncthreads_or(act && pend > 0);
+        const bool noscan = !anypend && S.u.k.kd[0][lastc] == 0 && S.u.k.kd[1][lastc] == 0 && S.u.k.kd[2][lastc] == 0;
+        const int fsrc = noscan ? lastc : GROUP - 1;        // where the tile's outgoing history is read
         STAMP(10);
         // ---- inclusive scan of carry functions: F_c = f_c o ... o f_0
-        for (int d = 1; d < GROUP; d <<= 1) {
+        for (int d = 1; d < (noscan ? 1 : GROUP); d <<= 1) {
             int kk[3];
             float vv[3];
 #pragma unroll
@@ -859,13 +864,13 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
             if (needs) S.need = 1;
             if (cx) S.cplx = 1;
         }
-        const int tk0 = S.u.k.kd[0][GROUP - 1], tk1 = S.u.k.kd[1][GROUP - 1], tk2 = S.u.k.kd[2][GROUP - 1];
+        const int tk0 = S.u.k.kd[0][fsrc], tk1 = S.u.k.kd[1][fsrc], tk2 = S.u.k.kd[2][fsrc];
         if (c == 0) {
             for (int i = 0; i < 3; i++)
-                st_relaxed(&D.hist[t * 6 + i], hpack(1, epoch, S.u.k.kd[i][GROUP - 1], S.u.k.fv[i][GROUP - 1]));
+                st_relaxed(&D.hist[t * 6 + i], hpack(1, epoch, S.u.k.kd[i][fsrc], S.u.k.fv[i][fsrc]));
             if (tk0 == 0 && tk1 == 0 && tk2 == 0)
                 for (int i = 0; i < 3; i++)
-                    st_relaxed(&D.hist[t * 6 + 3 + i], hpack(2, epoch, 0, S.u.k.fv[i][GROUP - 1]));
+                    st_relaxed(&D.hist[t * 6 + 3 + i], hpack(2, epoch, 0, S.u.k.fv[i][fsrc]));
             if (tk0 == 4 || tk1 == 4 || tk2 == 4) S.cplx = 1;
         }
         __syncthreads();
@@ -916,7 +921,7 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
             for (int i = 0; i < 3; i++)
                 st_relaxed(&D.hist[t * 6 + 3 + i],
                            defer ? hpack(2, epoch, 4, 0.0f)
-                                 : hpack(2, epoch, 0, kk[i] == 0 ? S.u.k.fv[i][GROUP - 1] : S.tin[kk[i] - 1]));
+                                 : hpack(2, epoch, 0, kk[i] == 0 ? S.u.k.fv[i][fsrc] : S.tin[kk[i] - 1]));
         }
         // deferred: prefixes that depend on the shard's incoming values wait for dc_decode_shard_fix
         const bool dchunk = defer && act && pend > 0 &&
