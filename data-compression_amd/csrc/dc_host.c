@@ -75,6 +75,7 @@ typedef struct {
     int* d_i;                        /* [0] type */
     uint32_t* d_crctab; uint32_t* d_x2n; uint32_t* d_crcparts; long long crcparts_cap; uint32_t* d_crc;
     unsigned long long* d_ham;
+    unsigned long long* d_ratio;     /* ratio estimators: [0] bits [1] -1.0 flag */
     /* CT1 byte-wise codec */
     void* c1_scr; size_t c1_scr_cap;
     void* c1_in; size_t c1_in_cap;
@@ -1328,4 +1329,151 @@ float* myDecompress(float array_float[], char array_char[], int array_char_displ
     if (hipMemcpy(out, G.c1_out, sizeof(float) * n, hipMemcpyDeviceToHost) != hipSuccess)
         abi_fail(fn, seterr(DC_ERR_HIP, "D2H copy failed"));
     return out;
+}
+
+/* ============================================================================================
+ * CT2 / CT3 compression-ratio estimators (impl/dataCompression.c:3622-3739, :4121-5219) on the GPU
+ * (dc_ratio.hip): a data-parallel pass sums every element's bits (the history is the original data);
+ * an input holding -1.0 (the reference's empty-history sentinel) is re-estimated by one lane running the
+ * reference loop; the area estimators pack per-element sizes greedily in one lane.  The returned float
+ * is formed with the reference's own integer / float types.
+ * ========================================================================================== */
+static int ratio_scratch(void) {
+    if (!G.d_ratio) HIPCHK(hipMalloc((void**)&G.d_ratio, 64));
+    return DC_OK;
+}
+
+/* bits (or, for the area mode, 512-bit blocks) of x[0..n) (host) under estimator `mode` */
+static int ratio_run(int is_double, int mode, const void* x, long long n, unsigned long long* out) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    *out = 0;
+    if (n <= 0) return DC_OK;
+    const size_t esz = is_double ? 8 : 4;
+    if ((rc = ratio_scratch()) || (rc = grow(&G.d_a, &G.d_a_cap, (size_t)n * esz + 64))) return rc;
+    if (mode == 4 && (rc = grow(&G.d_b, &G.d_b_cap, (size_t)n + 64))) return rc;
+    HIPCHK(hipMemcpyAsync(G.d_a, x, (size_t)n * esz, hipMemcpyHostToDevice, G.st));
+    HIPCHK(hipMemsetAsync(G.d_ratio, 0, 16, G.st));
+    const double bound = absErrBound;
+    const double tle = is_double ? bound : (double)thr_le(bound);
+    if (dc_launch_ratio(is_double, mode, G.d_a, n, bound_binary(bound), tle, G.d_ratio, (unsigned*)(G.d_ratio + 1),
+                        (uint8_t*)G.d_b, G.st))
+        return seterr(DC_ERR_HIP, "ratio launch failed");
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[10], G.d_ratio, 16, hipMemcpyDeviceToHost, G.st));
+    HIPCHK(hipStreamSynchronize(G.st));
+    const int neg1 = (int)(G.h_scratch[11] & 1u);
+    if (mode >= 2 && neg1) {                 /* the -1 history sentinel: the reference loop, one lane */
+        if (dc_launch_ratio_serial(is_double, mode, G.d_a, n, bound_binary(bound), tle, G.d_ratio, G.st))
+            return seterr(DC_ERR_HIP, "ratio launch failed");
+    } else if (mode == 4) {
+        if (dc_launch_ratio_area((const uint8_t*)G.d_b, n, G.d_ratio, G.st)) return seterr(DC_ERR_HIP, "ratio launch failed");
+    } else {
+        *out = G.h_scratch[10];
+        return DC_OK;
+    }
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[10], G.d_ratio, 8, hipMemcpyDeviceToHost, G.st));
+    HIPCHK(hipStreamSynchronize(G.st));
+    *out = G.h_scratch[10];
+    return DC_OK;
+}
+
+/* calCompressRatio_bitwise_* (:3622-3739): int bits_after_compress (wraps as the reference's int) over
+ * sizeof(T)*8*num */
+static float ratio_bitwise(int is_double, int mode, const void* x, int num, const char* fn, size_t wbytes) {
+    unsigned long long b = 0;
+    const int rc = ratio_run(is_double, mode, x, num, &b);
+    if (rc) { abi_fail(fn, rc); return 0.0f; }
+    const int bits = (int)(uint32_t)b;
+    return (float)bits / (wbytes * 8 * (size_t)num);
+}
+float calCompressRatio_bitwise_float(float data[], int num) {
+    return ratio_bitwise(0, 0, data, num, "calCompressRatio_bitwise_float", sizeof(float));
+}
+float calCompressRatio_bitwise_double(double data[], int num) {
+    return ratio_bitwise(1, 0, data, num, "calCompressRatio_bitwise_double", sizeof(double));
+}
+float calCompressRatio_bitwise_double2(float data[], int num) {
+    return ratio_bitwise(0, 1, data, num, "calCompressRatio_bitwise_double2", sizeof(double));
+}
+
+/* sz / nolossy: long compressed_bits / long origin_bits (:4636-5219) */
+static float ratio_bits(int is_double, int mode, const void* x, int num, const char* fn) {
+    unsigned long long b = 0;
+    const int rc = ratio_run(is_double, mode, x, num, &b);
+    if (rc) { abi_fail(fn, rc); return 0.0f; }
+    const long origin = (long)num * (long)(is_double ? 64 : 32);
+    const long cb = mode == 4 ? (long)b * 512 : (long)b;
+    return (float)cb / origin;
+}
+float calcCompressionRatio_sz_float(float data[], int num) { return ratio_bits(0, 2, data, num, "calcCompressionRatio_sz_float"); }
+float calcCompressionRatio_sz_double(double data[], int num) { return ratio_bits(1, 2, data, num, "calcCompressionRatio_sz_double"); }
+float calcCompressionRatio_nolossy_performance_float(float data[], int num) {
+    return ratio_bits(0, 3, data, num, "calcCompressionRatio_nolossy_performance_float");
+}
+float calcCompressionRatio_nolossy_performance_double(double data[], int num) {
+    return ratio_bits(1, 3, data, num, "calcCompressionRatio_nolossy_performance_double");
+}
+float calcCompressionRatio_nolossy_area_float(float data[], int num) {
+    return ratio_bits(0, 4, data, num, "calcCompressionRatio_nolossy_area_float");
+}
+float calcCompressionRatio_nolossy_area_double(double data[], int num) {
+    return ratio_bits(1, 4, data, num, "calcCompressionRatio_nolossy_area_double");
+}
+
+/* the Himeno variants (:4121-4635) walk plane ijk = v of p[MIMAX][MJMAX][MKMAX] in
+ * transform_3d_array_to_1d_array order: the plane, then the flat estimator */
+static float* himeno_plane(float data[MIMAX][MJMAX][MKMAX], int ijk, int v, int imax, int jmax, int kmax, int* n) {
+    int A = 0, B = 0;
+    if (plane_dims(ijk, imax, jmax, kmax, &A, &B)) return NULL;
+    *n = A * B;
+    return transform_3d_array_to_1d_array(data, ijk, v, imax, jmax, kmax);
+}
+float calcCompressionRatio_himeno_sz(float data[MIMAX][MJMAX][MKMAX], int ijk, int v, int imax, int jmax, int kmax) {
+    int n = 0;
+    float* p = himeno_plane(data, ijk, v, imax, jmax, kmax, &n);
+    if (!p) { abi_fail("calcCompressionRatio_himeno_sz", DC_ERR_ARG); return 0.0f; }
+    const float r = calcCompressionRatio_sz_float(p, n);
+    free(p);
+    return r;
+}
+float calcCompressionRatio_himeno_nolossy_performance(float data[MIMAX][MJMAX][MKMAX], int ijk, int v, int imax, int jmax,
+                                                       int kmax) {
+    int n = 0;
+    float* p = himeno_plane(data, ijk, v, imax, jmax, kmax, &n);
+    if (!p) { abi_fail("calcCompressionRatio_himeno_nolossy_performance", DC_ERR_ARG); return 0.0f; }
+    const float r = calcCompressionRatio_nolossy_performance_float(p, n);
+    free(p);
+    return r;
+}
+float calcCompressionRatio_himeno_nolossy_area(float data[MIMAX][MJMAX][MKMAX], int ijk, int v, int imax, int jmax,
+                                               int kmax) {
+    int n = 0;
+    float* p = himeno_plane(data, ijk, v, imax, jmax, kmax, &n);
+    if (!p) { abi_fail("calcCompressionRatio_himeno_nolossy_area", DC_ERR_ARG); return 0.0f; }
+    const float r = calcCompressionRatio_nolossy_area_float(p, n);
+    free(p);
+    return r;
+}
+/* :4121-4279: the CT1 byte-wise split of the plane (raw floats vs 2-bit codes) on the CT1 kernels */
+float calcCompressionRatio_himeno_ij_ik_jk(float data[MIMAX][MJMAX][MKMAX], int ijk, int v, int imax, int jmax, int kmax) {
+    const char* fn = "calcCompressionRatio_himeno_ij_ik_jk";
+    int n = 0;
+    float* p = himeno_plane(data, ijk, v, imax, jmax, kmax, &n);
+    if (!p) { abi_fail(fn, DC_ERR_ARG); return 0.0f; }
+    int rc = ensure_init();
+    long long nraw = 0;
+    if (!rc && n > 0) {
+        if ((rc = grow(&G.c1_in, &G.c1_in_cap, (size_t)n * 4 + 64)) || (rc = grow(&G.c1_out, &G.c1_out_cap, (size_t)n * 4 + 64)) ||
+            (rc = grow(&G.c1_codes, &G.c1_codes_cap, (size_t)n + 64)) ||
+            (rc = grow(&G.c1_pos, &G.c1_pos_cap, (size_t)n * 4 + 64))) {
+        } else if (hipMemcpyAsync(G.c1_in, p, (size_t)n * 4, hipMemcpyHostToDevice, G.st) != hipSuccess) {
+            rc = seterr(DC_ERR_HIP, "H2D copy failed");
+        } else {
+            rc = dc_ct1_encode_device(G.c1_in, n, G.c1_out, G.c1_codes, G.c1_pos, &nraw);
+        }
+    }
+    free(p);
+    if (rc) { abi_fail(fn, rc); return 0.0f; }
+    const long long nchar = n - nraw;
+    return (float)((size_t)nchar * 2 + (size_t)nraw * sizeof(float) * 8) / ((size_t)(nchar + nraw) * sizeof(float) * 8);
 }

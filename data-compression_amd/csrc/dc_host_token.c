@@ -218,10 +218,14 @@ double decompress_bitwise_double_mask(char* bits, int bits_num, double before_va
     return d_of(masked_pattern(bits, bits_num, type, mask, 20, 12, 64));
 }
 
-void getDoubleBin(double num, char bin[]) {            /* :5232-5242 (digits 0/1, not chars) */
+/* :5232-5242 (digits 0/1, not chars).  The reference reads the double through an int* and tests
+ * (*f) & (1 << (63-i)); as it compiles on x86-64 (shift counts taken mod 32) the 64 digits are the low
+ * 32-bit word twice, which the ratio estimators (c:5024, :5110, :5180) then read. */
+void getDoubleBin(double num, char bin[]) {
     uint64_t c;
     memcpy(&c, &num, 8);
-    for (int i = 0; i < 64; i++) bin[i] = (char)((c >> (63 - i)) & 1u);
+    const uint32_t lo = (uint32_t)c;
+    for (int i = 0; i < 64; i++) bin[i] = (char)((lo >> (31 - (i & 31))) & 1u);
 }
 
 /* ---- character-level Hamming SECDED (:5544-5855) ----------------------------------------------

@@ -239,6 +239,33 @@ void hamming_verify_bit(unsigned char* bits, char* c, int bytes, int r, char* v)
 /* h:156 c:5822 */
 void hamming_rectify_bit(unsigned char* bits, char* c, int bytes, int r, int error_bit_pos);
 
+/* ---- CT2 / CT3 compression-ratio estimators (GPU reductions, dc_ratio.hip): compressed / original bits
+ *      of the bit-wise raw tokens, the SZ-style prediction estimate and the lossless residual estimates -- */
+/* h:100 c:3702 */
+float calCompressRatio_bitwise_float(float data[], int num);
+/* h:101 c:3662 */
+float calCompressRatio_bitwise_double(double data[], int num);
+/* h:102 c:3622: the floats as doubles */
+float calCompressRatio_bitwise_double2(float data[], int num);
+/* h:103 c:4636 */
+float calcCompressionRatio_sz_float(float data[], int num);
+/* h:104 c:4928 */
+float calcCompressionRatio_sz_double(double data[], int num);
+/* h:105 c:4772 */
+float calcCompressionRatio_nolossy_performance_float(float data[], int num);
+/* h:106 c:5064 */
+float calcCompressionRatio_nolossy_performance_double(double data[], int num);
+/* h:107 c:4841 */
+float calcCompressionRatio_nolossy_area_float(float data[], int num);
+/* h:108 c:5133 */
+float calcCompressionRatio_nolossy_area_double(double data[], int num);
+/* h:109-112 c:4121-4635: the same on plane ijk = v of a Himeno array (transform_3d_array_to_1d_array order) */
+float calcCompressionRatio_himeno_ij_ik_jk(float data[MIMAX][MJMAX][MKMAX], int ijk, int v, int imax, int jmax, int kmax);
+float calcCompressionRatio_himeno_sz(float data[MIMAX][MJMAX][MKMAX], int ijk, int v, int imax, int jmax, int kmax);
+float calcCompressionRatio_himeno_nolossy_performance(float data[MIMAX][MJMAX][MKMAX], int ijk, int v, int imax, int jmax,
+                                                       int kmax);
+float calcCompressionRatio_himeno_nolossy_area(float data[MIMAX][MJMAX][MKMAX], int ijk, int v, int imax, int jmax, int kmax);
+
 /* h:132 c:5341 (NULL instead of exit(0) when the file cannot be opened) */
 float* readfrombinary_float(const char* file, int count);
 /* h:133 c:5362 */

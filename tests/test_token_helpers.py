@@ -240,3 +240,17 @@ def test_readfrombinary(tmp_path):
     assert np.array_equal(np.frombuffer(C.string_at(p, d.nbytes), np.float64), d)
     libc.free(p)
     assert O.readfrombinary_float(str(tmp_path / "missing").encode(), 4) is None
+
+
+def test_get_double_bin_vs_reference():
+    """getDoubleBin (c:5232-5242) as the reference compiles: the low 32-bit word, twice."""
+    R, O = _ref(1e-6), _ours(1e-6)
+    for L in (R, O):
+        L.getDoubleBin.argtypes = [C.c_double, C.c_char_p]
+    r = np.random.default_rng(3)
+    vals = [0.0, -0.0, 1.0, -2.0, 1e-3, 123.456, 1.0 + 2.0 ** -21, 2.0 ** -30 + 1] + list(r.normal(0, 50, 200))
+    for v in vals:
+        a, b = C.create_string_buffer(64), C.create_string_buffer(64)
+        R.getDoubleBin(float(v), a)
+        O.getDoubleBin(float(v), b)
+        assert a.raw == b.raw, v
