@@ -35,7 +35,7 @@ constexpr int UNK = 63;
 
 
 __global__ void plan_kernel(Plan* plan, const unsigned long long* dev_nbits, unsigned long long host_nbits,
-                            long long max_chunks) {
+                            long long max_chunks, int ct, long long num) {
     const unsigned long long nbits = dev_nbits ? *dev_nbits : host_nbits;
     Plan p;
     p.nbits = nbits;
@@ -44,6 +44,7 @@ __global__ void plan_kernel(Plan* plan, const unsigned long long* dev_nbits, uns
     if (nc > max_chunks) nc = max_chunks;
     p.nchunks = nc;
     p.ngroups = (nc + GROUP - 1) / GROUP;
+    p.runs = runs_mode(ct, nbits, num);
     *plan = p;
 }
 
@@ -61,8 +62,20 @@ __device__ void walk_entry(const uint8_t* s, const Plan& pl, const Params& P, lo
     }
     BitReader A, Bp;
     A.init(s, pl.nbytes, cs + e);
-    Bp.init(s, pl.nbytes, cs);
     uint32_t ca = 0, cb = 0;
+    if (CT != 6 && pl.runs) {                                  // A alone to the chunk end, whole runs
+        while (A.pos < cend) {
+            const uint32_t t = A.peek();
+            const int k = (int)t < 0 ? run3(t, A.pos, cend) : 1;
+            A.skip(k > 1 ? 3 * k : token_len<CT>(t, P));
+            ca += k;
+        }
+        const long long x = A.pos - ce;
+        *out_exit = (x >= 0 && x < 32) ? (int)x : 0;
+        *out_cnt = ca;
+        return;
+    }
+    Bp.init(s, pl.nbytes, cs);
     while (A.pos < cend) {
         if (A.pos == Bp.pos) {
             *out_exit = pexit;
@@ -97,8 +110,15 @@ __global__ __launch_bounds__(256) void chunk_paths_kernel(const uint8_t* __restr
         while (br.pos < cend) {
             const long long r = br.pos - cs;
             if (r < 32) mask |= 1u << r;
-            br.skip(token_len<CT>(br.peek(), P));
-            n++;
+            const uint32_t t = br.peek();
+            if (CT != 6 && pl.runs && (int)t < 0 && r >= 32) {         // past the mask word: whole runs
+                const int k = run3(t, br.pos, cend);
+                br.skip(3 * k);
+                n += k;
+            } else {
+                br.skip(token_len<CT>(t, P));
+                n++;
+            }
         }
         const long long x = br.pos - ce;
         D.p_exit[c] = (uint8_t)((x >= 0 && x < 32) ? x : 0);
@@ -457,7 +477,7 @@ extern "C" int dc_launch_decode(const uint8_t* s, const unsigned long long* dev_
                                 const DecBufs* D, float* out, long long num, uint32_t epoch, int rounds,
                                 int fix_iters, hipStream_t st) {
     const long long max_groups = (max_chunks + GROUP - 1) / GROUP;
-    hipLaunchKernelGGL(plan_kernel, dim3(1), dim3(1), 0, st, D->plan, dev_nbits, host_nbits, max_chunks);
+    hipLaunchKernelGGL(plan_kernel, dim3(1), dim3(1), 0, st, D->plan, dev_nbits, host_nbits, max_chunks, P->ct, num);
     const int gchunks = (int)std::min<long long>((max_chunks + 255) / 256, g_grid);
     const int ggroups = (int)std::min<long long>((max_groups * 32 + 255) / 256, g_grid);
     DC_DISPATCH(P->ct, chunk_paths_kernel, dim3(gchunks), dim3(256), 0, st, s, *P, *D);

@@ -164,8 +164,10 @@ __device__ __forceinline__ void stage_tile(uint32_t* L, const uint8_t* s, long l
 // walk entry e of chunk c (LDS bits [cs, cend)) alongside P_c (whose first boundary in the chunk is
 // pmask's lowest bit); the reader that is behind steps.  Returns the exit relative to the next chunk
 // and the number of tokens starting in the chunk.
+template <int CT>
 __device__ __forceinline__ void walk_lds(const uint32_t* L, const uint8_t* tl, int cs, int cend, int e,
-                                         uint32_t pmask, int pexit, int pcnt, int* out_exit, int* out_cnt) {
+                                         uint32_t pmask, int pexit, int pcnt, int* out_exit, int* out_cnt,
+                                         bool runs) {
     if ((pmask >> e) & 1u) {
         *out_exit = pexit;
         *out_cnt = pcnt - __popc(pmask & ((1u << e) - 1u));
@@ -173,6 +175,20 @@ __device__ __forceinline__ void walk_lds(const uint32_t* L, const uint8_t* tl, i
     }
     Rd A, B;
     A.init(L, cs + e);
+    if (CT != 6 && runs) {                     // runs mode: A alone to the chunk end, whole runs per step
+        int ca = 0;
+        while (A.pos < cend) {
+            A.fetch(L);
+            const uint32_t tk = A.peek();
+            const int k = (int)tk < 0 ? run3i(tk, A.pos, cend) : 1;
+            A.step(k > 1 ? 3 * k : (int)tl[tk >> 23]);
+            ca += k;
+        }
+        const int x = A.pos - (cs + CHUNK_BITS);
+        *out_exit = (x >= 0 && x < 32) ? x : 0;
+        *out_cnt = ca;
+        return;
+    }
     B.init(L, cs + (pmask ? __ffs(pmask) - 1 : 32));
     int ca = 0, cb = 0;
     bool merged = false;
@@ -231,7 +247,7 @@ __device__ __forceinline__ bool lookup_entry(const ParseShared& S, int c, int e,
 }
 
 __device__ __forceinline__ Plan make_plan(const unsigned long long* dev_nbits, unsigned long long host_nbits,
-                                          long long max_chunks) {
+                                          long long max_chunks, int ct, long long num) {
     const unsigned long long nbits = dev_nbits ? *dev_nbits : host_nbits;
     Plan p;
     p.nbits = nbits;
@@ -240,6 +256,7 @@ __device__ __forceinline__ Plan make_plan(const unsigned long long* dev_nbits, u
     if (nc > max_chunks) nc = max_chunks;
     p.nchunks = nc;
     p.ngroups = (nc + GROUP - 1) / GROUP;
+    p.runs = runs_mode(ct, nbits, num);
     return p;
 }
 
@@ -248,9 +265,9 @@ __device__ __forceinline__ Plan make_plan(const unsigned long long* dev_nbits, u
 template <int CT>
 __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict__ s, Params P, DecBufs D,
                                                     const unsigned long long* dev_nbits, unsigned long long host_nbits,
-                                                    long long max_chunks) {
+                                                    long long max_chunks, long long num) {
     __shared__ ParseShared S;
-    const Plan pl = make_plan(dev_nbits, host_nbits, max_chunks);
+    const Plan pl = make_plan(dev_nbits, host_nbits, max_chunks, CT, num);
     if (blockIdx.x == 0 && threadIdx.x == 0) *D.plan = pl;
     const int c = threadIdx.x, lane = c & 63, wid = c >> 6;
     build_lut_len<CT>(S.tl, P, c, GROUP);                             // visible after the first barrier
@@ -276,7 +293,15 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
             Rd r;
             r.init(S.L, gc == 0 ? cs : cs - OV);
             const unsigned long long q0 = D.dbg ? __builtin_amdgcn_s_memtime() : 0;
-            while (r.pos < cs) { r.fetch(S.L); r.step(PLEN(r.peek())); }
+            if (CT != 6 && pl.runs) {
+                while (r.pos < cs) {
+                    r.fetch(S.L);
+                    const uint32_t tk = r.peek();
+                    r.step((int)tk < 0 ? 3 * run3i(tk, r.pos, cs) : PLEN(tk));
+                }
+            } else {
+                while (r.pos < cs) { r.fetch(S.L); r.step(PLEN(r.peek())); }
+            }
             if (D.dbg && t < 4096 && (c & 63) == 0)                  // per-wave cycles (diagnostic)
                 D.dbg[t * 16 + 12 + (c >> 6)] = (__builtin_amdgcn_s_memtime() - q0) << 16;
             const int pend = min(cs + 32, cend);                      // boundaries in the first word
@@ -286,10 +311,20 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
                 r.step(PLEN(r.peek()));
                 n++;
             }
-            while (r.pos < cend) {
-                r.fetch(S.L);
-                r.step(PLEN(r.peek()));
-                n++;
+            if (CT != 6 && pl.runs) {
+                while (r.pos < cend) {
+                    r.fetch(S.L);
+                    const uint32_t tk = r.peek();
+                    const int k = (int)tk < 0 ? run3i(tk, r.pos, cend) : 1;
+                    r.step(k > 1 ? 3 * k : PLEN(tk));
+                    n += k;
+                }
+            } else {
+                while (r.pos < cend) {
+                    r.fetch(S.L);
+                    r.step(PLEN(r.peek()));
+                    n++;
+                }
             }
             const int xx = r.pos - (cs + CHUNK_BITS);
             x = (xx >= 0 && xx < 32) ? xx : 0;
@@ -304,7 +339,7 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
             const int e = S.x[c - 1];
             if (!((pm >> e) & 1u)) {
                 int ex, cn;
-                walk_lds(S.L, S.tl, cs, cend, e, pm, x, n, &ex, &cn);
+                walk_lds<CT>(S.L, S.tl, cs, cend, e, pm, x, n, &ex, &cn, pl.runs);
                 S.ke[c * KMAX] = ((uint32_t)e << 16) | ((uint32_t)ex << 10) | (uint32_t)cn;
                 nk = 1;
             }
@@ -332,7 +367,7 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
                     need &= need - 1;
                     if (nk >= KMAX) { atomicOr(D.err, 64u); break; }
                     int ex, cn;
-                    walk_lds(S.L, S.tl, cs, cend, e, pm, x, n, &ex, &cn);
+                    walk_lds<CT>(S.L, S.tl, cs, cend, e, pm, x, n, &ex, &cn, pl.runs);
                     S.ke[c * KMAX + nk] = ((uint32_t)e << 16) | ((uint32_t)ex << 10) | (uint32_t)cn;
                     nk++;
                         added = 1;
@@ -487,7 +522,7 @@ __global__ __launch_bounds__(256) void tile_fix_kernel(const uint8_t* __restrict
     if (lane != 0) return;
     const int cend0 = (int)min((long long)CHUNK_BITS, rem);
     int ex, c0;
-    walk_lds(L, S.tl, 0, cend0, E, pm0, x0, n0, &ex, &c0);
+    walk_lds<CT>(L, S.tl, 0, cend0, E, pm0, x0, n0, &ex, &c0, pl.runs);
     const long long g0 = t * GROUP;
     int k = 1;
     uint32_t acc = 0;
@@ -506,7 +541,7 @@ __global__ __launch_bounds__(256) void tile_fix_kernel(const uint8_t* __restrict
         if (!lookup_global(D, gk, ex, &nx, &cn)) {
             const int cs = k * CHUNK_BITS;
             const int ce = (int)min((long long)(cs + CHUNK_BITS), rem);
-            walk_lds(L, S.tl, cs, ce, ex, D.p_mask[gk], D.p_exit[gk], D.p_cnt[gk], &nx, &cn);
+            walk_lds<CT>(L, S.tl, cs, ce, ex, D.p_mask[gk], D.p_exit[gk], D.p_cnt[gk], &nx, &cn, pl.runs);
         }
         D.entry[gk] = (uint8_t)ex;
         D.tokoff[gk] = acc;
@@ -1001,7 +1036,7 @@ extern "C" int dc_launch_decode_fast(const uint8_t* s, const unsigned long long*
     }();
     const int gparse = (int)std::min<long long>(max_groups > 0 ? max_groups : 1, parse_grid);
     dc_mark_phase(4, st);
-    DC_DISPATCH_F(P->ct, parse_kernel, dim3(gparse), dim3(GROUP), 0, st, s, *P, *D, dev_nbits, host_nbits, max_chunks);
+    DC_DISPATCH_F(P->ct, parse_kernel, dim3(gparse), dim3(GROUP), 0, st, s, *P, *D, dev_nbits, host_nbits, max_chunks, num);
     dc_mark_phase(5, st);
     DC_DISPATCH_F(P->ct, tile_fix_kernel, dim3((unsigned)((max_groups + 3) / 4 > 0 ? (max_groups + 3) / 4 : 1)), dim3(256), 0, st,
                   s, *P, *D);

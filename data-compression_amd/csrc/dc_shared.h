@@ -36,6 +36,7 @@ typedef struct Plan {    /* device-resident sizes of the stream being decoded */
     long long nbytes;
     long long nchunks;
     long long ngroups;
+    int runs;            /* mostly 3-bit codes (< 6 bits per value, CT 5/7/11): boundary walks step whole runs */
 } Plan;
 
 typedef struct DecBufs { /* decoder metadata, sized for the maximum chunk count */
