@@ -493,6 +493,16 @@ extern "C" int dc_launch_decode(const uint8_t* s, const unsigned long long* dev_
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// runs-mode streams the fast path could not chain (tiles entered off their P_0): the parse already left
+// every chunk's map of the entries its tile reaches (chunk 0: all 32), so only the composition is left;
+// the values then come from the fast decode kernel (dc_launch_decode_fast_resolved)
+extern "C" int dc_launch_resolve(long long max_chunks, const DecBufs* D, uint32_t epoch, hipStream_t st) {
+    const long long max_groups = (max_chunks + GROUP - 1) / GROUP;
+    const int gres = (int)std::min<long long>(max_groups, 512);
+    hipLaunchKernelGGL(resolve_kernel, dim3(gres > 0 ? gres : 1), dim3(256), 0, st, *D, epoch);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // extra closure rounds + re-resolve + decode (slow path after an unknown entry was reported)
 // slow path after an unresolved entry: complete maps for every chunk, re-resolve, re-decode
 extern "C" int dc_launch_decode_more(const uint8_t* s, long long max_chunks, const Params* P, const DecBufs* D,

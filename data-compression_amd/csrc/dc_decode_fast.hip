@@ -220,6 +220,7 @@ struct ParseShared {
     uint16_t n[GROUP];
     uint8_t x[GROUP], nk[GROUP], stdexit[GROUP], dev[GROUP];
     uint32_t wsum[GROUP / 64];
+    uint32_t x0m;                              // runs mode: exits of all 32 entries of chunk 0
     int texit;
 #ifdef DC_PARSE_PAD
     uint32_t occpad[DC_PARSE_PAD / 4];          // occupancy experiment: extra LDS per workgroup
@@ -330,8 +331,23 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
             x = (xx >= 0 && xx < 32) ? xx : 0;
         }
         S.pm[c] = pm; S.n[c] = (uint16_t)n; S.x[c] = (uint8_t)x;
+        if (c == 0) S.x0m = 0;
         __syncthreads();
         STAMP(2);
+
+        // ---- runs mode: the complete 32-entry map of chunk 0 (one lane per entry), so that a tile
+        // entered off P_0 (period-3 streams never resynchronise) can be resolved exactly by composing
+        // chunk maps (dc_launch_decode_resolve) instead of re-deriving every map
+        if (CT != 6 && pl.runs) {
+            if (c < 32) {
+                int ex, cn;
+                walk_lds<CT>(S.L, S.tl, OV, OV + (int)min((long long)CHUNK_BITS, rem), c, S.pm[0], S.x[0], S.n[0],
+                             &ex, &cn, true);
+                D.fullmap[t * 32 + c] = ((uint32_t)ex << 26) | (uint32_t)cn;
+                atomicOr(&S.x0m, 1u << ex);
+            }
+            __syncthreads();
+        }
 
         // ---- round 2: P_{c-1}'s exit into chunk c, where P_c has no boundary there (rare)
         int nk = 0;
@@ -359,6 +375,7 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
                 for (int k = 0; k < nk; k++) known |= 1u << (S.ke[c * KMAX + k] >> 16);
                 // exits of the predecessor's entries known at the end of the previous round
                 uint32_t emp = 1u << S.x[c - 1];
+                if (CT != 6 && pl.runs && c == 1) emp |= S.x0m;
                 const int nkp = S.nkr[pp][c - 1];
                 for (int k = 0; k < nkp; k++) emp |= 1u << ((S.ke[(c - 1) * KMAX + k] >> 10) & 63u);
                 uint32_t need = emp & ~known;
@@ -447,7 +464,15 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
             D.p_cnt[gc] = (uint16_t)n;
             D.p_mask[gc] = pm;
             D.cmeta[gc] = (uint32_t)scnt | ((uint32_t)sex << 10) | ((uint32_t)nk << 16) | ((ok ? 1u : 0u) << 20);
-            for (int k = 0; k < nk; k++) D.map[gc * 32 + k] = S.ke[c * KMAX + k];
+            // extra entries in the exact path's format (map by entry + known mask), which resolve_kernel reads
+            uint32_t kn = 0;
+            for (int k = 0; k < nk; k++) {
+                const uint32_t v = S.ke[c * KMAX + k];
+                const int e = (int)(v >> 16);
+                kn |= 1u << e;
+                D.map[gc * 32 + e] = (((v >> 10) & 63u) << 26) | (v & 1023u);
+            }
+            D.known[gc] = c == 0 ? 0u : kn;
         }
         __syncthreads();
         STAMP(7);
@@ -458,10 +483,10 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
 __device__ __forceinline__ bool lookup_global(const DecBufs& D, long long gc, int e, int* ex, int* cn) {
     const uint32_t pm = D.p_mask[gc];
     if ((pm >> e) & 1u) { *ex = D.p_exit[gc]; *cn = D.p_cnt[gc] - __popc(pm & ((1u << e) - 1u)); return true; }
-    const int nk = (int)((D.cmeta[gc] >> 16) & 15);
-    for (int k = 0; k < nk; k++) {
-        const uint32_t v = D.map[gc * 32 + k];
-        if ((int)(v >> 16) == e) { *ex = (int)((v >> 10) & 63); *cn = (int)(v & 1023); return true; }
+    if ((D.known[gc] >> e) & 1u) {
+        const uint32_t v = D.map[gc * 32 + e];
+        *ex = (int)(v >> 26); *cn = (int)(v & 0x3FFFFFFu);
+        return true;
     }
     return false;
 }
@@ -716,6 +741,9 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
     __shared__ DecodeShared S;
     const Plan pl = *D.plan;
     const int c = threadIdx.x;
+    // a runs-mode stream whose tile chain failed (tile_fix reported an unknown entry) is resolved exactly
+    // by dc_decode_finish (resolve_kernel, then this kernel again): nothing to decode now
+    if (pl.runs && (__hip_atomic_load(D.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 8u)) return;
     build_lut<CT>(S.T, P, c, GROUP);                                  // visible after the first barrier
     while (true) {
         if (c == 0) S.tile = (long long)atomicAdd(&D.ctr[4], 1u);
@@ -1024,6 +1052,33 @@ static int decode_grid(int ct) {
     const char* e = getenv("DC_DECODE_GRID");                 // experiment override
     if (e && atoi(e) > 0) cache[ci] = atoi(e);
     return cache[ci];
+}
+
+// after resolve_kernel (exact entries and global first-token indices of every chunk): the tile records
+// the fast decode reads -- tile entry, token base, chunk offsets relative to it, no tile_fix join
+__global__ __launch_bounds__(GROUP) void tiles_from_resolved_kernel(DecBufs D) {
+    const Plan pl = *D.plan;
+    for (long long t = blockIdx.x; t < pl.ngroups; t += gridDim.x) {
+        const long long g0 = t * GROUP, gc = g0 + threadIdx.x;
+        const unsigned long long base = D.tokoff[g0];
+        if (threadIdx.x > 0 && gc < pl.nchunks) D.tokoff[gc] -= base;
+        if (threadIdx.x == 0) {
+            D.tentry[t] = (uint32_t)D.entry[g0] & 63u;       // UNK (63) stays UNKE: the decode reports it
+            D.tbase[t] = base;
+            D.tmap[t * 4 + 3] = 0;
+        }
+    }
+}
+
+extern "C" int dc_launch_decode_fast_resolved(const uint8_t* s, long long max_chunks, const Params* P,
+                                              const DecBufs* D, float* out, long long num, uint32_t epoch,
+                                              hipStream_t st) {
+    const long long max_groups = (max_chunks + GROUP - 1) / GROUP;
+    const int g = (int)std::min<long long>(max_groups > 0 ? max_groups : 1, 4096);
+    hipLaunchKernelGGL(tiles_from_resolved_kernel, dim3(g), dim3(GROUP), 0, st, *D);
+    const int gdec = (int)std::min<long long>(max_groups > 0 ? max_groups : 1, decode_grid(P->ct));
+    DC_DISPATCH_F(P->ct, decode_kernel_fast, dim3(gdec), dim3(GROUP), 0, st, s, *P, *D, out, num, epoch);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 extern "C" int dc_launch_decode_fast(const uint8_t* s, const unsigned long long* dev_nbits,

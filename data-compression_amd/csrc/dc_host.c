@@ -57,6 +57,7 @@ typedef struct {
     float* dec_out;
     long long dec_num;
     unsigned long long dec_nbits;
+    int dec_runs;                 /* the last decode's stream is in runs mode (Plan.runs) */
     int dec_shard;                   /* shard mode of the pending decode (DecBufs.shard) */
     const float* dec_hin;            /* its incoming values (shard mode 2) */
     int shard_deferred;              /* 1: tile-0 prefixes wait for dc_decode_shard_fix, 2: later tiles too */
@@ -529,10 +530,12 @@ int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsig
 
 static int read_dec_err(unsigned* err) {
     HIPCHK(hipMemcpyAsync(&G.h_scratch[2], G.D.err, 4, hipMemcpyDeviceToHost, G.st));
-    HIPCHK(hipMemcpyAsync(&G.h_scratch[3], G.D.plan, 8, hipMemcpyDeviceToHost, G.st));
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[12], G.D.plan, sizeof(Plan), hipMemcpyDeviceToHost, G.st));
     HIPCHK(hipStreamSynchronize(G.st));
     *err = (unsigned)(G.h_scratch[2] & 0xFFFFFFFFu);
-    G.dec_nbits = G.h_scratch[3];
+    const Plan* pl = (const Plan*)&G.h_scratch[12];
+    G.dec_nbits = pl->nbits;
+    G.dec_runs = pl->runs;
     return DC_OK;
 }
 
@@ -552,6 +555,7 @@ int dc_decode_finish(void) {
     rc = read_dec_err(&err);
     if (rc) return rc;
     const int queued = G.dec_queued;
+    int fast_values = 0;                   /* the values came from the fast decode (sentinel checked there) */
     G.dec_queued = 0;
     G.shard_deferred = 0;
     if (err && queued > 1 && !G.dec_shard) {
@@ -588,12 +592,21 @@ int dc_decode_finish(void) {
          * complete entry maps for every chunk if an entry is still unresolved) */
         HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
         if ((rc = dec_next_epoch())) return rc;
-        if (dc_launch_decode(G.dec_s, NULL, G.dec_nbits, G.dec_max_chunks, &G.dec_P, &G.D, G.dec_out, G.dec_num,
-                             G.dec_epoch, DEC_ROUNDS, DEC_FIX_ITERS, G.st))
+        if (G.dec_runs) {
+            /* runs mode: the parse left every chunk map its tiles reach -- compose them, then the fast
+             * decode kernel (which checks the history sentinel itself) from the resolved entries */
+            if (dc_launch_resolve(G.dec_max_chunks, &G.D, G.dec_epoch, G.st) ||
+                dc_launch_decode_fast_resolved(G.dec_s, G.dec_max_chunks, &G.dec_P, &G.D, G.dec_out, G.dec_num,
+                                               G.dec_epoch, G.st))
+                return seterr(DC_ERR_HIP, "decode launch failed");
+            fast_values = 1;
+        } else if (dc_launch_decode(G.dec_s, NULL, G.dec_nbits, G.dec_max_chunks, &G.dec_P, &G.D, G.dec_out, G.dec_num,
+                                    G.dec_epoch, DEC_ROUNDS, DEC_FIX_ITERS, G.st))
             return seterr(DC_ERR_HIP, "decode launch failed");
         rc = read_dec_err(&err);
         if (rc) return rc;
         if ((err & 8u) && !(err & 16u)) {
+            fast_values = 0;
             HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
             if ((rc = dec_next_epoch())) return rc;
             if (dc_launch_decode_more(G.dec_s, G.dec_max_chunks, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.dec_epoch,
@@ -604,6 +617,7 @@ int dc_decode_finish(void) {
         }
     }
     if ((err & 32u) && !(err & (8u | 16u | 128u)) && G.dec_pending) {
+        fast_values = 0;
         HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
         if (G.dec_shard == 2) {                      /* a shard with known incoming values */
             if (dc_launch_shard_fix(G.dec_s, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.dec_max_chunks, G.dec_hin, G.st))
@@ -613,7 +627,7 @@ int dc_decode_finish(void) {
         rc = read_dec_err(&err);
         if (rc) return rc;
     }
-    if (!err && G.dec_pending) {            /* a slow path wrote values: check for the history sentinel */
+    if (!err && G.dec_pending && !fast_values) {   /* a slow path wrote values: check for the history sentinel */
         if (dc_launch_find_sentinel(G.dec_out, G.dec_num, G.D.err, G.st))
             return seterr(DC_ERR_HIP, "decode launch failed");
         rc = read_dec_err(&err);

@@ -88,6 +88,9 @@ int dc_launch_encode_bits(const float* x, long long n, long long idx0, const DC_
 int dc_launch_decode(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
                      long long max_chunks, const DC_NS Params* P, const DC_NS DecBufs* D, float* out,
                      long long num, uint32_t epoch, int rounds, int fix_iters, dc_hip_stream st);
+int dc_launch_resolve(long long max_chunks, const DC_NS DecBufs* D, uint32_t epoch, dc_hip_stream st);
+int dc_launch_decode_fast_resolved(const uint8_t* s, long long max_chunks, const DC_NS Params* P,
+                                   const DC_NS DecBufs* D, float* out, long long num, uint32_t epoch, dc_hip_stream st);
 int dc_launch_decode_more(const uint8_t* s, long long max_chunks, const DC_NS Params* P,
                           const DC_NS DecBufs* D, float* out, long long num, uint32_t epoch,
                           int fix_iters, dc_hip_stream st);
