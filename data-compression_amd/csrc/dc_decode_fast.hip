@@ -673,6 +673,26 @@ __device__ __forceinline__ void flush_ring(const float* ring, float* outk, int r
     }
 }
 
+// runs-mode flush after every step: the head once complete, then every complete sector.  A lane then
+// holds < SECT unflushed values before a step, so a step may add up to RING - SECT + 1 values.
+constexpr int RUNK = RING - SECT;                  // values one run step may add
+__device__ __forceinline__ void flush_ring_all(const float* ring, float* outk, int r0, int& fl, int j, bool& hdone, int lim) {
+    if (!hdone && j >= fl) {
+        for (int ii = 0; ii < fl; ii++)
+            if (ii < lim) outk[ii] = ring[(ii + r0) & (RING - 1)];
+        hdone = true;
+    }
+    while (hdone && fl + SECT <= j) {
+        store_sector(ring, outk, fl, r0, lim);
+        fl += SECT;
+    }
+}
+__device__ __forceinline__ void ring_put(float* ring, int j, int r0, int kr, float v) {
+#pragma unroll
+    for (int q = 0; q < RUNK; q++)
+        if (q < kr) ring[(j + q + r0) & (RING - 1)] = v;
+}
+
 // Phase-B flushes with the global stores one flush behind the LDS reads: the sector read at flush k
 // sits in registers and leaves at flush k+1, so no flush waits on its own LDS read.
 struct PendSector {
@@ -806,7 +826,10 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
             Rd r;
             r.init(S.L, cs + e);
             int j = 0, it = 0;
-            // phase A: history still (partly) symbolic, or the stream's first three tokens
+            const bool runs = CT != 6 && pl.runs;
+            // phase A: history still (partly) symbolic, or the stream's first three tokens.  In runs mode
+            // a run of identical '100' / '101' codes is one step (Himeno planes start their chunks inside
+            // '101' runs, symbolic until the row's raw token)
             while (r.pos < cend && ((k1 | k2 | k3) != 0 || (first && j < 3))) {
                 r.fetch(S.L);
                 const uint32_t tk = r.peek();
@@ -818,12 +841,23 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
                     code = c3 ? (int)__builtin_amdgcn_ubfe(tk, 29u, 2u) : 0;
                     pat = c3 ? 0u : pat;
                 }
+                const int kr = (runs && !(first && j < 3)) ? run_same(tk, r.pos, cend, RUNK) : 1;
                 const float p2 = predict2(f1, f2), p3 = predict3(f1, f2, f3);
                 const float v = code == 0 ? __uint_as_float(pat) : (code == 1 ? f1 : (code == 2 ? p2 : p3));
                 const int kind = code == 0 ? 0 : (code == 1 ? k1 : (code == 2 ? ((k1 | k2) ? 4 : 0) : ((k1 | k2 | k3) ? 4 : 0)));
-                if (kind != 0) pend = j + 1;                         // re-decoded by the fix-up
+                if (kind != 0) pend = j + kr;                        // re-decoded by the fix-up
                 // history sentinel (-1.0f) or a prediction before the stream's history is full: exact path
                 sent |= (kind == 0 && __float_as_uint(v) == 0xBF800000u) || (first && j < 3 && code != 0);
+                if (runs) {
+                    ring_put(ring, j, r0, kr, v);
+                    f3 = kr >= 3 ? v : (kr == 2 ? f1 : f2); k3 = kr >= 3 ? kind : (kr == 2 ? k1 : k2);
+                    f2 = kr >= 2 ? v : f1; k2 = kr >= 2 ? kind : k1;
+                    f1 = v; k1 = kind;
+                    r.step(kr > 1 ? 3 * kr : (int)(meta >> 8));
+                    j += kr;
+                    flush_ring_all(ring, outk, r0, fl, j, hdone, lim);
+                    continue;
+                }
                 ring[(j + r0) & (RING - 1)] = v;
                 f3 = f2; k3 = k2; f2 = f1; k2 = k1; f1 = v; k1 = kind;
                 r.step((int)(meta >> 8));
@@ -835,13 +869,37 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
             }
             flush_ring(ring, outk, r0, fl, j, hdone, lim);
             it = 0;
+            const bool chk_all = (CT == 6 && P.B >= 23) || (CT == 7 && (P.mask17 >> 16) != 0u && P.mm == 23);
+            int sentv = 0;
+            // phase B in runs mode: one lane-divergent loop, a run of identical '100' / '101' codes per step
+            if (runs) {
+                while (r.pos < cend) {
+                    r.fetch(S.L);
+                    const uint32_t tk = r.peek();
+                    const uint32_t meta = S.T.meta[tk >> 23];
+                    const uint32_t pat = lut_pattern(S.T, tk, meta);
+                    const uint32_t cc = __builtin_amdgcn_ubfe(tk, 29u, 3u);    // 4..7 = '100'..'111'
+                    const int kr = run_same(tk, r.pos, cend, RUNK);
+                    float v = cc < 4u ? __uint_as_float(pat) : (cc == 5u ? f1 : 0.0f);
+                    if (cc >= 6u) {
+                        v = cc == 6u ? predict2(f1, f2) : predict3(f1, f2, f3);
+                        sentv |= __float_as_uint(v) == 0xBF800000u ? 1 : 0;
+                    }
+                    if (chk_all) sentv |= __float_as_uint(v) == 0xBF800000u ? 1 : 0;
+                    ring_put(ring, j, r0, kr, v);
+                    f3 = kr >= 3 ? v : (kr == 2 ? f1 : f2);
+                    f2 = kr >= 2 ? v : f1;
+                    f1 = v;
+                    r.step(kr > 1 ? 3 * kr : (int)(meta >> 8));
+                    j += kr;
+                    flush_ring_all(ring, outk, r0, fl, j, hdone, lim);
+                }
+            }
             // phase B: concrete history (kinds stay 0 from here on).  Runs in uniform blocks of SECT
             // steps with per-lane predication (a finished lane steps by 0 and keeps its history), so
             // the only branches are the block loop, the flush and the rare prediction branch.  Only
             // '110'/'111' predictions can make the -1.0f sentinel here unless chk_all (CT6 or a
             // negative mask with 23 kept mantissa bits: patterns without a midpoint bit).
-            const bool chk_all = (CT == 6 && P.B >= 23) || (CT == 7 && (P.mask17 >> 16) != 0u && P.mm == 23);
-            int sentv = 0;
             PendSector ps;
             ps.have = false;
             ps.s0 = 0;
@@ -997,7 +1055,8 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
             float g3 = ik[2] == 0 ? iv[2] : S.tin[ik[2] - 1];
             Rd r;
             r.init(S.L, cs + e);
-            for (int jj = 0; jj < pend; jj++) {
+            const bool runs = CT != 6 && pl.runs;
+            for (int jj = 0; jj < pend;) {
                 r.fetch(S.L);
                 const uint32_t tk = r.peek();
                 const uint32_t meta = S.T.meta[tk >> 23];
@@ -1009,11 +1068,17 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
                     code = c3 ? (int)__builtin_amdgcn_ubfe(tk, 29u, 2u) : 0;
                     pat = c3 ? 0u : pat;
                 }
+                // runs mode: a run of identical '100' / '101' codes inside the prefix is one step
+                const int kr = runs ? min(run_same(tk, 0, 30, 10), pend - jj) : 1;
                 const float v = code == 0 ? __uint_as_float(pat) : predict_value(code, g1, g2, g3);
-                if (k0 + jj < (unsigned long long)num) outk[jj] = v;
+                for (int q = 0; q < kr; q++)
+                    if (k0 + jj + q < (unsigned long long)num) outk[jj + q] = v;
                 sent |= __float_as_uint(v) == 0xBF800000u;
-                g3 = g2; g2 = g1; g1 = v;
-                r.step(len);
+                g3 = kr >= 3 ? v : (kr == 2 ? g1 : g2);
+                g2 = kr >= 2 ? v : g1;
+                g1 = v;
+                r.step(kr > 1 ? 3 * kr : len);
+                jj += kr;
             }
         }
         if (act) { D.pend[gc] = (uint16_t)min(pend, 65535); D.done[gc] = (pend && !dchunk) ? 1 : 0; }

@@ -319,6 +319,17 @@ __device__ __forceinline__ int run3i(uint32_t t, int pos, int tgt) {  // LDS pos
     return min(k, (tgt - pos + 2) / 3);
 }
 
+// decoders in runs mode step a run of IDENTICAL '100' (value 0) or '101' (value b1) codes at once: every
+// token of it has the same value and the history after it is that value repeated.  Returns the tokens of
+// the run at the reader (1 for any other token), at most kmax, counting only tokens that start before tgt.
+__device__ __forceinline__ int run_same(uint32_t t, int pos, int tgt, int kmax) {
+    const uint32_t hi = t >> 29;
+    if (hi != 4u && hi != 5u) return 1;
+    const uint32_t rep = hi == 4u ? 0x92492492u : 0xB6DB6DB6u;   // '100' / '101' repeated ten times
+    const int k = (int)((__clz((t ^ rep) | 3u) * 11u) >> 5);     // equal leading 3-bit groups (clz <= 30)
+    return max(1, min(min(k, kmax), (tgt - pos + 2) / 3));
+}
+
 // runs mode of a stream: below 6 bits per value it is mostly 3-bit codes (constant input: 3.0; Himeno
 // planes ~3.1; random data ~20), and the walks that find boundaries step whole runs and skip the
 // merge shortcut (period-3 paths in different phases never merge).  CT6 has no 3-bit codes.

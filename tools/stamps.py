@@ -7,16 +7,24 @@ import torch, dcamd
 L = dcamd.Lib(); L.init(0); L.set_bound(1e-3)
 n = 1 << int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 26
 kind = sys.argv[2] if len(sys.argv) > 2 else "u10"
-x = (torch.full((n,), 0.123456789, dtype=torch.float32) if kind == "eq" else torch.from_numpy(dcamd.gen_u10(n))).cuda()
+ct = int(sys.argv[3]) if len(sys.argv) > 3 else 7
+if kind == "eq":
+    x = torch.full((n,), 0.123456789, dtype=torch.float32)
+elif kind == "plane":            # a Himeno z-halo plane: p = i^2/(imax-1)^2, rows of 256 equal values
+    i = np.arange(n) // 256
+    x = torch.from_numpy((i * i).astype(np.float32) / np.float32(255 * 255))
+else:
+    x = torch.from_numpy(dcamd.gen_u10(n))
+x = x.cuda()
 cap = L.stream_capacity(n)
 st = torch.empty(cap, dtype=torch.uint8, device="cuda"); out = torch.empty(n, dtype=torch.float32, device="cuda")
 torch.cuda.synchronize()
 mean, t = L.med_device(x.data_ptr(), n)
 m17 = int(np.array([mean], np.float32).view(np.uint32)[0] >> 15)
-L.encode_device(7, x.data_ptr(), n, st.data_ptr(), type_=t, mask17=m17)
+L.encode_device(ct, x.data_ptr(), n, st.data_ptr(), type_=t, mask17=m17)
 nb = (L.encode_result() + 7) // 8
 for rep in range(3):
-    L.decode_device(7, st.data_ptr(), nb, n, out.data_ptr(), type_=t, mask17=m17)
+    L.decode_device(ct, st.data_ptr(), nb, n, out.data_ptr(), type_=t, mask17=m17)
     L.decode_finish()
 buf = (ctypes.c_ulonglong * (4096 * 16))()
 L.L.dc_debug_stamps(buf, 4096 * 16)
