@@ -180,8 +180,9 @@ __device__ __forceinline__ void walk_lds(const uint32_t* L, const uint8_t* tl, i
         while (A.pos < cend) {
             A.fetch(L);
             const uint32_t tk = A.peek();
-            const int k = (int)tk < 0 ? run3i(tk, A.pos, cend) : 1;
-            A.step(k > 1 ? 3 * k : (int)tl[tk >> 23]);
+            const int L = (int)tl[tk >> 23];
+            const int k = (int)tk < 0 ? run3i(tk, A.pos, cend) : run_per3(tk, L, A.pos, cend);
+            A.step(k > 1 ? ((int)tk < 0 ? 3 : L) * k : L);
             ca += k;
         }
         const int x = A.pos - (cs + CHUNK_BITS);
@@ -298,7 +299,8 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
                 while (r.pos < cs) {
                     r.fetch(S.L);
                     const uint32_t tk = r.peek();
-                    r.step((int)tk < 0 ? 3 * run3i(tk, r.pos, cs) : PLEN(tk));
+                    const int L = PLEN(tk);
+                    r.step((int)tk < 0 ? 3 * run3i(tk, r.pos, cs) : L * run_per3(tk, L, r.pos, cs));
                 }
             } else {
                 while (r.pos < cs) { r.fetch(S.L); r.step(PLEN(r.peek())); }
@@ -316,8 +318,9 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
                 while (r.pos < cend) {
                     r.fetch(S.L);
                     const uint32_t tk = r.peek();
-                    const int k = (int)tk < 0 ? run3i(tk, r.pos, cend) : 1;
-                    r.step(k > 1 ? 3 * k : PLEN(tk));
+                    const int L = PLEN(tk);
+                    const int k = (int)tk < 0 ? run3i(tk, r.pos, cend) : run_per3(tk, L, r.pos, cend);
+                    r.step(k > 1 ? ((int)tk < 0 ? 3 : L) * k : L);
                     n += k;
                 }
             } else {

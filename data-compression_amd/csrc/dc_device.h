@@ -319,6 +319,15 @@ __device__ __forceinline__ int run3i(uint32_t t, int pos, int tgt) {  // LDS pos
     return min(k, (tgt - pos + 2) / 3);
 }
 
+// boundary walks in runs mode, a token of length L not starting with '1': when the 32-bit window repeats
+// with period 3 (a constant input read out of phase: '001001...' parses as 9-bit raw tokens forever) and
+// 3 | L, the next tokens are copies of this one -- step every copy whose first 9 bits (which fix its
+// length) lie in the window, counting only tokens that start before tgt
+__device__ __forceinline__ int run_per3(uint32_t t, int L, int pos, int tgt) {
+    if (((t ^ (t << 3)) & 0xFFFFFFF8u) || L % 3 != 0 || L > 16) return 1;
+    return min(min(1 + 23 / L, 32 / L), (tgt - pos - 1) / L + 1);    // a reader step is at most 32 bits
+}
+
 // decoders in runs mode step a run of IDENTICAL '100' (value 0) or '101' (value b1) codes at once: every
 // token of it has the same value and the history after it is that value repeated.  Returns the tokens of
 // the run at the reader (1 for any other token), at most kmax, counting only tokens that start before tgt.
