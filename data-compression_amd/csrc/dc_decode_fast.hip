@@ -28,7 +28,7 @@
 
 namespace dc {
 
-constexpr int LROW = 32;                       // stream words per chunk
+constexpr int LROW = CHUNK_BITS / 32;          // stream words per chunk
 // LDS rows are padded to 33 words (stream word w sits at w + w/32): ds_read_b32 banks are
 // (address/4) mod 32 per 32-lane half, and the lanes of a wave walk their chunks at nearly the same
 // word offset, so unpadded rows put a whole half-wave on one or two banks (SQ_LDS_BANK_CONFLICT
@@ -293,7 +293,8 @@ __global__ __launch_bounds__(GROUP) void parse_kernel(const uint8_t* __restrict_
         int n = 0, x = 0;
         if (act) {
             Rd r;
-            r.init(S.L, gc == 0 ? cs : cs - OV);
+            // (tile 0: never before the stream's first bit, which is a true boundary)
+            r.init(S.L, gc == 0 ? cs : (t == 0 ? max(cs - OV, OV) : cs - OV));
             const unsigned long long q0 = D.dbg ? __builtin_amdgcn_s_memtime() : 0;
             if (CT != 6 && pl.runs) {
                 while (r.pos < cs) {
@@ -500,7 +501,7 @@ __device__ __forceinline__ bool lookup_global(const DecBufs& D, long long gc, in
 // tile t's own P_0 (P_0 had not synchronised by the tile start: a few % of tiles), one wave stages the
 // tile's first chunks and walks from E, chunk by chunk, until it joins the tile chain; the walked
 // chunks get their entries and offsets overridden.  One wave per tile.
-constexpr int FIXW = 8;                                   // chunks a fix-up walk may cover
+constexpr int FIXW = 8192 / CHUNK_BITS;                   // chunks a fix-up walk may cover (8 Kbit)
 struct FixShared {
     uint32_t L[4][padw(FIXW * LROW + 8)];
     uint8_t tl[512];
@@ -744,7 +745,7 @@ struct DecodeShared {
         } k;
     } u;
     float tin[3];
-    int need, cplx, defer;
+    int need, cplx, defer, badin;
     long long tile;
 #ifdef DC_DEC_PAD
     uint32_t occpad[DC_DEC_PAD / 4];            // occupancy experiment: extra LDS per workgroup
@@ -788,7 +789,7 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
         const bool act = c < nact;
         const int cs = c * CHUNK_BITS;
         const int cend = (int)min((long long)(cs + CHUNK_BITS), rem);
-        if (c == 0) { S.need = 0; S.cplx = 0; S.defer = 0; }
+        if (c == 0) { S.need = 0; S.cplx = 0; S.defer = 0; S.badin = 0; }
         // ---- entry and first token index of every chunk (parse kernel chain + tile_fix overrides)
         const int ein = (int)(te & 63), c0 = (int)((te >> 6) & 1023), kjoin = (int)(te >> 16);
         int e = UNKE;
@@ -1035,17 +1036,24 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
                 if (D.shard == 2) val = D.hin[j];
                 else if (D.shard == 1) S.defer = 1;
             }
-            if (bad) atomicOr(D.err, 32u);
+            if (bad) { atomicOr(D.err, 32u); S.badin = 1; }
             S.tin[c] = val;
         }
         __syncthreads();
         const bool defer = need && S.defer;                  // incoming values unknown yet (shard, mode 1)
+        // the incoming history came from a tile left to the serial fix-up (kind 4): so is this tile
+        const bool badin = need && S.badin;
         if (need && c == 0 && !(tk0 == 0 && tk1 == 0 && tk2 == 0)) {
             const int kk[3] = {tk0, tk1, tk2};
             for (int i = 0; i < 3; i++)
                 st_relaxed(&D.hist[t * 6 + 3 + i],
-                           defer ? hpack(2, epoch, 4, 0.0f)
-                                 : hpack(2, epoch, 0, kk[i] == 0 ? S.u.k.fv[i][fsrc] : S.tin[kk[i] - 1]));
+                           (defer || badin) ? hpack(2, epoch, 4, 0.0f)
+                                            : hpack(2, epoch, 0, kk[i] == 0 ? S.u.k.fv[i][fsrc] : S.tin[kk[i] - 1]));
+        }
+        if (badin) {                                         // every pending prefix: dc_launch_fixup_serial
+            if (act) { D.pend[gc] = (uint16_t)min(pend, 65535); D.done[gc] = 0; }
+            __syncthreads();
+            continue;
         }
         // deferred: prefixes that depend on the shard's incoming values wait for dc_decode_shard_fix
         const bool dchunk = defer && act && pend > 0 &&

@@ -14,7 +14,11 @@
 namespace dc {
 
 // decoder geometry: a chunk is the unit one lane parses; a group (tile) is one workgroup's chunks
-constexpr int CHUNK_BITS = 1024;
+// (a second build of the decoder objects uses 256-bit chunks for small streams: Makefile SMALLDEFS)
+#ifndef DC_CHUNK_BITS
+#define DC_CHUNK_BITS 1024
+#endif
+constexpr int CHUNK_BITS = DC_CHUNK_BITS;
 constexpr int GROUP = 256;
 
 

@@ -49,6 +49,7 @@ typedef struct {
     void* dec_pool;
     long long dec_cap_chunks;
     uint32_t dec_epoch;
+    int dec_small;                   /* the current decode runs the 256-bit-chunk decoder build */
     int dec_pending;
     int dec_queued;                  /* decodes issued since the last finish */
     Params dec_P;
@@ -104,6 +105,16 @@ static int seterr(int code, const char* fmt, ...) {
 
 const char* dc_last_error(void) { return G.msg; }
 #define ENC_ST (G.enc_st ? G.enc_st : G.st)
+/* the decoder build of the current decode: 1024-bit chunks, or 256-bit chunks (symbols with _s) */
+#define DV(fn) (G.dec_small ? fn##_s : fn)
+static long long small_chunk_max_bytes(void) {   /* DC_SMALL_CHUNK_MAX_BYTES overrides (0: never) */
+    static long long v = -2;
+    if (v == -2) {
+        const char* e = getenv("DC_SMALL_CHUNK_MAX_BYTES");
+        v = (e && *e) ? atoll(e) : (1ll << 20);
+    }
+    return v;
+}
 static int ensure_init(void);
 /* encoder launches go to this HIP stream (NULL: the library stream), so a caller can overlap the
  * encode of one buffer with the decode of another; the caller orders dependent work with events */
@@ -505,7 +516,9 @@ int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsig
     if ((uintptr_t)d_stream & 3u) return seterr(DC_ERR_ARG, "stream must be 4-byte aligned");
     if (nbytes < 0 && !d_nbits) return seterr(DC_ERR_ARG, "need nbytes or d_nbits");
     if (max_bytes < nbytes) max_bytes = nbytes;
-    long long cb = dc_decode_chunk_bits();
+    /* small streams (a Himeno halo plane: 25 KB) decode with 256-bit chunks: 4x more lanes, 4x shorter walks */
+    G.dec_small = max_bytes <= small_chunk_max_bytes();
+    long long cb = DV(dc_decode_chunk_bits)();
     long long max_chunks = (max_bytes * 8 + cb - 1) / cb;
     if (max_chunks < 1) max_chunks = 1;
     rc = dec_ensure(max_chunks);
@@ -513,7 +526,7 @@ int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsig
     if ((rc = dec_next_epoch())) return rc;
     Params P;
     make_params(&P, ct, type, mask17);
-    if (dc_launch_decode_fast((const uint8_t*)d_stream, nbytes >= 0 ? NULL : d_nbits,
+    if (DV(dc_launch_decode_fast)((const uint8_t*)d_stream, nbytes >= 0 ? NULL : d_nbits,
                               nbytes >= 0 ? (unsigned long long)nbytes * 8ull : 0ull, max_chunks, &P, &G.D,
                               (float*)d_out, num, G.dec_epoch, G.st))
         return seterr(DC_ERR_HIP, "decode launch failed: %s", hipGetErrorString(hipGetLastError()));
@@ -582,7 +595,7 @@ int dc_decode_finish(void) {
         DecBufs D = G.D;
         D.shard = 2;
         D.hin = G.dec_hin;
-        if (dc_launch_decode_serial(G.dec_s, &G.dec_P, &D, G.dec_out, G.dec_num, G.st))
+        if (DV(dc_launch_decode_serial)(G.dec_s, &G.dec_P, &D, G.dec_out, G.dec_num, G.st))
             return seterr(DC_ERR_HIP, "decode launch failed");
         HIPCHK(hipStreamSynchronize(G.st));
         return DC_OK;
@@ -595,12 +608,12 @@ int dc_decode_finish(void) {
         if (G.dec_runs) {
             /* runs mode: the parse left every chunk map its tiles reach -- compose them, then the fast
              * decode kernel (which checks the history sentinel itself) from the resolved entries */
-            if (dc_launch_resolve(G.dec_max_chunks, &G.D, G.dec_epoch, G.st) ||
-                dc_launch_decode_fast_resolved(G.dec_s, G.dec_max_chunks, &G.dec_P, &G.D, G.dec_out, G.dec_num,
+            if (DV(dc_launch_resolve)(G.dec_max_chunks, &G.D, G.dec_epoch, G.st) ||
+                DV(dc_launch_decode_fast_resolved)(G.dec_s, G.dec_max_chunks, &G.dec_P, &G.D, G.dec_out, G.dec_num,
                                                G.dec_epoch, G.st))
                 return seterr(DC_ERR_HIP, "decode launch failed");
             fast_values = 1;
-        } else if (dc_launch_decode(G.dec_s, NULL, G.dec_nbits, G.dec_max_chunks, &G.dec_P, &G.D, G.dec_out, G.dec_num,
+        } else if (DV(dc_launch_decode)(G.dec_s, NULL, G.dec_nbits, G.dec_max_chunks, &G.dec_P, &G.D, G.dec_out, G.dec_num,
                                     G.dec_epoch, DEC_ROUNDS, DEC_FIX_ITERS, G.st))
             return seterr(DC_ERR_HIP, "decode launch failed");
         rc = read_dec_err(&err);
@@ -609,7 +622,7 @@ int dc_decode_finish(void) {
             fast_values = 0;
             HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
             if ((rc = dec_next_epoch())) return rc;
-            if (dc_launch_decode_more(G.dec_s, G.dec_max_chunks, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.dec_epoch,
+            if (DV(dc_launch_decode_more)(G.dec_s, G.dec_max_chunks, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.dec_epoch,
                                       DEC_FIX_ITERS, G.st))
                 return seterr(DC_ERR_HIP, "decode launch failed");
             rc = read_dec_err(&err);
@@ -620,15 +633,15 @@ int dc_decode_finish(void) {
         fast_values = 0;
         HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
         if (G.dec_shard == 2) {                      /* a shard with known incoming values */
-            if (dc_launch_shard_fix(G.dec_s, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.dec_max_chunks, G.dec_hin, G.st))
+            if (DV(dc_launch_shard_fix)(G.dec_s, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.dec_max_chunks, G.dec_hin, G.st))
                 return seterr(DC_ERR_HIP, "decode launch failed");
-        } else if (dc_launch_fixup_serial(G.dec_s, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.st))
+        } else if (DV(dc_launch_fixup_serial)(G.dec_s, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.st))
             return seterr(DC_ERR_HIP, "decode launch failed");
         rc = read_dec_err(&err);
         if (rc) return rc;
     }
     if (!err && G.dec_pending && !fast_values) {   /* a slow path wrote values: check for the history sentinel */
-        if (dc_launch_find_sentinel(G.dec_out, G.dec_num, G.D.err, G.st))
+        if (DV(dc_launch_find_sentinel)(G.dec_out, G.dec_num, G.D.err, G.st))
             return seterr(DC_ERR_HIP, "decode launch failed");
         rc = read_dec_err(&err);
         if (rc) return rc;
@@ -636,7 +649,7 @@ int dc_decode_finish(void) {
     if ((err & 128u) && !(err & 16u) && G.dec_pending) {
         /* -1.0f history sentinel in the stream: exact sequential decode (reference semantics) */
         HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
-        if (dc_launch_decode_serial(G.dec_s, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.st))
+        if (DV(dc_launch_decode_serial)(G.dec_s, &G.dec_P, &G.D, G.dec_out, G.dec_num, G.st))
             return seterr(DC_ERR_HIP, "decode launch failed");
         rc = read_dec_err(&err);
         if (rc) return rc;
@@ -677,11 +690,11 @@ int dc_decode_shard_fix(const float* d_hin) {
     D.shard = 2;
     D.hin = d_hin;
     if (G.shard_deferred == 3) {                    /* exact sequential decode of the whole shard */
-        if (dc_launch_decode_serial(G.dec_s, &G.dec_P, &D, G.dec_out, G.dec_num, G.st))
+        if (DV(dc_launch_decode_serial)(G.dec_s, &G.dec_P, &D, G.dec_out, G.dec_num, G.st))
             return seterr(DC_ERR_HIP, "shard fix launch failed");
     } else {
         const long long nc = G.shard_deferred == 2 ? G.dec_max_chunks : dc_decode_group();
-        if (dc_launch_shard_fix(G.dec_s, &G.dec_P, &D, G.dec_out, G.dec_num, nc, d_hin, G.st))
+        if (DV(dc_launch_shard_fix)(G.dec_s, &G.dec_P, &D, G.dec_out, G.dec_num, nc, d_hin, G.st))
             return seterr(DC_ERR_HIP, "shard fix launch failed");
     }
     HIPCHK(hipStreamSynchronize(G.st));             /* re-runnable with other values until the next decode */

@@ -119,6 +119,26 @@ void dc_mark_next_set(void);
 int dc_timing_enable(int nsets);
 int dc_timing_read(int set, float* ms);
 long long dc_decode_group(void);
+/* the same decoder built with 256-bit chunks (Makefile SMALLDEFS renames its symbols with _s) */
+int dc_launch_decode_s(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                       long long max_chunks, const DC_NS Params* P, const DC_NS DecBufs* D, float* out,
+                       long long num, uint32_t epoch, int rounds, int fix_iters, dc_hip_stream st);
+int dc_launch_resolve_s(long long max_chunks, const DC_NS DecBufs* D, uint32_t epoch, dc_hip_stream st);
+int dc_launch_decode_fast_resolved_s(const uint8_t* s, long long max_chunks, const DC_NS Params* P,
+                                     const DC_NS DecBufs* D, float* out, long long num, uint32_t epoch, dc_hip_stream st);
+int dc_launch_decode_more_s(const uint8_t* s, long long max_chunks, const DC_NS Params* P,
+                            const DC_NS DecBufs* D, float* out, long long num, uint32_t epoch,
+                            int fix_iters, dc_hip_stream st);
+int dc_launch_decode_fast_s(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                            long long max_chunks, const DC_NS Params* P, const DC_NS DecBufs* D, float* out,
+                            long long num, uint32_t epoch, dc_hip_stream st);
+int dc_launch_decode_serial_s(const uint8_t* s, const DC_NS Params* P, const DC_NS DecBufs* D, float* out,
+                              long long num, dc_hip_stream st);
+int dc_launch_find_sentinel_s(const float* out, long long num, unsigned* err, dc_hip_stream st);
+int dc_launch_fixup_serial_s(const uint8_t* s, const DC_NS Params* P, const DC_NS DecBufs* D, float* out,
+                             long long num, dc_hip_stream st);
+long long dc_decode_chunk_bits_s(void);
+long long dc_decode_group_s(void);
 
 int dc_launch_to_small(const float* x, long long n, float* y, float* part_v, long long* part_i, float* d_min,
                        dc_hip_stream st);
@@ -139,6 +159,8 @@ int dc_launch_bit_shift_copy(const uint8_t* s, long long sbytes, unsigned long l
                              uint8_t* d, long long nout, dc_hip_stream st);
 int dc_launch_shard_fix(const uint8_t* s, const DC_NS Params* P, const DC_NS DecBufs* D, float* out, long long num,
                         long long nchunks, const float* hin, dc_hip_stream st);
+int dc_launch_shard_fix_s(const uint8_t* s, const DC_NS Params* P, const DC_NS DecBufs* D, float* out, long long num,
+                          long long nchunks, const float* hin, dc_hip_stream st);
 int dc_launch_plane_gather(const float* p, int mj, int mk, int ijk, int v, int A, int B, float* out, dc_hip_stream st);
 int dc_launch_plane_scatter(const float* x, const float* d_min, float* p, int mj, int mk, int ijk, int v, int A, int B,
                             dc_hip_stream st);
