@@ -107,13 +107,20 @@ const char* dc_last_error(void) { return G.msg; }
 #define ENC_ST (G.enc_st ? G.enc_st : G.st)
 /* the decoder build of the current decode: 1024-bit chunks, or 256-bit chunks (symbols with _s) */
 #define DV(fn) (G.dec_small ? fn##_s : fn)
+static long long g_small_max = -2;
 static long long small_chunk_max_bytes(void) {   /* DC_SMALL_CHUNK_MAX_BYTES overrides (0: never) */
-    static long long v = -2;
-    if (v == -2) {
+    if (g_small_max == -2) {
         const char* e = getenv("DC_SMALL_CHUNK_MAX_BYTES");
-        v = (e && *e) ? atoll(e) : (1ll << 20);
+        g_small_max = (e && *e) ? atoll(e) : (1ll << 20);
     }
-    return v;
+    return g_small_max;
+}
+/* streams of at most this capacity decode with the 256-bit-chunk build (< 0: the default, 1 MiB);
+ * returns the previous value */
+long long dc_set_small_chunk_max_bytes(long long v) {
+    const long long old = small_chunk_max_bytes();
+    g_small_max = v < 0 ? (1ll << 20) : v;
+    return old;
 }
 static int ensure_init(void);
 /* encoder launches go to this HIP stream (NULL: the library stream), so a caller can overlap the
@@ -131,7 +138,7 @@ int dc_set_error(int code, const char* msg) { return seterr(code, "%s", msg); }
 void* dc_get_stream(void) { return (void*)G.st; }
 void dc_set_abs_error_bound(double bound) { absErrBound = bound; absErrorBound_binary = -100; }
 double dc_get_abs_error_bound(void) { return absErrBound; }
-long long dc_decode_chunk_bits_value(void) { return dc_decode_chunk_bits(); }
+long long dc_decode_chunk_bits_value(void) { return DV(dc_decode_chunk_bits)(); }   /* of the last decode */
 
 /* diagnostic: copy the decoder phase stamps ([tile][16] s_memrealtime, 100 MHz) to the host */
 int dc_debug_stamps(unsigned long long* host, long long n) {

@@ -43,7 +43,7 @@ EXT_SYMBOLS = [
     "dc_halo_encode_device", "dc_halo_decode_device",
     "dc64_stream_capacity", "dc64_encode_device", "dc64_encode_result", "dc64_decode_device", "dc64_decode_finish",
     "dc64_last_decode_flags", "dc64_to_small_device", "dc64_med_device", "dc_set_encode_stream",
-    "dc_decode_status", "dc_abi_status", "dc_med_sum_device", "dc_type_from_max",
+    "dc_decode_status", "dc_abi_status", "dc_med_sum_device", "dc_type_from_max", "dc_set_small_chunk_max_bytes",
 ]
 
 
@@ -85,6 +85,8 @@ class Lib:
         L.dc_decode_status.argtypes = [C.POINTER(C.c_uint)]
         L.dc_crc32_device.argtypes = [vp, ll, C.POINTER(C.c_uint32)]
         L.dc_decode_chunk_bits_value.restype = ll
+        L.dc_set_small_chunk_max_bytes.argtypes = [ll]
+        L.dc_set_small_chunk_max_bytes.restype = ll
         pp = [_f32p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int), C.POINTER(C.c_int)]
         for nm in ("myCompress_bitwise", "myCompress_bitwise_np", "myCompress_bitwise_op"):
             getattr(L, nm).argtypes = pp
@@ -388,6 +390,15 @@ class Lib:
 
     def decode_finish(self):
         self.check(self.L.dc_decode_finish(), "dc_decode_finish")
+
+    def set_small_chunk_max_bytes(self, v):
+        """Streams of at most v bytes of capacity use the 256-bit-chunk decoder build (< 0: default 1 MiB,
+        0: never); returns the previous value."""
+        return int(self.L.dc_set_small_chunk_max_bytes(int(v)))
+
+    def chunk_bits(self):
+        """Chunk bits of the decoder build the last decode ran."""
+        return int(self.L.dc_decode_chunk_bits_value())
 
     def decode_status(self):
         """Fast-path status word OR-ed over every decode since the last finish (0: all on the fast path)."""

@@ -139,7 +139,10 @@ int dc64_to_small_device(const void* d_x, long long n, void* d_out, double* min_
 int dc64_med_device(const void* d_x, long long n, double* mean_out, int* type_out);     /* synchronous */
 
 /* Decoder/encoder geometry (for tests and bench). */
-long long dc_decode_chunk_bits_value(void);
+long long dc_decode_chunk_bits_value(void);                 /* chunk bits of the last decode's build */
+/* Streams of at most this capacity (bytes) decode with the 256-bit-chunk build of the decoder, larger
+ * ones with the 1024-bit build (< 0: the default, 1 MiB; 0: never).  Returns the previous value. */
+long long dc_set_small_chunk_max_bytes(long long max_bytes);
 
 #ifdef __cplusplus
 }

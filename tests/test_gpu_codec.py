@@ -129,6 +129,31 @@ def test_roundtrip_vs_oracle(dc, oracle, bound, kind, n, ct):
     assert np.array_equal(out.view(np.uint32), spec.view(np.uint32))
 
 
+@pytest.mark.parametrize("bound", [1e-3, 1e-6])
+@pytest.mark.parametrize("kind,n", [("u10", 1 << 18), ("eq", 1 << 18), ("himeno", 1 << 16), ("mixed", 1 << 17),
+                                    ("ramp", 100003)])
+@pytest.mark.parametrize("ct", CTS)
+def test_both_decoder_builds(dc, oracle, bound, kind, n, ct):
+    """The same stream through the 1024-bit-chunk and the 256-bit-chunk builds of the decoder (the
+    library picks one per decode from the stream capacity): both equal the oracle bit for bit."""
+    dc.set_bound(bound)
+    x = _inputs(oracle, kind, n)
+    _, xs = oracle.to_small(x)
+    t, m17 = oracle.type_mask(xs)
+    s, nb, pos = dc.compress(ct, xs, t, m17)
+    spec, got = oracle.decompress(ct, s, n, bound, t, m17)
+    assert got == n
+    old = dc.set_small_chunk_max_bytes(0)
+    try:
+        for thr, cb in ((0, 1024), (1 << 40, 256)):
+            dc.set_small_chunk_max_bytes(thr)
+            out = dc.decompress(ct, s, n, t, m17)
+            assert dc.chunk_bits() == cb
+            assert np.array_equal(out.view(np.uint32), spec.view(np.uint32)), f"chunk bits {cb}"
+    finally:
+        dc.set_small_chunk_max_bytes(old)
+
+
 @pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 63, 64, 65, 4095, 4096, 4097, 8191, 12345, 65537])
 @pytest.mark.parametrize("ct", CTS)
 def test_ragged_sizes(dc, oracle, n, ct):
