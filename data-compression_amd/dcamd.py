@@ -498,6 +498,64 @@ def gather_stream(local, start_bit, local_bits, group=None):
     return out, total
 
 
+def halo_exchange(streams, nbits, mins, down, up, group=None):
+    """Himeno z-halo exchange of compressed planes (impl/himenoBMTxps.c:644-690), one process per GPU.
+
+    streams[0] (plane k = 1) goes to rank `down`, streams[1] (plane k = kmax - 2) to rank `up`; None
+    stands for MPI_PROC_NULL (no neighbour: nothing is sent or received on that side).  nbits / mins:
+    per-plane stream bit counts and toSmallDataset minima (ints / floats, or 1-element tensors).  As
+    the reference, the sizes travel first (one int64 pair per direction: bits and the min's bit pattern),
+    then exactly the stream bytes.  Returns [(stream, nbits, min) received from up (for k = kmax - 1),
+    the same from down (for k = 0)], None where there is no neighbour.  P2P over RCCL with device
+    tensors, or over gloo with host copies."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    dev = streams[0].device
+    host = dev.type == "cuda" and dist.get_backend(group) == "gloo"
+    cdev = torch.device("cpu") if host else dev
+
+    def meta(h):
+        b = int(nbits[h])
+        m = int(np.array([float(mins[h])], np.float32).view(np.int32)[0])
+        return torch.tensor([b, m], dtype=torch.int64, device=cdev)
+
+    peers = [(0, down, 0), (1, up, 1)]          # (plane sent, to rank, tag): the receiver gets it from its up / down
+    sides = [(up, 0), (down, 1)]                 # (from rank, tag): the planes for k = kmax - 1 and k = 0
+    rmeta = [torch.zeros(2, dtype=torch.int64, device=cdev) for _ in sides]
+    ops = [dist.P2POp(dist.isend, meta(h), peer, group=group, tag=tag) for h, peer, tag in peers if peer is not None]
+    ops += [dist.P2POp(dist.irecv, rmeta[i], peer, group=group, tag=tag)
+            for i, (peer, tag) in enumerate(sides) if peer is not None]
+    if ops:
+        for r in dist.batch_isend_irecv(ops):
+            r.wait()
+    ops, rbuf = [], [None, None]
+    for h, peer, tag in peers:
+        nb = (int(nbits[h]) + 7) // 8
+        if peer is not None and nb > 0:
+            src = streams[h][:nb]
+            ops.append(dist.P2POp(dist.isend, src.cpu() if host else src.contiguous(), peer, group=group, tag=2 + tag))
+    for i, (peer, tag) in enumerate(sides):
+        if peer is None:
+            continue
+        nb = (int(rmeta[i][0]) + 7) // 8
+        rbuf[i] = torch.zeros(nb, dtype=torch.uint8, device=cdev)
+        if nb > 0:
+            ops.append(dist.P2POp(dist.irecv, rbuf[i], peer, group=group, tag=2 + tag))
+    if ops:
+        for r in dist.batch_isend_irecv(ops):
+            r.wait()
+    out = []
+    for i, (peer, _) in enumerate(sides):
+        if peer is None:
+            out.append(None)
+            continue
+        b, m = int(rmeta[i][0]), int(rmeta[i][1])
+        mn = float(np.array([m], np.int32).view(np.float32)[0])
+        out.append((rbuf[i].to(dev) if host else rbuf[i], b, mn))
+    return out
+
+
 def _bcast_scalar(v, src, dev, group=None, dtype=None):
     import torch
     import torch.distributed as dist

@@ -120,3 +120,60 @@ def test_settle_history_world3():
         p.join(timeout=60)
     for r in range(world):
         assert res[r] == [float(r)] * 3, res
+
+
+def _plane(rank, h, n=4096):
+    """Deterministic stand-in for rank `rank`'s z-halo plane h (Himeno-like rows of equal values)."""
+    i = np.arange(n) // 64
+    return ((i * i).astype(np.float32) / np.float32(63 * 63) + np.float32(0.25 * rank + 0.1 * h)).astype(np.float32)
+
+
+def _halo_worker(rank, world, port, ct, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import dcamd
+        from pyoracle import Oracle
+        O = Oracle()
+
+        def enc(r, h):
+            mn, xs = O.to_small(_plane(r, h))
+            s, nb, pos = O.compress(ct, xs, 1e-3, 0, 0)
+            return s, _bits_of(nb, pos), mn
+
+        mine = [enc(rank, 0), enc(rank, 1)]
+        down = rank - 1 if rank > 0 else None            # MPI_Cart, non-periodic: PROC_NULL at the ends
+        up = rank + 1 if rank + 1 < world else None
+        got = dcamd.halo_exchange([torch.from_numpy(m[0]) for m in mine], [m[1] for m in mine],
+                                  [m[2] for m in mine], down, up)
+        ok = True
+        # from up: its plane k = 1 (h = 0), for our k = kmax - 1; from down: its plane k = kmax - 2 (h = 1)
+        for peer, h, rec in ((up, 0, got[0]), (down, 1, got[1])):
+            if peer is None:
+                ok &= rec is None
+                continue
+            s, bits, mn = enc(peer, h)
+            rs, rbits, rmn = rec
+            ok &= rbits == bits and rmn == mn and np.array_equal(rs.numpy(), s)
+            d, n = O.decompress(ct, rs.numpy(), 4096, 1e-3, 0, 0)
+            ok &= n == 4096 and bool(np.all(np.abs(d + rmn - _plane(peer, h)) <= 1e-3 * 1.01))
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_halo_exchange(world):
+    """dcamd.halo_exchange (impl/himenoBMTxps.c:644-690: sizes first, then min + stream bytes, to the
+    z-neighbours of a non-periodic line of ranks) delivers every neighbour's compressed plane intact."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_halo_worker, args=(r, world, port, 5, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] for r in res), res
