@@ -141,6 +141,7 @@ def halo_bench(args):
     up = rank + 1 if rank + 1 < world else None
     rmins = torch.zeros(2, dtype=torch.float32, device=dev)
     xfer = [0, 0]                                   # stream bytes this rank received, per step
+    last = [None]                                   # the last step's received (stream, bits, min) per side
 
     def step():
         for h, v in enumerate(planes):
@@ -154,11 +155,15 @@ def halo_bench(args):
         L.synchronize()                             # the sizes leave first (impl/himenoBMTxps.c:648-670)
         nb, mn = bits.cpu().tolist(), mins.cpu().tolist()
         got = dcamd.halo_exchange(st, nb, mn, down, up)
-        for i, (rec, kk) in enumerate(zip(got, (kmax - 1, 0))):
+        last[0] = (got, nb, mn)
+        for i, rec in enumerate(got):
+            if rec is not None:
+                rmins[i] = rec[2]
+        torch.cuda.synchronize()                    # received bytes / minima land on torch's streams, the
+        for i, (rec, kk) in enumerate(zip(got, (kmax - 1, 0))):   # decoder runs on the library's own
             if rec is None:
                 continue
             rs, rb, rmn = rec
-            rmins[i] = rmn
             xfer[i] = (rb + 7) // 8
             L.halo_decode_device(ct, rs.data_ptr(), (rb + 7) // 8, 0, 0, 0, rmins.data_ptr() + 4 * i,
                                  q.data_ptr(), (mi, mj, mk), 3, kk, (imax, jmax, kmax))
@@ -177,12 +182,23 @@ def halo_bench(args):
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     xcheck = None
-    if dist is not None:                           # received planes = the neighbour's planes within the bound
-        errs = []
-        for i, (peer, kk, ks) in enumerate(((up, kmax - 1, 1), (down, 0, kmax - 2))):
-            if peer is not None:                   # every rank holds the same field p
-                errs.append(float((q[:imax, :jmax, kk] - p[:imax, :jmax, ks]).abs().max()))
-        xcheck = bool(all(e <= args.bound * 1.0001 for e in errs))
+    if dist is not None:
+        # every rank holds the same field p, so the plane received from up is this rank's own plane k = 1
+        # (h = 0) and the one from down its plane k = kmax - 2 (h = 1): same bits, min and stream bytes,
+        # and the halo decoded from the received stream equals the one decoded from the local stream
+        got, nb, mn = last[0]
+        q2 = torch.zeros_like(q)
+        xcheck = True
+        for rec, kk, h in zip(got, (kmax - 1, 0), (0, 1)):
+            if rec is None:
+                continue
+            rs, rb, rmn = rec
+            k = (rb + 7) // 8
+            xcheck &= rb == nb[h] and rmn == mn[h] and bool(torch.equal(rs[:k].cpu(), st[h][:k].cpu()))
+            L.halo_decode_device(ct, st[h].data_ptr(), -1, bits.data_ptr() + 8 * h, 0, 0, mins.data_ptr() + 4 * h,
+                                 q2.data_ptr(), (mi, mj, mk), 3, kk, (imax, jmax, kmax))
+            L.synchronize()
+            xcheck &= bool(torch.equal(q[:imax, :jmax, kk], q2[:imax, :jmax, kk]))
     planes_cd = 2.0 * world                        # (encodes + decodes) / 2 per step, all ranks
     if dist is not None:
         w = torch.tensor([wall], dtype=torch.float64, device=dev)
@@ -663,12 +679,12 @@ def side_config(C, ct, kind, log2n, steps, warmup, bound, ber=0.0):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     if args.halo:
         return halo_bench(args)
     if args.f64:
         return f64_bench(args)
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(spawn_ranks(args))
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if world_env != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
