@@ -128,7 +128,7 @@ def _plane(rank, h, n=4096):
     return ((i * i).astype(np.float32) / np.float32(63 * 63) + np.float32(0.25 * rank + 0.1 * h)).astype(np.float32)
 
 
-def _halo_worker(rank, world, port, ct, q):
+def _halo_worker(rank, world, port, ct, q, empty=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -142,7 +142,10 @@ def _halo_worker(rank, world, port, ct, q):
             s, nb, pos = O.compress(ct, xs, 1e-3, 0, 0)
             return s, _bits_of(nb, pos), mn
 
-        mine = [enc(rank, 0), enc(rank, 1)]
+        def enc_side(r, h):                              # empty: every plane k = kmax - 2 is a 0-bit stream
+            return (np.zeros(0, np.uint8), 0, 0.0) if (empty and h == 1) else enc(r, h)
+
+        mine = [enc_side(rank, 0), enc_side(rank, 1)]
         down = rank - 1 if rank > 0 else None            # MPI_Cart, non-periodic: PROC_NULL at the ends
         up = rank + 1 if rank + 1 < world else None
         got = dcamd.halo_exchange([torch.from_numpy(m[0]) for m in mine], [m[1] for m in mine],
@@ -153,9 +156,11 @@ def _halo_worker(rank, world, port, ct, q):
             if peer is None:
                 ok &= rec is None
                 continue
-            s, bits, mn = enc(peer, h)
+            s, bits, mn = enc_side(peer, h)
             rs, rbits, rmn = rec
             ok &= rbits == bits and rmn == mn and np.array_equal(rs.numpy(), s)
+            if bits == 0:
+                continue
             d, n = O.decompress(ct, rs.numpy(), 4096, 1e-3, 0, 0)
             ok &= n == 4096 and bool(np.all(np.abs(d + rmn - _plane(peer, h)) <= 1e-3 * 1.01))
         q.put((rank, bool(ok)))
@@ -163,14 +168,14 @@ def _halo_worker(rank, world, port, ct, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_halo_exchange(world):
+@pytest.mark.parametrize("world,empty", [(2, False), (3, False), (4, False), (3, True)])
+def test_halo_exchange(world, empty):
     """dcamd.halo_exchange (impl/himenoBMTxps.c:644-690: sizes first, then min + stream bytes, to the
     z-neighbours of a non-periodic line of ranks) delivers every neighbour's compressed plane intact."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_halo_worker, args=(r, world, port, 5, q)) for r in range(world)]
+    procs = [ctx.Process(target=_halo_worker, args=(r, world, port, 5, q, empty)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]
