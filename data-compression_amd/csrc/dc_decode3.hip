@@ -1,0 +1,689 @@
+// dc_decode3.hip -- segment decoder: the fast path of the bit-wise decoders of impl/dataCompression.c
+// (myDecompress_bitwise :2922, _np :2459, _mask :1703, _op :698) for streams of ordinary density.
+//
+// The token walk is one dependent chain per reader: each step reads the next stream word and a table
+// entry from LDS and is ~250 cycles of latency on gfx950.  Throughput therefore needs many chains per
+// SIMD and few LDS bank conflicts, with as few walks per token as possible:
+//
+// parse3_kernel  one wave per parse job.  Lane l walks SEGMENT l of the job (seg 256-bit chunks, tens
+//                of thousands of bits) after a 1024-bit pre-walk (self-synchronisation), reading the
+//                stream through a per-lane LDS ring of 16 words (+4 mirrored) refilled 128 bits at a
+//                time with loads issued two phases ahead.  The ring is stored [word][lane], so every
+//                ds_read_b32 of a wave hits 32 distinct banks whatever the lanes' offsets.  At every
+//                chunk boundary the lane records the chunk's entry offset and token count (16 bits).
+//                Links are checked afterwards: a segment's first entry must equal the previous
+//                segment's exit (in-wave shuffle; across jobs the previous job's published exit, which
+//                never waits on anything -- no chain).  A broken link (the pre-walk had not
+//                synchronised, ~0.3% of segments) is repaired by re-walking from the true entry until
+//                the path meets the recorded entries again.  The wave's token counts are scanned into
+//                job-relative first-token offsets of every decode job.
+// scan3_kernel   exclusive scan of the parse jobs' token counts.
+// decode3_kernel one wave per decode job of 64 chunks: lane = chunk, decoded from its recorded entry for
+//                its recorded token count.  Values go to a wave-private LDS buffer at their job-relative
+//                index (aligned to the output's 16-byte grid) and leave as whole float4 stores.
+//                Predicted codes ('101'/'110'/'111', rare in ordinary data) read their history from that
+//                buffer; the first tokens of a chunk that need the previous chunk's values are left
+//                pending and re-decoded lane by lane afterwards (the job's first chunk takes the previous
+//                job's last three values, published as epoch-tagged granules).
+// A stream outside these assumptions (runs mode: mostly 3-bit codes; a repair that does not converge;
+// more tokens per job than the buffer holds; the -1.0f history sentinel) sets status 512 and is decoded
+// by the chunk-map decoder of dc_decode_fast.hip instead (dc_decode_finish).
+#include "dc_device.h"
+#include <algorithm>
+#include <stdio.h>
+#include <stdlib.h>
+#include <unistd.h>
+
+namespace dc {
+
+constexpr int D3_PRE = 4;              // pre-walk chunks (1024 bits)
+constexpr int D3_RING = 16;            // ring words per lane (four 128-bit phases), + 4 mirrored words
+constexpr int D3_CAP = 1024 + 16;      // decode job output buffer (floats per wave)
+constexpr uint32_t D3_DECLINE = 512u;
+// why (diagnostic bits beside 512): 1024 runs mode / capacity, 2048 unresolved link, 4096 fewer tokens
+// than values, 8192 a job denser than its buffer, 16384 the history sentinel or an early prediction
+constexpr uint32_t D3_WHY_RUNS = 1024u, D3_WHY_LINK = 2048u, D3_WHY_SHORT = 4096u, D3_WHY_DENSE = 8192u,
+                   D3_WHY_SENT = 16384u;
+
+// DC_DEC3_PROF builds (make XDEFS=-DDC_DEC3_PROF B=build_p L=lib_p): per-section shader-clock totals
+// summed over waves into g_prof3 (read with dc_dec3_prof_read; tools/dec3_prof.py)
+#ifdef DC_DEC3_PROF
+__device__ unsigned long long g_prof3[32];
+#define P3_T(v) const long long v = clock64()
+#define P3_ADD(i, val) do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_prof3[i], (unsigned long long)(val)); } while (0)
+#else
+#define P3_T(v) do {} while (0)
+#define P3_ADD(i, val) do {} while (0)
+#endif
+
+__device__ __forceinline__ uint32_t bsw(uint32_t v) { return __builtin_bswap32(v); }
+
+// 4 stream words from word gw (a multiple of 4), MSB-first, through a buffer resource whose range is
+// the buffer's readable capacity (capw words, a multiple of 4, every stream byte inside it): groups
+// outside it -- before the stream (a negative offset wraps past the range) or past the capacity -- read
+// as 0 in hardware, so the load is one unconditional buffer_load_dwordx4 that stays in flight until its
+// words are used (a branchy or select-guarded global load made the compiler wait at once).  Bytes past
+// the stream's end read as 0, as the reference's reader sees them.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t stream_rsrc(const uint8_t* s, long long capw) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(s), (short)0, (int)(capw * 4), 0x00020000);
+}
+__device__ __forceinline__ uint32_t keep_bytes(uint32_t w, int rem) {     // rem = stream bytes left at w
+    return (uint32_t)(0xFFFFFFFF00000000ull >> (8 * min(max(rem, 0), 4))) & w;
+}
+// (stream offsets fit 31 bits: the host takes this decoder only for capacities below 2 GiB)
+__device__ __forceinline__ uint4 load_w4(__amdgpu_buffer_rsrc_t rs, long long nbytes, long long gw) {
+    const int off = (int)(uint32_t)(gw * 4);
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    uint4 w = make_uint4(bsw(v.x), bsw(v.y), bsw(v.z), bsw(v.w));
+    const int r0 = (int)nbytes - off;
+    if (r0 < 16) {                            // the group holding the stream's last byte (or past it: 0 already)
+        w.x = keep_bytes(w.x, r0);
+        w.y = keep_bytes(w.y, r0 - 4);
+        w.z = keep_bytes(w.z, r0 - 8);
+        w.w = keep_bytes(w.w, r0 - 12);
+    }
+    return w;
+}
+
+__device__ __forceinline__ bool declined_now(const Dec3Bufs& D3) {
+    return (__hip_atomic_load(D3.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & D3_DECLINE) != 0;
+}
+
+struct Geo3 {
+    unsigned long long nbits;
+    long long nbytes, nchunks, nseg, npjobs, ndjobs;
+    int seg;
+};
+__device__ __forceinline__ Geo3 geo3(const unsigned long long* dev_nbits, unsigned long long host_nbits, int seg) {
+    Geo3 g;
+    g.nbits = dev_nbits ? *dev_nbits : host_nbits;
+    g.nbytes = (long long)((g.nbits + 7) >> 3);
+    g.nchunks = (long long)((g.nbits + 255) >> 8);
+    g.seg = seg;
+    g.nseg = (g.nchunks + seg - 1) / seg;
+    g.npjobs = (g.nseg + 63) / 64;
+    g.ndjobs = (g.nchunks + 63) / 64;
+    return g;
+}
+
+// ------------------------------------------------------------------------------------------------
+// parse: the per-lane ring reader.  Ring-local word i of lane l lives at LDS dword i*64 + l; the ring
+// epoch's word 0 is segment-relative word 4*kbase; words 16..19 mirror 0..3, so a reader in the epoch's
+// last phase fetches ahead without wrapping, and after that phase every address moves back 16 words.
+struct Ring3 {
+    uint32_t* L;
+    uint32_t lc;                                    // lane * 4
+    uint32_t a, b, c, s, addr;                      // window (a:b) from bit 32 - s of a, c, next fetch address
+    int pos;                                        // segment-relative bit
+    __device__ __forceinline__ uint32_t R(int i) const { return L[(i << 6) + (int)(lc >> 2)]; }
+    __device__ __forceinline__ void init(int p, int kbase) {
+        const int wi = (p - 1) >> 5;                // word holding bit p - 1 (floor for p <= 0)
+        const int li = wi - 4 * kbase;
+        s = (uint32_t)(32 * (wi + 1) - p);
+        a = R(max(li, 0)); b = R(li + 1); c = R(li + 2);
+        addr = ((uint32_t)(li + 3) << 8) | lc;
+        pos = p;
+    }
+    __device__ __forceinline__ void put(int slot, uint4 v) {
+        L[((slot * 4 + 0) << 6) + (lc >> 2)] = v.x; L[((slot * 4 + 1) << 6) + (lc >> 2)] = v.y;
+        L[((slot * 4 + 2) << 6) + (lc >> 2)] = v.z; L[((slot * 4 + 3) << 6) + (lc >> 2)] = v.w;
+        if (slot == 0) {
+            L[(16 << 6) + (lc >> 2)] = v.x; L[(17 << 6) + (lc >> 2)] = v.y;
+            L[(18 << 6) + (lc >> 2)] = v.z; L[(19 << 6) + (lc >> 2)] = v.w;
+        }
+    }
+    // walk until pos >= pend; tokens stepped
+    __device__ __forceinline__ int walk(int pend, const uint8_t* tl) {
+        int n = 0;
+        while (pos < pend) {
+            const uint32_t nx = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(L) + addr);
+            const uint32_t t = __builtin_amdgcn_alignbit(a, b, s);
+            const int len = tl[t >> 23];
+            uint32_t d;
+            const bool adv = __builtin_usub_overflow(s, (uint32_t)len, &d);
+            s = d & 31u;
+            pos += len;
+            a = adv ? b : a;
+            b = adv ? c : b;
+            c = adv ? nx : c;
+            addr += adv ? 256u : 0u;
+            n++;
+        }
+        return n;
+    }
+};
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+template <int CT>
+__global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ s, Params P, Dec3Bufs D3,
+                                                    const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                                                    long long num, uint32_t epoch) {
+    __shared__ uint32_t ring[(D3_RING + 4) * 64];
+    __shared__ uint8_t tl[512];
+    const int lane = threadIdx.x;
+    build_lut_len<CT>(tl, P, lane, 64);
+    const Geo3 G = geo3(dev_nbits, host_nbits, D3.seg);
+    const int seg = G.seg;
+    const __amdgpu_buffer_rsrc_t rs = stream_rsrc(s, D3.capw);
+    const bool decline = G.nchunks > D3.max_chunks || runs_mode(CT, G.nbits, num);
+    if (decline && blockIdx.x == 0 && lane == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_RUNS);
+    __syncthreads();
+    Ring3 r;
+    r.L = ring;
+    r.lc = (uint32_t)lane << 2;
+    constexpr int kb = -2 * D3_PRE;                 // first pre-walk phase (128 bits each)
+    while (!decline) {
+        unsigned job = 0;
+        if (lane == 0) job = atomicAdd(&D3.ctr[0], 1u);
+        job = __builtin_amdgcn_readfirstlane(job);     // wave-uniform (SGPR)
+        if ((long long)job >= G.npjobs) break;
+        const long long sidx = (long long)job * 64 + lane;              // this lane's segment
+        const long long sbit = sidx * seg * 256;
+        const bool act = sidx < G.nseg;
+        const int lim = act ? (int)min((long long)G.nbits - sbit, (long long)seg * 256 + 64) : -(1 << 30);
+        const long long gw0 = sbit >> 5;
+        const long long c0 = sidx * seg;                                   // first chunk of the segment
+        P3_T(t0);
+
+        // ---- main walk: pre-walk from 1024 bits before the segment, then its chunks
+        r.put(0, load_w4(rs, G.nbytes, gw0 + 4 * kb));
+        r.put(1, load_w4(rs, G.nbytes, gw0 + 4 * (kb + 1)));
+        uint4 q0 = load_w4(rs, G.nbytes, gw0 + 4 * (kb + 2));
+        int kbase = kb;
+        r.init(128 * kb, kbase);
+        if (!act) r.pos = 1 << 30;
+        uint32_t tot = 0;
+        int e0 = 0;
+        for (int c = kb / 2; c < seg; c++) {
+            const int k = 2 * c;
+            const uint4 q1 = load_w4(rs, G.nbytes, gw0 + 4 * (k + 3));
+            if (c == 0 && sidx == 0) r.init(0, kbase);                     // the stream's first bit
+            const int e = r.pos - 256 * c;
+            const int n0 = r.walk(min(128 * (k + 1), lim), tl);
+            r.put((k + 2 - kb) & 3, q0);
+            q0 = load_w4(rs, G.nbytes, gw0 + 4 * (k + 4));
+            const int n1 = r.walk(min(128 * (k + 2), lim), tl);
+            r.put((k + 3 - kb) & 3, q1);
+            if (((k + 1 - kb) & 3) == 3) { kbase += 4; r.addr -= 4096u; }
+            if (c >= 0) {
+                const uint32_t cnt = (uint32_t)(n0 + n1);
+                if (act && c0 + c < G.nchunks) D3.rec[c0 + c] = (uint16_t)((uint32_t)(e & 31) | (cnt << 8));
+                tot += cnt;
+                if (c == 0) e0 = e;
+            }
+        }
+        const int X = r.pos - 256 * seg;                                 // entry of the next segment
+        P3_T(t1);
+        P3_ADD(0, t1 - t0);
+#ifdef DC_DEC3_PROF
+        { const uint32_t tt = wave_incl_scan(act ? tot : 0u, lane); if (lane == 63) atomicAdd(&g_prof3[4], (unsigned long long)tt); }
+#endif
+        if (lane == 63) st_relaxed(&D3.pexit[job], ((uint64_t)epoch << 32) | (uint32_t)(X & 0xFFFF));
+
+        // ---- links: this segment's first entry = the previous segment's exit
+        int xprev = __shfl_up(X, 1, 64);
+        if (lane == 0 && act && sidx > 0) {
+            unsigned spins = 0;
+            uint64_t v;
+            while (((v = ld_relaxed(&D3.pexit[job - 1])) >> 32) != (uint64_t)epoch) {
+                if (++spins > (1u << 22) || declined_now(D3)) { atomicOr(D3.err, D3_DECLINE | 16u); break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            xprev = (int)(v & 0xFFFF);
+        }
+        P3_T(t2);
+        P3_ADD(1, t2 - t1);
+        // ---- repair: a lane whose entry is not its predecessor's exit re-walks from that exit, rewriting
+        // its records until the path meets a recorded entry again; a path that reaches the segment end
+        // without meeting it moves the exit, and the successor is checked again (rounds within the wave;
+        // the next job checked its link against this job's main-walk exit, so a moved last exit declines)
+        int xin = xprev, ecur = e0, Xcur = X, rounds = 0;
+        bool bad = act && sidx > 0 && ecur != xin;
+        while (__any(bad)) {
+            if (++rounds > 64) { if (lane == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK); break; }
+            r.put(0, load_w4(rs, G.nbytes, gw0));
+            r.put(1, load_w4(rs, G.nbytes, gw0 + 4));
+            q0 = load_w4(rs, G.nbytes, gw0 + 8);
+            r.init(bad ? xin : 0, 0);
+            bool live = bad;
+            if (!live) r.pos = 1 << 30;
+            for (int c = 0; c < seg; c++) {
+                const int k = 2 * c;
+                const uint4 q1 = load_w4(rs, G.nbytes, gw0 + 4 * (k + 3));
+                const bool inside = c0 + c < G.nchunks;
+                const uint32_t old = (live && inside) ? (uint32_t)D3.rec[c0 + c] : 0u;
+                if (live && c > 0 && r.pos - 256 * c == (int)(old & 31u) && 256 * c < lim) {
+                    live = false;                                           // met the recorded path
+                    r.pos = 1 << 30;
+                }
+                const int e = r.pos - 256 * c;
+                const int n0 = r.walk(min(128 * (k + 1), lim), tl);
+                r.put((k + 2) & 3, q0);
+                q0 = load_w4(rs, G.nbytes, gw0 + 4 * (k + 4));
+                const int n1 = r.walk(min(128 * (k + 2), lim), tl);
+                r.put((k + 3) & 3, q1);
+                if (((k + 1) & 3) == 3) r.addr -= 4096u;
+                if (live) {
+                    const uint32_t cnt = (uint32_t)(n0 + n1);
+                    if (inside) D3.rec[c0 + c] = (uint16_t)((uint32_t)(e & 31) | (cnt << 8));
+                    tot += cnt - (old >> 8);
+                    if (c == 0) ecur = e;
+                }
+            }
+            const bool whole = 256 * seg < lim;                              // a successor segment exists
+            const int Xn = live ? r.pos - 256 * seg : Xcur;
+            const bool moved = live && whole && Xn != Xcur;
+            Xcur = Xn;
+            if (moved && lane == 63) atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK);
+            const int xp = __shfl_up(Xcur, 1, 64);
+            const bool mp = __shfl_up((int)moved, 1, 64) != 0;
+            bad = lane >= 1 && act && mp && ecur != xp;
+            xin = bad ? xp : xin;
+        }
+
+        P3_T(t3);
+        P3_ADD(2, t3 - t2);
+        P3_ADD(3, rounds);
+        P3_ADD(5, 1);
+        // ---- token offsets: the job's total and every decode job's first token relative to the job
+        const uint32_t inc = wave_incl_scan(tot, lane);
+        if (lane == 63) D3.ptot[job] = inc;
+        if (((lane * seg) & 63) == 0) {
+            const long long dj = (long long)job * seg + (lane * seg) / 64;
+            if (dj * 64 < D3.max_chunks) D3.rel[dj] = inc - tot;
+        }
+    }
+    if (lane == 0) {
+        __threadfence();
+        if (atomicAdd(&D3.ctr[2], 1u) == gridDim.x - 1) { atomicExch(&D3.ctr[0], 0u); atomicExch(&D3.ctr[2], 0u); }
+    }
+}
+
+// exclusive scan of the parse jobs' token counts (one workgroup); a stream with fewer tokens than num
+// is left to the other decoder (it reads past the stream as the reference does)
+__global__ __launch_bounds__(1024) void scan3_kernel(Dec3Bufs D3, const unsigned long long* dev_nbits,
+                                                     unsigned long long host_nbits, long long num) {
+    __shared__ unsigned long long wtot[16];
+    const Geo3 G = geo3(dev_nbits, host_nbits, D3.seg);
+    const long long np = G.npjobs;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const long long per = (np + 1023) / 1024;
+    const long long t0 = tid * per, t1 = min(np, t0 + per);
+    unsigned long long sum = 0;
+    for (long long t = t0; t < t1; t++) sum += D3.ptot[t];
+    unsigned long long inc = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long u = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += u;
+    }
+    if (lane == 63) wtot[wid] = inc;
+    __syncthreads();
+    unsigned long long wpre = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < 16; w++) { wpre += w < wid ? wtot[w] : 0ull; all += wtot[w]; }
+    unsigned long long run = wpre + inc - sum;
+    for (long long t = t0; t < t1; t++) { D3.pbase[t] = run; run += D3.ptot[t]; }
+    if (tid == 0) {
+        D3.pbase[np] = all;
+        if ((long long)all < num) atomicOr(D3.err, D3_DECLINE | D3_WHY_SHORT);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// decode
+struct Lut3 {
+    uint16_t meta[512];                 // sh | len << 8
+    uint2 kv[512];                      // pattern = ((t >> sh) & x) | y; 3-bit codes: {0, 0}
+};
+
+template <int CT>
+__device__ __forceinline__ void build_lut3(Lut3& T, const Params& P, int tid, int nthr) {
+    build_lut_meta<CT>(T.meta, P, tid, nthr);
+    for (int i = tid; i < 512; i += nthr) {
+        const uint32_t t = (uint32_t)i << 23;
+        uint32_t keep, add;
+        if (CT != 6 && (int)t < 0) {
+            keep = 0u; add = 0u;                     // '1xx': zero, or a prediction (filled in by the caller)
+        } else if (CT == 11) {
+            keep = 0xFFFFFFFFu; add = 0u;
+        } else {
+            const int len = token_len_bf<6>(t, P);   // raw length 9 + m(E)
+            const uint32_t y = len >= 32 ? 0u : 0xFFFFFFFFu >> len;
+            keep = ~y; add = y & ~(y >> 1);
+            if (CT == 7 && (t & P.hm) == P.hm) {
+                const bool f1 = (t >> P.fsh) & 1u;
+                keep = f1 ? P.k1 : P.k0;
+                add = f1 ? P.c1 : P.c0;
+            }
+        }
+        T.kv[i] = make_uint2(keep, add);
+    }
+}
+
+struct Rd3 {                                        // reader over a lane's 12 staged words, [word][lane]
+    const uint32_t* L;
+    uint32_t a, b, c, s, addr;
+    __device__ __forceinline__ void init(const uint32_t* Lw, int lane, int p) {   // p in [0, 32)
+        L = Lw;
+        const int wi = (p - 1) >> 5;                   // -1 or 0
+        s = (uint32_t)(32 * (wi + 1) - p);
+        a = L[(max(wi, 0) << 6) + lane]; b = L[((wi + 1) << 6) + lane]; c = L[((wi + 2) << 6) + lane];
+        addr = ((uint32_t)(wi + 3) << 8) | ((uint32_t)lane << 2);
+    }
+    __device__ __forceinline__ uint32_t fetch() const {
+        return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(L) + addr);
+    }
+    __device__ __forceinline__ uint32_t peek() const { return __builtin_amdgcn_alignbit(a, b, s); }
+    __device__ __forceinline__ void step(uint32_t nx, int len) {
+        uint32_t d;
+        const bool adv = __builtin_usub_overflow(s, (uint32_t)len, &d);
+        s = d & 31u;
+        a = adv ? b : a;
+        b = adv ? c : b;
+        c = adv ? nx : c;
+        addr += adv ? 256u : 0u;
+    }
+};
+
+// the previous decode job's k-th last value (k = 1..3), published by that job's wave
+__device__ __forceinline__ float prev_job_value(const Dec3Bufs& D3, long long job, int k, uint32_t epoch) {
+    const uint64_t* p = &D3.hist[(job - 1) * 3 + (k - 1)];
+    unsigned spins = 0;
+    uint64_t v;
+    while (((v = ld_relaxed(p)) >> 32) != (uint64_t)epoch) {
+        if (++spins > (1u << 22) || declined_now(D3)) { atomicOr(D3.err, D3_DECLINE | 16u); return 0.0f; }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return __uint_as_float((uint32_t)v);
+}
+
+template <int CT>
+__global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict__ s, Params P, Dec3Bufs D3,
+                                                     const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                                                     float* __restrict__ out, long long num, uint32_t epoch) {
+    __shared__ Lut3 T;
+    __shared__ uint32_t stg[4][12 * 64];
+    __shared__ __attribute__((aligned(16))) float obuf[4][D3_CAP];
+    build_lut3<CT>(T, P, threadIdx.x, 256);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const Geo3 G = geo3(dev_nbits, host_nbits, D3.seg);
+    const __amdgpu_buffer_rsrc_t rs = stream_rsrc(s, D3.capw);
+    const bool declined = (__hip_atomic_load(D3.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & D3_DECLINE) != 0;
+    // patterns without a midpoint bit can equal the -1.0f history sentinel: check every value then
+    const bool chk_all = (CT == 6 && P.B >= 23) || (CT == 7 && (P.mask17 >> 16) != 0u && P.mm == 23);
+    uint32_t* L = stg[w];
+    float* ob = obuf[w];
+    while (!declined) {
+        P3_T(u0);
+        unsigned job = 0;
+        if (lane == 0) job = atomicAdd(&D3.ctr[1], 1u);
+        job = __builtin_amdgcn_readfirstlane(job);     // wave-uniform (SGPR)
+        if ((long long)job >= G.ndjobs) break;
+        const long long g = (long long)job * 64 + lane;
+        const uint32_t rc = g < G.nchunks ? (uint32_t)D3.rec[g] : 0u;
+        const int e = (int)(rc & 31u), n = (int)(rc >> 8);
+        const unsigned long long base = D3.pbase[job / G.seg] + D3.rel[job];
+        const uint32_t inc = wave_incl_scan((uint32_t)n, lane);
+        const int off = (int)inc - n;
+        const int Tn = (int)__builtin_amdgcn_readlane(inc, 63);
+        const int al = (int)(base & 3ull);
+        P3_T(u1);
+        P3_ADD(8, u1 - u0);
+        // (no `continue` after a lane-conditional store here: the structurizer then peeled the loop head
+        // for lanes 1..63 with lane 0 inactive, and their readfirstlane claimed job 0 again, forever)
+        const bool fits = al + Tn <= D3_CAP;
+        if (!fits) atomicOr(D3.err, D3_DECLINE | D3_WHY_DENSE);        // every lane: OR is idempotent
+        if (fits) {
+        {   // stage the chunk's 8 words + 4 words of the next chunk
+            const uint4 v0 = load_w4(rs, G.nbytes, 8 * g), v1 = load_w4(rs, G.nbytes, 8 * g + 4),
+                        v2 = load_w4(rs, G.nbytes, 8 * g + 8);
+            L[(0 << 6) + lane] = v0.x; L[(1 << 6) + lane] = v0.y; L[(2 << 6) + lane] = v0.z; L[(3 << 6) + lane] = v0.w;
+            L[(4 << 6) + lane] = v1.x; L[(5 << 6) + lane] = v1.y; L[(6 << 6) + lane] = v1.z; L[(7 << 6) + lane] = v1.w;
+            L[(8 << 6) + lane] = v2.x; L[(9 << 6) + lane] = v2.y; L[(10 << 6) + lane] = v2.z; L[(11 << 6) + lane] = v2.w;
+        }
+        P3_T(u2);
+        P3_ADD(9, u2 - u1);
+        const int o0 = al + off;
+        int pend = 0;
+        bool sent = false;
+        {
+            Rd3 r;
+            r.init(L, lane, e);
+            int o = o0;
+            for (int t = 0; t < n; t++) {
+                const uint32_t nx = r.fetch();
+                const uint32_t tk = r.peek();
+                const uint32_t idx = tk >> 23;
+                const uint32_t meta = T.meta[idx];
+                const uint2 kv = T.kv[idx];
+                uint32_t v = ((tk >> (meta & 31u)) & kv.x) | kv.y;
+                if (CT != 6) {
+                    const uint32_t cc = tk >> 29;                            // 5..7: '101' '110' '111'
+                    if (__builtin_expect(__any(cc >= 5u), 0)) {
+                        if (cc >= 5u) {
+                            const int need = (int)cc - 4;
+                            if (t < need || t - need < pend || (g == 0 && t < 3)) {
+                                pend = t + 1;                                // needs the previous chunk's values
+                                sent |= g == 0 && t < 3;                     // a prediction among the stream's first 3
+                                v = 0u;
+                            } else {
+                                const float pv = predict_value(need, ob[o - 1], ob[o - 2], ob[o - 3]);
+                                v = __float_as_uint(pv);
+                                sent |= v == 0xBF800000u;
+                            }
+                        }
+                    }
+                }
+                ob[o] = __uint_as_float(v);
+                o++;
+                r.step(nx, (int)(meta >> 8));
+            }
+        }
+        P3_T(u3);
+        P3_ADD(10, u3 - u2);
+        // ---- pending prefixes, lane by lane in stream order (rare)
+        unsigned long long pm = __ballot(pend > 0);
+        P3_ADD(14, __popcll(pm));
+        P3_ADD(15, Tn);
+        while (pm) {
+            const int Lp = __ffsll((long long)pm) - 1;
+            pm &= pm - 1;
+            if (lane == Lp) {
+                float h[3];
+#pragma unroll
+                for (int k = 1; k <= 3; k++) {
+                    const int i = o0 - k;
+                    // (job 0 has no predecessor: a prediction among its first tokens declined above)
+                    h[k - 1] = i >= al ? ob[i] : (job > 0 ? prev_job_value(D3, job, al - i, epoch) : 0.0f);
+                }
+                float b1 = h[0], b2 = h[1], b3 = h[2];
+                Rd3 r;
+                r.init(L, lane, e);
+                for (int t = 0; t < pend; t++) {
+                    const uint32_t nx = r.fetch();
+                    const uint32_t tk = r.peek();
+                    const uint32_t idx = tk >> 23;
+                    const uint32_t meta = T.meta[idx];
+                    const uint2 kv = T.kv[idx];
+                    uint32_t v = ((tk >> (meta & 31u)) & kv.x) | kv.y;
+                    const uint32_t cc = tk >> 29;
+                    if (CT != 6 && cc >= 5u) {
+                        v = __float_as_uint(predict_value((int)cc - 4, b1, b2, b3));
+                        sent |= v == 0xBF800000u;
+                    }
+                    ob[o0 + t] = __uint_as_float(v);
+                    b3 = b2; b2 = b1; b1 = __uint_as_float(v);
+                    r.step(nx, (int)(meta >> 8));
+                }
+            }
+        }
+        P3_T(u4);
+        P3_ADD(11, u4 - u3);
+        // ---- publish the job's last three values (the next job's first chunk may need them)
+        if (lane < 3 && Tn >= 3)
+            st_relaxed(&D3.hist[(long long)job * 3 + lane], ((uint64_t)epoch << 32) | __float_as_uint(ob[al + Tn - 1 - lane]));
+        // ---- store: whole float4s of the output's 16-byte grid
+        const int span = al + Tn;
+        const int Q = (span + 3) >> 2;
+        const long long gi0 = (long long)(base - (unsigned long long)al);
+        bool sv = false;
+        for (int q = lane; q < Q; q += 64) {
+            const float4 v = reinterpret_cast<const float4*>(ob)[q];
+            const long long gi = gi0 + 4 * q;
+            if (chk_all)
+                sv |= __float_as_uint(v.x) == 0xBF800000u || __float_as_uint(v.y) == 0xBF800000u ||
+                      __float_as_uint(v.z) == 0xBF800000u || __float_as_uint(v.w) == 0xBF800000u;
+            if (4 * q >= al && 4 * q + 4 <= span && gi + 4 <= num) {
+                *reinterpret_cast<float4*>(out + gi) = v;
+            } else {
+                const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    if (4 * q + i >= al && 4 * q + i < span && gi + i < num) out[gi + i] = vv[i];
+            }
+        }
+        if (__any(sent || sv) && lane == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_SENT);
+        P3_T(u5);
+        P3_ADD(12, u5 - u4);
+        P3_ADD(13, 1);
+        }
+    }
+    // the waves of a block finish independently: the last WAVE out resets the tickets for the next call
+    if (lane == 0) {
+        __threadfence();
+        if (atomicAdd(&D3.ctr[3], 1u) == 4 * gridDim.x - 1) { atomicExch(&D3.ctr[1], 0u); atomicExch(&D3.ctr[3], 0u); }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+#define DC_DISPATCH_3(CTV, KER, ...)                                                                 \
+    switch (CTV) {                                                                                   \
+        case 5: hipLaunchKernelGGL(KER<5>, __VA_ARGS__); break;                                      \
+        case 6: hipLaunchKernelGGL(KER<6>, __VA_ARGS__); break;                                      \
+        case 7: hipLaunchKernelGGL(KER<7>, __VA_ARGS__); break;                                      \
+        case 11: hipLaunchKernelGGL(KER<11>, __VA_ARGS__); break;                                    \
+        default: return -2;                                                                          \
+    }
+
+static int resident3(const void* f, int threads) {
+    int dev = 0, ncu = 256, per = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, threads, 0) != hipSuccess || per < 1) per = 1;
+    return per * ncu;
+}
+
+// segment length for a stream of at most max_chunks chunks: long segments (fewer pre-walk bits per
+// token) as long as there are about two segments per resident lane (latency hiding)
+extern "C" int dc_decode3_seg(long long max_chunks) {
+    static long long lanes = 0;
+    if (!lanes) lanes = 64ll * resident3((const void*)parse3_kernel<7>, 64);
+    // at least 16 chunks (4096 bits): a link whose pre-walk had not synchronised is repaired within the
+    // segment in practice; with shorter segments a repair that runs off the segment end moves the exit
+    int seg = 16;
+    while (seg < 32 && (long long)seg * 2 * lanes * 2 <= max_chunks) seg *= 2;
+    return seg;
+}
+
+// DC_DEC3_DEBUG=1: wait for every kernel (at most 2 s each) and report one that does not finish
+static void dbg_wait(const char* what, hipStream_t st) {
+    static int on = -1;
+    if (on < 0) on = getenv("DC_DEC3_DEBUG") ? 1 : 0;
+    if (!on) return;
+    for (int i = 0; i < 2000; i++) {
+        if (hipStreamQuery(st) == hipSuccess) return;
+        usleep(1000);
+    }
+    fprintf(stderr, "[dcamd] %s has not finished after 2 s\n", what);
+    fflush(stderr);
+}
+
+// DC_DEC3_DEBUG: a snapshot of the decoder state while a kernel is still running (another stream)
+static void dbg_dump(const Dec3Bufs* D3) {
+    static int on = -1;
+    if (on < 0) on = getenv("DC_DEC3_DEBUG") ? 1 : 0;
+    if (!on) return;
+    hipStream_t s2;
+    if (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) != hipSuccess) return;
+    unsigned ctr[4] = {0}, err = 0;
+    uint64_t hist[12] = {0};
+    unsigned long long pb[4] = {0};
+    uint32_t rel[4] = {0}, pt[4] = {0};
+    uint16_t rec[16] = {0};
+    (void)hipMemcpyAsync(ctr, D3->ctr, sizeof ctr, hipMemcpyDeviceToHost, s2);
+    (void)hipMemcpyAsync(&err, D3->err, 4, hipMemcpyDeviceToHost, s2);
+    (void)hipMemcpyAsync(hist, D3->hist, sizeof hist, hipMemcpyDeviceToHost, s2);
+    (void)hipMemcpyAsync(pb, D3->pbase, sizeof pb, hipMemcpyDeviceToHost, s2);
+    (void)hipMemcpyAsync(rel, D3->rel, sizeof rel, hipMemcpyDeviceToHost, s2);
+    (void)hipMemcpyAsync(pt, D3->ptot, sizeof pt, hipMemcpyDeviceToHost, s2);
+    (void)hipMemcpyAsync(rec, D3->rec, sizeof rec, hipMemcpyDeviceToHost, s2);
+    (void)hipStreamSynchronize(s2);
+    fprintf(stderr, "[dcamd] ctr %u %u %u %u err 0x%x seg %d\n", ctr[0], ctr[1], ctr[2], ctr[3], err, D3->seg);
+    for (int i = 0; i < 4; i++)
+        fprintf(stderr, "  job %d hist %llx %llx %llx pbase %llu rel %u ptot %u\n", i, (unsigned long long)hist[3 * i],
+                (unsigned long long)hist[3 * i + 1], (unsigned long long)hist[3 * i + 2], pb[i], rel[i], pt[i]);
+    for (int i = 0; i < 16; i++) fprintf(stderr, " rec%d=%u/%u", i, rec[i] & 31u, rec[i] >> 8);
+    fprintf(stderr, "\n");
+    fflush(stderr);
+    (void)hipStreamDestroy(s2);
+}
+
+extern "C" int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                                 const Params* P, const Dec3Bufs* D3, float* out, long long num, uint32_t epoch,
+                                 hipStream_t st) {
+    static int gp[12], gd[12];
+    const int ci = (P->ct > 0 && P->ct < 12) ? P->ct : 0;
+    if (!gp[ci]) {
+        const void* fp = P->ct == 5 ? (const void*)parse3_kernel<5> : P->ct == 6 ? (const void*)parse3_kernel<6>
+                       : P->ct == 7 ? (const void*)parse3_kernel<7> : (const void*)parse3_kernel<11>;
+        const void* fd = P->ct == 5 ? (const void*)decode3_kernel<5> : P->ct == 6 ? (const void*)decode3_kernel<6>
+                       : P->ct == 7 ? (const void*)decode3_kernel<7> : (const void*)decode3_kernel<11>;
+        gp[ci] = resident3(fp, 64);
+        gd[ci] = resident3(fd, 256);
+    }
+    const long long maxseg = (D3->max_chunks + D3->seg - 1) / D3->seg;
+    const long long maxpj = (maxseg + 63) / 64, maxdj = (D3->max_chunks + 63) / 64;
+    const int g1 = (int)std::max<long long>(1, std::min<long long>(maxpj, gp[ci]));
+    const int g3 = (int)std::max<long long>(1, std::min<long long>((maxdj + 3) / 4, gd[ci]));
+    dc_mark_phase(4, st);
+    DC_DISPATCH_3(P->ct, parse3_kernel, dim3(g1), dim3(64), 0, st, s, *P, *D3, dev_nbits, host_nbits, num, epoch);
+    dbg_wait("parse3_kernel", st);
+    dc_mark_phase(5, st);
+    hipLaunchKernelGGL(scan3_kernel, dim3(1), dim3(1024), 0, st, *D3, dev_nbits, host_nbits, num);
+    dbg_wait("scan3_kernel", st);
+    dc_mark_phase(6, st);
+    DC_DISPATCH_3(P->ct, decode3_kernel, dim3(g3), dim3(256), 0, st, s, *P, *D3, dev_nbits, host_nbits, out, num, epoch);
+    dbg_wait("decode3_kernel", st);
+    if (getenv("DC_DEC3_DEBUG") && hipStreamQuery(st) != hipSuccess) dbg_dump(D3);
+    dc_mark_phase(7, st);
+    dc_mark_next_set();
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int dc_dec3_prof_read(unsigned long long* out, int reset) {
+#ifdef DC_DEC3_PROF
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof3), sizeof g_prof3) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long z[32] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof3), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+#else
+    (void)out; (void)reset;
+    return -1;
+#endif
+}
+
+}  // namespace dc

@@ -767,9 +767,10 @@ __global__ __launch_bounds__(GROUP) void decode_kernel_fast(const uint8_t* __res
     const int c = threadIdx.x;
     // a runs-mode stream whose tile chain failed (tile_fix reported an unknown entry) is resolved exactly
     // by dc_decode_finish (resolve_kernel, then this kernel again): nothing to decode now
-    if (pl.runs && (__hip_atomic_load(D.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 8u)) return;
+    // (the tile loop is skipped, not the epilogue: the ticket counters below must still be reset)
+    const bool skip_all = pl.runs && (__hip_atomic_load(D.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 8u);
     build_lut<CT>(S.T, P, c, GROUP);                                  // visible after the first barrier
-    while (true) {
+    while (!skip_all) {
         if (c == 0) S.tile = (long long)atomicAdd(&D.ctr[4], 1u);
         __syncthreads();
         const long long t = S.tile;

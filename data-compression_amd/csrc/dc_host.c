@@ -60,6 +60,13 @@ typedef struct {
     unsigned long long dec_nbits;
     int dec_runs;                 /* the last decode's stream is in runs mode (Plan.runs) */
     int dec_shard;                   /* shard mode of the pending decode (DecBufs.shard) */
+    Dec3Bufs D3;                     /* segment decoder (dc_decode3.hip) */
+    void* dec3_pool;
+    long long dec3_cap;              /* 256-bit chunks the pool holds */
+    int dec3_used;                   /* the pending decode ran the segment decoder */
+    int dec3_last;                   /* the last finished decode's values came from it */
+    const unsigned long long* dec_dnbits;   /* the pending decode's device bit count (or NULL) */
+    unsigned long long dec_hnbits;          /* ... or its host bit count */
     const float* dec_hin;            /* its incoming values (shard mode 2) */
     int shard_deferred;              /* 1: tile-0 prefixes wait for dc_decode_shard_fix, 2: later tiles too */
     void* shard_buf; size_t shard_cap;
@@ -506,9 +513,68 @@ static int dec_next_epoch(void) {
         HIPCHK(hipMemsetAsync(G.D.gran, 0, (size_t)GR * 34 * 8, G.st));
         HIPCHK(hipMemsetAsync(G.D.hist, 0, (size_t)GR * 6 * 8, G.st));
         HIPCHK(hipMemsetAsync(G.D.tflag, 0, (size_t)GR * 8, G.st));
+        if (G.dec3_pool) {
+            HIPCHK(hipMemsetAsync(G.D3.pexit, 0, (size_t)(G.dec3_cap + 4096) / 256 * 8 + 64 * 8, G.st));
+            HIPCHK(hipMemsetAsync(G.D3.hist, 0, (size_t)((G.dec3_cap + 4096) / 64 + 64) * 3 * 8, G.st));
+        }
         G.dec_epoch = 1;
     }
     return DC_OK;
+}
+
+/* segment decoder buffers for streams of up to max_chunks 256-bit chunks */
+static int dec3_ensure(long long max_chunks) {
+    const int seg = dc_decode3_seg(max_chunks);
+    if (max_chunks <= G.dec3_cap && seg == G.D3.seg) return DC_OK;
+    if (max_chunks > G.dec3_cap) {
+        if (G.dec3_pool) HIPCHK(hipFree(G.dec3_pool));
+        G.dec3_pool = NULL;
+        const long long C = max_chunks + 4096;
+        const long long DJ = C / 64 + 64, PJ = C / (64 * 4) + 64;
+        size_t sz[7], off = 0, tot = 0;
+        sz[0] = (size_t)C * 2;                /* rec */
+        sz[1] = (size_t)DJ * 4;               /* rel */
+        sz[2] = (size_t)PJ * 4;               /* ptot */
+        sz[3] = (size_t)(PJ + 1) * 8;         /* pbase */
+        sz[4] = (size_t)PJ * 8;               /* pexit */
+        sz[5] = (size_t)DJ * 3 * 8;           /* hist */
+        sz[6] = 64;                           /* ctr */
+        for (int i = 0; i < 7; i++) tot += (sz[i] + 255) & ~(size_t)255;
+        HIPCHK(hipMalloc(&G.dec3_pool, tot));
+        HIPCHK(hipMemsetAsync(G.dec3_pool, 0, tot, G.st));
+        char* b = (char*)G.dec3_pool;
+        void* ptr[7];
+        for (int i = 0; i < 7; i++) { ptr[i] = b + off; off += (sz[i] + 255) & ~(size_t)255; }
+        G.D3.rec = (uint16_t*)ptr[0];
+        G.D3.rel = (uint32_t*)ptr[1];
+        G.D3.ptot = (uint32_t*)ptr[2];
+        G.D3.pbase = (unsigned long long*)ptr[3];
+        G.D3.pexit = (uint64_t*)ptr[4];
+        G.D3.hist = (uint64_t*)ptr[5];
+        G.D3.ctr = (unsigned*)ptr[6];
+        G.dec3_cap = max_chunks;
+    }
+    G.D3.max_chunks = G.dec3_cap;
+    G.D3.seg = seg;
+    return DC_OK;
+}
+
+/* streams of at least this capacity use the segment decoder (DC_DEC3_MIN_BYTES; DC_DEC3=0 disables it) */
+static long long g_dec3_min = -2;
+static long long dec3_min_bytes(void) {
+    if (g_dec3_min == -2) {
+        const char* d = getenv("DC_DEC3");
+        const char* e = getenv("DC_DEC3_MIN_BYTES");
+        g_dec3_min = (d && *d == '0') ? -1 : ((e && *e) ? atoll(e) : (1ll << 20) + 1);
+    }
+    return g_dec3_min;
+}
+/* < -1: the default; -1 disables the segment decoder; returns the previous value */
+int dc_last_decode_was_v3(void) { return G.dec3_last; }
+long long dc_set_decode3_min_bytes(long long v) {
+    const long long old = dec3_min_bytes();
+    g_dec3_min = v < -1 ? (1ll << 20) + 1 : v;
+    return old;
 }
 
 #define DEC_ROUNDS 3
@@ -533,9 +599,23 @@ int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsig
     if ((rc = dec_next_epoch())) return rc;
     Params P;
     make_params(&P, ct, type, mask17);
-    if (DV(dc_launch_decode_fast)((const uint8_t*)d_stream, nbytes >= 0 ? NULL : d_nbits,
-                              nbytes >= 0 ? (unsigned long long)nbytes * 8ull : 0ull, max_chunks, &P, &G.D,
-                              (float*)d_out, num, G.dec_epoch, G.st))
+    const long long m3 = dec3_min_bytes();
+    /* the segment decoder reads whole 16-byte groups through a buffer resource (32-bit byte range): every
+       stream byte must lie in one inside max_bytes, and max_bytes must stay below 2 GiB */
+    const long long need16 = nbytes >= 0 ? (nbytes + 15) / 16 * 16 : 0;
+    G.dec3_used = m3 >= 0 && max_bytes >= m3 && max_bytes >= 16 && max_bytes >= need16 && max_bytes < (1ll << 31) && !G.D.shard &&
+                  !((uintptr_t)d_stream & 15u) && !((uintptr_t)d_out & 15u);
+    G.dec_dnbits = nbytes >= 0 ? NULL : d_nbits;
+    G.dec_hnbits = nbytes >= 0 ? (unsigned long long)nbytes * 8ull : 0ull;
+    if (G.dec3_used) {
+        if ((rc = dec3_ensure((max_bytes * 8 + 255) / 256 + 1))) return rc;
+        G.D3.err = G.D.err;
+        G.D3.capw = max_bytes / 16 * 4;
+        if (dc_launch_decode3((const uint8_t*)d_stream, G.dec_dnbits, G.dec_hnbits, &P, &G.D3, (float*)d_out, num,
+                              G.dec_epoch, G.st))
+            return seterr(DC_ERR_HIP, "decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+    } else if (DV(dc_launch_decode_fast)((const uint8_t*)d_stream, G.dec_dnbits, G.dec_hnbits, max_chunks, &P, &G.D,
+                                         (float*)d_out, num, G.dec_epoch, G.st))
         return seterr(DC_ERR_HIP, "decode launch failed: %s", hipGetErrorString(hipGetLastError()));
     G.dec_pending = 1;
     G.dec_queued++;
@@ -585,6 +665,20 @@ int dc_decode_finish(void) {
         HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
         return seterr(DC_ERR_STREAM, "decoder status 0x%x over %d queued decodes: an earlier decode left the fast "
                                      "path and was not completed (call dc_decode_finish after each decode)", err, queued);
+    }
+    G.dec3_last = G.dec3_used && !(err & 512u);
+    if ((err & 512u) && G.dec_pending && G.dec3_used) {
+        /* the segment decoder declined the stream (runs mode, an unconverged repair, a dense job, the
+         * history sentinel): decode it again with the chunk-map decoder, then its slow paths below */
+        if (getenv("DC_DEBUG_ERR")) fprintf(stderr, "[dcamd] segment decoder declined (status 0x%x)\n", err);
+        HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
+        G.dec3_used = 0;
+        if ((rc = dec_next_epoch())) return rc;
+        if (DV(dc_launch_decode_fast)(G.dec_s, G.dec_dnbits, G.dec_hnbits, G.dec_max_chunks, &G.dec_P, &G.D, G.dec_out,
+                                      G.dec_num, G.dec_epoch, G.st))
+            return seterr(DC_ERR_HIP, "decode launch failed");
+        rc = read_dec_err(&err);
+        if (rc) return rc;
     }
     if (G.dec_shard == 1 && (err & (256u | 32u))) {  /* shard prefixes waiting for their incoming values */
         G.shard_deferred = (err & 32u) ? 2 : 1;
@@ -933,7 +1027,7 @@ static float* abi_decompress(const char* fn, int ct, const unsigned char* data_b
     if (hipMemcpyAsync(G.d_a, data_bits, (size_t)bytes, hipMemcpyHostToDevice, G.st) != hipSuccess) {
         abi_fail(fn, seterr(DC_ERR_HIP, "H2D copy failed")); memset(out, 0, osz); return out;
     }
-    if ((rc = dc_decode_device(ct, G.d_a, bytes, NULL, bytes, num, type, mask17, G.d_b)) || (rc = dc_decode_finish())) {
+    if ((rc = dc_decode_device(ct, G.d_a, bytes, NULL, bytes + 64, num, type, mask17, G.d_b)) || (rc = dc_decode_finish())) {
         abi_fail(fn, rc); memset(out, 0, osz); return out;
     }
     if (hipMemcpy(out, G.d_b, (size_t)num * 4, hipMemcpyDeviceToHost) != hipSuccess) {

@@ -37,6 +37,8 @@ static double ber(void) {
 }
 
 static int compress_ct(int ct, const double* x, int n, unsigned char** bits, int* bytes, double* mn) {
+    const char* inj = getenv("DC_TEST_FAIL_COMPRESS");   /* test hook: the root's compress fails */
+    if (inj && *inj == '1') return -1;
     double* small = NULL;
     *mn = toSmallDataset_double((double*)x, &small, n);
     if (!small) return -1;
@@ -145,6 +147,9 @@ int MPI_Bcast_bitwise_double(void* buf, int count, MPI_Datatype datatype, int ro
             memcpy(aux, &bytes, sizeof(int));
             memcpy(aux + sizeof(int), &mn, sizeof(double));
             if (bytes) memcpy(aux + HDR64, bits, (size_t)bytes);
+        } else {
+            const int bad = -1;              /* tells every receiver the root failed: it never touches buf */
+            memcpy(aux, &bad, sizeof(int));
         }
         free(bits);
     }

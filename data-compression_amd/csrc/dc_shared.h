@@ -67,6 +67,22 @@ typedef struct DecBufs { /* decoder metadata, sized for the maximum chunk count 
     const float* hin;    /* [3] b1, b2, b3 before the shard (device), shard == 2 */
 } DecBufs;
 
+/* segment decoder (dc_decode3.hip): 256-bit chunks; a parse lane walks a segment of `seg` chunks
+ * after a 1024-bit pre-walk and records every chunk's entry offset and token count */
+typedef struct Dec3Bufs {
+    uint16_t* rec;                 /* [chunk] entry (bits 0..4) | tokens << 8 */
+    uint32_t* rel;                 /* [decode job = 64 chunks] first token, relative to its parse job */
+    uint32_t* ptot;                /* [parse job = 64 segments] tokens */
+    unsigned long long* pbase;     /* [parse job + 1] first token of the parse job (exclusive scan) */
+    uint64_t* pexit;               /* [parse job] epoch << 32 | its last lane's exit (main walk) */
+    uint64_t* hist;                /* [decode job][3] the job's last three values, epoch-tagged granules */
+    unsigned* ctr;                 /* [0] parse ticket, [1] decode ticket, [2] parse done, [3] decode done */
+    unsigned* err;                 /* the DecBufs status word; 512 = this path declined the stream */
+    int seg;                       /* chunks per parse segment: 16 or 32 */
+    long long max_chunks;          /* capacity of rec */
+    long long capw;                /* readable words of the stream buffer (a multiple of 4, >= 4) */
+} Dec3Bufs;
+
 #ifdef __cplusplus
 }  /* namespace dc */
 extern "C" {
@@ -99,6 +115,10 @@ int dc_launch_decode_fast(const uint8_t* s, const unsigned long long* dev_nbits,
                           long long num, uint32_t epoch, dc_hip_stream st);
 int dc_launch_decode_serial(const uint8_t* s, const DC_NS Params* P, const DC_NS DecBufs* D, float* out,
                             long long num, dc_hip_stream st);
+int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                      const DC_NS Params* P, const DC_NS Dec3Bufs* D3, float* out, long long num, uint32_t epoch,
+                      dc_hip_stream st);
+int dc_decode3_seg(long long max_chunks);
 long long dc_ct1_tiles(long long n);
 int dc_launch_ct1_encode(const float* x, long long n, float thr_le, uint32_t* traw, unsigned long long* rawoff,
                          float* raw, char* codes, int* pos1, unsigned* err, dc_hip_stream st);

@@ -44,6 +44,7 @@ EXT_SYMBOLS = [
     "dc64_stream_capacity", "dc64_encode_device", "dc64_encode_result", "dc64_decode_device", "dc64_decode_finish",
     "dc64_last_decode_flags", "dc64_to_small_device", "dc64_med_device", "dc_set_encode_stream",
     "dc_decode_status", "dc_abi_status", "dc_med_sum_device", "dc_type_from_max", "dc_set_small_chunk_max_bytes",
+    "dc_set_decode3_min_bytes", "dc_last_decode_was_v3",
 ]
 
 
@@ -87,6 +88,8 @@ class Lib:
         L.dc_decode_chunk_bits_value.restype = ll
         L.dc_set_small_chunk_max_bytes.argtypes = [ll]
         L.dc_set_small_chunk_max_bytes.restype = ll
+        L.dc_set_decode3_min_bytes.argtypes = [ll]
+        L.dc_set_decode3_min_bytes.restype = ll
         pp = [_f32p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int), C.POINTER(C.c_int)]
         for nm in ("myCompress_bitwise", "myCompress_bitwise_np", "myCompress_bitwise_op"):
             getattr(L, nm).argtypes = pp
@@ -395,6 +398,15 @@ class Lib:
         """Streams of at most v bytes of capacity use the 256-bit-chunk decoder build (< 0: default 1 MiB,
         0: never); returns the previous value."""
         return int(self.L.dc_set_small_chunk_max_bytes(int(v)))
+
+    def set_decode3_min_bytes(self, v):
+        """Streams of at least v bytes of capacity use the segment decoder (< -1: default 1 MiB + 1,
+        -1: never, 0: always); returns the previous value."""
+        return int(self.L.dc_set_decode3_min_bytes(int(v)))
+
+    def last_decode_was_v3(self):
+        """Whether the last finished decode's values came from the segment decoder."""
+        return bool(self.L.dc_last_decode_was_v3())
 
     def chunk_bits(self):
         """Chunk bits of the decoder build the last decode ran."""

@@ -143,6 +143,12 @@ long long dc_decode_chunk_bits_value(void);                 /* chunk bits of the
 /* Streams of at most this capacity (bytes) decode with the 256-bit-chunk build of the decoder, larger
  * ones with the 1024-bit build (< 0: the default, 1 MiB; 0: never).  Returns the previous value. */
 long long dc_set_small_chunk_max_bytes(long long max_bytes);
+/* Streams of at least this capacity (bytes) decode with the segment decoder (dc_decode3.hip), which
+ * hands streams it cannot take to the chunk-map decoder (< -1: the default, 1 MiB + 1; -1: never;
+ * 0: every stream).  Returns the previous value. */
+long long dc_set_decode3_min_bytes(long long min_bytes);
+/* 1 if the last decode's values came from the segment decoder (after dc_decode_finish). */
+int dc_last_decode_was_v3(void);
 
 #ifdef __cplusplus
 }

@@ -116,6 +116,19 @@ int main(int argc, char** argv) {
             fails++;
         }
     }
+    /* a root whose compress fails: every rank returns an error and no receiver touches its buffer */
+    memset(y, 0, sizeof(double) * (size_t)n);
+    if (rank == 0) { memcpy(y, x, sizeof(double) * (size_t)n); setenv("DC_TEST_FAIL_COMPRESS", "1", 1); }
+    {
+        const int rc = MPI_Bcast_bitwise_double(y, n, MPI_DOUBLE, 0, MPI_COMM_WORLD);
+        if (rank == 0) unsetenv("DC_TEST_FAIL_COMPRESS");
+        int touched = 0;
+        if (rank != 0) for (int i = 0; i < n; i++) touched |= y[i] != 0.0;
+        if (rc == MPI_SUCCESS || touched) {
+            printf("bcast_double root failure: rank %d rc=%d touched=%d (want an error, buffer untouched)\n", rank, rc, touched);
+            fails++;
+        }
+    }
     /* broadcasts: CT8 (crc), CT9 (mask_crc), CT10 (crc_hamming) */
     for (int mode = 8; mode <= 10; mode++) {
         memcpy(y, x, sizeof(double) * (size_t)n);

@@ -1,0 +1,127 @@
+"""GPU parity of the segment decoder (csrc/dc_decode3.hip): forced on for every stream size, its
+decode must equal the oracle's grammar decoder bit for bit, and it must take (not decline) every stream
+of ordinary density.  Streams it declines (runs mode: mostly 3-bit codes) must still decode exactly
+through the chunk-map decoder it hands them to."""
+import numpy as np
+import pytest
+
+from conftest import BOUNDS, CASES, golden
+
+pytestmark = pytest.mark.gpu
+CTS = [5, 6, 7, 11]
+
+
+@pytest.fixture
+def v3(dc):
+    old = dc.set_decode3_min_bytes(0)             # every stream through the segment decoder
+    yield dc
+    dc.set_decode3_min_bytes(old)
+
+
+def _inputs(oracle, kind, n):
+    if kind == "u10":
+        return oracle.gen_u10(n)
+    if kind == "eq":
+        return np.full(n, np.float32(0.123456789))
+    if kind == "unit":
+        return np.random.RandomState(n).rand(n).astype(np.float32)
+    if kind == "ramp":
+        return (np.float32(0.0005) * np.arange(n, dtype=np.float32)).astype(np.float32)
+    if kind == "himeno":
+        return np.tile(oracle.gen_himeno_plane(256, 256), max(1, n // 65536))[:n]
+    if kind == "mixed":
+        rs = np.random.RandomState(3)
+        x = oracle.gen_u10(n)
+        for r in rs.randint(0, n, 64):           # constant runs -> prediction chains across chunks
+            x[r:r + 3000] = x[r]
+        return x
+    if kind == "sparse":                          # every 5th value near a predictor: '101'..'111' codes
+        x = oracle.gen_u10(n)
+        x[1::5] = x[0::5][: x[1::5].size]
+        x[2::7] = 0.0
+        return x
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("bound", BOUNDS)
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("ct", CTS)
+def test_decode3_golden(v3, oracle, bound, case, ct):
+    g = golden(bound)
+    v3.set_bound(bound)
+    key = f"{case}/ct{ct}"
+    s = g[key + "/stream"]
+    n = g[f"{case}/input"].size
+    t, m17 = int(g[f"{case}/type"]), int(g[f"{case}/mask17"])
+    out = v3.decompress(ct, s, n, t, m17)
+    spec, got = oracle.decompress(ct, s, n, bound, t, m17)
+    assert got == n
+    assert np.array_equal(out.view(np.uint32), spec.view(np.uint32))
+    if bool(g[key + "/ref_consistent"]):
+        assert np.array_equal(out.view(np.uint32), g[key + "/ref_decoded"].view(np.uint32))
+
+
+@pytest.mark.parametrize("bound", [1e-3, 1e-6])
+@pytest.mark.parametrize("kind,n", [("u10", 1 << 20), ("u10", 100003), ("eq", 1 << 18), ("unit", 300001),
+                                    ("ramp", 200000), ("himeno", 1 << 18), ("mixed", 500000), ("sparse", 400009)])
+@pytest.mark.parametrize("ct", CTS)
+def test_decode3_roundtrip(v3, oracle, bound, kind, n, ct):
+    v3.set_bound(bound)
+    x = _inputs(oracle, kind, n)
+    _, xs = oracle.to_small(x)
+    t, m17 = oracle.type_mask(xs)
+    s, nb, pos = v3.compress(ct, xs, t, m17)
+    out = v3.decompress(ct, s, n, t, m17)
+    spec, got = oracle.decompress(ct, s, n, bound, t, m17)
+    assert got == n
+    assert np.array_equal(out.view(np.uint32), spec.view(np.uint32))
+    if kind == "u10":
+        # (a constant input, the Himeno rows and a slow ramp are locally periodic: paths read out of phase
+        # meet late or never; denser streams can overflow a job's output buffer: the segment decoder hands
+        # both to the chunk-map decoder)
+        assert v3.last_decode_was_v3(), "an ordinary stream left the segment decoder"
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 63, 64, 65, 255, 256, 257, 4095, 4096, 4097, 8191, 12345, 65537,
+                               262143])
+@pytest.mark.parametrize("ct", CTS)
+def test_decode3_ragged(v3, oracle, n, ct):
+    v3.set_bound(1e-3)
+    x = oracle.gen_u10(n, seed=n)
+    x[::7] = x[0]
+    _, xs = oracle.to_small(x)
+    t, m17 = oracle.type_mask(xs)
+    s, nb, pos = v3.compress(ct, xs, t, m17)
+    out = v3.decompress(ct, s, n, t, m17)
+    spec, _ = oracle.decompress(ct, s, n, 1e-3, t, m17)
+    assert np.array_equal(out.view(np.uint32), spec.view(np.uint32))
+
+
+@pytest.mark.parametrize("ct", CTS)
+@pytest.mark.parametrize("log2n", [22, 24])
+def test_decode3_device_chain(dc, oracle, ct, log2n):
+    """encode_device -> decode_device with the bit count left on the device (the bench's path, default
+    thresholds): the segment decoder runs and equals the oracle."""
+    import torch
+    n = 1 << log2n
+    dc.set_bound(1e-3)
+    x = oracle.gen_u10(n)
+    _, xs = oracle.to_small(x)
+    t, m17 = oracle.type_mask(xs)
+    dev = torch.device("cuda", 0)
+    xd = torch.from_numpy(xs).to(dev)
+    cap = dc.stream_capacity(n)
+    st = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    out = torch.empty(n, dtype=torch.float32, device=dev)
+    nbits = torch.zeros(1, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    dc.encode_device(ct, xd.data_ptr(), n, st.data_ptr(), type_=t, mask17=m17, total_ptr=nbits.data_ptr())
+    dc.decode_device(ct, st.data_ptr(), -1, n, out.data_ptr(), type_=t, mask17=m17, d_nbits=nbits.data_ptr(),
+                     max_bytes=cap)
+    dc.decode_finish()
+    assert dc.last_decode_was_v3()
+    nb = (int(nbits.item()) + 7) // 8
+    s = st[:nb].cpu().numpy()
+    spec, got = oracle.decompress(ct, s, n, 1e-3, t, m17)
+    assert got == n
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), spec.view(np.uint32))
