@@ -36,7 +36,8 @@
 
 namespace dc {
 
-constexpr int D3_PRE = 4;              // pre-walk chunks (1024 bits)
+// pre-walk: 1024 bits (4 chunks, one region line) before every segment
+constexpr int D3_SEG = 16;             // chunks per parse segment (4 region lines)
 constexpr int D3_RING = 16;            // ring words per lane (four 128-bit phases), + 4 mirrored words
 constexpr int D3_CAP = 1024 + 16;      // decode job output buffer (floats per wave)
 constexpr uint32_t D3_DECLINE = 512u;
@@ -49,11 +50,20 @@ constexpr uint32_t D3_WHY_RUNS = 1024u, D3_WHY_LINK = 2048u, D3_WHY_SHORT = 4096
 // summed over waves into g_prof3 (read with dc_dec3_prof_read; tools/dec3_prof.py)
 #ifdef DC_DEC3_PROF
 __device__ unsigned long long g_prof3[32];
+#define P3_DECL() unsigned long long p3a[16] = {0}
 #define P3_T(v) const long long v = clock64()
-#define P3_ADD(i, val) do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_prof3[i], (unsigned long long)(val)); } while (0)
+#define P3_ADD(i, val) (p3a[i] += (unsigned long long)(val))
+#define P3_FLUSH()                                                                                     \
+    do {                                                                                               \
+        if ((threadIdx.x & 63) == 0)                                                                   \
+            for (int i_ = 0; i_ < 16; i_++)                                                            \
+                if (p3a[i_]) atomicAdd(&g_prof3[i_], p3a[i_]);                                         \
+    } while (0)
 #else
+#define P3_DECL() do {} while (0)
 #define P3_T(v) do {} while (0)
 #define P3_ADD(i, val) do {} while (0)
+#define P3_FLUSH() do {} while (0)
 #endif
 
 __device__ __forceinline__ uint32_t bsw(uint32_t v) { return __builtin_bswap32(v); }
@@ -71,12 +81,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t stream_rsrc(const uint8_t* s, 
 __device__ __forceinline__ uint32_t keep_bytes(uint32_t w, int rem) {     // rem = stream bytes left at w
     return (uint32_t)(0xFFFFFFFF00000000ull >> (8 * min(max(rem, 0), 4))) & w;
 }
-// (stream offsets fit 31 bits: the host takes this decoder only for capacities below 2 GiB)
-__device__ __forceinline__ uint4 load_w4(__amdgpu_buffer_rsrc_t rs, long long nbytes, long long gw) {
-    const int off = (int)(uint32_t)(gw * 4);
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+// (stream offsets fit 31 bits: the host takes this decoder only for capacities below 2 GiB).  The raw
+// load and its finishing (byte order, the stream's end) are separate, so that nothing touches the loaded
+// registers before the words are needed and the load stays in flight.
+__device__ __forceinline__ uint4 load_raw4(__amdgpu_buffer_rsrc_t rs, long long gw) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(uint32_t)(gw * 4), 0, 0);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint4 finish4(uint4 v, long long nbytes, long long gw) {
     uint4 w = make_uint4(bsw(v.x), bsw(v.y), bsw(v.z), bsw(v.w));
-    const int r0 = (int)nbytes - off;
+    const int r0 = (int)nbytes - (int)(uint32_t)(gw * 4);
     if (r0 < 16) {                            // the group holding the stream's last byte (or past it: 0 already)
         w.x = keep_bytes(w.x, r0);
         w.y = keep_bytes(w.y, r0 - 4);
@@ -84,6 +98,9 @@ __device__ __forceinline__ uint4 load_w4(__amdgpu_buffer_rsrc_t rs, long long nb
         w.w = keep_bytes(w.w, r0 - 12);
     }
     return w;
+}
+__device__ __forceinline__ uint4 load_w4(__amdgpu_buffer_rsrc_t rs, long long nbytes, long long gw) {
+    return finish4(load_raw4(rs, gw), nbytes, gw);
 }
 
 __device__ __forceinline__ bool declined_now(const Dec3Bufs& D3) {
@@ -93,14 +110,13 @@ __device__ __forceinline__ bool declined_now(const Dec3Bufs& D3) {
 struct Geo3 {
     unsigned long long nbits;
     long long nbytes, nchunks, nseg, npjobs, ndjobs;
-    int seg;
 };
-__device__ __forceinline__ Geo3 geo3(const unsigned long long* dev_nbits, unsigned long long host_nbits, int seg) {
+__device__ __forceinline__ Geo3 geo3(const unsigned long long* dev_nbits, unsigned long long host_nbits) {
+    constexpr int seg = D3_SEG;
     Geo3 g;
     g.nbits = dev_nbits ? *dev_nbits : host_nbits;
     g.nbytes = (long long)((g.nbits + 7) >> 3);
     g.nchunks = (long long)((g.nbits + 255) >> 8);
-    g.seg = seg;
     g.nseg = (g.nchunks + seg - 1) / seg;
     g.npjobs = (g.nseg + 63) / 64;
     g.ndjobs = (g.nchunks + 63) / 64;
@@ -163,16 +179,64 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
     return v;
 }
 
+// The lane's region is read one 128-byte line (8 phases, 4 chunks) at a time through 8 staged uint4
+// (VGPRs): a line's first half is requested right after the staging it reuses went to the ring, 5
+// phases before it is needed, and its halves close together -- each stream line leaves HBM once (16-byte
+// loads spread over 8 phases let L2 drop the line between them: 8x the stream in fetch).  Region line
+// L covers segment phases 8(L-1) .. 8(L-1)+7 (line 0: the 1024-bit pre-walk).
+struct Stage8 {
+    uint4 S[8];
+};
+__device__ __forceinline__ void stage_half(Stage8& st, int h0, __amdgpu_buffer_rsrc_t rs, long long gw) {
+#pragma unroll
+    for (int h = 0; h < 4; h++) st.S[h0 + h] = load_raw4(rs, gw + 4 * h);
+}
+
+// walk region lines L0 .. L1-1; the reader starts at segment bit pinit (a lane that is not live walks
+// nothing).  `start(c, kbase)` runs before chunk c is walked (c < 0 in the pre-walk), `end(c, count)`
+// after it.
+template <class Start, class End>
+__device__ __forceinline__ void run_lines(Ring3& r, __amdgpu_buffer_rsrc_t rs, long long nbytes, long long gw0, int L0,
+                                          int L1, int lim, int pinit, bool live, const uint8_t* tl, Start start,
+                                          End end) {
+    Stage8 st;
+    const long long w0 = gw0 + 32ll * (L0 - 1);
+    stage_half(st, 0, rs, w0);
+    stage_half(st, 4, rs, w0 + 16);
+    r.put(0, finish4(st.S[0], nbytes, w0));
+    r.put(1, finish4(st.S[1], nbytes, w0 + 4));
+    int kbase = 8 * (L0 - 1);
+    r.init(pinit, kbase);
+    if (!live) r.pos = 1 << 30;
+    for (int L = L0; L < L1; L++) {
+        const long long wn = gw0 + 32ll * L;                        // the next line's first word
+        int n0 = 0;
+#pragma unroll
+        for (int h = 0; h < 8; h++) {
+            const int k = 8 * (L - 1) + h;
+            if ((h & 1) == 0) start(k >> 1, kbase);
+            const int n = r.walk(min(128 * (k + 1), lim), tl);
+            r.put((h + 2) & 3, finish4(st.S[(h + 2) & 7], nbytes, gw0 + 4ll * (k + 2)));
+            if (h == 1) stage_half(st, 0, rs, wn);
+            if (h == 5) stage_half(st, 4, rs, wn + 16);
+            if ((h & 3) == 3) { kbase += 4; r.addr -= 4096u; }
+            if (h & 1) end(k >> 1, n0 + n);
+            else n0 = n;
+        }
+    }
+}
+
 template <int CT>
 __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ s, Params P, Dec3Bufs D3,
                                                     const unsigned long long* dev_nbits, unsigned long long host_nbits,
-                                                    long long num, uint32_t epoch) {
+                                                    long long num) {
+    constexpr int seg = D3_SEG;
     __shared__ uint32_t ring[(D3_RING + 4) * 64];
+    __shared__ uint16_t recs[seg * 64];                          // [chunk][lane]: the wave's records
     __shared__ uint8_t tl[512];
     const int lane = threadIdx.x;
     build_lut_len<CT>(tl, P, lane, 64);
-    const Geo3 G = geo3(dev_nbits, host_nbits, D3.seg);
-    const int seg = G.seg;
+    const Geo3 G = geo3(dev_nbits, host_nbits);
     const __amdgpu_buffer_rsrc_t rs = stream_rsrc(s, D3.capw);
     const bool decline = G.nchunks > D3.max_chunks || runs_mode(CT, G.nbits, num);
     if (decline && blockIdx.x == 0 && lane == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_RUNS);
@@ -180,12 +244,9 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
     Ring3 r;
     r.L = ring;
     r.lc = (uint32_t)lane << 2;
-    constexpr int kb = -2 * D3_PRE;                 // first pre-walk phase (128 bits each)
-    while (!decline) {
-        unsigned job = 0;
-        if (lane == 0) job = atomicAdd(&D3.ctr[0], 1u);
-        job = __builtin_amdgcn_readfirstlane(job);     // wave-uniform (SGPR)
-        if ((long long)job >= G.npjobs) break;
+    P3_DECL();
+    // jobs by a fixed stride (a shared ticket counter serialised every wave on one L2 line)
+    for (unsigned job = blockIdx.x; !decline && (long long)job < G.npjobs; job += gridDim.x) {
         const long long sidx = (long long)job * 64 + lane;              // this lane's segment
         const long long sbit = sidx * seg * 256;
         const bool act = sidx < G.nseg;
@@ -194,91 +255,54 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
         const long long c0 = sidx * seg;                                   // first chunk of the segment
         P3_T(t0);
 
-        // ---- main walk: pre-walk from 1024 bits before the segment, then its chunks
-        r.put(0, load_w4(rs, G.nbytes, gw0 + 4 * kb));
-        r.put(1, load_w4(rs, G.nbytes, gw0 + 4 * (kb + 1)));
-        uint4 q0 = load_w4(rs, G.nbytes, gw0 + 4 * (kb + 2));
-        int kbase = kb;
-        r.init(128 * kb, kbase);
-        if (!act) r.pos = 1 << 30;
+        // ---- main walk: the pre-walk line (1024 bits before the segment), then the segment's lines
         uint32_t tot = 0;
-        int e0 = 0;
-        for (int c = kb / 2; c < seg; c++) {
-            const int k = 2 * c;
-            const uint4 q1 = load_w4(rs, G.nbytes, gw0 + 4 * (k + 3));
-            if (c == 0 && sidx == 0) r.init(0, kbase);                     // the stream's first bit
-            const int e = r.pos - 256 * c;
-            const int n0 = r.walk(min(128 * (k + 1), lim), tl);
-            r.put((k + 2 - kb) & 3, q0);
-            q0 = load_w4(rs, G.nbytes, gw0 + 4 * (k + 4));
-            const int n1 = r.walk(min(128 * (k + 2), lim), tl);
-            r.put((k + 3 - kb) & 3, q1);
-            if (((k + 1 - kb) & 3) == 3) { kbase += 4; r.addr -= 4096u; }
-            if (c >= 0) {
-                const uint32_t cnt = (uint32_t)(n0 + n1);
-                if (act && c0 + c < G.nchunks) D3.rec[c0 + c] = (uint16_t)((uint32_t)(e & 31) | (cnt << 8));
-                tot += cnt;
-                if (c == 0) e0 = e;
-            }
-        }
+        int e0 = 0, ec = 0;
+        run_lines(r, rs, G.nbytes, gw0, 0, seg / 4 + 1, lim, -1024, act, tl,
+                  [&](int c, int kbase) {
+                      if (c == 0 && sidx == 0) r.init(0, kbase);             // the stream's first bit
+                      ec = r.pos - 256 * c;
+                  },
+                  [&](int c, int cnt) {
+                      if (c >= 0) {
+                          recs[c * 64 + lane] = (uint16_t)((uint32_t)(ec & 31) | ((uint32_t)cnt << 8));
+                          tot += (uint32_t)cnt;
+                          if (c == 0) e0 = ec;
+                      }
+                  });
         const int X = r.pos - 256 * seg;                                 // entry of the next segment
+        // (the link into the next job is checked by scan3_kernel against this exit)
+        if (lane == 63) D3.pexit[job] = (uint64_t)(uint32_t)X;
         P3_T(t1);
         P3_ADD(0, t1 - t0);
-#ifdef DC_DEC3_PROF
-        { const uint32_t tt = wave_incl_scan(act ? tot : 0u, lane); if (lane == 63) atomicAdd(&g_prof3[4], (unsigned long long)tt); }
-#endif
-        if (lane == 63) st_relaxed(&D3.pexit[job], ((uint64_t)epoch << 32) | (uint32_t)(X & 0xFFFF));
+        P3_ADD(4, act ? tot : 0u);
 
-        // ---- links: this segment's first entry = the previous segment's exit
-        int xprev = __shfl_up(X, 1, 64);
-        if (lane == 0 && act && sidx > 0) {
-            unsigned spins = 0;
-            uint64_t v;
-            while (((v = ld_relaxed(&D3.pexit[job - 1])) >> 32) != (uint64_t)epoch) {
-                if (++spins > (1u << 22) || declined_now(D3)) { atomicOr(D3.err, D3_DECLINE | 16u); break; }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            xprev = (int)(v & 0xFFFF);
-        }
-        P3_T(t2);
-        P3_ADD(1, t2 - t1);
-        // ---- repair: a lane whose entry is not its predecessor's exit re-walks from that exit, rewriting
-        // its records until the path meets a recorded entry again; a path that reaches the segment end
-        // without meeting it moves the exit, and the successor is checked again (rounds within the wave;
-        // the next job checked its link against this job's main-walk exit, so a moved last exit declines)
-        int xin = xprev, ecur = e0, Xcur = X, rounds = 0;
-        bool bad = act && sidx > 0 && ecur != xin;
+        // ---- links within the job: a segment's first entry = the previous segment's exit.  A lane whose
+        // entry is not re-walks from that exit, rewriting its records until the path meets a recorded
+        // entry again; a path that reaches the segment end without meeting it moves the exit, and the
+        // successor is checked again (rounds; a moved exit of the last segment declines)
+        int xin = __shfl_up(X, 1, 64), ecur = e0, Xcur = X, rounds = 0;
+        bool bad = act && lane > 0 && ecur != xin;
         while (__any(bad)) {
             if (++rounds > 64) { if (lane == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK); break; }
-            r.put(0, load_w4(rs, G.nbytes, gw0));
-            r.put(1, load_w4(rs, G.nbytes, gw0 + 4));
-            q0 = load_w4(rs, G.nbytes, gw0 + 8);
-            r.init(bad ? xin : 0, 0);
             bool live = bad;
-            if (!live) r.pos = 1 << 30;
-            for (int c = 0; c < seg; c++) {
-                const int k = 2 * c;
-                const uint4 q1 = load_w4(rs, G.nbytes, gw0 + 4 * (k + 3));
-                const bool inside = c0 + c < G.nchunks;
-                const uint32_t old = (live && inside) ? (uint32_t)D3.rec[c0 + c] : 0u;
-                if (live && c > 0 && r.pos - 256 * c == (int)(old & 31u) && 256 * c < lim) {
-                    live = false;                                           // met the recorded path
-                    r.pos = 1 << 30;
-                }
-                const int e = r.pos - 256 * c;
-                const int n0 = r.walk(min(128 * (k + 1), lim), tl);
-                r.put((k + 2) & 3, q0);
-                q0 = load_w4(rs, G.nbytes, gw0 + 4 * (k + 4));
-                const int n1 = r.walk(min(128 * (k + 2), lim), tl);
-                r.put((k + 3) & 3, q1);
-                if (((k + 1) & 3) == 3) r.addr -= 4096u;
-                if (live) {
-                    const uint32_t cnt = (uint32_t)(n0 + n1);
-                    if (inside) D3.rec[c0 + c] = (uint16_t)((uint32_t)(e & 31) | (cnt << 8));
-                    tot += cnt - (old >> 8);
-                    if (c == 0) ecur = e;
-                }
-            }
+            run_lines(r, rs, G.nbytes, gw0, 1, seg / 4 + 1, lim, bad ? xin : 0, bad, tl,
+                      [&](int c, int) {
+                          const int old = (int)(recs[c * 64 + lane] & 31u);
+                          if (live && c > 0 && r.pos - 256 * c == old && 256 * c < lim) {
+                              live = false;                                 // met the recorded path
+                              r.pos = 1 << 30;
+                          }
+                          ec = r.pos - 256 * c;
+                      },
+                      [&](int c, int cnt) {
+                          if (live) {
+                              const uint32_t old = recs[c * 64 + lane];
+                              recs[c * 64 + lane] = (uint16_t)((uint32_t)(ec & 31) | ((uint32_t)cnt << 8));
+                              tot += (uint32_t)cnt - (old >> 8);
+                              if (c == 0) ecur = ec;
+                          }
+                      });
             const bool whole = 256 * seg < lim;                              // a successor segment exists
             const int Xn = live ? r.pos - 256 * seg : Xcur;
             const bool moved = live && whole && Xn != Xcur;
@@ -289,11 +313,22 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
             bad = lane >= 1 && act && mp && ecur != xp;
             xin = bad ? xp : xin;
         }
-
-        P3_T(t3);
-        P3_ADD(2, t3 - t2);
+        P3_T(t2);
+        P3_ADD(2, t2 - t1);
         P3_ADD(3, rounds);
         P3_ADD(5, 1);
+
+        // ---- the segment's records: 32 bytes per lane, one contiguous 2 KB block per wave
+        if (act) {
+            uint32_t w[seg / 2];
+#pragma unroll
+            for (int i = 0; i < seg / 2; i++)
+                w[i] = (uint32_t)recs[(2 * i) * 64 + lane] | ((uint32_t)recs[(2 * i + 1) * 64 + lane] << 16);
+            uint4* dst = reinterpret_cast<uint4*>(D3.rec + c0);
+#pragma unroll
+            for (int i = 0; i < seg / 8; i++) dst[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+        }
+
         // ---- token offsets: the job's total and every decode job's first token relative to the job
         const uint32_t inc = wave_incl_scan(tot, lane);
         if (lane == 63) D3.ptot[job] = inc;
@@ -302,22 +337,65 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
             if (dj * 64 < D3.max_chunks) D3.rel[dj] = inc - tot;
         }
     }
-    if (lane == 0) {
-        __threadfence();
-        if (atomicAdd(&D3.ctr[2], 1u) == gridDim.x - 1) { atomicExch(&D3.ctr[0], 0u); atomicExch(&D3.ctr[2], 0u); }
+    P3_FLUSH();
+}
+
+// the 9-bit token prefix at stream bit `pos` (bytes past the stream read as 0)
+__device__ __forceinline__ uint32_t peek9(const uint8_t* __restrict__ s, long long nbytes, long long pos) {
+    const long long i = pos >> 3;
+    const uint32_t b0 = i < nbytes ? s[i] : 0u, b1 = i + 1 < nbytes ? s[i + 1] : 0u;
+    return (((b0 << 8) | b1) >> (7 - (int)(pos & 7))) & 511u;
+}
+
+// the link into parse job t: its first segment's entry must be job t-1's exit.  A broken link (the
+// pre-walk had not synchronised; rare) is re-walked here, serially, until the path meets the recorded
+// entries again; the changed token counts move the job's total and its decode jobs' offsets.
+template <int CT>
+__device__ void link_fix(const uint8_t* __restrict__ s, const Geo3& G, const Dec3Bufs& D3, const uint8_t* tl, long long t) {
+    constexpr int seg = D3_SEG;
+    const long long cf = t * 64 * seg;                           // the job's first chunk
+    if (t == 0 || cf >= G.nchunks) return;
+    const int X = (int)(uint32_t)D3.pexit[t - 1];
+    if ((int)(D3.rec[cf] & 31u) == X) return;
+    const long long cend = (t + 1) * 64 * seg;
+    long long pos = cf * 256 + X;
+    for (long long c = cf;; c++) {
+        if (c > cf) {
+            if (c >= G.nchunks) break;                                       // the stream's end
+            if (c >= cend) { atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK); return; }  // the job's exit moved
+            if (pos - 256 * c == (long long)(D3.rec[c] & 31u)) break;           // met the recorded path
+        }
+        const long long pe = min(256 * (c + 1), (long long)G.nbits);
+        const int e = (int)(pos - 256 * c);
+        uint32_t cnt = 0;
+        while (pos < pe) { pos += tl[peek9(s, G.nbytes, pos)]; cnt++; }
+        const uint32_t old = D3.rec[c];
+        D3.rec[c] = (uint16_t)((uint32_t)(e & 31) | (cnt << 8));
+        const int d = (int)cnt - (int)(old >> 8);
+        if (d) {
+            D3.ptot[t] += (uint32_t)d;
+            for (int q = (int)((c - cf) / 64) + 1; q < seg; q++) D3.rel[t * seg + q] += (uint32_t)d;
+        }
     }
 }
 
-// exclusive scan of the parse jobs' token counts (one workgroup); a stream with fewer tokens than num
-// is left to the other decoder (it reads past the stream as the reference does)
-__global__ __launch_bounds__(1024) void scan3_kernel(Dec3Bufs D3, const unsigned long long* dev_nbits,
+// the links between parse jobs, then the exclusive scan of their token counts (one workgroup); a stream
+// with fewer tokens than num is left to the other decoder (it reads past the stream as the reference does)
+template <int CT>
+__global__ __launch_bounds__(1024) void scan3_kernel(const uint8_t* __restrict__ s, Params P, Dec3Bufs D3,
+                                                     const unsigned long long* dev_nbits,
                                                      unsigned long long host_nbits, long long num) {
     __shared__ unsigned long long wtot[16];
-    const Geo3 G = geo3(dev_nbits, host_nbits, D3.seg);
-    const long long np = G.npjobs;
+    __shared__ uint8_t tl[512];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    build_lut_len<CT>(tl, P, tid, 1024);
+    __syncthreads();
+    const Geo3 G = geo3(dev_nbits, host_nbits);
+    if ((__hip_atomic_load(D3.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & D3_DECLINE) != 0) return;
+    const long long np = G.npjobs;
     const long long per = (np + 1023) / 1024;
     const long long t0 = tid * per, t1 = min(np, t0 + per);
+    for (long long t = t0; t < t1; t++) link_fix<CT>(s, G, D3, tl, t);
     unsigned long long sum = 0;
     for (long long t = t0; t < t1; t++) sum += D3.ptot[t];
     unsigned long long inc = sum;
@@ -417,23 +495,24 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
     build_lut3<CT>(T, P, threadIdx.x, 256);
     __syncthreads();
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const Geo3 G = geo3(dev_nbits, host_nbits, D3.seg);
+    const Geo3 G = geo3(dev_nbits, host_nbits);
     const __amdgpu_buffer_rsrc_t rs = stream_rsrc(s, D3.capw);
     const bool declined = (__hip_atomic_load(D3.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & D3_DECLINE) != 0;
     // patterns without a midpoint bit can equal the -1.0f history sentinel: check every value then
     const bool chk_all = (CT == 6 && P.B >= 23) || (CT == 7 && (P.mask17 >> 16) != 0u && P.mm == 23);
     uint32_t* L = stg[w];
     float* ob = obuf[w];
-    while (!declined) {
+    P3_DECL();
+    // jobs by a fixed stride (a shared ticket counter serialised every wave on one L2 line: 80k jobs
+    // at ~13 ns each).  A job waits only for its predecessor's published values, rarely, and every
+    // predecessor belongs to an earlier wave of the same round or to an earlier round.
+    for (unsigned job = blockIdx.x * 4 + w; !declined; job += gridDim.x * 4) {
         P3_T(u0);
-        unsigned job = 0;
-        if (lane == 0) job = atomicAdd(&D3.ctr[1], 1u);
-        job = __builtin_amdgcn_readfirstlane(job);     // wave-uniform (SGPR)
         if ((long long)job >= G.ndjobs) break;
         const long long g = (long long)job * 64 + lane;
         const uint32_t rc = g < G.nchunks ? (uint32_t)D3.rec[g] : 0u;
         const int e = (int)(rc & 31u), n = (int)(rc >> 8);
-        const unsigned long long base = D3.pbase[job / G.seg] + D3.rel[job];
+        const unsigned long long base = D3.pbase[job / D3_SEG] + D3.rel[job];
         const uint32_t inc = wave_incl_scan((uint32_t)n, lane);
         const int off = (int)inc - n;
         const int Tn = (int)__builtin_amdgcn_readlane(inc, 63);
@@ -559,11 +638,7 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
         P3_ADD(13, 1);
         }
     }
-    // the waves of a block finish independently: the last WAVE out resets the tickets for the next call
-    if (lane == 0) {
-        __threadfence();
-        if (atomicAdd(&D3.ctr[3], 1u) == 4 * gridDim.x - 1) { atomicExch(&D3.ctr[1], 0u); atomicExch(&D3.ctr[3], 0u); }
-    }
+    P3_FLUSH();
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -584,16 +659,10 @@ static int resident3(const void* f, int threads) {
     return per * ncu;
 }
 
-// segment length for a stream of at most max_chunks chunks: long segments (fewer pre-walk bits per
-// token) as long as there are about two segments per resident lane (latency hiding)
+// segment length (chunks): fixed; the host sizes the scratch with it
 extern "C" int dc_decode3_seg(long long max_chunks) {
-    static long long lanes = 0;
-    if (!lanes) lanes = 64ll * resident3((const void*)parse3_kernel<7>, 64);
-    // at least 16 chunks (4096 bits): a link whose pre-walk had not synchronised is repaired within the
-    // segment in practice; with shorter segments a repair that runs off the segment end moves the exit
-    int seg = 16;
-    while (seg < 32 && (long long)seg * 2 * lanes * 2 <= max_chunks) seg *= 2;
-    return seg;
+    (void)max_chunks;
+    return D3_SEG;
 }
 
 // DC_DEC3_DEBUG=1: wait for every kernel (at most 2 s each) and report one that does not finish
@@ -657,10 +726,10 @@ extern "C" int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev
     const int g1 = (int)std::max<long long>(1, std::min<long long>(maxpj, gp[ci]));
     const int g3 = (int)std::max<long long>(1, std::min<long long>((maxdj + 3) / 4, gd[ci]));
     dc_mark_phase(4, st);
-    DC_DISPATCH_3(P->ct, parse3_kernel, dim3(g1), dim3(64), 0, st, s, *P, *D3, dev_nbits, host_nbits, num, epoch);
+    DC_DISPATCH_3(P->ct, parse3_kernel, dim3(g1), dim3(64), 0, st, s, *P, *D3, dev_nbits, host_nbits, num);
     dbg_wait("parse3_kernel", st);
     dc_mark_phase(5, st);
-    hipLaunchKernelGGL(scan3_kernel, dim3(1), dim3(1024), 0, st, *D3, dev_nbits, host_nbits, num);
+    DC_DISPATCH_3(P->ct, scan3_kernel, dim3(1), dim3(1024), 0, st, s, *P, *D3, dev_nbits, host_nbits, num);
     dbg_wait("scan3_kernel", st);
     dc_mark_phase(6, st);
     DC_DISPATCH_3(P->ct, decode3_kernel, dim3(g3), dim3(256), 0, st, s, *P, *D3, dev_nbits, host_nbits, out, num, epoch);
