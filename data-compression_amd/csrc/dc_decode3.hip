@@ -75,6 +75,7 @@ __device__ __forceinline__ uint32_t bsw(uint32_t v) { return __builtin_bswap32(v
 // words are used (a branchy or select-guarded global load made the compiler wait at once).  Bytes past
 // the stream's end read as 0, as the reference's reader sees them.
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t stream_rsrc(const uint8_t* s, long long capw) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(s), (short)0, (int)(capw * 4), 0x00020000);
 }
@@ -485,6 +486,32 @@ __device__ __forceinline__ float prev_job_value(const Dec3Bufs& D3, long long jo
     return __uint_as_float((uint32_t)v);
 }
 
+// a decode job's inputs, requested one job ahead (the job's records, its token offset, 12 stream words
+// per lane) so that their latency hides behind the previous job's walk and stores
+constexpr int D3_OOB = 0x7FFFFFF0;                  // a buffer offset past every range below: reads 0, drops writes
+                                                    // (ranges end below 0x7FFFFF00)
+struct Pre3 {
+    uint32_t rc, rl;
+    u32x2 pb;
+    uint4 v0, v1, v2;
+};
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t any_rsrc(const void* p, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes, 0x00020000);
+}
+__device__ __forceinline__ Pre3 prefetch3(__amdgpu_buffer_rsrc_t rr, __amdgpu_buffer_rsrc_t rp, __amdgpu_buffer_rsrc_t rl,
+                                          __amdgpu_buffer_rsrc_t rs, const Geo3& G, unsigned job, int lane) {
+    Pre3 q;
+    const long long g = (long long)job * 64 + lane;
+    const bool ok = (long long)job < G.ndjobs;
+    q.rc = __builtin_amdgcn_raw_buffer_load_b16(rr, g < G.nchunks ? (int)(2 * g) : D3_OOB, 0, 0);
+    q.pb = __builtin_amdgcn_raw_buffer_load_b64(rp, ok ? (int)(8 * (job / D3_SEG)) : D3_OOB, 0, 0);
+    q.rl = __builtin_amdgcn_raw_buffer_load_b32(rl, ok ? (int)(4 * job) : D3_OOB, 0, 0);
+    q.v0 = load_raw4(rs, 8 * g);
+    q.v1 = load_raw4(rs, 8 * g + 4);
+    q.v2 = load_raw4(rs, 8 * g + 8);
+    return q;
+}
+
 template <int CT>
 __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict__ s, Params P, Dec3Bufs D3,
                                                      const unsigned long long* dev_nbits, unsigned long long host_nbits,
@@ -497,6 +524,8 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const Geo3 G = geo3(dev_nbits, host_nbits);
     const __amdgpu_buffer_rsrc_t rs = stream_rsrc(s, D3.capw);
+    const __amdgpu_buffer_rsrc_t rr = any_rsrc(D3.rec, 0x7FFFFF00), rp = any_rsrc(D3.pbase, 0x7FFFFF00),
+                                 rl = any_rsrc(D3.rel, 0x7FFFFF00), ro = any_rsrc(out, (int)(num * 4));
     const bool declined = (__hip_atomic_load(D3.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & D3_DECLINE) != 0;
     // patterns without a midpoint bit can equal the -1.0f history sentinel: check every value then
     const bool chk_all = (CT == 6 && P.B >= 23) || (CT == 7 && (P.mask17 >> 16) != 0u && P.mm == 23);
@@ -506,13 +535,12 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
     // jobs by a fixed stride (a shared ticket counter serialised every wave on one L2 line: 80k jobs
     // at ~13 ns each).  A job waits only for its predecessor's published values, rarely, and every
     // predecessor belongs to an earlier wave of the same round or to an earlier round.
-    for (unsigned job = blockIdx.x * 4 + w; !declined; job += gridDim.x * 4) {
+    const unsigned stride = gridDim.x * 4;
+    auto process = [&](const Pre3& cur, unsigned job) {
         P3_T(u0);
-        if ((long long)job >= G.ndjobs) break;
         const long long g = (long long)job * 64 + lane;
-        const uint32_t rc = g < G.nchunks ? (uint32_t)D3.rec[g] : 0u;
-        const int e = (int)(rc & 31u), n = (int)(rc >> 8);
-        const unsigned long long base = D3.pbase[job / D3_SEG] + D3.rel[job];
+        const int e = (int)(cur.rc & 31u), n = (int)(cur.rc >> 8);
+        const unsigned long long base = ((unsigned long long)cur.pb.y << 32 | cur.pb.x) + cur.rl;
         const uint32_t inc = wave_incl_scan((uint32_t)n, lane);
         const int off = (int)inc - n;
         const int Tn = (int)__builtin_amdgcn_readlane(inc, 63);
@@ -523,10 +551,11 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
         // for lanes 1..63 with lane 0 inactive, and their readfirstlane claimed job 0 again, forever)
         const bool fits = al + Tn <= D3_CAP;
         if (!fits) atomicOr(D3.err, D3_DECLINE | D3_WHY_DENSE);        // every lane: OR is idempotent
+        bool sent = false;
         if (fits) {
         {   // stage the chunk's 8 words + 4 words of the next chunk
-            const uint4 v0 = load_w4(rs, G.nbytes, 8 * g), v1 = load_w4(rs, G.nbytes, 8 * g + 4),
-                        v2 = load_w4(rs, G.nbytes, 8 * g + 8);
+            const uint4 v0 = finish4(cur.v0, G.nbytes, 8 * g), v1 = finish4(cur.v1, G.nbytes, 8 * g + 4),
+                        v2 = finish4(cur.v2, G.nbytes, 8 * g + 8);
             L[(0 << 6) + lane] = v0.x; L[(1 << 6) + lane] = v0.y; L[(2 << 6) + lane] = v0.z; L[(3 << 6) + lane] = v0.w;
             L[(4 << 6) + lane] = v1.x; L[(5 << 6) + lane] = v1.y; L[(6 << 6) + lane] = v1.z; L[(7 << 6) + lane] = v1.w;
             L[(8 << 6) + lane] = v2.x; L[(9 << 6) + lane] = v2.y; L[(10 << 6) + lane] = v2.z; L[(11 << 6) + lane] = v2.w;
@@ -535,7 +564,6 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
         P3_ADD(9, u2 - u1);
         const int o0 = al + off;
         int pend = 0;
-        bool sent = false;
         {
             Rd3 r;
             r.init(L, lane, e);
@@ -612,30 +640,67 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
         // ---- publish the job's last three values (the next job's first chunk may need them)
         if (lane < 3 && Tn >= 3)
             st_relaxed(&D3.hist[(long long)job * 3 + lane], ((uint64_t)epoch << 32) | __float_as_uint(ob[al + Tn - 1 - lane]));
-        // ---- store: whole float4s of the output's 16-byte grid
+        }
+        P3_T(u4s);
+        // ---- store: the job's values as whole float4s of the output's 16-byte grid (a fixed count of
+        // buffer stores, lanes outside the job writing past the range), the partial float4s at its two
+        // ends float by float (lanes 0..3: the first, 4..7: the last)
         const int span = al + Tn;
         const int Q = (span + 3) >> 2;
         const long long gi0 = (long long)(base - (unsigned long long)al);
         bool sv = false;
-        for (int q = lane; q < Q; q += 64) {
-            const float4 v = reinterpret_cast<const float4*>(ob)[q];
+        const float4* ob4 = reinterpret_cast<const float4*>(ob);
+#pragma unroll
+        for (int i = 0; i < (D3_CAP + 3) / 4 / 64 + 1; i++) {
+            const int q = lane + 64 * i;
+            const float4 v = ob4[min(q, D3_CAP / 4 - 1)];
             const long long gi = gi0 + 4 * q;
-            if (chk_all)
+            const bool full = fits && q < Q && 4 * q >= al && 4 * q + 4 <= span && gi + 4 <= num;
+            if (chk_all && q < Q)
                 sv |= __float_as_uint(v.x) == 0xBF800000u || __float_as_uint(v.y) == 0xBF800000u ||
                       __float_as_uint(v.z) == 0xBF800000u || __float_as_uint(v.w) == 0xBF800000u;
-            if (4 * q >= al && 4 * q + 4 <= span && gi + 4 <= num) {
-                *reinterpret_cast<float4*>(out + gi) = v;
-            } else {
-                const float vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-                    if (4 * q + i >= al && 4 * q + i < span && gi + i < num) out[gi + i] = vv[i];
-            }
+            const u32x4 raw = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+            __builtin_amdgcn_raw_buffer_store_b128(raw, ro, full ? (int)(4 * gi) : D3_OOB, 0, 0);
+        }
+        {
+            const int qe = lane < 4 ? 0 : Q - 1;
+            const int idx = 4 * qe + (lane & 3);
+            const long long gi = gi0 + idx;
+            const bool qfull = 4 * qe >= al && 4 * qe + 4 <= span && gi0 + 4 * qe + 4 <= num;
+            const bool ok = fits && lane < 8 && !qfull && idx >= al && idx < span && gi < num;
+            const float v = ob[min(max(idx, 0), D3_CAP - 1)];
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ro, ok ? (int)(4 * gi) : D3_OOB, 0, 0);
         }
         if (__any(sent || sv) && lane == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_SENT);
         P3_T(u5);
-        P3_ADD(12, u5 - u4);
+        P3_ADD(12, u5 - u4s);
         P3_ADD(13, 1);
+    };
+    // two jobs per round, their inputs in two register sets: each job's loads are in flight during the
+    // other's walk and stores (one set copied into the other would wait for the loads -- and for every
+    // store issued since, as stores count in the same counter)
+    unsigned job = blockIdx.x * 4 + w;
+    if (!declined && (long long)job < G.ndjobs) {
+        Pre3 A = prefetch3(rr, rp, rl, rs, G, job, lane), B;
+        // as many (dropped, distinct) stores after the first prefetch as a job issues after its
+        // successor's: the loop's entry then looks like its back edge to the wait-count placement,
+        // which otherwise waits for every store of the previous job before using a job's inputs
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("" ::: "memory");
+        const u32x4 z4 = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int i = 0; i < (D3_CAP + 3) / 4 / 64 + 1; i++)
+            __builtin_amdgcn_raw_buffer_store_b128(z4, ro, D3_OOB - 64 * (i + 1), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(0u, ro, D3_OOB, 0, 0);
+        for (;;) {
+            B = prefetch3(rr, rp, rl, rs, G, job + stride, lane);
+            process(A, job);
+            job += stride;
+            if ((long long)job >= G.ndjobs) break;
+            A = prefetch3(rr, rp, rl, rs, G, job + stride, lane);
+            process(B, job);
+            job += stride;
+            if ((long long)job >= G.ndjobs) break;
         }
     }
     P3_FLUSH();

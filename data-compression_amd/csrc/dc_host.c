@@ -601,9 +601,9 @@ int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsig
     make_params(&P, ct, type, mask17);
     const long long m3 = dec3_min_bytes();
     /* the segment decoder reads whole 16-byte groups through a buffer resource (32-bit byte range): every
-       stream byte must lie in one inside max_bytes, and max_bytes must stay below 2 GiB */
+       stream byte must lie in one inside max_bytes, and max_bytes and the output below 2 GiB */
     const long long need16 = nbytes >= 0 ? (nbytes + 15) / 16 * 16 : 0;
-    G.dec3_used = m3 >= 0 && max_bytes >= m3 && max_bytes >= 16 && max_bytes >= need16 && max_bytes < (1ll << 31) && !G.D.shard &&
+    G.dec3_used = m3 >= 0 && max_bytes >= m3 && max_bytes >= 16 && max_bytes >= need16 && max_bytes < (1ll << 31) && num < (1ll << 29) && !G.D.shard &&
                   !((uintptr_t)d_stream & 15u) && !((uintptr_t)d_out & 15u);
     G.dec_dnbits = nbytes >= 0 ? NULL : d_nbits;
     G.dec_hnbits = nbytes >= 0 ? (unsigned long long)nbytes * 8ull : 0ull;
