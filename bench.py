@@ -557,7 +557,7 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
     kavg = kms.mean(axis=0)
     res = {"nbits": int(nbits), "nbytes": int(nbytes), "wall": wall, "enc_ms": enc_ms, "dec_ms": dec_ms,
            "kavg": kavg, "status": int(status | warm_status), "warm_status": int(warm_status), "resends": resends[0],
-           "slow_path_timed": slow[0]}
+           "slow_path_timed": slow[0], "v3": bool(L.last_decode_was_v3())}
 
     if pipelined and ber <= 0:
         # the same K steps pipelined (encode k+1 || decode k, two stream buffers), reported beside value
@@ -626,19 +626,23 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
     return res
 
 
-def kernel_table(ct, n, nbytes, kavg):
+def kernel_table(ct, n, nbytes, kavg, v3=True):
+    """The six timed launches of a step (library timing slots, HIP events on the library stream) and their
+    algorithmic bytes: the encoder's count / scan / pack launches, then the decoder's three -- the segment
+    decoder (parse3, link fixes + scan3, decode3) or, for streams it hands over, the chunk-map decoder."""
     kernels = {   # name: (avg ms, algorithmic bytes per launch)
         f"encode_count_kernel<{ct}>": (float(kavg[0]), 4.0 * n),
         "encode_scan_kernel": (float(kavg[1]), 0.0),
-        f"encode_write_kernel<{ct}>": (float(kavg[2]), 4.0 * n + nbytes),
-        f"parse_kernel<{ct}>": (float(kavg[3]), float(nbytes)),
-        "tile_fix_kernel+tile_scan_kernel": (float(kavg[4]), 0.0),
-        f"decode_kernel_fast<{ct}>": (float(kavg[5]), nbytes + 4.0 * n),
+        f"encode_pack_kernel<{ct}>": (float(kavg[2]), 4.0 * n + nbytes),
     }
-    if kavg[0] < 1e-3 and kavg[1] < 1e-3:             # single-pass encoder: one fused launch
-        kernels.pop(f"encode_count_kernel<{ct}>")
-        kernels.pop("encode_scan_kernel")
-        kernels[f"encode_fused_kernel<{ct}>"] = kernels.pop(f"encode_write_kernel<{ct}>")
+    if v3:
+        kernels.update({f"parse3_kernel<{ct}>": (float(kavg[3]), float(nbytes)),
+                        f"scan3_kernel<{ct}>": (float(kavg[4]), 0.0),
+                        f"decode3_kernel<{ct}>": (float(kavg[5]), nbytes + 4.0 * n)})
+    else:
+        kernels.update({f"parse_kernel<{ct}>": (float(kavg[3]), float(nbytes)),
+                        "tile_fix_kernel+tile_scan_kernel": (float(kavg[4]), 0.0),
+                        f"decode_kernel_fast<{ct}>": (float(kavg[5]), nbytes + 4.0 * n)})
     return kernels
 
 
@@ -647,7 +651,7 @@ def line_for(C, W, R, steps):
     kernel (algorithmic bytes / its HIP-event duration on the library stream) and of the whole step."""
     n, nbytes = W["n"], R["nbytes"]
     ms = R["wall"] / steps * 1e3
-    kernels = kernel_table(W["ct"], n, nbytes, R["kavg"])
+    kernels = kernel_table(W["ct"], n, nbytes, R["kavg"], R["v3"])
     dname = max(kernels, key=lambda k: kernels[k][0])
     dms, dbytes = kernels[dname]
     ach = dbytes / (dms * 1e-3) / 1e9 if dms > 0 else 0.0
@@ -701,7 +705,7 @@ def main():
         # warm-up on run it inside every timed step and are reported with fast_path false)
         print(f"bench.py: decoder status 0x{R['status']:x} in the timed steps (slow path not timed)", file=sys.stderr)
         sys.exit(1)
-    kernels = kernel_table(ct, n, nbytes, R["kavg"])
+    kernels = kernel_table(ct, n, nbytes, R["kavg"], R["v3"])
     dname = main_line["dominant"]["kernel"]
     traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")

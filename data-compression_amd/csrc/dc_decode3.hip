@@ -488,6 +488,9 @@ __device__ __forceinline__ float prev_job_value(const Dec3Bufs& D3, long long jo
 
 // a decode job's inputs, requested one job ahead (the job's records, its token offset, 12 stream words
 // per lane) so that their latency hides behind the previous job's walk and stores
+#ifndef DC_DEC3_NT
+#define DC_DEC3_NT 1                                // the decoded floats stored past the caches (streaming)
+#endif
 constexpr int D3_OOB = 0x7FFFFFF0;                  // a buffer offset past every range below: reads 0, drops writes
                                                     // (ranges end below 0x7FFFFF00)
 struct Pre3 {
@@ -660,7 +663,7 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
                 sv |= __float_as_uint(v.x) == 0xBF800000u || __float_as_uint(v.y) == 0xBF800000u ||
                       __float_as_uint(v.z) == 0xBF800000u || __float_as_uint(v.w) == 0xBF800000u;
             const u32x4 raw = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
-            __builtin_amdgcn_raw_buffer_store_b128(raw, ro, full ? (int)(4 * gi) : D3_OOB, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(raw, ro, full ? (int)(4 * gi) : D3_OOB, 0, DC_DEC3_NT ? 2 : 0);
         }
         {
             const int qe = lane < 4 ? 0 : Q - 1;
@@ -669,7 +672,7 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
             const bool qfull = 4 * qe >= al && 4 * qe + 4 <= span && gi0 + 4 * qe + 4 <= num;
             const bool ok = fits && lane < 8 && !qfull && idx >= al && idx < span && gi < num;
             const float v = ob[min(max(idx, 0), D3_CAP - 1)];
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ro, ok ? (int)(4 * gi) : D3_OOB, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ro, ok ? (int)(4 * gi) : D3_OOB, 0, DC_DEC3_NT ? 2 : 0);
         }
         if (__any(sent || sv) && lane == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_SENT);
         P3_T(u5);

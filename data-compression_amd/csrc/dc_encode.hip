@@ -6,16 +6,15 @@
 // bit (:5456-5489).
 //
 // The encoder history is the ORIGINAL input (:2095-2097), so every token is a pure function of
-// x[i-3..i].  Three launches, no inter-workgroup waiting:
-//   encode_count_kernel : per tile of ENC_TILE floats, the total token bit length
+// x[i-3..i].  Three launches, no workgroup ever waits for another:
+//   encode_count_kernel : per tile of ENC_TILE floats, the total token bit length and the tile's last
+//                         31 bits (its successor's first word starts with them)
 //   encode_scan_kernel  : exclusive scan of the tile lengths -> every tile's global bit offset G
-//   encode_write_kernel : tokens again, ORed MSB-first into a zeroed LDS bit buffer at offset
-//                         G mod 32 + their prefix (one 64-bit shift, two ds_or each), then the tile
-//                         writes every 32-bit word whose first bit lies in [G, G+T) as byte-swapped
-//                         dwords, completing its last word with the first <= 31 bits of the
-//                         following elements (recomputed locally, <= 11 tokens).
-// The write kernel walks the tiles in reverse so the input the count kernel read last is still in
-// the 256 MiB Infinity Cache when it is read again.
+//   encode_pack_kernel  : the tile's tokens packed MSB-first into an LDS bit buffer (plain word
+//                         writes, neighbour words merged through DPP), then stored shifted by G mod 32:
+//                         every word from the one holding the tile's first bit to its last full word.
+// (A single pass with published tile totals was measured slower: a tile waits for the slowest of
+// its predecessors' loads, 220-700 us against 140 us, see DESIGN.md.)
 #include "dc_device.h"
 #include <algorithm>
 #include <stdlib.h>
@@ -25,12 +24,8 @@ namespace dc {
 constexpr int ENC_TILE = 4096;                  // floats per tile (one offset per tile)
 constexpr int ENC_TPB = 256;                    // write kernel: 4 waves per tile
 constexpr int ENC_K = ENC_TILE / ENC_TPB;       // 16 consecutive floats per lane
-constexpr int ENC_Q = ENC_TILE / 4 / ENC_TPB;   // coalesced float4 loads per lane
 #ifndef DC_CNT_Q
 #define DC_CNT_Q 4
-#endif
-#ifndef DC_WR_NT
-#define DC_WR_NT 0
 #endif
 #ifndef DC_CNT_NT
 #define DC_CNT_NT 1                     // the count pass streams x past the caches: measured count 85 -> 57 us
@@ -38,19 +33,6 @@ constexpr int ENC_Q = ENC_TILE / 4 / ENC_TPB;   // coalesced float4 loads per la
 constexpr int CNT_Q = DC_CNT_Q;                 // count kernel: one wave per tile part, CNT_Q float4 per lane
 constexpr int CNT_SUB = 256 * CNT_Q;            // floats per count wave
 constexpr int CNT_PARTS = ENC_TILE / CNT_SUB;   // count parts per tile (tbits entries)
-constexpr int ENC_LDS_WORDS = ENC_TILE + 48;    // 32 bits/elem max + offset + head slack
-constexpr int STG_WORDS = ENC_TILE + ENC_TILE / 16 + 8;   // staged floats, one pad word per 16
-
-__device__ __forceinline__ void lds_place(uint32_t* s, uint32_t off, uint32_t val, int len) {
-    const uint32_t w = off >> 5, b = off & 31u;
-    const int end = (int)b + len;                                  // 1..63
-    if (end <= 32) {
-        atomicOr(&s[w], val << (32 - end));
-    } else {
-        atomicOr(&s[w], val >> (end - 32));
-        atomicOr(&s[w + 1], val << (64 - end));
-    }
-}
 
 __device__ __forceinline__ float halo_x(const float* __restrict__ x, long long idx0, long long e) {
     // element e - (its history) when it precedes the array: unused by make_token (predict = false)
@@ -152,7 +134,7 @@ __device__ __forceinline__ void count_part(const float* __restrict__ x, long lon
 template <int CT>
 __global__ __launch_bounds__(256) void encode_count_kernel(const float* __restrict__ x, long long n, long long idx0,
                                                            Params P, uint32_t* __restrict__ tcnt, long long ntiles,
-                                                           unsigned* __restrict__ err) {
+                                                           unsigned* __restrict__ err, uint32_t* __restrict__ tails) {
     static_assert(CNT_PARTS == 4, "one workgroup of four waves per tile");
     __shared__ uint32_t wsum[4];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -161,6 +143,34 @@ __global__ __launch_bounds__(256) void encode_count_kernel(const float* __restri
     float hist[3];
     load_part(x, n, idx0, h * CNT_SUB, lane, f, hist);
     count_part<CT>(x, n, idx0, P, h, f, hist, lane, wsum + wid, err);
+    // the tile's last 31 bits (its successor's first word starts with them): the tokens of its last 16
+    // floats (lanes 60..63 of the last wave, last float4 row; >= 48 bits, all predicted), joined in lane 63
+    if (tails && wid == 3 && (long long)(blockIdx.x + 1) * ENC_TILE <= n) {
+        constexpr int q = CNT_Q - 1;
+        const float xs[7] = {wave_shr1(f[q].y, 0.0f), wave_shr1(f[q].z, 0.0f), wave_shr1(f[q].w, 0.0f),
+                             f[q].x, f[q].y, f[q].z, f[q].w};
+        uint64_t acc = 0;
+        uint32_t L = 0;
+        if (lane >= 60) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                uint32_t tv;
+                int len;
+                make_token_bf<CT>(xs[3 + r], xs[2 + r], xs[1 + r], xs[r], true, P, tv, len);
+                acc = (acc << len) | tv;
+                L += (uint32_t)len;
+            }
+        }
+        uint64_t t = 0;
+#pragma unroll
+        for (int l = 60; l < 64; l++) {
+            const uint64_t a = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(acc >> 32), l) << 32) |
+                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)acc, l);
+            const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((int)L, l);
+            t = (sl >= 64u ? 0ull : (t << sl)) | a;
+        }
+        if (lane == 63) tails[blockIdx.x] = (uint32_t)t & 0x7FFFFFFFu;
+    }
     __syncthreads();
     if (threadIdx.x == 0) tcnt[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
     (void)ntiles;
@@ -173,7 +183,8 @@ constexpr int SCAN_T = 16;
 constexpr int SCAN_CH = 1024 * SCAN_T;
 __global__ __launch_bounds__(1024) void encode_scan_kernel(const uint32_t* __restrict__ tcnt, uint64_t* __restrict__ toff,
                                                            long long ntiles, int start_bit,
-                                                           unsigned long long* __restrict__ total_bits) {
+                                                           unsigned long long* __restrict__ total_bits,
+                                                           unsigned long long* __restrict__ total_bits2) {
     __shared__ uint32_t cnt[SCAN_CH + SCAN_CH / 16];           // also the u64 offsets of half the tiles
     __shared__ unsigned long long wtot[1024 / 64];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -239,396 +250,207 @@ __global__ __launch_bounds__(1024) void encode_scan_kernel(const uint32_t* __res
         carry += tot;
         __syncthreads();                                             // cnt / wtot are rewritten
     }
-    if (tid == 0) *total_bits = carry;
-}
-
-// a tile's floats as coalesced float4s: thread tid holds float4 number tid + ENC_TPB*q
-__device__ __forceinline__ void load_tile4(const float* __restrict__ x, long long n, long long tbase, int tid, float4* f) {
-    if (tbase + ENC_TILE <= n) {
-        const float4* p4 = reinterpret_cast<const float4*>(x + tbase);
-#pragma unroll
-        for (int q = 0; q < ENC_Q; q++) {
-#if DC_WR_NT
-            typedef float f4v __attribute__((ext_vector_type(4)));
-            const f4v w = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p4 + tid + ENC_TPB * q));
-            f[q] = make_float4(w.x, w.y, w.z, w.w);
-#else
-            f[q] = p4[tid + ENC_TPB * q];
-#endif
-        }
-    } else {
-#pragma unroll
-        for (int q = 0; q < ENC_Q; q++) {
-            const long long e = tbase + 4 * (tid + ENC_TPB * q);
-            f[q].x = e < n ? x[e] : 0.0f; f[q].y = e + 1 < n ? x[e + 1] : 0.0f;
-            f[q].z = e + 2 < n ? x[e + 2] : 0.0f; f[q].w = e + 3 < n ? x[e + 3] : 0.0f;
-        }
-    }
-}
-
-template <int CT>
-__global__ __launch_bounds__(ENC_TPB) void encode_write_kernel(
-    const float* __restrict__ x, long long n, long long idx0, Params P, uint32_t* __restrict__ out,
-    const uint64_t* __restrict__ toff, unsigned ntiles, unsigned long long* __restrict__ dbg) {
-    __shared__ uint32_t s_bits[STG_WORDS > ENC_LDS_WORDS ? STG_WORDS : ENC_LDS_WORDS];   // staging, then bits
-    __shared__ uint32_t s_wsum[ENC_TPB / 64];
-    __shared__ uint32_t s_head_val[12];
-    __shared__ int s_head_len[12];
-
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    for (unsigned k = blockIdx.x; k < ntiles; k += gridDim.x) {
-    const unsigned tile = ntiles - 1 - k;
-#define ESTAMP(ph) do { if (dbg && tid == 0 && tile < 8192) dbg[tile * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-    ESTAMP(0);
-    const long long tbase = (long long)tile * ENC_TILE;
-    const long long base = tbase + (long long)tid * ENC_K;
-    const unsigned long long G = toff[tile];
-    const bool full = tbase + ENC_TILE <= n && idx0 + tbase >= 3;
-    // the first elements of the next tile (for the head tokens) are loaded now, used after the tokens
-    float h0 = 0.0f, h1 = 0.0f, h2 = 0.0f, h3 = 0.0f;
-    const bool hin = wid == 1 && lane < 11 && tbase + ENC_TILE + lane < n;
-    if (hin) {
-        const long long e = tbase + ENC_TILE + lane;
-        h0 = x[e]; h1 = x[e - 1]; h2 = x[e - 2]; h3 = x[e - 3];
-    }
-    // ---- coalesced float4 loads -> LDS (one pad word per 16 floats), then 16 consecutive per lane
-    {
-        float4 f[ENC_Q];
-        load_tile4(x, n, tbase, tid, f);
-#pragma unroll
-        for (int q = 0; q < ENC_Q; q++) {
-            const int e = 4 * (tid + ENC_TPB * q);
-            float* d = reinterpret_cast<float*>(s_bits) + 8 + e + (e >> 4);
-            d[0] = f[q].x; d[1] = f[q].y; d[2] = f[q].z; d[3] = f[q].w;
-        }
-        if (tid < 3) reinterpret_cast<float*>(s_bits)[5 + tid] = halo_x(x, idx0, tbase - 3 + tid);
-    }
-    __syncthreads();
-    float v[ENC_K + 4];
-#pragma unroll
-    for (int j = 1; j < ENC_K + 4; j++) {
-        const int e = tid * ENC_K + j - 4;                           // tile-relative element (>= -3)
-        v[j] = reinterpret_cast<const float*>(s_bits)[e < 0 ? 8 + e : 8 + e + (e >> 4)];
-    }
-    __syncthreads();
-    for (int i = tid; i < ENC_LDS_WORDS; i += ENC_TPB) s_bits[i] = 0u;
-
-    // ---- tokens
-    uint32_t tv[ENC_K];
-    uint32_t tlp[ENC_K / 4];                                         // token lengths, 4 per register
-#pragma unroll
-    for (int q = 0; q < ENC_K / 4; q++) tlp[q] = 0u;
-    uint32_t mysum = 0;
-    if (full) {
-#pragma unroll
-        for (int j = 0; j < ENC_K; j++) {
-            int len;
-            make_token_bf<CT>(v[4 + j], v[3 + j], v[2 + j], v[1 + j], true, P, tv[j], len);
-            tlp[j >> 2] |= (uint32_t)len << (8 * (j & 3));
-            mysum += (uint32_t)len;
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < ENC_K; j++) {
-            int len;
-            make_token_bf<CT>(v[4 + j], v[3 + j], v[2 + j], v[1 + j], idx0 + base + j >= 3, P, tv[j], len);
-            len = base + j < n ? len : 0;
-            tv[j] = len ? tv[j] : 0u;
-            tlp[j >> 2] |= (uint32_t)len << (8 * (j & 3));
-            mysum += (uint32_t)len;
-        }
-    }
-    ESTAMP(1);
-
-    // ---- workgroup exclusive scan of bit lengths
-    uint32_t inc = mysum;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t t = __shfl_up(inc, d, 64);
-        if (lane >= d) inc += t;
-    }
-    if (lane == 63) s_wsum[wid] = inc;
-
-    // ---- head: first <= 31 bits of the elements after this tile (completes our last word)
-    if (wid == 1 && lane < 12) {
-        uint32_t hv = 0u; int hl = 0;
-        if (lane < 11 && hin) make_token<CT>(h0, h1, h2, h3, idx0 + tbase + ENC_TILE + lane >= 3, P, hv, hl);
-        s_head_val[lane] = hv;
-        s_head_len[lane] = hl;
-    }
-    __syncthreads();
-    uint32_t wpre = 0, T = 0;
-#pragma unroll
-    for (int w = 0; w < ENC_TPB / 64; w++) {
-        if (w < wid) wpre += s_wsum[w];
-        T += s_wsum[w];
-    }
-    const uint32_t boff = (uint32_t)(G & 31ull);
-    const long long wb = (long long)(G >> 5);
-    ESTAMP(2);
-
-    // ---- MSB-first packing: the LDS bit buffer is zeroed, so every token is ORed in at its bit
-    // offset (measured faster than lane-local word assembly with divergent stores)
-    {
-        uint32_t off = boff + wpre + inc - mysum;
-#pragma unroll
-        for (int j = 0; j < ENC_K; j++) {
-            const int len = (int)((tlp[j >> 2] >> (8 * (j & 3))) & 0xFFu);
-            const uint64_t v = (uint64_t)tv[j] << ((64 - (int)(off & 31u) - len) & 63);   // len 0: tv = 0
-            uint32_t* d = s_bits + (off >> 5);
-            atomicOr(d, (uint32_t)(v >> 32));
-            atomicOr(d + 1, (uint32_t)v);
-            off += (uint32_t)len;
-        }
-    }
-    __syncthreads();
     if (tid == 0) {
-        uint32_t ho = boff + T;
-        for (int j = 0; j < 11 && s_head_len[j]; j++) {
-            if (ho - boff - T >= 32u) break;
-            lds_place(s_bits, ho, s_head_val[j], s_head_len[j]);
-            ho += (uint32_t)s_head_len[j];
-        }
-    }
-    __syncthreads();
-    ESTAMP(3);
-
-    // ---- write owned words: first bit in [G, G+T) (tile 0 also owns the start_bit prefix word)
-    const unsigned long long Gend = G + T;
-    long long w0 = (long long)((G + 31) >> 5);
-    if (tile == 0) w0 = 0;
-    const long long w1 = (long long)((Gend + 31) >> 5);
-    for (long long w = w0 + tid; w < w1; w += ENC_TPB) out[w] = __builtin_bswap32(s_bits[w - wb]);
-    ESTAMP(4);
-    ESTAMP(5);
-    __syncthreads();                                                 // s_bits is restaged next tile
+        *total_bits = carry;
+        if (total_bits2) *total_bits2 = carry;
     }
 }
 
 // ------------------------------------------------------------------------------------------------
-// Single-pass encoder: encode_write_kernel's tile work with the tile offset from a decoupled
-// look-back instead of the count + scan launches.  A tile publishes its bit count as soon as its
-// workgroup scan is done (flag status 1), packs its tokens into LDS at a tile-relative offset (bit 0
-// of buffer word 1; word 0 stays zero), and only then looks back: wave 0 reads the flags of the 64
-// preceding tiles at once, adds the counts up to the nearest inclusive prefix (status 2) and moves
-// 64 tiles further back if there is none.  Tiles are claimed in increasing order from an atomic
-// counter, so every predecessor is running or done (no deadlock).  The tile publishes its inclusive
-// prefix, then stores its owned words shifted into place with v_alignbit (G mod 32).
-// flags[t] = status << 62 | (epoch mod 2^22) << 40 | value (40 bits)
-__device__ __forceinline__ uint64_t eflag(uint64_t st, uint32_t epoch, unsigned long long v) {
-    return (st << 62) | ((uint64_t)(epoch & 0x3FFFFFu) << 40) | (v & 0xFFFFFFFFFFull);
+// Pack kernel (third launch): one workgroup per tile reads its floats, makes the tokens, packs them into
+// an LDS bit buffer and stores them at the tile's bit offset G from the scan.  The word holding the
+// tile's first bit starts with the last G mod 32 bits of the previous tile (its tail, from the count
+// kernel): the tile stores every word from there up to its last full word; the last tile also stores
+// its final partial word.  No tile waits for another.
+// Registers decide the occupancy (LDS: 17 KB per tile): the lengths are made first (token_len_enc,
+// the same decision as make_token_bf) and the token values again while packing.
+#ifndef DC_PACK_NT
+#define DC_PACK_NT 1                            // x read and the stream written past the caches (streaming)
+#endif
+constexpr int E3_WORDS = ENC_TILE + 64;                 // bit buffer words (4096 at 32 bits per float)
+constexpr int E3_STG = 64 * ENC_K / 16 * 20;            // a wave's staged floats (rows of 16 + 4 pad)
+constexpr int E3_LDS = E3_WORDS > 4 * E3_STG ? E3_WORDS : 4 * E3_STG;
+__device__ __forceinline__ uint32_t wave_shr1_u(uint32_t v, uint32_t first) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xF, 0xF, false);
 }
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int FBUF = (STG_WORDS > ENC_LDS_WORDS ? STG_WORDS : ENC_LDS_WORDS) + 1;
-
-// tile work up to the packed bits: stage, tokens, workgroup scan, head tokens, publish the count
-// (flag status 1, tile 0: inclusive), pack at the tile-relative offset into buf (buf[0] = 0).
-// Returns the tile's bit count T.
 template <int CT>
-__device__ __forceinline__ uint32_t fused_compute(const float* __restrict__ x, long long n, long long idx0, const Params& P,
-                                                  uint64_t* __restrict__ flags, uint32_t epoch, int start_bit,
-                                                  unsigned tile, uint32_t* buf, uint32_t* s_wsum, uint32_t* s_head_val,
-                                                  int* s_head_len, bool& neg1) {
+__global__ __launch_bounds__(ENC_TPB) void encode_pack_kernel(
+    const float* __restrict__ x, long long n, long long idx0, Params P, uint32_t* __restrict__ out,
+    const uint64_t* __restrict__ toff, const uint32_t* __restrict__ tails, unsigned ntiles,
+    unsigned long long* __restrict__ dbg) {
+    static_assert(ENC_K == 16 && ENC_TPB == 256, "16 consecutive floats per thread, 4 waves per tile");
+#define E3STAMP(ph) do { if (dbg && threadIdx.x == 0 && blockIdx.x < 8192) dbg[blockIdx.x * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+    E3STAMP(0);
+    __shared__ __attribute__((aligned(16))) uint32_t sb[E3_LDS];
+    __shared__ uint32_t s_w[ENC_TPB / 64];
+    __shared__ uint32_t s_hw[4], s_hi[4], s_tw[4], s_ti[4];           // the waves' first and last words
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const unsigned tile = blockIdx.x;
+    const unsigned long long Gt = toff[tile];                          // (requested first: scalar loads)
+    const uint32_t tp0 = tile > 0 ? tails[tile - 1] : 0u;
     const long long tbase = (long long)tile * ENC_TILE;
-    const long long base = tbase + (long long)tid * ENC_K;
+    const long long base = tbase + (long long)ENC_K * tid;
     const bool full = tbase + ENC_TILE <= n && idx0 + tbase >= 3;
-    float h0 = 0.0f, h1 = 0.0f, h2 = 0.0f, h3 = 0.0f;
-    const bool hin = wid == 1 && lane < 11 && tbase + ENC_TILE + lane < n;
-    if (hin) {
-        const long long e = tbase + ENC_TILE + lane;
-        h0 = x[e]; h1 = x[e - 1]; h2 = x[e - 2]; h3 = x[e - 3];
-    }
+    // ---- the thread's 16 consecutive floats.  Coalesced float4 loads (lane l: float4 l + 64q of the
+    // wave's 1024 floats; x through a buffer resource up to the 16-byte granule of its last float:
+    // out-of-range floats read 0, a granule never straddles a page), turned into 16 consecutive floats
+    // per lane through the wave's part of the bit buffer (element e at word e + 4 (e >> 4): rows of 20
+    // words, conflict-free b128 reads; before the packing).  History: the previous thread's last three
+    // (DPP), for lane 0 the three floats before the wave's first.
+    float h[ENC_K + 3];
     {
-        float4 f[ENC_Q];
-        load_tile4(x, n, tbase, tid, f);
+        const __amdgpu_buffer_rsrc_t rsx =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), (short)0, (int)((n + 3) / 4 * 16), 0x00020000);
+        float* stg = reinterpret_cast<float*>(sb) + wid * E3_STG;
+        const long long wb = tbase + 64ll * ENC_K * wid;
+        f32x4 f[ENC_K / 4];
 #pragma unroll
-        for (int q = 0; q < ENC_Q; q++) {
-            const int e = 4 * (tid + ENC_TPB * q);
-            float* d = reinterpret_cast<float*>(buf) + 8 + e + (e >> 4);
-            d[0] = f[q].x; d[1] = f[q].y; d[2] = f[q].z; d[3] = f[q].w;
+        for (int q = 0; q < ENC_K / 4; q++)
+            f[q] = __builtin_amdgcn_raw_buffer_load_b128(rsx, (int)(4 * (wb + 4 * (lane + 64 * q))), 0, DC_PACK_NT ? 2 : 0);
+#pragma unroll
+        for (int q = 0; q < ENC_K / 4; q++) {
+            const int m = lane + 64 * q;
+            *reinterpret_cast<f32x4*>(stg + 4 * m + 4 * (m >> 2)) = f[q];
         }
-        if (tid < 3) reinterpret_cast<float*>(buf)[5 + tid] = halo_x(x, idx0, tbase - 3 + tid);
-    }
-    __syncthreads();
-    float v[ENC_K + 4];
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int j = 1; j < ENC_K + 4; j++) {
-        const int e = tid * ENC_K + j - 4;
-        v[j] = reinterpret_cast<const float*>(buf)[e < 0 ? 8 + e : 8 + e + (e >> 4)];
-    }
-    __syncthreads();
-    for (int i = tid; i < FBUF; i += ENC_TPB) buf[i] = 0u;
-
-    uint32_t tv[ENC_K];
-    uint32_t tlp[ENC_K / 4];
+        for (int q = 0; q < ENC_K / 4; q++) {
+            const f32x4 u = *reinterpret_cast<const f32x4*>(stg + 20 * lane + 4 * q);
+            h[3 + 4 * q] = u.x; h[4 + 4 * q] = u.y; h[5 + 4 * q] = u.z; h[6 + 4 * q] = u.w;
+        }
+        const long long w0 = tbase + 64ll * ENC_K * wid;                   // the wave's first element
+        float hw[3];
 #pragma unroll
-    for (int q = 0; q < ENC_K / 4; q++) tlp[q] = 0u;
+        for (int k = 1; k <= 3; k++) {
+            const long long e = w0 - k;
+            hw[k - 1] = (e < n && e >= -3 && idx0 + e >= 0) ? x[e] : 0.0f;
+        }
+        h[2] = wave_shr1(h[3 + ENC_K - 1], hw[0]);
+        h[1] = wave_shr1(h[3 + ENC_K - 2], hw[1]);
+        h[0] = wave_shr1(h[3 + ENC_K - 3], hw[2]);
+    }
+    if (!full)
+#pragma unroll
+        for (int j = 0; j < ENC_K; j++) h[3 + j] = base + j < n ? h[3 + j] : 0.0f;
+    // ---- token lengths
+    uint32_t lp[ENC_K / 4];
+#pragma unroll
+    for (int q = 0; q < ENC_K / 4; q++) lp[q] = 0u;
     uint32_t mysum = 0;
-    if (full) {
 #pragma unroll
-        for (int j = 0; j < ENC_K; j++) {
-            int len;
-            make_token_bf<CT>(v[4 + j], v[3 + j], v[2 + j], v[1 + j], true, P, tv[j], len);
-            tlp[j >> 2] |= (uint32_t)len << (8 * (j & 3));
-            mysum += (uint32_t)len;
-            neg1 |= v[4 + j] == -1.0f;
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < ENC_K; j++) {
-            int len;
-            make_token_bf<CT>(v[4 + j], v[3 + j], v[2 + j], v[1 + j], idx0 + base + j >= 3, P, tv[j], len);
-            len = base + j < n ? len : 0;
-            tv[j] = len ? tv[j] : 0u;
-            tlp[j >> 2] |= (uint32_t)len << (8 * (j & 3));
-            mysum += (uint32_t)len;
-            neg1 |= base + j < n && v[4 + j] == -1.0f;
-        }
+    for (int j = 0; j < ENC_K; j++) {
+        const bool in = full || base + j < n;
+        int len = token_len_enc<CT>(h[3 + j], h[2 + j], h[1 + j], h[j], full || idx0 + base + j >= 3, P);
+        len = in ? len : 0;
+        lp[j >> 2] |= (uint32_t)len << (8 * (j & 3));
+        mysum += (uint32_t)len;
     }
     uint32_t inc = mysum;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t t = __shfl_up(inc, d, 64);
-        if (lane >= d) inc += t;
+        const uint32_t u = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += u;
     }
-    if (lane == 63) s_wsum[wid] = inc;
-    if (wid == 1 && lane < 12) {
-        uint32_t hv = 0u; int hl = 0;
-        if (lane < 11 && hin) make_token<CT>(h0, h1, h2, h3, idx0 + tbase + ENC_TILE + lane >= 3, P, hv, hl);
-        s_head_val[lane] = hv;
-        s_head_len[lane] = hl;
-    }
+    if (lane == 63) s_w[wid] = inc;
+    E3STAMP(1);
     __syncthreads();
     uint32_t wpre = 0, T = 0;
 #pragma unroll
     for (int w = 0; w < ENC_TPB / 64; w++) {
-        if (w < wid) wpre += s_wsum[w];
-        T += s_wsum[w];
+        if (w < wid) wpre += s_w[w];
+        T += s_w[w];
     }
-    if (tid == 0)                                                    // publish the count early
-        st_relaxed(&flags[tile], tile == 0 ? eflag(2, epoch, (unsigned long long)start_bit + T) : eflag(1, epoch, T));
-    uint32_t* bb = buf + 1;                                          // tile bit 0 = MSB of buf[1]
-    {
-        uint32_t off = wpre + inc - mysum;
+    const uint32_t off = wpre + inc - mysum;                          // the thread's first tile bit
+
+    // the floats made opaque: otherwise the compiler keeps every predictor term of the length pass
+    // alive across the barrier for the value pass (200+ VGPRs, 2 waves per SIMD)
+#pragma unroll
+    for (int j = 0; j < ENC_K + 3; j++) asm volatile("" : "+v"(h[j]));
+    // ---- pack, MSB-first (token values made again here).  Full tiles: every thread holds >= 48 bits,
+    // so a word is shared by at most two neighbouring threads: each writes the words it completes, its
+    // first merged with the previous lane's unfinished last one (DPP); a wave's first and last words
+    // are merged after the barrier
+    if (full) {
+        uint32_t wi = off >> 5, nb = off & 31u, headw = 0u;
+        const uint32_t hi = wi;
+        uint64_t acc = 0;
+        bool have = false;
 #pragma unroll
         for (int j = 0; j < ENC_K; j++) {
-            const int len = (int)((tlp[j >> 2] >> (8 * (j & 3))) & 0xFFu);
-            const uint64_t vv = (uint64_t)tv[j] << ((64 - (int)(off & 31u) - len) & 63);
-            uint32_t* d = bb + (off >> 5);
-            atomicOr(d, (uint32_t)(vv >> 32));
-            atomicOr(d + 1, (uint32_t)vv);
-            off += (uint32_t)len;
-        }
-    }
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t ho = T;
-        for (int j = 0; j < 11 && s_head_len[j]; j++) {
-            if (ho - T >= 32u) break;
-            lds_place(bb, ho, s_head_val[j], s_head_len[j]);
-            ho += (uint32_t)s_head_len[j];
-        }
-    }
-    __syncthreads();
-    return T;
-}
-
-// look-back for the tile's exclusive prefix G (wave 0), publish the inclusive prefix, store the owned
-// words of buf shifted into place
-__device__ __forceinline__ void fused_finish(uint32_t* __restrict__ out, uint64_t* __restrict__ flags, uint32_t epoch,
-                                             int start_bit, unsigned tile, unsigned ntiles, uint32_t T, const uint32_t* buf,
-                                             unsigned long long* __restrict__ total_bits, unsigned* __restrict__ err,
-                                             unsigned long long* s_G) {
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    if (wid == 0) {
-        unsigned long long G = (unsigned long long)start_bit;
-        if (tile > 0) {
-            unsigned long long acc = 0;
-            long long k = (long long)tile - 1;
-            unsigned spins = 0;
-            while (true) {
-                const long long q = k - lane;
-                const uint64_t fv = q >= 0 ? ld_relaxed(&flags[q]) : eflag(2, epoch, 0);
-                const bool mine = ((fv >> 40) & 0x3FFFFFu) == (epoch & 0x3FFFFFu);
-                const int stt = mine ? (int)(fv >> 62) : 0;
-                const unsigned long long incl = __ballot(stt == 2);
-                const int fi = incl ? __ffsll((long long)incl) - 1 : 64;
-                const unsigned long long need = fi == 64 ? ~0ull : ((2ull << fi) - 1ull);
-                if (__ballot(stt == 0) & need) {                     // a predecessor has not published yet
-                    if (++spins > (1u << 22)) { if (lane == 0) atomicOr(err, 4u); break; }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                unsigned long long val = (lane <= fi) ? (fv & 0xFFFFFFFFFFull) : 0ull;
-#pragma unroll
-                for (int d = 32; d >= 1; d >>= 1) val += __shfl_xor(val, d, 64);
-                acc += val;
-                if (fi < 64) break;
-                k -= 64;
+            uint32_t tv;
+            int len;
+            make_token_bf<CT>(h[3 + j], h[2 + j], h[1 + j], h[j], true, P, tv, len);
+            acc |= (uint64_t)tv << ((64u - nb - (uint32_t)len) & 63u);
+            nb += (uint32_t)len;
+            if (nb >= 32u) {
+                const uint32_t w = (uint32_t)(acc >> 32);
+                if (have) sb[wi] = w;
+                else headw = w;
+                have = true;
+                wi++;
+                acc <<= 32;
+                nb -= 32u;
             }
-            G = acc;
         }
-        if (lane == 0) {
-            *s_G = G;
-            if (tile > 0) st_relaxed(&flags[tile], eflag(2, epoch, G + T));
-            if (tile == ntiles - 1) *total_bits = G + T;
+        const uint32_t tailw = (uint32_t)(acc >> 32);                 // nb bits (0: none)
+        const uint32_t pt = wave_shr1_u(tailw, 0u);
+        if (lane == 0) { s_hw[wid] = headw; s_hi[wid] = hi; }
+        else sb[hi] = headw | pt;
+        if (lane == 63) { s_tw[wid] = tailw; s_ti[wid] = nb ? wi : 0xFFFFFFFFu; }
+    } else {
+        // tile 0 of a stream and the last tile: ORed in token by token over a cleared buffer
+        for (int i = tid; i < E3_WORDS / 4; i += ENC_TPB) reinterpret_cast<uint4*>(sb)[i] = make_uint4(0u, 0u, 0u, 0u);
+        __syncthreads();
+        uint32_t o = off;
+#pragma unroll
+        for (int j = 0; j < ENC_K; j++) {
+            const uint32_t lj = (lp[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            uint32_t tv;
+            int len;
+            make_token_bf<CT>(h[3 + j], h[2 + j], h[1 + j], h[j], idx0 + base + j >= 3, P, tv, len);
+            if (lj) {
+                const uint64_t v = (uint64_t)tv << ((64u - (o & 31u) - lj) & 63u);
+                atomicOr(&sb[o >> 5], (uint32_t)(v >> 32));
+                if ((o & 31u) + lj > 32u) atomicOr(&sb[(o >> 5) + 1], (uint32_t)v);
+            }
+            o += lj;
         }
+        if (lane == 0) s_hi[wid] = 0xFFFFFFFFu;
+        if (lane == 63) s_ti[wid] = 0xFFFFFFFFu;
+    }
+    E3STAMP(2);
+    __syncthreads();
+    // ---- the waves' boundary words: the head of wave w merged with the tail of wave w - 1
+    if (tid < 4) {
+        const uint32_t hi = s_hi[tid];
+        if (hi != 0xFFFFFFFFu) {
+            uint32_t w = s_hw[tid];
+            if (tid > 0 && s_ti[tid - 1] == hi) w |= s_tw[tid - 1];
+            sb[hi] = w;
+        }
+        if (tid == 3 && s_ti[3] != 0xFFFFFFFFu) sb[s_ti[3]] = s_tw[3];     // the tile's last word
     }
     __syncthreads();
-    const unsigned long long G = *s_G;
-    const int sh = (int)(G & 31ull);
-    const long long wb = (long long)(G >> 5);
-    long long w0 = (long long)((G + 31) >> 5);
-    if (tile == 0) w0 = 0;
-    const long long w1 = (long long)((G + T + 31) >> 5);
-    for (long long w = w0 + tid; w < w1; w += ENC_TPB) {
-        const long long i = w - wb;
-        const uint32_t val = sh ? __builtin_amdgcn_alignbit(buf[i], buf[i + 1], (uint32_t)sh) : buf[i + 1];
-        out[w] = __builtin_bswap32(val);
+    E3STAMP(3);
+    // ---- store the words from the one holding the tile's first bit to its last full one
+    const uint32_t sh = (uint32_t)(Gt & 31ull);
+    const long long W0 = (long long)(Gt >> 5);
+    const int nw = (int)((long long)((Gt + T) >> 5) - W0) + ((tile == ntiles - 1 && ((Gt + T) & 31ull)) ? 1 : 0);
+    const int tw = (int)((T + 31u) >> 5);                              // buffer words holding tile bits
+    for (int i = tid; i < nw; i += ENC_TPB) {
+        const uint32_t cur = i < tw ? sb[i] : 0u;                      // (stale past the tile's bits)
+        const uint32_t prev = i ? sb[i - 1] : tp0;
+        const uint32_t w = sh ? __builtin_amdgcn_alignbit(prev, cur, sh) : cur;
+#if DC_PACK_NT
+        __builtin_nontemporal_store(__builtin_bswap32(w), out + W0 + i);
+#else
+        out[W0 + i] = __builtin_bswap32(w);
+#endif
     }
-}
-
-// Tiles are software-pipelined: the workgroup computes and packs tile t+1 into its second buffer
-// before it looks back for tile t, so the look-back latency overlaps the next tile's work.
-template <int CT>
-__global__ __launch_bounds__(ENC_TPB) void encode_fused_kernel(
-    const float* __restrict__ x, long long n, long long idx0, Params P, uint32_t* __restrict__ out,
-    uint64_t* __restrict__ flags, unsigned* __restrict__ ctr, uint32_t epoch, int start_bit, unsigned ntiles,
-    unsigned long long* __restrict__ total_bits, unsigned* __restrict__ err) {
-    __shared__ uint32_t s_buf[2][FBUF];
-    __shared__ uint32_t s_wsum[ENC_TPB / 64];
-    __shared__ uint32_t s_head_val[12];
-    __shared__ int s_head_len[12];
-    __shared__ unsigned s_tile;
-    __shared__ unsigned long long s_G;
-    const int tid = threadIdx.x, lane = tid & 63;
-    bool neg1 = false;
-    if (tid == 0) s_tile = atomicAdd(&ctr[0], 1u);
-    __syncthreads();
-    unsigned cur = s_tile;
-    int cb = 0;
-    uint32_t Tcur = 0;
-    if (cur < ntiles) Tcur = fused_compute<CT>(x, n, idx0, P, flags, epoch, start_bit, cur, s_buf[0], s_wsum, s_head_val,
-                                               s_head_len, neg1);
-    while (cur < ntiles) {
-        __syncthreads();
-        if (tid == 0) s_tile = atomicAdd(&ctr[0], 1u);
-        __syncthreads();
-        const unsigned nxt = s_tile;
-        uint32_t Tn = 0;
-        if (nxt < ntiles) Tn = fused_compute<CT>(x, n, idx0, P, flags, epoch, start_bit, nxt, s_buf[cb ^ 1], s_wsum,
-                                                 s_head_val, s_head_len, neg1);
-        fused_finish(out, flags, epoch, start_bit, cur, ntiles, Tcur, s_buf[cb], total_bits, err, &s_G);
-        cur = nxt;
-        Tcur = Tn;
-        cb ^= 1;
-    }
-    if (CT != 6 && __any(neg1) && lane == 0) atomicOr(err, 1u);      // -1.0f is the reference's sentinel
-    if (tid == 0) {
-        __threadfence();
-        if (atomicAdd(&ctr[1], 1u) == gridDim.x - 1) { atomicExch(&ctr[0], 0u); atomicExch(&ctr[1], 0u); }
-    }
+    E3STAMP(4);
+#undef E3STAMP
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -641,65 +463,27 @@ __global__ __launch_bounds__(ENC_TPB) void encode_fused_kernel(
         default: return -2;                                                                        \
     }
 
-// write kernel grid: one workgroup per tile (measured best: write 165 -> 159 us against a resident-count
-// persistent grid, 2048 and 4096 in between); DC_WRITE_GRID overrides it for sweeps
-static unsigned write_grid() {
-    static unsigned g = [] {
-        const char* e = getenv("DC_WRITE_GRID");
-        return (e && atoi(e) > 0) ? (unsigned)atoi(e) : (1u << 30);
-    }();
-    return g;
-}
-
-static unsigned fused_grid(int ct) {
-    static unsigned cache[12];
-    const int ci = (ct > 0 && ct < 12) ? ct : 0;
-    if (cache[ci]) return cache[ci];
-    int dev = 0, ncu = 256, per = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    const void* f = ct == 5 ? (const void*)encode_fused_kernel<5> : ct == 6 ? (const void*)encode_fused_kernel<6>
-                  : ct == 7 ? (const void*)encode_fused_kernel<7> : (const void*)encode_fused_kernel<11>;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, ENC_TPB, 0) != hipSuccess || per < 1) per = 1;
-    cache[ci] = (unsigned)(per * ncu);
-    return cache[ci];
-}
-
 extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, const Params* P,
                                 uint32_t* out, uint64_t* desc, unsigned* tile_ctr, uint32_t epoch,
-                                int start_bit, unsigned long long* total_bits, unsigned* err,
-                                unsigned long long* dbg, hipStream_t stream) {
+                                int start_bit, unsigned long long* total_bits, unsigned long long* total_bits2,
+                                unsigned* err, unsigned long long* dbg, hipStream_t stream) {
+    (void)tile_ctr;
     if (n <= 0) return 0;
     const unsigned ntiles = (unsigned)((n + ENC_TILE - 1) / ENC_TILE);
-    // single pass (decoupled look-back, software-pipelined tiles): measured 284 us against 257 us for
-    // count + scan + write at 2^26 U10 (the write kernel re-reads its tiles from the Infinity Cache
-    // and hides their latency across 65536 count workgroups); kept as an option, DC_ENC_FUSED=1
-    static int fused = -1;
-    if (fused < 0) fused = getenv("DC_ENC_FUSED") ? 1 : 0;
-    if (fused && !dbg) {
-        const unsigned gf = std::min<unsigned>(ntiles, fused_grid(P->ct));
-        dc_mark_phase(0, stream);
-        dc_mark_phase(1, stream);
-        dc_mark_phase(2, stream);
-        DC_ENC_DISPATCH(encode_fused_kernel, dim3(gf), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, desc, tile_ctr,
-                        epoch, start_bit, ntiles, total_bits, err);
-        dc_mark_phase(3, stream);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    }
-    uint32_t* tbits = reinterpret_cast<uint32_t*>(desc + ntiles);     // tile counts; desc: dc_encode_desc_words(n)
+    // desc: tile offsets (u64) | tile bit counts (u32) | tile tails (u32)
+    uint32_t* tbits = reinterpret_cast<uint32_t*>(desc + ntiles);
+    uint32_t* tails = tbits + ntiles + (ntiles & 1u);
     dc_mark_phase(0, stream);
-    // count: one workgroup per tile (a persistent count grid with prefetch measured slower)
-    const unsigned gc = ntiles;                                    // count: one workgroup per tile
-    const unsigned gw = std::min<unsigned>(ntiles, write_grid());
-    DC_ENC_DISPATCH(encode_count_kernel, dim3(gc), dim3(256), 0, stream, x, n, idx0, *P, tbits,
-                    (long long)ntiles, err);
+    DC_ENC_DISPATCH(encode_count_kernel, dim3(ntiles), dim3(256), 0, stream, x, n, idx0, *P, tbits,
+                    (long long)ntiles, err, tails);
     dc_mark_phase(1, stream);
     hipLaunchKernelGGL(encode_scan_kernel, dim3(1), dim3(1024), 0, stream, tbits, desc, (long long)ntiles, start_bit,
-                       total_bits);
+                       total_bits, total_bits2);
     dc_mark_phase(2, stream);
-    DC_ENC_DISPATCH(encode_write_kernel, dim3(gw), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, desc, ntiles,
-                    dbg);
+    DC_ENC_DISPATCH(encode_pack_kernel, dim3(ntiles), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, desc, tails,
+                    ntiles, dbg);
     dc_mark_phase(3, stream);
+    (void)tile_ctr; (void)epoch;
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -710,17 +494,19 @@ extern "C" int dc_launch_encode_bits(const float* x, long long n, long long idx0
     const unsigned ntiles = (unsigned)((n + ENC_TILE - 1) / ENC_TILE);
     uint32_t* tbits = reinterpret_cast<uint32_t*>(desc + ntiles);
     const unsigned gc = ntiles;
-    DC_ENC_DISPATCH(encode_count_kernel, dim3(gc), dim3(256), 0, stream, x, n, idx0, *P, tbits, (long long)ntiles, err);
-    hipLaunchKernelGGL(encode_scan_kernel, dim3(1), dim3(1024), 0, stream, tbits, desc, (long long)ntiles, 0, total_bits);
+    DC_ENC_DISPATCH(encode_count_kernel, dim3(gc), dim3(256), 0, stream, x, n, idx0, *P, tbits, (long long)ntiles, err,
+                    nullptr);
+    hipLaunchKernelGGL(encode_scan_kernel, dim3(1), dim3(1024), 0, stream, tbits, desc, (long long)ntiles, 0, total_bits,
+                       nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 extern "C" long long dc_encode_tile_count(long long n) { return (n + ENC_TILE - 1) / ENC_TILE; }
 
-// u64 words of the encode descriptor buffer: tile offsets + 32-bit tile-part counts
+// u64 words of the encode descriptor buffer: tile offsets + 32-bit tile counts + 32-bit tile tails
 extern "C" long long dc_encode_desc_words(long long n) {
     const long long nt = dc_encode_tile_count(n);
-    return nt + (nt + 1) / 2;
+    return nt + (nt + 1) / 2 + (nt + 1) / 2 + 1;                          // offsets, counts, tails
 }
 
 }  // namespace dc

@@ -363,7 +363,7 @@ static int encode_on(hipStream_t st, int ct, const void* d_x, long long n, long 
         G.enc_desc_cap = cap;
         G.enc_epoch = 1;
     }
-    if (++G.enc_epoch >= (1u << 22)) {          /* flags carry 22 epoch bits */
+    if (++G.enc_epoch >= (1u << 14)) {          /* tile totals carry 14 epoch bits */
         HIPCHK(hipMemsetAsync(G.enc_desc, 0, G.enc_desc_cap * sizeof(uint64_t), st));
         G.enc_epoch = 1;
     }
@@ -379,10 +379,10 @@ static int encode_on(hipStream_t st, int ct, const void* d_x, long long n, long 
         HIPCHK(hipMalloc((void**)&G.enc_dbg, 8192 * 8 * 8));
         HIPCHK(hipMemset(G.enc_dbg, 0, 8192 * 8 * 8));
     }
+    /* the kernel writes the total to both (no copy node per encode) */
     if (dc_launch_encode((const float*)d_x, n, idx0, &P, (uint32_t*)d_out, G.enc_desc, G.enc_ctr, G.enc_epoch,
-                         start_bit, tot, G.d_enc_err, G.enc_dbg, st))
+                         start_bit, tot, tot != G.d_total ? G.d_total : NULL, G.d_enc_err, G.enc_dbg, st))
         return seterr(DC_ERR_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
-    if (tot != G.d_total) HIPCHK(hipMemcpyAsync(G.d_total, tot, 8, hipMemcpyDeviceToDevice, st));
     return DC_OK;
 }
 

@@ -95,7 +95,8 @@ typedef struct ihipStream_t* dc_hip_stream;
 
 int dc_launch_encode(const float* x, long long n, long long idx0, const DC_NS Params* P, uint32_t* out,
                      uint64_t* desc, unsigned* tile_ctr, uint32_t epoch, int start_bit,
-                     unsigned long long* total_bits, unsigned* err, unsigned long long* dbg, dc_hip_stream stream);
+                     unsigned long long* total_bits, unsigned long long* total_bits2, unsigned* err,
+                     unsigned long long* dbg, dc_hip_stream stream);
 long long dc_encode_tile_count(long long n);
 long long dc_encode_desc_words(long long n);
 int dc_launch_encode_bits(const float* x, long long n, long long idx0, const DC_NS Params* P, uint64_t* desc,
