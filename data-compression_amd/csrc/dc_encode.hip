@@ -49,15 +49,16 @@ __device__ __forceinline__ float lane63(float v) { return __int_as_float(__built
 // lane 0's first element)
 template <int CT>
 __device__ __forceinline__ void count_tokens(const float4* f, float h1, float h2, float h3, const Params& P,
-                                             uint32_t& sum, bool& neg1) {
+                                             uint32_t* qsum, bool& neg1) {
 #pragma unroll
     for (int q = 0; q < CNT_Q; q++) {
         const float b1 = wave_shr1(f[q].w, h1), b2 = wave_shr1(f[q].z, h2), b3 = wave_shr1(f[q].y, h3);
         h1 = lane63(f[q].w); h2 = lane63(f[q].z); h3 = lane63(f[q].y);
         const float xs[7] = {b3, b2, b1, f[q].x, f[q].y, f[q].z, f[q].w};
+        qsum[q] = 0u;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-            sum += (uint32_t)token_len_enc<CT>(xs[3 + r], xs[2 + r], xs[1 + r], xs[r], true, P);
+            qsum[q] += (uint32_t)token_len_enc<CT>(xs[3 + r], xs[2 + r], xs[1 + r], xs[r], true, P);
             neg1 |= xs[3 + r] == -1.0f;
         }
     }
@@ -96,11 +97,13 @@ __device__ __forceinline__ void load_part(const float* __restrict__ x, long long
 template <int CT>
 __device__ __forceinline__ void count_part(const float* __restrict__ x, long long n, long long idx0, const Params& P,
                                            long long h, const float4* f, const float* hist, int lane,
-                                           uint32_t* psum, unsigned* __restrict__ err) {
+                                           uint32_t* psum, unsigned* __restrict__ err, uint32_t* qsum) {
     const long long tb = h * CNT_SUB;
-    uint32_t sum = 0;
     bool neg1 = false;
-    count_tokens<CT>(f, hist[0], hist[1], hist[2], P, sum, neg1);
+    count_tokens<CT>(f, hist[0], hist[1], hist[2], P, qsum, neg1);
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < CNT_Q; q++) sum += qsum[q];
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
     if (lane == 0) {
@@ -134,15 +137,29 @@ __device__ __forceinline__ void count_part(const float* __restrict__ x, long lon
 template <int CT>
 __global__ __launch_bounds__(256) void encode_count_kernel(const float* __restrict__ x, long long n, long long idx0,
                                                            Params P, uint32_t* __restrict__ tcnt, long long ntiles,
-                                                           unsigned* __restrict__ err, uint32_t* __restrict__ tails) {
+                                                           unsigned* __restrict__ err, uint32_t* __restrict__ tails,
+                                                           uint16_t* __restrict__ psum16) {
     static_assert(CNT_PARTS == 4, "one workgroup of four waves per tile");
     __shared__ uint32_t wsum[4];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const long long h = (long long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(wid);
     float4 f[CNT_Q];
     float hist[3];
+    uint32_t qsum[CNT_Q];
     load_part(x, n, idx0, h * CNT_SUB, lane, f, hist);
-    count_part<CT>(x, n, idx0, P, h, f, hist, lane, wsum + wid, err);
+    count_part<CT>(x, n, idx0, P, h, f, hist, lane, wsum + wid, err, qsum);
+    // the bit counts of the pack kernel's threads (16 consecutive floats = float4s 4k..4k+3 of a row q:
+    // a lane quad), for the tiles it packs without counting (whole, every float predicted)
+    const long long tb0 = (long long)blockIdx.x * ENC_TILE;
+    if (psum16 && tb0 + ENC_TILE <= n && idx0 + tb0 >= 3) {
+#pragma unroll
+        for (int q = 0; q < CNT_Q; q++) {
+            uint32_t v = qsum[q];
+            v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
+            v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm 2,3,0,1
+            if ((lane & 3) == 0) psum16[blockIdx.x * ENC_TPB + 64 * wid + 16 * q + (lane >> 2)] = (uint16_t)v;
+        }
+    }
     // the tile's last 31 bits (its successor's first word starts with them): the tokens of its last 16
     // floats (lanes 60..63 of the last wave, last float4 row; >= 48 bits, all predicted), joined in lane 63
     if (tails && wid == 3 && (long long)(blockIdx.x + 1) * ENC_TILE <= n) {
@@ -278,8 +295,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 template <int CT>
 __global__ __launch_bounds__(ENC_TPB) void encode_pack_kernel(
     const float* __restrict__ x, long long n, long long idx0, Params P, uint32_t* __restrict__ out,
-    const uint64_t* __restrict__ toff, const uint32_t* __restrict__ tails, unsigned ntiles,
-    unsigned long long* __restrict__ dbg) {
+    const uint64_t* __restrict__ toff, const uint32_t* __restrict__ tails, const uint16_t* __restrict__ psum16,
+    unsigned ntiles, unsigned long long* __restrict__ dbg) {
     static_assert(ENC_K == 16 && ENC_TPB == 256, "16 consecutive floats per thread, 4 waves per tile");
 #define E3STAMP(ph) do { if (dbg && threadIdx.x == 0 && blockIdx.x < 8192) dbg[blockIdx.x * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); } while (0)
     E3STAMP(0);
@@ -290,6 +307,7 @@ __global__ __launch_bounds__(ENC_TPB) void encode_pack_kernel(
     const unsigned tile = blockIdx.x;
     const unsigned long long Gt = toff[tile];                          // (requested first: scalar loads)
     const uint32_t tp0 = tile > 0 ? tails[tile - 1] : 0u;
+    const uint32_t psum_full = psum16[(long long)tile * ENC_TPB + threadIdx.x];
     const long long tbase = (long long)tile * ENC_TILE;
     const long long base = tbase + (long long)ENC_K * tid;
     const bool full = tbase + ENC_TILE <= n && idx0 + tbase >= 3;
@@ -334,18 +352,22 @@ __global__ __launch_bounds__(ENC_TPB) void encode_pack_kernel(
     if (!full)
 #pragma unroll
         for (int j = 0; j < ENC_K; j++) h[3 + j] = base + j < n ? h[3 + j] : 0.0f;
-    // ---- token lengths
+    // ---- token lengths: whole tiles take the thread's bit count from the count kernel; the first tile
+    // of a stream and the last one count here
     uint32_t lp[ENC_K / 4];
 #pragma unroll
     for (int q = 0; q < ENC_K / 4; q++) lp[q] = 0u;
-    uint32_t mysum = 0;
+    uint32_t mysum = psum_full;
+    if (!full) {
+        mysum = 0;
 #pragma unroll
-    for (int j = 0; j < ENC_K; j++) {
-        const bool in = full || base + j < n;
-        int len = token_len_enc<CT>(h[3 + j], h[2 + j], h[1 + j], h[j], full || idx0 + base + j >= 3, P);
-        len = in ? len : 0;
-        lp[j >> 2] |= (uint32_t)len << (8 * (j & 3));
-        mysum += (uint32_t)len;
+        for (int j = 0; j < ENC_K; j++) {
+            const bool in = base + j < n;
+            int len = token_len_enc<CT>(h[3 + j], h[2 + j], h[1 + j], h[j], idx0 + base + j >= 3, P);
+            len = in ? len : 0;
+            lp[j >> 2] |= (uint32_t)len << (8 * (j & 3));
+            mysum += (uint32_t)len;
+        }
     }
     uint32_t inc = mysum;
 #pragma unroll
@@ -473,15 +495,16 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
     // desc: tile offsets (u64) | tile bit counts (u32) | tile tails (u32)
     uint32_t* tbits = reinterpret_cast<uint32_t*>(desc + ntiles);
     uint32_t* tails = tbits + ntiles + (ntiles & 1u);
+    uint16_t* psum16 = reinterpret_cast<uint16_t*>(tails + ntiles + (ntiles & 1u));
     dc_mark_phase(0, stream);
     DC_ENC_DISPATCH(encode_count_kernel, dim3(ntiles), dim3(256), 0, stream, x, n, idx0, *P, tbits,
-                    (long long)ntiles, err, tails);
+                    (long long)ntiles, err, tails, psum16);
     dc_mark_phase(1, stream);
     hipLaunchKernelGGL(encode_scan_kernel, dim3(1), dim3(1024), 0, stream, tbits, desc, (long long)ntiles, start_bit,
                        total_bits, total_bits2);
     dc_mark_phase(2, stream);
     DC_ENC_DISPATCH(encode_pack_kernel, dim3(ntiles), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, desc, tails,
-                    ntiles, dbg);
+                    psum16, ntiles, dbg);
     dc_mark_phase(3, stream);
     (void)tile_ctr; (void)epoch;
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -495,7 +518,7 @@ extern "C" int dc_launch_encode_bits(const float* x, long long n, long long idx0
     uint32_t* tbits = reinterpret_cast<uint32_t*>(desc + ntiles);
     const unsigned gc = ntiles;
     DC_ENC_DISPATCH(encode_count_kernel, dim3(gc), dim3(256), 0, stream, x, n, idx0, *P, tbits, (long long)ntiles, err,
-                    nullptr);
+                    nullptr, nullptr);
     hipLaunchKernelGGL(encode_scan_kernel, dim3(1), dim3(1024), 0, stream, tbits, desc, (long long)ntiles, 0, total_bits,
                        nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -503,10 +526,11 @@ extern "C" int dc_launch_encode_bits(const float* x, long long n, long long idx0
 
 extern "C" long long dc_encode_tile_count(long long n) { return (n + ENC_TILE - 1) / ENC_TILE; }
 
-// u64 words of the encode descriptor buffer: tile offsets + 32-bit tile counts + 32-bit tile tails
+// u64 words of the encode descriptor buffer: tile offsets + 32-bit tile counts + 32-bit tile tails +
+// 16-bit per-thread counts of the pack kernel
 extern "C" long long dc_encode_desc_words(long long n) {
     const long long nt = dc_encode_tile_count(n);
-    return nt + (nt + 1) / 2 + (nt + 1) / 2 + 1;                          // offsets, counts, tails
+    return nt + (nt + 1) / 2 + (nt + 1) / 2 + 1 + nt * (ENC_TPB / 4);     // offsets, counts, tails, thread counts
 }
 
 }  // namespace dc
