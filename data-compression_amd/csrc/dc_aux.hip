@@ -106,46 +106,6 @@ __global__ __launch_bounds__(256) void sub_min_kernel(const float* __restrict__ 
 }
 
 // ---------------------------------------------------------------- med_dataset_float
-constexpr int MED_BLK = 8192;
-
-__global__ __launch_bounds__(256) void med_kernel(const float* __restrict__ x, long long n,
-                                                  float* __restrict__ out_mean, int* __restrict__ out_type) {
-    __shared__ float buf[2][MED_BLK];
-    __shared__ float smax[256];
-    float mx = x[0];
-    float total = 0.0f;
-    const long long nblk = (n + MED_BLK - 1) / MED_BLK;
-    // prime buffer 0
-    for (int i = threadIdx.x; i < MED_BLK; i += 256) buf[0][i] = (i < n) ? x[i] : 0.0f;
-    __syncthreads();
-    for (long long b = 0; b < nblk; b++) {
-        const int cur = (int)(b & 1);
-        const long long nb = (b + 1) * MED_BLK;
-        if (b + 1 < nblk)                                 // stage the next block while lane 0 sums
-            for (int i = threadIdx.x; i < MED_BLK; i += 256) buf[cur ^ 1][i] = (nb + i < n) ? x[nb + i] : 0.0f;
-        const long long lim = (n - b * MED_BLK) < MED_BLK ? (n - b * MED_BLK) : MED_BLK;
-        for (int i = threadIdx.x; i < lim; i += 256) { const float v = buf[cur][i]; if (v > mx) mx = v; }
-        if (threadIdx.x == 0) {
-            const float* p = buf[cur];
-            for (int i = 0; i < (int)lim; i++) total = __fadd_rn(total, p[i]);
-        }
-        __syncthreads();
-    }
-    smax[threadIdx.x] = mx;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        float m = smax[0];
-        for (int i = 1; i < 256; i++) if (smax[i] > m) m = smax[i];
-        int type = 0, add = 0;                             // :3605-3614
-        for (int i = 7; i > 0; i--) {
-            add += 1 << i;
-            if ((double)m < ldexp(1.0, add - 127)) { type = 8 - i; break; }
-        }
-        *out_type = type;
-        *out_mean = __fdiv_rn(total, (float)n);
-    }
-}
-
 // ---------------------------------------------------------------- exact parallel mean
 // med_dataset_float (:3593-3620) sums left to right in float.  While the running sum s stays in one
 // binade [2^(E-127), 2^(E-126)) its ulp u = 2^(E-150) is fixed and fl(s + x) = s + u*r(x), with r =

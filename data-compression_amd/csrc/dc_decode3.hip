@@ -341,23 +341,21 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
     P3_FLUSH();
 }
 
-// the 9-bit token prefix at stream bit `pos` (bytes past the stream read as 0)
-__device__ __forceinline__ uint32_t peek9(const uint8_t* __restrict__ s, long long nbytes, long long pos) {
-    const long long i = pos >> 3;
-    const uint32_t b0 = i < nbytes ? s[i] : 0u, b1 = i + 1 < nbytes ? s[i + 1] : 0u;
-    return (((b0 << 8) | b1) >> (7 - (int)(pos & 7))) & 511u;
-}
-
 // the link into parse job t: its first segment's entry must be job t-1's exit.  A broken link (the
 // pre-walk had not synchronised; rare) is re-walked here, serially, until the path meets the recorded
-// entries again; the changed token counts move the job's total and its decode jobs' offsets.
+// entries again; the changed token counts move the job's total and its decode jobs' offsets.  Each
+// chunk's 8 words (+4 after it) are loaded at once and walked from registers.
+__device__ __forceinline__ uint32_t pick12(const uint32_t (&w)[12], int i) {
+    uint32_t r = w[0];
+#pragma unroll
+    for (int k = 1; k < 12; k++) r = i == k ? w[k] : r;
+    return r;
+}
 template <int CT>
-__device__ void link_fix(const uint8_t* __restrict__ s, const Geo3& G, const Dec3Bufs& D3, const uint8_t* tl, long long t) {
+__device__ void link_fix(__amdgpu_buffer_rsrc_t rs, const Geo3& G, const Dec3Bufs& D3, const uint8_t* tl, long long t,
+                         int X) {
     constexpr int seg = D3_SEG;
     const long long cf = t * 64 * seg;                           // the job's first chunk
-    if (t == 0 || cf >= G.nchunks) return;
-    const int X = (int)(uint32_t)D3.pexit[t - 1];
-    if ((int)(D3.rec[cf] & 31u) == X) return;
     const long long cend = (t + 1) * 64 * seg;
     long long pos = cf * 256 + X;
     for (long long c = cf;; c++) {
@@ -366,10 +364,25 @@ __device__ void link_fix(const uint8_t* __restrict__ s, const Geo3& G, const Dec
             if (c >= cend) { atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK); return; }  // the job's exit moved
             if (pos - 256 * c == (long long)(D3.rec[c] & 31u)) break;           // met the recorded path
         }
-        const long long pe = min(256 * (c + 1), (long long)G.nbits);
+        uint32_t w[12];
+        {
+            const uint4 q0 = load_w4(rs, G.nbytes, 8 * c), q1 = load_w4(rs, G.nbytes, 8 * c + 4),
+                        q2 = load_w4(rs, G.nbytes, 8 * c + 8);
+            w[0] = q0.x; w[1] = q0.y; w[2] = q0.z; w[3] = q0.w; w[4] = q1.x; w[5] = q1.y;
+            w[6] = q1.z; w[7] = q1.w; w[8] = q2.x; w[9] = q2.y; w[10] = q2.z; w[11] = q2.w;
+        }
+        const int pe = (int)min(256ll, (long long)G.nbits - 256 * c);
         const int e = (int)(pos - 256 * c);
+        int p = e;
         uint32_t cnt = 0;
-        while (pos < pe) { pos += tl[peek9(s, G.nbytes, pos)]; cnt++; }
+        while (p < pe) {
+            const int i = p >> 5, sh = p & 31;
+            const uint32_t hi = pick12(w, i), lo = pick12(w, i + 1);
+            const uint32_t tk = sh ? ((hi << sh) | (lo >> (32 - sh))) : hi;
+            p += tl[tk >> 23];
+            cnt++;
+        }
+        pos = 256 * c + p;
         const uint32_t old = D3.rec[c];
         D3.rec[c] = (uint16_t)((uint32_t)(e & 31) | (cnt << 8));
         const int d = (int)cnt - (int)(old >> 8);
@@ -394,9 +407,28 @@ __global__ __launch_bounds__(1024) void scan3_kernel(const uint8_t* __restrict__
     const Geo3 G = geo3(dev_nbits, host_nbits);
     if ((__hip_atomic_load(D3.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & D3_DECLINE) != 0) return;
     const long long np = G.npjobs;
+    // the links: every job's first entry against its predecessor's exit, four jobs' loads in flight
+    {
+        const __amdgpu_buffer_rsrc_t rs = stream_rsrc(s, D3.capw);
+        constexpr int U = 4;
+        for (long long tb = 1 + tid; tb < np; tb += 1024 * U) {
+            int X[U];
+            uint32_t R[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const long long t = tb + 1024ll * u;
+                const bool in = t < np && t * 64 * D3_SEG < G.nchunks;
+                X[u] = in ? (int)(uint32_t)D3.pexit[t - 1] : 0;
+                R[u] = in ? (uint32_t)D3.rec[t * 64 * D3_SEG] & 31u : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if ((int)R[u] != X[u]) link_fix<CT>(rs, G, D3, tl, tb + 1024ll * u, X[u]);
+        }
+    }
+    __syncthreads();
     const long long per = (np + 1023) / 1024;
     const long long t0 = tid * per, t1 = min(np, t0 + per);
-    for (long long t = t0; t < t1; t++) link_fix<CT>(s, G, D3, tl, t);
     unsigned long long sum = 0;
     for (long long t = t0; t < t1; t++) sum += D3.ptot[t];
     unsigned long long inc = sum;

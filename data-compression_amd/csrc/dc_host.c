@@ -445,7 +445,7 @@ static int dec_ensure(long long max_chunks) {
     G.dec_pool = NULL;
     long long C = max_chunks + 4096;
     long long GR = (C + dc_decode_group() - 1) / dc_decode_group() + 1;
-    size_t off = 0, sz[21];
+    size_t off = 0, sz[20];
     sz[0] = 256;                          /* plan */
     sz[1] = (size_t)C;                    /* p_exit */
     sz[2] = (size_t)C * 2;                /* p_cnt */
@@ -466,14 +466,13 @@ static int dec_ensure(long long max_chunks) {
     sz[17] = (size_t)GR * 32 * 4;         /* tmap */
     sz[18] = (size_t)GR * 4;              /* tentry */
     sz[19] = (size_t)GR * 8;              /* tbase */
-    sz[20] = (size_t)GR * 8;              /* tflag */
     size_t tot = 0;
-    for (int i = 0; i < 21; i++) tot += (sz[i] + 255) & ~(size_t)255;
+    for (int i = 0; i < 20; i++) tot += (sz[i] + 255) & ~(size_t)255;
     HIPCHK(hipMalloc(&G.dec_pool, tot));
     HIPCHK(hipMemsetAsync(G.dec_pool, 0, tot, G.st));
     char* b = (char*)G.dec_pool;
-    void* ptr[21];
-    for (int i = 0; i < 21; i++) { ptr[i] = b + off; off += (sz[i] + 255) & ~(size_t)255; }
+    void* ptr[20];
+    for (int i = 0; i < 20; i++) { ptr[i] = b + off; off += (sz[i] + 255) & ~(size_t)255; }
     G.D.plan = (Plan*)ptr[0];
     G.D.p_exit = (uint8_t*)ptr[1];
     G.D.p_cnt = (uint16_t*)ptr[2];
@@ -486,7 +485,6 @@ static int dec_ensure(long long max_chunks) {
     G.D.tmap = (uint32_t*)ptr[17];
     G.D.tentry = (uint32_t*)ptr[18];
     G.D.tbase = (unsigned long long*)ptr[19];
-    G.D.tflag = (uint64_t*)ptr[20];
     G.D.fullmap = (uint32_t*)ptr[5];
     G.D.gran = (uint64_t*)ptr[6];
     G.D.entry = (uint8_t*)ptr[7];
@@ -512,7 +510,6 @@ static int dec_next_epoch(void) {
         const long long GR = (G.dec_cap_chunks + dc_decode_group() - 1) / dc_decode_group() + 1;
         HIPCHK(hipMemsetAsync(G.D.gran, 0, (size_t)GR * 34 * 8, G.st));
         HIPCHK(hipMemsetAsync(G.D.hist, 0, (size_t)GR * 6 * 8, G.st));
-        HIPCHK(hipMemsetAsync(G.D.tflag, 0, (size_t)GR * 8, G.st));
         if (G.dec3_pool) {
             HIPCHK(hipMemsetAsync(G.D3.pexit, 0, (size_t)(G.dec3_cap + 4096) / 256 * 8 + 64 * 8, G.st));
             HIPCHK(hipMemsetAsync(G.D3.hist, 0, (size_t)((G.dec3_cap + 4096) / 64 + 64) * 3 * 8, G.st));

@@ -54,7 +54,6 @@ typedef struct DecBufs { /* decoder metadata, sized for the maximum chunk count 
     uint32_t* tmap;      /* [group][4]  tile record: P_0 mask, n_0 | x_0<<16 | tile exit<<24, rest count */
     uint32_t* tentry;    /* [group] true entry of the tile's first chunk | its token count << 8 */
     unsigned long long* tbase;   /* [group] first token index of the tile */
-    uint64_t* tflag;     /* [group] token-count look-back: status<<62 | epoch<<40 | tokens (1 aggregate, 2 inclusive) */
     uint8_t* entry;
     unsigned long long* tokoff;
     uint16_t* pend;
