@@ -125,7 +125,14 @@ def halo_bench(args):
     mi, mj, mk = 257, 257, 8                       # L-size i/j extent; a thin z slab per rank
     imax, jmax, kmax = 256, 256, 7
     ii = torch.arange(mi, dtype=torch.float32, device=dev).view(mi, 1, 1)
-    p = (ii * ii / float((imax - 1) * (imax - 1))).expand(mi, mj, mk).contiguous()     # initmt (it = 0)
+    kk3 = torch.arange(mk, dtype=torch.float32, device=dev).view(1, 1, mk)
+
+    def field(r):
+        # initmt's p = i^2 / (imax-1)^2 (it = 0), offset per rank and plane so that a swapped direction
+        # or a wrong plane in the exchange cannot pass the check below
+        return (ii * ii / float((imax - 1) * (imax - 1)) + 0.25 * r + 0.01 * kk3).expand(mi, mj, mk).contiguous()
+
+    p = field(rank)
     q = torch.zeros_like(p)
     n = imax * jmax
     cap = L.stream_capacity(n)
@@ -183,19 +190,26 @@ def halo_bench(args):
     wall = time.perf_counter() - t0
     xcheck = None
     if dist is not None:
-        # every rank holds the same field p, so the plane received from up is this rank's own plane k = 1
-        # (h = 0) and the one from down its plane k = kmax - 2 (h = 1): same bits, min and stream bytes,
-        # and the halo decoded from the received stream equals the one decoded from the local stream
+        # the plane received from up must be up's plane k = 1 and the one from down down's plane
+        # k = kmax - 2 (each rank's field differs): encoded here from the neighbour's field, the same
+        # bits, min and stream bytes, and the received halo decodes to the same plane
         got, nb, mn = last[0]
         q2 = torch.zeros_like(q)
         xcheck = True
-        for rec, kk, h in zip(got, (kmax - 1, 0), (0, 1)):
+        for rec, kk, src, h in zip(got, (kmax - 1, 0), (up, down), (0, 1)):
             if rec is None:
                 continue
             rs, rb, rmn = rec
+            pn = field(src)
+            sn = torch.zeros(cap, dtype=torch.uint8, device=dev)
+            bn = torch.zeros(1, dtype=torch.int64, device=dev)
+            mnn = torch.zeros(1, dtype=torch.float32, device=dev)
+            L.halo_encode_device(ct, pn.data_ptr(), (mi, mj, mk), 3, planes[h], (imax, jmax, kmax), sn.data_ptr(),
+                                 bn.data_ptr(), mnn.data_ptr())
+            L.synchronize()
             k = (rb + 7) // 8
-            xcheck &= rb == nb[h] and rmn == mn[h] and bool(torch.equal(rs[:k].cpu(), st[h][:k].cpu()))
-            L.halo_decode_device(ct, st[h].data_ptr(), -1, bits.data_ptr() + 8 * h, 0, 0, mins.data_ptr() + 4 * h,
+            xcheck &= rb == int(bn.item()) and rmn == float(mnn.item()) and bool(torch.equal(rs[:k].cpu(), sn[:k].cpu()))
+            L.halo_decode_device(ct, sn.data_ptr(), -1, bn.data_ptr(), 0, 0, mnn.data_ptr(),
                                  q2.data_ptr(), (mi, mj, mk), 3, kk, (imax, jmax, kmax))
             L.synchronize()
             xcheck &= bool(torch.equal(q[:imax, :jmax, kk], q2[:imax, :jmax, kk]))

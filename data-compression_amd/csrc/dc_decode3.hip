@@ -402,11 +402,18 @@ __global__ __launch_bounds__(1024) void scan3_kernel(const uint8_t* __restrict__
     __shared__ unsigned long long wtot[16];
     __shared__ uint8_t tl[512];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+#ifdef DC_DEC3_PROF
+    const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     build_lut_len<CT>(tl, P, tid, 1024);
     __syncthreads();
     const Geo3 G = geo3(dev_nbits, host_nbits);
     if ((__hip_atomic_load(D3.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & D3_DECLINE) != 0) return;
     const long long np = G.npjobs;
+#ifdef DC_DEC3_PROF
+    const long long s0 = clock64();
+    unsigned nfix = 0;
+#endif
     // the links: every job's first entry against its predecessor's exit, four jobs' loads in flight
     {
         const __amdgpu_buffer_rsrc_t rs = stream_rsrc(s, D3.capw);
@@ -423,9 +430,18 @@ __global__ __launch_bounds__(1024) void scan3_kernel(const uint8_t* __restrict__
             }
 #pragma unroll
             for (int u = 0; u < U; u++)
-                if ((int)R[u] != X[u]) link_fix<CT>(rs, G, D3, tl, tb + 1024ll * u, X[u]);
+                if ((int)R[u] != X[u]) {
+                    link_fix<CT>(rs, G, D3, tl, tb + 1024ll * u, X[u]);
+#ifdef DC_DEC3_PROF
+                    nfix++;
+#endif
+                }
         }
     }
+#ifdef DC_DEC3_PROF
+    atomicMax(&g_prof3[16], (unsigned long long)(clock64() - s0));
+    if (nfix) atomicAdd(&g_prof3[17], (unsigned long long)nfix);
+#endif
     __syncthreads();
     const long long per = (np + 1023) / 1024;
     const long long t0 = tid * per, t1 = min(np, t0 + per);
@@ -447,6 +463,10 @@ __global__ __launch_bounds__(1024) void scan3_kernel(const uint8_t* __restrict__
     if (tid == 0) {
         D3.pbase[np] = all;
         if ((long long)all < num) atomicOr(D3.err, D3_DECLINE | D3_WHY_SHORT);
+#ifdef DC_DEC3_PROF
+        atomicAdd(&g_prof3[18], (unsigned long long)(clock64() - s0));
+        atomicAdd(&g_prof3[19], __builtin_amdgcn_s_memrealtime() - rt0);
+#endif
     }
 }
 

@@ -519,7 +519,12 @@ def halo_exchange(streams, nbits, mins, down, up, group=None):
     the reference, the sizes travel first (one int64 pair per direction: bits and the min's bit pattern),
     then exactly the stream bytes.  Returns [(stream, nbits, min) received from up (for k = kmax - 1),
     the same from down (for k = 0)], None where there is no neighbour.  P2P over RCCL with device
-    tensors, or over gloo with host copies."""
+    tensors, or over gloo with host copies.
+
+    The received buffers are complete on torch's current stream; before returning, the library's own
+    HIP stream (where halo_decode_device runs) is made to wait for them, so the caller can decode at
+    once.  (The sends read streams[] on torch's stream: the caller must have finished the encodes --
+    L.synchronize() -- before calling, as the sizes are read on the host anyway.)"""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -565,6 +570,10 @@ def halo_exchange(streams, nbits, mins, down, up, group=None):
         b, m = int(rmeta[i][0]), int(rmeta[i][1])
         mn = float(np.array([m], np.int32).view(np.float32)[0])
         out.append((rbuf[i].to(dev) if host else rbuf[i], b, mn))
+    if dev.type == "cuda":                      # the library stream waits for the received bytes
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        torch.cuda.ExternalStream(lib().L.dc_get_stream(), device=dev).wait_event(ev)
     return out
 
 

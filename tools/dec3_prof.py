@@ -64,6 +64,8 @@ def main():
     print(f"  per job (kcycles): claim {p[8] / dj / 1e3:.2f} stage {p[9] / dj / 1e3:.2f} walk {p[10] / dj / 1e3:.2f} "
           f"pend {p[11] / dj / 1e3:.2f} store {p[12] / dj / 1e3:.2f}")
     print(f"  walk cycles per token step: {p[10] / max(p[15] / 64, 1):.1f}")
+    print(f"scan3: link phase max {p[16] / 1e3:.1f} kcycles (per call, summed over {reps}: max of max), fixes {p[17]:.1f}, "
+          f"whole kernel (thread 0) {p[18] / 1e3:.1f} kcycles, realtime {p[19] * 0.01:.2f} us")
     spec = np.array([v for v in out[:8].cpu().numpy()])
     print("first values", spec)
 
