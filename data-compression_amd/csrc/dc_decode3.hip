@@ -12,8 +12,8 @@
 //                ds_read_b32 of a wave hits 32 distinct banks whatever the lanes' offsets.  At every
 //                chunk boundary the lane records the chunk's entry offset and token count (16 bits).
 //                Links are checked afterwards: a segment's first entry must equal the previous
-//                segment's exit (in-wave shuffle; across jobs the previous job's published exit, which
-//                never waits on anything -- no chain).  A broken link (the pre-walk had not
+//                segment's exit (in-wave shuffle; across jobs the previous job's published exit when it
+//                is there -- never waited for, no chain -- else later, in scan3_kernel).  A broken link (the pre-walk had not
 //                synchronised, ~0.3% of segments) is repaired by re-walking from the true entry until
 //                the path meets the recorded entries again.  The wave's token counts are scanned into
 //                job-relative first-token offsets of every decode job.
@@ -230,7 +230,7 @@ __device__ __forceinline__ void run_lines(Ring3& r, __amdgpu_buffer_rsrc_t rs, l
 template <int CT>
 __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ s, Params P, Dec3Bufs D3,
                                                     const unsigned long long* dev_nbits, unsigned long long host_nbits,
-                                                    long long num) {
+                                                    long long num, uint32_t epoch) {
     constexpr int seg = D3_SEG;
     __shared__ uint32_t ring[(D3_RING + 4) * 64];
     __shared__ uint16_t recs[seg * 64];                          // [chunk][lane]: the wave's records
@@ -272,8 +272,7 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
                       }
                   });
         const int X = r.pos - 256 * seg;                                 // entry of the next segment
-        // (the link into the next job is checked by scan3_kernel against this exit)
-        if (lane == 63) D3.pexit[job] = (uint64_t)(uint32_t)X;
+        if (lane == 63) st_relaxed(&D3.pexit[job], ((uint64_t)epoch << 32) | (uint32_t)X);
         P3_T(t1);
         P3_ADD(0, t1 - t0);
         P3_ADD(4, act ? tot : 0u);
@@ -282,8 +281,24 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
         // entry is not re-walks from that exit, rewriting its records until the path meets a recorded
         // entry again; a path that reaches the segment end without meeting it moves the exit, and the
         // successor is checked again (rounds; a moved exit of the last segment declines)
+        // (the link into the job: checked here if the previous job has published its exit -- jobs run
+        // side by side, so it usually has -- never waited for; scan3_kernel checks the others)
         int xin = __shfl_up(X, 1, 64), ecur = e0, Xcur = X, rounds = 0;
-        bool bad = act && lane > 0 && ecur != xin;
+        bool link0 = false;
+        if (lane == 0 && act && sidx > 0) {
+            const uint64_t v = ld_relaxed(&D3.pexit[job - 1]);
+            if ((v >> 32) == (uint64_t)epoch) { xin = (int)(uint32_t)v; link0 = true; }
+        }
+        bool bad = act && (lane > 0 || link0) && ecur != xin;
+        for (int pass = 0; pass < 2; pass++) {
+        if (pass == 1) {                            // a second look at the job's first link (now often there)
+            bool chk = false;
+            if (lane == 0 && act && sidx > 0 && !link0) {
+                const uint64_t v = ld_relaxed(&D3.pexit[job - 1]);
+                if ((v >> 32) == (uint64_t)epoch) { xin = (int)(uint32_t)v; link0 = true; chk = true; }
+            }
+            bad = chk && ecur != xin;
+        }
         while (__any(bad)) {
             if (++rounds > 64) { if (lane == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK); break; }
             bool live = bad;
@@ -314,11 +329,13 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
             bad = lane >= 1 && act && mp && ecur != xp;
             xin = bad ? xp : xin;
         }
+        }
         P3_T(t2);
         P3_ADD(2, t2 - t1);
         P3_ADD(3, rounds);
         P3_ADD(5, 1);
 
+        if (lane == 0) D3.lver[job] = link0 ? 1u : 0u;
         // ---- the segment's records: 32 bytes per lane, one contiguous 2 KB block per wave
         if (act) {
             uint32_t w[seg / 2];
@@ -424,7 +441,7 @@ __global__ __launch_bounds__(1024) void scan3_kernel(const uint8_t* __restrict__
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 const long long t = tb + 1024ll * u;
-                const bool in = t < np && t * 64 * D3_SEG < G.nchunks;
+                const bool in = t < np && t * 64 * D3_SEG < G.nchunks && D3.lver[t] == 0u;
                 X[u] = in ? (int)(uint32_t)D3.pexit[t - 1] : 0;
                 R[u] = in ? (uint32_t)D3.rec[t * 64 * D3_SEG] & 31u : 0u;
             }
@@ -805,12 +822,12 @@ static void dbg_dump(const Dec3Bufs* D3) {
     if (!on) return;
     hipStream_t s2;
     if (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) != hipSuccess) return;
-    unsigned ctr[4] = {0}, err = 0;
+    unsigned lv[4] = {0}, err = 0;
     uint64_t hist[12] = {0};
     unsigned long long pb[4] = {0};
     uint32_t rel[4] = {0}, pt[4] = {0};
     uint16_t rec[16] = {0};
-    (void)hipMemcpyAsync(ctr, D3->ctr, sizeof ctr, hipMemcpyDeviceToHost, s2);
+    (void)hipMemcpyAsync(lv, D3->lver, sizeof lv, hipMemcpyDeviceToHost, s2);
     (void)hipMemcpyAsync(&err, D3->err, 4, hipMemcpyDeviceToHost, s2);
     (void)hipMemcpyAsync(hist, D3->hist, sizeof hist, hipMemcpyDeviceToHost, s2);
     (void)hipMemcpyAsync(pb, D3->pbase, sizeof pb, hipMemcpyDeviceToHost, s2);
@@ -818,7 +835,7 @@ static void dbg_dump(const Dec3Bufs* D3) {
     (void)hipMemcpyAsync(pt, D3->ptot, sizeof pt, hipMemcpyDeviceToHost, s2);
     (void)hipMemcpyAsync(rec, D3->rec, sizeof rec, hipMemcpyDeviceToHost, s2);
     (void)hipStreamSynchronize(s2);
-    fprintf(stderr, "[dcamd] ctr %u %u %u %u err 0x%x seg %d\n", ctr[0], ctr[1], ctr[2], ctr[3], err, D3->seg);
+    fprintf(stderr, "[dcamd] lver %u %u %u %u err 0x%x seg %d\n", lv[0], lv[1], lv[2], lv[3], err, D3->seg);
     for (int i = 0; i < 4; i++)
         fprintf(stderr, "  job %d hist %llx %llx %llx pbase %llu rel %u ptot %u\n", i, (unsigned long long)hist[3 * i],
                 (unsigned long long)hist[3 * i + 1], (unsigned long long)hist[3 * i + 2], pb[i], rel[i], pt[i]);
@@ -846,7 +863,7 @@ extern "C" int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev
     const int g1 = (int)std::max<long long>(1, std::min<long long>(maxpj, gp[ci]));
     const int g3 = (int)std::max<long long>(1, std::min<long long>((maxdj + 3) / 4, gd[ci]));
     dc_mark_phase(4, st);
-    DC_DISPATCH_3(P->ct, parse3_kernel, dim3(g1), dim3(64), 0, st, s, *P, *D3, dev_nbits, host_nbits, num);
+    DC_DISPATCH_3(P->ct, parse3_kernel, dim3(g1), dim3(64), 0, st, s, *P, *D3, dev_nbits, host_nbits, num, epoch);
     dbg_wait("parse3_kernel", st);
     dc_mark_phase(5, st);
     DC_DISPATCH_3(P->ct, scan3_kernel, dim3(1), dim3(1024), 0, st, s, *P, *D3, dev_nbits, host_nbits, num);

@@ -535,7 +535,7 @@ static int dec3_ensure(long long max_chunks) {
         sz[3] = (size_t)(PJ + 1) * 8;         /* pbase */
         sz[4] = (size_t)PJ * 8;               /* pexit */
         sz[5] = (size_t)DJ * 3 * 8;           /* hist */
-        sz[6] = 64;                           /* ctr */
+        sz[6] = (size_t)PJ * 4;               /* lver */
         for (int i = 0; i < 7; i++) tot += (sz[i] + 255) & ~(size_t)255;
         HIPCHK(hipMalloc(&G.dec3_pool, tot));
         HIPCHK(hipMemsetAsync(G.dec3_pool, 0, tot, G.st));
@@ -548,7 +548,7 @@ static int dec3_ensure(long long max_chunks) {
         G.D3.pbase = (unsigned long long*)ptr[3];
         G.D3.pexit = (uint64_t*)ptr[4];
         G.D3.hist = (uint64_t*)ptr[5];
-        G.D3.ctr = (unsigned*)ptr[6];
+        G.D3.lver = (uint32_t*)ptr[6];
         G.dec3_cap = max_chunks;
     }
     G.D3.max_chunks = G.dec3_cap;

@@ -75,7 +75,7 @@ typedef struct Dec3Bufs {
     unsigned long long* pbase;     /* [parse job + 1] first token of the parse job (exclusive scan) */
     uint64_t* pexit;               /* [parse job] epoch << 32 | its last lane's exit (main walk) */
     uint64_t* hist;                /* [decode job][3] the job's last three values, epoch-tagged granules */
-    unsigned* ctr;                 /* [0] parse ticket, [1] decode ticket, [2] parse done, [3] decode done */
+    uint32_t* lver;                /* [parse job] 1: its first segment's link was checked (and repaired) in parse */
     unsigned* err;                 /* the DecBufs status word; 512 = this path declined the stream */
     int seg;                       /* chunks per parse segment: 16 or 32 */
     long long max_chunks;          /* capacity of rec */
