@@ -417,6 +417,7 @@ __global__ __launch_bounds__(1024) void scan3_kernel(const uint8_t* __restrict__
                                                      const unsigned long long* dev_nbits,
                                                      unsigned long long host_nbits, long long num) {
     __shared__ unsigned long long wtot[16];
+    __shared__ uint32_t stot[8 * 1024];
     __shared__ uint8_t tl[512];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
 #ifdef DC_DEC3_PROF
@@ -460,23 +461,45 @@ __global__ __launch_bounds__(1024) void scan3_kernel(const uint8_t* __restrict__
     if (nfix) atomicAdd(&g_prof3[17], (unsigned long long)nfix);
 #endif
     __syncthreads();
-    const long long per = (np + 1023) / 1024;
-    const long long t0 = tid * per, t1 = min(np, t0 + per);
-    unsigned long long sum = 0;
-    for (long long t = t0; t < t1; t++) sum += D3.ptot[t];
-    unsigned long long inc = sum;
+    // exclusive scan of the job totals in chunks of 8192: all of a chunk's loads at once (coalesced),
+    // through LDS to 8 consecutive totals per thread
+    unsigned long long carry = 0;
+    for (long long c0 = 0; c0 < np; c0 += 8 * 1024) {
+        uint32_t v[8];
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const unsigned long long u = __shfl_up(inc, d, 64);
-        if (lane >= d) inc += u;
+        for (int k = 0; k < 8; k++) {
+            const long long t = c0 + k * 1024 + tid;
+            v[k] = t < np ? D3.ptot[t] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) stot[k * 1024 + tid] = v[k];
+        __syncthreads();
+        uint32_t c[8];
+        unsigned long long sum = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) { c[i] = stot[tid * 8 + i]; sum += c[i]; }
+        unsigned long long inc = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const unsigned long long u = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += u;
+        }
+        if (lane == 63) wtot[wid] = inc;
+        __syncthreads();
+        unsigned long long wpre = 0, all = 0;
+#pragma unroll
+        for (int w = 0; w < 16; w++) { wpre += w < wid ? wtot[w] : 0ull; all += wtot[w]; }
+        unsigned long long run = carry + wpre + inc - sum;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const long long t = c0 + tid * 8 + i;
+            if (t < np) D3.pbase[t] = run;
+            run += c[i];
+        }
+        carry += all;
+        __syncthreads();                                             // stot / wtot are rewritten
     }
-    if (lane == 63) wtot[wid] = inc;
-    __syncthreads();
-    unsigned long long wpre = 0, all = 0;
-#pragma unroll
-    for (int w = 0; w < 16; w++) { wpre += w < wid ? wtot[w] : 0ull; all += wtot[w]; }
-    unsigned long long run = wpre + inc - sum;
-    for (long long t = t0; t < t1; t++) { D3.pbase[t] = run; run += D3.ptot[t]; }
+    const unsigned long long all = carry;
     if (tid == 0) {
         D3.pbase[np] = all;
         if ((long long)all < num) atomicOr(D3.err, D3_DECLINE | D3_WHY_SHORT);
