@@ -539,16 +539,14 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
             L.decode_finish()
         resends[0] = 0
 
-    # ---- timed region: barrier + sync on both sides, max over ranks.  Per-kernel HIP events are
-    # recorded by the library on its own stream (dc_timing_enable), one event set per step.
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
-    L.L.dc_timing_enable(steps)
+    # ---- timed region: barrier + sync on both sides, max over ranks, nothing but the steps (an event
+    # record between launches costs a few microseconds of dispatch gap)
     C.barrier()
     torch.cuda.synchronize()
     L.synchronize()
     t0 = time.perf_counter()
     for k in range(steps):
-        step(evs[k])
+        step()
     L.synchronize()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -560,6 +558,23 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
         if status == 0:
             raise
     wall = C.max_over_ranks(t1 - t0)
+    # ---- the same steps again with per-kernel HIP events, recorded by the library on its own stream
+    # (dc_timing_enable, one event set per step): the kernel table and the roofline's launch duration
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    L.L.dc_timing_enable(steps)
+    torch.cuda.synchronize()
+    L.synchronize()
+    for k in range(steps):
+        step(evs[k])
+    L.synchronize()
+    torch.cuda.synchronize()
+    st2 = L.decode_status()
+    try:
+        L.decode_finish()
+    except C.dcamd.DCError:
+        if st2 == 0:
+            raise
+    status |= st2
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     kms = np.zeros((steps, 6), np.float32)
