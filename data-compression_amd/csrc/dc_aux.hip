@@ -849,9 +849,11 @@ extern "C" int dc_timing_read(int set, float* ms) {
     if (!g_events || set < 0 || set >= g_nsets) return -1;
     hipEvent_t* e = g_events + set * 8;
     const int a[6] = {0, 1, 2, 4, 5, 6};
+    // (an event a step did not record -- a decode finished on a slow path marks the next set -- fails
+    // here: the error is cleared so that it cannot surface at the caller's next HIP call)
     for (int i = 0; i < 6; i++) {
-        if (hipEventSynchronize(e[a[i] + 1]) != hipSuccess) return -1;
-        if (hipEventElapsedTime(&ms[i], e[a[i]], e[a[i] + 1]) != hipSuccess) ms[i] = -1.0f;
+        if (hipEventSynchronize(e[a[i] + 1]) != hipSuccess) { (void)hipGetLastError(); return -1; }
+        if (hipEventElapsedTime(&ms[i], e[a[i]], e[a[i] + 1]) != hipSuccess) { ms[i] = -1.0f; (void)hipGetLastError(); }
     }
     return 0;
 }
