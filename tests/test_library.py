@@ -25,3 +25,16 @@ def test_library_exports_header_symbols():
             if name in ("if", "while", "for", "sizeof", "return"):
                 continue
             assert hasattr(L.L, name), f"{h}: {name} not exported"
+
+
+def test_host_asan():
+    """The host C of the library under AddressSanitizer + UBSan: `make asan` builds
+    tests/native/host_asan_check.c against ASan-instrumented dc_host*.c and runs it (no GPU call)."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None or not os.path.exists("/opt/rocm/lib/libamdhip64.so"):
+        pytest.skip("gcc / the HIP runtime library not available")
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "data-compression_amd")
+    r = subprocess.run(["make", "-s", "-C", d, "asan"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "host_asan_check: ok" in r.stdout
