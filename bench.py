@@ -655,6 +655,25 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
     return res
 
 
+def copy_bandwidth(dev, n, reps=10):
+    """Achievable HBM rate on this GPU: a device-to-device copy of n floats (torch copy_, one kernel),
+    read + written bytes over its HIP-event time (the practical ceiling a streaming kernel meets)."""
+    import torch
+    a = torch.ones(n, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    for _ in range(3):
+        b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    return 8.0 * n / (ms * 1e-3) / 1e9
+
+
 def kernel_table(ct, n, nbytes, kavg, v3=True):
     """The six timed launches of a step (library timing slots, HIP events on the library stream) and their
     algorithmic bytes: the encoder's count / scan / pack launches, then the decoder's three -- the segment
@@ -736,6 +755,7 @@ def main():
         sys.exit(1)
     kernels = kernel_table(ct, n, nbytes, R["kavg"], R["v3"])
     dname = main_line["dominant"]["kernel"]
+    achievable = copy_bandwidth(C.dev, n)
     traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if os.path.exists(pmc):
@@ -771,7 +791,10 @@ def main():
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": main_line["dominant"]["frac"],
                      "traffic": traffic, "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": int(kernels[dname][1]),
-                     "avg_launch_ms": main_line["dominant"]["avg_launch_ms"]},
+                     "avg_launch_ms": main_line["dominant"]["avg_launch_ms"],
+                     "achievable": round(achievable, 1),
+                     "achievable_source": f"device copy of 2^{args.log2n} floats (torch copy_), read + written bytes",
+                     "frac_of_achievable": round(main_line["dominant"]["achieved_GBs"] / achievable, 4)},
         "kernels_ms": main_line["kernels_ms"],
         "phases_ms": {"encode": round(R["enc_ms"], 4), "decode": round(R["dec_ms"], 4),
                       "med_dataset_s": round(W["t_med"], 4)},
