@@ -583,48 +583,73 @@ __global__ __launch_bounds__(256) void crc_blocks_kernel(const uint8_t* __restri
     }
 }
 
-__global__ __launch_bounds__(256) void crc_final_kernel(const uint32_t* __restrict__ part, long long nbytes,
-                                                        const uint32_t* __restrict__ x2n_g, uint32_t init,
+// Constants of the final combine, computed on the host from nbytes (Kb = x^(8 CRC_BLK); the full blocks
+// are padded at the front to 256 threads x `per` blocks -- leading zero blocks add nothing)
+struct CrcFin {
+    uint32_t kb, lvl[8], kl, xn;   // lvl[l] = x^(8 CRC_BLK per 2^l), kl = x^(8 * last block), xn = x^(8 nbytes)
+    long long nblk, per, pad;
+};
+
+// part[] = raw CRC of every block; the stream's zlib CRC: thread t folds its `per` consecutive blocks by
+// Horner (r = r Kb ^ part), an 8-level tree joins neighbours with one constant each, and the last
+// (partial) block and the zlib init / final xor are applied by thread 0 -- about 40 carry-less
+// multiplies on the critical path (the generic x^(8n) per tree node took 80-100 us)
+__global__ __launch_bounds__(256) void crc_final_kernel(const uint32_t* __restrict__ part, CrcFin F, uint32_t init,
                                                         uint32_t* __restrict__ out) {
-    __shared__ uint32_t x2n[32];
     __shared__ uint32_t red[256];
-    __shared__ long long rl[256];
-    if (threadIdx.x < 32) x2n[threadIdx.x] = x2n_g[threadIdx.x];
-    __syncthreads();
-    const long long nblk = (nbytes + CRC_BLK - 1) / CRC_BLK;
-    const long long per = (nblk + 255) / 256;
-    const long long b0 = threadIdx.x * per;
-    const uint32_t cfull = xpow8n((unsigned long long)CRC_BLK, x2n);
+    const int t = threadIdx.x;
     uint32_t r = 0;
-    long long len = 0;
-    for (long long b = b0; b < b0 + per && b < nblk; b++) {
-        long long bl = nbytes - b * CRC_BLK;
-        if (bl >= CRC_BLK) r = multmodp(cfull, r) ^ part[b];
-        else r = multmodp(xpow8n((unsigned long long)bl, x2n), r) ^ part[b];
-        len += bl < CRC_BLK ? bl : CRC_BLK;
+    const long long m = F.nblk > 0 ? F.nblk - 1 : 0;                 // full blocks
+    for (long long i = 0; i < F.per; i++) {
+        const long long b = (long long)t * F.per + i - F.pad;
+        r = multmodp(F.kb, r) ^ (b >= 0 && b < m ? part[b] : 0u);
     }
-    red[threadIdx.x] = r;
-    rl[threadIdx.x] = len;
+    red[t] = r;
     __syncthreads();
-    for (int w = 1; w < 256; w <<= 1) {                   // tree: left shifted by right's length
-        const int t = threadIdx.x;
-        const bool act = (t % (2 * w)) == 0;
+#pragma unroll
+    for (int l = 0; l < 8; l++) {
+        const int w = 1 << l;
         uint32_t v = 0;
-        long long l = 0;
-        if (act) {
-            const long long rlen = rl[t + w];
-            v = (rlen ? multmodp(xpow8n((unsigned long long)rlen, x2n), red[t]) : red[t]) ^ red[t + w];
-            l = rl[t] + rlen;
-        }
+        const bool act = (t & (2 * w - 1)) == 0;
+        if (act) v = multmodp(F.lvl[l], red[t]) ^ red[t + w];
         __syncthreads();
-        if (act) { red[t] = v; rl[t] = l; }
+        if (act) red[t] = v;
         __syncthreads();
     }
-    if (threadIdx.x == 0) {
+    if (t == 0) {
+        uint32_t R = red[0];
+        if (F.nblk > 0) R = multmodp(F.kl, R) ^ part[F.nblk - 1];
         // zlib: crc32(init, buf) = ~(raw(buf) ^ shift(~init, n))
-        const uint32_t v = red[0] ^ multmodp(xpow8n((unsigned long long)nbytes, x2n), ~init);
-        *out = ~v;
+        *out = ~(R ^ multmodp(F.xn, ~init));
     }
+}
+
+static uint32_t h_mult(uint32_t a, uint32_t b) {
+    uint32_t m = 1u << 31, p = 0;
+    for (int i = 0; i < 32; i++) {
+        if (a & m) p ^= b;
+        m >>= 1;
+        b = (b & 1u) ? (b >> 1) ^ CRC_POLY : b >> 1;
+    }
+    return p;
+}
+static uint32_t h_xpow8n(unsigned long long n) {                      // x^(8n) mod P
+    static uint32_t x2n[64];
+    static bool init = false;
+    if (!init) {
+        uint32_t p = 1u << 30;                                          // x^1
+        x2n[0] = p;
+        for (int k = 1; k < 64; k++) x2n[k] = p = h_mult(p, p);
+        init = true;
+    }
+    uint32_t p = 1u << 31;
+    int k = 3;
+    while (n) {
+        if (n & 1) p = h_mult(x2n[k & 63], p);
+        n >>= 1;
+        k++;
+    }
+    return p;
 }
 
 // ---------------------------------------------------------------- Hamming SECDED
@@ -703,7 +728,18 @@ extern "C" int dc_launch_crc32(const uint8_t* s, long long nbytes, const uint32_
         hipLaunchKernelGGL(crc_blocks_kernel, dim3((unsigned)g), dim3(256), 0, st, s, nbytes, d_tab, d_tab + 1024,
                            d_x2n, d_parts);
     }
-    hipLaunchKernelGGL(crc_final_kernel, dim3(1), dim3(256), 0, st, d_parts, nbytes, d_x2n, init, d_out);
+    CrcFin F;
+    F.nblk = nbytes > 0 ? nblk : 0;
+    const long long m = F.nblk > 0 ? F.nblk - 1 : 0;
+    F.per = m > 0 ? (m + 255) / 256 : 0;
+    F.pad = 256 * F.per - m;
+    F.kb = h_xpow8n((unsigned long long)CRC_BLK);
+    uint32_t kp = h_xpow8n((unsigned long long)CRC_BLK * (unsigned long long)F.per);
+    for (int l = 0; l < 8; l++) { F.lvl[l] = kp; kp = h_mult(kp, kp); }
+    F.kl = h_xpow8n((unsigned long long)(nbytes - m * CRC_BLK));
+    F.xn = h_xpow8n((unsigned long long)nbytes);
+    (void)d_x2n;
+    hipLaunchKernelGGL(crc_final_kernel, dim3(1), dim3(256), 0, st, d_parts, F, init, d_out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
