@@ -578,16 +578,16 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
     status |= st2
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
-    kms = np.zeros((steps, 6), np.float32)
+    kms = np.zeros((steps, 11), np.float32)
     for k in range(steps):
-        buf = (ctypes.c_float * 6)()
-        if L.L.dc_timing_read(k, buf) == 0:
+        buf = (ctypes.c_float * 11)()
+        if L.L.dc_timing_read_all(k, buf) == 0:
             kms[k] = np.frombuffer(buf, np.float32)
     L.L.dc_timing_enable(0)
     kavg = kms.mean(axis=0)
     res = {"nbits": int(nbits), "nbytes": int(nbytes), "wall": wall, "enc_ms": enc_ms, "dec_ms": dec_ms,
            "kavg": kavg, "status": int(status | warm_status), "warm_status": int(warm_status), "resends": timed_resends,
-           "slow_path_timed": slow[0], "v3": bool(L.last_decode_was_v3())}
+           "slow_path_timed": slow[0], "v3": bool(L.L.dc_last_decode_launched_v3())}
 
     if pipelined and ber <= 0:
         # the same K steps pipelined (encode k+1 || decode k, two stream buffers), reported beside value
@@ -676,22 +676,35 @@ def copy_bandwidth(dev, n, reps=10):
 
 
 def kernel_table(ct, n, nbytes, kavg, v3=True):
-    """The six timed launches of a step (library timing slots, HIP events on the library stream) and their
-    algorithmic bytes: the encoder's count / scan / pack launches, then the decoder's three -- the segment
-    decoder (parse3, link fixes + scan3, decode3) or, for streams it hands over, the chunk-map decoder."""
+    """The timed launches of a step (library timing slots, HIP events on the library stream) and their
+    algorithmic bytes: the encoder's count, scan and pack launches, then the decoder's -- the segment decoder (parse3, whose jobs check the
+    link into them, and decode3, which sums the parse jobs' totals itself: no scan launch) or the
+    chunk-map decoder (parse, tile fix + scan, decode) -- and, when the first decoder handed the stream
+    over inside the step (dc_decode_finish), the chunk-map decoder's launches and the runs-mode resolve
+    and resolved decode.  The decode bytes go to the launch whose values were kept."""
+    k = [float(v) for v in kavg]
+    fin = any(v > 0 for v in k[6:11])
+    res = k[9] > 0
+    dec_b = nbytes + 4.0 * n
     kernels = {   # name: (avg ms, algorithmic bytes per launch)
-        f"encode_count_kernel<{ct}>": (float(kavg[0]), 4.0 * n),
-        "encode_scan_kernel": (float(kavg[1]), 0.0),
-        f"encode_pack_kernel<{ct}>": (float(kavg[2]), 4.0 * n + nbytes),
+        f"encode_count_kernel<{ct}>": (k[0], 4.0 * n),
+        "encode_scan_kernel": (k[1], 0.0),
+        f"encode_pack_kernel<{ct}>": (k[2], 4.0 * n + nbytes),
     }
     if v3:
-        kernels.update({f"parse3_kernel<{ct}>": (float(kavg[3]), float(nbytes)),
-                        f"scan3_kernel<{ct}>": (float(kavg[4]), 0.0),
-                        f"decode3_kernel<{ct}>": (float(kavg[5]), nbytes + 4.0 * n)})
+        kernels.update({f"parse3_kernel<{ct}>": (k[3], 0.0 if fin else float(nbytes)),
+                        f"decode3_kernel<{ct}>": (k[5], 0.0 if fin else dec_b)})
     else:
-        kernels.update({f"parse_kernel<{ct}>": (float(kavg[3]), float(nbytes)),
-                        "tile_fix_kernel+tile_scan_kernel": (float(kavg[4]), 0.0),
-                        f"decode_kernel_fast<{ct}>": (float(kavg[5]), nbytes + 4.0 * n)})
+        kernels.update({f"parse_kernel<{ct}>": (k[3], 0.0 if fin else float(nbytes)),
+                        "tile_fix_kernel+tile_scan_kernel": (k[4], 0.0),
+                        f"decode_kernel_fast<{ct}>": (k[5], 0.0 if fin else dec_b)})
+    if fin:
+        kernels.update({f"parse_kernel<{ct}> (finish)": (k[6], float(nbytes)),
+                        "tile_fix_kernel+tile_scan_kernel (finish)": (k[7], 0.0),
+                        f"decode_kernel_fast<{ct}> (finish)": (k[8], 0.0 if res else dec_b)})
+    if res:
+        kernels.update({"resolve_kernel": (k[9], 0.0),
+                        f"decode_kernel_fast<{ct}> (resolved)": (k[10], dec_b)})
     return kernels
 
 
@@ -711,9 +724,7 @@ def line_for(C, W, R, steps):
             "slow_path_in_timed_step": bool(R.get("slow_path_timed", False)),
             "dominant": {"kernel": dname, "avg_launch_ms": round(dms, 4), "achieved_GBs": round(ach, 1),
                          "frac": round(ach / HBM_PEAK_GBS, 4)},
-            "kernels_note": None if min(v[0] for v in kernels.values()) >= 0 else
-            "the decode finished on the chunk-map decoder inside the step (slow path): the per-kernel events of "
-            "the library's timing sets do not line up with its launches, ignore kernels_ms",
+            "kernels_sum_ms": round(sum(v[0] for v in kernels.values()), 4),
             "step_roofline_frac": round(step_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "kernels_ms": {k: round(v[0], 4) for k, v in kernels.items()}}
 

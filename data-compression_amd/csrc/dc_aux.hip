@@ -852,45 +852,76 @@ extern "C" int dc_launch_ham_syndrome(const uint8_t* s, long long nbytes, unsign
 
 // ------------------------------------------------------------------------------------------------
 // Per-kernel timing hooks (bench.py's roofline): when enabled, the launchers record HIP events on
-// their stream between kernels; event set s holds marks 0..3 (encode: start, count, scan, write) and
-// 4..7 (decode: start, parse, tile fix + scan, decode).
+// their stream between kernels; event set s holds marks 0..3 (encode: start, count, -, pack) and 4..7
+// (decode: start, parse, tile fix + scan (chunk-map decoder only), decode).  dc_decode_finish's slow
+// paths record into the set of the step that queued the decode: the chunk-map decoder's marks 4..7 go
+// to 8..11, and 12..15 bracket the runs-mode resolve and the resolved decode.
+constexpr int DC_MARKS = 16;
 static hipEvent_t* g_events = nullptr;
-static int g_nsets = 0, g_set = 0;
+static int g_nsets = 0, g_set = 0, g_finish = 0;
+static unsigned char* g_rec = nullptr;         // [set * DC_MARKS + mark] recorded in this session
 
+extern "C" void dc_timing_finish(int on) { g_finish = on; }
 extern "C" void dc_mark_phase(int k, hipStream_t st) {
-    if (!g_events || g_set >= g_nsets) return;
-    (void)hipEventRecord(g_events[g_set * 8 + k], st);
+    if (!g_events) return;
+    int set = g_set;
+    if (g_finish) {
+        if (g_set == 0) return;
+        set = g_set - 1;
+        if (k >= 4 && k < 8) k += 4;
+    } else if (k >= 8) {
+        return;
+    }
+    if (set >= g_nsets) return;
+    if (hipEventRecord(g_events[set * DC_MARKS + k], st) == hipSuccess) g_rec[set * DC_MARKS + k] = 1;
 }
 extern "C" void dc_mark_next_set(void) {
-    if (g_events && g_set < g_nsets) g_set++;
+    if (g_events && !g_finish && g_set < g_nsets) g_set++;
 }
 extern "C" int dc_timing_enable(int nsets) {
     if (g_events) {
-        for (int i = 0; i < g_nsets * 8; i++) (void)hipEventDestroy(g_events[i]);
+        for (int i = 0; i < g_nsets * DC_MARKS; i++) (void)hipEventDestroy(g_events[i]);
         free(g_events);
+        free(g_rec);
         g_events = nullptr;
+        g_rec = nullptr;
     }
     g_nsets = 0;
     g_set = 0;
     if (nsets <= 0) return 0;
-    g_events = (hipEvent_t*)calloc((size_t)nsets * 8, sizeof(hipEvent_t));
-    if (!g_events) return -1;
-    for (int i = 0; i < nsets * 8; i++)
+    g_events = (hipEvent_t*)calloc((size_t)nsets * DC_MARKS, sizeof(hipEvent_t));
+    g_rec = (unsigned char*)calloc((size_t)nsets * DC_MARKS, 1);
+    if (!g_events || !g_rec) return -1;
+    for (int i = 0; i < nsets * DC_MARKS; i++)
         if (hipEventCreate(&g_events[i]) != hipSuccess) return -1;
     g_nsets = nsets;
     return 0;
 }
-/* ms[0..5] = encode count, encode scan, encode write, decode parse, decode tile fix+scan, decode */
+// elapsed ms between two marks of a set; 0 when either was not recorded (that launch did not run)
+static int mark_ms(int set, int a, int b, float* ms) {
+    hipEvent_t* e = g_events + set * DC_MARKS;
+    *ms = 0.0f;
+    if (!g_rec[set * DC_MARKS + a] || !g_rec[set * DC_MARKS + b]) return 1;
+    if (hipEventSynchronize(e[b]) != hipSuccess) { (void)hipGetLastError(); return -1; }
+    if (hipEventElapsedTime(ms, e[a], e[b]) != hipSuccess) { *ms = -1.0f; (void)hipGetLastError(); }
+    return 0;
+}
+/* ms[0..5] = encode count, (empty: the group scans run in the count kernel), encode pack, decode parse,
+ * decode tile fix + scan (chunk-map decoder), decode */
 extern "C" int dc_timing_read(int set, float* ms) {
     if (!g_events || set < 0 || set >= g_nsets) return -1;
-    hipEvent_t* e = g_events + set * 8;
     const int a[6] = {0, 1, 2, 4, 5, 6};
-    // (an event a step did not record -- a decode finished on a slow path marks the next set -- fails
-    // here: the error is cleared so that it cannot surface at the caller's next HIP call)
-    for (int i = 0; i < 6; i++) {
-        if (hipEventSynchronize(e[a[i] + 1]) != hipSuccess) { (void)hipGetLastError(); return -1; }
-        if (hipEventElapsedTime(&ms[i], e[a[i]], e[a[i] + 1]) != hipSuccess) { ms[i] = -1.0f; (void)hipGetLastError(); }
-    }
+    for (int i = 0; i < 6; i++)
+        if (mark_ms(set, a[i], a[i] + 1, &ms[i]) < 0) return -1;
+    return 0;
+}
+/* ms[0..5] as dc_timing_read; ms[6..8] the chunk-map decoder's parse, tile fix + scan and decode run by
+ * dc_decode_finish; ms[9] the runs-mode resolve, ms[10] the resolved decode (0: not run) */
+extern "C" int dc_timing_read_all(int set, float* ms) {
+    if (dc_timing_read(set, ms)) return -1;
+    const int a[5] = {8, 9, 10, 12, 14};
+    for (int i = 0; i < 5; i++)
+        if (mark_ms(set, a[i], a[i] + 1, &ms[6 + i]) < 0) return -1;
     return 0;
 }
 

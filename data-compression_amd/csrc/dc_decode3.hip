@@ -12,14 +12,15 @@
 //                ds_read_b32 of a wave hits 32 distinct banks whatever the lanes' offsets.  At every
 //                chunk boundary the lane records the chunk's entry offset and token count (16 bits).
 //                Links are checked afterwards: a segment's first entry must equal the previous
-//                segment's exit (in-wave shuffle; across jobs the previous job's published exit when it
-//                is there -- never waited for, no chain -- else later, in scan3_kernel).  A broken link (the pre-walk had not
-//                synchronised, ~0.3% of segments) is repaired by re-walking from the true entry until
-//                the path meets the recorded entries again.  The wave's token counts are scanned into
-//                job-relative first-token offsets of every decode job.
-// scan3_kernel   exclusive scan of the parse jobs' token counts.
+//                segment's exit (in-wave shuffle; across jobs the previous job's exit, published right
+//                after its main walk and waited for -- no chain: an exit never waits for anything;
+//                a wait past its bound, never seen, hands the stream to the chunk-map decoder).  A
+//                broken link (the pre-walk had not synchronised, ~0.3% of segments) is repaired by
+//                re-walking from the true entry until the path meets the recorded entries again.  The
+//                wave's token counts are scanned into job-relative first-token offsets of every decode job.
 // decode3_kernel one wave per decode job of 64 chunks: lane = chunk, decoded from its recorded entry for
-//                its recorded token count.  Values go to a wave-private LDS buffer at their job-relative
+//                its recorded token count (the job's first token: the wave's running sum of the parse
+//                jobs' totals, advanced by a prefetched window per job -- no scan launch).  Values go to a wave-private LDS buffer at their job-relative
 //                index (aligned to the output's 16-byte grid) and leave as whole float4 stores.
 //                Predicted codes ('101'/'110'/'111', rare in ordinary data) read their history from that
 //                buffer; the first tokens of a chunk that need the previous chunk's values are left
@@ -41,6 +42,7 @@ constexpr int D3_SEG = 16;             // chunks per parse segment (4 region lin
 constexpr int D3_RING = 16;            // ring words per lane (four 128-bit phases), + 4 mirrored words
 constexpr int D3_CAP = 1024 + 16;      // decode job output buffer (floats per wave)
 constexpr uint32_t D3_DECLINE = 512u;
+constexpr unsigned long long D3_LINK_WAIT = 20000;  // s_memrealtime ticks (100 MHz): 200 us
 // why (diagnostic bits beside 512): 1024 runs mode / capacity, 2048 unresolved link, 4096 fewer tokens
 // than values, 8192 a job denser than its buffer, 16384 the history sentinel or an early prediction
 constexpr uint32_t D3_WHY_RUNS = 1024u, D3_WHY_LINK = 2048u, D3_WHY_SHORT = 4096u, D3_WHY_DENSE = 8192u,
@@ -196,21 +198,23 @@ __device__ __forceinline__ void stage_half(Stage8& st, int h0, __amdgpu_buffer_r
 // walk region lines L0 .. L1-1; the reader starts at segment bit pinit (a lane that is not live walks
 // nothing).  `start(c, kbase)` runs before chunk c is walked (c < 0 in the pre-walk), `end(c, count)`
 // after it.
-template <class Start, class End>
+// EARLY (the repair rounds): the walk ends after the first line in which no lane is left walking; a lane
+// that is not live loads nothing (its requests point past the buffer's range: 0, no memory traffic).
+template <bool EARLY, class Start, class End>
 __device__ __forceinline__ void run_lines(Ring3& r, __amdgpu_buffer_rsrc_t rs, long long nbytes, long long gw0, int L0,
                                           int L1, int lim, int pinit, bool live, const uint8_t* tl, Start start,
                                           End end) {
     Stage8 st;
+    const long long gl = (EARLY && !live) ? (1ll << 29) : gw0;        // the lane's load base
     const long long w0 = gw0 + 32ll * (L0 - 1);
-    stage_half(st, 0, rs, w0);
-    stage_half(st, 4, rs, w0 + 16);
+    stage_half(st, 0, rs, gl + 32ll * (L0 - 1));
+    stage_half(st, 4, rs, gl + 32ll * (L0 - 1) + 16);
     r.put(0, finish4(st.S[0], nbytes, w0));
     r.put(1, finish4(st.S[1], nbytes, w0 + 4));
     int kbase = 8 * (L0 - 1);
     r.init(pinit, kbase);
     if (!live) r.pos = 1 << 30;
     for (int L = L0; L < L1; L++) {
-        const long long wn = gw0 + 32ll * L;                        // the next line's first word
         int n0 = 0;
 #pragma unroll
         for (int h = 0; h < 8; h++) {
@@ -218,12 +222,13 @@ __device__ __forceinline__ void run_lines(Ring3& r, __amdgpu_buffer_rsrc_t rs, l
             if ((h & 1) == 0) start(k >> 1, kbase);
             const int n = r.walk(min(128 * (k + 1), lim), tl);
             r.put((h + 2) & 3, finish4(st.S[(h + 2) & 7], nbytes, gw0 + 4ll * (k + 2)));
-            if (h == 1) stage_half(st, 0, rs, wn);
-            if (h == 5) stage_half(st, 4, rs, wn + 16);
+            if (h == 1) stage_half(st, 0, rs, gl + 32ll * L);
+            if (h == 5) stage_half(st, 4, rs, gl + 32ll * L + 16);
             if ((h & 3) == 3) { kbase += 4; r.addr -= 4096u; }
             if (h & 1) end(k >> 1, n0 + n);
             else n0 = n;
         }
+        if (EARLY && !__any(r.pos < (1 << 30))) break;               // every lane met its recorded path
     }
 }
 
@@ -239,6 +244,8 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
     build_lut_len<CT>(tl, P, lane, 64);
     const Geo3 G = geo3(dev_nbits, host_nbits);
     const __amdgpu_buffer_rsrc_t rs = stream_rsrc(s, D3.capw);
+    const __amdgpu_buffer_rsrc_t rrec =
+        __builtin_amdgcn_make_buffer_rsrc(D3.rec, (short)0, (int)min(2 * (D3.max_chunks + 4096), 0x7FFFFF00ll), 0x00020000);   // (the pool pads rec by 4096 chunks)
     const bool decline = G.nchunks > D3.max_chunks || runs_mode(CT, G.nbits, num);
     if (decline && blockIdx.x == 0 && lane == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_RUNS);
     __syncthreads();
@@ -259,7 +266,7 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
         // ---- main walk: the pre-walk line (1024 bits before the segment), then the segment's lines
         uint32_t tot = 0;
         int e0 = 0, ec = 0;
-        run_lines(r, rs, G.nbytes, gw0, 0, seg / 4 + 1, lim, -1024, act, tl,
+        run_lines<false>(r, rs, G.nbytes, gw0, 0, seg / 4 + 1, lim, -1024, act, tl,
                   [&](int c, int kbase) {
                       if (c == 0 && sidx == 0) r.init(0, kbase);             // the stream's first bit
                       ec = r.pos - 256 * c;
@@ -281,8 +288,8 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
         // entry is not re-walks from that exit, rewriting its records until the path meets a recorded
         // entry again; a path that reaches the segment end without meeting it moves the exit, and the
         // successor is checked again (rounds; a moved exit of the last segment declines)
-        // (the link into the job: checked here if the previous job has published its exit -- jobs run
-        // side by side, so it usually has -- never waited for; scan3_kernel checks the others)
+        // (the link into the job: checked at once if the previous job has published its exit, else after
+        // the in-job links with a bounded wait)
         int xin = __shfl_up(X, 1, 64), ecur = e0, Xcur = X, rounds = 0;
         bool link0 = false;
         if (lane == 0 && act && sidx > 0) {
@@ -291,18 +298,28 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
         }
         bool bad = act && (lane > 0 || link0) && ecur != xin;
         for (int pass = 0; pass < 2; pass++) {
-        if (pass == 1) {                            // a second look at the job's first link (now often there)
+        if (pass == 1) {                            // the job's first link: wait (bounded) for the exit
             bool chk = false;
             if (lane == 0 && act && sidx > 0 && !link0) {
-                const uint64_t v = ld_relaxed(&D3.pexit[job - 1]);
+                // the previous job is resident (a lower workgroup, or this grid's previous round) and
+                // publishes its exit right after its main walk
+                const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
+                P3_T(tw0);
+                uint64_t v;
+                while (((v = ld_relaxed(&D3.pexit[job - 1])) >> 32) != (uint64_t)epoch &&
+                       __builtin_amdgcn_s_memrealtime() - w0 < D3_LINK_WAIT)
+                    __builtin_amdgcn_s_sleep(2);
                 if ((v >> 32) == (uint64_t)epoch) { xin = (int)(uint32_t)v; link0 = true; chk = true; }
+                else atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK);   // (never seen: the chunk-map decoder takes it)
+                P3_T(tw1);
+                P3_ADD(1, tw1 - tw0);
             }
             bad = chk && ecur != xin;
         }
         while (__any(bad)) {
             if (++rounds > 64) { if (lane == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK); break; }
             bool live = bad;
-            run_lines(r, rs, G.nbytes, gw0, 1, seg / 4 + 1, lim, bad ? xin : 0, bad, tl,
+            run_lines<true>(r, rs, G.nbytes, gw0, 1, seg / 4 + 1, lim, bad ? xin : 0, bad, tl,
                       [&](int c, int) {
                           const int old = (int)(recs[c * 64 + lane] & 31u);
                           if (live && c > 0 && r.pos - 256 * c == old && 256 * c < lim) {
@@ -335,16 +352,17 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
         P3_ADD(3, rounds);
         P3_ADD(5, 1);
 
-        if (lane == 0) D3.lver[job] = link0 ? 1u : 0u;
         // ---- the segment's records: 32 bytes per lane, one contiguous 2 KB block per wave
         if (act) {
             uint32_t w[seg / 2];
 #pragma unroll
             for (int i = 0; i < seg / 2; i++)
                 w[i] = (uint32_t)recs[(2 * i) * 64 + lane] | ((uint32_t)recs[(2 * i + 1) * 64 + lane] << 16);
-            uint4* dst = reinterpret_cast<uint4*>(D3.rec + c0);
 #pragma unroll
-            for (int i = 0; i < seg / 8; i++) dst[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+            for (int i = 0; i < seg / 8; i++) {
+                const u32x4 v = {w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
+                __builtin_amdgcn_raw_buffer_store_b128(v, rrec, (int)(2 * c0 + 16 * i), 0, 0);
+            }
         }
 
         // ---- token offsets: the job's total and every decode job's first token relative to the job
@@ -356,158 +374,6 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
         }
     }
     P3_FLUSH();
-}
-
-// the link into parse job t: its first segment's entry must be job t-1's exit.  A broken link (the
-// pre-walk had not synchronised; rare) is re-walked here, serially, until the path meets the recorded
-// entries again; the changed token counts move the job's total and its decode jobs' offsets.  Each
-// chunk's 8 words (+4 after it) are loaded at once and walked from registers.
-__device__ __forceinline__ uint32_t pick12(const uint32_t (&w)[12], int i) {
-    uint32_t r = w[0];
-#pragma unroll
-    for (int k = 1; k < 12; k++) r = i == k ? w[k] : r;
-    return r;
-}
-template <int CT>
-__device__ void link_fix(__amdgpu_buffer_rsrc_t rs, const Geo3& G, const Dec3Bufs& D3, const uint8_t* tl, long long t,
-                         int X) {
-    constexpr int seg = D3_SEG;
-    const long long cf = t * 64 * seg;                           // the job's first chunk
-    const long long cend = (t + 1) * 64 * seg;
-    long long pos = cf * 256 + X;
-    for (long long c = cf;; c++) {
-        if (c > cf) {
-            if (c >= G.nchunks) break;                                       // the stream's end
-            if (c >= cend) { atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK); return; }  // the job's exit moved
-            if (pos - 256 * c == (long long)(D3.rec[c] & 31u)) break;           // met the recorded path
-        }
-        uint32_t w[12];
-        {
-            const uint4 q0 = load_w4(rs, G.nbytes, 8 * c), q1 = load_w4(rs, G.nbytes, 8 * c + 4),
-                        q2 = load_w4(rs, G.nbytes, 8 * c + 8);
-            w[0] = q0.x; w[1] = q0.y; w[2] = q0.z; w[3] = q0.w; w[4] = q1.x; w[5] = q1.y;
-            w[6] = q1.z; w[7] = q1.w; w[8] = q2.x; w[9] = q2.y; w[10] = q2.z; w[11] = q2.w;
-        }
-        const int pe = (int)min(256ll, (long long)G.nbits - 256 * c);
-        const int e = (int)(pos - 256 * c);
-        int p = e;
-        uint32_t cnt = 0;
-        while (p < pe) {
-            const int i = p >> 5, sh = p & 31;
-            const uint32_t hi = pick12(w, i), lo = pick12(w, i + 1);
-            const uint32_t tk = sh ? ((hi << sh) | (lo >> (32 - sh))) : hi;
-            p += tl[tk >> 23];
-            cnt++;
-        }
-        pos = 256 * c + p;
-        const uint32_t old = D3.rec[c];
-        D3.rec[c] = (uint16_t)((uint32_t)(e & 31) | (cnt << 8));
-        const int d = (int)cnt - (int)(old >> 8);
-        if (d) {
-            D3.ptot[t] += (uint32_t)d;
-            for (int q = (int)((c - cf) / 64) + 1; q < seg; q++) D3.rel[t * seg + q] += (uint32_t)d;
-        }
-    }
-}
-
-// the links between parse jobs, then the exclusive scan of their token counts (one workgroup); a stream
-// with fewer tokens than num is left to the other decoder (it reads past the stream as the reference does)
-template <int CT>
-__global__ __launch_bounds__(1024) void scan3_kernel(const uint8_t* __restrict__ s, Params P, Dec3Bufs D3,
-                                                     const unsigned long long* dev_nbits,
-                                                     unsigned long long host_nbits, long long num) {
-    __shared__ unsigned long long wtot[16];
-    __shared__ uint32_t stot[8 * 1024];
-    __shared__ uint8_t tl[512];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-#ifdef DC_DEC3_PROF
-    const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
-#endif
-    build_lut_len<CT>(tl, P, tid, 1024);
-    __syncthreads();
-    const Geo3 G = geo3(dev_nbits, host_nbits);
-    if ((__hip_atomic_load(D3.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & D3_DECLINE) != 0) return;
-    const long long np = G.npjobs;
-#ifdef DC_DEC3_PROF
-    const long long s0 = clock64();
-    unsigned nfix = 0;
-#endif
-    // the links: every job's first entry against its predecessor's exit, four jobs' loads in flight
-    {
-        const __amdgpu_buffer_rsrc_t rs = stream_rsrc(s, D3.capw);
-        constexpr int U = 4;
-        for (long long tb = 1 + tid; tb < np; tb += 1024 * U) {
-            int X[U];
-            uint32_t R[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const long long t = tb + 1024ll * u;
-                const bool in = t < np && t * 64 * D3_SEG < G.nchunks && D3.lver[t] == 0u;
-                X[u] = in ? (int)(uint32_t)D3.pexit[t - 1] : 0;
-                R[u] = in ? (uint32_t)D3.rec[t * 64 * D3_SEG] & 31u : 0u;
-            }
-#pragma unroll
-            for (int u = 0; u < U; u++)
-                if ((int)R[u] != X[u]) {
-                    link_fix<CT>(rs, G, D3, tl, tb + 1024ll * u, X[u]);
-#ifdef DC_DEC3_PROF
-                    nfix++;
-#endif
-                }
-        }
-    }
-#ifdef DC_DEC3_PROF
-    atomicMax(&g_prof3[16], (unsigned long long)(clock64() - s0));
-    if (nfix) atomicAdd(&g_prof3[17], (unsigned long long)nfix);
-#endif
-    __syncthreads();
-    // exclusive scan of the job totals in chunks of 8192: all of a chunk's loads at once (coalesced),
-    // through LDS to 8 consecutive totals per thread
-    unsigned long long carry = 0;
-    for (long long c0 = 0; c0 < np; c0 += 8 * 1024) {
-        uint32_t v[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const long long t = c0 + k * 1024 + tid;
-            v[k] = t < np ? D3.ptot[t] : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < 8; k++) stot[k * 1024 + tid] = v[k];
-        __syncthreads();
-        uint32_t c[8];
-        unsigned long long sum = 0;
-#pragma unroll
-        for (int i = 0; i < 8; i++) { c[i] = stot[tid * 8 + i]; sum += c[i]; }
-        unsigned long long inc = sum;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const unsigned long long u = __shfl_up(inc, d, 64);
-            if (lane >= d) inc += u;
-        }
-        if (lane == 63) wtot[wid] = inc;
-        __syncthreads();
-        unsigned long long wpre = 0, all = 0;
-#pragma unroll
-        for (int w = 0; w < 16; w++) { wpre += w < wid ? wtot[w] : 0ull; all += wtot[w]; }
-        unsigned long long run = carry + wpre + inc - sum;
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const long long t = c0 + tid * 8 + i;
-            if (t < np) D3.pbase[t] = run;
-            run += c[i];
-        }
-        carry += all;
-        __syncthreads();                                             // stot / wtot are rewritten
-    }
-    const unsigned long long all = carry;
-    if (tid == 0) {
-        D3.pbase[np] = all;
-        if ((long long)all < num) atomicOr(D3.err, D3_DECLINE | D3_WHY_SHORT);
-#ifdef DC_DEC3_PROF
-        atomicAdd(&g_prof3[18], (unsigned long long)(clock64() - s0));
-        atomicAdd(&g_prof3[19], __builtin_amdgcn_s_memrealtime() - rt0);
-#endif
-    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -587,24 +453,38 @@ constexpr int D3_OOB = 0x7FFFFFF0;                  // a buffer offset past ever
                                                     // (ranges end below 0x7FFFFF00)
 struct Pre3 {
     uint32_t rc, rl;
-    u32x2 pb;
+    uint32_t pt[4];                                 // parse-job token totals of the job's window (below)
     uint4 v0, v1, v2;
 };
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t any_rsrc(const void* p, int bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes, 0x00020000);
 }
-__device__ __forceinline__ Pre3 prefetch3(__amdgpu_buffer_rsrc_t rr, __amdgpu_buffer_rsrc_t rp, __amdgpu_buffer_rsrc_t rl,
-                                          __amdgpu_buffer_rsrc_t rs, const Geo3& G, unsigned job, int lane) {
+// (the first token of parse job pj is the sum of ptot[0..pj): a wave keeps that sum for the parse job of
+// its previous decode job, plo, and adds the window ptot[plo..pj) -- 256 totals, 4 per lane, when the
+// grid's stride is 4096 decode jobs -- so no scan kernel and no wait on another wave)
+__device__ __forceinline__ Pre3 prefetch3(__amdgpu_buffer_rsrc_t rr, __amdgpu_buffer_rsrc_t rt, __amdgpu_buffer_rsrc_t rl,
+                                          __amdgpu_buffer_rsrc_t rs, const Geo3& G, unsigned job, long long plo,
+                                          int lane) {
     Pre3 q;
     const long long g = (long long)job * 64 + lane;
     const bool ok = (long long)job < G.ndjobs;
+    const long long phi = ok ? (long long)(job / D3_SEG) : plo;
     q.rc = __builtin_amdgcn_raw_buffer_load_b16(rr, g < G.nchunks ? (int)(2 * g) : D3_OOB, 0, 0);
-    q.pb = __builtin_amdgcn_raw_buffer_load_b64(rp, ok ? (int)(8 * (job / D3_SEG)) : D3_OOB, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const long long k = plo + 4 * lane + i;
+        q.pt[i] = __builtin_amdgcn_raw_buffer_load_b32(rt, k < phi ? (int)(4 * k) : D3_OOB, 0, 0);
+    }
     q.rl = __builtin_amdgcn_raw_buffer_load_b32(rl, ok ? (int)(4 * job) : D3_OOB, 0, 0);
     q.v0 = load_raw4(rs, 8 * g);
     q.v1 = load_raw4(rs, 8 * g + 4);
     q.v2 = load_raw4(rs, 8 * g + 8);
     return q;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += (uint32_t)__shfl_xor((int)v, d, 64);
+    return v;
 }
 
 template <int CT>
@@ -619,7 +499,7 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const Geo3 G = geo3(dev_nbits, host_nbits);
     const __amdgpu_buffer_rsrc_t rs = stream_rsrc(s, D3.capw);
-    const __amdgpu_buffer_rsrc_t rr = any_rsrc(D3.rec, 0x7FFFFF00), rp = any_rsrc(D3.pbase, 0x7FFFFF00),
+    const __amdgpu_buffer_rsrc_t rr = any_rsrc(D3.rec, 0x7FFFFF00), rt = any_rsrc(D3.ptot, 0x7FFFFF00),
                                  rl = any_rsrc(D3.rel, 0x7FFFFF00), ro = any_rsrc(out, (int)(num * 4));
     const bool declined = (__hip_atomic_load(D3.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & D3_DECLINE) != 0;
     // patterns without a midpoint bit can equal the -1.0f history sentinel: check every value then
@@ -631,14 +511,33 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
     // at ~13 ns each).  A job waits only for its predecessor's published values, rarely, and every
     // predecessor belongs to an earlier wave of the same round or to an earlier round.
     const unsigned stride = gridDim.x * 4;
+    unsigned long long pcar = 0;                    // first token of parse job plo
+    long long plo = 0;
     auto process = [&](const Pre3& cur, unsigned job) {
         P3_T(u0);
         const long long g = (long long)job * 64 + lane;
         const int e = (int)(cur.rc & 31u), n = (int)(cur.rc >> 8);
-        const unsigned long long base = ((unsigned long long)cur.pb.y << 32 | cur.pb.x) + cur.rl;
+        const long long pj = (long long)(job / D3_SEG);
+        uint32_t wsum = wave_sum(cur.pt[0] + cur.pt[1] + cur.pt[2] + cur.pt[3]);
+        for (long long k0 = plo + 256; k0 < pj; k0 += 256) {     // a window longer than one prefetch (rare)
+            uint32_t v = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const long long k = k0 + 4 * lane + i;
+                v += k < pj ? D3.ptot[k] : 0u;
+            }
+            wsum += wave_sum(v);
+        }
+        pcar += wsum;
+        plo = pj;
+        const unsigned long long base = pcar + cur.rl;
         const uint32_t inc = wave_incl_scan((uint32_t)n, lane);
         const int off = (int)inc - n;
         const int Tn = (int)__builtin_amdgcn_readlane(inc, 63);
+        // the stream's last decode job: a stream with fewer tokens than num is left to the other decoder
+        // (it reads past the stream as the reference does)
+        if ((long long)job == G.ndjobs - 1 && (long long)(base + (unsigned long long)Tn) < num && lane == 0)
+            atomicOr(D3.err, D3_DECLINE | D3_WHY_SHORT);
         const int al = (int)(base & 3ull);
         P3_T(u1);
         P3_ADD(8, u1 - u0);
@@ -776,7 +675,7 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
     // store issued since, as stores count in the same counter)
     unsigned job = blockIdx.x * 4 + w;
     if (!declined && (long long)job < G.ndjobs) {
-        Pre3 A = prefetch3(rr, rp, rl, rs, G, job, lane), B;
+        Pre3 A = prefetch3(rr, rt, rl, rs, G, job, 0, lane), B;
         // as many (dropped, distinct) stores after the first prefetch as a job issues after its
         // successor's: the loop's entry then looks like its back edge to the wait-count placement,
         // which otherwise waits for every store of the previous job before using a job's inputs
@@ -788,11 +687,11 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
             __builtin_amdgcn_raw_buffer_store_b128(z4, ro, D3_OOB - 64 * (i + 1), 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(0u, ro, D3_OOB, 0, 0);
         for (;;) {
-            B = prefetch3(rr, rp, rl, rs, G, job + stride, lane);
+            B = prefetch3(rr, rt, rl, rs, G, job + stride, (long long)(job / D3_SEG), lane);
             process(A, job);
             job += stride;
             if ((long long)job >= G.ndjobs) break;
-            A = prefetch3(rr, rp, rl, rs, G, job + stride, lane);
+            A = prefetch3(rr, rt, rl, rs, G, job + stride, (long long)(job / D3_SEG), lane);
             process(B, job);
             job += stride;
             if ((long long)job >= G.ndjobs) break;
@@ -845,23 +744,20 @@ static void dbg_dump(const Dec3Bufs* D3) {
     if (!on) return;
     hipStream_t s2;
     if (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) != hipSuccess) return;
-    unsigned lv[4] = {0}, err = 0;
+    unsigned err = 0;
     uint64_t hist[12] = {0};
-    unsigned long long pb[4] = {0};
     uint32_t rel[4] = {0}, pt[4] = {0};
     uint16_t rec[16] = {0};
-    (void)hipMemcpyAsync(lv, D3->lver, sizeof lv, hipMemcpyDeviceToHost, s2);
     (void)hipMemcpyAsync(&err, D3->err, 4, hipMemcpyDeviceToHost, s2);
     (void)hipMemcpyAsync(hist, D3->hist, sizeof hist, hipMemcpyDeviceToHost, s2);
-    (void)hipMemcpyAsync(pb, D3->pbase, sizeof pb, hipMemcpyDeviceToHost, s2);
     (void)hipMemcpyAsync(rel, D3->rel, sizeof rel, hipMemcpyDeviceToHost, s2);
     (void)hipMemcpyAsync(pt, D3->ptot, sizeof pt, hipMemcpyDeviceToHost, s2);
     (void)hipMemcpyAsync(rec, D3->rec, sizeof rec, hipMemcpyDeviceToHost, s2);
     (void)hipStreamSynchronize(s2);
-    fprintf(stderr, "[dcamd] lver %u %u %u %u err 0x%x seg %d\n", lv[0], lv[1], lv[2], lv[3], err, D3->seg);
+    fprintf(stderr, "[dcamd] err 0x%x seg %d\n", err, D3->seg);
     for (int i = 0; i < 4; i++)
-        fprintf(stderr, "  job %d hist %llx %llx %llx pbase %llu rel %u ptot %u\n", i, (unsigned long long)hist[3 * i],
-                (unsigned long long)hist[3 * i + 1], (unsigned long long)hist[3 * i + 2], pb[i], rel[i], pt[i]);
+        fprintf(stderr, "  job %d hist %llx %llx %llx rel %u ptot %u\n", i, (unsigned long long)hist[3 * i],
+                (unsigned long long)hist[3 * i + 1], (unsigned long long)hist[3 * i + 2], rel[i], pt[i]);
     for (int i = 0; i < 16; i++) fprintf(stderr, " rec%d=%u/%u", i, rec[i] & 31u, rec[i] >> 8);
     fprintf(stderr, "\n");
     fflush(stderr);
@@ -889,8 +785,6 @@ extern "C" int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev
     DC_DISPATCH_3(P->ct, parse3_kernel, dim3(g1), dim3(64), 0, st, s, *P, *D3, dev_nbits, host_nbits, num, epoch);
     dbg_wait("parse3_kernel", st);
     dc_mark_phase(5, st);
-    DC_DISPATCH_3(P->ct, scan3_kernel, dim3(1), dim3(1024), 0, st, s, *P, *D3, dev_nbits, host_nbits, num);
-    dbg_wait("scan3_kernel", st);
     dc_mark_phase(6, st);
     DC_DISPATCH_3(P->ct, decode3_kernel, dim3(g3), dim3(256), 0, st, s, *P, *D3, dev_nbits, host_nbits, out, num, epoch);
     dbg_wait("decode3_kernel", st);

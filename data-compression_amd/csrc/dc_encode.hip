@@ -14,7 +14,9 @@
 //                         writes, neighbour words merged through DPP), then stored shifted by G mod 32:
 //                         every word from the one holding the tile's first bit to its last full word.
 // (A single pass with published tile totals was measured slower: a tile waits for the slowest of
-// its predecessors' loads, 220-700 us against 140 us, see DESIGN.md.)
+// its predecessors' loads, 220-700 us against 140 us; so was a scan folded into the count and pack
+// kernels -- a device-scope atomic add of every tile's total into its group's, which the pack then sums:
+// count 65 -> 143 us, see DESIGN.md.)
 #include "dc_device.h"
 #include <algorithm>
 #include <stdlib.h>
@@ -296,7 +298,7 @@ template <int CT>
 __global__ __launch_bounds__(ENC_TPB) void encode_pack_kernel(
     const float* __restrict__ x, long long n, long long idx0, Params P, uint32_t* __restrict__ out,
     const uint64_t* __restrict__ toff, const uint32_t* __restrict__ tails, const uint16_t* __restrict__ psum16,
-    unsigned ntiles, unsigned long long* __restrict__ dbg) {
+    unsigned ntiles, int start_bit, unsigned* __restrict__ err, unsigned long long* __restrict__ dbg) {
     static_assert(ENC_K == 16 && ENC_TPB == 256, "16 consecutive floats per thread, 4 waves per tile");
 #define E3STAMP(ph) do { if (dbg && threadIdx.x == 0 && blockIdx.x < 8192) dbg[blockIdx.x * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); } while (0)
     E3STAMP(0);
@@ -461,6 +463,12 @@ __global__ __launch_bounds__(ENC_TPB) void encode_pack_kernel(
     const long long W0 = (long long)(Gt >> 5);
     const int nw = (int)((long long)((Gt + T) >> 5) - W0) + ((tile == ntiles - 1 && ((Gt + T) & 31ull)) ? 1 : 0);
     const int tw = (int)((T + 31u) >> 5);                              // buffer words holding tile bits
+    // (a guard, never taken by a correct encode: a tile's bits end within the stream's capacity, 32 bits
+    // per float after the start bit -- a stale offset must not send the stores outside the buffer)
+    if (Gt + T > (unsigned long long)start_bit + 32ull * (unsigned long long)min(n, tbase + ENC_TILE)) {
+        if (tid == 0) atomicOr(err, 2u);
+        return;
+    }
     for (int i = tid; i < nw; i += ENC_TPB) {
         const uint32_t cur = i < tw ? sb[i] : 0u;                      // (stale past the tile's bits)
         const uint32_t prev = i ? sb[i - 1] : tp0;
@@ -486,10 +494,8 @@ __global__ __launch_bounds__(ENC_TPB) void encode_pack_kernel(
     }
 
 extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, const Params* P,
-                                uint32_t* out, uint64_t* desc, unsigned* tile_ctr, uint32_t epoch,
-                                int start_bit, unsigned long long* total_bits, unsigned long long* total_bits2,
+                                uint32_t* out, uint64_t* desc, int start_bit, unsigned long long* total_bits, unsigned long long* total_bits2,
                                 unsigned* err, unsigned long long* dbg, hipStream_t stream) {
-    (void)tile_ctr;
     if (n <= 0) return 0;
     const unsigned ntiles = (unsigned)((n + ENC_TILE - 1) / ENC_TILE);
     // desc: tile offsets (u64) | tile bit counts (u32) | tile tails (u32)
@@ -504,9 +510,8 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
                        total_bits, total_bits2);
     dc_mark_phase(2, stream);
     DC_ENC_DISPATCH(encode_pack_kernel, dim3(ntiles), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, desc, tails,
-                    psum16, ntiles, dbg);
+                    psum16, ntiles, start_bit, err, dbg);
     dc_mark_phase(3, stream);
-    (void)tile_ctr; (void)epoch;
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -40,10 +40,8 @@ typedef struct {
     uint64_t* enc_desc;
     long long enc_desc_cap;
     unsigned long long* enc_dbg;   /* DC_DEBUG_STAMPS: [tile][8] encoder phase stamps */
-    unsigned* enc_ctr;
     unsigned long long* d_total;
     unsigned* d_enc_err;
-    uint32_t enc_epoch;
     /* decoder */
     DecBufs D;
     void* dec_pool;
@@ -65,6 +63,7 @@ typedef struct {
     long long dec3_cap;              /* 256-bit chunks the pool holds */
     int dec3_used;                   /* the pending decode ran the segment decoder */
     int dec3_last;                   /* the last finished decode's values came from it */
+    int dec3_launched;               /* the last dc_decode_device launched it (it may decline later) */
     const unsigned long long* dec_dnbits;   /* the pending decode's device bit count (or NULL) */
     unsigned long long dec_hnbits;          /* ... or its host bit count */
     const float* dec_hin;            /* its incoming values (shard mode 2) */
@@ -205,8 +204,6 @@ int dc_init(int device) {
     HIPCHK(hipEventCreateWithFlags(&G.ev_enc, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&G.ev_lib, hipEventDisableTiming));
     HIPCHK(hipHostMalloc((void**)&G.h_scratch, 64 * sizeof(unsigned long long), 0));
-    HIPCHK(hipMalloc((void**)&G.enc_ctr, 64));
-    HIPCHK(hipMemset(G.enc_ctr, 0, 64));
     HIPCHK(hipMalloc((void**)&G.d_total, 64));
     HIPCHK(hipMalloc((void**)&G.d_enc_err, 64));
     HIPCHK(hipMemset(G.d_enc_err, 0, 64));
@@ -237,7 +234,6 @@ int dc_init(int device) {
     HIPCHK(hipMalloc((void**)&G.d_x2n, sizeof x2n));
     HIPCHK(hipMemcpy(G.d_crctab, tab, sizeof tab, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(G.d_x2n, x2n, sizeof x2n, hipMemcpyHostToDevice));
-    G.enc_epoch = 1;
     G.dec_epoch = 1;
     G.inited = 1;
     return DC_OK;
@@ -361,11 +357,6 @@ static int encode_on(hipStream_t st, int ct, const void* d_x, long long n, long 
         HIPCHK(hipMalloc((void**)&G.enc_desc, cap * sizeof(uint64_t)));
         HIPCHK(hipMemsetAsync(G.enc_desc, 0, cap * sizeof(uint64_t), st));
         G.enc_desc_cap = cap;
-        G.enc_epoch = 1;
-    }
-    if (++G.enc_epoch >= (1u << 14)) {          /* tile totals carry 14 epoch bits */
-        HIPCHK(hipMemsetAsync(G.enc_desc, 0, G.enc_desc_cap * sizeof(uint64_t), st));
-        G.enc_epoch = 1;
     }
     unsigned long long* tot = d_total_bits ? d_total_bits : G.d_total;
     G.last_enc_st = st;
@@ -380,8 +371,7 @@ static int encode_on(hipStream_t st, int ct, const void* d_x, long long n, long 
         HIPCHK(hipMemset(G.enc_dbg, 0, 8192 * 8 * 8));
     }
     /* the kernel writes the total to both (no copy node per encode) */
-    if (dc_launch_encode((const float*)d_x, n, idx0, &P, (uint32_t*)d_out, G.enc_desc, G.enc_ctr, G.enc_epoch,
-                         start_bit, tot, tot != G.d_total ? G.d_total : NULL, G.d_enc_err, G.enc_dbg, st))
+    if (dc_launch_encode((const float*)d_x, n, idx0, &P, (uint32_t*)d_out, G.enc_desc, start_bit, tot, tot != G.d_total ? G.d_total : NULL, G.d_enc_err, G.enc_dbg, st))
         return seterr(DC_ERR_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
     return DC_OK;
 }
@@ -432,7 +422,7 @@ int dc_encode_result(unsigned long long* total_bits) {
         if (err & 1u)
             return seterr(DC_ERR_INPUT, "input contains -1.0f, the reference encoder's empty-history sentinel "
                                         "(impl/dataCompression.c:2032); CT5/7/11 inputs must be >= 0 (toSmallDataset_float)");
-        return seterr(DC_ERR_HIP, "encoder look-back timed out (err=%u)", err);
+        return seterr(DC_ERR_HIP, "encoder tile offsets inconsistent, nothing stored (err=%u)", err);
     }
     if (total_bits) *total_bits = G.h_scratch[0];
     return DC_OK;
@@ -528,27 +518,23 @@ static int dec3_ensure(long long max_chunks) {
         G.dec3_pool = NULL;
         const long long C = max_chunks + 4096;
         const long long DJ = C / 64 + 64, PJ = C / (64 * 4) + 64;
-        size_t sz[7], off = 0, tot = 0;
+        size_t sz[5], off = 0, tot = 0;
         sz[0] = (size_t)C * 2;                /* rec */
         sz[1] = (size_t)DJ * 4;               /* rel */
         sz[2] = (size_t)PJ * 4;               /* ptot */
-        sz[3] = (size_t)(PJ + 1) * 8;         /* pbase */
-        sz[4] = (size_t)PJ * 8;               /* pexit */
-        sz[5] = (size_t)DJ * 3 * 8;           /* hist */
-        sz[6] = (size_t)PJ * 4;               /* lver */
-        for (int i = 0; i < 7; i++) tot += (sz[i] + 255) & ~(size_t)255;
+        sz[3] = (size_t)PJ * 8;               /* pexit */
+        sz[4] = (size_t)DJ * 3 * 8;           /* hist */
+        for (int i = 0; i < 5; i++) tot += (sz[i] + 255) & ~(size_t)255;
         HIPCHK(hipMalloc(&G.dec3_pool, tot));
         HIPCHK(hipMemsetAsync(G.dec3_pool, 0, tot, G.st));
         char* b = (char*)G.dec3_pool;
-        void* ptr[7];
-        for (int i = 0; i < 7; i++) { ptr[i] = b + off; off += (sz[i] + 255) & ~(size_t)255; }
+        void* ptr[5];
+        for (int i = 0; i < 5; i++) { ptr[i] = b + off; off += (sz[i] + 255) & ~(size_t)255; }
         G.D3.rec = (uint16_t*)ptr[0];
         G.D3.rel = (uint32_t*)ptr[1];
         G.D3.ptot = (uint32_t*)ptr[2];
-        G.D3.pbase = (unsigned long long*)ptr[3];
-        G.D3.pexit = (uint64_t*)ptr[4];
-        G.D3.hist = (uint64_t*)ptr[5];
-        G.D3.lver = (uint32_t*)ptr[6];
+        G.D3.pexit = (uint64_t*)ptr[3];
+        G.D3.hist = (uint64_t*)ptr[4];
         G.dec3_cap = max_chunks;
     }
     G.D3.max_chunks = G.dec3_cap;
@@ -568,6 +554,7 @@ static long long dec3_min_bytes(void) {
 }
 /* < -1: the default; -1 disables the segment decoder; returns the previous value */
 int dc_last_decode_was_v3(void) { return G.dec3_last; }
+int dc_last_decode_launched_v3(void) { return G.dec3_launched; }
 long long dc_set_decode3_min_bytes(long long v) {
     const long long old = dec3_min_bytes();
     g_dec3_min = v < -1 ? (1ll << 20) + 1 : v;
@@ -602,6 +589,7 @@ int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsig
     const long long need16 = nbytes >= 0 ? (nbytes + 15) / 16 * 16 : 0;
     G.dec3_used = m3 >= 0 && max_bytes >= m3 && max_bytes >= 16 && max_bytes >= need16 && max_bytes < (1ll << 31) && num < (1ll << 29) && !G.D.shard &&
                   !((uintptr_t)d_stream & 15u) && !((uintptr_t)d_out & 15u);
+    G.dec3_launched = G.dec3_used;
     G.dec_dnbits = nbytes >= 0 ? NULL : d_nbits;
     G.dec_hnbits = nbytes >= 0 ? (unsigned long long)nbytes * 8ull : 0ull;
     if (G.dec3_used) {
@@ -645,7 +633,16 @@ int dc_decode_status(unsigned* status_out) {
     return DC_OK;
 }
 
+static int decode_finish_body(void);
+/* the slow paths' launches are timed into the current step's event set (dc_timing_read_all) */
 int dc_decode_finish(void) {
+    dc_timing_finish(1);
+    const int rc = decode_finish_body();
+    dc_timing_finish(0);
+    return rc;
+}
+
+static int decode_finish_body(void) {
     int rc = ensure_init();
     if (rc) return rc;
     unsigned err = 0;
@@ -706,10 +703,15 @@ int dc_decode_finish(void) {
         if (G.dec_runs) {
             /* runs mode: the parse left every chunk map its tiles reach -- compose them, then the fast
              * decode kernel (which checks the history sentinel itself) from the resolved entries */
-            if (DV(dc_launch_resolve)(G.dec_max_chunks, &G.D, G.dec_epoch, G.st) ||
-                DV(dc_launch_decode_fast_resolved)(G.dec_s, G.dec_max_chunks, &G.dec_P, &G.D, G.dec_out, G.dec_num,
+            dc_mark_phase(12, G.st);
+            if (DV(dc_launch_resolve)(G.dec_max_chunks, &G.D, G.dec_epoch, G.st))
+                return seterr(DC_ERR_HIP, "decode launch failed");
+            dc_mark_phase(13, G.st);
+            dc_mark_phase(14, G.st);
+            if (DV(dc_launch_decode_fast_resolved)(G.dec_s, G.dec_max_chunks, &G.dec_P, &G.D, G.dec_out, G.dec_num,
                                                G.dec_epoch, G.st))
                 return seterr(DC_ERR_HIP, "decode launch failed");
+            dc_mark_phase(15, G.st);
             fast_values = 1;
         } else if (DV(dc_launch_decode)(G.dec_s, NULL, G.dec_nbits, G.dec_max_chunks, &G.dec_P, &G.D, G.dec_out, G.dec_num,
                                     G.dec_epoch, DEC_ROUNDS, DEC_FIX_ITERS, G.st))

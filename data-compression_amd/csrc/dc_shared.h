@@ -72,10 +72,8 @@ typedef struct Dec3Bufs {
     uint16_t* rec;                 /* [chunk] entry (bits 0..4) | tokens << 8 */
     uint32_t* rel;                 /* [decode job = 64 chunks] first token, relative to its parse job */
     uint32_t* ptot;                /* [parse job = 64 segments] tokens */
-    unsigned long long* pbase;     /* [parse job + 1] first token of the parse job (exclusive scan) */
     uint64_t* pexit;               /* [parse job] epoch << 32 | its last lane's exit (main walk) */
     uint64_t* hist;                /* [decode job][3] the job's last three values, epoch-tagged granules */
-    uint32_t* lver;                /* [parse job] 1: its first segment's link was checked (and repaired) in parse */
     unsigned* err;                 /* the DecBufs status word; 512 = this path declined the stream */
     int seg;                       /* chunks per parse segment: 16 or 32 */
     long long max_chunks;          /* capacity of rec */
@@ -93,9 +91,10 @@ extern "C" {
 typedef struct ihipStream_t* dc_hip_stream;
 
 int dc_launch_encode(const float* x, long long n, long long idx0, const DC_NS Params* P, uint32_t* out,
-                     uint64_t* desc, unsigned* tile_ctr, uint32_t epoch, int start_bit,
+                     uint64_t* desc, int start_bit,
                      unsigned long long* total_bits, unsigned long long* total_bits2, unsigned* err,
                      unsigned long long* dbg, dc_hip_stream stream);
+long long dc_encode_group_count(long long n);
 long long dc_encode_tile_count(long long n);
 long long dc_encode_desc_words(long long n);
 int dc_launch_encode_bits(const float* x, long long n, long long idx0, const DC_NS Params* P, uint64_t* desc,
@@ -138,6 +137,8 @@ void dc_mark_phase(int k, dc_hip_stream st);
 void dc_mark_next_set(void);
 int dc_timing_enable(int nsets);
 int dc_timing_read(int set, float* ms);
+int dc_timing_read_all(int set, float* ms);
+void dc_timing_finish(int on);
 long long dc_decode_group(void);
 /* the same decoder built with 256-bit chunks (Makefile SMALLDEFS renames its symbols with _s) */
 int dc_launch_decode_s(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,

@@ -44,7 +44,7 @@ EXT_SYMBOLS = [
     "dc64_stream_capacity", "dc64_encode_device", "dc64_encode_result", "dc64_decode_device", "dc64_decode_finish",
     "dc64_last_decode_flags", "dc64_to_small_device", "dc64_med_device", "dc_set_encode_stream",
     "dc_decode_status", "dc_abi_status", "dc_med_sum_device", "dc_type_from_max", "dc_set_small_chunk_max_bytes",
-    "dc_set_decode3_min_bytes", "dc_last_decode_was_v3",
+    "dc_set_decode3_min_bytes", "dc_last_decode_was_v3", "dc_last_decode_launched_v3",
 ]
 
 

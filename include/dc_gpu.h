@@ -149,6 +149,9 @@ long long dc_set_small_chunk_max_bytes(long long max_bytes);
 long long dc_set_decode3_min_bytes(long long min_bytes);
 /* 1 if the last decode's values came from the segment decoder (after dc_decode_finish). */
 int dc_last_decode_was_v3(void);
+/* 1: the last dc_decode_device launched the segment decoder (its values may still come from the chunk-map
+ * decoder if it declined the stream: dc_last_decode_was_v3 after dc_decode_finish tells) */
+int dc_last_decode_launched_v3(void);
 
 #ifdef __cplusplus
 }

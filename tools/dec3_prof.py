@@ -58,14 +58,12 @@ def main():
           f"v3 {L.last_decode_was_v3()} wall {wall * 1e3:.3f} ms/decode")
     pj, dj = max(p[5], 1), max(p[13], 1)
     print(f"parse: jobs {p[5]:.0f} tokens {p[4]:.0f} repair rounds {p[3]:.0f}")
-    print(f"  per job (kcycles): main {p[0] / pj / 1e3:.1f} link {p[1] / pj / 1e3:.1f} repair {p[2] / pj / 1e3:.1f}")
+    print(f"  per job (kcycles): main {p[0] / pj / 1e3:.1f} link wait {p[1] / pj / 1e3:.1f} repair {p[2] / pj / 1e3:.1f}")
     print(f"  per token per lane-walk (cycles): {p[0] / max(p[4] / 64, 1):.1f}")
     print(f"decode: jobs {p[13]:.0f} tokens {p[15]:.0f} pending lanes {p[14]:.0f}")
     print(f"  per job (kcycles): claim {p[8] / dj / 1e3:.2f} stage {p[9] / dj / 1e3:.2f} walk {p[10] / dj / 1e3:.2f} "
           f"pend {p[11] / dj / 1e3:.2f} store {p[12] / dj / 1e3:.2f}")
     print(f"  walk cycles per token step: {p[10] / max(p[15] / 64, 1):.1f}")
-    print(f"scan3: link phase max {p[16] / 1e3:.1f} kcycles (per call, summed over {reps}: max of max), fixes {p[17]:.1f}, "
-          f"whole kernel (thread 0) {p[18] / 1e3:.1f} kcycles, realtime {p[19] * 0.01:.2f} us")
     spec = np.array([v for v in out[:8].cpu().numpy()])
     print("first values", spec)
 
