@@ -232,6 +232,37 @@ __device__ __forceinline__ void run_lines(Ring3& r, __amdgpu_buffer_rsrc_t rs, l
     }
 }
 
+// A runs-mode stream (mostly 3-bit codes) that is nothing but num '100' codes -- every value within the
+// bound of 0, e.g. a constant input after toSmallDataset (BASELINE config 3) -- decodes to num zeros
+// (impl/dataCompression.c:1712-1716: '100' -> 0).  parse3 checks the first 3*num stream bits against the
+// period-3 pattern 100100... (grid-stride over 32-bit words, MSB-first) and flags any difference;
+// decode3 then writes the zeros at streaming speed, or hands the stream to the chunk-map decoder.
+constexpr uint32_t D3_ZMISS = 32768u;
+__device__ __forceinline__ void zero_run_check(__amdgpu_buffer_rsrc_t rs, const Geo3& G, long long num, unsigned* err) {
+    const unsigned long long need = 3ull * (unsigned long long)num;
+    if (need > G.nbits) {                                     // fewer bits than num tokens: not this case
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err, D3_ZMISS);
+        return;
+    }
+    const long long nw = (long long)((need + 31) >> 5);
+    bool bad = false;
+    const long long step = (long long)gridDim.x * blockDim.x * 4;
+    for (long long w0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4; w0 < nw; w0 += step) {
+        const uint4 q = load_w4(rs, G.nbytes, w0);
+        const uint32_t v[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const long long w = w0 + i;
+            const uint32_t ph = (uint32_t)((2 * w) % 3);                   // (32 w) mod 3
+            const uint32_t pat = ph == 0 ? 0x92492492u : (ph == 1 ? 0x24924924u : 0x49249249u);
+            const long long rem = (long long)need - 32 * w;               // bits of the word to check
+            const uint32_t m = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ~(0xFFFFFFFFu >> rem));
+            bad |= ((v[i] ^ pat) & m) != 0u;
+        }
+    }
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(err, D3_ZMISS);
+}
+
 template <int CT>
 __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ s, Params P, Dec3Bufs D3,
                                                     const unsigned long long* dev_nbits, unsigned long long host_nbits,
@@ -246,8 +277,10 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
     const __amdgpu_buffer_rsrc_t rs = stream_rsrc(s, D3.capw);
     const __amdgpu_buffer_rsrc_t rrec =
         __builtin_amdgcn_make_buffer_rsrc(D3.rec, (short)0, (int)min(2 * (D3.max_chunks + 4096), 0x7FFFFF00ll), 0x00020000);   // (the pool pads rec by 4096 chunks)
-    const bool decline = G.nchunks > D3.max_chunks || runs_mode(CT, G.nbits, num);
-    if (decline && blockIdx.x == 0 && lane == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_RUNS);
+    const bool over = G.nchunks > D3.max_chunks, runs = !over && runs_mode(CT, G.nbits, num);
+    const bool decline = over || runs;
+    if (over && blockIdx.x == 0 && lane == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_RUNS);
+    if (runs) zero_run_check(rs, G, num, D3.err);      // decode3 fills zeros, or hands the stream over
     __syncthreads();
     Ring3 r;
     r.L = ring;
@@ -501,7 +534,21 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
     const __amdgpu_buffer_rsrc_t rs = stream_rsrc(s, D3.capw);
     const __amdgpu_buffer_rsrc_t rr = any_rsrc(D3.rec, 0x7FFFFF00), rt = any_rsrc(D3.ptot, 0x7FFFFF00),
                                  rl = any_rsrc(D3.rel, 0x7FFFFF00), ro = any_rsrc(out, (int)(num * 4));
-    const bool declined = (__hip_atomic_load(D3.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & D3_DECLINE) != 0;
+    const unsigned err0 = __hip_atomic_load(D3.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool declined = (err0 & D3_DECLINE) != 0;
+    if (!declined && G.nchunks <= D3.max_chunks && runs_mode(CT, G.nbits, num)) {
+        // a runs-mode stream: num zeros if parse3 found nothing but '100' codes, else the chunk-map decoder's
+        if (err0 & D3_ZMISS) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_RUNS);
+            return;
+        }
+        const u32x4 z4 = {0u, 0u, 0u, 0u};
+        const __amdgpu_buffer_rsrc_t rz = any_rsrc(out, (int)(num * 4));
+        for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; 4 * i < num; i += (long long)gridDim.x * blockDim.x)
+            if (4 * i + 4 <= num) __builtin_amdgcn_raw_buffer_store_b128(z4, rz, (int)(16 * i), 0, DC_DEC3_NT ? 2 : 0);
+            else for (long long j = 4 * i; j < num; j++) out[j] = 0.0f;
+        return;
+    }
     // patterns without a midpoint bit can equal the -1.0f history sentinel: check every value then
     const bool chk_all = (CT == 6 && P.B >= 23) || (CT == 7 && (P.mask17 >> 16) != 0u && P.mm == 23);
     uint32_t* L = stg[w];

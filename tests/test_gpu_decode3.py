@@ -125,3 +125,31 @@ def test_decode3_device_chain(dc, oracle, ct, log2n):
     spec, got = oracle.decompress(ct, s, n, 1e-3, t, m17)
     assert got == n
     assert np.array_equal(out.cpu().numpy().view(np.uint32), spec.view(np.uint32))
+
+
+@pytest.mark.parametrize("ct", [5, 7, 11])
+@pytest.mark.parametrize("n,kind", [(1 << 18, "zeros"), (100003, "zeros"), (5, "zeros"), (1 << 18, "one"),
+                                    (1 << 18, "last"), (65537, "tiny")])
+def test_decode3_zero_runs(v3, oracle, ct, n, kind):
+    """Runs-mode streams of '100' codes only (constant input after toSmallDataset, BASELINE config 3) decode
+    to zeros inside the segment decoder; one value outside the bound anywhere (first, last) makes it hand
+    the stream to the chunk-map decoder -- both exact against the oracle's grammar decoder."""
+    v3.set_bound(1e-3)
+    x = np.full(n, np.float32(0.123456789))
+    if kind == "one":
+        x[n // 3] = np.float32(5.0)
+    elif kind == "last":
+        x[-1] = np.float32(5.0)
+    elif kind == "tiny":                                  # values inside the bound: still '100' codes
+        x[::17] = np.float32(0.123456789 + 4e-4)
+    _, xs = oracle.to_small(x)
+    t, m17 = oracle.type_mask(xs)
+    s, nb, pos = v3.compress(ct, xs, t, m17)
+    out = v3.decompress(ct, s, n, t, m17)
+    spec, got = oracle.decompress(ct, s, n, 1e-3, t, m17)
+    assert got == n
+    assert np.array_equal(out.view(np.uint32), spec.view(np.uint32))
+    if kind in ("zeros", "tiny"):
+        assert v3.last_decode_was_v3() and not out.view(np.uint32).any()
+    else:
+        assert not v3.last_decode_was_v3()
