@@ -670,16 +670,22 @@ def decode_sharded(L, ct, stream, stream_bytes, start_bit, nbits, num, out, type
 
 
 def gen_u10(n, seed=42, offset=0):
-    """Synthetic U10 input: counter-based splitmix64 -> uniform [0,10) float32."""
-    i = np.arange(offset, offset + n, dtype=np.uint64) + np.uint64(1)
-    with np.errstate(over="ignore"):
-        z = np.uint64(0x9E3779B97F4A7C15) * i + np.uint64(seed)
-        z ^= z >> np.uint64(30)
-        z *= np.uint64(0xBF58476D1CE4E5B9)
-        z ^= z >> np.uint64(27)
-        z *= np.uint64(0x94D049BB133111EB)
-        z ^= z >> np.uint64(31)
-    return ((z >> np.uint64(40)).astype(np.float32) * np.float32(2.0 ** -24)) * np.float32(10.0)
+    """Synthetic U10 input: counter-based splitmix64 -> uniform [0,10) float32.  Generated in
+    blocks of 2^22 so that the uint64 temporaries stay small (~100 MB) at any n (2^28: 1 GB of output)."""
+    out = np.empty(n, dtype=np.float32)
+    blk = 1 << 22
+    for b0 in range(0, n, blk):
+        m = min(blk, n - b0)
+        i = np.arange(offset + b0, offset + b0 + m, dtype=np.uint64) + np.uint64(1)
+        with np.errstate(over="ignore"):
+            z = np.uint64(0x9E3779B97F4A7C15) * i + np.uint64(seed)
+            z ^= z >> np.uint64(30)
+            z *= np.uint64(0xBF58476D1CE4E5B9)
+            z ^= z >> np.uint64(27)
+            z *= np.uint64(0x94D049BB133111EB)
+            z ^= z >> np.uint64(31)
+        out[b0:b0 + m] = ((z >> np.uint64(40)).astype(np.float32) * np.float32(2.0 ** -24)) * np.float32(10.0)
+    return out
 
 
 _lib = None

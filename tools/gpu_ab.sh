@@ -1,8 +1,17 @@
-# A/B: default library vs an experiment variant (lib_v0), then the GPU test suite on the default
+# A/B of two library builds on one box: tools/gpu_ab.sh LIB_B [tests]
+# bench (no extras) A B A B, kernel table of each; optional decode3 parity with build B first
 set -o pipefail
-cd /root/repo
-timeout -k 10 300 python -u bench.py --no-cpu --no-pipelined --steps 10 > gpurun_out/ab_new.json 2> gpurun_out/ab_new.err && \
-DCAMD_LIB=$PWD/data-compression_amd/lib_v0/libdcamd.so timeout -k 10 300 python -u bench.py --no-cpu --no-pipelined --steps 10 > gpurun_out/ab_old.json 2> gpurun_out/ab_old.err && \
-timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 240 --timeout-method thread > gpurun_out/gt.log 2>&1; rc=$?
-tail -5 gpurun_out/gt.log
-exit $rc
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+echo "tools/gpu_ab.sh $* $(date -u +%FT%TZ)" >> gpurun_out/script_log.txt
+LB=$1
+if [ "$2" = "tests" ]; then
+  DCAMD_LIB=$LB timeout -k 10 400 python3 -u -m pytest tests/test_gpu_decode3.py tests/test_gpu_codec.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/ab_t.log 2>&1 || { tail -30 gpurun_out/ab_t.log; exit 1; }
+  tail -1 gpurun_out/ab_t.log
+fi
+for i in 1 2; do
+  for lib in data-compression_amd/lib/libdcamd.so $LB; do
+    DCAMD_LIB=$lib timeout -k 10 200 python3 -u bench.py --no-cpu --no-pipelined --no-extra --steps 20 > gpurun_out/ab.json 2> gpurun_out/ab.err || { tail -20 gpurun_out/ab.err; exit 1; }
+    python3 -c "import json,sys;d=json.loads(open('gpurun_out/ab.json').readline());print(sys.argv[1].split('/')[1],d['value'],d['ms_per_step'],d['kernels_ms'])" $lib
+  done
+done
