@@ -1,0 +1,97 @@
+"""GPU multi-process test of the sharded path (bench.py's end-to-end step): two gloo ranks
+share cuda:0.  Every rank counts its shard's bits (dc_encode_bits_device), the counts are all-gathered into
+global start bits, each rank encodes its shard at (start mod 8) with its global index and predictor halo,
+the shards are gathered into the single global stream (dcamd.gather_stream) and each rank decodes its
+shard of that stream (dcamd.decode_sharded: deferred history, 12-byte exchange, prefix fix).  The
+gathered stream must equal the library's single-stream encode of the whole array, and every rank's values
+the single-stream decode's slice, bit for bit."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "data-compression_amd"))
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits_of(nbytes, pos):
+    return nbytes * 8 if pos == 8 else (nbytes - 1) * 8 + (8 - pos)
+
+
+def _worker(rank, world, port, ct, n, kind, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import dcamd
+        from pyoracle import Oracle
+        L = dcamd.Lib()
+        L.init(0)
+        L.set_bound(1e-3)
+        O = Oracle()
+        N = world * n
+        x = O.gen_u10(N)
+        if kind == "chain":                   # a constant run across every cut: a prediction chain enters
+            for r in range(1, world):         # the next shard, whose first values wait for the exchange
+                x[r * n - 700:r * n + 900] = x[r * n - 701]
+        _, xs = O.to_small(x)
+        t, m17 = O.type_mask(xs)
+        dev = torch.device("cuda", 0)
+        lo = rank * n
+        buf = torch.zeros(n + 4, dtype=torch.float32, device=dev)      # [halo | shard], shard 16-B aligned
+        halo = xs[max(lo - 3, 0):lo]
+        if halo.size:
+            buf[4 - halo.size:4] = torch.from_numpy(halo.copy())
+        buf[4:] = torch.from_numpy(xs[lo:lo + n].copy())
+        xd = buf[4:]
+        bits = L.encode_bits(ct, xd.data_ptr(), n, lo, t, m17)
+        meta = torch.tensor([bits], dtype=torch.int64)
+        parts = [torch.zeros_like(meta) for _ in range(world)]
+        dist.all_gather(parts, meta)
+        starts, total = dcamd.shard_offsets([int(p[0]) for p in parts])
+        sb = starts[rank] % 8
+        local = torch.zeros(L.stream_capacity(n) + 8, dtype=torch.uint8, device=dev)
+        L.encode_device(ct, xd.data_ptr(), n, local.data_ptr(), idx0=lo, type_=t, mask17=m17, start_bit=sb)
+        L.synchronize()
+        glob, tot = dcamd.gather_stream(local[:(sb + bits + 7) // 8], sb, sb + bits)
+        out = torch.empty(n, dtype=torch.float32, device=dev)
+        dcamd.decode_sharded(L, ct, glob, glob.numel(), starts[rank], bits, n, out, t, m17)
+        torch.cuda.synchronize()
+        s_all, nb_all, pos_all = L.compress(ct, xs, t, m17)             # the single stream, same GPU
+        dec_all = L.decompress(ct, s_all, N, t, m17)
+        ok_stream = bool(tot == _bits_of(nb_all, pos_all) and np.array_equal(glob.cpu().numpy(), s_all))
+        ok_dec = bool(np.array_equal(out.cpu().numpy().view(np.uint32), dec_all[lo:lo + n].view(np.uint32)))
+        q.put((rank, ok_stream, ok_dec))
+    except Exception as e:                    # report, do not hang the parent
+        q.put((rank, False, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+@pytest.mark.parametrize("ct,n,kind", [(7, (1 << 18) + 5, "u10"), (5, 100003, "chain"), (6, 65536, "u10"),
+                                       (11, 40001, "chain"), (7, 300007, "chain")])
+def test_sharded_encode_gather_decode_world2(ct, n, kind):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, ct, n, kind, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] is True and r[2] is True for r in res), res
