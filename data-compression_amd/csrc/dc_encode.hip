@@ -287,7 +287,10 @@ __global__ __launch_bounds__(1024) void encode_scan_kernel(const uint32_t* __res
 #define DC_PACK_NT 1                            // x read and the stream written past the caches (streaming)
 #endif
 constexpr int E3_WORDS = ENC_TILE + 64;                 // bit buffer words (4096 at 32 bits per float)
-constexpr int E3_STG = 64 * ENC_K / 16 * 20;            // a wave's staged floats (rows of 16 + 4 pad)
+#ifndef DC_PACK_STG2
+#define DC_PACK_STG2 1                          // transpose in two halves: half the staging LDS, 8 tiles per CU
+#endif
+constexpr int E3_STG = 64 * ENC_K / 16 * 20 / (DC_PACK_STG2 ? 2 : 1);   // a wave's staged floats (rows of 16 + 4 pad)
 constexpr int E3_LDS = E3_WORDS > 4 * E3_STG ? E3_WORDS : 4 * E3_STG;
 __device__ __forceinline__ uint32_t wave_shr1_u(uint32_t v, uint32_t first) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xF, 0xF, false);
@@ -295,7 +298,7 @@ __device__ __forceinline__ uint32_t wave_shr1_u(uint32_t v, uint32_t first) {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int CT>
-__global__ __launch_bounds__(ENC_TPB) void encode_pack_kernel(
+__global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_kernel(
     const float* __restrict__ x, long long n, long long idx0, Params P, uint32_t* __restrict__ out,
     const uint64_t* __restrict__ toff, const uint32_t* __restrict__ tails, const uint16_t* __restrict__ psum16,
     unsigned ntiles, int start_bit, unsigned* __restrict__ err, unsigned long long* __restrict__ dbg) {
@@ -329,6 +332,28 @@ __global__ __launch_bounds__(ENC_TPB) void encode_pack_kernel(
 #pragma unroll
         for (int q = 0; q < ENC_K / 4; q++)
             f[q] = __builtin_amdgcn_raw_buffer_load_b128(rsx, (int)(4 * (wb + 4 * (lane + 64 * q))), 0, DC_PACK_NT ? 2 : 0);
+#if DC_PACK_STG2
+        // two halves: float4s 0..127 (rows of lanes 0..31), then 128..255 (lanes 32..63) in the same 32 rows
+        // (a wave's LDS accesses run in order: the first half's reads precede the second half's writes)
+        f32x4 u[ENC_K / 4];
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                const int m = lane + 64 * q;
+                *reinterpret_cast<f32x4*>(stg + 4 * m + 4 * (m >> 2)) = f[2 * half + q];
+            }
+            __builtin_amdgcn_wave_barrier();
+            if ((lane >> 5) == half)
+#pragma unroll
+                for (int q = 0; q < ENC_K / 4; q++) u[q] = *reinterpret_cast<const f32x4*>(stg + 20 * (lane & 31) + 4 * q);
+            __builtin_amdgcn_wave_barrier();
+        }
+#pragma unroll
+        for (int q = 0; q < ENC_K / 4; q++) {
+            h[3 + 4 * q] = u[q].x; h[4 + 4 * q] = u[q].y; h[5 + 4 * q] = u[q].z; h[6 + 4 * q] = u[q].w;
+        }
+#else
 #pragma unroll
         for (int q = 0; q < ENC_K / 4; q++) {
             const int m = lane + 64 * q;
@@ -340,6 +365,7 @@ __global__ __launch_bounds__(ENC_TPB) void encode_pack_kernel(
             const f32x4 u = *reinterpret_cast<const f32x4*>(stg + 20 * lane + 4 * q);
             h[3 + 4 * q] = u.x; h[4 + 4 * q] = u.y; h[5 + 4 * q] = u.z; h[6 + 4 * q] = u.w;
         }
+#endif
         const long long w0 = tbase + 64ll * ENC_K * wid;                   // the wave's first element
         float hw[3];
 #pragma unroll
