@@ -38,7 +38,7 @@
 namespace dc {
 
 // pre-walk: 1024 bits (4 chunks, one region line) before every segment
-constexpr int D3_SEG = 16;             // chunks per parse segment (4 region lines)
+constexpr int D3_SEG = 16;             // chunks per parse segment (4 region lines); 8 for small streams
 constexpr int D3_RING = 16;            // ring words per lane (four 128-bit phases), + 4 mirrored words
 constexpr int D3_CAP = 1024 + 16;      // decode job output buffer (floats per wave)
 constexpr uint32_t D3_DECLINE = 512u;
@@ -114,8 +114,9 @@ struct Geo3 {
     unsigned long long nbits;
     long long nbytes, nchunks, nseg, npjobs, ndjobs;
 };
+template <int SEG>
 __device__ __forceinline__ Geo3 geo3(const unsigned long long* dev_nbits, unsigned long long host_nbits) {
-    constexpr int seg = D3_SEG;
+    constexpr int seg = SEG;
     Geo3 g;
     g.nbits = dev_nbits ? *dev_nbits : host_nbits;
     g.nbytes = (long long)((g.nbits + 7) >> 3);
@@ -263,17 +264,18 @@ __device__ __forceinline__ void zero_run_check(__amdgpu_buffer_rsrc_t rs, const 
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(err, D3_ZMISS);
 }
 
-template <int CT>
+template <int CT, int SEG>
 __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ s, Params P, Dec3Bufs D3,
                                                     const unsigned long long* dev_nbits, unsigned long long host_nbits,
                                                     long long num, uint32_t epoch) {
-    constexpr int seg = D3_SEG;
+    constexpr int seg = SEG;
+    static_assert(SEG % 8 == 0, "whole region lines and 16-byte record stores per lane");
     __shared__ uint32_t ring[(D3_RING + 4) * 64];
     __shared__ uint16_t recs[seg * 64];                          // [chunk][lane]: the wave's records
     __shared__ uint8_t tl[512];
     const int lane = threadIdx.x;
     build_lut_len<CT>(tl, P, lane, 64);
-    const Geo3 G = geo3(dev_nbits, host_nbits);
+    const Geo3 G = geo3<SEG>(dev_nbits, host_nbits);
     const __amdgpu_buffer_rsrc_t rs = stream_rsrc(s, D3.capw);
     const __amdgpu_buffer_rsrc_t rrec =
         __builtin_amdgcn_make_buffer_rsrc(D3.rec, (short)0, (int)min(2 * (D3.max_chunks + 4096), 0x7FFFFF00ll), 0x00020000);   // (the pool pads rec by 4096 chunks)
@@ -495,13 +497,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t any_rsrc(const void* p, int by
 // (the first token of parse job pj is the sum of ptot[0..pj): a wave keeps that sum for the parse job of
 // its previous decode job, plo, and adds the window ptot[plo..pj) -- 256 totals, 4 per lane, when the
 // grid's stride is 4096 decode jobs -- so no scan kernel and no wait on another wave)
+template <int SEG>
 __device__ __forceinline__ Pre3 prefetch3(__amdgpu_buffer_rsrc_t rr, __amdgpu_buffer_rsrc_t rt, __amdgpu_buffer_rsrc_t rl,
                                           __amdgpu_buffer_rsrc_t rs, const Geo3& G, unsigned job, long long plo,
                                           int lane) {
     Pre3 q;
     const long long g = (long long)job * 64 + lane;
     const bool ok = (long long)job < G.ndjobs;
-    const long long phi = ok ? (long long)(job / D3_SEG) : plo;
+    const long long phi = ok ? (long long)(job / SEG) : plo;
     q.rc = __builtin_amdgcn_raw_buffer_load_b16(rr, g < G.nchunks ? (int)(2 * g) : D3_OOB, 0, 0);
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -520,7 +523,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
-template <int CT>
+template <int CT, int SEG>
 __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict__ s, Params P, Dec3Bufs D3,
                                                      const unsigned long long* dev_nbits, unsigned long long host_nbits,
                                                      float* __restrict__ out, long long num, uint32_t epoch) {
@@ -530,7 +533,7 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
     build_lut3<CT>(T, P, threadIdx.x, 256);
     __syncthreads();
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const Geo3 G = geo3(dev_nbits, host_nbits);
+    const Geo3 G = geo3<SEG>(dev_nbits, host_nbits);
     const __amdgpu_buffer_rsrc_t rs = stream_rsrc(s, D3.capw);
     const __amdgpu_buffer_rsrc_t rr = any_rsrc(D3.rec, 0x7FFFFF00), rt = any_rsrc(D3.ptot, 0x7FFFFF00),
                                  rl = any_rsrc(D3.rel, 0x7FFFFF00), ro = any_rsrc(out, (int)(num * 4));
@@ -564,7 +567,7 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
         P3_T(u0);
         const long long g = (long long)job * 64 + lane;
         const int e = (int)(cur.rc & 31u), n = (int)(cur.rc >> 8);
-        const long long pj = (long long)(job / D3_SEG);
+        const long long pj = (long long)(job / SEG);
         uint32_t wsum = wave_sum(cur.pt[0] + cur.pt[1] + cur.pt[2] + cur.pt[3]);
         for (long long k0 = plo + 256; k0 < pj; k0 += 256) {     // a window longer than one prefetch (rare)
             uint32_t v = 0;
@@ -722,7 +725,7 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
     // store issued since, as stores count in the same counter)
     unsigned job = blockIdx.x * 4 + w;
     if (!declined && (long long)job < G.ndjobs) {
-        Pre3 A = prefetch3(rr, rt, rl, rs, G, job, 0, lane), B;
+        Pre3 A = prefetch3<SEG>(rr, rt, rl, rs, G, job, 0, lane), B;
         // as many (dropped, distinct) stores after the first prefetch as a job issues after its
         // successor's: the loop's entry then looks like its back edge to the wait-count placement,
         // which otherwise waits for every store of the previous job before using a job's inputs
@@ -734,11 +737,11 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
             __builtin_amdgcn_raw_buffer_store_b128(z4, ro, D3_OOB - 64 * (i + 1), 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(0u, ro, D3_OOB, 0, 0);
         for (;;) {
-            B = prefetch3(rr, rt, rl, rs, G, job + stride, (long long)(job / D3_SEG), lane);
+            B = prefetch3<SEG>(rr, rt, rl, rs, G, job + stride, (long long)(job / SEG), lane);
             process(A, job);
             job += stride;
             if ((long long)job >= G.ndjobs) break;
-            A = prefetch3(rr, rt, rl, rs, G, job + stride, (long long)(job / D3_SEG), lane);
+            A = prefetch3<SEG>(rr, rt, rl, rs, G, job + stride, (long long)(job / SEG), lane);
             process(B, job);
             job += stride;
             if ((long long)job >= G.ndjobs) break;
@@ -748,12 +751,16 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
 }
 
 // ------------------------------------------------------------------------------------------------
-#define DC_DISPATCH_3(CTV, KER, ...)                                                                 \
-    switch (CTV) {                                                                                   \
-        case 5: hipLaunchKernelGGL(KER<5>, __VA_ARGS__); break;                                      \
-        case 6: hipLaunchKernelGGL(KER<6>, __VA_ARGS__); break;                                      \
-        case 7: hipLaunchKernelGGL(KER<7>, __VA_ARGS__); break;                                      \
-        case 11: hipLaunchKernelGGL(KER<11>, __VA_ARGS__); break;                                    \
+#define DC_DISPATCH_3(CTV, SEGV, KER, ...)                                                           \
+    switch ((CTV) * 100 + (SEGV)) {                                                                  \
+        case 508: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<5, 8>), __VA_ARGS__); break;                \
+        case 608: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<6, 8>), __VA_ARGS__); break;                \
+        case 708: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<7, 8>), __VA_ARGS__); break;                \
+        case 1108: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<11, 8>), __VA_ARGS__); break;              \
+        case 516: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<5, 16>), __VA_ARGS__); break;               \
+        case 616: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<6, 16>), __VA_ARGS__); break;               \
+        case 716: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<7, 16>), __VA_ARGS__); break;               \
+        case 1116: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<11, 16>), __VA_ARGS__); break;             \
         default: return -2;                                                                          \
     }
 
@@ -765,10 +772,21 @@ static int resident3(const void* f, int threads) {
     return per * ncu;
 }
 
-// segment length (chunks): fixed; the host sizes the scratch with it
-extern "C" int dc_decode3_seg(long long max_chunks) {
-    (void)max_chunks;
-    return D3_SEG;
+// segment length (chunks) for a stream of up to max_chunks chunks: 16, or 8 for streams too small to
+// fill the GPU with 16-chunk segments (<= 2.5 M chunks of capacity, 80 MB: the parse's walk per lane
+// is then 1024 + 2048 bits instead of 1024 + 4096, and there are twice the jobs) whose tokens are short
+// enough (bound exponent B <= 12, e.g. 1e-3: tokens of <= ~21 bits) for a repaired path to meet the
+// recorded one within a 2048-bit segment -- at 1e-6 a job's last segment could move its exit and
+// decline the stream.  The host sizes the scratch for 4-chunk segments, so both fit (DC_DEC3_SEG=8|16
+// forces one)
+extern "C" int dc_decode3_seg(long long max_chunks, int B) {
+    static int forced = -1;
+    if (forced < 0) {
+        const char* e = getenv("DC_DEC3_SEG");
+        forced = (e && (atoi(e) == 8 || atoi(e) == 16)) ? atoi(e) : 0;
+    }
+    if (forced) return forced;
+    return (max_chunks <= 2500000ll && B <= 12) ? 8 : D3_SEG;
 }
 
 // DC_DEC3_DEBUG=1: wait for every kernel (at most 2 s each) and report one that does not finish
@@ -814,13 +832,14 @@ static void dbg_dump(const Dec3Bufs* D3) {
 extern "C" int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
                                  const Params* P, const Dec3Bufs* D3, float* out, long long num, uint32_t epoch,
                                  hipStream_t st) {
-    static int gp[12], gd[12];
+    static int gp[12], gd[12];                  // (the occupancy does not depend on the segment length)
     const int ci = (P->ct > 0 && P->ct < 12) ? P->ct : 0;
+    if (D3->seg != 8 && D3->seg != 16) return -2;
     if (!gp[ci]) {
-        const void* fp = P->ct == 5 ? (const void*)parse3_kernel<5> : P->ct == 6 ? (const void*)parse3_kernel<6>
-                       : P->ct == 7 ? (const void*)parse3_kernel<7> : (const void*)parse3_kernel<11>;
-        const void* fd = P->ct == 5 ? (const void*)decode3_kernel<5> : P->ct == 6 ? (const void*)decode3_kernel<6>
-                       : P->ct == 7 ? (const void*)decode3_kernel<7> : (const void*)decode3_kernel<11>;
+        const void* fp = P->ct == 5 ? (const void*)parse3_kernel<5, 16> : P->ct == 6 ? (const void*)parse3_kernel<6, 16>
+                       : P->ct == 7 ? (const void*)parse3_kernel<7, 16> : (const void*)parse3_kernel<11, 16>;
+        const void* fd = P->ct == 5 ? (const void*)decode3_kernel<5, 16> : P->ct == 6 ? (const void*)decode3_kernel<6, 16>
+                       : P->ct == 7 ? (const void*)decode3_kernel<7, 16> : (const void*)decode3_kernel<11, 16>;
         gp[ci] = resident3(fp, 64);
         gd[ci] = resident3(fd, 256);
     }
@@ -829,11 +848,12 @@ extern "C" int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev
     const int g1 = (int)std::max<long long>(1, std::min<long long>(maxpj, gp[ci]));
     const int g3 = (int)std::max<long long>(1, std::min<long long>((maxdj + 3) / 4, gd[ci]));
     dc_mark_phase(4, st);
-    DC_DISPATCH_3(P->ct, parse3_kernel, dim3(g1), dim3(64), 0, st, s, *P, *D3, dev_nbits, host_nbits, num, epoch);
+    DC_DISPATCH_3(P->ct, D3->seg, parse3_kernel, dim3(g1), dim3(64), 0, st, s, *P, *D3, dev_nbits, host_nbits, num, epoch);
     dbg_wait("parse3_kernel", st);
     dc_mark_phase(5, st);
     dc_mark_phase(6, st);
-    DC_DISPATCH_3(P->ct, decode3_kernel, dim3(g3), dim3(256), 0, st, s, *P, *D3, dev_nbits, host_nbits, out, num, epoch);
+    DC_DISPATCH_3(P->ct, D3->seg, decode3_kernel, dim3(g3), dim3(256), 0, st, s, *P, *D3, dev_nbits, host_nbits, out, num,
+                  epoch);
     dbg_wait("decode3_kernel", st);
     if (getenv("DC_DEC3_DEBUG") && hipStreamQuery(st) != hipSuccess) dbg_dump(D3);
     dc_mark_phase(7, st);

@@ -510,8 +510,8 @@ static int dec_next_epoch(void) {
 }
 
 /* segment decoder buffers for streams of up to max_chunks 256-bit chunks */
-static int dec3_ensure(long long max_chunks) {
-    const int seg = dc_decode3_seg(max_chunks);
+static int dec3_ensure(long long max_chunks, int B) {
+    const int seg = dc_decode3_seg(max_chunks, B);
     if (max_chunks <= G.dec3_cap && seg == G.D3.seg) return DC_OK;
     if (max_chunks > G.dec3_cap) {
         if (G.dec3_pool) HIPCHK(hipFree(G.dec3_pool));
@@ -593,7 +593,7 @@ int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsig
     G.dec_dnbits = nbytes >= 0 ? NULL : d_nbits;
     G.dec_hnbits = nbytes >= 0 ? (unsigned long long)nbytes * 8ull : 0ull;
     if (G.dec3_used) {
-        if ((rc = dec3_ensure((max_bytes * 8 + 255) / 256 + 1))) return rc;
+        if ((rc = dec3_ensure((max_bytes * 8 + 255) / 256 + 1, P.B))) return rc;
         G.D3.err = G.D.err;
         G.D3.capw = max_bytes / 16 * 4;
         if (dc_launch_decode3((const uint8_t*)d_stream, G.dec_dnbits, G.dec_hnbits, &P, &G.D3, (float*)d_out, num,

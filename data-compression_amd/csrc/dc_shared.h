@@ -117,7 +117,7 @@ int dc_launch_decode_serial(const uint8_t* s, const DC_NS Params* P, const DC_NS
 int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
                       const DC_NS Params* P, const DC_NS Dec3Bufs* D3, float* out, long long num, uint32_t epoch,
                       dc_hip_stream st);
-int dc_decode3_seg(long long max_chunks);
+int dc_decode3_seg(long long max_chunks, int B);
 long long dc_ct1_tiles(long long n);
 int dc_launch_ct1_encode(const float* x, long long n, float thr_le, uint32_t* traw, unsigned long long* rawoff,
                          float* raw, char* codes, int* pos1, unsigned* err, dc_hip_stream st);
