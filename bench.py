@@ -677,7 +677,8 @@ def copy_bandwidth(dev, n, reps=10):
 
 def kernel_table(ct, n, nbytes, kavg, v3=True):
     """The timed launches of a step (library timing slots, HIP events on the library stream) and their
-    algorithmic bytes: the encoder's count, scan and pack launches, then the decoder's -- the segment decoder (parse3, whose jobs check the
+    algorithmic bytes: the encoder's count and pack launches (the pack's workgroup 0 scans the tile
+    offsets), then the decoder's -- the segment decoder (parse3, whose jobs check the
     link into them, and decode3, which sums the parse jobs' totals itself: no scan launch) or the
     chunk-map decoder (parse, tile fix + scan, decode) -- and, when the first decoder handed the stream
     over inside the step (dc_decode_finish), the chunk-map decoder's launches and the runs-mode resolve
@@ -688,7 +689,6 @@ def kernel_table(ct, n, nbytes, kavg, v3=True):
     dec_b = nbytes + 4.0 * n
     kernels = {   # name: (avg ms, algorithmic bytes per launch)
         f"encode_count_kernel<{ct}>": (k[0], 4.0 * n),
-        "encode_scan_kernel": (k[1], 0.0),
         f"encode_pack_kernel<{ct}>": (k[2], 4.0 * n + nbytes),
     }
     if v3:

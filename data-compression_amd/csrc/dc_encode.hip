@@ -6,13 +6,15 @@
 // bit (:5456-5489).
 //
 // The encoder history is the ORIGINAL input (:2095-2097), so every token is a pure function of
-// x[i-3..i].  Three launches, no workgroup ever waits for another:
+// x[i-3..i].  Two launches:
 //   encode_count_kernel : per tile of ENC_TILE floats, the total token bit length and the tile's last
 //                         31 bits (its successor's first word starts with them)
-//   encode_scan_kernel  : exclusive scan of the tile lengths -> every tile's global bit offset G
-//   encode_pack_kernel  : the tile's tokens packed MSB-first into an LDS bit buffer (plain word
-//                         writes, neighbour words merged through DPP), then stored shifted by G mod 32:
-//                         every word from the one holding the tile's first bit to its last full word.
+//   encode_pack_kernel  : workgroup 0 first scans the tile lengths -> every tile's global bit offset G
+//                         and publishes them; every tile packs its tokens MSB-first into an LDS bit
+//                         buffer (plain word writes, neighbour words merged through DPP), then -- the
+//                         offsets long published -- stores them shifted by G mod 32: every word from the
+//                         one holding the tile's first bit to its last full word.
+// (encode_scan_kernel, the scan as a launch of its own, serves dc_launch_encode_bits.)
 // (A single pass with published tile totals was measured slower: a tile waits for the slowest of
 // its predecessors' loads, 220-700 us against 140 us; so was a scan folded into the count and pack
 // kernels -- a device-scope atomic add of every tile's total into its group's, which the pack then sums:
@@ -291,17 +293,92 @@ constexpr int E3_WORDS = ENC_TILE + 64;                 // bit buffer words (409
 #define DC_PACK_STG2 1                          // transpose in two halves: half the staging LDS, 8 tiles per CU
 #endif
 constexpr int E3_STG = 64 * ENC_K / 16 * 20 / (DC_PACK_STG2 ? 2 : 1);   // a wave's staged floats (rows of 16 + 4 pad)
-constexpr int E3_LDS = E3_WORDS > 4 * E3_STG ? E3_WORDS : 4 * E3_STG;
+constexpr int E3_LDS0 = E3_WORDS > 4 * E3_STG ? E3_WORDS : 4 * E3_STG;
+constexpr int E3_LDS = E3_LDS0 > 4096 + 256 ? E3_LDS0 : 4096 + 256;   // (+ workgroup 0's scan chunk)
 __device__ __forceinline__ uint32_t wave_shr1_u(uint32_t v, uint32_t first) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xF, 0xF, false);
 }
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Workgroup 0 of the pack kernel first scans the tile bit counts (no scan launch, no gap): chunks of 2048
+// counts (the next one's loads in flight), 8 consecutive per thread through the bit buffer's LDS (a pad
+// word per 16), a wave scan and the four wave totals; every offset is stored sc1 (written through), each wave drains its stores, and after
+// a barrier one lane publishes the encode's epoch in `flag` (the hand-off of MI355X_MICROARCH.md: sc1
+// stores, vmcnt(0) in every storing wave, barrier, one sc1 flag store; consumers poll and load sc1).
+// Workgroup 0 is dispatched first, so the others never wait for a workgroup that is not running.
+__device__ void pack_scan_block(const uint32_t* __restrict__ tcnt, uint64_t* __restrict__ toff, unsigned ntiles,
+                                int start_bit, unsigned long long* __restrict__ total_bits,
+                                unsigned long long* __restrict__ total_bits2, uint32_t* lds, uint32_t* s_w,
+                                unsigned* __restrict__ flag, uint32_t epoch) {
+    constexpr int PS = 8, PCH = 256 * PS;         // counts per thread and per chunk
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    unsigned long long carry = (unsigned long long)start_bit;
+    uint32_t nxt[PS];                             // the next chunk's counts, requested one chunk ahead
+#pragma unroll
+    for (int k = 0; k < PS; k++) {
+        const unsigned t = (unsigned)(k * 256 + tid);
+        nxt[k] = t < ntiles ? tcnt[t] : 0u;
+    }
+    for (unsigned c0 = 0; c0 < ntiles; c0 += PCH) {
+#pragma unroll
+        for (int k = 0; k < PS; k++) {
+            const int i = k * 256 + tid;
+            lds[i + (i >> 4)] = nxt[k];
+        }
+#pragma unroll
+        for (int k = 0; k < PS; k++) {
+            const unsigned t = c0 + PCH + (unsigned)(k * 256 + tid);
+            nxt[k] = t < ntiles ? tcnt[t] : 0u;
+        }
+        __syncthreads();
+        uint32_t c[PS], sum = 0;
+#pragma unroll
+        for (int i = 0; i < PS; i++) {
+            const int j = tid * PS + i;
+            c[i] = lds[j + (j >> 4)];
+            sum += c[i];
+        }
+        uint32_t inc = sum;                       // (a chunk's 2048 tiles hold < 2^28 bits)
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t u = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += u;
+        }
+        if (lane == 63) s_w[wid] = inc;
+        __syncthreads();
+        uint32_t wpre = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            wpre += w < wid ? s_w[w] : 0u;
+            tot += s_w[w];
+        }
+        unsigned long long run = carry + wpre + inc - sum;
+#pragma unroll
+        for (int i = 0; i < PS; i++) {
+            const unsigned t = c0 + (unsigned)(tid * PS + i);
+            if (t < ntiles) __hip_atomic_store(&toff[t], run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            run += c[i];
+        }
+        carry += tot;
+        // the chunk's offsets are out: published for its tiles at once (the early tiles wait for the first
+        // chunk only)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();                          // (also: lds / s_w are reused)
+        if (tid == 0) __hip_atomic_store(&flag[c0 / PCH], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tid == 0) {
+        *total_bits = carry;
+        if (total_bits2) *total_bits2 = carry;
+    }
+}
+
 template <int CT>
 __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_kernel(
     const float* __restrict__ x, long long n, long long idx0, Params P, uint32_t* __restrict__ out,
-    const uint64_t* __restrict__ toff, const uint32_t* __restrict__ tails, const uint16_t* __restrict__ psum16,
-    unsigned ntiles, int start_bit, unsigned* __restrict__ err, unsigned long long* __restrict__ dbg) {
+    uint64_t* __restrict__ toff, const uint32_t* __restrict__ tcnt, const uint32_t* __restrict__ tails,
+    const uint16_t* __restrict__ psum16, unsigned ntiles, int start_bit, unsigned long long* __restrict__ total_bits,
+    unsigned long long* __restrict__ total_bits2, unsigned* __restrict__ flag, uint32_t epoch,
+    unsigned* __restrict__ err, unsigned long long* __restrict__ dbg) {
     static_assert(ENC_K == 16 && ENC_TPB == 256, "16 consecutive floats per thread, 4 waves per tile");
 #define E3STAMP(ph) do { if (dbg && threadIdx.x == 0 && blockIdx.x < 8192) dbg[blockIdx.x * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); } while (0)
     E3STAMP(0);
@@ -310,7 +387,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
     __shared__ uint32_t s_hw[4], s_hi[4], s_tw[4], s_ti[4];           // the waves' first and last words
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const unsigned tile = blockIdx.x;
-    const unsigned long long Gt = toff[tile];                          // (requested first: scalar loads)
+    if (tile == 0) pack_scan_block(tcnt, toff, ntiles, start_bit, total_bits, total_bits2, sb, s_w, flag, epoch);
     const uint32_t tp0 = tile > 0 ? tails[tile - 1] : 0u;
     const uint32_t psum_full = psum16[(long long)tile * ENC_TPB + threadIdx.x];
     const long long tbase = (long long)tile * ENC_TILE;
@@ -482,7 +559,21 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
         }
         if (tid == 3 && s_ti[3] != 0xFFFFFFFFu) sb[s_ti[3]] = s_tw[3];     // the tile's last word
     }
+    // the tile's offset from workgroup 0's scan: published long before (its scan takes ~6 us, a tile's
+    // loads and tokens longer), polled by one lane, read by all after the barrier (sc1 loads)
+    if (tid == 0) {
+        s_hw[0] = 1u;
+        if (tile != 0) {
+            unsigned spins = 0;
+            while (__hip_atomic_load(&flag[tile / 2048u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+                if (++spins > (1u << 24)) { atomicOr(err, 4u); s_hw[0] = 0u; break; }   // (never seen)
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+    }
     __syncthreads();
+    if (s_hw[0] == 0u) return;                                         // no offset: nothing stored
+    const unsigned long long Gt = __hip_atomic_load(&toff[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     E3STAMP(3);
     // ---- store the words from the one holding the tile's first bit to its last full one
     const uint32_t sh = (uint32_t)(Gt & 31ull);
@@ -520,7 +611,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
     }
 
 extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, const Params* P,
-                                uint32_t* out, uint64_t* desc, int start_bit, unsigned long long* total_bits, unsigned long long* total_bits2,
+                                uint32_t* out, uint64_t* desc, unsigned* flag, uint32_t epoch, int start_bit, unsigned long long* total_bits, unsigned long long* total_bits2,
                                 unsigned* err, unsigned long long* dbg, hipStream_t stream) {
     if (n <= 0) return 0;
     const unsigned ntiles = (unsigned)((n + ENC_TILE - 1) / ENC_TILE);
@@ -532,11 +623,9 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
     DC_ENC_DISPATCH(encode_count_kernel, dim3(ntiles), dim3(256), 0, stream, x, n, idx0, *P, tbits,
                     (long long)ntiles, err, tails, psum16);
     dc_mark_phase(1, stream);
-    hipLaunchKernelGGL(encode_scan_kernel, dim3(1), dim3(1024), 0, stream, tbits, desc, (long long)ntiles, start_bit,
-                       total_bits, total_bits2);
     dc_mark_phase(2, stream);
-    DC_ENC_DISPATCH(encode_pack_kernel, dim3(ntiles), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, desc, tails,
-                    psum16, ntiles, start_bit, err, dbg);
+    DC_ENC_DISPATCH(encode_pack_kernel, dim3(ntiles), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, desc, tbits,
+                    tails, psum16, ntiles, start_bit, total_bits, total_bits2, flag, epoch, err, dbg);
     dc_mark_phase(3, stream);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

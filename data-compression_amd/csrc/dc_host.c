@@ -42,6 +42,8 @@ typedef struct {
     unsigned long long* enc_dbg;   /* DC_DEBUG_STAMPS: [tile][8] encoder phase stamps */
     unsigned long long* d_total;
     unsigned* d_enc_err;
+    unsigned* d_enc_flag;            /* the pack kernel's scan-published flag (encode epoch) */
+    uint32_t enc_epoch;
     /* decoder */
     DecBufs D;
     void* dec_pool;
@@ -207,6 +209,9 @@ int dc_init(int device) {
     HIPCHK(hipMalloc((void**)&G.d_total, 64));
     HIPCHK(hipMalloc((void**)&G.d_enc_err, 64));
     HIPCHK(hipMemset(G.d_enc_err, 0, 64));
+    HIPCHK(hipMalloc((void**)&G.d_enc_flag, 4096));          /* a flag per 2048 tiles: up to 2^33 floats */
+    HIPCHK(hipMemset(G.d_enc_flag, 0, 4096));
+    G.enc_epoch = 0;
     HIPCHK(hipMalloc((void**)&G.part_v, DC_MIN_PARTS * sizeof(float)));
     HIPCHK(hipMalloc((void**)&G.part_i, DC_MIN_PARTS * sizeof(long long)));
     HIPCHK(hipMalloc((void**)&G.d_f, 64));
@@ -347,6 +352,7 @@ static int encode_on(hipStream_t st, int ct, const void* d_x, long long n, long 
                      int start_bit, void* d_out, unsigned long long* d_total_bits) {
     if (!valid_ct(ct)) return seterr(DC_ERR_ARG, "unsupported CT %d", ct);
     if (start_bit < 0 || start_bit > 7 || n < 0) return seterr(DC_ERR_ARG, "bad start_bit/n");
+    if (n > (1ll << 33)) return seterr(DC_ERR_ARG, "n above 2^33 floats");
     if (ct == 7 && (type < 1 || type > 7)) return seterr(DC_ERR_ARG, "CT7 type %d outside 1..7", type);
     if (((uintptr_t)d_x & 15u) || ((uintptr_t)d_out & 3u)) return seterr(DC_ERR_ARG, "misaligned device buffer");
     Params P;
@@ -371,7 +377,9 @@ static int encode_on(hipStream_t st, int ct, const void* d_x, long long n, long 
         HIPCHK(hipMemset(G.enc_dbg, 0, 8192 * 8 * 8));
     }
     /* the kernel writes the total to both (no copy node per encode) */
-    if (dc_launch_encode((const float*)d_x, n, idx0, &P, (uint32_t*)d_out, G.enc_desc, start_bit, tot, tot != G.d_total ? G.d_total : NULL, G.d_enc_err, G.enc_dbg, st))
+    if (++G.enc_epoch == 0) G.enc_epoch = 1;      /* (the flag starts at 0: never a live epoch) */
+    if (dc_launch_encode((const float*)d_x, n, idx0, &P, (uint32_t*)d_out, G.enc_desc, G.d_enc_flag, G.enc_epoch,
+                         start_bit, tot, tot != G.d_total ? G.d_total : NULL, G.d_enc_err, G.enc_dbg, st))
         return seterr(DC_ERR_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
     return DC_OK;
 }
