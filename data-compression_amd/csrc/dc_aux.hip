@@ -852,8 +852,8 @@ extern "C" int dc_launch_ham_syndrome(const uint8_t* s, long long nbytes, unsign
 
 // ------------------------------------------------------------------------------------------------
 // Per-kernel timing hooks (bench.py's roofline): when enabled, the launchers record HIP events on
-// their stream between kernels; event set s holds marks 0..3 (encode: start, count, -, pack) and 4..7
-// (decode: start, parse, tile fix + scan (chunk-map decoder only), decode).  dc_decode_finish's slow
+// their stream between kernels; event set s holds marks 0..3 (encode: start, after count, -, after pack)
+// and 4..7 (decode: start, after parse, after tile fix + scan (chunk-map decoder only), after decode).  dc_decode_finish's slow
 // paths record into the set of the step that queued the decode: the chunk-map decoder's marks 4..7 go
 // to 8..11, and 12..15 bracket the runs-mode resolve and the resolved decode.
 constexpr int DC_MARKS = 16;
@@ -906,13 +906,19 @@ static int mark_ms(int set, int a, int b, float* ms) {
     if (hipEventElapsedTime(ms, e[a], e[b]) != hipSuccess) { *ms = -1.0f; (void)hipGetLastError(); }
     return 0;
 }
-/* ms[0..5] = encode count, (empty: the group scans run in the count kernel), encode pack, decode parse,
- * decode tile fix + scan (chunk-map decoder), decode */
+/* ms[0..5] = encode count, (empty: the scan runs in the pack kernel's workgroup 0), encode pack, decode parse,
+ * decode tile fix + scan (chunk-map decoder; empty for the segment decoder), decode */
 extern "C" int dc_timing_read(int set, float* ms) {
     if (!g_events || set < 0 || set >= g_nsets) return -1;
     const int a[6] = {0, 1, 2, 4, 5, 6};
-    for (int i = 0; i < 6; i++)
-        if (mark_ms(set, a[i], a[i] + 1, &ms[i]) < 0) return -1;
+    for (int i = 0; i < 6; i++) {
+        int b = a[i];
+        // a launcher that records no mark between two kernels (encoder: 2, segment decoder: 6): the second
+        // kernel's slot starts at the first one's end mark, the empty slot stays 0
+        if ((i == 2 || i == 5) && !g_rec[set * DC_MARKS + b]) b -= 1;
+        else if ((i == 1 || i == 4) && !g_rec[set * DC_MARKS + b + 1]) { ms[i] = 0.0f; continue; }
+        if (mark_ms(set, b, a[i] + 1, &ms[i]) < 0) return -1;
+    }
     return 0;
 }
 /* ms[0..5] as dc_timing_read; ms[6..8] the chunk-map decoder's parse, tile fix + scan and decode run by

@@ -850,8 +850,7 @@ extern "C" int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev
     dc_mark_phase(4, st);
     DC_DISPATCH_3(P->ct, D3->seg, parse3_kernel, dim3(g1), dim3(64), 0, st, s, *P, *D3, dev_nbits, host_nbits, num, epoch);
     dbg_wait("parse3_kernel", st);
-    dc_mark_phase(5, st);
-    dc_mark_phase(6, st);
+    dc_mark_phase(5, st);                       // (no mark 6: decode3's slot starts at mark 5)
     DC_DISPATCH_3(P->ct, D3->seg, decode3_kernel, dim3(g3), dim3(256), 0, st, s, *P, *D3, dev_nbits, host_nbits, out, num,
                   epoch);
     dbg_wait("decode3_kernel", st);

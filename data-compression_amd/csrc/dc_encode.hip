@@ -566,8 +566,8 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
         if (tile != 0) {
             unsigned spins = 0;
             while (__hip_atomic_load(&flag[tile / 2048u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-                if (++spins > (1u << 24)) { atomicOr(err, 4u); s_hw[0] = 0u; break; }   // (never seen)
-                __builtin_amdgcn_s_sleep(2);
+                if (++spins > (1u << 22)) { atomicOr(err, 4u); s_hw[0] = 0u; break; }   // (never seen)
+                __builtin_amdgcn_s_sleep(8);            // (~500 cycles: thousands of early tiles poll one word)
             }
         }
     }
@@ -622,8 +622,7 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
     dc_mark_phase(0, stream);
     DC_ENC_DISPATCH(encode_count_kernel, dim3(ntiles), dim3(256), 0, stream, x, n, idx0, *P, tbits,
                     (long long)ntiles, err, tails, psum16);
-    dc_mark_phase(1, stream);
-    dc_mark_phase(2, stream);
+    dc_mark_phase(1, stream);                   // (no mark 2: the pack's slot starts at mark 1)
     DC_ENC_DISPATCH(encode_pack_kernel, dim3(ntiles), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, desc, tbits,
                     tails, psum16, ntiles, start_bit, total_bits, total_bits2, flag, epoch, err, dbg);
     dc_mark_phase(3, stream);

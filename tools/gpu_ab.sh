@@ -12,7 +12,7 @@ if [ "$2" = "tests" ]; then
 fi
 for i in 1 2; do
   for lib in data-compression_amd/lib/libdcamd.so $LB; do
-    DCAMD_LIB=$lib timeout -k 10 200 python3 -u bench.py --no-cpu --no-pipelined --no-extra --steps 20 > gpurun_out/ab.json 2> gpurun_out/ab.err || { tail -20 gpurun_out/ab.err; exit 1; }
+    DCAMD_LIB=$lib timeout -k 10 200 python3 -u bench.py --no-cpu --no-pipelined --no-extra --steps 20 $BENCH_ARGS > gpurun_out/ab.json 2> gpurun_out/ab.err || { tail -20 gpurun_out/ab.err; exit 1; }
     python3 -c "import json,sys;d=json.loads(open('gpurun_out/ab.json').readline());print(sys.argv[1].split('/')[1],d['value'],d['ms_per_step'],d['kernels_ms'])" $lib | tee -a gpurun_out/ab_results.txt
   done
 done
