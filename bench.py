@@ -551,6 +551,10 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     C.barrier()
+    enc_status = L.encode_status()                    # the encoder's error word over all timed encodes
+    if enc_status:
+        print(f"bench.py: encoder error word 0x{enc_status:x} after the timed steps", file=sys.stderr)
+        sys.exit(1)
     status = L.decode_status()                        # OR over all timed decodes, no slow path run
     try:
         L.decode_finish()
@@ -587,7 +591,8 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
     kavg = kms.mean(axis=0)
     res = {"nbits": int(nbits), "nbytes": int(nbytes), "wall": wall, "enc_ms": enc_ms, "dec_ms": dec_ms,
            "kavg": kavg, "status": int(status | warm_status), "warm_status": int(warm_status), "resends": timed_resends,
-           "slow_path_timed": slow[0], "v3": bool(L.L.dc_last_decode_launched_v3())}
+           "slow_path_timed": slow[0], "v3": bool(L.L.dc_last_decode_launched_v3()),
+           "enc_mode": int(L.L.dc_encode_mode())}
 
     if pipelined and ber <= 0:
         # the same K steps pipelined (encode k+1 || decode k, two stream buffers), reported beside value
@@ -675,7 +680,7 @@ def copy_bandwidth(dev, n, reps=10):
     return 8.0 * n / (ms * 1e-3) / 1e9
 
 
-def kernel_table(ct, n, nbytes, kavg, v3=True):
+def kernel_table(ct, n, nbytes, kavg, v3=True, enc_mode=1):
     """The timed launches of a step (library timing slots, HIP events on the library stream) and their
     algorithmic bytes: the encoder's count and pack launches (the pack's workgroup 0 scans the tile
     offsets), then the decoder's -- the segment decoder (parse3, whose jobs check the
@@ -687,10 +692,13 @@ def kernel_table(ct, n, nbytes, kavg, v3=True):
     fin = any(v > 0 for v in k[6:11])
     res = k[9] > 0
     dec_b = nbytes + 4.0 * n
-    kernels = {   # name: (avg ms, algorithmic bytes per launch)
-        f"encode_count_kernel<{ct}>": (k[0], 4.0 * n),
-        f"encode_pack_kernel<{ct}>": (k[2], 4.0 * n + nbytes),
-    }
+    if enc_mode == 1:     # the single-pass encoder: one launch reads x once and writes the stream
+        kernels = {f"encode_fused_kernel<{ct}>": (k[0], 4.0 * n + nbytes)}
+    else:
+        kernels = {   # name: (avg ms, algorithmic bytes per launch)
+            f"encode_count_kernel<{ct}>": (k[0], 4.0 * n),
+            f"encode_pack_kernel<{ct}>": (k[2], 4.0 * n + nbytes),
+        }
     if v3:
         kernels.update({f"parse3_kernel<{ct}>": (k[3], 0.0 if fin else float(nbytes)),
                         f"decode3_kernel<{ct}>": (k[5], 0.0 if fin else dec_b)})
@@ -713,7 +721,7 @@ def line_for(C, W, R, steps):
     kernel (algorithmic bytes / its HIP-event duration on the library stream) and of the whole step."""
     n, nbytes = W["n"], R["nbytes"]
     ms = R["wall"] / steps * 1e3
-    kernels = kernel_table(W["ct"], n, nbytes, R["kavg"], R["v3"])
+    kernels = kernel_table(W["ct"], n, nbytes, R["kavg"], R["v3"], R.get("enc_mode", 1))
     dname = max(kernels, key=lambda k: kernels[k][0])
     dms, dbytes = kernels[dname]
     ach = dbytes / (dms * 1e-3) / 1e9 if dms > 0 else 0.0
@@ -768,7 +776,7 @@ def main():
         # warm-up on run it inside every timed step and are reported with fast_path false)
         print(f"bench.py: decoder status 0x{R['status']:x} in the timed steps (slow path not timed)", file=sys.stderr)
         sys.exit(1)
-    kernels = kernel_table(ct, n, nbytes, R["kavg"], R["v3"])
+    kernels = kernel_table(ct, n, nbytes, R["kavg"], R["v3"], R.get("enc_mode", 1))
     dname = main_line["dominant"]["kernel"]
     achievable = copy_bandwidth(C.dev, n)
     traffic, traffic_src = None, None

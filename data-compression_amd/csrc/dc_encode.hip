@@ -300,6 +300,20 @@ __device__ __forceinline__ uint32_t wave_shr1_u(uint32_t v, uint32_t first) {
 }
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// a tile's floats: lane l of wave w gets float4s l + 64q (q < 4) of the wave's 1024 floats, through a buffer
+// resource based at the tile (its range: the tile's floats, up to the 16-byte granule of the last one;
+// granules past it read 0, and a granule never straddles a page), so offsets stay small for any n
+__device__ __forceinline__ void load_tile_x(f32x4 (&f)[ENC_K / 4], const float* __restrict__ x, long long n,
+                                            long long tbase, int lane, int wid) {
+    const long long m = min(n - tbase, (long long)ENC_TILE);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x + tbase), (short)0, (int)((m + 3) / 4 * 16), 0x00020000);
+#pragma unroll
+    for (int q = 0; q < ENC_K / 4; q++)
+        f[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, 4 * (1024 * wid + 4 * (lane + 64 * q)), 0, DC_PACK_NT ? 2 : 0);
+}
+
+
 // Workgroup 0 of the pack kernel first scans the tile bit counts (no scan launch, no gap): chunks of 2048
 // counts (the next one's loads in flight), 8 consecutive per thread through the bit buffer's LDS (a pad
 // word per 16), a wave scan and the four wave totals; every offset is stored sc1 (written through), each wave drains its stores, and after
@@ -387,7 +401,8 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
     __shared__ uint32_t s_hw[4], s_hi[4], s_tw[4], s_ti[4];           // the waves' first and last words
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const unsigned tile = blockIdx.x;
-    if (tile == 0) pack_scan_block(tcnt, toff, ntiles, start_bit, total_bits, total_bits2, sb, s_w, flag, epoch);
+    // (flag == nullptr: the offsets come from encode_scan_kernel, launched before -- the wait-free fallback)
+    if (tile == 0 && flag) pack_scan_block(tcnt, toff, ntiles, start_bit, total_bits, total_bits2, sb, s_w, flag, epoch);
     const uint32_t tp0 = tile > 0 ? tails[tile - 1] : 0u;
     const uint32_t psum_full = psum16[(long long)tile * ENC_TPB + threadIdx.x];
     const long long tbase = (long long)tile * ENC_TILE;
@@ -401,14 +416,9 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
     // (DPP), for lane 0 the three floats before the wave's first.
     float h[ENC_K + 3];
     {
-        const __amdgpu_buffer_rsrc_t rsx =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), (short)0, (int)((n + 3) / 4 * 16), 0x00020000);
         float* stg = reinterpret_cast<float*>(sb) + wid * E3_STG;
-        const long long wb = tbase + 64ll * ENC_K * wid;
         f32x4 f[ENC_K / 4];
-#pragma unroll
-        for (int q = 0; q < ENC_K / 4; q++)
-            f[q] = __builtin_amdgcn_raw_buffer_load_b128(rsx, (int)(4 * (wb + 4 * (lane + 64 * q))), 0, DC_PACK_NT ? 2 : 0);
+        load_tile_x(f, x, n, tbase, lane, wid);
 #if DC_PACK_STG2
         // two halves: float4s 0..127 (rows of lanes 0..31), then 128..255 (lanes 32..63) in the same 32 rows
         // (a wave's LDS accesses run in order: the first half's reads precede the second half's writes)
@@ -563,7 +573,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
     // loads and tokens longer), polled by one lane, read by all after the barrier (sc1 loads)
     if (tid == 0) {
         s_hw[0] = 1u;
-        if (tile != 0) {
+        if (tile != 0 && flag) {
             unsigned spins = 0;
             while (__hip_atomic_load(&flag[tile / 2048u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
                 if (++spins > (1u << 22)) { atomicOr(err, 4u); s_hw[0] = 0u; break; }   // (never seen)
@@ -601,6 +611,327 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
 }
 
 // ------------------------------------------------------------------------------------------------
+// Single-pass encoder (the default, dc_launch_encode): ONE launch that reads x once.
+//
+// One workgroup per tile, dispatched in order (per XCD), so a tile's predecessors are running or done
+// whenever it waits.  Per tile: the 4096 floats, their tokens made once (values parked in LDS, lengths in
+// registers: tokens and history never share the register file), the thread bit counts scanned, the
+// tile's total published at once as an AGGREGATE state, the tokens packed into the LDS bit buffer, and
+// then -- the packing has given the predecessors time to publish -- the tile's bit offset from a decoupled
+// look-back over its predecessors' states (rocPRIM's lookback_scan_state scheme made wide: each lane
+// inspects 8 consecutive tiles, so one round trip covers 512 tiles); the INCLUSIVE state is published and
+// the words stored shifted by G mod 32.  The word holding a tile's first bit starts with its
+// predecessor's last bits, published as a granule of their own beside the aggregate.
+//
+// States are 8-byte granules written by ONE agent-scope (sc1) store and polled with agent-scope loads
+// (MI355X_MICROARCH.md, hand-off granules: the data is the flag, no fence): tag (the encode's epoch, 22
+// bits) << 42 | status << 40 | value (40 bits: a bit count or a bit offset).  A stale state of an earlier
+// encode never matches the tag (the host clears the array when the epoch wraps).  Every wait is bounded:
+// a look-back that times out poisons its tile (status 3, successors give up at once), stores nothing and
+// sets err bit 4; the host then re-encodes with the wait-free three-launch path (dc_encode_result).
+constexpr int LB_K = 8;                                           // look-back: tiles per lane per round trip
+constexpr unsigned long long ST_VAL = (1ull << 40) - 1;
+constexpr unsigned long long ST_MASK = 3ull << 40, ST_AGG = 1ull << 40, ST_INC = 2ull << 40, ST_BAD = 3ull << 40;
+constexpr uint32_t ST_TAGM = (1u << 22) - 1;
+constexpr unsigned long long LB_WAIT = 2000000ull;                // s_memrealtime ticks (100 MHz): 20 ms
+
+__device__ __forceinline__ uint64_t st_word(uint32_t tag, unsigned long long status, unsigned long long v) {
+    return ((uint64_t)tag << 42) | status | (v & ST_VAL);
+}
+__device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+// exclusive bit offset of tile t >= 1 (one whole wave; wave-uniform result).  Lane l inspects tiles
+// base - 8l - 7 .. base - 8l of the window [base - 511, base], all loads in flight at once; every state from
+// tile t - 1 down to the nearest INCLUSIVE one must be published (else the window is re-read), and their
+// values summed.  A window without an inclusive state adds its 512 aggregates and the next one is read.
+// Returns 0, or 1 when a needed state is poisoned or the wait timed out.
+__device__ __forceinline__ int enc_lookback(const uint64_t* __restrict__ st, long long t, uint32_t tag,
+                                            unsigned long long& excl) {
+    const int lane = threadIdx.x & 63;
+    long long base = t - 1;
+    excl = 0;
+    const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        uint64_t v[LB_K];
+        int kneed, kinc;
+        for (;;) {
+#pragma unroll
+            for (int k = 0; k < LB_K; k++) {
+                const long long ti = base - (long long)(lane * LB_K + k);
+                const uint64_t w = ld_relaxed(st + (ti >= 0 ? ti : 0));
+                v[k] = ti >= 0 ? w : st_word(tag, ST_INC, 0);           // (before tile 0: offset 0)
+            }
+            kinc = LB_K;
+            int kinv = LB_K;
+#pragma unroll
+            for (int k = LB_K - 1; k >= 0; k--) {
+                const bool live = (uint32_t)(v[k] >> 42) == tag && (v[k] & ST_MASK) != 0;
+                if (!live) kinv = k;
+                else if ((v[k] & ST_MASK) != ST_AGG) kinc = k;           // inclusive (or poisoned): stop there
+            }
+            const unsigned long long im = __ballot(kinc < LB_K);
+            const int li = im ? __ffsll((long long)im) - 1 : 64;
+            kneed = lane < li ? LB_K : (lane == li ? kinc + 1 : 0);
+            if (!__any(kinv < kneed)) break;
+            if (__builtin_amdgcn_s_memrealtime() - w0 > LB_WAIT) return 1;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        unsigned long long s = 0;
+        bool bad = false;
+#pragma unroll
+        for (int k = 0; k < LB_K; k++) {
+            if (k < kneed) {
+                s += v[k] & ST_VAL;
+                bad |= (v[k] & ST_MASK) == ST_BAD;
+            }
+        }
+        if (__any(bad)) return 1;
+        excl += wave_sum64(s);
+        if (__any(kinc < LB_K)) return 0;
+        base -= 64 * LB_K;
+    }
+}
+
+// the 16 tokens of a thread: values to tvs[256 j], lengths packed 4 per word in lp, their sum.  Not FAST: the
+// thread's elements j >= rem are past the end (no token), those j < g3 precede global index 3 (no prediction)
+template <int CT, bool FAST>
+__device__ __forceinline__ uint32_t make_tokens16(const float* h, const Params& P, int g3, int rem,
+                                                  uint32_t* tvs, uint32_t (&lp)[ENC_K / 4], bool& neg1) {
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < ENC_K / 4; q++) lp[q] = 0u;
+#pragma unroll
+    for (int j = 0; j < ENC_K; j++) {
+        int len;
+        uint32_t tv;
+        make_token_bf<CT>(h[3 + j], h[2 + j], h[1 + j], h[j], FAST ? true : j >= g3, P, tv, len);
+        tvs[ENC_TPB * j] = tv;
+        if (CT != 6) neg1 |= h[3 + j] == -1.0f;                              // the reference's sentinel
+        if (!FAST) len = j < rem ? len : 0;                                  // past the end: no token
+        lp[j >> 2] |= (uint32_t)len << (8 * (j & 3));
+        sum += (uint32_t)len;
+    }
+    return sum;
+}
+
+// (6 waves per SIMD asked: the tokens' branch-free selects need ~92 SGPRs of lane masks and 69 VGPRs, which
+// hold 7 workgroups per CU; 8 spilled SGPRs to VGPR lanes and VGPRs to scratch)
+#ifndef DC_FUSED_WAVES
+#define DC_FUSED_WAVES 6
+#endif
+template <int CT>
+__global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
+    const float* __restrict__ x, long long n, long long idx0, Params P, uint32_t* __restrict__ out,
+    uint64_t* __restrict__ st, uint64_t* __restrict__ tl, unsigned ntiles, int start_bit,
+    unsigned long long* __restrict__ total_bits, unsigned long long* __restrict__ total_bits2, uint32_t epoch,
+    unsigned* __restrict__ err) {
+    static_assert(ENC_K == 16 && ENC_TPB == 256, "16 consecutive floats per thread, 4 waves per tile");
+    // sb: first the load transpose (each wave its part), then the tokens (token j of thread t at word
+    // 256 j + t), then the bit buffer
+    __shared__ __attribute__((aligned(16))) uint32_t sb[E3_WORDS];
+    __shared__ uint32_t s_w[4], s_hw[4], s_hi[4], s_tw[4], s_ti[4];
+    __shared__ unsigned long long s_G;
+    __shared__ uint32_t s_tp, s_ok;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t tag = epoch & ST_TAGM;
+    const unsigned tile = blockIdx.x;
+    const long long tbase = (long long)tile * ENC_TILE;
+    const long long base = tbase + (long long)ENC_K * tid;
+    const bool full = tbase + ENC_TILE <= n;
+    // ---- the thread's 16 consecutive floats (transposed through the wave's part of sb in two halves,
+    // rows of 16 + 4 words) and their history: the previous thread's last three (DPP), for lane 0 the
+    // three floats before the wave's first
+    float h[ENC_K + 3];
+    {
+        f32x4 f[ENC_K / 4];
+        load_tile_x(f, x, n, tbase, lane, wid);
+        float* stg = reinterpret_cast<float*>(sb) + wid * E3_STG;
+        f32x4 u[ENC_K / 4];
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                const int m = lane + 64 * q;
+                *reinterpret_cast<f32x4*>(stg + 4 * m + 4 * (m >> 2)) = f[2 * half + q];
+            }
+            __builtin_amdgcn_wave_barrier();
+            if ((lane >> 5) == half)
+#pragma unroll
+                for (int q = 0; q < ENC_K / 4; q++) u[q] = *reinterpret_cast<const f32x4*>(stg + 20 * (lane & 31) + 4 * q);
+            __builtin_amdgcn_wave_barrier();
+        }
+#pragma unroll
+        for (int q = 0; q < ENC_K / 4; q++) {
+            h[3 + 4 * q] = u[q].x; h[4 + 4 * q] = u[q].y; h[5 + 4 * q] = u[q].z; h[6 + 4 * q] = u[q].w;
+        }
+        const long long w0 = tbase + 64ll * ENC_K * wid;                  // the wave's first element
+        float hw[3];
+#pragma unroll
+        for (int k = 1; k <= 3; k++) {
+            const long long e = w0 - k;
+            hw[k - 1] = (e < n && e >= -3 && idx0 + e >= 0) ? x[e] : 0.0f;
+        }
+        h[2] = wave_shr1(h[3 + ENC_K - 1], hw[0]);
+        h[1] = wave_shr1(h[3 + ENC_K - 2], hw[1]);
+        h[0] = wave_shr1(h[3 + ENC_K - 3], hw[2]);
+    }
+    __syncthreads();                                                      // every wave's transpose is done
+    // ---- the tokens, once: values to sb, lengths packed in lp
+    uint32_t lp[ENC_K / 4], mysum;
+    {
+        bool neg1 = false;
+        if (full && idx0 + tbase >= 3) {
+            mysum = make_tokens16<CT, true>(h, P, 0, ENC_K, sb + tid, lp, neg1);
+        } else {
+            const int rem = (int)min(max(n - base, 0ll), (long long)ENC_K);
+            const int g3 = (int)min(max(3 - (idx0 + base), 0ll), (long long)ENC_K);
+#pragma unroll
+            for (int j = 0; j < ENC_K; j++) h[3 + j] = j < rem ? h[3 + j] : 0.0f;
+            mysum = make_tokens16<CT, false>(h, P, g3, rem, sb + tid, lp, neg1);
+        }
+        if (CT != 6 && __any(neg1) && lane == 0) atomicOr(err, 1u);    // -1.0f: the reference's sentinel
+    }
+    // ---- the tile's total and the thread's first bit
+    uint32_t inc = mysum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t u = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += u;
+    }
+    if (lane == 63) s_w[wid] = inc;
+    __syncthreads();
+    uint32_t tv[ENC_K];
+#pragma unroll
+    for (int j = 0; j < ENC_K; j++) tv[j] = sb[ENC_TPB * j + tid];
+    uint32_t wpre = 0, T = 0;
+#pragma unroll
+    for (int w = 0; w < ENC_TPB / 64; w++) {
+        if (w < wid) wpre += s_w[w];
+        T += s_w[w];
+    }
+    // publish the aggregate (tile 0: its inclusive state) and the tile's last 31 bits (the successor's
+    // first word starts with them): the last thread's tokens (>= 48 bits)
+    if (tid == 0)
+        st_relaxed(st + tile, tile == 0 ? st_word(tag, ST_INC, (unsigned long long)start_bit + T) : st_word(tag, ST_AGG, T));
+    if (tid == ENC_TPB - 1 && tile + 1 < ntiles) {
+        uint64_t acc = 0;
+#pragma unroll
+        for (int j = 0; j < ENC_K; j++) acc = (acc << ((lp[j >> 2] >> (8 * (j & 3))) & 0xFFu)) | tv[j];
+        st_relaxed(tl + tile, ((uint64_t)epoch << 32) | ((uint32_t)acc & 0x7FFFFFFFu));
+    }
+    const uint32_t off = wpre + inc - mysum;                              // the thread's first tile bit
+    __syncthreads();                                                      // every thread has its tokens back
+    // ---- pack, MSB-first.  Full tiles: every thread holds >= 48 bits, so a word is shared by at most
+    // two neighbouring threads: each writes the words it completes, its first merged with the previous
+    // lane's unfinished last one (DPP); a wave's first and last words are merged after the barrier
+    if (full) {
+        uint32_t wi = off >> 5, nb = off & 31u, headw = 0u;
+        const uint32_t hi = wi;
+        uint64_t acc = 0;
+        bool have = false;
+#pragma unroll
+        for (int j = 0; j < ENC_K; j++) {
+            const uint32_t len = (lp[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            acc |= (uint64_t)tv[j] << ((64u - nb - len) & 63u);
+            nb += len;
+            if (nb >= 32u) {
+                const uint32_t w = (uint32_t)(acc >> 32);
+                if (have) sb[wi] = w;
+                else headw = w;
+                have = true;
+                wi++;
+                acc <<= 32;
+                nb -= 32u;
+            }
+        }
+        const uint32_t tailw = (uint32_t)(acc >> 32);                     // nb bits (0: none)
+        const uint32_t pt = wave_shr1_u(tailw, 0u);
+        if (lane == 0) { s_hw[wid] = headw; s_hi[wid] = hi; }
+        else sb[hi] = headw | pt;
+        if (lane == 63) { s_tw[wid] = tailw; s_ti[wid] = nb ? wi : 0xFFFFFFFFu; }
+    } else {
+        // the last tile (some threads hold few or no bits): ORed in token by token over a cleared buffer
+        for (int i = tid; i < E3_WORDS / 4; i += ENC_TPB) reinterpret_cast<uint4*>(sb)[i] = make_uint4(0u, 0u, 0u, 0u);
+        __syncthreads();
+        uint32_t o = off;
+#pragma unroll
+        for (int j = 0; j < ENC_K; j++) {
+            const uint32_t lj = (lp[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            if (lj) {
+                const uint64_t v = (uint64_t)tv[j] << ((64u - (o & 31u) - lj) & 63u);
+                atomicOr(&sb[o >> 5], (uint32_t)(v >> 32));
+                if ((o & 31u) + lj > 32u) atomicOr(&sb[(o >> 5) + 1], (uint32_t)v);
+            }
+            o += lj;
+        }
+        if (lane == 0) s_hi[wid] = 0xFFFFFFFFu;
+        if (lane == 63) s_ti[wid] = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    // ---- wave 0: the waves' boundary words, then the look-back for the tile's offset
+    if (wid == 0) {
+        if (lane < 4) {
+            const uint32_t hi = s_hi[lane];
+            if (hi != 0xFFFFFFFFu) {
+                uint32_t w = s_hw[lane];
+                if (lane > 0 && s_ti[lane - 1] == hi) w |= s_tw[lane - 1];
+                sb[hi] = w;
+            }
+            if (lane == 3 && s_ti[3] != 0xFFFFFFFFu) sb[s_ti[3]] = s_tw[3];   // the tile's last word
+        }
+        unsigned long long G = (unsigned long long)start_bit;
+        int bad = tile > 0 ? enc_lookback(st, tile, tag, G) : 0;
+        if (lane == 0) {
+            uint32_t tp = 0;
+            if (tile > 0 && !bad) {                                       // the predecessor's last bits
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                uint64_t v;
+                while (((v = ld_relaxed(tl + tile - 1)) >> 32) != (uint64_t)epoch) {
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > LB_WAIT) { bad = 1; break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                tp = (uint32_t)v;
+            }
+            // (a guard, never taken by a correct encode: a tile's bits end within the stream's capacity,
+            // 32 bits per float after the start bit -- a stale offset must not send the stores outside it)
+            if (!bad && G + T > (unsigned long long)start_bit + 32ull * (unsigned long long)min(n, tbase + ENC_TILE)) bad = 2;
+            if (tile > 0) st_relaxed(st + tile, bad ? st_word(tag, ST_BAD, 0) : st_word(tag, ST_INC, G + T));
+            if (bad) atomicOr(err, bad == 2 ? 2u : 4u);
+            else if (tile == ntiles - 1) {
+                *total_bits = G + T;
+                if (total_bits2) *total_bits2 = G + T;
+            }
+            s_G = G;
+            s_tp = tp;
+            s_ok = bad ? 0u : 1u;
+        }
+    }
+    __syncthreads();
+    if (!s_ok) return;                                                    // no offset: nothing stored
+    // ---- store the words from the one holding the tile's first bit to its last full one
+    const unsigned long long Gt = s_G;
+    const uint32_t tp0 = s_tp;
+    const uint32_t sh = (uint32_t)(Gt & 31ull);
+    const long long W0 = (long long)(Gt >> 5);
+    const int nw = (int)((long long)((Gt + T) >> 5) - W0) + ((tile == ntiles - 1 && ((Gt + T) & 31ull)) ? 1 : 0);
+    const int tw = (int)((T + 31u) >> 5);                                  // buffer words holding tile bits
+    for (int i = tid; i < nw; i += ENC_TPB) {
+        const uint32_t cur = i < tw ? sb[i] : 0u;                          // (stale past the tile's bits)
+        const uint32_t prev = i ? sb[i - 1] : tp0;
+        const uint32_t w = sh ? __builtin_amdgcn_alignbit(prev, cur, sh) : cur;
+#if DC_PACK_NT
+        __builtin_nontemporal_store(__builtin_bswap32(w), out + W0 + i);
+#else
+        out[W0 + i] = __builtin_bswap32(w);
+#endif
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 #define DC_ENC_DISPATCH(KER, ...)                                                                  \
     switch (P->ct) {                                                                               \
         case 5: hipLaunchKernelGGL(KER<5>, __VA_ARGS__); break;                                    \
@@ -610,12 +941,40 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
         default: return -2;                                                                        \
     }
 
+static long long desc_words_multi(long long nt);
+static int g_enc_mode_last = 0;
+// encoder variant: 1 = single pass (default), 2 = count + pack (the pack's workgroup 0 scans the tile
+// counts, the other tiles wait for its flag), 3 = count + scan launch + pack (no wait anywhere: the
+// fallback after a single-pass timeout).  DC_ENC_PASSES=2|3 selects the others.
+static int enc_mode_default(void) {
+    static int m = 0;
+    if (!m) {
+        const char* e = getenv("DC_ENC_PASSES");
+        m = (e && (atoi(e) == 2 || atoi(e) == 3)) ? atoi(e) : 1;
+    }
+    return m;
+}
+extern "C" int dc_encode_mode(void) { return g_enc_mode_last; }
+
+// mode 0: the default variant.  desc (dc_encode_desc_words): single pass -- tile states (u64) | tail
+// granules (u64); two/three launches -- tile offsets (u64) | tile bit counts (u32) | tile tails (u32) |
+// per-thread bit counts (u16)
 extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, const Params* P,
                                 uint32_t* out, uint64_t* desc, unsigned* flag, uint32_t epoch, int start_bit, unsigned long long* total_bits, unsigned long long* total_bits2,
-                                unsigned* err, unsigned long long* dbg, hipStream_t stream) {
+                                unsigned* err, unsigned long long* dbg, int mode, hipStream_t stream) {
     if (n <= 0) return 0;
+    if (mode == 0) mode = enc_mode_default();
+    g_enc_mode_last = mode;
     const unsigned ntiles = (unsigned)((n + ENC_TILE - 1) / ENC_TILE);
-    // desc: tile offsets (u64) | tile bit counts (u32) | tile tails (u32)
+    if (mode == 1) {
+        const int grid = (int)ntiles;
+        dc_mark_phase(0, stream);
+        uint64_t* st = desc + desc_words_multi(ntiles);
+        DC_ENC_DISPATCH(encode_fused_kernel, dim3(grid), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, st,
+                        st + ntiles, ntiles, start_bit, total_bits, total_bits2, epoch, err);
+        dc_mark_phase(1, stream);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     uint32_t* tbits = reinterpret_cast<uint32_t*>(desc + ntiles);
     uint32_t* tails = tbits + ntiles + (ntiles & 1u);
     uint16_t* psum16 = reinterpret_cast<uint16_t*>(tails + ntiles + (ntiles & 1u));
@@ -623,6 +982,11 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
     DC_ENC_DISPATCH(encode_count_kernel, dim3(ntiles), dim3(256), 0, stream, x, n, idx0, *P, tbits,
                     (long long)ntiles, err, tails, psum16);
     dc_mark_phase(1, stream);                   // (no mark 2: the pack's slot starts at mark 1)
+    if (mode == 3) {
+        hipLaunchKernelGGL(encode_scan_kernel, dim3(1), dim3(1024), 0, stream, tbits, desc, (long long)ntiles, start_bit,
+                           total_bits, total_bits2);
+        flag = nullptr;
+    }
     DC_ENC_DISPATCH(encode_pack_kernel, dim3(ntiles), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, desc, tbits,
                     tails, psum16, ntiles, start_bit, total_bits, total_bits2, flag, epoch, err, dbg);
     dc_mark_phase(3, stream);
@@ -647,9 +1011,16 @@ extern "C" long long dc_encode_tile_count(long long n) { return (n + ENC_TILE - 
 
 // u64 words of the encode descriptor buffer: tile offsets + 32-bit tile counts + 32-bit tile tails +
 // 16-bit per-thread counts of the pack kernel
-extern "C" long long dc_encode_desc_words(long long n) {
-    const long long nt = dc_encode_tile_count(n);
+// + the single pass's 2 words per tile (states, tail granules) in a region of their own, which the other
+// variants and dc_launch_encode_bits never write (their counts could read as a live tag)
+static long long desc_words_multi(long long nt) {
     return nt + (nt + 1) / 2 + (nt + 1) / 2 + 1 + nt * (ENC_TPB / 4);     // offsets, counts, tails, thread counts
 }
+extern "C" long long dc_encode_desc_words(long long n) {
+    const long long nt = dc_encode_tile_count(n);
+    return desc_words_multi(nt) + 2 * nt;
+}
+// the epochs a state tag tells apart: the host clears desc when its encode epoch reaches this
+extern "C" unsigned dc_encode_epoch_limit(void) { return ST_TAGM; }
 
 }  // namespace dc

@@ -44,6 +44,11 @@ typedef struct {
     unsigned* d_enc_err;
     unsigned* d_enc_flag;            /* the pack kernel's scan-published flag (encode epoch) */
     uint32_t enc_epoch;
+    struct {                         /* the last encode's launch, re-run wait-free after a look-back timeout */
+        const float* x; long long n, idx0; Params P; uint32_t* out; int start_bit;
+        unsigned long long* tot; hipStream_t st; int valid;
+    } last_enc;
+    int enc_retries;                 /* encodes re-run wait-free (dc_encode_retries) */
     /* decoder */
     DecBufs D;
     void* dec_pool;
@@ -376,11 +381,19 @@ static int encode_on(hipStream_t st, int ct, const void* d_x, long long n, long 
         HIPCHK(hipMalloc((void**)&G.enc_dbg, 8192 * 8 * 8));
         HIPCHK(hipMemset(G.enc_dbg, 0, 8192 * 8 * 8));
     }
-    /* the kernel writes the total to both (no copy node per encode) */
-    if (++G.enc_epoch == 0) G.enc_epoch = 1;      /* (the flag starts at 0: never a live epoch) */
+    /* the kernel writes the total to both (no copy node per encode).  Epochs tag the tile states and flags:
+       when they wrap, every old tag is cleared (a state of an old encode must never read as published) */
+    if (++G.enc_epoch >= dc_encode_epoch_limit() || G.enc_epoch == 1) {
+        HIPCHK(hipMemsetAsync(G.enc_desc, 0, (size_t)G.enc_desc_cap * sizeof(uint64_t), st));
+        HIPCHK(hipMemsetAsync(G.d_enc_flag, 0, 4096, st));
+        G.enc_epoch = 1;
+    }
     if (dc_launch_encode((const float*)d_x, n, idx0, &P, (uint32_t*)d_out, G.enc_desc, G.d_enc_flag, G.enc_epoch,
-                         start_bit, tot, tot != G.d_total ? G.d_total : NULL, G.d_enc_err, G.enc_dbg, st))
+                         start_bit, tot, tot != G.d_total ? G.d_total : NULL, G.d_enc_err, G.enc_dbg, 0, st))
         return seterr(DC_ERR_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
+    G.last_enc.x = (const float*)d_x; G.last_enc.n = n; G.last_enc.idx0 = idx0; G.last_enc.P = P;
+    G.last_enc.out = (uint32_t*)d_out; G.last_enc.start_bit = start_bit; G.last_enc.tot = tot; G.last_enc.st = st;
+    G.last_enc.valid = 1;
     return DC_OK;
 }
 
@@ -417,6 +430,36 @@ int dc_encode_bits_device(int ct, const void* d_x, long long n, long long idx0, 
     return DC_OK;
 }
 
+/* re-run the last encode with no wait between workgroups (count, scan launch, pack) */
+static int encode_retry(hipStream_t st) {
+    HIPCHK(hipMemsetAsync(G.d_enc_err, 0, 4, st));
+    if (++G.enc_epoch >= dc_encode_epoch_limit()) {
+        HIPCHK(hipMemsetAsync(G.enc_desc, 0, (size_t)G.enc_desc_cap * sizeof(uint64_t), st));
+        HIPCHK(hipMemsetAsync(G.d_enc_flag, 0, 4096, st));
+        G.enc_epoch = 1;
+    }
+    unsigned long long* tot = G.last_enc.tot;
+    if (dc_launch_encode(G.last_enc.x, G.last_enc.n, G.last_enc.idx0, &G.last_enc.P, G.last_enc.out, G.enc_desc,
+                         G.d_enc_flag, G.enc_epoch, G.last_enc.start_bit, tot, tot != G.d_total ? G.d_total : NULL,
+                         G.d_enc_err, NULL, 3, st))
+        return seterr(DC_ERR_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
+    G.enc_retries++;
+    return DC_OK;
+}
+int dc_encode_retries(void) { return G.enc_retries; }
+
+/* the encoder's error word as the kernels left it (synchronous; nothing cleared, nothing re-run): bit 0 the
+   -1.0f sentinel in the input, 2 a tile offset outside the stream, 4 a look-back / flag wait timed out */
+int dc_encode_status(unsigned* status_out) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    hipStream_t st = G.last_enc_st ? G.last_enc_st : G.st;
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[1], G.d_enc_err, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    *status_out = (unsigned)(G.h_scratch[1] & 0xFFFFFFFFu);
+    return DC_OK;
+}
+
 int dc_encode_result(unsigned long long* total_bits) {
     int rc = ensure_init();
     if (rc) return rc;
@@ -425,6 +468,16 @@ int dc_encode_result(unsigned long long* total_bits) {
     HIPCHK(hipMemcpyAsync(&G.h_scratch[1], G.d_enc_err, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     unsigned err = (unsigned)(G.h_scratch[1] & 0xFFFFFFFFu);
+    if ((err & 4u) && !(err & 1u) && G.last_enc.valid) {
+        /* a single-pass tile waited past its bound for a predecessor (a workgroup not resident: another
+           process on the GPU) and stored nothing: encode again with the wait-free three-launch variant */
+        const int ok = encode_retry(st);
+        if (ok) return ok;
+        HIPCHK(hipMemcpyAsync(&G.h_scratch[0], G.d_total, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(&G.h_scratch[1], G.d_enc_err, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        err = (unsigned)(G.h_scratch[1] & 0xFFFFFFFFu);
+    }
     if (err) {
         HIPCHK(hipMemsetAsync(G.d_enc_err, 0, 4, st));
         if (err & 1u)

@@ -45,6 +45,7 @@ EXT_SYMBOLS = [
     "dc64_last_decode_flags", "dc64_to_small_device", "dc64_med_device", "dc_set_encode_stream",
     "dc_decode_status", "dc_abi_status", "dc_med_sum_device", "dc_type_from_max", "dc_set_small_chunk_max_bytes",
     "dc_set_decode3_min_bytes", "dc_last_decode_was_v3", "dc_last_decode_launched_v3",
+    "dc_encode_status", "dc_encode_mode", "dc_encode_retries",
 ]
 
 
@@ -358,6 +359,11 @@ class Lib:
     def encode_bits(self, ct, x_ptr, n, idx0=0, type_=0, mask17=0):
         v = C.c_ulonglong(0)
         self.check(self.L.dc_encode_bits_device(ct, x_ptr, n, idx0, type_, mask17, C.byref(v)), "dc_encode_bits_device")
+        return v.value
+
+    def encode_status(self):
+        v = C.c_uint(0)
+        self.check(self.L.dc_encode_status(C.byref(v)), "dc_encode_status")
         return v.value
 
     def encode_result(self):

@@ -56,6 +56,13 @@ int dc_encode_bits_device(int ct, const void* d_x, long long n, long long idx0, 
                           unsigned long long* bits_out);
 /* Wait for the last encode and return start_bit + bits written (host value). */
 int dc_encode_result(unsigned long long* total_bits);
+/* the encoder's error word, read as is (bit 0: a -1.0f input; 2: an offset outside the stream; 4: a
+   single-pass look-back timed out -- dc_encode_result then re-encodes wait-free); synchronous */
+int dc_encode_status(unsigned* status_out);
+/* encoder variant of the last encode: 1 single pass, 2 count + pack, 3 count + scan + pack */
+int dc_encode_mode(void);
+/* encodes re-run wait-free after a look-back timeout (process lifetime) */
+int dc_encode_retries(void);
 
 /* Decode num floats from a device stream of nbytes bytes (nbytes < 0: take the length in bits
  * from *d_nbits, device memory, e.g. the d_total_bits of a preceding dc_encode_device).
