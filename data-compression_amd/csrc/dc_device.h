@@ -104,6 +104,85 @@ __device__ __forceinline__ void make_token_bf(float x, float b1, float b2, float
     len = l;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Encoder token table (per workgroup, LDS, 1 KB): a raw token's length and bit extraction depend only on
+// the float's top 9 bits (sign + exponent), so tab[u >> 23] = sh | len << 8 gives v = u >> sh (the top
+// len = 9 + m bits) and len (for CT7's masked exponent len = lm1, the flag-1 length; sh stays 32 - (9 + mm)).
+// A CT7 masked token is v ^ K1 (flag 1) or v ^ K0 with length lm0 (flag 0: (u >> 15) == mask17).  The same
+// tokens as make_token / make_token_bf with ~10 fewer VALU per float.
+template <int CT>
+__device__ __forceinline__ void build_enc_tab(uint16_t* tab, const Params& P, int tid, int nthr) {
+    for (int i = tid; i < 512; i += nthr) {
+        const int l9 = min(max((i & 0xFF) + P.rawadd, 9), 32);   // the bits v keeps: 9 + m
+        const int len = (CT == 7 && (uint32_t)i == (P.mask17 >> 8)) ? P.lm1 : l9;
+        tab[i] = (uint16_t)((uint32_t)(32 - l9) | ((uint32_t)len << 8));
+    }
+}
+
+// a token from the table; b1..b3 the ORIGINAL previous inputs.  The predicted code ('101'/'110'/'111') is
+// chosen under a wave-uniform branch, when some lane predicts (rare in ordinary data).
+template <int CT>
+__device__ __forceinline__ void make_token_t(float x, float b1, float b2, float b3, bool predict, const Params& P,
+                                             const uint16_t* tab, uint32_t& val, int& len) {
+    const uint32_t u = __float_as_uint(x);
+    uint32_t v;
+    int l;
+    if (CT == 11) {
+        v = u; l = 32;
+    } else {
+        const uint32_t i9 = u >> 23;
+        const uint32_t e = tab[i9];
+        v = u >> (e & 31u);
+        l = (int)(e >> 8);
+        if (CT == 7) {
+            const bool f0 = (u >> 15) == P.mask17;
+            v ^= f0 ? P.K0 : (i9 == (P.mask17 >> 8) ? P.K1 : 0u);
+            l = f0 ? P.lm0 : l;
+        }
+    }
+    if (CT != 6) {
+        const float p2 = __fsub_rn(__fmul_rn(2.0f, b1), b2);
+        const float p3 = __fadd_rn(__fsub_rn(__fmul_rn(3.0f, b1), __fmul_rn(3.0f, b2)), b3);
+        const float d1 = fabsf(__fsub_rn(b1, x));
+        const float d2 = fabsf(__fsub_rn(p2, x));
+        const float d3 = fabsf(__fsub_rn(p3, x));
+        const bool pr = predict && d1 == d1 && fminf(fminf(d1, d2), d3) <= P.thr_le;
+        const bool z = fabsf(x) <= P.thr_lt;
+        if (__builtin_expect(__any(pr), 0)) {
+            const float d12 = fminf(d1, d2);
+            const uint32_t code = d3 < d12 ? 7u : (d2 < d1 ? 6u : 5u);
+            v = pr ? code : v;
+        }
+        v = z ? 4u : v;
+        l = (pr || z) ? 3 : l;
+    }
+    val = v;
+    len = l;
+}
+
+// the length only (count pass)
+template <int CT>
+__device__ __forceinline__ int token_len_t(float x, float b1, float b2, float b3, bool predict, const Params& P,
+                                           const uint16_t* tab) {
+    const uint32_t u = __float_as_uint(x);
+    int l;
+    if (CT == 11) {
+        l = 32;
+    } else {
+        l = (int)((uint32_t)tab[u >> 23] >> 8);
+        if (CT == 7) l = (u >> 15) == P.mask17 ? P.lm0 : l;
+    }
+    if (CT != 6) {
+        const float p2 = __fsub_rn(__fmul_rn(2.0f, b1), b2);
+        const float p3 = __fadd_rn(__fsub_rn(__fmul_rn(3.0f, b1), __fmul_rn(3.0f, b2)), b3);
+        const float d1 = fabsf(__fsub_rn(b1, x));
+        const float dmin = fminf(fminf(d1, fabsf(__fsub_rn(p2, x))), fabsf(__fsub_rn(p3, x)));
+        const bool pr = predict && d1 == d1 && dmin <= P.thr_le;
+        l = (pr || fabsf(x) <= P.thr_lt) ? 3 : l;
+    }
+    return l;
+}
+
 // Encoder: token LENGTH only (count pass).  Same decision as make_token_bf: the predicted code is
 // the first strict minimum of (d1, d2, d3), so "some prediction within threshold" is
 // min(d1, d2, d3) <= thr_le, where a NaN d1 keeps dmin = NaN (never predicts) and NaN d2 / d3 are

@@ -53,7 +53,7 @@ __device__ __forceinline__ float lane63(float v) { return __int_as_float(__built
 // lane 0's first element)
 template <int CT>
 __device__ __forceinline__ void count_tokens(const float4* f, float h1, float h2, float h3, const Params& P,
-                                             uint32_t* qsum, bool& neg1) {
+                                             const uint16_t* tab, uint32_t* qsum, bool& neg1) {
 #pragma unroll
     for (int q = 0; q < CNT_Q; q++) {
         const float b1 = wave_shr1(f[q].w, h1), b2 = wave_shr1(f[q].z, h2), b3 = wave_shr1(f[q].y, h3);
@@ -62,7 +62,7 @@ __device__ __forceinline__ void count_tokens(const float4* f, float h1, float h2
         qsum[q] = 0u;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-            qsum[q] += (uint32_t)token_len_enc<CT>(xs[3 + r], xs[2 + r], xs[1 + r], xs[r], true, P);
+            qsum[q] += (uint32_t)token_len_t<CT>(xs[3 + r], xs[2 + r], xs[1 + r], xs[r], true, P, tab);
             neg1 |= xs[3 + r] == -1.0f;
         }
     }
@@ -100,11 +100,11 @@ __device__ __forceinline__ void load_part(const float* __restrict__ x, long long
 // bit count of one tile part from its loaded floats; lane 0 corrects the padding and head elements
 template <int CT>
 __device__ __forceinline__ void count_part(const float* __restrict__ x, long long n, long long idx0, const Params& P,
-                                           long long h, const float4* f, const float* hist, int lane,
+                                           const uint16_t* tab, long long h, const float4* f, const float* hist, int lane,
                                            uint32_t* psum, unsigned* __restrict__ err, uint32_t* qsum) {
     const long long tb = h * CNT_SUB;
     bool neg1 = false;
-    count_tokens<CT>(f, hist[0], hist[1], hist[2], P, qsum, neg1);
+    count_tokens<CT>(f, hist[0], hist[1], hist[2], P, tab, qsum, neg1);
     uint32_t sum = 0;
 #pragma unroll
     for (int q = 0; q < CNT_Q; q++) sum += qsum[q];
@@ -115,13 +115,13 @@ __device__ __forceinline__ void count_part(const float* __restrict__ x, long lon
         if (tb + CNT_SUB > n) {                                      // the 0.0f padding's tokens
             const int rem = (int)max(n - tb, 0ll);                   // 0: a part past the end
             vend = rem & ~3;
-            sum -= (uint32_t)token_len_enc<CT>(0.0f, 0.0f, 0.0f, 0.0f, true, P) * (uint32_t)(CNT_SUB - vend);
+            sum -= (uint32_t)token_len_t<CT>(0.0f, 0.0f, 0.0f, 0.0f, true, P, tab) * (uint32_t)(CNT_SUB - vend);
             for (int j = vend; j < rem; j++) {                       // the straddling float4
                 const long long e = tb + j;
                 const float v = x[e];
                 neg1 |= v == -1.0f;
-                sum += (uint32_t)token_len_enc<CT>(v, halo_x(x, idx0, e - 1), halo_x(x, idx0, e - 2),
-                                                   halo_x(x, idx0, e - 3), idx0 + e >= 3, P);
+                sum += (uint32_t)token_len_t<CT>(v, halo_x(x, idx0, e - 1), halo_x(x, idx0, e - 2),
+                                                 halo_x(x, idx0, e - 3), idx0 + e >= 3, P, tab);
             }
         }
         if (CT != 6) {                                               // unpredicted head elements
@@ -129,7 +129,7 @@ __device__ __forceinline__ void count_part(const float* __restrict__ x, long lon
                 const long long e = tb + j;
                 const float v = x[e], b1 = halo_x(x, idx0, e - 1), b2 = halo_x(x, idx0, e - 2),
                             b3 = halo_x(x, idx0, e - 3);
-                sum += (uint32_t)(token_len_enc<CT>(v, b1, b2, b3, false, P) - token_len_enc<CT>(v, b1, b2, b3, true, P));
+                sum += (uint32_t)(token_len_t<CT>(v, b1, b2, b3, false, P, tab) - token_len_t<CT>(v, b1, b2, b3, true, P, tab));
             }
         }
     }
@@ -145,13 +145,16 @@ __global__ __launch_bounds__(256) void encode_count_kernel(const float* __restri
                                                            uint16_t* __restrict__ psum16) {
     static_assert(CNT_PARTS == 4, "one workgroup of four waves per tile");
     __shared__ uint32_t wsum[4];
+    __shared__ uint16_t tab[512];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const long long h = (long long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(wid);
     float4 f[CNT_Q];
     float hist[3];
     uint32_t qsum[CNT_Q];
     load_part(x, n, idx0, h * CNT_SUB, lane, f, hist);
-    count_part<CT>(x, n, idx0, P, h, f, hist, lane, wsum + wid, err, qsum);
+    build_enc_tab<CT>(tab, P, threadIdx.x, 256);
+    __syncthreads();
+    count_part<CT>(x, n, idx0, P, tab, h, f, hist, lane, wsum + wid, err, qsum);
     // the bit counts of the pack kernel's threads (16 consecutive floats = float4s 4k..4k+3 of a row q:
     // a lane quad), for the tiles it packs without counting (whole, every float predicted)
     const long long tb0 = (long long)blockIdx.x * ENC_TILE;
@@ -177,7 +180,7 @@ __global__ __launch_bounds__(256) void encode_count_kernel(const float* __restri
             for (int r = 0; r < 4; r++) {
                 uint32_t tv;
                 int len;
-                make_token_bf<CT>(xs[3 + r], xs[2 + r], xs[1 + r], xs[r], true, P, tv, len);
+                make_token_t<CT>(xs[3 + r], xs[2 + r], xs[1 + r], xs[r], true, P, tab, tv, len);
                 acc = (acc << len) | tv;
                 L += (uint32_t)len;
             }
@@ -399,8 +402,10 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
     __shared__ __attribute__((aligned(16))) uint32_t sb[E3_LDS];
     __shared__ uint32_t s_w[ENC_TPB / 64];
     __shared__ uint32_t s_hw[4], s_hi[4], s_tw[4], s_ti[4];           // the waves' first and last words
+    __shared__ uint16_t tab[512];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const unsigned tile = blockIdx.x;
+    build_enc_tab<CT>(tab, P, tid, ENC_TPB);                          // (read after the barrier below)
     // (flag == nullptr: the offsets come from encode_scan_kernel, launched before -- the wait-free fallback)
     if (tile == 0 && flag) pack_scan_block(tcnt, toff, ntiles, start_bit, total_bits, total_bits2, sb, s_w, flag, epoch);
     const uint32_t tp0 = tile > 0 ? tails[tile - 1] : 0u;
@@ -478,7 +483,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
 #pragma unroll
         for (int j = 0; j < ENC_K; j++) {
             const bool in = base + j < n;
-            int len = token_len_enc<CT>(h[3 + j], h[2 + j], h[1 + j], h[j], idx0 + base + j >= 3, P);
+            int len = token_len_t<CT>(h[3 + j], h[2 + j], h[1 + j], h[j], idx0 + base + j >= 3, P, tab);
             len = in ? len : 0;
             lp[j >> 2] |= (uint32_t)len << (8 * (j & 3));
             mysum += (uint32_t)len;
@@ -518,7 +523,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
         for (int j = 0; j < ENC_K; j++) {
             uint32_t tv;
             int len;
-            make_token_bf<CT>(h[3 + j], h[2 + j], h[1 + j], h[j], true, P, tv, len);
+            make_token_t<CT>(h[3 + j], h[2 + j], h[1 + j], h[j], true, P, tab, tv, len);
             acc |= (uint64_t)tv << ((64u - nb - (uint32_t)len) & 63u);
             nb += (uint32_t)len;
             if (nb >= 32u) {
@@ -546,7 +551,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
             const uint32_t lj = (lp[j >> 2] >> (8 * (j & 3))) & 0xFFu;
             uint32_t tv;
             int len;
-            make_token_bf<CT>(h[3 + j], h[2 + j], h[1 + j], h[j], idx0 + base + j >= 3, P, tv, len);
+            make_token_t<CT>(h[3 + j], h[2 + j], h[1 + j], h[j], idx0 + base + j >= 3, P, tab, tv, len);
             if (lj) {
                 const uint64_t v = (uint64_t)tv << ((64u - (o & 31u) - lj) & 63u);
                 atomicOr(&sb[o >> 5], (uint32_t)(v >> 32));
@@ -629,7 +634,13 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
 // encode never matches the tag (the host clears the array when the epoch wraps).  Every wait is bounded:
 // a look-back that times out poisons its tile (status 3, successors give up at once), stores nothing and
 // sets err bit 4; the host then re-encodes with the wait-free three-launch path (dc_encode_result).
-constexpr int LB_K = 8;                                           // look-back: tiles per lane per round trip
+#ifndef DC_LB_K
+#define DC_LB_K 8
+#endif
+#ifndef DC_LB_SLEEP
+#define DC_LB_SLEEP 1
+#endif
+constexpr int LB_K = DC_LB_K;                                     // look-back: tiles per lane per round trip
 constexpr unsigned long long ST_VAL = (1ull << 40) - 1;
 constexpr unsigned long long ST_MASK = 3ull << 40, ST_AGG = 1ull << 40, ST_INC = 2ull << 40, ST_BAD = 3ull << 40;
 constexpr uint32_t ST_TAGM = (1u << 22) - 1;
@@ -644,62 +655,77 @@ __device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
     return v;
 }
 
-// exclusive bit offset of tile t >= 1 (one whole wave; wave-uniform result).  Lane l inspects tiles
-// base - 8l - 7 .. base - 8l of the window [base - 511, base], all loads in flight at once; every state from
-// tile t - 1 down to the nearest INCLUSIVE one must be published (else the window is re-read), and their
-// values summed.  A window without an inclusive state adds its 512 aggregates and the next one is read.
-// Returns 0, or 1 when a needed state is poisoned or the wait timed out.
+// exclusive bit offset of tile t >= 1 (one whole wave; wave-uniform result).  Position p = 64 k + l of the
+// window [base - 64 LB_K + 1, base] (tile base - p) is lane l's k-th state, so each of the LB_K loads reads
+// 512 contiguous bytes (a strided layout, 64 segments per load, made the look-back traffic exceed the
+// codec's); every load is in flight at once.  The states from tile t - 1 down to the nearest INCLUSIVE one
+// must all be published.  While one is not, ONE lane polls that state (a whole window re-read per poll by
+// ~1800 waiting tiles tripled the encode), then the window is read again.  A window without an inclusive
+// state adds its aggregates and the next one is read.  Returns 0, or 1 when a needed state is poisoned or a
+// wait timed out.
 __device__ __forceinline__ int enc_lookback(const uint64_t* __restrict__ st, long long t, uint32_t tag,
-                                            unsigned long long& excl) {
+                                            unsigned long long& excl, uint32_t& stat) {
     const int lane = threadIdx.x & 63;
     long long base = t - 1;
     excl = 0;
     const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         uint64_t v[LB_K];
-        int kneed, kinc;
+        int pinc;                                                         // first inclusive position (64 LB_K: none)
         for (;;) {
 #pragma unroll
             for (int k = 0; k < LB_K; k++) {
-                const long long ti = base - (long long)(lane * LB_K + k);
+                const long long ti = base - (long long)(64 * k + lane);
                 const uint64_t w = ld_relaxed(st + (ti >= 0 ? ti : 0));
                 v[k] = ti >= 0 ? w : st_word(tag, ST_INC, 0);           // (before tile 0: offset 0)
             }
-            kinc = LB_K;
-            int kinv = LB_K;
+            pinc = 64 * LB_K;
+            int pinv = 64 * LB_K;                                         // first unpublished position
 #pragma unroll
             for (int k = LB_K - 1; k >= 0; k--) {
                 const bool live = (uint32_t)(v[k] >> 42) == tag && (v[k] & ST_MASK) != 0;
-                if (!live) kinv = k;
-                else if ((v[k] & ST_MASK) != ST_AGG) kinc = k;           // inclusive (or poisoned): stop there
+                const unsigned long long um = __ballot(!live);
+                const unsigned long long im = __ballot(live && (v[k] & ST_MASK) != ST_AGG);   // inclusive / poisoned
+                if (um) pinv = 64 * k + __ffsll((long long)um) - 1;
+                if (im) pinc = 64 * k + __ffsll((long long)im) - 1;
             }
-            const unsigned long long im = __ballot(kinc < LB_K);
-            const int li = im ? __ffsll((long long)im) - 1 : 64;
-            kneed = lane < li ? LB_K : (lane == li ? kinc + 1 : 0);
-            if (!__any(kinv < kneed)) break;
+            if (pinv > pinc) break;                                       // every needed state is published
+            stat++;
+            if (lane == (pinv & 63)) {                                    // its lane polls it alone
+                const long long ti = base - pinv;
+                for (;;) {
+                    const uint64_t w = ld_relaxed(st + ti);
+                    if ((uint32_t)(w >> 42) == tag && (w & ST_MASK) != 0) break;
+                    if (__builtin_amdgcn_s_memrealtime() - w0 > LB_WAIT) break;
+                    stat += 1u << 16;
+                    __builtin_amdgcn_s_sleep(DC_LB_SLEEP);
+                }
+            }
             if (__builtin_amdgcn_s_memrealtime() - w0 > LB_WAIT) return 1;
-            __builtin_amdgcn_s_sleep(1);
         }
         unsigned long long s = 0;
         bool bad = false;
 #pragma unroll
         for (int k = 0; k < LB_K; k++) {
-            if (k < kneed) {
+            if (64 * k + lane <= pinc) {
                 s += v[k] & ST_VAL;
                 bad |= (v[k] & ST_MASK) == ST_BAD;
             }
         }
         if (__any(bad)) return 1;
         excl += wave_sum64(s);
-        if (__any(kinc < LB_K)) return 0;
+        if (pinc < 64 * LB_K) return 0;
         base -= 64 * LB_K;
     }
 }
 
+#ifndef DC_TOK_SB
+#define DC_TOK_SB 0                     // (experiments: tokens the scheduler may interleave)
+#endif
 // the 16 tokens of a thread: values to tvs[256 j], lengths packed 4 per word in lp, their sum.  Not FAST: the
 // thread's elements j >= rem are past the end (no token), those j < g3 precede global index 3 (no prediction)
 template <int CT, bool FAST>
-__device__ __forceinline__ uint32_t make_tokens16(const float* h, const Params& P, int g3, int rem,
+__device__ __forceinline__ uint32_t make_tokens16(const float* h, const Params& P, const uint16_t* tab, int g3, int rem,
                                                   uint32_t* tvs, uint32_t (&lp)[ENC_K / 4], bool& neg1) {
     uint32_t sum = 0;
 #pragma unroll
@@ -708,12 +734,15 @@ __device__ __forceinline__ uint32_t make_tokens16(const float* h, const Params& 
     for (int j = 0; j < ENC_K; j++) {
         int len;
         uint32_t tv;
-        make_token_bf<CT>(h[3 + j], h[2 + j], h[1 + j], h[j], FAST ? true : j >= g3, P, tv, len);
+        make_token_t<CT>(h[3 + j], h[2 + j], h[1 + j], h[j], FAST ? true : j >= g3, P, tab, tv, len);
         tvs[ENC_TPB * j] = tv;
         if (CT != 6) neg1 |= h[3 + j] == -1.0f;                              // the reference's sentinel
         if (!FAST) len = j < rem ? len : 0;                                  // past the end: no token
         lp[j >> 2] |= (uint32_t)len << (8 * (j & 3));
         sum += (uint32_t)len;
+#if DC_TOK_SB
+        if ((j % DC_TOK_SB) == DC_TOK_SB - 1) __builtin_amdgcn_sched_barrier(0);
+#endif
     }
     return sum;
 }
@@ -728,17 +757,22 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
     const float* __restrict__ x, long long n, long long idx0, Params P, uint32_t* __restrict__ out,
     uint64_t* __restrict__ st, uint64_t* __restrict__ tl, unsigned ntiles, int start_bit,
     unsigned long long* __restrict__ total_bits, unsigned long long* __restrict__ total_bits2, uint32_t epoch,
-    unsigned* __restrict__ err) {
+    unsigned* __restrict__ err, unsigned long long* __restrict__ dbg) {
     static_assert(ENC_K == 16 && ENC_TPB == 256, "16 consecutive floats per thread, 4 waves per tile");
+    // (DC_DEBUG_STAMPS: phase stamps of the first 16384 tiles, s_memrealtime)
+#define E1STAMP(ph) do { if (dbg && threadIdx.x == 0 && blockIdx.x < 16384) dbg[blockIdx.x * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+    E1STAMP(0);
     // sb: first the load transpose (each wave its part), then the tokens (token j of thread t at word
     // 256 j + t), then the bit buffer
     __shared__ __attribute__((aligned(16))) uint32_t sb[E3_WORDS];
     __shared__ uint32_t s_w[4], s_hw[4], s_hi[4], s_tw[4], s_ti[4];
     __shared__ unsigned long long s_G;
     __shared__ uint32_t s_tp, s_ok;
+    __shared__ uint16_t tab[512];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t tag = epoch & ST_TAGM;
     const unsigned tile = blockIdx.x;
+    build_enc_tab<CT>(tab, P, tid, ENC_TPB);                          // (read after the barrier below)
     const long long tbase = (long long)tile * ENC_TILE;
     const long long base = tbase + (long long)ENC_K * tid;
     const bool full = tbase + ENC_TILE <= n;
@@ -785,17 +819,18 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
     {
         bool neg1 = false;
         if (full && idx0 + tbase >= 3) {
-            mysum = make_tokens16<CT, true>(h, P, 0, ENC_K, sb + tid, lp, neg1);
+            mysum = make_tokens16<CT, true>(h, P, tab, 0, ENC_K, sb + tid, lp, neg1);
         } else {
             const int rem = (int)min(max(n - base, 0ll), (long long)ENC_K);
             const int g3 = (int)min(max(3 - (idx0 + base), 0ll), (long long)ENC_K);
 #pragma unroll
             for (int j = 0; j < ENC_K; j++) h[3 + j] = j < rem ? h[3 + j] : 0.0f;
-            mysum = make_tokens16<CT, false>(h, P, g3, rem, sb + tid, lp, neg1);
+            mysum = make_tokens16<CT, false>(h, P, tab, g3, rem, sb + tid, lp, neg1);
         }
         if (CT != 6 && __any(neg1) && lane == 0) atomicOr(err, 1u);    // -1.0f: the reference's sentinel
     }
     // ---- the tile's total and the thread's first bit
+    E1STAMP(1);
     uint32_t inc = mysum;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -804,6 +839,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
     }
     if (lane == 63) s_w[wid] = inc;
     __syncthreads();
+    E1STAMP(2);
     uint32_t tv[ENC_K];
 #pragma unroll
     for (int j = 0; j < ENC_K; j++) tv[j] = sb[ENC_TPB * j + tid];
@@ -884,7 +920,10 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
             if (lane == 3 && s_ti[3] != 0xFFFFFFFFu) sb[s_ti[3]] = s_tw[3];   // the tile's last word
         }
         unsigned long long G = (unsigned long long)start_bit;
-        int bad = tile > 0 ? enc_lookback(st, tile, tag, G) : 0;
+        uint32_t lbst = 0;
+        E1STAMP(3);
+        int bad = tile > 0 ? enc_lookback(st, tile, tag, G, lbst) : 0;
+        E1STAMP(4);
         if (lane == 0) {
             uint32_t tp = 0;
             if (tile > 0 && !bad) {                                       // the predecessor's last bits
@@ -908,6 +947,10 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
             s_G = G;
             s_tp = tp;
             s_ok = bad ? 0u : 1u;
+            if (dbg && tile < 16384) {
+                dbg[tile * 8 + 6] = lbst;
+                dbg[tile * 8 + 7] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & 7u;   // HW_REG_XCC_ID
+            }
         }
     }
     __syncthreads();
@@ -929,6 +972,8 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
         out[W0 + i] = __builtin_bswap32(w);
 #endif
     }
+    E1STAMP(5);
+#undef E1STAMP
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -971,7 +1016,7 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
         dc_mark_phase(0, stream);
         uint64_t* st = desc + desc_words_multi(ntiles);
         DC_ENC_DISPATCH(encode_fused_kernel, dim3(grid), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, st,
-                        st + ntiles, ntiles, start_bit, total_bits, total_bits2, epoch, err);
+                        st + ntiles, ntiles, start_bit, total_bits, total_bits2, epoch, err, dbg);
         dc_mark_phase(1, stream);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }

@@ -164,7 +164,7 @@ int dc_debug_stamps(unsigned long long* host, long long n) {
 
 int dc_debug_enc_stamps(unsigned long long* host, long long n) {
     if (!G.enc_dbg) return DC_ERR_ARG;
-    if (n > 8192 * 8) n = 8192 * 8;
+    if (n > 16384 * 8) n = 16384 * 8;
     HIPCHK(hipStreamSynchronize(G.st));
     HIPCHK(hipMemcpy(host, G.enc_dbg, (size_t)n * 8, hipMemcpyDeviceToHost));
     return DC_OK;
@@ -320,6 +320,12 @@ static void make_params(Params* P, int ct, int type, uint32_t mask17) {
         P->eh0 = head << tl0;
         P->em1 = tl1 >= 32 ? 0xFFFFFFFFu : (1u << tl1) - 1u;
         P->eh1 = (head | 1u) << tl1;
+        /* v of a masked float with flag 0 (mantissa top 8 bits = the mask's) and zero bits below them:
+           the mask's 17 bits cut to 9 + mm bits; its low tl0 bits are the token's tail bits */
+        const uint32_t v0 = (P->mask17 << 15) >> (23 - tl1);
+        P->K0 = v0 ^ P->eh0;
+        P->K1 = ((P->mask17 >> 8) << tl1) ^ P->eh1;
+        P->lm1 = P->lm0 + P->dlm;
     }
 }
 
@@ -378,8 +384,8 @@ static int encode_on(hipStream_t st, int ct, const void* d_x, long long n, long 
         return DC_OK;
     }
     if (getenv("DC_DEBUG_STAMPS") && !G.enc_dbg) {
-        HIPCHK(hipMalloc((void**)&G.enc_dbg, 8192 * 8 * 8));
-        HIPCHK(hipMemset(G.enc_dbg, 0, 8192 * 8 * 8));
+        HIPCHK(hipMalloc((void**)&G.enc_dbg, 16384 * 8 * 8));
+        HIPCHK(hipMemset(G.enc_dbg, 0, 16384 * 8 * 8));
     }
     /* the kernel writes the total to both (no copy node per encode).  Epochs tag the tile states and flags:
        when they wrap, every old tag is cleared (a state of an old encode must never read as published) */

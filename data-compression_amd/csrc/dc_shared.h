@@ -29,6 +29,10 @@ typedef struct Params {  /* per-call codec parameters, computed on the host */
     int s0, s1;          /* CT7: the same as c0 | ((t >> s0) & k0), c1 | ((t >> s1) & k1): 17 - rs, 9 - rs */
     uint32_t em0, eh0;   /* CT7 encoder, flag 0 token = (v & em0) | eh0 (v = top 9+mm bits of the float) */
     uint32_t em1, eh1;   /* CT7 encoder, flag 1 token = (v & em1) | eh1 */
+    /* CT7 encoder, as XOR constants on v = the top 9+mm bits of a masked float (whose top 9 bits are the
+       mask's): flag 1 token = v ^ K1 (length lm1), flag 0 token = v ^ K0 (length lm0) */
+    uint32_t K0, K1;
+    int lm1;
 } Params;
 
 typedef struct Plan {    /* device-resident sizes of the stream being decoded */
