@@ -498,46 +498,66 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
     nbits = L.encode_result()
     nbytes = (nbits + 7) // 8
 
-    # CT9 flow (--ber): sender CRC, channel copy with floor(bits*BER) flipped bits, receiver CRC check
-    # (one host round trip, as the MPI receiver's compare), resend of the clean stream, decode of the
-    # received copy.  The stream length is the warm-up's (same input every step).
+    # CT9 flow (--ber): sender CRC, channel copy with floor(bits*BER) flipped bits, receiver CRC check, resend
+    # of the clean stream on a mismatch, CRC check of the resent copy, decode of the received copy.  The
+    # checks and the resend run on the device (dc_crc_resend_device: no host round trip inside the step);
+    # the host reads each step's counters (resends, mismatches left) asynchronously as the protocol's ack
+    # and checks them after the loop.  The stream length is the warm-up's (same input every step).
     resends = [0]
+    ct9 = {}
     if ber > 0:
         rcv = torch.empty(cap, dtype=torch.uint8, device=dev)
         d_crc = torch.zeros(2, dtype=torch.int32, device=dev)
+        d_cnt = torch.zeros(2, dtype=torch.int32, device=dev)
         nflip = int(nbits * ber)
         seed = [1]
+        acks = []
+        ack_buf = torch.zeros((max(steps, warmup) + 1, 2), dtype=torch.int32, pin_memory=True)
+        CT9_PHASES = ["crc32 (sender)", "channel copy", "flip_bits_kernel", "crc32 (receiver)",
+                      "crc_resend_kernel (compare + resend copy)", "crc32 (resent copy)", "crc_resend_kernel (check)"]
 
-        def step(ev=None):                                   # noqa: F811 -- the CT9 variant of the step
+        def step(ev=None, ph=None):                          # noqa: F811 -- the CT9 variant of the step
+            def mark(i):
+                if ph is not None:
+                    ph[i].record(ext)
             if ev:
                 ev[0].record(ext)
             L.encode_device(ct, xs.data_ptr(), n, stream.data_ptr(), idx0=idx0, type_=typ, mask17=mask17,
                             total_ptr=d_nbits.data_ptr())
+            mark(0)
             L.crc32_device_async(stream.data_ptr(), nbytes, d_crc.data_ptr())
+            mark(1)
             with torch.cuda.stream(ext):
                 rcv[:nbytes].copy_(stream[:nbytes])
+            mark(2)
             L.flip_bits_device(rcv.data_ptr(), nbits, nflip, seed[0])
             seed[0] += nflip
+            mark(3)
             L.crc32_device_async(rcv.data_ptr(), nbytes, d_crc.data_ptr() + 4)
-            L.synchronize()
-            c = d_crc.cpu().numpy()
-            while c[0] != c[1]:                               # damaged: resend and check again
-                resends[0] += 1
-                with torch.cuda.stream(ext):
-                    rcv[:nbytes].copy_(stream[:nbytes])
-                L.crc32_device_async(rcv.data_ptr(), nbytes, d_crc.data_ptr() + 4)
-                L.synchronize()
-                c = d_crc.cpu().numpy()
+            mark(4)
+            L.crc_resend_device(d_crc.data_ptr(), stream.data_ptr(), rcv.data_ptr(), nbytes, 1, d_cnt.data_ptr())
+            mark(5)
+            L.crc32_device_async(rcv.data_ptr(), nbytes, d_crc.data_ptr() + 4)
+            mark(6)
+            L.crc_resend_device(d_crc.data_ptr(), stream.data_ptr(), rcv.data_ptr(), nbytes, 0, d_cnt.data_ptr())
+            mark(7)
             if ev:
                 ev[1].record(ext)
             L.decode_device(ct, rcv.data_ptr(), nbytes, n, out.data_ptr(), type_=typ, mask17=mask17, max_bytes=cap)
             if ev:
                 ev[2].record(ext)
+            with torch.cuda.stream(ext):                     # the ack: this step's counters, copied async
+                a = ack_buf[len(acks) % ack_buf.shape[0]]
+                a.copy_(d_cnt, non_blocking=True)
+                acks.append(a)
 
         for _ in range(warmup):
             step()
             L.decode_finish()
-        resends[0] = 0
+        L.synchronize()
+        d_cnt.zero_()
+        acks.clear()
+        ct9 = {"d_cnt": d_cnt, "acks": acks, "phases": CT9_PHASES, "nflip": nflip}
 
     # ---- timed region: barrier + sync on both sides, max over ranks, nothing but the steps (an event
     # record between launches costs a few microseconds of dispatch gap)
@@ -563,14 +583,24 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
             raise
     wall = C.max_over_ranks(t1 - t0)
     timed_resends = resends[0]
+    if ber > 0:                                       # every step's ack: one resend (its damaged copy detected),
+        acks = [a.numpy().copy() for a in ct9["acks"]]   # no mismatch left after it
+        timed_resends = int(acks[-1][0]) if acks else 0
+        ct9["acks_ok"] = all(int(a[0]) == k + 1 and int(a[1]) == 0 for k, a in enumerate(acks)) and len(acks) == steps
+        ct9["d_cnt"].zero_()
+        ct9["acks"].clear()
     # ---- the same steps again with per-kernel HIP events, recorded by the library on its own stream
     # (dc_timing_enable, one event set per step): the kernel table and the roofline's launch duration
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    phs = [[torch.cuda.Event(enable_timing=True) for _ in range(8)] for _ in range(steps)] if ber > 0 else None
     L.L.dc_timing_enable(steps)
     torch.cuda.synchronize()
     L.synchronize()
     for k in range(steps):
-        step(evs[k])
+        if ber > 0:
+            step(evs[k], phs[k])
+        else:
+            step(evs[k])
     L.synchronize()
     torch.cuda.synchronize()
     st2 = L.decode_status()
@@ -589,10 +619,13 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
             kms[k] = np.frombuffer(buf, np.float32)
     L.L.dc_timing_enable(0)
     kavg = kms.mean(axis=0)
+    if ber > 0:                                       # the CT9 launches between encode and decode, per step
+        ct9["phase_ms"] = {nm: float(np.mean([p[i].elapsed_time(p[i + 1]) for p in phs]))
+                           for i, nm in enumerate(ct9["phases"])}
     res = {"nbits": int(nbits), "nbytes": int(nbytes), "wall": wall, "enc_ms": enc_ms, "dec_ms": dec_ms,
            "kavg": kavg, "status": int(status | warm_status), "warm_status": int(warm_status), "resends": timed_resends,
            "slow_path_timed": slow[0], "v3": bool(L.L.dc_last_decode_launched_v3()),
-           "enc_mode": int(L.L.dc_encode_mode())}
+           "enc_mode": int(L.L.dc_encode_mode()), "ct9": {k: v for k, v in ct9.items() if k in ("phase_ms", "acks_ok", "nflip")}}
 
     if pipelined and ber <= 0:
         # the same K steps pipelined (encode k+1 || decode k, two stream buffers), reported beside value
@@ -722,6 +755,9 @@ def line_for(C, W, R, steps):
     n, nbytes = W["n"], R["nbytes"]
     ms = R["wall"] / steps * 1e3
     kernels = kernel_table(W["ct"], n, nbytes, R["kavg"], R["v3"], R.get("enc_mode", 1))
+    for nm, ms_ in R.get("ct9", {}).get("phase_ms", {}).items():   # CT9: every launch of the step
+        kernels[nm] = (ms_, 2.0 * nbytes if "copy" in nm and "compare" not in nm else
+                       (2.0 * nbytes if "resend copy" in nm else (float(nbytes) if "crc32" in nm else 0.0)))
     dname = max(kernels, key=lambda k: kernels[k][0])
     dms, dbytes = kernels[dname]
     ach = dbytes / (dms * 1e-3) / 1e9 if dms > 0 else 0.0
@@ -746,7 +782,7 @@ def side_config(C, ct, kind, log2n, steps, warmup, bound, ber=0.0):
     out.update({"ct": ct, "input": kind, "floats": W["n"], "type": W["type"], "mask17": f"{W['mask17']:05x}"})
     if ber > 0:
         out.update({"ber": ber, "flips_per_step": int(R["nbits"] * ber), "resends": R["resends"],
-                    "detected_all": R["resends"] == steps})
+                    "detected_all": R["resends"] == steps and bool(R["ct9"].get("acks_ok"))})
     del W
     torch.cuda.empty_cache()
     return out
@@ -834,7 +870,7 @@ def main():
         res["config"]["workload"] = (f"CT9 (CT7 stream + CRC-32) at BER={args.ber:g} with real bit flips, "
                                      f"{args.input.upper()} 2^{args.log2n} float32 per GPU, absErrorBound={args.bound:g}")
         res["config"].update({"ber": args.ber, "flips_per_step": int(R["nbits"] * args.ber), "resends": R["resends"],
-                              "detected_all": R["resends"] == args.steps})
+                              "detected_all": R["resends"] == args.steps and bool(R["ct9"].get("acks_ok"))})
     if C.world > 1 and not args.no_e2e:
         res["end_to_end"] = e2e_run(C, W, args.steps, args.warmup)
     del W

@@ -652,6 +652,34 @@ static uint32_t h_xpow8n(unsigned long long n) {                      // x^(8n) 
     return p;
 }
 
+// CT9 receiver check (the MPI_Bcast_bitwise_mask_crc protocol, impl/dataCompression.c:968-1090; the
+// pingpong CT9 exchange impl/pingpong.c:363-447) without a host round trip: crc[0] is the sender's CRC-32,
+// crc[1] the receiver's.  copy != 0: a mismatch is a damaged receive -- the sender's stream is sent again
+// (copied over dst) and counted in count[0]; copy == 0: a mismatch left after the resend counts in count[1].
+// Every workgroup reads the two words (written by earlier launches on the stream) and leaves at once when
+// they agree.
+__global__ __launch_bounds__(256) void crc_resend_kernel(const uint32_t* __restrict__ crc, const uint8_t* __restrict__ src,
+                                                         uint8_t* __restrict__ dst, long long nbytes, int copy,
+                                                         unsigned* __restrict__ count) {
+    if (crc[0] == crc[1]) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(count + (copy ? 0 : 1), 1u);
+    if (!copy) return;
+    const long long n16 = nbytes >> 4;
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) d4[i] = s4[i];
+    for (long long i = (n16 << 4) + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nbytes; i += stride) dst[i] = src[i];
+}
+
+extern "C" int dc_launch_crc_resend(const uint32_t* crc, const uint8_t* src, uint8_t* dst, long long nbytes, int copy,
+                                    unsigned* count, hipStream_t st) {
+    long long g = copy ? (nbytes / 16 + 255) / 256 : 1;
+    g = std::max<long long>(1, std::min<long long>(g, 4096));
+    hipLaunchKernelGGL(crc_resend_kernel, dim3((unsigned)g), dim3(256), 0, st, crc, src, dst, nbytes, copy, count);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // ---------------------------------------------------------------- Hamming SECDED
 // Hamming position of data bit d (0-based): the (d+1)-th positive integer that is not a power of 2.
 __device__ __forceinline__ unsigned long long ham_pos(unsigned long long d) {

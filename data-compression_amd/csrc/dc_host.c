@@ -996,6 +996,17 @@ int dc_flip_bits_device(void* d_s, unsigned long long nbits, long long count, un
 
 static int crc_into(const void* d_s, long long nbytes, uint32_t* d_out);
 
+int dc_crc_resend_device(const uint32_t* d_crc2, const void* d_src, void* d_dst, long long nbytes, int copy,
+                         unsigned* d_count) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (nbytes < 0) return seterr(DC_ERR_ARG, "nbytes < 0");
+    if (copy && (((uintptr_t)d_src | (uintptr_t)d_dst) & 15u)) return seterr(DC_ERR_ARG, "streams must be 16-byte aligned");
+    if (dc_launch_crc_resend(d_crc2, (const uint8_t*)d_src, (uint8_t*)d_dst, nbytes, copy, d_count, G.st))
+        return seterr(DC_ERR_HIP, "resend launch failed");
+    return DC_OK;
+}
+
 int dc_crc32_device_async(const void* d_s, long long nbytes, uint32_t* d_crc) {
     int rc = ensure_init();
     if (rc) return rc;

@@ -193,6 +193,8 @@ int dc_launch_plane_scatter(const float* x, const float* d_min, float* p, int mj
                             dc_hip_stream st);
 int dc_launch_flip_bits(uint8_t* s, unsigned long long nbits, long long count, unsigned long long seed,
                         dc_hip_stream st);
+int dc_launch_crc_resend(const uint32_t* crc, const uint8_t* src, uint8_t* dst, long long nbytes, int copy,
+                         unsigned* count, dc_hip_stream st);
 int dc_launch_ham_syndrome(const uint8_t* s, long long nbytes, unsigned long long* d_syn_ones, dc_hip_stream st);
 
 #ifdef __cplusplus

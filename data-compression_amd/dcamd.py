@@ -45,7 +45,7 @@ EXT_SYMBOLS = [
     "dc64_last_decode_flags", "dc64_to_small_device", "dc64_med_device", "dc_set_encode_stream",
     "dc_decode_status", "dc_abi_status", "dc_med_sum_device", "dc_type_from_max", "dc_set_small_chunk_max_bytes",
     "dc_set_decode3_min_bytes", "dc_last_decode_was_v3", "dc_last_decode_launched_v3",
-    "dc_encode_status", "dc_encode_mode", "dc_encode_retries",
+    "dc_encode_status", "dc_encode_mode", "dc_encode_retries", "dc_crc_resend_device",
 ]
 
 
@@ -453,6 +453,11 @@ class Lib:
     def crc32_device_async(self, s_ptr, nbytes, d_crc_ptr):
         self.check(self.L.dc_crc32_device_async(C.c_void_p(s_ptr), C.c_longlong(nbytes), C.c_void_p(d_crc_ptr)),
                    "dc_crc32_device_async")
+
+    def crc_resend_device(self, d_crc2_ptr, src_ptr, dst_ptr, nbytes, copy, d_count_ptr):
+        self.check(self.L.dc_crc_resend_device(C.c_void_p(d_crc2_ptr), C.c_void_p(src_ptr), C.c_void_p(dst_ptr),
+                                               C.c_longlong(nbytes), C.c_int(copy), C.c_void_p(d_count_ptr)),
+                   "dc_crc_resend_device")
 
     def flip_bits_device(self, s_ptr, nbits, count, seed):
         self.check(self.L.dc_flip_bits_device(C.c_void_p(s_ptr), C.c_ulonglong(nbits), C.c_longlong(count),

@@ -120,6 +120,11 @@ int dc_crc32_device_async(const void* d_s, long long nbytes, uint32_t* d_crc);
  * splitmix64(seed + i) mod nbits (MSB-first in each byte, as bit_flip).  The stream buffer must be
  * 4-byte aligned and padded to whole words.  Asynchronous. */
 int dc_flip_bits_device(void* d_s, unsigned long long nbits, long long count, unsigned long long seed);
+/* CT9 receiver check on the device, on the library stream (no host round trip): d_crc2[0] = sender's CRC-32,
+   d_crc2[1] = receiver's.  copy = 1: on a mismatch d_src (nbytes) is copied over d_dst (the resend) and
+   d_count[0] incremented; copy = 0: a mismatch increments d_count[1].  16-byte aligned streams. */
+int dc_crc_resend_device(const uint32_t* d_crc2, const void* d_src, void* d_dst, long long nbytes, int copy,
+                         unsigned* d_count);
 
 /* CT1 byte-wise codec on device buffers: d_raw (n floats), d_codes (n chars), d_pos1 (n ints) must
  * hold the worst case; *nraw_out = raw count (codes = n - raw).  Synchronous. */
