@@ -832,21 +832,33 @@ static void dbg_dump(const Dec3Bufs* D3) {
 extern "C" int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
                                  const Params* P, const Dec3Bufs* D3, float* out, long long num, uint32_t epoch,
                                  hipStream_t st) {
-    static int gp[12], gd[12];                  // (the occupancy does not depend on the segment length)
+    // resident grids per (CT, segment length) instantiation: every job of a call must be resident at once
+    // (parse3's link wait, decode3's history wait), so each grid is sized from its own kernel's occupancy
+    static int gp[2][12], gd[2][12];
     const int ci = (P->ct > 0 && P->ct < 12) ? P->ct : 0;
     if (D3->seg != 8 && D3->seg != 16) return -2;
-    if (!gp[ci]) {
-        const void* fp = P->ct == 5 ? (const void*)parse3_kernel<5, 16> : P->ct == 6 ? (const void*)parse3_kernel<6, 16>
-                       : P->ct == 7 ? (const void*)parse3_kernel<7, 16> : (const void*)parse3_kernel<11, 16>;
-        const void* fd = P->ct == 5 ? (const void*)decode3_kernel<5, 16> : P->ct == 6 ? (const void*)decode3_kernel<6, 16>
-                       : P->ct == 7 ? (const void*)decode3_kernel<7, 16> : (const void*)decode3_kernel<11, 16>;
-        gp[ci] = resident3(fp, 64);
-        gd[ci] = resident3(fd, 256);
+    const int si = D3->seg == 16;
+    if (!gp[si][ci]) {
+        const void* fp;
+        const void* fd;
+        if (si) {
+            fp = P->ct == 5 ? (const void*)parse3_kernel<5, 16> : P->ct == 6 ? (const void*)parse3_kernel<6, 16>
+               : P->ct == 7 ? (const void*)parse3_kernel<7, 16> : (const void*)parse3_kernel<11, 16>;
+            fd = P->ct == 5 ? (const void*)decode3_kernel<5, 16> : P->ct == 6 ? (const void*)decode3_kernel<6, 16>
+               : P->ct == 7 ? (const void*)decode3_kernel<7, 16> : (const void*)decode3_kernel<11, 16>;
+        } else {
+            fp = P->ct == 5 ? (const void*)parse3_kernel<5, 8> : P->ct == 6 ? (const void*)parse3_kernel<6, 8>
+               : P->ct == 7 ? (const void*)parse3_kernel<7, 8> : (const void*)parse3_kernel<11, 8>;
+            fd = P->ct == 5 ? (const void*)decode3_kernel<5, 8> : P->ct == 6 ? (const void*)decode3_kernel<6, 8>
+               : P->ct == 7 ? (const void*)decode3_kernel<7, 8> : (const void*)decode3_kernel<11, 8>;
+        }
+        gp[si][ci] = resident3(fp, 64);
+        gd[si][ci] = resident3(fd, 256);
     }
     const long long maxseg = (D3->max_chunks + D3->seg - 1) / D3->seg;
     const long long maxpj = (maxseg + 63) / 64, maxdj = (D3->max_chunks + 63) / 64;
-    const int g1 = (int)std::max<long long>(1, std::min<long long>(maxpj, gp[ci]));
-    const int g3 = (int)std::max<long long>(1, std::min<long long>((maxdj + 3) / 4, gd[ci]));
+    const int g1 = (int)std::max<long long>(1, std::min<long long>(maxpj, gp[si][ci]));
+    const int g3 = (int)std::max<long long>(1, std::min<long long>((maxdj + 3) / 4, gd[si][ci]));
     dc_mark_phase(4, st);
     DC_DISPATCH_3(P->ct, D3->seg, parse3_kernel, dim3(g1), dim3(64), 0, st, s, *P, *D3, dev_nbits, host_nbits, num, epoch);
     dbg_wait("parse3_kernel", st);

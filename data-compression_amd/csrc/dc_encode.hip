@@ -320,9 +320,15 @@ __device__ __forceinline__ void load_tile_x(f32x4 (&f)[ENC_K / 4], const float* 
 // Workgroup 0 of the pack kernel first scans the tile bit counts (no scan launch, no gap): chunks of 2048
 // counts (the next one's loads in flight), 8 consecutive per thread through the bit buffer's LDS (a pad
 // word per 16), a wave scan and the four wave totals; every offset is stored sc1 (written through), each wave drains its stores, and after
-// a barrier one lane publishes the encode's epoch in `flag` (the hand-off of MI355X_MICROARCH.md: sc1
-// stores, vmcnt(0) in every storing wave, barrier, one sc1 flag store; consumers poll and load sc1).
-// Workgroup 0 is dispatched first, so the others never wait for a workgroup that is not running.
+// a barrier one lane publishes the encode's epoch in `flag`.  This is the fence-free hand-off form of
+// MI355X_MICROARCH.md (section "Workgroup dispatch ... inter-workgroup visibility", Valid forms, first
+// table row): every payload store is an agent-scope (sc1) store, every storing wave runs s_waitcnt
+// vmcnt(0) before the workgroup barrier behind which ONE lane stores the flag sc1; the consumer polls the
+// flag with sc1 loads and reads every offset with sc1 loads (never L1, never flat), so neither a release
+// nor an acquire fence is needed.  The pack relies on workgroup 0 being dispatched first and staying
+// resident while the others poll (bounded: a tile whose poll times out sets err bit 4 and stores nothing;
+// dc_encode_result then re-encodes with the wait-free three-launch variant, where the scan is a launch of
+// its own).  A concurrent process on the same GPU can delay workgroup 0, never wedge the encode.
 __device__ void pack_scan_block(const uint32_t* __restrict__ tcnt, uint64_t* __restrict__ toff, unsigned ntiles,
                                 int start_bit, unsigned long long* __restrict__ total_bits,
                                 unsigned long long* __restrict__ total_bits2, uint32_t* lds, uint32_t* s_w,

@@ -79,7 +79,8 @@ typedef struct Dec3Bufs {
     uint64_t* pexit;               /* [parse job] epoch << 32 | its last lane's exit (main walk) */
     uint64_t* hist;                /* [decode job][3] the job's last three values, epoch-tagged granules */
     unsigned* err;                 /* the DecBufs status word; 512 = this path declined the stream */
-    int seg;                       /* chunks per parse segment: 16 or 32 */
+    int seg;                       /* chunks per parse segment: 8 or 16 (dc_decode3_seg); the pre-walk is
+                                      1024 bits either way */
     long long max_chunks;          /* capacity of rec */
     long long capw;                /* readable words of the stream buffer (a multiple of 4, >= 4) */
 } Dec3Bufs;

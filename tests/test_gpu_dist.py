@@ -3,8 +3,9 @@ share cuda:0.  Every rank counts its shard's bits (dc_encode_bits_device), the c
 global start bits, each rank encodes its shard at (start mod 8) with its global index and predictor halo,
 the shards are gathered into the single global stream (dcamd.gather_stream) and each rank decodes its
 shard of that stream (dcamd.decode_sharded: deferred history, 12-byte exchange, prefix fix).  The
-gathered stream must equal the library's single-stream encode of the whole array, and every rank's values
-the single-stream decode's slice, bit for bit."""
+gathered stream must equal the oracle's single-stream encode of the whole array (oracle/dc_oracle.c, the
+restatement pinned to the compiled reference), and every rank's values the oracle decode's slice, bit
+for bit."""
 import os
 import socket
 import sys
@@ -65,8 +66,8 @@ def _worker(rank, world, port, ct, n, kind, q):
         out = torch.empty(n, dtype=torch.float32, device=dev)
         dcamd.decode_sharded(L, ct, glob, glob.numel(), starts[rank], bits, n, out, t, m17)
         torch.cuda.synchronize()
-        s_all, nb_all, pos_all = L.compress(ct, xs, t, m17)             # the single stream, same GPU
-        dec_all = L.decompress(ct, s_all, N, t, m17)
+        s_all, nb_all, pos_all = O.compress(ct, xs, 1e-3, t, m17)       # the oracle's single stream
+        dec_all, _ = O.decompress(ct, s_all, N, 1e-3, t, m17)            # and its decode of it
         ok_stream = bool(tot == _bits_of(nb_all, pos_all) and np.array_equal(glob.cpu().numpy(), s_all))
         ok_dec = bool(np.array_equal(out.cpu().numpy().view(np.uint32), dec_all[lo:lo + n].view(np.uint32)))
         q.put((rank, ok_stream, ok_dec))
