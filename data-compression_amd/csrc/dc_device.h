@@ -469,6 +469,24 @@ struct BitReader {
     }
 };
 
+// Wave-wide inclusive prefix sum without LDS: Hillis-Steele inside each 16-lane row (DPP row_shr 1, 2, 4,
+// 8), then row_bcast:15 (lane 15 of rows 0 / 2 into rows 1 / 3) and row_bcast:31 (lane 31 into rows 2, 3)
+// -- the GFX9-family DPP scan.  (__shfl_up / __shfl_xor lower to ds_bpermute: one LDS round trip per step.)
+// Every lane of the wave must be active.
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31
+    return v;
+}
+// the wave's total (every lane)
+__device__ __forceinline__ uint32_t wave_total(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_incl(v), 63);
+}
+
 __device__ __forceinline__ uint64_t ld_relaxed(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

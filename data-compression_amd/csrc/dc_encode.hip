@@ -108,8 +108,7 @@ __device__ __forceinline__ void count_part(const float* __restrict__ x, long lon
     uint32_t sum = 0;
 #pragma unroll
     for (int q = 0; q < CNT_Q; q++) sum += qsum[q];
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
+    sum = wave_total(sum);
     if (lane == 0) {
         int vend = CNT_SUB;                                          // elements the vector pass saw
         if (tb + CNT_SUB > n) {                                      // the 0.0f padding's tokens
@@ -495,12 +494,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
             mysum += (uint32_t)len;
         }
     }
-    uint32_t inc = mysum;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t u = __shfl_up(inc, d, 64);
-        if (lane >= d) inc += u;
-    }
+    const uint32_t inc = wave_scan_incl(mysum);
     if (lane == 63) s_w[wid] = inc;
     E3STAMP(1);
     __syncthreads();
@@ -753,6 +747,72 @@ __device__ __forceinline__ uint32_t make_tokens16(const float* h, const Params& 
     return sum;
 }
 
+// The scanner (block 0 of the single-pass launch when DC_ENC_SCAN, the default): it publishes every tile's
+// INCLUSIVE state as soon as that tile and all its predecessors have published their aggregates.  Each
+// round reads the 1024 states after the frontier F (4 consecutive per thread: 32 coalesced bytes), finds
+// the first one not yet an aggregate, scans the counts before it (wave scans + wave totals in LDS) and
+// stores their inclusive states; F moves past them.  A tile then needs ONE poll of its own state instead
+// of a look-back: the chained look-back cost ~3 state round trips (~4.5 us) per tile, as each tile's
+// predecessors were looking back at the same time.
+__device__ void enc_scanner(uint64_t* __restrict__ st, unsigned ntiles, uint32_t tag, int start_bit,
+                            unsigned* __restrict__ err, uint32_t* s_gap, uint32_t* s_kb, uint32_t* s_tot) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    unsigned long long carry = (unsigned long long)start_bit;
+    unsigned F = 0;
+    unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (F < ntiles) {
+        uint64_t v[4];
+        int kb = 4;                                                       // the thread's first state not ready
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const unsigned i = F + 4u * (unsigned)tid + (unsigned)k;
+            v[k] = ld_relaxed(st + (i < ntiles ? i : ntiles - 1));
+            const bool ok = i < ntiles && (uint32_t)(v[k] >> 42) == tag && (v[k] & ST_MASK) == ST_AGG;
+            if (!ok && kb == 4) kb = k;
+        }
+        const unsigned long long bm = __ballot(kb < 4);
+        const int fl = bm ? __ffsll((long long)bm) - 1 : 64;              // the wave's first lane with a gap
+        const int fkb = fl < 64 ? __builtin_amdgcn_readlane(kb, fl) : 4;
+        if (lane == 0) { s_gap[wid] = (uint32_t)fl; s_kb[wid] = (uint32_t)fkb; }
+        __syncthreads();
+        unsigned p = 1024;                                                // ready states after F
+#pragma unroll
+        for (int w = 3; w >= 0; w--)
+            if (s_gap[w] < 64u) p = 4u * (64u * (unsigned)w + s_gap[w]) + s_kb[w];
+        uint32_t c[4], sum = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            c[k] = 4u * (unsigned)tid + (unsigned)k < p ? (uint32_t)(v[k] & ST_VAL) : 0u;
+            sum += c[k];
+        }
+        const uint32_t inc = wave_scan_incl(sum);
+        if (lane == 63) s_tot[wid] = inc;
+        __syncthreads();
+        uint32_t wpre = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            wpre += w < wid ? s_tot[w] : 0u;
+            tot += s_tot[w];
+        }
+        unsigned long long run = carry + wpre + inc - sum;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            run += c[k];
+            const unsigned i = F + 4u * (unsigned)tid + (unsigned)k;
+            if (4u * (unsigned)tid + (unsigned)k < p) st_relaxed(st + i, st_word(tag, ST_INC, run));
+        }
+        carry += tot;
+        F += p;
+        if (p) {
+            t0 = __builtin_amdgcn_s_memrealtime();
+        } else {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > LB_WAIT) { if (tid == 0) atomicOr(err, 4u); return; }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        __syncthreads();                                                  // the LDS words are rewritten
+    }
+}
+
 // (6 waves per SIMD asked: the tokens' branch-free selects need ~92 SGPRs of lane masks and 69 VGPRs, which
 // hold 7 workgroups per CU; 8 spilled SGPRs to VGPR lanes and VGPRs to scratch)
 #ifndef DC_FUSED_WAVES
@@ -763,11 +823,10 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
     const float* __restrict__ x, long long n, long long idx0, Params P, uint32_t* __restrict__ out,
     uint64_t* __restrict__ st, uint64_t* __restrict__ tl, unsigned ntiles, int start_bit,
     unsigned long long* __restrict__ total_bits, unsigned long long* __restrict__ total_bits2, uint32_t epoch,
-    unsigned* __restrict__ err, unsigned long long* __restrict__ dbg) {
+    unsigned* __restrict__ err, unsigned long long* __restrict__ dbg, int scan) {
     static_assert(ENC_K == 16 && ENC_TPB == 256, "16 consecutive floats per thread, 4 waves per tile");
     // (DC_DEBUG_STAMPS: phase stamps of the first 16384 tiles, s_memrealtime)
-#define E1STAMP(ph) do { if (dbg && threadIdx.x == 0 && blockIdx.x < 16384) dbg[blockIdx.x * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-    E1STAMP(0);
+#define E1STAMP(ph) do { if (dbg && threadIdx.x == 0 && tile < 16384) dbg[tile * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); } while (0)
     // sb: first the load transpose (each wave its part), then the tokens (token j of thread t at word
     // 256 j + t), then the bit buffer
     __shared__ __attribute__((aligned(16))) uint32_t sb[E3_WORDS];
@@ -777,7 +836,12 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
     __shared__ uint16_t tab[512];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t tag = epoch & ST_TAGM;
-    const unsigned tile = blockIdx.x;
+    if (scan && blockIdx.x == 0) {                                    // the scanner (dispatched first)
+        enc_scanner(st, ntiles, tag, start_bit, err, s_hw, s_hi, s_tw);
+        return;
+    }
+    const unsigned tile = blockIdx.x - (scan ? 1u : 0u);
+    E1STAMP(0);
     build_enc_tab<CT>(tab, P, tid, ENC_TPB);                          // (read after the barrier below)
     const long long tbase = (long long)tile * ENC_TILE;
     const long long base = tbase + (long long)ENC_K * tid;
@@ -837,12 +901,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
     }
     // ---- the tile's total and the thread's first bit
     E1STAMP(1);
-    uint32_t inc = mysum;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t u = __shfl_up(inc, d, 64);
-        if (lane >= d) inc += u;
-    }
+    const uint32_t inc = wave_scan_incl(mysum);
     if (lane == 63) s_w[wid] = inc;
     __syncthreads();
     E1STAMP(2);
@@ -858,7 +917,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
     // publish the aggregate (tile 0: its inclusive state) and the tile's last 31 bits (the successor's
     // first word starts with them): the last thread's tokens (>= 48 bits)
     if (tid == 0)
-        st_relaxed(st + tile, tile == 0 ? st_word(tag, ST_INC, (unsigned long long)start_bit + T) : st_word(tag, ST_AGG, T));
+        st_relaxed(st + tile, tile == 0 && !scan ? st_word(tag, ST_INC, (unsigned long long)start_bit + T) : st_word(tag, ST_AGG, T));
     if (tid == ENC_TPB - 1 && tile + 1 < ntiles) {
         uint64_t acc = 0;
 #pragma unroll
@@ -928,7 +987,23 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
         unsigned long long G = (unsigned long long)start_bit;
         uint32_t lbst = 0;
         E1STAMP(3);
-        int bad = tile > 0 ? enc_lookback(st, tile, tag, G, lbst) : 0;
+        int bad = 0;
+        if (scan) {                                                       // the scanner publishes the offset
+            if (lane == 0) {
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                uint64_t v;
+                for (;;) {
+                    v = ld_relaxed(st + tile);
+                    if ((uint32_t)(v >> 42) == tag && (v & ST_MASK) == ST_INC) break;
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > LB_WAIT) { bad = 1; break; }
+                    lbst += 1u << 16;
+                    __builtin_amdgcn_s_sleep(DC_LB_SLEEP);
+                }
+                G = (v & ST_VAL) - T;
+            }
+        } else if (tile > 0) {
+            bad = enc_lookback(st, tile, tag, G, lbst);
+        }
         E1STAMP(4);
         if (lane == 0) {
             uint32_t tp = 0;
@@ -944,7 +1019,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
             // (a guard, never taken by a correct encode: a tile's bits end within the stream's capacity,
             // 32 bits per float after the start bit -- a stale offset must not send the stores outside it)
             if (!bad && G + T > (unsigned long long)start_bit + 32ull * (unsigned long long)min(n, tbase + ENC_TILE)) bad = 2;
-            if (tile > 0) st_relaxed(st + tile, bad ? st_word(tag, ST_BAD, 0) : st_word(tag, ST_INC, G + T));
+            if (tile > 0 && !scan) st_relaxed(st + tile, bad ? st_word(tag, ST_BAD, 0) : st_word(tag, ST_INC, G + T));
             if (bad) atomicOr(err, bad == 2 ? 2u : 4u);
             else if (tile == ntiles - 1) {
                 *total_bits = G + T;
@@ -1021,8 +1096,10 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
         const int grid = (int)ntiles;
         dc_mark_phase(0, stream);
         uint64_t* st = desc + desc_words_multi(ntiles);
-        DC_ENC_DISPATCH(encode_fused_kernel, dim3(grid), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, st,
-                        st + ntiles, ntiles, start_bit, total_bits, total_bits2, epoch, err, dbg);
+        static int scan = -1;                                            // DC_ENC_SCAN=0: chained look-back
+        if (scan < 0) scan = (getenv("DC_ENC_SCAN") && *getenv("DC_ENC_SCAN") == '0') ? 0 : 1;
+        DC_ENC_DISPATCH(encode_fused_kernel, dim3(grid + scan), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, st,
+                        st + ntiles, ntiles, start_bit, total_bits, total_bits2, epoch, err, dbg, scan);
         dc_mark_phase(1, stream);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
