@@ -39,7 +39,8 @@ namespace dc {
 
 // pre-walk: 1024 bits (4 chunks, one region line) before every segment
 constexpr int D3_SEG = 16;             // chunks per parse segment (4 region lines); 8 for small streams
-constexpr int D3_RING = 16;            // ring words per lane (four 128-bit phases), + 4 mirrored words
+
+constexpr int D3_RING = 16;            // ring words per lane (four 128-bit phases; a power of two: the fetch wraps)
 constexpr int D3_CAP = 1024 + 16;      // decode job output buffer (floats per wave)
 constexpr uint32_t D3_DECLINE = 512u;
 constexpr unsigned long long D3_LINK_WAIT = 20000;  // s_memrealtime ticks (100 MHz): 200 us
@@ -128,30 +129,28 @@ __device__ __forceinline__ Geo3 geo3(const unsigned long long* dev_nbits, unsign
 }
 
 // ------------------------------------------------------------------------------------------------
-// parse: the per-lane ring reader.  Ring-local word i of lane l lives at LDS dword i*64 + l; the ring
-// epoch's word 0 is segment-relative word 4*kbase; words 16..19 mirror 0..3, so a reader in the epoch's
-// last phase fetches ahead without wrapping, and after that phase every address moves back 16 words.
+// parse: the per-lane ring reader.  Ring word i of lane l lives at LDS dword (i mod 16)*64 + l; ring word 0
+// is segment-relative word 4*kbase of the current epoch.  The fetch address wraps inside the 16 words
+// ((addr + 256) & 0xFFF keeps the lane's byte offset, < 256), so no mirror words are needed: 4 KB of ring
+// per wave (was 5 KB with a 4-word mirror), which holds 6 parse waves per SIMD instead of 5.
+constexpr uint32_t D3_RMASK = (uint32_t)(D3_RING * 256 - 1);
 struct Ring3 {
     uint32_t* L;
     uint32_t lc;                                    // lane * 4
     uint32_t a, b, c, s, addr;                      // window (a:b) from bit 32 - s of a, c, next fetch address
     int pos;                                        // segment-relative bit
-    __device__ __forceinline__ uint32_t R(int i) const { return L[(i << 6) + (int)(lc >> 2)]; }
+    __device__ __forceinline__ uint32_t R(int i) const { return L[((i & (D3_RING - 1)) << 6) + (int)(lc >> 2)]; }
     __device__ __forceinline__ void init(int p, int kbase) {
         const int wi = (p - 1) >> 5;                // word holding bit p - 1 (floor for p <= 0)
         const int li = wi - 4 * kbase;
         s = (uint32_t)(32 * (wi + 1) - p);
         a = R(max(li, 0)); b = R(li + 1); c = R(li + 2);
-        addr = ((uint32_t)(li + 3) << 8) | lc;
+        addr = (((uint32_t)(li + 3) << 8) | lc) & D3_RMASK;
         pos = p;
     }
     __device__ __forceinline__ void put(int slot, uint4 v) {
         L[((slot * 4 + 0) << 6) + (lc >> 2)] = v.x; L[((slot * 4 + 1) << 6) + (lc >> 2)] = v.y;
         L[((slot * 4 + 2) << 6) + (lc >> 2)] = v.z; L[((slot * 4 + 3) << 6) + (lc >> 2)] = v.w;
-        if (slot == 0) {
-            L[(16 << 6) + (lc >> 2)] = v.x; L[(17 << 6) + (lc >> 2)] = v.y;
-            L[(18 << 6) + (lc >> 2)] = v.z; L[(19 << 6) + (lc >> 2)] = v.w;
-        }
     }
     // walk until pos >= pend; tokens stepped
     __device__ __forceinline__ int walk(int pend, const uint8_t* tl) {
@@ -167,7 +166,7 @@ struct Ring3 {
             a = adv ? b : a;
             b = adv ? c : b;
             c = adv ? nx : c;
-            addr += adv ? 256u : 0u;
+            addr = (addr + (adv ? 256u : 0u)) & D3_RMASK;
             n++;
         }
         return n;
@@ -221,7 +220,7 @@ __device__ __forceinline__ void run_lines(Ring3& r, __amdgpu_buffer_rsrc_t rs, l
             r.put((h + 2) & 3, finish4(st.S[(h + 2) & 7], nbytes, gw0 + 4ll * (k + 2)));
             if (h == 1) stage_half(st, 0, rs, gl + 32ll * L);
             if (h == 5) stage_half(st, 4, rs, gl + 32ll * L + 16);
-            if ((h & 3) == 3) { kbase += 4; r.addr -= 4096u; }
+            if ((h & 3) == 3) kbase += 4;
             if (h & 1) end(k >> 1, n0 + n);
             else n0 = n;
         }
@@ -266,7 +265,7 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
                                                     long long num, uint32_t epoch) {
     constexpr int seg = SEG;
     static_assert(SEG % 8 == 0, "whole region lines and 16-byte record stores per lane");
-    __shared__ uint32_t ring[(D3_RING + 4) * 64];
+    __shared__ uint32_t ring[D3_RING * 64];
     __shared__ uint16_t recs[seg * 64];                          // [chunk][lane]: the wave's records
     __shared__ uint8_t tl[512];
     const int lane = threadIdx.x;

@@ -637,10 +637,13 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
 #ifndef DC_LB_K
 #define DC_LB_K 8
 #endif
+#ifndef DC_SCAN_POLL
+#define DC_SCAN_POLL 0
+#endif
 #ifndef DC_LB_SLEEP
 #define DC_LB_SLEEP 1
 #endif
-constexpr int LB_K = DC_LB_K;                                     // look-back: tiles per lane per round trip
+constexpr int LB_KW = DC_LB_K;                                    // look-back: tiles per lane per round trip
 constexpr unsigned long long ST_VAL = (1ull << 40) - 1;
 constexpr unsigned long long ST_MASK = 3ull << 40, ST_AGG = 1ull << 40, ST_INC = 2ull << 40, ST_BAD = 3ull << 40;
 constexpr uint32_t ST_TAGM = (1u << 22) - 1;
@@ -663,6 +666,7 @@ __device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
 // ~1800 waiting tiles tripled the encode), then the window is read again.  A window without an inclusive
 // state adds its aggregates and the next one is read.  Returns 0, or 1 when a needed state is poisoned or a
 // wait timed out.
+template <int LB_K>
 __device__ __forceinline__ int enc_lookback(const uint64_t* __restrict__ st, long long t, uint32_t tag,
                                             unsigned long long& excl, uint32_t& stat) {
     const int lane = threadIdx.x & 63;
@@ -988,7 +992,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
         uint32_t lbst = 0;
         E1STAMP(3);
         int bad = 0;
-        if (scan) {                                                       // the scanner publishes the offset
+        if (scan && DC_SCAN_POLL) {                                      // (A/B: wait for the scanner itself)
             if (lane == 0) {
                 const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
                 uint64_t v;
@@ -1001,8 +1005,13 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
                 }
                 G = (v & ST_VAL) - T;
             }
+        } else if (scan) {
+            // the scanner keeps the inclusive states close behind the published aggregates: a one-load
+            // look-back over the 64 predecessors mostly meets one (waiting for the scanner to reach this
+            // tile itself cost ~4 us per tile)
+            if (tile > 0) bad = enc_lookback<1>(st, tile, tag, G, lbst);
         } else if (tile > 0) {
-            bad = enc_lookback(st, tile, tag, G, lbst);
+            bad = enc_lookback<LB_KW>(st, tile, tag, G, lbst);
         }
         E1STAMP(4);
         if (lane == 0) {

@@ -13,7 +13,7 @@ done
 done
 DCAMD_LIB=data-compression_amd/lib_k4/libdcamd.so DC_DEBUG_STAMPS=1 timeout -k 10 120 python3 -u tools/fused_stamps.py > gpurun_out/fs.txt 2>&1 || { tail -20 gpurun_out/fs.txt; exit 1; }
 head -12 gpurun_out/fs.txt; sed -n 13,40p gpurun_out/fs.txt | awk 'NR%3==1'
-for lib in lib_k4 lib_ns; do
+for lib in lib_k4 lib_ns lib_2p; do
   DCAMD_LIB=data-compression_amd/$lib/libdcamd.so timeout -k 10 200 python3 -u bench.py --no-cpu --no-pipelined --no-extra --steps 20 > gpurun_out/ab.json 2> gpurun_out/ab.err || { tail -20 gpurun_out/ab.err; exit 1; }
   python3 -c "import json,sys;d=json.loads(open('gpurun_out/ab.json').readline());print(sys.argv[1],d['value'],d['ms_per_step'],d['kernels_ms'])" $lib
 done
