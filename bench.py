@@ -815,13 +815,26 @@ def main():
     kernels = kernel_table(ct, n, nbytes, R["kavg"], R["v3"], R.get("enc_mode", 1))
     dname = main_line["dominant"]["kernel"]
     achievable = copy_bandwidth(C.dev, n)
-    traffic, traffic_src = None, None
+    traffic, traffic_src, ktraffic = None, None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if os.path.exists(pmc):
         try:
             pj = json.load(open(pmc))
             if pj.get("n") == n and pj.get("ct") == ct and pj.get("input", "u10") == args.input:
-                traffic = pj.get("hbm_bytes_per_launch", {}).get(dname)
+                hb = pj.get("hbm_bytes_per_launch", {})
+
+                def pmc_bytes(name):       # table "parse3_kernel<7>" = rocprof "parse3_kernel<7, 16>"
+                    if name in hb:
+                        return hb[name]
+                    stem = name[:-1] if name.endswith(">") else name
+                    hits = [v for k, v in hb.items() if k.startswith(stem) and k[len(stem):len(stem) + 1] in (",", ">")]
+                    return hits[0] if len(hits) == 1 else None
+                traffic = pmc_bytes(dname)
+                ktraffic = {}
+                for kn, (_, ab) in kernels.items():
+                    tb = pmc_bytes(kn)
+                    if tb is not None and ab > 0:
+                        ktraffic[kn] = {"hbm_bytes": int(tb), "algorithmic_bytes": int(ab), "ratio": round(tb / ab, 3)}
                 traffic_src = (f"profiles/pmc_latest.json: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE of this "
                                f"bench command, separate passes ({pj.get('source', 'tools/profile.sh')}); not measured "
                                f"in this run") if traffic is not None else None
@@ -855,6 +868,7 @@ def main():
                      "achievable_source": f"device copy of 2^{args.log2n} floats (torch copy_), read + written bytes",
                      "frac_of_achievable": round(main_line["dominant"]["achieved_GBs"] / achievable, 4)},
         "kernels_ms": main_line["kernels_ms"],
+        "kernels_traffic": ktraffic,
         "phases_ms": {"encode": round(R["enc_ms"], 4), "decode": round(R["dec_ms"], 4),
                       "med_dataset_s": round(W["t_med"], 4)},
         "pipeline_roofline_frac": round((8.0 * n + 2 * nbytes) / ((R["enc_ms"] + R["dec_ms"]) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

@@ -6,17 +6,18 @@
 // SIMD and few LDS bank conflicts, with as few walks per token as possible:
 //
 // parse3_kernel  one wave per parse job.  Lane l walks SEGMENT l of the job (seg 256-bit chunks, tens
-//                of thousands of bits) after a 1024-bit pre-walk (self-synchronisation), reading the
-//                stream through a per-lane LDS ring of 16 words (+4 mirrored) refilled 128 bits at a
-//                time with loads issued two phases ahead.  The ring is stored [word][lane], so every
-//                ds_read_b32 of a wave hits 32 distinct banks whatever the lanes' offsets.  At every
-//                chunk boundary the lane records the chunk's entry offset and token count (16 bits).
-//                Links are checked afterwards: a segment's first entry must equal the previous
-//                segment's exit (in-wave shuffle; across jobs the previous job's exit, published right
-//                after its main walk and waited for -- no chain: an exit never waits for anything;
-//                a wait past its bound, never seen, hands the stream to the chunk-map decoder).  A
-//                broken link (the pre-walk had not synchronised, ~0.3% of segments) is repaired by
-//                re-walking from the true entry until the path meets the recorded entries again.  The
+//                of thousands of bits; 4, 8 or 16 chunks by stream size) after a 1024-bit pre-walk
+//                (self-synchronisation), reading the stream through a per-lane LDS ring of
+//                16 words refilled 128 bits at a time with loads issued two phases ahead.  The ring is
+//                stored [word][lane], so every ds_read_b32 of a wave hits 32 distinct banks whatever the
+//                lanes' offsets.  At every chunk boundary the lane records the chunk's entry offset and
+//                token count (16 bits).  Links are checked afterwards: a segment's first entry must
+//                equal the previous segment's exit (in-wave shuffle; across jobs the previous job's
+//                exit, published after its main walk and in-job repairs and waited for -- no chain: an
+//                exit never waits for another job; a wait past its bound, never seen, hands the stream
+//                to the chunk-map decoder).  A broken link (the pre-walk had not synchronised, ~0.24% of
+//                CT7 segments at 1e-3, tools/sync_sim.py) is repaired by re-walking from the true entry
+//                until the path meets the recorded entries again (~1.25 chunks on average).  The
 //                wave's token counts are scanned into job-relative first-token offsets of every decode job.
 // decode3_kernel one wave per decode job of 64 chunks: lane = chunk, decoded from its recorded entry for
 //                its recorded token count (the job's first token: the wave's running sum of the parse
@@ -37,7 +38,11 @@
 
 namespace dc {
 
-// pre-walk: 1024 bits (4 chunks, one region line) before every segment
+// pre-walk: 1024 bits (4 chunks, one region line) before every segment (DC_PARSE_PL6=2: 2048 for CT6 --
+// 12% instead of 94% of its jobs repair, but the longer walk cost more: config 2 parse3 98 vs 92 us)
+#ifndef DC_PARSE_PL6
+#define DC_PARSE_PL6 1
+#endif
 constexpr int D3_SEG = 16;             // chunks per parse segment (4 region lines); 8 for small streams
 
 constexpr int D3_RING = 16;            // ring words per lane (four 128-bit phases; a power of two: the fetch wraps)
@@ -56,6 +61,7 @@ __device__ unsigned long long g_prof3[32];
 #define P3_DECL() unsigned long long p3a[16] = {0}
 #define P3_T(v) const long long v = clock64()
 #define P3_ADD(i, val) (p3a[i] += (unsigned long long)(val))
+#define P3_MAX(i, val) (((threadIdx.x & 63) == 0) ? (void)atomicMax(&g_prof3[i], (unsigned long long)(val)) : (void)0)
 #define P3_FLUSH()                                                                                     \
     do {                                                                                               \
         if ((threadIdx.x & 63) == 0)                                                                   \
@@ -66,6 +72,7 @@ __device__ unsigned long long g_prof3[32];
 #define P3_DECL() do {} while (0)
 #define P3_T(v) do {} while (0)
 #define P3_ADD(i, val) do {} while (0)
+#define P3_MAX(i, val) do {} while (0)
 #define P3_FLUSH() do {} while (0)
 #endif
 
@@ -194,10 +201,10 @@ __device__ __forceinline__ void stage_half(Stage8& st, int h0, __amdgpu_buffer_r
 // walk region lines L0 .. L1-1; the reader starts at segment bit pinit (a lane that is not live walks
 // nothing).  `start(c, kbase)` runs before chunk c is walked (c < 0 in the pre-walk), `end(c, count)`
 // after it.
-// EARLY (the repair rounds): the walk ends after the first line in which no lane is left walking; a lane
+// EARLY (the repair rounds): the walk ends at the first chunk entry at which no lane is left walking; a lane
 // that is not live loads nothing (its requests point past the buffer's range: 0, no memory traffic).
 template <bool EARLY, class Start, class End>
-__device__ __forceinline__ void run_lines(Ring3& r, __amdgpu_buffer_rsrc_t rs, long long nbytes, long long gw0, int L0,
+__device__ __forceinline__ int run_lines(Ring3& r, __amdgpu_buffer_rsrc_t rs, long long nbytes, long long gw0, int L0,
                                           int L1, int lim, int pinit, bool live, const uint8_t* tl, Start start,
                                           End end) {
     Stage8 st;
@@ -215,7 +222,12 @@ __device__ __forceinline__ void run_lines(Ring3& r, __amdgpu_buffer_rsrc_t rs, l
 #pragma unroll
         for (int h = 0; h < 8; h++) {
             const int k = 8 * (L - 1) + h;
-            if ((h & 1) == 0) start(k >> 1, kbase);
+            if ((h & 1) == 0) {
+                start(k >> 1, kbase);
+                // (repairs: ~1.25 chunks on average -- stop at the first chunk entry where every lane has
+                // met its recorded path, not at the end of the line)
+                if (EARLY && h > 0 && !__any(r.pos < (1 << 30))) return L - L0 + 1;
+            }
             const int n = r.walk(min(128 * (k + 1), lim), tl);
             r.put((h + 2) & 3, finish4(st.S[(h + 2) & 7], nbytes, gw0 + 4ll * (k + 2)));
             if (h == 1) stage_half(st, 0, rs, gl + 32ll * L);
@@ -224,8 +236,9 @@ __device__ __forceinline__ void run_lines(Ring3& r, __amdgpu_buffer_rsrc_t rs, l
             if (h & 1) end(k >> 1, n0 + n);
             else n0 = n;
         }
-        if (EARLY && !__any(r.pos < (1 << 30))) break;               // every lane met its recorded path
+        if (EARLY && !__any(r.pos < (1 << 30))) return L - L0 + 1;   // every lane met its recorded path
     }
+    return L1 - L0;
 }
 
 // A runs-mode stream (mostly 3-bit codes) that is nothing but num '100' codes -- every value within the
@@ -264,7 +277,8 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
                                                     const unsigned long long* dev_nbits, unsigned long long host_nbits,
                                                     long long num, uint32_t epoch) {
     constexpr int seg = SEG;
-    static_assert(SEG % 8 == 0, "whole region lines and 16-byte record stores per lane");
+    static_assert(SEG == 4 || SEG % 8 == 0, "whole region lines; 8- or 16-byte record stores per lane");
+    constexpr int PL = CT == 6 ? DC_PARSE_PL6 : 1;              // pre-walk lines (1024 bits each)
     __shared__ uint32_t ring[D3_RING * 64];
     __shared__ uint16_t recs[seg * 64];                          // [chunk][lane]: the wave's records
     __shared__ uint8_t tl[512];
@@ -296,7 +310,7 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
         // ---- main walk: the pre-walk line (1024 bits before the segment), then the segment's lines
         uint32_t tot = 0;
         int e0 = 0, ec = 0;
-        run_lines<false>(r, rs, G.nbytes, gw0, 0, seg / 4 + 1, lim, -1024, act, tl,
+        run_lines<false>(r, rs, G.nbytes, gw0, 1 - PL, seg / 4 + 1, lim, -1024 * PL, act, tl,
                   [&](int c, int kbase) {
                       if (c == 0 && sidx == 0) r.init(0, kbase);             // the stream's first bit
                       ec = r.pos - 256 * c;
@@ -309,7 +323,6 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
                       }
                   });
         const int X = r.pos - 256 * seg;                                 // entry of the next segment
-        if (lane == 63) st_relaxed(&D3.pexit[job], ((uint64_t)epoch << 32) | (uint32_t)X);
         P3_T(t1);
         P3_ADD(0, t1 - t0);
         P3_ADD(4, act ? tot : 0u);
@@ -329,6 +342,11 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
         bool bad = act && (lane > 0 || link0) && ecur != xin;
         for (int pass = 0; pass < 2; pass++) {
         if (pass == 1) {                            // the job's first link: wait (bounded) for the exit
+            // the job's exit, after the links within the job are repaired (a repair that reaches the end
+            // of the last segment moves it -- with 4-chunk segments not rare enough to decline the stream
+            // for): it depends on nothing outside the job, so no job waits for more than one main walk
+            // and one round of in-job repairs
+            if (lane == 63) st_relaxed(&D3.pexit[job], ((uint64_t)epoch << 32) | (uint32_t)Xcur);
             bool chk = false;
             if (lane == 0 && act && sidx > 0 && !link0) {
                 // the previous job is resident (a lower workgroup, or this grid's previous round) and
@@ -349,7 +367,8 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
         while (__any(bad)) {
             if (++rounds > 64) { if (lane == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK); break; }
             bool live = bad;
-            run_lines<true>(r, rs, G.nbytes, gw0, 1, seg / 4 + 1, lim, bad ? xin : 0, bad, tl,
+            P3_T(tr0);
+            const int nl = run_lines<true>(r, rs, G.nbytes, gw0, 1, seg / 4 + 1, lim, bad ? xin : 0, bad, tl,
                       [&](int c, int) {
                           const int old = (int)(recs[c * 64 + lane] & 31u);
                           if (live && c > 0 && r.pos - 256 * c == old && 256 * c < lim) {
@@ -366,11 +385,15 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
                               if (c == 0) ecur = ec;
                           }
                       });
+            P3_T(tr1);
+            P3_ADD(6, tr1 - tr0);
+            P3_ADD(7, nl);
+            (void)nl;
             const bool whole = 256 * seg < lim;                              // a successor segment exists
             const int Xn = live ? r.pos - 256 * seg : Xcur;
             const bool moved = live && whole && Xn != Xcur;
             Xcur = Xn;
-            if (moved && lane == 63) atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK);
+            if (moved && lane == 63 && pass == 1) atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK);   // (published)
             const int xp = __shfl_up(Xcur, 1, 64);
             const bool mp = __shfl_up((int)moved, 1, 64) != 0;
             bad = lane >= 1 && act && mp && ecur != xp;
@@ -379,6 +402,9 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
         }
         P3_T(t2);
         P3_ADD(2, t2 - t1);
+        P3_MAX(16, t2 - t0);
+        P3_MAX(17, t1 - t0);
+        P3_MAX(18, t2 - t1);
         P3_ADD(3, rounds);
         P3_ADD(5, 1);
 
@@ -388,10 +414,15 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
 #pragma unroll
             for (int i = 0; i < seg / 2; i++)
                 w[i] = (uint32_t)recs[(2 * i) * 64 + lane] | ((uint32_t)recs[(2 * i + 1) * 64 + lane] << 16);
+            if constexpr (seg == 4) {
+                const u32x2 v = {w[0], w[1]};
+                __builtin_amdgcn_raw_buffer_store_b64(v, rrec, (int)(2 * c0), 0, 0);
+            } else {
 #pragma unroll
-            for (int i = 0; i < seg / 8; i++) {
-                const u32x4 v = {w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
-                __builtin_amdgcn_raw_buffer_store_b128(v, rrec, (int)(2 * c0 + 16 * i), 0, 0);
+                for (int i = 0; i < seg / 8; i++) {
+                    const u32x4 v = {w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
+                    __builtin_amdgcn_raw_buffer_store_b128(v, rrec, (int)(2 * c0 + 16 * i), 0, 0);
+                }
             }
         }
 
@@ -751,6 +782,10 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
 // ------------------------------------------------------------------------------------------------
 #define DC_DISPATCH_3(CTV, SEGV, KER, ...)                                                           \
     switch ((CTV) * 100 + (SEGV)) {                                                                  \
+        case 504: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<5, 4>), __VA_ARGS__); break;                \
+        case 604: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<6, 4>), __VA_ARGS__); break;                \
+        case 704: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<7, 4>), __VA_ARGS__); break;                \
+        case 1104: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<11, 4>), __VA_ARGS__); break;              \
         case 508: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<5, 8>), __VA_ARGS__); break;                \
         case 608: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<6, 8>), __VA_ARGS__); break;                \
         case 708: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<7, 8>), __VA_ARGS__); break;                \
@@ -770,21 +805,36 @@ static int resident3(const void* f, int threads) {
     return per * ncu;
 }
 
-// segment length (chunks) for a stream of up to max_chunks chunks: 16, or 8 for streams too small to
-// fill the GPU with 16-chunk segments (<= 2.5 M chunks of capacity, 80 MB: the parse's walk per lane
-// is then 1024 + 2048 bits instead of 1024 + 4096, and there are twice the jobs) whose tokens are short
-// enough (bound exponent B <= 12, e.g. 1e-3: tokens of <= ~21 bits) for a repaired path to meet the
-// recorded one within a 2048-bit segment -- at 1e-6 a job's last segment could move its exit and
-// decline the stream.  The host sizes the scratch for 4-chunk segments, so both fit (DC_DEC3_SEG=8|16
-// forces one)
-extern "C" int dc_decode3_seg(long long max_chunks, int B) {
-    static int forced = -1;
-    if (forced < 0) {
+// segment length (chunks) for a stream of up to max_chunks chunks: 16; 8 for streams too small to fill
+// the GPU with 16-chunk segments (<= 2.5 M chunks of capacity, 80 MB: the parse's walk per lane is then
+// 1024 + 2048 bits instead of 1024 + 4096, and there are twice the jobs); 4 below 1 M chunks (32 MB:
+// 1024 + 1024 bits, four times the jobs -- still one round of parse waves, and a small stream's parse is
+// the length of one walk).  Short segments need tokens short enough (bound exponent B <= 12, e.g. 1e-3:
+// tokens of <= ~21 bits) for a repaired path to meet the recorded one within the segment -- at 1e-6 a
+// job's last segment could move its exit and decline the stream.  CT6 (no 3-bit codes: its paths run
+// side by side for longer, tools/sync_sim.py: 4% of 1024-bit pre-walks unsynchronised, 0.4% not met
+// within 4 chunks) takes 8 chunks or more; CT11 (32-bit verbatim tokens, a path
+// read out of phase stays out of phase until a 3-bit code realigns it) takes 8 or more.  The host sizes the scratch for
+// 4-chunk segments (DC_DEC3_SEG=4|8|16 forces one)
+static int g_seg_forced = -1;
+static int seg_forced() {
+    if (g_seg_forced < 0) {
         const char* e = getenv("DC_DEC3_SEG");
-        forced = (e && (atoi(e) == 8 || atoi(e) == 16)) ? atoi(e) : 0;
+        g_seg_forced = (e && (atoi(e) == 4 || atoi(e) == 8 || atoi(e) == 16)) ? atoi(e) : 0;
     }
+    return g_seg_forced;
+}
+// tests: force a segment length (4, 8 or 16; 0: by size); returns the previous setting
+extern "C" int dc_set_decode3_seg(int seg) {
+    const int old = seg_forced();
+    g_seg_forced = (seg == 4 || seg == 8 || seg == 16) ? seg : 0;
+    return old;
+}
+extern "C" int dc_decode3_seg(long long max_chunks, int B, int ct) {
+    const int forced = seg_forced();
     if (forced) return forced;
-    return (max_chunks <= 2500000ll && B <= 12) ? 8 : D3_SEG;
+    if (B > 12) return D3_SEG;
+    return (max_chunks <= 1000000ll && (ct == 5 || ct == 7)) ? 4 : (max_chunks <= 2500000ll ? 8 : D3_SEG);
 }
 
 // DC_DEC3_DEBUG=1: wait for every kernel (at most 2 s each) and report one that does not finish
@@ -832,24 +882,26 @@ extern "C" int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev
                                  hipStream_t st) {
     // resident grids per (CT, segment length) instantiation: every job of a call must be resident at once
     // (parse3's link wait, decode3's history wait), so each grid is sized from its own kernel's occupancy
-    static int gp[2][12], gd[2][12];
+    static int gp[3][12], gd[3][12];
     const int ci = (P->ct > 0 && P->ct < 12) ? P->ct : 0;
-    if (D3->seg != 8 && D3->seg != 16) return -2;
-    const int si = D3->seg == 16;
+    if (D3->seg != 4 && D3->seg != 8 && D3->seg != 16) return -2;
+    const int si = D3->seg == 16 ? 1 : (D3->seg == 4 ? 2 : 0);
     if (!gp[si][ci]) {
         const void* fp;
         const void* fd;
-        if (si) {
-            fp = P->ct == 5 ? (const void*)parse3_kernel<5, 16> : P->ct == 6 ? (const void*)parse3_kernel<6, 16>
-               : P->ct == 7 ? (const void*)parse3_kernel<7, 16> : (const void*)parse3_kernel<11, 16>;
-            fd = P->ct == 5 ? (const void*)decode3_kernel<5, 16> : P->ct == 6 ? (const void*)decode3_kernel<6, 16>
-               : P->ct == 7 ? (const void*)decode3_kernel<7, 16> : (const void*)decode3_kernel<11, 16>;
+#define DC_PICK3(KER, SEGV) (P->ct == 5 ? (const void*)KER<5, SEGV> : P->ct == 6 ? (const void*)KER<6, SEGV>   \
+                             : P->ct == 7 ? (const void*)KER<7, SEGV> : (const void*)KER<11, SEGV>)
+        if (si == 1) {
+            fp = DC_PICK3(parse3_kernel, 16);
+            fd = DC_PICK3(decode3_kernel, 16);
+        } else if (si == 2) {
+            fp = DC_PICK3(parse3_kernel, 4);
+            fd = DC_PICK3(decode3_kernel, 4);
         } else {
-            fp = P->ct == 5 ? (const void*)parse3_kernel<5, 8> : P->ct == 6 ? (const void*)parse3_kernel<6, 8>
-               : P->ct == 7 ? (const void*)parse3_kernel<7, 8> : (const void*)parse3_kernel<11, 8>;
-            fd = P->ct == 5 ? (const void*)decode3_kernel<5, 8> : P->ct == 6 ? (const void*)decode3_kernel<6, 8>
-               : P->ct == 7 ? (const void*)decode3_kernel<7, 8> : (const void*)decode3_kernel<11, 8>;
+            fp = DC_PICK3(parse3_kernel, 8);
+            fd = DC_PICK3(decode3_kernel, 8);
         }
+#undef DC_PICK3
         gp[si][ci] = resident3(fp, 64);
         gd[si][ci] = resident3(fd, 256);
     }

@@ -634,6 +634,9 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
 // encode never matches the tag (the host clears the array when the epoch wraps).  Every wait is bounded:
 // a look-back that times out poisons its tile (status 3, successors give up at once), stores nothing and
 // sets err bit 4; the host then re-encodes with the wait-free three-launch path (dc_encode_result).
+#ifndef DC_LB_KS
+#define DC_LB_KS 4                      // look-back windows of 64 states per round trip, with the scanner
+#endif
 #ifndef DC_LB_K
 #define DC_LB_K 8
 #endif
@@ -643,6 +646,8 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
 #ifndef DC_LB_SLEEP
 #define DC_LB_SLEEP 1
 #endif
+static_assert(DC_LB_K <= 8 && DC_LB_KS <= 8, "look-back windows read at most LB_PAD words before tile 0");
+constexpr long long LB_PAD = 512;                                 // readable words in front of the tile states
 constexpr int LB_KW = DC_LB_K;                                    // look-back: tiles per lane per round trip
 constexpr unsigned long long ST_VAL = (1ull << 40) - 1;
 constexpr unsigned long long ST_MASK = 3ull << 40, ST_AGG = 1ull << 40, ST_INC = 2ull << 40, ST_BAD = 3ull << 40;
@@ -668,7 +673,7 @@ __device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
 // wait timed out.
 template <int LB_K>
 __device__ __forceinline__ int enc_lookback(const uint64_t* __restrict__ st, long long t, uint32_t tag,
-                                            unsigned long long& excl, uint32_t& stat) {
+                                            unsigned long long& excl, uint32_t& stat, int start_bit) {
     const int lane = threadIdx.x & 63;
     long long base = t - 1;
     excl = 0;
@@ -677,11 +682,14 @@ __device__ __forceinline__ int enc_lookback(const uint64_t* __restrict__ st, lon
         uint64_t v[LB_K];
         int pinc;                                                         // first inclusive position (64 LB_K: none)
         for (;;) {
+            // one address, immediate offsets: positions before tile 0 read the LB_PAD words in front of the
+            // states (any value) and are replaced by the virtual inclusive state start_bit
+            const uint64_t* p = st + (base - lane);
 #pragma unroll
             for (int k = 0; k < LB_K; k++) {
                 const long long ti = base - (long long)(64 * k + lane);
-                const uint64_t w = ld_relaxed(st + (ti >= 0 ? ti : 0));
-                v[k] = ti >= 0 ? w : st_word(tag, ST_INC, 0);           // (before tile 0: offset 0)
+                const uint64_t w = ld_relaxed(p - 64 * k);
+                v[k] = ti >= 0 ? w : st_word(tag, ST_INC, (unsigned long long)start_bit);   // (before tile 0)
             }
             pinc = 64 * LB_K;
             int pinv = 64 * LB_K;                                         // first unpublished position
@@ -693,7 +701,9 @@ __device__ __forceinline__ int enc_lookback(const uint64_t* __restrict__ st, lon
                 if (um) pinv = 64 * k + __ffsll((long long)um) - 1;
                 if (im) pinc = 64 * k + __ffsll((long long)im) - 1;
             }
-            if (pinv > pinc) break;                                       // every needed state is published
+            // every needed state is published (pinv == pinc: the whole window, no inclusive state: go on
+            // past it)
+            if (pinv >= pinc) break;
             stat++;
             if (lane == (pinv & 63)) {                                    // its lane polls it alone
                 const long long ti = base - pinv;
@@ -979,6 +989,9 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
     __syncthreads();
     // ---- wave 0: the waves' boundary words, then the look-back for the tile's offset
     if (wid == 0) {
+        // the predecessor's last bits are requested before the look-back (published with its aggregate,
+        // they are there by now: one round trip less after the look-back)
+        const uint64_t tl0 = (lane == 0 && tile > 0) ? ld_relaxed(tl + tile - 1) : 0ull;
         if (lane < 4) {
             const uint32_t hi = s_hi[lane];
             if (hi != 0xFFFFFFFFu) {
@@ -1006,20 +1019,23 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
                 G = (v & ST_VAL) - T;
             }
         } else if (scan) {
-            // the scanner keeps the inclusive states close behind the published aggregates: a one-load
-            // look-back over the 64 predecessors mostly meets one (waiting for the scanner to reach this
-            // tile itself cost ~4 us per tile)
-            if (tile > 0) bad = enc_lookback<1>(st, tile, tag, G, lbst);
+            // the scanner keeps the inclusive states close behind the published aggregates, ~2-3 us
+            // behind this tile's own neighbours (which started with it): a look-back over DC_LB_KS x 64
+            // predecessors in one round trip mostly meets one (waiting for the scanner to reach this tile
+            // itself cost ~4 us per tile)
+            if (tile > 0) bad = enc_lookback<DC_LB_KS>(st, tile, tag, G, lbst, start_bit);
         } else if (tile > 0) {
-            bad = enc_lookback<LB_KW>(st, tile, tag, G, lbst);
+            bad = enc_lookback<LB_KW>(st, tile, tag, G, lbst, start_bit);
         }
         E1STAMP(4);
         if (lane == 0) {
             uint32_t tp = 0;
             if (tile > 0 && !bad) {                                       // the predecessor's last bits
                 const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-                uint64_t v;
-                while (((v = ld_relaxed(tl + tile - 1)) >> 32) != (uint64_t)epoch) {
+                uint64_t v = tl0;
+                while ((v >> 32) != (uint64_t)epoch) {
+                    v = ld_relaxed(tl + tile - 1);
+                    if ((v >> 32) == (uint64_t)epoch) break;
                     if (__builtin_amdgcn_s_memrealtime() - t0 > LB_WAIT) { bad = 1; break; }
                     __builtin_amdgcn_s_sleep(1);
                 }
@@ -1104,7 +1120,7 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
     if (mode == 1) {
         const int grid = (int)ntiles;
         dc_mark_phase(0, stream);
-        uint64_t* st = desc + desc_words_multi(ntiles);
+        uint64_t* st = desc + desc_words_multi(ntiles) + LB_PAD;
         static int scan = -1;                                            // DC_ENC_SCAN=0: chained look-back
         if (scan < 0) scan = (getenv("DC_ENC_SCAN") && *getenv("DC_ENC_SCAN") == '0') ? 0 : 1;
         DC_ENC_DISPATCH(encode_fused_kernel, dim3(grid + scan), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, st,
@@ -1155,7 +1171,7 @@ static long long desc_words_multi(long long nt) {
 }
 extern "C" long long dc_encode_desc_words(long long n) {
     const long long nt = dc_encode_tile_count(n);
-    return desc_words_multi(nt) + 2 * nt;
+    return desc_words_multi(nt) + LB_PAD + 2 * nt;
 }
 // the epochs a state tag tells apart: the host clears desc when its encode epoch reaches this
 extern "C" unsigned dc_encode_epoch_limit(void) { return ST_TAGM; }

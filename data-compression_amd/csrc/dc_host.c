@@ -71,6 +71,7 @@ typedef struct {
     int dec3_used;                   /* the pending decode ran the segment decoder */
     int dec3_last;                   /* the last finished decode's values came from it */
     int dec3_launched;               /* the last dc_decode_device launched it (it may decline later) */
+    int dec3_skip_once;              /* the next dc_decode_device takes the chunk-map decoder (halo planes) */
     const unsigned long long* dec_dnbits;   /* the pending decode's device bit count (or NULL) */
     unsigned long long dec_hnbits;          /* ... or its host bit count */
     const float* dec_hin;            /* its incoming values (shard mode 2) */
@@ -577,9 +578,11 @@ static int dec_next_epoch(void) {
 }
 
 /* segment decoder buffers for streams of up to max_chunks 256-bit chunks */
-static int dec3_ensure(long long max_chunks, int B) {
-    const int seg = dc_decode3_seg(max_chunks, B);
-    if (max_chunks <= G.dec3_cap && seg == G.D3.seg) return DC_OK;
+static int dec3_ensure(long long max_chunks, int B, int ct) {
+    const int seg = dc_decode3_seg(max_chunks, B, ct);
+    /* the kernels size their grids from D3.max_chunks: this stream's capacity, not the pool's (a small
+       stream after a large one would otherwise launch thousands of idle workgroups) */
+    if (max_chunks <= G.dec3_cap && seg == G.D3.seg) { G.D3.max_chunks = max_chunks; return DC_OK; }
     if (max_chunks > G.dec3_cap) {
         if (G.dec3_pool) HIPCHK(hipFree(G.dec3_pool));
         G.dec3_pool = NULL;
@@ -604,18 +607,20 @@ static int dec3_ensure(long long max_chunks, int B) {
         G.D3.hist = (uint64_t*)ptr[4];
         G.dec3_cap = max_chunks;
     }
-    G.D3.max_chunks = G.dec3_cap;
+    G.D3.max_chunks = max_chunks;
     G.D3.seg = seg;
     return DC_OK;
 }
 
-/* streams of at least this capacity use the segment decoder (DC_DEC3_MIN_BYTES; DC_DEC3=0 disables it) */
+/* streams of at least this capacity use the segment decoder (DC_DEC3_MIN_BYTES; DC_DEC3=0 disables it):
+   16 KiB -- from 2^12 floats on (r03: 1 MiB; 4-chunk segments made small streams one short walk) */
+#define DEC3_MIN_DEFAULT ((16ll << 10) + 1)
 static long long g_dec3_min = -2;
 static long long dec3_min_bytes(void) {
     if (g_dec3_min == -2) {
         const char* d = getenv("DC_DEC3");
         const char* e = getenv("DC_DEC3_MIN_BYTES");
-        g_dec3_min = (d && *d == '0') ? -1 : ((e && *e) ? atoll(e) : (1ll << 20) + 1);
+        g_dec3_min = (d && *d == '0') ? -1 : ((e && *e) ? atoll(e) : DEC3_MIN_DEFAULT);
     }
     return g_dec3_min;
 }
@@ -624,7 +629,7 @@ int dc_last_decode_was_v3(void) { return G.dec3_last; }
 int dc_last_decode_launched_v3(void) { return G.dec3_launched; }
 long long dc_set_decode3_min_bytes(long long v) {
     const long long old = dec3_min_bytes();
-    g_dec3_min = v < -1 ? (1ll << 20) + 1 : v;
+    g_dec3_min = v < -1 ? DEC3_MIN_DEFAULT : v;
     return old;
 }
 
@@ -654,13 +659,15 @@ int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsig
     /* the segment decoder reads whole 16-byte groups through a buffer resource (32-bit byte range): every
        stream byte must lie in one inside max_bytes, and max_bytes and the output below 2 GiB */
     const long long need16 = nbytes >= 0 ? (nbytes + 15) / 16 * 16 : 0;
-    G.dec3_used = m3 >= 0 && max_bytes >= m3 && max_bytes >= 16 && max_bytes >= need16 && max_bytes < (1ll << 31) && num < (1ll << 29) && !G.D.shard &&
+    const int no3 = G.dec3_skip_once;
+    G.dec3_skip_once = 0;
+    G.dec3_used = !no3 && m3 >= 0 && max_bytes >= m3 && max_bytes >= 16 && max_bytes >= need16 && max_bytes < (1ll << 31) && num < (1ll << 29) && !G.D.shard &&
                   !((uintptr_t)d_stream & 15u) && !((uintptr_t)d_out & 15u);
     G.dec3_launched = G.dec3_used;
     G.dec_dnbits = nbytes >= 0 ? NULL : d_nbits;
     G.dec_hnbits = nbytes >= 0 ? (unsigned long long)nbytes * 8ull : 0ull;
     if (G.dec3_used) {
-        if ((rc = dec3_ensure((max_bytes * 8 + 255) / 256 + 1, P.B))) return rc;
+        if ((rc = dec3_ensure((max_bytes * 8 + 255) / 256 + 1, P.B, ct))) return rc;
         G.D3.err = G.D.err;
         G.D3.capw = max_bytes / 16 * 4;
         if (dc_launch_decode3((const uint8_t*)d_stream, G.dec_dnbits, G.dec_hnbits, &P, &G.D3, (float*)d_out, num,
@@ -919,6 +926,9 @@ int dc_halo_decode_device(int ct, const void* d_stream, long long nbytes, const 
     const long long n = (long long)A * B;
     if (grow(&G.halo_a, &G.halo_a_cap, (size_t)n * 4 + 64)) return DC_ERR_HIP;
     const long long cap = nbytes >= 0 ? nbytes : (long long)dc_stream_capacity(n);
+    /* a plane is a runs-mode stream (copy runs), which the segment decoder declines: straight to the
+       chunk-map decoder */
+    G.dec3_skip_once = 1;
     if ((rc = dc_decode_device(ct, d_stream, nbytes, d_bits, cap, n, type, mask17, G.halo_a))) return rc;
     if ((rc = dc_decode_finish())) return rc;
     if (dc_launch_plane_scatter((const float*)G.halo_a, d_min, (float*)d_p, mj, mk, ijk, v, A, B, G.st))

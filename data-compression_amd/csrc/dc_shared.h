@@ -79,9 +79,9 @@ typedef struct Dec3Bufs {
     uint64_t* pexit;               /* [parse job] epoch << 32 | its last lane's exit (main walk) */
     uint64_t* hist;                /* [decode job][3] the job's last three values, epoch-tagged granules */
     unsigned* err;                 /* the DecBufs status word; 512 = this path declined the stream */
-    int seg;                       /* chunks per parse segment: 8 or 16 (dc_decode3_seg); the pre-walk is
-                                      1024 bits either way */
-    long long max_chunks;          /* capacity of rec */
+    int seg;                       /* chunks per parse segment: 4, 8 or 16 (dc_decode3_seg); the pre-walk is
+                                      1024 bits whatever seg */
+    long long max_chunks;          /* this stream's chunk capacity (<= the rec pool's) */
     long long capw;                /* readable words of the stream buffer (a multiple of 4, >= 4) */
 } Dec3Bufs;
 
@@ -124,7 +124,7 @@ int dc_launch_decode_serial(const uint8_t* s, const DC_NS Params* P, const DC_NS
 int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
                       const DC_NS Params* P, const DC_NS Dec3Bufs* D3, float* out, long long num, uint32_t epoch,
                       dc_hip_stream st);
-int dc_decode3_seg(long long max_chunks, int B);
+int dc_decode3_seg(long long max_chunks, int B, int ct);
 long long dc_ct1_tiles(long long n);
 int dc_launch_ct1_encode(const float* x, long long n, float thr_le, uint32_t* traw, unsigned long long* rawoff,
                          float* raw, char* codes, int* pos1, unsigned* err, dc_hip_stream st);

@@ -44,7 +44,7 @@ EXT_SYMBOLS = [
     "dc64_stream_capacity", "dc64_encode_device", "dc64_encode_result", "dc64_decode_device", "dc64_decode_finish",
     "dc64_last_decode_flags", "dc64_to_small_device", "dc64_med_device", "dc_set_encode_stream",
     "dc_decode_status", "dc_abi_status", "dc_med_sum_device", "dc_type_from_max", "dc_set_small_chunk_max_bytes",
-    "dc_set_decode3_min_bytes", "dc_last_decode_was_v3", "dc_last_decode_launched_v3",
+    "dc_set_decode3_min_bytes", "dc_set_decode3_seg", "dc_last_decode_was_v3", "dc_last_decode_launched_v3",
     "dc_encode_status", "dc_encode_mode", "dc_encode_retries", "dc_crc_resend_device",
 ]
 
@@ -406,9 +406,14 @@ class Lib:
         return int(self.L.dc_set_small_chunk_max_bytes(int(v)))
 
     def set_decode3_min_bytes(self, v):
-        """Streams of at least v bytes of capacity use the segment decoder (< -1: default 1 MiB + 1,
+        """Streams of at least v bytes of capacity use the segment decoder (< -1: default 16 KiB + 1,
         -1: never, 0: always); returns the previous value."""
         return int(self.L.dc_set_decode3_min_bytes(int(v)))
+
+    def set_decode3_seg(self, seg):
+        """Force the segment decoder's parse segment length (4, 8 or 16 chunks; 0: by size); returns the
+        previous setting."""
+        return int(self.L.dc_set_decode3_seg(int(seg)))
 
     def last_decode_was_v3(self):
         """Whether the last finished decode's values came from the segment decoder."""

@@ -156,9 +156,12 @@ long long dc_decode_chunk_bits_value(void);                 /* chunk bits of the
  * ones with the 1024-bit build (< 0: the default, 1 MiB; 0: never).  Returns the previous value. */
 long long dc_set_small_chunk_max_bytes(long long max_bytes);
 /* Streams of at least this capacity (bytes) decode with the segment decoder (dc_decode3.hip), which
- * hands streams it cannot take to the chunk-map decoder (< -1: the default, 1 MiB + 1; -1: never;
+ * hands streams it cannot take to the chunk-map decoder (< -1: the default, 16 KiB + 1; -1: never;
  * 0: every stream).  Returns the previous value. */
 long long dc_set_decode3_min_bytes(long long min_bytes);
+/* The segment decoder's parse segment length in 256-bit chunks: 4, 8 or 16 forces one, 0 chooses by the
+ * stream's capacity and bound (dc_decode3.hip dc_decode3_seg).  Returns the previous setting. */
+int dc_set_decode3_seg(int seg);
 /* 1 if the last decode's values came from the segment decoder (after dc_decode_finish). */
 int dc_last_decode_was_v3(void);
 /* 1: the last dc_decode_device launched the segment decoder (its values may still come from the chunk-map

@@ -153,3 +153,27 @@ def test_decode3_zero_runs(v3, oracle, ct, n, kind):
         assert v3.last_decode_was_v3() and not out.view(np.uint32).any()
     else:
         assert not v3.last_decode_was_v3()
+
+
+@pytest.mark.parametrize("seg", [4, 8, 16])
+@pytest.mark.parametrize("kind,n", [("u10", 1 << 20), ("u10", 12345), ("mixed", 500000), ("sparse", 400009),
+                                    ("u10", 4097)])
+@pytest.mark.parametrize("ct", CTS)
+def test_decode3_segment_lengths(v3, oracle, seg, kind, n, ct):
+    """Every parse segment length (4, 8, 16 chunks: the pre-walk, the record stores, the jobs per parse
+    job) decodes exactly; ordinary streams stay in the segment decoder at each."""
+    old = v3.set_decode3_seg(seg)
+    try:
+        v3.set_bound(1e-3)
+        x = _inputs(oracle, kind, n)
+        _, xs = oracle.to_small(x)
+        t, m17 = oracle.type_mask(xs)
+        s, nb, pos = v3.compress(ct, xs, t, m17)
+        out = v3.decompress(ct, s, n, t, m17)
+        spec, got = oracle.decompress(ct, s, n, 1e-3, t, m17)
+        assert got == n
+        assert np.array_equal(out.view(np.uint32), spec.view(np.uint32))
+        if kind == "u10":
+            assert v3.last_decode_was_v3(), "an ordinary stream left the segment decoder"
+    finally:
+        v3.set_decode3_seg(old)

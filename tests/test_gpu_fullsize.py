@@ -6,8 +6,8 @@ pinned to the compiled reference's fixtures in test_oracle.py):
   * the stream: its bit length (-> bytes and pos) and every byte (orc_compress),
   * the decode of that stream (orc_decompress_spec, the reference decoder's grammar),
   * that the decode completed on the fast path (dc_decode_status == 0) where the bench relies on it.
-At 2^28 floats the encoder has 65,536 tiles, so encode_scan_kernel runs its multi-pass carry loop
-(SCAN_CH = 16,384 tiles per pass, dc_encode.hip); 2^26 is exactly one pass.
+At 2^28 floats the single-pass encoder has 65,536 tiles (4x the bench's 16,384): its scanner workgroup and the
+tiles' look-backs over the scanner's inclusive states run 4x as long (encode_fused_kernel, dc_encode.hip).
 """
 import numpy as np
 import pytest
@@ -74,7 +74,7 @@ def test_config3_ct7_eq_2p28(dc, oracle):
 
 
 def test_ct7_u10_2p28(dc, oracle):
-    """The 2^28 end of the north_star sweep on real data (multi-pass encoder scan, 2^28 decode)."""
+    """The 2^28 end of the north_star sweep on real data (65,536 encoder tiles, 2^28 decode)."""
     _check(dc, oracle, 7, _u10(oracle, 1 << 28), 1e-3)
 
 
@@ -184,3 +184,37 @@ def test_encode_stream_orders_after_library_stream(dc, oracle):
             assert nb == nbo and pos == poso and np.array_equal(s, so)
     finally:
         dc.L.dc_set_encode_stream(None)
+
+
+def test_back_to_back_encodes_2p26(dc, oracle):
+    """The bench's timed loop: 48 single-pass encodes of the CT7 2^26 workload back to back on one stream.
+    The encoder's error word is sticky (only dc_encode_result's retry clears it), so any look-back or hand-off
+    timeout in any of them shows; every stream must equal the first, which equals the oracle's."""
+    import torch
+    dc.set_bound(1e-3)
+    n = 1 << 26
+    _, xs = oracle.to_small(_u10(oracle, n))
+    t, m17 = oracle.type_mask(xs)
+    dx = torch.from_numpy(xs).cuda()
+    cap = dc.stream_capacity(n)
+    st = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    first = torch.empty_like(st)
+    torch.cuda.synchronize()
+    dc.encode_device(7, dx.data_ptr(), n, first.data_ptr(), type_=t, mask17=m17)
+    nbits = dc.encode_result()
+    assert dc.encode_status() == 0
+    nb = (nbits + 7) // 8
+    so, nbo, _ = oracle.compress(7, xs, 1e-3, t, m17)
+    assert nb == nbo and np.array_equal(first[:nb].cpu().numpy(), so)
+    del so
+    same = True
+    for _ in range(48):
+        st.zero_()
+        dc.encode_device(7, dx.data_ptr(), n, st.data_ptr(), type_=t, mask17=m17)
+        dc.synchronize()
+        same &= bool(torch.equal(st[:nb], first[:nb]))
+    status = dc.encode_status()
+    assert status == 0, f"encoder error word 0x{status:x}"
+    assert same
+    del dx, st, first
+    torch.cuda.empty_cache()

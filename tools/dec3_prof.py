@@ -60,6 +60,9 @@ def main():
     print(f"parse: jobs {p[5]:.0f} tokens {p[4]:.0f} repair rounds {p[3]:.0f}")
     print(f"  per job (kcycles): main {p[0] / pj / 1e3:.1f} link wait {p[1] / pj / 1e3:.1f} repair {p[2] / pj / 1e3:.1f}")
     print(f"  per token per lane-walk (cycles): {p[0] / max(p[4] / 64, 1):.1f}")
+    print(f"  repair walks: {p[6] / max(p[3], 1) / 1e3:.1f} kcycles and {p[7] / max(p[3], 1):.2f} lines per round; "
+          f"max per job over {reps} decodes (kcycles): "
+          f"total {buf[16] / 1e3:.1f} main {buf[17] / 1e3:.1f} links {buf[18] / 1e3:.1f}")
     print(f"decode: jobs {p[13]:.0f} tokens {p[15]:.0f} pending lanes {p[14]:.0f}")
     print(f"  per job (kcycles): claim {p[8] / dj / 1e3:.2f} stage {p[9] / dj / 1e3:.2f} walk {p[10] / dj / 1e3:.2f} "
           f"pend {p[11] / dj / 1e3:.2f} store {p[12] / dj / 1e3:.2f}")

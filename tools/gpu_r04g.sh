@@ -3,7 +3,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-timeout -k 10 700 python3 -u -m pytest tests/test_gpu_codec.py tests/test_gpu_fullsize.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04_t.log 2>&1 || { tail -40 gpurun_out/r04_t.log; exit 1; }
+timeout -k 10 700 python3 -u -m pytest tests/test_gpu_codec.py tests/test_gpu_fullsize.py tests/test_gpu_decode3.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04_t.log 2>&1 || { tail -40 gpurun_out/r04_t.log; exit 1; }
 tail -1 gpurun_out/r04_t.log
 run() {  # lib passes
   DC_ENC_PASSES=$2 DCAMD_LIB=data-compression_amd/$1/libdcamd.so timeout -k 10 200 python3 -u bench.py --no-cpu --no-pipelined --no-extra --steps 20 > gpurun_out/ab.json 2> gpurun_out/ab.err || { tail -20 gpurun_out/ab.err; return 1; }
@@ -12,3 +12,5 @@ run() {  # lib passes
 for i in 1 2; do run lib 1 && run lib_sp 1 && run lib 2 || exit 1; done
 DC_DEBUG_STAMPS=1 timeout -k 10 120 python3 -u tools/fused_stamps.py > gpurun_out/fs.txt 2>&1 || { tail -20 gpurun_out/fs.txt; exit 1; }
 head -12 gpurun_out/fs.txt
+DCAMD_LIB=data-compression_amd/lib_p/libdcamd.so timeout -k 10 150 python3 -u tools/dec3_prof.py > gpurun_out/p3.txt 2>&1 || { tail -20 gpurun_out/p3.txt; exit 1; }
+cat gpurun_out/p3.txt
