@@ -909,36 +909,40 @@ def main():
 
 
 def e2e_run(C, W, steps, warmup):
-    """End-to-end multi-GPU step: every rank counts its shard's bits, the counts are
-    all-gathered (exclusive scan -> global start bit), each rank encodes its shard at (start mod 8), the
-    padded shards are all-gathered (RCCL over xGMI) into the single global stream on every rank, and each
-    rank decodes its own shard of that stream (deferred history, 12-byte exchange, prefix fix)."""
+    """End-to-end multi-GPU step, device-side: each rank encodes its shard at start bit 0 with
+    its global index (bit count left on the device), the bit counts and the shards are all-gathered (RCCL
+    over xGMI; slots sized from the warm-up's largest shard), one merge kernel scans the counts and lays
+    the shards into the single global stream on every rank, and each rank decodes its own shard with the
+    segment decoder, its first predictions fixed after a 12-byte all-gather of the previous shard's last
+    values.  No host read inside the timed steps; the status words are checked after them."""
     import torch
     L, dev, dcamd = C.L, C.dev, C.dcamd
     n, ct, typ, mask17, xs = W["n"], W["ct"], W["type"], W["mask17"], W["xs"]
     cap = L.stream_capacity(n)
-    local = torch.empty(cap, dtype=torch.uint8, device=dev)
+    local = torch.zeros(cap + 64, dtype=torch.uint8, device=dev)
     out = torch.empty(n, dtype=torch.float32, device=dev)
+    glob = torch.zeros((C.world * cap + 64) // 4 * 4, dtype=torch.uint8, device=dev)
+    d_count = torch.zeros(1, dtype=torch.int64, device=dev)
+    d_total = torch.zeros(1, dtype=torch.int64, device=dev)
     idx0 = C.rank * n
-    ws = C.world
-    meta = torch.zeros(1, dtype=torch.int64, device=dev)
+    slot = [(cap + 8 + 3) // 4 * 4]
 
     def step():
-        bits = L.encode_bits(ct, xs.data_ptr(), n, idx0, typ, mask17)
-        meta[0] = bits
-        parts = [torch.zeros_like(meta) for _ in range(ws)]
-        C.dist.all_gather(parts, meta)
-        counts = [int(p[0]) for p in parts]
-        starts, total = dcamd.shard_offsets(counts)
-        sb = starts[C.rank] % 8
-        L.encode_device(ct, xs.data_ptr(), n, local.data_ptr(), idx0=idx0, type_=typ, mask17=mask17, start_bit=sb)
-        L.synchronize()
-        glob, tot = dcamd.gather_stream(local[: (sb + bits + 7) // 8], sb, sb + bits)
-        dcamd.decode_sharded(L, ct, glob, glob.numel(), starts[C.rank], bits, n, out, typ, mask17)
-        return tot
+        L.encode_device(ct, xs.data_ptr(), n, local.data_ptr(), idx0=idx0, type_=typ, mask17=mask17, start_bit=0,
+                        total_ptr=d_count.data_ptr())
+        dcamd.gather_stream_device(L, local, d_count, slot[0], glob, d_total)
+        dcamd.decode_sharded_device(L, ct, local, d_count, (cap + 64) // 16 * 16, n, out, typ, mask17)
 
     for _ in range(max(warmup, 1)):
-        total = step()
+        step()
+    L.synchronize()
+    torch.cuda.synchronize()
+    # the slot for the timed steps: the warm-up's largest shard (a real run takes the previous step's)
+    mx = torch.tensor([int(d_count.item())], dtype=torch.int64, device=dev)
+    C.dist.all_reduce(mx, op=C.dist.ReduceOp.MAX)
+    slot[0] = min((int(mx.item()) + 7) // 8 + 64 + 3, cap + 8 + 3) // 4 * 4
+    for _ in range(max(warmup, 1)):
+        step()
     C.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -947,11 +951,18 @@ def e2e_run(C, W, steps, warmup):
     L.synchronize()
     torch.cuda.synchronize()
     wall = C.max_over_ranks(time.perf_counter() - t0)
+    st = {"encode": L.encode_status(), "merge": L.merge_status(), "decode": L.decode_status()}
+    if any(st.values()):
+        print(f"bench.py: end-to-end status words {st} after the timed steps", file=sys.stderr)
+        sys.exit(1)
+    total = int(d_total.item())
     return {"value": round(C.world * 4.0 * n / (wall / steps) / 1e9, 3), "ms_per_step": round(wall / steps * 1e3, 4),
-            "global_stream_bytes": (int(total) + 7) // 8,
-            "how": "count + all-gather of shard bit counts + encode at the global bit offset + all-gather of the "
-                   "padded shards into the single global stream + per-rank shard decode with the 12-byte history "
-                   "exchange, host-synchronised between phases"}
+            "global_stream_bytes": (total + 7) // 8, "slot_bytes": slot[0],
+            "how": "encode at start bit 0 (device bit count) + all-gather of the bit counts and of the shards "
+                   "(slots from the warm-up's largest) + one merge kernel (device exscan, shifted shards, "
+                   "OR-ed shared words) into the single global stream on every rank + segment-decoder shard "
+                   "decode with a 12-byte all-gather of the previous shard's last values and a one-wave "
+                   "prefix fix; no host read inside the timed steps"}
 
 
 if __name__ == "__main__":

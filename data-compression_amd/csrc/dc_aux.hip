@@ -530,16 +530,28 @@ __device__ __forceinline__ uint32_t xpow8n(unsigned long long n, const uint32_t*
 // on the host from zlib's byte table); CRC is linear over GF(2), so the block value is the XOR of
 // every run's CRC times x^(8 * bytes after it) -- for full blocks a per-lane host constant
 // kpow[j] = x^(8 * CRC_RUN * j), so the combine is one carry-less multiply and an XOR reduction.
+// DC_CRC_NIB (default): the word step by eight 16-entry nibble tables (nib[j][v] = the byte table entry of
+// nibble j alone: CRC is linear, T[b] = T[b & 15] ^ T[b & 0xF0]).  A wave's 64 lookups into one 16-entry
+// table hit at most 16 banks, each address once or broadcast -- no bank conflicts -- where the four
+// 256-entry byte tables' random lookups serialised on conflicts (the CRC pass ran at ~2 TB/s).
+#ifndef DC_CRC_NIB
+#define DC_CRC_NIB 1
+#endif
 __global__ __launch_bounds__(256) void crc_blocks_kernel(const uint8_t* __restrict__ s, long long nbytes,
                                                          const uint32_t* __restrict__ tab_g,
                                                          const uint32_t* __restrict__ kpow_g,
                                                          const uint32_t* __restrict__ x2n_g,
                                                          uint32_t* __restrict__ part) {
     __shared__ uint32_t tab[4][256];
+    __shared__ uint32_t nib[8 * 16];
     __shared__ uint32_t x2n[32];
     __shared__ uint32_t red[4];
     const int t = threadIdx.x;
     for (int k = 0; k < 4; k++) tab[k][t] = tab_g[k * 256 + t];
+    if (t < 128) {                                   // nibble j of the word c: byte table 3 - j/2
+        const int j = t >> 4, v = t & 15;
+        nib[t] = tab_g[(3 - (j >> 1)) * 256 + ((j & 1) ? (v << 4) : v)];
+    }
     if (t < 32) x2n[t] = x2n_g[t];
     const uint32_t kfull = kpow_g[255 - t];
     __syncthreads();
@@ -559,7 +571,14 @@ __global__ __launch_bounds__(256) void crc_blocks_kernel(const uint8_t* __restri
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const uint32_t c = r ^ w[j];
-                    r = tab[3][c & 0xFFu] ^ tab[2][(c >> 8) & 0xFFu] ^ tab[1][(c >> 16) & 0xFFu] ^ tab[0][c >> 24];
+                    if (DC_CRC_NIB) {
+                        r = (nib[0 * 16 + (c & 15u)] ^ nib[1 * 16 + ((c >> 4) & 15u)]) ^
+                            (nib[2 * 16 + ((c >> 8) & 15u)] ^ nib[3 * 16 + ((c >> 12) & 15u)]) ^
+                            ((nib[4 * 16 + ((c >> 16) & 15u)] ^ nib[5 * 16 + ((c >> 20) & 15u)]) ^
+                             (nib[6 * 16 + ((c >> 24) & 15u)] ^ nib[7 * 16 + (c >> 28)]));
+                    } else {
+                        r = tab[3][c & 0xFFu] ^ tab[2][(c >> 8) & 0xFFu] ^ tab[1][(c >> 16) & 0xFFu] ^ tab[0][c >> 24];
+                    }
                 }
             }
         } else {
@@ -795,6 +814,89 @@ extern "C" int dc_launch_bit_shift_copy(const uint8_t* s, long long sbytes, unsi
     long long g = (nout + 255) / 256;
     if (g > 8192) g = 8192;
     hipLaunchKernelGGL(bit_shift_copy_kernel, dim3((unsigned)g), dim3(256), 0, st, s, sbytes, start_bit, nbits, d, nout);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// The multi-GPU all-gather's product: world shard streams, each encoded
+// at start bit 0 and all-gathered into slots of P bytes (g[r * P ..]), with their bit counts counts[r]
+// (device), become the single global stream: shard r's bits land at the exclusive sum of the counts
+// before it, shifted across byte boundaries, the words two shards share OR-ed.  Every workgroup scans
+// the counts itself (no scan launch, no host read); thread = one 32-bit output word, MSB-first (stored
+// byte-swapped: the stream's bytes in order).  err |= 1: a shard longer than its slot (P < bytes + 8);
+// 2: the global stream longer than the output (nothing is written then).
+constexpr int MERGE_MAXW = 1024;
+__device__ __forceinline__ uint32_t be_word(const uint8_t* p, long long i) {
+    return __builtin_bswap32(reinterpret_cast<const uint32_t*>(p)[i]);
+}
+__global__ __launch_bounds__(256) void merge_shards_kernel(const uint8_t* __restrict__ g, long long P, int world,
+                                                           const unsigned long long* __restrict__ counts,
+                                                           uint32_t* __restrict__ out, long long out_bytes,
+                                                           unsigned long long* __restrict__ total_out,
+                                                           unsigned* __restrict__ err) {
+    __shared__ unsigned long long st[MERGE_MAXW + 1];
+    __shared__ int bad;
+    if (threadIdx.x == 0) {
+        unsigned long long acc = 0;
+        int b = 0;
+        for (int r = 0; r < world; r++) {
+            st[r] = acc;
+            acc += counts[r];
+            if ((long long)((counts[r] + 7) / 8) + 8 > P) b |= 1;
+        }
+        st[world] = acc;
+        if ((long long)((acc + 31) / 32) * 4 > out_bytes) b |= 2;
+        bad = b;
+        if (blockIdx.x == 0) {
+            *total_out = acc;
+            if (b) atomicOr(err, (unsigned)b);
+        }
+    }
+    __syncthreads();
+    if (bad) return;
+    const unsigned long long total = st[world];
+    const long long nw = (long long)((total + 31) / 32);
+    for (long long w = (long long)blockIdx.x * 256 + threadIdx.x; w < nw; w += (long long)gridDim.x * 256) {
+        const long long lo = 32 * w;
+        int r0 = 0, r1 = world - 1;                 // the last shard starting at or before bit lo
+        while (r0 < r1) {
+            const int m = (r0 + r1 + 1) >> 1;
+            if ((long long)st[m] <= lo) r0 = m;
+            else r1 = m - 1;
+        }
+        uint32_t acc = 0;
+        for (int r = r0; r < world && (long long)st[r] < lo + 32; r++) {
+            const long long cnt = (long long)counts[r];
+            if (cnt == 0) continue;
+            const long long o = lo - (long long)st[r];                    // shard bit at the word's first bit
+            const uint8_t* b = g + (long long)r * P;
+            uint32_t v, keep;
+            if (o >= 0) {
+                if (o >= cnt) continue;
+                const long long i = o >> 5;
+                const int sh = (int)(o & 31);
+                v = sh ? __builtin_amdgcn_alignbit(be_word(b, i), be_word(b, i + 1), 32 - sh) : be_word(b, i);
+                const long long nv = min(cnt - o, 32ll);                  // valid bits from the word's top
+                keep = nv >= 32 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> nv);
+            } else {
+                const int sh = (int)(-o);                                  // the shard starts at bit sh
+                v = be_word(b, 0) >> sh;
+                const long long nv = min(cnt, (long long)(32 - sh));
+                keep = (0xFFFFFFFFu >> sh) & ~(nv + sh >= 32 ? 0u : 0xFFFFFFFFu >> (nv + sh));
+            }
+            acc |= v & keep;
+        }
+        out[w] = __builtin_bswap32(acc);
+    }
+}
+
+extern "C" int dc_launch_merge_shards(const uint8_t* g, long long P, int world, const unsigned long long* counts,
+                                      uint8_t* out, long long out_bytes, unsigned long long* total_out, unsigned* err,
+                                      long long max_bytes, hipStream_t st) {
+    if (world < 1 || world > MERGE_MAXW || (P & 3) || ((uintptr_t)g & 3) || ((uintptr_t)out & 3)) return -2;
+    long long grid = (max_bytes / 4 + 255) / 256 + 1;
+    if (grid > 8192) grid = 8192;
+    hipLaunchKernelGGL(merge_shards_kernel, dim3((unsigned)grid), dim3(256), 0, st, g, P, world, counts,
+                       reinterpret_cast<uint32_t*>(out), out_bytes, total_out, err);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -52,7 +52,7 @@ constexpr unsigned long long D3_LINK_WAIT = 20000;  // s_memrealtime ticks (100 
 // why (diagnostic bits beside 512): 1024 runs mode / capacity, 2048 unresolved link, 4096 fewer tokens
 // than values, 8192 a job denser than its buffer, 16384 the history sentinel or an early prediction
 constexpr uint32_t D3_WHY_RUNS = 1024u, D3_WHY_LINK = 2048u, D3_WHY_SHORT = 4096u, D3_WHY_DENSE = 8192u,
-                   D3_WHY_SENT = 16384u;
+                   D3_WHY_SENT = 16384u, D3_WHY_SHARD = 65536u;   // (32768: D3_ZMISS)
 
 // DC_DEC3_PROF builds (make XDEFS=-DDC_DEC3_PROF B=build_p L=lib_p): per-section shader-clock totals
 // summed over waves into g_prof3 (read with dc_dec3_prof_read; tools/dec3_prof.py)
@@ -291,6 +291,7 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
     const bool over = G.nchunks > D3.max_chunks, runs = !over && runs_mode(CT, G.nbits, num);
     const bool decline = over || runs;
     if (over && blockIdx.x == 0 && lane == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_RUNS);
+    if (D3.shard && blockIdx.x == 0 && lane == 0) D3.spend[0] = 0u;     // (decode3 runs after this kernel)
     if (runs) zero_run_check(rs, G, num, D3.err);      // decode3 fills zeros, or hands the stream over
     __syncthreads();
     Ring3 r;
@@ -648,7 +649,8 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
                             const int need = (int)cc - 4;
                             if (t < need || t - need < pend || (g == 0 && t < 3)) {
                                 pend = t + 1;                                // needs the previous chunk's values
-                                sent |= g == 0 && t < 3;                     // a prediction among the stream's first 3
+                                // a prediction among the stream's first 3 (a shard's: its incoming values)
+                                sent |= g == 0 && t < 3 && !D3.shard;
                                 v = 0u;
                             } else {
                                 const float pv = predict_value(need, ob[o - 1], ob[o - 2], ob[o - 3]);
@@ -681,6 +683,13 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
                     h[k - 1] = i >= al ? ob[i] : (job > 0 ? prev_job_value(D3, job, al - i, epoch) : 0.0f);
                 }
                 float b1 = h[0], b2 = h[1], b3 = h[2];
+                if (D3.shard && g == 0) {
+                    // a shard's first chunk: its prefix waits for the values before the shard (zeros here,
+                    // re-decoded by shard3_fix_kernel).  Values after the prefix never read it; if the
+                    // prefix reaches the chunk's last three (read by the next chunk), hand the shard over
+                    D3.spend[0] = (uint32_t)pend;
+                    if (pend > n - 3) atomicOr(D3.err, D3_DECLINE | D3_WHY_SHARD);
+                }
                 Rd3 r;
                 r.init(L, lane, e);
                 for (int t = 0; t < pend; t++) {
@@ -777,6 +786,44 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
         }
     }
     P3_FLUSH();
+}
+
+// A shard's first pending tokens (D3.spend[0] of its first chunk, which starts at stream bit 0), decoded
+// again from the three values before the shard (hin: b1, b2, b3 = the previous shard's last three values,
+// last first), one token after another as impl/dataCompression.c:1900-2027 reads them.
+template <int CT>
+__global__ __launch_bounds__(64) void shard3_fix_kernel(const uint8_t* __restrict__ s, Params P, Dec3Bufs D3,
+                                                       const float* __restrict__ hin, float* __restrict__ out,
+                                                       long long num) {
+    if (threadIdx.x != 0) return;
+    const int np = (int)min((long long)D3.spend[0], num);
+    if (np <= 0) return;
+    const __amdgpu_buffer_rsrc_t rs = stream_rsrc(s, D3.capw);
+    float b1 = hin[0], b2 = hin[1], b3 = hin[2];
+    uint4 w = load_w4(rs, 1ll << 40, 0);           // (the prefix lies in the chunk's first 288 bits)
+    uint32_t win[12] = {w.x, w.y, w.z, w.w};
+    w = load_w4(rs, 1ll << 40, 4);
+    win[4] = w.x; win[5] = w.y; win[6] = w.z; win[7] = w.w;
+    w = load_w4(rs, 1ll << 40, 8);
+    win[8] = w.x; win[9] = w.y; win[10] = w.z; win[11] = w.w;
+    int pos = 0;
+    bool sent = false;
+    for (int t = 0; t < np; t++) {
+        const int wi = pos >> 5, sh = pos & 31;
+        if (wi + 1 >= 12) break;                    // (never: a chunk's tokens start within its 256 bits)
+        const uint32_t tk = sh ? __builtin_amdgcn_alignbit(win[wi], win[wi + 1], 32 - sh) : win[wi];
+        const int len = token_len_bf<CT>(tk, P);
+        int code = 0;
+        uint32_t v = token_pattern_bf<CT>(tk, len, P, &code);
+        if (code > 0) {
+            v = __float_as_uint(predict_value(code, b1, b2, b3));
+            sent |= v == 0xBF800000u;
+        }
+        out[t] = __uint_as_float(v);
+        b3 = b2; b2 = b1; b1 = __uint_as_float(v);
+        pos += len;
+    }
+    if (sent) atomicOr(D3.err, D3_DECLINE | D3_WHY_SENT);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -919,6 +966,18 @@ extern "C" int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev
     if (getenv("DC_DEC3_DEBUG") && hipStreamQuery(st) != hipSuccess) dbg_dump(D3);
     dc_mark_phase(7, st);
     dc_mark_next_set();
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int dc_launch_shard3_fix(const uint8_t* s, const Params* P, const Dec3Bufs* D3, const float* hin, float* out,
+                                    long long num, hipStream_t st) {
+    switch (P->ct) {
+        case 5: hipLaunchKernelGGL(shard3_fix_kernel<5>, dim3(1), dim3(64), 0, st, s, *P, *D3, hin, out, num); break;
+        case 6: hipLaunchKernelGGL(shard3_fix_kernel<6>, dim3(1), dim3(64), 0, st, s, *P, *D3, hin, out, num); break;
+        case 7: hipLaunchKernelGGL(shard3_fix_kernel<7>, dim3(1), dim3(64), 0, st, s, *P, *D3, hin, out, num); break;
+        case 11: hipLaunchKernelGGL(shard3_fix_kernel<11>, dim3(1), dim3(64), 0, st, s, *P, *D3, hin, out, num); break;
+        default: return -2;
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -72,6 +72,12 @@ typedef struct {
     int dec3_last;                   /* the last finished decode's values came from it */
     int dec3_launched;               /* the last dc_decode_device launched it (it may decline later) */
     int dec3_skip_once;              /* the next dc_decode_device takes the chunk-map decoder (halo planes) */
+    const uint8_t* sh3_s;            /* the last dc_decode_shard3_device call (for its fix) */
+    Params sh3_P;
+    Dec3Bufs sh3_D3;
+    float* sh3_out;
+    long long sh3_num;
+    int sh3_ok;
     const unsigned long long* dec_dnbits;   /* the pending decode's device bit count (or NULL) */
     unsigned long long dec_hnbits;          /* ... or its host bit count */
     const float* dec_hin;            /* its incoming values (shard mode 2) */
@@ -588,23 +594,25 @@ static int dec3_ensure(long long max_chunks, int B, int ct) {
         G.dec3_pool = NULL;
         const long long C = max_chunks + 4096;
         const long long DJ = C / 64 + 64, PJ = C / (64 * 4) + 64;
-        size_t sz[5], off = 0, tot = 0;
+        size_t sz[6], off = 0, tot = 0;
         sz[0] = (size_t)C * 2;                /* rec */
         sz[1] = (size_t)DJ * 4;               /* rel */
         sz[2] = (size_t)PJ * 4;               /* ptot */
         sz[3] = (size_t)PJ * 8;               /* pexit */
         sz[4] = (size_t)DJ * 3 * 8;           /* hist */
-        for (int i = 0; i < 5; i++) tot += (sz[i] + 255) & ~(size_t)255;
+        sz[5] = 256;                          /* spend */
+        for (int i = 0; i < 6; i++) tot += (sz[i] + 255) & ~(size_t)255;
         HIPCHK(hipMalloc(&G.dec3_pool, tot));
         HIPCHK(hipMemsetAsync(G.dec3_pool, 0, tot, G.st));
         char* b = (char*)G.dec3_pool;
-        void* ptr[5];
-        for (int i = 0; i < 5; i++) { ptr[i] = b + off; off += (sz[i] + 255) & ~(size_t)255; }
+        void* ptr[6];
+        for (int i = 0; i < 6; i++) { ptr[i] = b + off; off += (sz[i] + 255) & ~(size_t)255; }
         G.D3.rec = (uint16_t*)ptr[0];
         G.D3.rel = (uint32_t*)ptr[1];
         G.D3.ptot = (uint32_t*)ptr[2];
         G.D3.pexit = (uint64_t*)ptr[3];
         G.D3.hist = (uint64_t*)ptr[4];
+        G.D3.spend = (uint32_t*)ptr[5];
         G.dec3_cap = max_chunks;
     }
     G.D3.max_chunks = max_chunks;
@@ -687,6 +695,80 @@ int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsig
     return DC_OK;
 }
 
+/* ---- a shard of a longer stream through the segment decoder (the multi-GPU step):
+   the shard was encoded at start bit 0 with its global index (its first predictions read the previous
+   shard's last values), its bit count is on the device.  Nothing is read back: predictions among its
+   first tokens are decoded as pending and fixed by dc_decode_shard3_fix once the previous shard's last
+   three values are here; a stream the segment decoder declines sets the status word (dc_decode_status),
+   and the caller decodes the shard again on the chunk-map path (dc_decode_shard_device). */
+int dc_decode_shard3_device(int ct, const void* d_stream, const unsigned long long* d_nbits, long long max_bytes,
+                            long long num, int type, uint32_t mask17, void* d_out) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (!valid_ct(ct)) return seterr(DC_ERR_ARG, "unsupported CT %d", ct);
+    if (ct == 7 && (type < 1 || type > 7)) return seterr(DC_ERR_ARG, "CT7 type %d outside 1..7", type);
+    if (!d_nbits || num < 3) return seterr(DC_ERR_ARG, "need the device bit count and num >= 3");
+    if (((uintptr_t)d_stream & 15u) || ((uintptr_t)d_out & 15u) || max_bytes < 16 || max_bytes >= (1ll << 31) ||
+        num >= (1ll << 29))
+        return seterr(DC_ERR_ARG, "shard outside the segment decoder's limits (16-byte aligned, < 2 GiB)");
+    if ((rc = dec_ensure((max_bytes * 8 + 1023) / 1024 + 1))) return rc;
+    if ((rc = dec_next_epoch())) return rc;
+    Params P;
+    make_params(&P, ct, type, mask17);
+    if ((rc = dec3_ensure((max_bytes * 8 + 255) / 256 + 1, P.B, ct))) return rc;
+    G.D3.err = G.D.err;
+    G.D3.capw = max_bytes / 16 * 4;
+    G.D3.shard = 1;
+    const int lrc = dc_launch_decode3((const uint8_t*)d_stream, d_nbits, 0ull, &P, &G.D3, (float*)d_out, num,
+                                      G.dec_epoch, G.st);
+    G.D3.shard = 0;
+    if (lrc) return seterr(DC_ERR_HIP, "shard decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+    G.sh3_s = (const uint8_t*)d_stream;
+    G.sh3_P = P;
+    G.sh3_D3 = G.D3;
+    G.sh3_out = (float*)d_out;
+    G.sh3_num = num;
+    G.sh3_ok = 1;
+    return DC_OK;
+}
+
+/* the all-gathered shards (world slots of slot_bytes, each a shard encoded at start bit 0) and their
+   all-gathered bit counts (device) -> the single global stream in d_out (out_bytes of room) and its bit
+   count in d_total; no host read (the status word: dc_merge_status) */
+int dc_merge_shards_device(const void* d_gathered, long long slot_bytes, int world, const unsigned long long* d_counts,
+                           void* d_out, long long out_bytes, unsigned long long* d_total) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (!d_gathered || !d_counts || !d_out || !d_total || world < 1 || slot_bytes < 16 || (slot_bytes & 3) ||
+        ((uintptr_t)d_gathered & 3u) || ((uintptr_t)d_out & 3u))
+        return seterr(DC_ERR_ARG, "merge: bad buffers (4-byte aligned, slot a multiple of 4 bytes)");
+    if (dc_launch_merge_shards((const uint8_t*)d_gathered, slot_bytes, world, d_counts, (uint8_t*)d_out, out_bytes,
+                               d_total, G.d_enc_err + 4, out_bytes, G.st))
+        return seterr(DC_ERR_HIP, "merge launch failed");
+    return DC_OK;
+}
+
+/* 1: a shard longer than its slot, 2: the global stream longer than the output (sticky; reset = 1 clears) */
+int dc_merge_status(unsigned* status_out, int reset) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[3], G.d_enc_err + 4, 4, hipMemcpyDeviceToHost, G.st));
+    HIPCHK(hipStreamSynchronize(G.st));
+    *status_out = (unsigned)(G.h_scratch[3] & 0xFFFFFFFFu);
+    if (reset) HIPCHK(hipMemsetAsync(G.d_enc_err + 4, 0, 4, G.st));
+    return DC_OK;
+}
+
+/* d_hin: the previous shard's last three values, last first (device, 3 floats) */
+int dc_decode_shard3_fix(const float* d_hin) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (!G.sh3_ok) return seterr(DC_ERR_ARG, "no shard decode to fix");
+    if (dc_launch_shard3_fix(G.sh3_s, &G.sh3_P, &G.sh3_D3, d_hin, G.sh3_out, G.sh3_num, G.st))
+        return seterr(DC_ERR_HIP, "shard fix launch failed");
+    return DC_OK;
+}
+
 static int read_dec_err(unsigned* err) {
     HIPCHK(hipMemcpyAsync(&G.h_scratch[2], G.D.err, 4, hipMemcpyDeviceToHost, G.st));
     HIPCHK(hipMemcpyAsync(&G.h_scratch[12], G.D.plan, sizeof(Plan), hipMemcpyDeviceToHost, G.st));
@@ -704,6 +786,17 @@ int dc_decode_status(unsigned* status_out) {
     unsigned err = 0;
     if ((rc = read_dec_err(&err))) return rc;
     if (status_out) *status_out = err;
+    return DC_OK;
+}
+
+/* clear the decoder's status word (after a dc_decode_shard3_device that declined, before the caller
+   decodes the shard again on the other path) */
+int dc_decode_status_clear(void) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
+    G.dec_pending = 0;
+    G.dec_queued = 0;
     return DC_OK;
 }
 

@@ -83,6 +83,11 @@ typedef struct Dec3Bufs {
                                       1024 bits whatever seg */
     long long max_chunks;          /* this stream's chunk capacity (<= the rec pool's) */
     long long capw;                /* readable words of the stream buffer (a multiple of 4, >= 4) */
+    int shard;                     /* 1: the stream is a shard of a longer one (dc_decode_shard3_device):
+                                      predictions among its first tokens read the three values before
+                                      it, which come later -- decoded as pending, fixed by
+                                      dc_decode_shard3_fix */
+    uint32_t* spend;               /* [0] tokens of the shard's first chunk that wait for those values */
 } Dec3Bufs;
 
 #ifdef __cplusplus
@@ -124,6 +129,11 @@ int dc_launch_decode_serial(const uint8_t* s, const DC_NS Params* P, const DC_NS
 int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
                       const DC_NS Params* P, const DC_NS Dec3Bufs* D3, float* out, long long num, uint32_t epoch,
                       dc_hip_stream st);
+int dc_launch_merge_shards(const uint8_t* g, long long P, int world, const unsigned long long* counts, uint8_t* out,
+                           long long out_bytes, unsigned long long* total_out, unsigned* err, long long max_bytes,
+                           dc_hip_stream st);
+int dc_launch_shard3_fix(const uint8_t* s, const DC_NS Params* P, const DC_NS Dec3Bufs* D3, const float* hin,
+                         float* out, long long num, dc_hip_stream st);
 int dc_decode3_seg(long long max_chunks, int B, int ct);
 long long dc_ct1_tiles(long long n);
 int dc_launch_ct1_encode(const float* x, long long n, float thr_le, uint32_t* traw, unsigned long long* rawoff,

@@ -46,6 +46,8 @@ EXT_SYMBOLS = [
     "dc_decode_status", "dc_abi_status", "dc_med_sum_device", "dc_type_from_max", "dc_set_small_chunk_max_bytes",
     "dc_set_decode3_min_bytes", "dc_set_decode3_seg", "dc_last_decode_was_v3", "dc_last_decode_launched_v3",
     "dc_encode_status", "dc_encode_mode", "dc_encode_retries", "dc_crc_resend_device",
+    "dc_merge_shards_device", "dc_merge_status", "dc_decode_shard3_device", "dc_decode_shard3_fix",
+    "dc_decode_status_clear",
 ]
 
 
@@ -80,6 +82,10 @@ class Lib:
         L.dc_decode_device.argtypes = [C.c_int, vp, ll, vp, ll, ll, C.c_int, u32, vp]
         L.dc_decode_shard_device.argtypes = [C.c_int, vp, ll, C.c_ulonglong, C.c_ulonglong, ll, C.c_int, u32, vp, vp]
         L.dc_decode_shard_fix.argtypes = [vp]
+        L.dc_merge_shards_device.argtypes = [vp, ll, C.c_int, vp, vp, ll, vp]
+        L.dc_merge_status.argtypes = [C.POINTER(C.c_uint), C.c_int]
+        L.dc_decode_shard3_device.argtypes = [C.c_int, vp, vp, ll, ll, C.c_int, u32, vp]
+        L.dc_decode_shard3_fix.argtypes = [vp]
         L.dc_to_small_device.argtypes = [vp, ll, vp, C.POINTER(C.c_float)]
         L.dc_med_device.argtypes = [vp, ll, C.POINTER(C.c_float), C.POINTER(C.c_int)]
         L.dc_med_sum_device.argtypes = [vp, ll, C.c_float, C.POINTER(C.c_float), C.POINTER(C.c_float)]
@@ -400,6 +406,28 @@ class Lib:
     def decode_finish(self):
         self.check(self.L.dc_decode_finish(), "dc_decode_finish")
 
+    def merge_shards_device(self, gathered_ptr, slot_bytes, world, counts_ptr, out_ptr, out_bytes, total_ptr):
+        """World all-gathered shards (slots of slot_bytes) + their device bit counts -> the global stream
+        and its device bit count (dc_gpu.h); no host read."""
+        self.check(self.L.dc_merge_shards_device(gathered_ptr, slot_bytes, world, counts_ptr, out_ptr, out_bytes,
+                                                 total_ptr), "dc_merge_shards_device")
+
+    def merge_status(self, reset=False):
+        v = C.c_uint(0)
+        self.check(self.L.dc_merge_status(C.byref(v), 1 if reset else 0), "dc_merge_status")
+        return v.value
+
+    def decode_shard3_device(self, ct, s_ptr, nbits_ptr, max_bytes, num, out_ptr, type_=0, mask17=0):
+        """A shard encoded at start bit 0 through the segment decoder, its first predictions pending."""
+        self.check(self.L.dc_decode_shard3_device(ct, s_ptr, nbits_ptr, max_bytes, num, type_, mask17, out_ptr),
+                   "dc_decode_shard3_device")
+
+    def decode_shard3_fix(self, hin_ptr):
+        self.check(self.L.dc_decode_shard3_fix(hin_ptr), "dc_decode_shard3_fix")
+
+    def decode_status_clear(self):
+        self.check(self.L.dc_decode_status_clear(), "dc_decode_status_clear")
+
     def set_small_chunk_max_bytes(self, v):
         """Streams of at most v bytes of capacity use the 256-bit-chunk decoder build (< 0: default 1 MiB,
         0: never); returns the previous value."""
@@ -682,6 +710,77 @@ def decode_sharded(L, ct, stream, stream_bytes, start_bit, nbits, num, out, type
         return tail3()
 
     settle_history(tail3, fix, group)
+    return out
+
+
+# ---- the device-side multi-GPU step (no host reads inside the step) ---------------
+def _lib_stream(L, dev):
+    import torch
+    return torch.cuda.ExternalStream(L.L.dc_get_stream(), device=dev)
+
+
+def _after(src, dst):
+    """dst waits for the work queued on src so far."""
+    import torch
+    ev = torch.cuda.Event()
+    ev.record(src)
+    dst.wait_event(ev)
+
+
+def _all_gather_flat(t, world, group):
+    """all_gather of one tensor per rank into a flat tensor: RCCL on device tensors; gloo on host copies."""
+    import torch
+    import torch.distributed as dist
+    if t.device.type == "cuda" and dist.get_backend(group) == "gloo":
+        parts = [torch.empty_like(t, device="cpu") for _ in range(world)]
+        dist.all_gather(parts, t.cpu(), group=group)
+        return torch.cat(parts).to(t.device)
+    out = torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, t.contiguous(), group=group)
+    return out
+
+
+def gather_stream_device(L, local, d_count, slot_bytes, out, d_total, group=None):
+    """All-gather this rank's shard (encoded at start bit 0 with its global idx0, bit count d_count: a
+    1-element int64 device tensor) into the single global stream in `out` (a uint8 device tensor, bit count
+    -> d_total), with no host read: the bit counts and the shards (slot_bytes each: >= the largest shard's
+    bytes + 8, a multiple of 4 -- e.g. the previous step's largest) are all-gathered, and one merge kernel
+    scans the counts and places every shard at its global bit offset (dc_merge_shards_device).  A shard
+    longer than its slot sets L.merge_status().  The library stream is ordered after the collectives."""
+    import torch.distributed as dist
+    import torch
+    world = dist.get_world_size(group)
+    dev = local.device
+    cur, ls = torch.cuda.current_stream(dev), _lib_stream(L, dev)
+    _after(ls, cur)                                   # the encode before the collectives
+    counts = _all_gather_flat(d_count.view(1), world, group)
+    shards = _all_gather_flat(local[:slot_bytes], world, group)
+    _after(cur, ls)
+    L.merge_shards_device(shards.data_ptr(), slot_bytes, world, counts.data_ptr(), out.data_ptr(), out.numel(),
+                          d_total.data_ptr())
+    counts.record_stream(ls)
+    shards.record_stream(ls)
+    return counts
+
+
+def decode_sharded_device(L, ct, local, d_count, max_bytes, num, out, type_=0, mask17=0, group=None):
+    """Decode this rank's shard from its own encoded buffer (start bit 0, bit count on the device) with the
+    segment decoder; its first predictions wait for the previous rank's last three values, which arrive
+    by one all-gather of 12 bytes per rank, and a one-wave fix decodes them (dc_decode_shard3_fix).  No
+    host read: L.decode_status() after the steps tells whether every shard stayed on this path."""
+    import torch.distributed as dist
+    import torch
+    rank = dist.get_rank(group)
+    dev = out.device
+    L.decode_shard3_device(ct, local.data_ptr(), d_count.data_ptr(), max_bytes, num, out.data_ptr(), type_, mask17)
+    cur, ls = torch.cuda.current_stream(dev), _lib_stream(L, dev)
+    _after(ls, cur)
+    hin = exchange_history(out[num - 3:num].flip(0).contiguous(), group)
+    _after(cur, ls)
+    if hin is not None:
+        hin = hin.to(dev)
+        L.decode_shard3_fix(hin.data_ptr())
+        hin.record_stream(ls)
     return out
 
 

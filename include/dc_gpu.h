@@ -92,6 +92,25 @@ int dc_decode_shard_device(int ct, const void* d_stream, long long stream_bytes,
                            void* d_out);
 int dc_decode_shard_fix(const float* d_hin);
 
+/* The device-side multi-GPU step (nothing is read back on the host):
+ * dc_merge_shards_device: world shards, each encoded at start bit 0 (dc_encode_device with its global
+ *   idx0) and all-gathered into slots of slot_bytes (a multiple of 4, >= each shard's bytes + 8), with
+ *   their all-gathered bit counts (device u64[world]) -> the single global stream, byte-identical to one
+ *   encode of the whole array, in d_out (out_bytes of room, 4-byte aligned) and its bit count in d_total.
+ *   Problems set a sticky status word read by dc_merge_status (1: a shard longer than its slot, 2: the
+ *   stream longer than the output).
+ * dc_decode_shard3_device: decode one such shard (its own encoded buffer, bit count on the device) with
+ *   the segment decoder; predictions among its first tokens wait for the previous shard's last three
+ *   values: dc_decode_shard3_fix(d_hin) decodes them once they are on the device (b1 = x[-1], b2, b3).
+ *   A shard the segment decoder declines sets dc_decode_status (decode it with dc_decode_shard_device). */
+int dc_merge_shards_device(const void* d_gathered, long long slot_bytes, int world, const unsigned long long* d_counts,
+                           void* d_out, long long out_bytes, unsigned long long* d_total);
+int dc_merge_status(unsigned* status_out, int reset);
+int dc_decode_shard3_device(int ct, const void* d_stream, const unsigned long long* d_nbits, long long max_bytes,
+                            long long num, int type, uint32_t mask17, void* d_out);
+int dc_decode_shard3_fix(const float* d_hin);
+int dc_decode_status_clear(void);           /* clear the decoder status word (after a declined shard) */
+
 /* Himeno halo planes on device-resident p[mi][mj][mk] (the fused form of transform_3d_array_to_1d_array +
  * toSmallDataset_float + compress, impl/himenoBMTxps.c:483-706): encode the plane ijk (1: i = v,
  * 2: j = v, 3: k = v) of extent imax x jmax x kmax; *d_min (device) gets the plane minimum.  CT7 with

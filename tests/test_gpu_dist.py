@@ -77,6 +77,76 @@ def _worker(rank, world, port, ct, n, kind, q):
         dist.destroy_process_group()
 
 
+def _worker_device(rank, world, port, ct, n, kind, q):
+    """The device-side step (bench.py e2e): encode at start bit 0 with the global index, device bit count;
+    gather_stream_device (all-gathered counts and shards, one merge kernel); decode_sharded_device (the
+    segment decoder on the rank's own shard, 12-byte exchange, one-wave prefix fix).  No host read until
+    the checks.  A shard the segment decoder declines (a prediction chain through its whole first chunk)
+    is decoded again on the host-synchronised path from the gathered stream."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import dcamd
+        from pyoracle import Oracle
+        L = dcamd.Lib()
+        L.init(0)
+        L.set_bound(1e-3)
+        O = Oracle()
+        N = world * n
+        x = O.gen_u10(N)
+        if kind == "chain":
+            for r in range(1, world):
+                x[r * n - 700:r * n + 900] = x[r * n - 701]
+        _, xs = O.to_small(x)
+        t, m17 = O.type_mask(xs)
+        dev = torch.device("cuda", 0)
+        lo = rank * n
+        buf = torch.zeros(n + 4, dtype=torch.float32, device=dev)
+        halo = xs[max(lo - 3, 0):lo]
+        if halo.size:
+            buf[4 - halo.size:4] = torch.from_numpy(halo.copy())
+        buf[4:] = torch.from_numpy(xs[lo:lo + n].copy())
+        xd = buf[4:]
+        cap = L.stream_capacity(n)
+        local = torch.zeros(cap + 64, dtype=torch.uint8, device=dev)
+        d_count = torch.zeros(1, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()
+        L.encode_device(ct, xd.data_ptr(), n, local.data_ptr(), idx0=lo, type_=t, mask17=m17, start_bit=0,
+                        total_ptr=d_count.data_ptr())
+        slot = (cap + 8 + 3) // 4 * 4
+        glob = torch.zeros((world * cap + 64) // 4 * 4, dtype=torch.uint8, device=dev)
+        d_total = torch.zeros(1, dtype=torch.int64, device=dev)
+        dcamd.gather_stream_device(L, local, d_count, slot, glob, d_total)
+        out = torch.empty(n, dtype=torch.float32, device=dev)
+        dcamd.decode_sharded_device(L, ct, local, d_count, (cap + 64) // 16 * 16, n, out, t, m17)
+        L.synchronize()
+        torch.cuda.synchronize()
+        st_enc, st_merge, st_dec = L.encode_status(), L.merge_status(reset=True), L.decode_status()
+        tot = int(d_total.item())
+        fallback = st_dec != 0
+        if fallback:                           # the host-synchronised shard path, from the gathered stream
+            L.decode_status_clear()
+            bits = int(d_count.item())
+            counts = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+            dist.all_gather(counts, torch.tensor([bits], dtype=torch.int64))
+            starts, _ = dcamd.shard_offsets([int(c[0]) for c in counts])
+            g = glob[:(tot + 7) // 8]
+            dcamd.decode_sharded(L, ct, g, g.numel(), starts[rank], bits, n, out, t, m17)
+            torch.cuda.synchronize()
+        s_all, nb_all, pos_all = O.compress(ct, xs, 1e-3, t, m17)
+        dec_all, _ = O.decompress(ct, s_all, N, 1e-3, t, m17)
+        nb = (tot + 7) // 8
+        ok_stream = bool(st_enc == 0 and st_merge == 0 and tot == _bits_of(nb_all, pos_all) and
+                         np.array_equal(glob[:nb].cpu().numpy(), s_all) and not glob[nb:nb + 16].cpu().numpy().any())
+        ok_dec = bool(np.array_equal(out.cpu().numpy().view(np.uint32), dec_all[lo:lo + n].view(np.uint32)))
+        q.put((rank, ok_stream, ok_dec, fallback))
+    except Exception as e:
+        q.put((rank, False, repr(e), None))
+    finally:
+        dist.destroy_process_group()
+
+
 def _free_port():
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
@@ -96,3 +166,22 @@ def test_sharded_encode_gather_decode_world2(ct, n, kind):
     for p in procs:
         p.join(timeout=60)
     assert all(r[1] is True and r[2] is True for r in res), res
+
+
+@pytest.mark.parametrize("ct,n,kind", [(7, (1 << 18) + 5, "u10"), (5, 100003, "chain"), (6, 65536, "u10"),
+                                       (11, 40001, "u10"), (7, 300007, "chain"), (7, 1 << 20, "u10")])
+def test_device_step_world2(ct, n, kind):
+    """The device-side multi-GPU step against the oracle's single stream and its decode; ordinary shards
+    stay on the device path (no fallback)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_device, args=(r, 2, port, ct, n, kind, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] is True and r[2] is True for r in res), res
+    if kind == "u10":
+        assert not any(r[3] for r in res), res
