@@ -625,6 +625,7 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
     res = {"nbits": int(nbits), "nbytes": int(nbytes), "wall": wall, "enc_ms": enc_ms, "dec_ms": dec_ms,
            "kavg": kavg, "status": int(status | warm_status), "warm_status": int(warm_status), "resends": timed_resends,
            "slow_path_timed": slow[0], "v3": bool(L.L.dc_last_decode_launched_v3()),
+           "runs": bool(L.L.dc_last_decode_launched_runs()),
            "enc_mode": int(L.L.dc_encode_mode()), "ct9": {k: v for k, v in ct9.items() if k in ("phase_ms", "acks_ok", "nflip")}}
 
     if pipelined and ber <= 0:
@@ -713,7 +714,7 @@ def copy_bandwidth(dev, n, reps=10):
     return 8.0 * n / (ms * 1e-3) / 1e9
 
 
-def kernel_table(ct, n, nbytes, kavg, v3=True, enc_mode=1):
+def kernel_table(ct, n, nbytes, kavg, v3=True, enc_mode=1, runs=False):
     """The timed launches of a step (library timing slots, HIP events on the library stream) and their
     algorithmic bytes: the encoder's count and pack launches (the pack's workgroup 0 scans the tile
     offsets), then the decoder's -- the segment decoder (parse3, whose jobs check the
@@ -732,7 +733,10 @@ def kernel_table(ct, n, nbytes, kavg, v3=True, enc_mode=1):
             f"encode_count_kernel<{ct}>": (k[0], 4.0 * n),
             f"encode_pack_kernel<{ct}>": (k[2], 4.0 * n + nbytes),
         }
-    if v3:
+    if runs:              # the small-stream decoder: chunk maps + one-workgroup scans, then the values
+        kernels.update({f"runs_map_kernel<{ct}>+runs_scan_kernel<{ct}>": (k[3], 0.0 if fin else float(nbytes)),
+                        f"runs_values_kernel<{ct}>": (k[5], 0.0 if fin else dec_b)})
+    elif v3:
         kernels.update({f"parse3_kernel<{ct}>": (k[3], 0.0 if fin else float(nbytes)),
                         f"decode3_kernel<{ct}>": (k[5], 0.0 if fin else dec_b)})
     else:
@@ -754,7 +758,7 @@ def line_for(C, W, R, steps):
     kernel (algorithmic bytes / its HIP-event duration on the library stream) and of the whole step."""
     n, nbytes = W["n"], R["nbytes"]
     ms = R["wall"] / steps * 1e3
-    kernels = kernel_table(W["ct"], n, nbytes, R["kavg"], R["v3"], R.get("enc_mode", 1))
+    kernels = kernel_table(W["ct"], n, nbytes, R["kavg"], R["v3"], R.get("enc_mode", 1), R.get("runs", False))
     for nm, ms_ in R.get("ct9", {}).get("phase_ms", {}).items():   # CT9: every launch of the step
         kernels[nm] = (ms_, 2.0 * nbytes if "copy" in nm and "compare" not in nm else
                        (2.0 * nbytes if "resend copy" in nm else (float(nbytes) if "crc32" in nm else 0.0)))
@@ -812,7 +816,7 @@ def main():
         # warm-up on run it inside every timed step and are reported with fast_path false)
         print(f"bench.py: decoder status 0x{R['status']:x} in the timed steps (slow path not timed)", file=sys.stderr)
         sys.exit(1)
-    kernels = kernel_table(ct, n, nbytes, R["kavg"], R["v3"], R.get("enc_mode", 1))
+    kernels = kernel_table(ct, n, nbytes, R["kavg"], R["v3"], R.get("enc_mode", 1), R.get("runs", False))
     dname = main_line["dominant"]["kernel"]
     achievable = copy_bandwidth(C.dev, n)
     traffic, traffic_src, ktraffic = None, None, None

@@ -38,6 +38,9 @@
 
 namespace dc {
 
+#ifndef DC_WALK2
+#define DC_WALK2 0
+#endif
 // pre-walk: 1024 bits (4 chunks, one region line) before every segment (DC_PARSE_PL6=2: 2048 for CT6 --
 // 12% instead of 94% of its jobs repair, but the longer walk cost more: config 2 parse3 98 vs 92 us)
 #ifndef DC_PARSE_PL6
@@ -162,6 +165,29 @@ struct Ring3 {
     // walk until pos >= pend; tokens stepped
     __device__ __forceinline__ int walk(int pend, const uint8_t* tl) {
         int n = 0;
+#if DC_WALK2
+        // two steps per loop round, the second predicated (a lane past pend steps by 0): one exit test and
+        // one exec update per two tokens
+        while (pos < pend) {
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const uint32_t nx = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(L) + addr);
+                const uint32_t t = __builtin_amdgcn_alignbit(a, b, s);
+                int len = tl[t >> 23];
+                if (u == 1) len = pos < pend ? len : 0;
+                uint32_t d;
+                const bool adv = __builtin_usub_overflow(s, (uint32_t)len, &d);
+                s = d & 31u;
+                pos += len;
+                a = adv ? b : a;
+                b = adv ? c : b;
+                c = adv ? nx : c;
+                addr = (addr + (adv ? 256u : 0u)) & D3_RMASK;
+                n += len > 0 ? 1 : 0;
+            }
+        }
+        return n;
+#endif
         while (pos < pend) {
             const uint32_t nx = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(L) + addr);
             const uint32_t t = __builtin_amdgcn_alignbit(a, b, s);

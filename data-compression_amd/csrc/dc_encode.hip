@@ -386,7 +386,9 @@ __device__ void pack_scan_block(const uint32_t* __restrict__ tcnt, uint64_t* __r
         // chunk only)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();                          // (also: lds / s_w are reused)
-        if (tid == 0) __hip_atomic_store(&flag[c0 / PCH], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // (release at agent scope on top of the sc1 form above: the memory model's own guarantee, ADVICE r03;
+        // this variant runs only for A/B, DC_ENC_PASSES=2)
+        if (tid == 0) __hip_atomic_store(&flag[c0 / PCH], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (tid == 0) {
         *total_bits = carry;
@@ -584,6 +586,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
                 if (++spins > (1u << 22)) { atomicOr(err, 4u); s_hw[0] = 0u; break; }   // (never seen)
                 __builtin_amdgcn_s_sleep(8);            // (~500 cycles: thousands of early tiles poll one word)
             }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");          // (pairs with the flag's release)
         }
     }
     __syncthreads();

@@ -71,7 +71,10 @@ typedef struct {
     int dec3_used;                   /* the pending decode ran the segment decoder */
     int dec3_last;                   /* the last finished decode's values came from it */
     int dec3_launched;               /* the last dc_decode_device launched it (it may decline later) */
-    int dec3_skip_once;              /* the next dc_decode_device takes the chunk-map decoder (halo planes) */
+    int dec3_skip_once;              /* the next dc_decode_device takes the small-stream decoder (halo planes) */
+    int runs_used;                   /* the pending decode ran the small-stream decoder (dc_decode_runs.hip) */
+    int runs_last;                   /* the last finished decode's values came from it */
+    uint8_t* runs_maps;              /* its chunk maps */
     const uint8_t* sh3_s;            /* the last dc_decode_shard3_device call (for its fix) */
     Params sh3_P;
     Dec3Bufs sh3_D3;
@@ -634,6 +637,23 @@ static long long dec3_min_bytes(void) {
 }
 /* < -1: the default; -1 disables the segment decoder; returns the previous value */
 int dc_last_decode_was_v3(void) { return G.dec3_last; }
+int dc_last_decode_was_runs(void) { return G.runs_last; }
+int dc_last_decode_launched_runs(void) { return G.runs_used; }
+/* streams of at most this capacity (bytes) use the small-stream decoder (dc_decode_runs.hip), unless the
+   segment decoder is forced (dc_set_decode3_min_bytes(0)); halo planes use it up to its chunk limit */
+static long long g_runs_max = -2;
+static long long runs_max_bytes(void) {
+    if (g_runs_max == -2) {
+        const char* e = getenv("DC_RUNS_MAX_BYTES");
+        g_runs_max = (e && *e) ? atoll(e) : (64ll << 10) + 256;
+    }
+    return g_runs_max;
+}
+long long dc_set_runs_max_bytes(long long v) {
+    const long long old = runs_max_bytes();
+    g_runs_max = v < -1 ? (64ll << 10) + 256 : v;
+    return old;
+}
 int dc_last_decode_launched_v3(void) { return G.dec3_launched; }
 long long dc_set_decode3_min_bytes(long long v) {
     const long long old = dec3_min_bytes();
@@ -667,14 +687,23 @@ int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsig
     /* the segment decoder reads whole 16-byte groups through a buffer resource (32-bit byte range): every
        stream byte must lie in one inside max_bytes, and max_bytes and the output below 2 GiB */
     const long long need16 = nbytes >= 0 ? (nbytes + 15) / 16 * 16 : 0;
-    const int no3 = G.dec3_skip_once;
+    const int halo = G.dec3_skip_once;
     G.dec3_skip_once = 0;
-    G.dec3_used = !no3 && m3 >= 0 && max_bytes >= m3 && max_bytes >= 16 && max_bytes >= need16 && max_bytes < (1ll << 31) && num < (1ll << 29) && !G.D.shard &&
+    const long long mc256 = (max_bytes * 8 + 255) / 256 + 1;
+    G.runs_used = !G.D.shard && num >= 1 && mc256 <= dc_decode_runs_max_chunks() + 8 && m3 != 0 &&
+                  (halo || max_bytes <= runs_max_bytes());
+    G.dec3_used = !halo && !G.runs_used && m3 >= 0 && max_bytes >= m3 && max_bytes >= 16 && max_bytes >= need16 && max_bytes < (1ll << 31) && num < (1ll << 29) && !G.D.shard &&
                   !((uintptr_t)d_stream & 15u) && !((uintptr_t)d_out & 15u);
     G.dec3_launched = G.dec3_used;
     G.dec_dnbits = nbytes >= 0 ? NULL : d_nbits;
     G.dec_hnbits = nbytes >= 0 ? (unsigned long long)nbytes * 8ull : 0ull;
-    if (G.dec3_used) {
+    if (G.runs_used) {
+        if (!G.runs_maps) HIPCHK(hipMalloc((void**)&G.runs_maps, dc_decode_runs_scratch_bytes()));
+        if (dc_launch_decode_runs((const uint8_t*)d_stream, G.dec_dnbits, G.dec_hnbits, mc256, &P, G.runs_maps, G.D.err,
+                                  (float*)d_out, num, G.st))
+            return seterr(DC_ERR_HIP, "decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+        G.dec3_used = 1;                  /* (a first decoder that may decline: dc_decode_finish falls back) */
+    } else if (G.dec3_used) {
         if ((rc = dec3_ensure((max_bytes * 8 + 255) / 256 + 1, P.B, ct))) return rc;
         G.D3.err = G.D.err;
         G.D3.capw = max_bytes / 16 * 4;
@@ -827,7 +856,8 @@ static int decode_finish_body(void) {
         return seterr(DC_ERR_STREAM, "decoder status 0x%x over %d queued decodes: an earlier decode left the fast "
                                      "path and was not completed (call dc_decode_finish after each decode)", err, queued);
     }
-    G.dec3_last = G.dec3_used && !(err & 512u);
+    G.dec3_last = G.dec3_used && !G.runs_used && !(err & 512u);
+    G.runs_last = G.dec3_used && G.runs_used && !(err & 512u);
     if ((err & 512u) && G.dec_pending && G.dec3_used) {
         /* the segment decoder declined the stream (runs mode, an unconverged repair, a dense job, the
          * history sentinel): decode it again with the chunk-map decoder, then its slow paths below */

@@ -134,6 +134,11 @@ int dc_launch_merge_shards(const uint8_t* g, long long P, int world, const unsig
                            dc_hip_stream st);
 int dc_launch_shard3_fix(const uint8_t* s, const DC_NS Params* P, const DC_NS Dec3Bufs* D3, const float* hin,
                          float* out, long long num, dc_hip_stream st);
+int dc_launch_decode_runs(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                          long long max_chunks, const DC_NS Params* P, uint8_t* maps, unsigned* err, float* out,
+                          long long num, dc_hip_stream st);
+long long dc_decode_runs_max_chunks(void);
+size_t dc_decode_runs_scratch_bytes(void);
 int dc_decode3_seg(long long max_chunks, int B, int ct);
 long long dc_ct1_tiles(long long n);
 int dc_launch_ct1_encode(const float* x, long long n, float thr_le, uint32_t* traw, unsigned long long* rawoff,

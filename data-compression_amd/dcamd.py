@@ -47,7 +47,8 @@ EXT_SYMBOLS = [
     "dc_set_decode3_min_bytes", "dc_set_decode3_seg", "dc_last_decode_was_v3", "dc_last_decode_launched_v3",
     "dc_encode_status", "dc_encode_mode", "dc_encode_retries", "dc_crc_resend_device",
     "dc_merge_shards_device", "dc_merge_status", "dc_decode_shard3_device", "dc_decode_shard3_fix",
-    "dc_decode_status_clear",
+    "dc_decode_status_clear", "dc_set_runs_max_bytes", "dc_last_decode_was_runs",
+    "dc_last_decode_launched_runs",
 ]
 
 
@@ -97,6 +98,8 @@ class Lib:
         L.dc_set_small_chunk_max_bytes.restype = ll
         L.dc_set_decode3_min_bytes.argtypes = [ll]
         L.dc_set_decode3_min_bytes.restype = ll
+        L.dc_set_runs_max_bytes.argtypes = [ll]
+        L.dc_set_runs_max_bytes.restype = ll
         pp = [_f32p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int), C.POINTER(C.c_int)]
         for nm in ("myCompress_bitwise", "myCompress_bitwise_np", "myCompress_bitwise_op"):
             getattr(L, nm).argtypes = pp
@@ -442,6 +445,15 @@ class Lib:
         """Force the segment decoder's parse segment length (4, 8 or 16 chunks; 0: by size); returns the
         previous setting."""
         return int(self.L.dc_set_decode3_seg(int(seg)))
+
+    def set_runs_max_bytes(self, v):
+        """Streams of at most v bytes of capacity use the small-stream decoder (< -1: default 64 KiB + 256,
+        -1: never); returns the previous value."""
+        return int(self.L.dc_set_runs_max_bytes(int(v)))
+
+    def last_decode_was_runs(self):
+        """Whether the last finished decode's values came from the small-stream decoder."""
+        return bool(self.L.dc_last_decode_was_runs())
 
     def last_decode_was_v3(self):
         """Whether the last finished decode's values came from the segment decoder."""

@@ -183,6 +183,14 @@ long long dc_set_decode3_min_bytes(long long min_bytes);
 int dc_set_decode3_seg(int seg);
 /* 1 if the last decode's values came from the segment decoder (after dc_decode_finish). */
 int dc_last_decode_was_v3(void);
+/* Streams of at most this capacity (bytes) decode with the small-stream decoder (dc_decode_runs.hip: chunk
+ * entry maps composed by a scan, one workgroup), unless dc_set_decode3_min_bytes(0) forces the segment
+ * decoder; Himeno halo planes take it whatever their capacity (< -1: the default, 64 KiB + 256: 2^14 floats; -1:
+ * never).  Returns the previous value. */
+long long dc_set_runs_max_bytes(long long max_bytes);
+/* 1 if the last decode's values came from the small-stream decoder (after dc_decode_finish). */
+int dc_last_decode_was_runs(void);
+int dc_last_decode_launched_runs(void);     /* 1: the last dc_decode_device launched it (it may decline) */
 /* 1: the last dc_decode_device launched the segment decoder (its values may still come from the chunk-map
  * decoder if it declined the stream: dc_last_decode_was_v3 after dc_decode_finish tells) */
 int dc_last_decode_launched_v3(void);

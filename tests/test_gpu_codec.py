@@ -414,6 +414,19 @@ def test_halo_plane_device(dc, oracle, ct, size, ijk, v):
     bench's halo step) gathered in transform_3d_array_to_1d_array order, toSmallDataset_float'ed and
     encoded on the GPU equals the oracle stream of the host-side plane; the decode writes plane + min
     back into p exactly as impl/himenoBMTxps.c:699-706."""
+    _halo_plane_case(dc, oracle, ct, size, ijk, v, noise=True)
+
+
+@pytest.mark.parametrize("ct", CTS)
+@pytest.mark.parametrize("ijk,v", [(3, 1), (3, 5), (1, 255), (2, 100)])
+def test_halo_plane_device_initmt(dc, oracle, ct, ijk, v):
+    """The L-size plane exactly as BASELINE config 4 produces it: initmt's p = i^2/(imax-1)^2 with no noise,
+    so a z-plane is rows of one repeated value -- a runs-mode stream of '101' copy runs (the bench's --halo
+    stream) -- through the fused device encode and decode, against the oracle."""
+    _halo_plane_case(dc, oracle, ct, "L", ijk, v, noise=False)
+
+
+def _halo_plane_case(dc, oracle, ct, size, ijk, v, noise):
     import torch
     dc.set_bound(1e-3)
     if size == "M":
@@ -425,7 +438,8 @@ def test_halo_plane_device(dc, oracle, ct, size, ijk, v):
     ii = np.arange(mi, dtype=np.float32)[:, None, None]
     rs = np.random.RandomState(ijk * 1000 + v)
     p = (ii * ii / np.float32((imax - 1) * (imax - 1)) + np.zeros((mi, mj, mk), np.float32)).astype(np.float32)
-    p += (rs.rand(mi, mj, mk).astype(np.float32) * np.float32(0.01))
+    if noise:
+        p += (rs.rand(mi, mj, mk).astype(np.float32) * np.float32(0.01))
     A, B = {1: (jmax, kmax), 2: (imax, kmax), 3: (imax, jmax)}[ijk]
     a, b = np.meshgrid(np.arange(A), np.arange(B), indexing="ij")
     idx = {1: (v, a, b), 2: (a, v, b), 3: (a, b, v)}[ijk]
