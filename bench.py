@@ -150,6 +150,9 @@ def halo_bench(args):
     xfer = [0, 0]                                   # stream bytes this rank received, per step
     last = [None]                                   # the last step's received (stream, bits, min) per side
 
+    # no host read inside a step: the planes' decoder status is read after the timed steps
+    L.L.dc_set_halo_async(1)
+
     def step():
         for h, v in enumerate(planes):
             L.halo_encode_device(ct, p.data_ptr(), (mi, mj, mk), 3, v, (imax, jmax, kmax), st[h].data_ptr(),
@@ -188,6 +191,11 @@ def halo_bench(args):
     L.synchronize()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    dstat = L.decode_status()
+    L.L.dc_set_halo_async(0)
+    if dstat != 0:
+        print(f"bench.py: halo decoder status 0x{dstat:x} after the timed steps", file=sys.stderr)
+        sys.exit(1)
     xcheck = None
     if dist is not None:
         # the plane received from up must be up's plane k = 1 and the one from down down's plane

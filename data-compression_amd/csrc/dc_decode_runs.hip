@@ -100,10 +100,13 @@ struct Hs {
 
 // the stream words a reader needs: from LDS when the whole stream was staged there, else from global
 struct RsWords {
-    const uint32_t* lw;             // staged words (nullptr: read global)
+    const uint32_t* lw;             // staged words (nullptr: read global), lw[0] = stream word `base`
     const uint8_t* s;
     long long nbytes;
-    __device__ __forceinline__ uint32_t at(long long wi) const { return lw ? lw[wi] : rs_word(s, nbytes, wi); }
+    long long base;
+    __device__ __forceinline__ uint32_t at(long long wi) const {
+        return lw ? lw[wi - base] : rs_word(s, nbytes, wi);
+    }
     __device__ __forceinline__ uint32_t peek(long long pos) const {
         const long long wi = pos >> 5;
         const int sh = (int)(pos & 31);
@@ -262,7 +265,7 @@ __global__ __launch_bounds__(RUNS_T) void runs_scan_kernel(const uint8_t* __rest
         return;
     }
     // (4) pass 1: the block with symbolic incoming history -> its carry (last three values)
-    RsWords W{staged ? pool : nullptr, s, nbytes};
+    RsWords W{staged ? pool : nullptr, s, nbytes, 0};
     Hs h1 = {1u, 0.f}, h2 = {2u, 0.f}, h3 = {3u, 0.f};
     bool sent = false;
     if (c0 < c1) block_walk<CT, false>(W, P, c0, c1, y, cn, T0, num, nbits, h1, h2, h3, sent, nullptr);
@@ -326,6 +329,8 @@ __global__ __launch_bounds__(64) void runs_values_kernel(const uint8_t* __restri
                                                         const unsigned long long* dev_nbits,
                                                         unsigned long long host_nbits, float* __restrict__ out,
                                                         long long num) {
+    constexpr int ROW = 8 * RUNS_BMAX + 2;                      // a block's stream words (+ 2 past its end)
+    __shared__ uint32_t kw[64 * ROW];
     const unsigned long long nbits = dev_nbits ? *dev_nbits : host_nbits;
     const long long nch = (long long)((nbits + 255) >> 8), nbytes = (long long)((nbits + 7) >> 3);
     if (nch > RUNS_MAXC || (__hip_atomic_load(R.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & RUNS_DECLINE))
@@ -337,13 +342,16 @@ __global__ __launch_bounds__(64) void runs_values_kernel(const uint8_t* __restri
     const uint4 b = R.blk[i];
     const int nc = (int)(b.x >> 8);
     if (nc <= 0) return;
+    // the block's words into this lane's LDS row (independent loads, all in flight), read back per token
+    uint32_t* row = kw + threadIdx.x * ROW;
+    for (int q = 0; q < 8 * nc + 2; q++) row[q] = rs_word(s, nbytes, 8 * c0 + q);
     const float4 hb = R.bhist[i];
     uint8_t cn[RUNS_BMAX];
 #pragma unroll
     for (int j = 0; j < RUNS_BMAX; j++) cn[j] = R.bcnt[i * RUNS_BMAX + j];
     Hs h1 = {0u, hb.x}, h2 = {0u, hb.y}, h3 = {0u, hb.z};
     bool sent = false;
-    RsWords W{nullptr, s, nbytes};
+    RsWords W{row, s, nbytes, 8 * c0};
     block_walk<CT, true>(W, P, c0, c0 + nc, (int)(b.x & 0xFFu), cn, (long long)b.y, num, nbits, h1, h2, h3, sent, out);
     if (sent) atomicOr(R.err, RUNS_DECLINE | RUNS_WHY_SENT);
 }

@@ -640,6 +640,9 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
 #ifndef DC_LB_KS
 #define DC_LB_KS 4                      // look-back windows of 64 states per round trip, with the scanner
 #endif
+#ifndef DC_LB_DMA
+#define DC_LB_DMA 1                     // the first window into LDS before the pack (lb_dma)
+#endif
 #ifndef DC_LB_K
 #define DC_LB_K 8
 #endif
@@ -650,6 +653,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
 #define DC_LB_SLEEP 1
 #endif
 static_assert(DC_LB_K <= 8 && DC_LB_KS <= 8, "look-back windows read at most LB_PAD words before tile 0");
+static_assert(!DC_LB_DMA || DC_LB_KS <= 4, "the LDS window holds 256 predecessors");
 constexpr long long LB_PAD = 512;                                 // readable words in front of the tile states
 constexpr int LB_KW = DC_LB_K;                                    // look-back: tiles per lane per round trip
 constexpr unsigned long long ST_VAL = (1ull << 40) - 1;
@@ -674,13 +678,17 @@ __device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
 // ~1800 waiting tiles tripled the encode), then the window is read again.  A window without an inclusive
 // state adds its aggregates and the next one is read.  Returns 0, or 1 when a needed state is poisoned or a
 // wait timed out.
+// lw0 (optional): the first window as loaded into LDS before the tile's pack (lw0[q] = state s0 + q,
+// lb_dma below); a state it saw unpublished is polled and the window read again as usual.
 template <int LB_K>
 __device__ __forceinline__ int enc_lookback(const uint64_t* __restrict__ st, long long t, uint32_t tag,
-                                            unsigned long long& excl, uint32_t& stat, int start_bit) {
+                                            unsigned long long& excl, uint32_t& stat, int start_bit,
+                                            const uint64_t* lw0 = nullptr, long long s0 = 0) {
     const int lane = threadIdx.x & 63;
     long long base = t - 1;
     excl = 0;
     const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
+    bool first = lw0 != nullptr;
     for (;;) {
         uint64_t v[LB_K];
         int pinc;                                                         // first inclusive position (64 LB_K: none)
@@ -691,9 +699,10 @@ __device__ __forceinline__ int enc_lookback(const uint64_t* __restrict__ st, lon
 #pragma unroll
             for (int k = 0; k < LB_K; k++) {
                 const long long ti = base - (long long)(64 * k + lane);
-                const uint64_t w = ld_relaxed(p - 64 * k);
+                const uint64_t w = first ? lw0[ti - s0] : ld_relaxed(p - 64 * k);
                 v[k] = ti >= 0 ? w : st_word(tag, ST_INC, (unsigned long long)start_bit);   // (before tile 0)
             }
+            first = false;
             pinc = 64 * LB_K;
             int pinv = 64 * LB_K;                                         // first unpublished position
 #pragma unroll
@@ -734,6 +743,21 @@ __device__ __forceinline__ int enc_lookback(const uint64_t* __restrict__ st, lon
         if (pinc < 64 * LB_K) return 0;
         base -= 64 * LB_K;
     }
+}
+
+// The first look-back window requested straight into LDS (global_load_lds, agent-coherent sc1: no
+// VGPRs held across the pack, where a register window spilled) before the tile packs its words: the
+// ~3 us round trip of state loads under the stream then overlaps the pack.  Lane l of load m brings
+// states s0 + 128 m + 2 l, +1 (16 bytes); s0 is even (16-byte aligned: st is) and the three loads cover
+// the 256 states base - 255 .. base.  Positions before tile 0 read LB_PAD words in front of st.
+constexpr int LB_DMA_N = 3;
+__device__ __forceinline__ long long lb_dma(const uint64_t* __restrict__ st, long long base, uint64_t* lw) {
+    const long long s0 = (base - 256) & ~1ll;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int m = 0; m < LB_DMA_N; m++)
+        __builtin_amdgcn_global_load_lds(st + s0 + 128 * m + 2 * lane, lw + 128 * m, 16, 0, 16 /* sc1 */);
+    return s0;
 }
 
 #ifndef DC_TOK_SB
@@ -851,6 +875,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
     __shared__ unsigned long long s_G;
     __shared__ uint32_t s_tp, s_ok;
     __shared__ uint16_t tab[512];
+    __shared__ __attribute__((aligned(16))) uint64_t lbw[128 * LB_DMA_N];   // the first look-back window
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t tag = epoch & ST_TAGM;
     if (scan && blockIdx.x == 0) {                                    // the scanner (dispatched first)
@@ -942,6 +967,8 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
         st_relaxed(tl + tile, ((uint64_t)epoch << 32) | ((uint32_t)acc & 0x7FFFFFFFu));
     }
     const uint32_t off = wpre + inc - mysum;                              // the thread's first tile bit
+    long long lb_s0 = 0;
+    if (DC_LB_DMA && scan && !DC_SCAN_POLL && wid == 0 && tile > 0) lb_s0 = lb_dma(st, (long long)tile - 1, lbw);
     __syncthreads();                                                      // every thread has its tokens back
     // ---- pack, MSB-first.  Full tiles: every thread holds >= 48 bits, so a word is shared by at most
     // two neighbouring threads: each writes the words it completes, its first merged with the previous
@@ -1026,7 +1053,14 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
             // behind this tile's own neighbours (which started with it): a look-back over DC_LB_KS x 64
             // predecessors in one round trip mostly meets one (waiting for the scanner to reach this tile
             // itself cost ~4 us per tile)
-            if (tile > 0) bad = enc_lookback<DC_LB_KS>(st, tile, tag, G, lbst, start_bit);
+            if (tile > 0) {
+                if (DC_LB_DMA) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the window's LDS writes landed
+                    bad = enc_lookback<DC_LB_KS>(st, tile, tag, G, lbst, start_bit, lbw, lb_s0);
+                } else {
+                    bad = enc_lookback<DC_LB_KS>(st, tile, tag, G, lbst, start_bit);
+                }
+            }
         } else if (tile > 0) {
             bad = enc_lookback<LB_KW>(st, tile, tag, G, lbst, start_bit);
         }
@@ -1123,7 +1157,7 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
     if (mode == 1) {
         const int grid = (int)ntiles;
         dc_mark_phase(0, stream);
-        uint64_t* st = desc + desc_words_multi(ntiles) + LB_PAD;
+        uint64_t* st = desc + ((desc_words_multi(ntiles) + 1) & ~1ll) + LB_PAD;   // 16-byte aligned (lb_dma)
         static int scan = -1;                                            // DC_ENC_SCAN=0: chained look-back
         if (scan < 0) scan = (getenv("DC_ENC_SCAN") && *getenv("DC_ENC_SCAN") == '0') ? 0 : 1;
         DC_ENC_DISPATCH(encode_fused_kernel, dim3(grid + scan), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, st,
@@ -1174,7 +1208,7 @@ static long long desc_words_multi(long long nt) {
 }
 extern "C" long long dc_encode_desc_words(long long n) {
     const long long nt = dc_encode_tile_count(n);
-    return desc_words_multi(nt) + LB_PAD + 2 * nt;
+    return desc_words_multi(nt) + 1 + LB_PAD + 2 * nt;
 }
 // the epochs a state tag tells apart: the host clears desc when its encode epoch reaches this
 extern "C" unsigned dc_encode_epoch_limit(void) { return ST_TAGM; }

@@ -72,6 +72,7 @@ typedef struct {
     int dec3_last;                   /* the last finished decode's values came from it */
     int dec3_launched;               /* the last dc_decode_device launched it (it may decline later) */
     int dec3_skip_once;              /* the next dc_decode_device takes the small-stream decoder (halo planes) */
+    int halo_async;                  /* dc_halo_decode_device without dc_decode_finish (dc_set_halo_async) */
     int runs_used;                   /* the pending decode ran the small-stream decoder (dc_decode_runs.hip) */
     int runs_last;                   /* the last finished decode's values came from it */
     uint8_t* runs_maps;              /* its chunk maps */
@@ -638,6 +639,11 @@ static long long dec3_min_bytes(void) {
 /* < -1: the default; -1 disables the segment decoder; returns the previous value */
 int dc_last_decode_was_v3(void) { return G.dec3_last; }
 int dc_last_decode_was_runs(void) { return G.runs_last; }
+int dc_set_halo_async(int on) {
+    const int old = G.halo_async;
+    G.halo_async = on ? 1 : 0;
+    return old;
+}
 int dc_last_decode_launched_runs(void) { return G.runs_used; }
 /* streams of at most this capacity (bytes) use the small-stream decoder (dc_decode_runs.hip), unless the
    segment decoder is forced (dc_set_decode3_min_bytes(0)); halo planes use it up to its chunk limit */
@@ -1053,7 +1059,9 @@ int dc_halo_decode_device(int ct, const void* d_stream, long long nbytes, const 
        chunk-map decoder */
     G.dec3_skip_once = 1;
     if ((rc = dc_decode_device(ct, d_stream, nbytes, d_bits, cap, n, type, mask17, G.halo_a))) return rc;
-    if ((rc = dc_decode_finish())) return rc;
+    /* async (dc_set_halo_async): no host read here -- the caller reads dc_decode_status() after its steps
+       and decodes a plane again synchronously if it is not 0 */
+    if (!G.halo_async && (rc = dc_decode_finish())) return rc;
     if (dc_launch_plane_scatter((const float*)G.halo_a, d_min, (float*)d_p, mj, mk, ijk, v, A, B, G.st))
         return seterr(DC_ERR_HIP, "plane scatter launch failed");
     return DC_OK;

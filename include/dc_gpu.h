@@ -122,6 +122,10 @@ int dc_halo_encode_device(int ct, const void* d_p, int mi, int mj, int mk, int i
 int dc_halo_decode_device(int ct, const void* d_stream, long long nbytes, const unsigned long long* d_bits, int type,
                           uint32_t mask17, const float* d_min, void* d_p, int mi, int mj, int mk, int ijk, int v,
                           int imax, int jmax, int kmax);
+/* 1: dc_halo_decode_device returns without a host read (the plane is complete on the library stream if
+ * dc_decode_status() reads 0 after the caller's steps; else decode it again with this off).  Returns the
+ * previous setting. */
+int dc_set_halo_async(int on);
 
 /* Pre-passes on device data: toSmallDataset_float and med_dataset_float (exact). */
 int dc_to_small_device(const void* d_x, long long n, void* d_out, float* min_out);
