@@ -52,6 +52,8 @@ struct RunsBufs {
     uint4* blk;                     // [block] first chunk's entry | chunks << 8, first token
     float4* bhist;                  // [block] incoming history b1, b2, b3
     uint8_t* bcnt;                  // [block][RUNS_BMAX] tokens of its chunks
+    uint8_t* pm;                    // [chunk][32] group-first entry -> the chunk's entry (8-chunk groups)
+    uint8_t* gmap;                  // [group][32] group-first entry -> the next group's entry
     unsigned* err;                  // the decoder status word (shared with the other decoders)
 };
 
@@ -70,10 +72,9 @@ __global__ __launch_bounds__(256) void runs_map_kernel(const uint8_t* __restrict
     const long long c = (long long)blockIdx.x * 8 + h;
     if (e < 10) w[h][e] = c < nch ? rs_word(s, nbytes, 8 * c + e) : 0u;
     __syncthreads();
-    if (c >= nch) return;
     // tokens that start before the stream's end (the last byte's padding is not a token start of the
     // true path; a walk counting one more there only ever runs past num, see runs_decode_kernel)
-    const int lim = (int)min(256ll, (long long)nbits - 256 * c);
+    const int lim = c < nch ? (int)min(256ll, (long long)nbits - 256 * c) : 0;   // (past the stream: no walk)
     int pos = e, cnt = 0;
     while (pos < lim) {
         const int wi = pos >> 5, sh = pos & 31;
@@ -87,8 +88,26 @@ __global__ __launch_bounds__(256) void runs_map_kernel(const uint8_t* __restrict
             cnt++;
         }
     }
-    R.exitm[c * 32 + e] = (uint8_t)((pos - 256) & 31);
-    R.cntm[c * 32 + e] = (uint8_t)cnt;
+    if (c >= nch) pos = 256 + e;                                // (identity past the stream's end)
+    const uint8_t ex = (uint8_t)((pos - 256) & 31);
+    if (c < nch) {
+        R.exitm[c * 32 + e] = ex;
+        R.cntm[c * 32 + e] = (uint8_t)cnt;
+    }
+    // the workgroup's 8 chunks are a group: every chunk's prefix map inside the group (entry of the
+    // group's first chunk -> the chunk's entry) and the group's map, so the scan kernel scans groups
+    __shared__ uint8_t gx[8][32];
+    gx[h][e] = ex;
+    __syncthreads();
+    if (h == 0) {
+        int x = e;
+        const long long g0 = (long long)blockIdx.x * 8;
+        for (int j = 0; j < 8; j++) {
+            if (g0 + j < nch) R.pm[(g0 + j) * 32 + e] = (uint8_t)x;
+            x = gx[j][x];
+        }
+        R.gmap[blockIdx.x * 32 + e] = (uint8_t)x;
+    }
 }
 
 // a history slot of pass 1: kind 0 = the constant v, 1..3 = the k-th value before the block (b1..b3),
@@ -104,8 +123,11 @@ struct RsWords {
     const uint8_t* s;
     long long nbytes;
     long long base;
+    int pad;                        // 1: word w staged at w + w/8 (the scan kernel's whole-stream copy)
     __device__ __forceinline__ uint32_t at(long long wi) const {
-        return lw ? lw[wi - base] : rs_word(s, nbytes, wi);
+        if (!lw) return rs_word(s, nbytes, wi);
+        const long long q = wi - base;
+        return lw[pad ? q + (q >> 3) : q];
     }
     __device__ __forceinline__ uint32_t peek(long long pos) const {
         const long long wi = pos >> 5;
@@ -168,6 +190,22 @@ __device__ __forceinline__ void block_walk(const RsWords& W, const Params& P, lo
     }
 }
 
+#ifdef DC_RUNS_PROF
+__device__ unsigned long long g_runs_prof[16];
+#define RSTAMP(k) do { if (threadIdx.x == 0) g_runs_prof[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define RSTAMP(k) do {} while (0)
+#endif
+extern "C" int dc_runs_prof_read(unsigned long long* out) {
+#ifdef DC_RUNS_PROF
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_runs_prof), sizeof g_runs_prof) == hipSuccess ? 0 : -1;
+#else
+    (void)out;
+    return -1;
+#endif
+}
+
 constexpr int RUNS_SW = 28 * 1024;              // stream words staged in LDS (112 KiB; larger: global reads)
 
 // one workgroup: block maps and their scan, entries and token offsets, pass 1 (carries), carry scan ->
@@ -177,12 +215,13 @@ __global__ __launch_bounds__(RUNS_T) void runs_scan_kernel(const uint8_t* __rest
                                                           const unsigned long long* dev_nbits,
                                                           unsigned long long host_nbits, long long num) {
     __shared__ uint32_t pool[RUNS_SW];                          // block maps (steps 1-2), then the stream
-    __shared__ uint32_t ctA[RUNS_T], ctB[RUNS_T];               // token count scan
-    __shared__ uint32_t hkA[RUNS_T], hkB[RUNS_T];               // carry kinds (3 x 8 bits)
-    __shared__ float hvA[RUNS_T * 3], hvB[RUNS_T * 3];          // carry constants
+    __shared__ uint32_t ctA[RUNS_T / 64], ctB[RUNS_T / 64 + 1];    // wave token totals, their offsets
+    __shared__ uint32_t hkA[RUNS_T / 64];                           // wave carries: kinds (3 x 8 bits)
+    __shared__ float hvA[RUNS_T / 64 * 3], hvB[RUNS_T / 64 * 3];    // their constants, wave histories
     __shared__ int bad;
     static_assert(2 * RUNS_T * 8 <= RUNS_SW, "the map double buffer fits the pool");
     const int i = threadIdx.x;
+    RSTAMP(0);
     const unsigned long long nbits = dev_nbits ? *dev_nbits : host_nbits;
     const long long nch = (long long)((nbits + 255) >> 8), nbytes = (long long)((nbits + 7) >> 3);
     if (i == 0) bad = 0;
@@ -192,47 +231,83 @@ __global__ __launch_bounds__(RUNS_T) void runs_scan_kernel(const uint8_t* __rest
     const int Bc = (int)((nch + RUNS_T - 1) / RUNS_T);          // chunks per thread (<= RUNS_BMAX)
     const long long c0 = (long long)i * Bc, c1 = min(c0 + Bc, nch);
 
-    // (1) the block's map: entry bit e of its first chunk -> entry bit of the chunk after it
-    uint8_t bm[32];
+    // (1)+(2) every group's entry.  Inside a wave: an inclusive scan of the group maps over its 64 lanes
+    // by shuffles (X_g <- X_g o X_{g-d}, X_{g-d} applied first; no barrier), the lane's map in registers
+    // and four entries of X_{g-d} at a time looked up in it with v_perm (byte e of the map is byte (e & 7)
+    // of register pair e >> 3: four perms give every pair's candidate, a per-byte select keeps the right
+    // one).  Across waves only one value is needed: the entry of each wave's first group, which thread 0
+    // carries through the wave totals (one byte lookup each).  A block's entry is then its group's entry
+    // through the chunk's prefix map inside the group (runs_map_kernel): one lookup.
+    RSTAMP(1);
+    const long long ngr = (nch + 7) / 8;
+    const int nwv = (int)((ngr + 63) / 64);                     // waves with groups
+    uint32_t m[8];
+    {
+        const uint32_t* gm = reinterpret_cast<const uint32_t*>(R.gmap);
 #pragma unroll
-    for (int e = 0; e < 32; e++) bm[e] = (uint8_t)e;
-    for (long long c = c0; c < c1; c++) {
-#pragma unroll
-        for (int e = 0; e < 32; e++) bm[e] = R.exitm[c * 32 + bm[e]];
+        for (int q = 0; q < 8; q++) m[q] = i < ngr ? gm[i * 8 + q] : 0x03020100u + 0x04040404u * (uint32_t)q;
     }
-    uint32_t* cur = pool;
-    uint32_t* nxt = pool + RUNS_T * 8;
+    auto lookup4 = [&](uint32_t pw) {                            // m at four entries (bytes of pw, < 32)
+        const uint32_t sel = pw & 0x07070707u;
+        const uint32_t pr = (pw >> 3) & 0x03030303u;
+        uint32_t r = __builtin_amdgcn_perm(m[1], m[0], sel);
 #pragma unroll
-    for (int q = 0; q < 8; q++)
-        cur[i * 8 + q] = (uint32_t)bm[4 * q] | (uint32_t)bm[4 * q + 1] << 8 | (uint32_t)bm[4 * q + 2] << 16 |
-                         (uint32_t)bm[4 * q + 3] << 24;
-    __syncthreads();
-    // (2) inclusive scan of the maps (X_i <- X_i o X_{i-d}: X_{i-d} applied first)
-    for (int d = 1; d < RUNS_T; d <<= 1) {
-        const uint8_t* mine = reinterpret_cast<const uint8_t*>(cur + i * 8);
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            uint32_t v = cur[i * 8 + q];
-            if (i >= d) {
-                const uint32_t pw = cur[(i - d) * 8 + q];
-                v = (uint32_t)mine[pw & 31u] | (uint32_t)mine[(pw >> 8) & 31u] << 8 |
-                    (uint32_t)mine[(pw >> 16) & 31u] << 16 | (uint32_t)mine[(pw >> 24) & 31u] << 24;
-            }
-            nxt[i * 8 + q] = v;
+        for (int pp = 1; pp < 4; pp++) {
+            const uint32_t c = __builtin_amdgcn_perm(m[2 * pp + 1], m[2 * pp], sel);
+            const uint32_t t = pr ^ (0x01010101u * (uint32_t)pp);
+            const uint32_t msk = ((((t | (t >> 1)) & 0x01010101u) ^ 0x01010101u)) * 0xFFu;
+            r = (c & msk) | (r & ~msk);
         }
-        __syncthreads();
-        uint32_t* t = cur; cur = nxt; nxt = t;
+        return r;
+    };
+    const int lane = i & 63, wv = i >> 6;
+    if (wv < nwv) {                                             // (wave-uniform)
+        for (int d = 1; d < 64; d <<= 1) {
+            uint32_t pw[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) pw[q] = __shfl_up(m[q], d, 64);
+            if (lane >= d) {
+                uint32_t nm[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) nm[q] = lookup4(pw[q]);
+#pragma unroll
+                for (int q = 0; q < 8; q++) m[q] = nm[q];
+            }
+        }
     }
-    // the block's entry: the maps of every block before it applied to bit 0
-    const int y = i == 0 ? 0 : (int)(reinterpret_cast<const uint8_t*>(cur + (i - 1) * 8)[0]);
+    uint32_t* tot = pool;                                       // the wave totals, then their entries
+    uint8_t* gent = reinterpret_cast<uint8_t*>(pool + 256);     // every group's entry
+    if (lane == 63 && wv < nwv) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) tot[wv * 8 + q] = m[q];
+    }
+    __syncthreads();
+    if (i == 0) {
+        uint32_t v = 0;                                         // the stream's first token: bit 0
+        for (int w = 0; w < nwv; w++) {
+            tot[128 + w] = v;
+            v = (tot[w * 8 + (v >> 2)] >> (8 * (v & 3))) & 0xFFu;
+        }
+    }
+    __syncthreads();
+    if (wv < nwv) {
+        const uint32_t vin = tot[128 + wv];
+        const uint32_t zin = lookup4(vin) & 0xFFu;              // this lane's inclusive map at the wave's entry
+        const int yp = __shfl_up((int)zin, 1, 64);
+        if (i < ngr) gent[i] = (uint8_t)(lane == 0 ? (int)vin : yp);
+    }
+    __syncthreads();
+    const int y = c0 < c1 ? (int)R.pm[c0 * 32 + gent[c0 >> 3]] : 0;   // the block's entry
     __syncthreads();                                            // (the pool takes the stream next)
-
+    RSTAMP(2);
     // the stream into LDS when it fits (coalesced 16-byte loads), for pass 1's walks
+    // (word w at w + w/8: the lanes' blocks lie 8 words apart, unpadded they would share banks)
     const long long nw = (long long)((nbits + 31) >> 5) + 2;
-    const bool staged = nw <= RUNS_SW;
+    const bool staged = nw + (nw >> 3) + 1 <= RUNS_SW;
     if (staged) {
-        for (long long q = i; q < nw; q += RUNS_T) pool[q] = rs_word(s, nbytes, q);
+        for (long long q = i; q < nw; q += RUNS_T) pool[q + (q >> 3)] = rs_word(s, nbytes, q);
     }
+    RSTAMP(3);
     // (3) chunk entries and token counts (needed by pass 1 and the values kernel)
     uint8_t cn[RUNS_BMAX];
     uint32_t nblk = 0;
@@ -249,74 +324,91 @@ __global__ __launch_bounds__(RUNS_T) void runs_scan_kernel(const uint8_t* __rest
             }
         }
     }
-    uint32_t* ca = ctA;
-    uint32_t* cb = ctB;
-    ca[i] = nblk;
+    // token offsets: DPP wave scans, the 16 wave totals scanned by thread 0
+    const uint32_t cinc = wave_scan_incl(nblk);
+    if (lane == 63) ctA[wv] = cinc;
     __syncthreads();
-    for (int d = 1; d < RUNS_T; d <<= 1) {
-        cb[i] = ca[i] + (i >= d ? ca[i - d] : 0u);
-        __syncthreads();
-        uint32_t* t = ca; ca = cb; cb = t;
+    if (i == 0) {
+        uint32_t acc = 0;
+        for (int w = 0; w < RUNS_T / 64; w++) { ctB[w] = acc; acc += ctA[w]; }
+        ctB[RUNS_T / 64] = acc;
     }
-    const long long T0 = (long long)ca[i] - nblk;               // the block's first token
-    const long long total = ca[RUNS_T - 1];
+    __syncthreads();
+    const long long T0 = (long long)ctB[wv] + cinc - nblk;      // the block's first token
+    const long long total = ctB[RUNS_T / 64];
     if (total < num) {                                          // fewer tokens than values: the reference
         if (i == 0) atomicOr(R.err, RUNS_DECLINE | RUNS_WHY_SHORT);   // reads zeros past the end -> other path
         return;
     }
+    RSTAMP(4);
     // (4) pass 1: the block with symbolic incoming history -> its carry (last three values)
-    RsWords W{staged ? pool : nullptr, s, nbytes, 0};
+    RsWords W{staged ? pool : nullptr, s, nbytes, 0, 1};
     Hs h1 = {1u, 0.f}, h2 = {2u, 0.f}, h3 = {3u, 0.f};
     bool sent = false;
     if (c0 < c1) block_walk<CT, false>(W, P, c0, c1, y, cn, T0, num, nbits, h1, h2, h3, sent, nullptr);
     if (h1.k == 4u || h2.k == 4u || h3.k == 4u) atomicOr(&bad, 1);
     if (sent) atomicOr(&bad, 2);
-    // (5) scan of the carries: slot map composition (later o earlier)
-    uint32_t* ka = hkA;
-    uint32_t* kb = hkB;
-    float* va = hvA;
-    float* vb = hvB;
-    ka[i] = h1.k | h2.k << 8 | h3.k << 16;
-    va[3 * i] = h1.v; va[3 * i + 1] = h2.v; va[3 * i + 2] = h3.v;
+    RSTAMP(5);
+    // (5) the blocks' incoming histories: an inclusive scan of the carries (slot maps: later o earlier)
+    // inside each wave by shuffles, thread 0 carrying the concrete history through the wave totals, and
+    // each block's incoming history = its predecessor's inclusive carry applied to its wave's history
     __syncthreads();
     if (bad) {
         if (i == 0) atomicOr(R.err, RUNS_DECLINE | ((bad & 1) ? RUNS_WHY_EXPR : 0u) | ((bad & 2) ? RUNS_WHY_SENT : 0u));
         return;
     }
-    for (int d = 1; d < RUNS_T; d <<= 1) {
-        uint32_t kk = ka[i];
-        float v0 = va[3 * i], v1 = va[3 * i + 1], v2 = va[3 * i + 2];
-        if (i >= d) {
-            const uint32_t ek = ka[i - d];
-            float r[3] = {v0, v1, v2};
+    uint32_t kk = h1.k | h2.k << 8 | h3.k << 16;
+    float cv[3] = {h1.v, h2.v, h3.v};
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t ek = (uint32_t)__shfl_up((int)kk, d, 64);
+        float ev[3];
+#pragma unroll
+        for (int q = 0; q < 3; q++) ev[q] = __shfl_up(cv[q], d, 64);
+        if (lane >= d) {
             uint32_t nk = 0;
 #pragma unroll
             for (int q = 0; q < 3; q++) {
                 const uint32_t sk = (kk >> (8 * q)) & 0xFFu;
                 if (sk >= 1u && sk <= 3u) {                     // a copy of the earlier carry's slot sk
                     nk |= ((ek >> (8 * (sk - 1))) & 0xFFu) << (8 * q);
-                    r[q] = va[3 * (i - d) + (sk - 1)];
+                    cv[q] = sk == 1u ? ev[0] : (sk == 2u ? ev[1] : ev[2]);
                 } else {
                     nk |= sk << (8 * q);
                 }
             }
-            kk = nk; v0 = r[0]; v1 = r[1]; v2 = r[2];
+            kk = nk;
         }
-        kb[i] = kk;
-        vb[3 * i] = v0; vb[3 * i + 1] = v1; vb[3 * i + 2] = v2;
-        __syncthreads();
-        uint32_t* t = ka; ka = kb; kb = t;
-        float* tv = va; va = vb; vb = tv;
     }
-    // the block's incoming history: every block before it (the stream starts with none -- a prediction
-    // there declined above -- so remaining slot references read 0)
-    float b1 = 0.f, b2 = 0.f, b3 = 0.f;
-    if (i > 0) {
-        const uint32_t kk = ka[i - 1];
-        b1 = ((kk & 0xFFu) == 0u) ? va[3 * (i - 1)] : 0.f;
-        b2 = (((kk >> 8) & 0xFFu) == 0u) ? va[3 * (i - 1) + 1] : 0.f;
-        b3 = (((kk >> 16) & 0xFFu) == 0u) ? va[3 * (i - 1) + 2] : 0.f;
+    if (lane == 63) {
+        hkA[wv] = kk;
+        hvA[3 * wv] = cv[0]; hvA[3 * wv + 1] = cv[1]; hvA[3 * wv + 2] = cv[2];
     }
+    __syncthreads();
+    if (i == 0) {                                               // the stream starts with no history (zeros)
+        float H[3] = {0.f, 0.f, 0.f};
+        for (int w = 0; w < RUNS_T / 64; w++) {
+            hvB[3 * w] = H[0]; hvB[3 * w + 1] = H[1]; hvB[3 * w + 2] = H[2];
+            const uint32_t tk = hkA[w];
+            float nh[3];
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                const uint32_t sk = (tk >> (8 * q)) & 0xFFu;
+                nh[q] = sk == 0u ? hvA[3 * w + q] : H[sk - 1];
+            }
+            H[0] = nh[0]; H[1] = nh[1]; H[2] = nh[2];
+        }
+    }
+    __syncthreads();
+    const float Hw[3] = {hvB[3 * wv], hvB[3 * wv + 1], hvB[3 * wv + 2]};
+    float z[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        const uint32_t sk = (kk >> (8 * q)) & 0xFFu;
+        z[q] = sk == 0u ? cv[q] : (sk == 1u ? Hw[0] : (sk == 2u ? Hw[1] : Hw[2]));
+    }
+    float b1 = __shfl_up(z[0], 1, 64), b2 = __shfl_up(z[1], 1, 64), b3 = __shfl_up(z[2], 1, 64);
+    if (lane == 0) { b1 = Hw[0]; b2 = Hw[1]; b3 = Hw[2]; }
+    RSTAMP(6);
     R.blk[i] = make_uint4((uint32_t)y | (uint32_t)(c1 > c0 ? c1 - c0 : 0) << 8, (uint32_t)T0, 0u, 0u);
     R.bhist[i] = make_float4(b1, b2, b3, 0.0f);
 #pragma unroll
@@ -351,7 +443,7 @@ __global__ __launch_bounds__(64) void runs_values_kernel(const uint8_t* __restri
     for (int j = 0; j < RUNS_BMAX; j++) cn[j] = R.bcnt[i * RUNS_BMAX + j];
     Hs h1 = {0u, hb.x}, h2 = {0u, hb.y}, h3 = {0u, hb.z};
     bool sent = false;
-    RsWords W{row, s, nbytes, 8 * c0};
+    RsWords W{row, s, nbytes, 8 * c0, 0};
     block_walk<CT, true>(W, P, c0, c0 + nc, (int)(b.x & 0xFFu), cn, (long long)b.y, num, nbits, h1, h2, h3, sent, out);
     if (sent) atomicOr(R.err, RUNS_DECLINE | RUNS_WHY_SENT);
 }
@@ -367,6 +459,8 @@ extern "C" int dc_launch_decode_runs(const uint8_t* s, const unsigned long long*
     R.blk = reinterpret_cast<uint4*>(maps + 2 * mb);
     R.bhist = reinterpret_cast<float4*>(maps + 2 * mb + 16 * RUNS_T);
     R.bcnt = maps + 2 * mb + 32 * RUNS_T;
+    R.pm = maps + 2 * mb + 32 * RUNS_T + RUNS_BMAX * RUNS_T;
+    R.gmap = R.pm + mb;
     R.err = err;
     const int g1 = (int)((max_chunks + 7) / 8);
     dc_mark_phase(4, st);
@@ -393,7 +487,7 @@ extern "C" int dc_launch_decode_runs(const uint8_t* s, const unsigned long long*
 }
 extern "C" long long dc_decode_runs_max_chunks(void) { return RUNS_MAXC; }
 extern "C" size_t dc_decode_runs_scratch_bytes(void) {
-    return (size_t)(RUNS_MAXC + 8) * 32 * 2 + (size_t)RUNS_T * (16 + 16 + RUNS_BMAX);
+    return (size_t)(RUNS_MAXC + 8) * 32 * 3 + (size_t)RUNS_T * (16 + 16 + RUNS_BMAX) + (size_t)(RUNS_MAXC / 8 + 8) * 32;
 }
 
 }  // namespace dc

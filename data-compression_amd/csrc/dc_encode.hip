@@ -641,7 +641,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
 #define DC_LB_KS 4                      // look-back windows of 64 states per round trip, with the scanner
 #endif
 #ifndef DC_LB_DMA
-#define DC_LB_DMA 1                     // the first window into LDS before the pack (lb_dma)
+#define DC_LB_DMA 0                     // the first window into LDS before the pack (lb_dma): 194 vs 147 us, off
 #endif
 #ifndef DC_LB_K
 #define DC_LB_K 8
@@ -854,10 +854,11 @@ __device__ void enc_scanner(uint64_t* __restrict__ st, unsigned ntiles, uint32_t
     }
 }
 
-// (6 waves per SIMD asked: the tokens' branch-free selects need ~92 SGPRs of lane masks and 69 VGPRs, which
-// hold 7 workgroups per CU; 8 spilled SGPRs to VGPR lanes and VGPRs to scratch)
+// (7 workgroups per CU: 72 VGPRs, 2 of them spilled, and ~120 SGPRs spilled to VGPR lanes in the CT7 build;
+// the tiles idle through their look-back round trips, so one more resident tile per CU paid: fused
+// 147-148 -> 145 us, 754-762 -> 769-777 GB/s; 6 per CU kept every register)
 #ifndef DC_FUSED_WAVES
-#define DC_FUSED_WAVES 6
+#define DC_FUSED_WAVES 7
 #endif
 template <int CT>
 __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(

@@ -651,13 +651,13 @@ static long long g_runs_max = -2;
 static long long runs_max_bytes(void) {
     if (g_runs_max == -2) {
         const char* e = getenv("DC_RUNS_MAX_BYTES");
-        g_runs_max = (e && *e) ? atoll(e) : (64ll << 10) + 256;
+        g_runs_max = (e && *e) ? atoll(e) : (16ll << 10) + 256;
     }
     return g_runs_max;
 }
 long long dc_set_runs_max_bytes(long long v) {
     const long long old = runs_max_bytes();
-    g_runs_max = v < -1 ? (64ll << 10) + 256 : v;
+    g_runs_max = v < -1 ? (16ll << 10) + 256 : v;
     return old;
 }
 int dc_last_decode_launched_v3(void) { return G.dec3_launched; }

@@ -447,7 +447,7 @@ class Lib:
         return int(self.L.dc_set_decode3_seg(int(seg)))
 
     def set_runs_max_bytes(self, v):
-        """Streams of at most v bytes of capacity use the small-stream decoder (< -1: default 64 KiB + 256,
+        """Streams of at most v bytes of capacity use the small-stream decoder (< -1: default 16 KiB + 256,
         -1: never); returns the previous value."""
         return int(self.L.dc_set_runs_max_bytes(int(v)))
 

@@ -189,7 +189,7 @@ int dc_set_decode3_seg(int seg);
 int dc_last_decode_was_v3(void);
 /* Streams of at most this capacity (bytes) decode with the small-stream decoder (dc_decode_runs.hip: chunk
  * entry maps composed by a scan, one workgroup), unless dc_set_decode3_min_bytes(0) forces the segment
- * decoder; Himeno halo planes take it whatever their capacity (< -1: the default, 64 KiB + 256: 2^14 floats; -1:
+ * decoder; Himeno halo planes take it whatever their capacity (< -1: the default, 16 KiB + 256: 2^12 floats; -1:
  * never).  Returns the previous value. */
 long long dc_set_runs_max_bytes(long long max_bytes);
 /* 1 if the last decode's values came from the small-stream decoder (after dc_decode_finish). */

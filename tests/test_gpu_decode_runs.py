@@ -70,10 +70,10 @@ def test_runs_long_copy_chains(rd, oracle, ct):
 
 
 def test_runs_device_chain_default_threshold(dc, oracle):
-    """The bench's 2^14 sweep point with default thresholds: encode_device -> decode_device from the device
-    bit count goes through the small-stream decoder and equals the oracle."""
+    """2^12 floats with default thresholds (16 KiB + 68 of capacity): encode_device -> decode_device from
+    the device bit count goes through the small-stream decoder and equals the oracle."""
     import torch
-    n = 1 << 14
+    n = 1 << 12
     dc.set_bound(1e-3)
     _, xs = oracle.to_small(oracle.gen_u10(n))
     t, m17 = oracle.type_mask(xs)

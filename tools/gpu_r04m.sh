@@ -11,8 +11,8 @@ run() {
   DCAMD_LIB=data-compression_amd/$1/libdcamd.so timeout -k 10 200 python3 -u bench.py --no-cpu --no-pipelined --no-extra --steps 20 $2 > gpurun_out/ab.json 2> gpurun_out/ab.err || { tail -20 gpurun_out/ab.err; return 1; }
   python3 -c "import json,sys;d=json.loads(open('gpurun_out/ab.json').readline());print(*sys.argv[1:],d['value'],d['ms_per_step'],d['kernels_ms'])" $1 "$2"
 }
-run lib "--log2n 14 --steps 50" && run lib "--log2n 16 --steps 50" || exit 1
-for i in 1 2; do run lib && run lib_w2 && run lib_nd || exit 1; done
+run lib "--log2n 12 --steps 50" && run lib "--log2n 14 --steps 50" || exit 1
+for i in 1 2; do run lib && run lib_w2 && run lib_f7 || exit 1; done
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_halo -o run -- python3 bench.py --halo --steps 20 > gpurun_out/prof_halo.log 2>&1 || { tail -20 gpurun_out/prof_halo.log; exit 1; }
 python3 tools/kstats.py gpurun_out/prof_halo/run_kernel_stats.csv | head -12
