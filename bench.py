@@ -847,7 +847,8 @@ def main():
                     tb = pmc_bytes(kn)
                     if tb is not None and ab > 0:
                         ktraffic[kn] = {"hbm_bytes": int(tb), "algorithmic_bytes": int(ab), "ratio": round(tb / ab, 3)}
-                traffic_src = (f"profiles/pmc_latest.json: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE of this "
+                traffic_src = (f"profiles/pmc_latest.json: rocprofv3 --pmc FETCH_SIZE (x the kernel's calibrated "
+                               f"read-pattern factor, {pj.get('fetch_calibration', 'x2 gfx950')}) + WRITE_SIZE of this "
                                f"bench command, separate passes ({pj.get('source', 'tools/profile.sh')}); not measured "
                                f"in this run") if traffic is not None else None
         except Exception:
