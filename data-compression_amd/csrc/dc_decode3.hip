@@ -41,6 +41,9 @@ namespace dc {
 #ifndef DC_WALK2
 #define DC_WALK2 0
 #endif
+#ifndef DC_EXIT_EARLY
+#define DC_EXIT_EARLY 1                 // 8/16-chunk segments: a job's exit published right after its main walk
+#endif
 // pre-walk: 1024 bits (4 chunks, one region line) before every segment (DC_PARSE_PL6=2: 2048 for CT6 --
 // 12% instead of 94% of its jobs repair, but the longer walk cost more: config 2 parse3 98 vs 92 us)
 #ifndef DC_PARSE_PL6
@@ -51,7 +54,11 @@ constexpr int D3_SEG = 16;             // chunks per parse segment (4 region lin
 constexpr int D3_RING = 16;            // ring words per lane (four 128-bit phases; a power of two: the fetch wraps)
 constexpr int D3_CAP = 1024 + 16;      // decode job output buffer (floats per wave)
 constexpr uint32_t D3_DECLINE = 512u;
+#ifdef DC_DEC3_PROF
+constexpr unsigned long long D3_LINK_WAIT = 200000; // (the profiling build's stamps slow the walks: 2 ms)
+#else
 constexpr unsigned long long D3_LINK_WAIT = 20000;  // s_memrealtime ticks (100 MHz): 200 us
+#endif
 // why (diagnostic bits beside 512): 1024 runs mode / capacity, 2048 unresolved link, 4096 fewer tokens
 // than values, 8192 a job denser than its buffer, 16384 the history sentinel or an early prediction
 constexpr uint32_t D3_WHY_RUNS = 1024u, D3_WHY_LINK = 2048u, D3_WHY_SHORT = 4096u, D3_WHY_DENSE = 8192u,
@@ -350,6 +357,10 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
                       }
                   });
         const int X = r.pos - 256 * seg;                                 // entry of the next segment
+        // the job's exit: 8- and 16-chunk segments publish it right after the main walk (a repair that
+        // moves it is rare enough to decline the stream for), 4-chunk segments after the in-job repairs
+        constexpr bool EARLY_EXIT = seg >= 8 && DC_EXIT_EARLY;
+        if (EARLY_EXIT && lane == 63) st_relaxed(&D3.pexit[job], ((uint64_t)epoch << 32) | (uint32_t)X);
         P3_T(t1);
         P3_ADD(0, t1 - t0);
         P3_ADD(4, act ? tot : 0u);
@@ -373,11 +384,11 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
             // of the last segment moves it -- with 4-chunk segments not rare enough to decline the stream
             // for): it depends on nothing outside the job, so no job waits for more than one main walk
             // and one round of in-job repairs
-            if (lane == 63) st_relaxed(&D3.pexit[job], ((uint64_t)epoch << 32) | (uint32_t)Xcur);
+            if (!EARLY_EXIT && lane == 63) st_relaxed(&D3.pexit[job], ((uint64_t)epoch << 32) | (uint32_t)Xcur);
             bool chk = false;
             if (lane == 0 && act && sidx > 0 && !link0) {
                 // the previous job is resident (a lower workgroup, or this grid's previous round) and
-                // publishes its exit right after its main walk
+                // publishes its exit after its main walk (and in-job repairs, 4-chunk segments)
                 const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
                 P3_T(tw0);
                 uint64_t v;
@@ -420,7 +431,7 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
             const int Xn = live ? r.pos - 256 * seg : Xcur;
             const bool moved = live && whole && Xn != Xcur;
             Xcur = Xn;
-            if (moved && lane == 63 && pass == 1) atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK);   // (published)
+            if (moved && lane == 63 && (pass == 1 || EARLY_EXIT)) atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK);   // (published)
             const int xp = __shfl_up(Xcur, 1, 64);
             const bool mp = __shfl_up((int)moved, 1, 64) != 0;
             bad = lane >= 1 && act && mp && ecur != xp;
