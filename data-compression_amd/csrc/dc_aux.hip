@@ -486,6 +486,92 @@ __global__ __launch_bounds__(MX_T) void med_compose_kernel(const T* __restrict__
     }
 }
 
+// A rank's contiguous shard of the global array (multi-GPU med_dataset_float, dcamd.global_med), one
+// workgroup over the chunk records:
+//   trans = 0: the shard's double sum (an estimate of what it adds), the max of its chunk maxes (NaNs
+//              never win) and x[0]; the global max folds the first shard's x[0] with every shard's max,
+//              strict >, as med_compose_kernel
+//   trans = 1: the whole shard as one transducer for each binade E of the first chunk's window
+//              [elo[0], elo[0] + MW): start parity -> (units added, end parity), "bad" where some chunk has
+//              no transducer for E (E outside its window, or an element it cannot take).  A rank whose
+//              running sum enters in such a binade and stays in it (k + units < 2^24) ends at k + units
+//              without a pass of its own; composing these over the ranks is the exscan of global_med.
+// rec: [0] sum (double bits) [1] max (bits) [2] x[0] (bits) | elo[0] [3 + 2w + p] units from parity p [15 + w] flags
+template <typename T>
+__global__ __launch_bounds__(MX_T) void med_shard_kernel(const T* __restrict__ x, long long nch, MedScratch<T> M,
+                                                         int trans, long long* __restrict__ rec) {
+    typedef MedFP<T> FP;
+    typedef typename FP::D D;
+    __shared__ double ws[MX_T / 64];
+    __shared__ T wm[MX_T / 64];
+    __shared__ D sd[MW][MX_T / 64][2];
+    __shared__ int sf[MW][MX_T / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const long long per = (nch + MX_T - 1) / MX_T, c0 = min(nch, tid * per), c1 = min(nch, c0 + per);
+    if (!trans) {
+        double sm = 0.0;
+        T mx = -INFINITY;
+        for (long long c = c0; c < c1; c++) { sm += M.csum[c]; const T v = M.cmax[c]; mx = v > mx ? v : mx; }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            sm += __shfl_xor(sm, d, 64);
+            const T o = __shfl_xor(mx, d, 64);
+            mx = o > mx ? o : mx;
+        }
+        if (lane == 0) { ws[wid] = sm; wm[wid] = mx; }
+        __syncthreads();
+        if (tid == 0) {
+            double t = 0.0;
+            T mm = -INFINITY;
+            for (int w = 0; w < MX_T / 64; w++) { t += ws[w]; if (wm[w] > mm) mm = wm[w]; }
+            rec[0] = __double_as_longlong(t);
+            rec[1] = (long long)FP::bits(mm);
+            rec[2] = (long long)FP::bits(x[0]);
+        }
+        return;
+    }
+    const int e0 = M.elo[0];
+#pragma unroll 1
+    for (int w = 0; w < MW; w++) {
+        const int E = e0 + w;
+        D a0 = 0, a1 = 0;
+        int q0 = 0, q1 = 1;
+        bool bad = false;
+        for (long long c = c0; c < c1; c++) {
+            const int wc = E - M.elo[c];
+            if (wc < 0 || wc >= MW) { bad = true; break; }
+            const int f = M.F[c * MW + wc];
+            compose(a0, a1, q0, q1, M.Td[(c * MW + wc) * 2], M.Td[(c * MW + wc) * 2 + 1], f & 1, (f >> 1) & 1, FP::SAT);
+            bad |= (f & 4) != 0;
+        }
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {                  // ordered: lane i absorbs lane i + d
+            const D b0 = __shfl_down(a0, d, 64), b1 = __shfl_down(a1, d, 64);
+            const int f = __shfl_down(q0 | (q1 << 1) | ((int)bad << 2), d, 64);
+            if ((lane & (2 * d - 1)) == 0) {
+                compose(a0, a1, q0, q1, b0, b1, f & 1, (f >> 1) & 1, FP::SAT);
+                bad |= (f & 4) != 0;
+            }
+        }
+        if (lane == 0) { sd[w][wid][0] = a0; sd[w][wid][1] = a1; sf[w][wid] = q0 | (q1 << 1) | ((int)bad << 2); }
+    }
+    __syncthreads();
+    if (tid < MW) {
+        const int w = tid;
+        D a0 = sd[w][0][0], a1 = sd[w][0][1];
+        int q0 = sf[w][0] & 1, q1 = (sf[w][0] >> 1) & 1;
+        bool bad = (sf[w][0] & 4) != 0;
+        for (int k = 1; k < MX_T / 64; k++) {
+            compose(a0, a1, q0, q1, sd[w][k][0], sd[w][k][1], sf[w][k] & 1, (sf[w][k] >> 1) & 1, FP::SAT);
+            bad |= (sf[w][k] & 4) != 0;
+        }
+        rec[3 + 2 * w] = (long long)a0;
+        rec[4 + 2 * w] = (long long)a1;
+        rec[15 + w] = q0 | (q1 << 1) | (bad ? 4 : 0);
+        if (w == 0) rec[2] = e0;
+    }
+}
+
 template <typename T>
 static int launch_med(const T* x, long long n, T s_init, void* scratch, T* d_mean, int* d_type, T* d_sum, T* d_max,
                       hipStream_t st) {
@@ -780,6 +866,27 @@ extern "C" int dc_launch_med(const float* x, long long n, float s_init, void* sc
                              float* d_sum, float* d_max, hipStream_t st) {
     return launch_med<float>(x, n, s_init, scratch, d_mean, d_type, d_sum, d_max, st);
 }
+// a rank's shard (med_shard_kernel): trans = 0 its double sum and max; trans = 1 its whole-shard transducer,
+// the chunk windows opened from s_est (the estimated running sum the shard starts at).  The 21-word record
+// lives in the scratch's tail; *d_rec points at it.
+extern "C" int dc_launch_med_shard(const float* x, long long n, double s_est, int trans, void* scratch,
+                                   long long** d_rec, hipStream_t st) {
+    if (n <= 0) return -1;
+    const long long nch = (n + MC - 1) / MC;
+    const MedScratch<float> M = med_scratch<float>(scratch, nch);
+    long long* rec = (long long*)(((uintptr_t)(M.Z + nch) + 7) & ~(uintptr_t)7);
+    *d_rec = rec;
+    hipLaunchKernelGGL(med_chunk_sum_kernel<float>, dim3((unsigned)nch), dim3(MC_T), 0, st, x, n, M);
+    if (trans) {
+        const float se = (float)fmin(fmax(s_est, 0.0), 3.0e38);
+        hipLaunchKernelGGL(med_chunk_scan_kernel<float>, dim3(1), dim3(1024), 0, st, M, nch, se);
+        hipLaunchKernelGGL(med_chunk_trans_kernel<float>, dim3((unsigned)nch), dim3(MC_T), 0, st, x, n, M);
+    }
+    hipLaunchKernelGGL(med_shard_kernel<float>, dim3(1), dim3(MX_T), 0, st, x, nch, M, trans, rec);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+extern "C" int dc_med_shard_binades(void) { return MW; }
+
 // med_dataset_double (:3564-3590): the same on doubles (scratch: dc_med_scratch_bytes64(n))
 extern "C" int dc_launch_med64(const double* x, long long n, void* scratch, double* d_mean, int* d_type, hipStream_t st) {
     return launch_med<double>(x, n, 0.0, scratch, d_mean, d_type, (double*)nullptr, (double*)nullptr, st);

@@ -1117,6 +1117,46 @@ int dc_med_sum_device(const void* d_x, long long n, float s_init, float* sum_out
     return DC_OK;
 }
 
+/* multi-GPU med_dataset_float, the exscan form (dcamd.global_med): a shard's double sum and max (stats), or
+ * its whole-shard transducer for the MW binades [*e_lo, *e_lo + MW) of the window its running sum is
+ * estimated to enter at s_est: units[2w + p] units of 2^(E-150) added from start parity p, flags[w] end
+ * parity from 0 | end parity from 1 << 1 | 4 when the shard is no transducer for that binade; synchronous */
+static int med_shard(const void* d_x, long long n, double s_est, int trans, long long* h) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (n <= 0) return seterr(DC_ERR_ARG, "empty input");
+    if (grow(&G.med_scr, &G.med_scr_cap, (size_t)dc_med_scratch_bytes(n))) return DC_ERR_HIP;
+    long long* d_rec = NULL;
+    if (dc_launch_med_shard((const float*)d_x, n, s_est, trans, G.med_scr, &d_rec, G.st))
+        return seterr(DC_ERR_HIP, "med shard launch failed");
+    HIPCHK(hipMemcpyAsync(h, d_rec, 21 * 8, hipMemcpyDeviceToHost, G.st));
+    HIPCHK(hipStreamSynchronize(G.st));
+    return DC_OK;
+}
+
+int dc_med_shard_stats(const void* d_x, long long n, double* sum_out, float* max_out, float* first_out) {
+    long long h[21];
+    int rc = med_shard(d_x, n, 0.0, 0, h);
+    if (rc) return rc;
+    if (sum_out) memcpy(sum_out, &h[0], 8);
+    if (max_out) { const uint32_t b = (uint32_t)h[1]; memcpy(max_out, &b, 4); }
+    if (first_out) { const uint32_t b = (uint32_t)h[2]; memcpy(first_out, &b, 4); }
+    return DC_OK;
+}
+
+int dc_med_shard_trans(const void* d_x, long long n, double s_est, int* e_lo, long long* units, unsigned char* flags) {
+    long long h[21];
+    const int mw = dc_med_shard_binades();
+    int rc = med_shard(d_x, n, s_est, 1, h);
+    if (rc) return rc;
+    if (e_lo) *e_lo = (int)h[2];
+    for (int w = 0; w < mw; w++) {
+        if (units) { units[2 * w] = h[3 + 2 * w]; units[2 * w + 1] = h[4 + 2 * w]; }
+        if (flags) flags[w] = (unsigned char)h[15 + w];
+    }
+    return DC_OK;
+}
+
 /* type of med_dataset_float from a (global) max (impl/dataCompression.c:3605-3614) */
 int dc_type_from_max(float mx) {
     int add = 0;

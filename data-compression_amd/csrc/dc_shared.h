@@ -188,6 +188,9 @@ int dc_launch_to_small(const float* x, long long n, float* y, float* part_v, lon
 #define DC_MIN_PARTS 2048                /* toSmallDataset: per-workgroup minima combined by min_final */
 int dc_launch_med(const float* x, long long n, float s_init, void* scratch, float* d_mean, int* d_type, float* d_sum,
                   float* d_max, dc_hip_stream st);
+int dc_launch_med_shard(const float* x, long long n, double s_est, int trans, void* scratch, long long** d_rec,
+                        dc_hip_stream st);
+int dc_med_shard_binades(void);
 int dc_launch_ratio(int is_double, int mode, const void* x, long long n, int B, double thr_le, unsigned long long* d_sum,
                     unsigned* d_flag, uint8_t* sizes, dc_hip_stream st);
 int dc_launch_ratio_area(const uint8_t* sizes, long long n, unsigned long long* d_out, dc_hip_stream st);

@@ -48,7 +48,8 @@ EXT_SYMBOLS = [
     "dc_encode_status", "dc_encode_mode", "dc_encode_retries", "dc_crc_resend_device",
     "dc_merge_shards_device", "dc_merge_status", "dc_decode_shard3_device", "dc_decode_shard3_fix",
     "dc_decode_status_clear", "dc_set_runs_max_bytes", "dc_last_decode_was_runs",
-    "dc_last_decode_launched_runs", "dc_set_halo_async",
+    "dc_last_decode_launched_runs", "dc_set_halo_async", "dc_med_shard_stats", "dc_med_shard_trans",
+    "dc_med_shard_binades",
 ]
 
 
@@ -90,6 +91,9 @@ class Lib:
         L.dc_to_small_device.argtypes = [vp, ll, vp, C.POINTER(C.c_float)]
         L.dc_med_device.argtypes = [vp, ll, C.POINTER(C.c_float), C.POINTER(C.c_int)]
         L.dc_med_sum_device.argtypes = [vp, ll, C.c_float, C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.dc_med_shard_stats.argtypes = [vp, ll, C.POINTER(C.c_double), C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.dc_med_shard_trans.argtypes = [vp, ll, C.c_double, C.POINTER(C.c_int), C.POINTER(C.c_longlong),
+                                         C.POINTER(C.c_ubyte)]
         L.dc_type_from_max.argtypes = [C.c_float]
         L.dc_decode_status.argtypes = [C.POINTER(C.c_uint)]
         L.dc_crc32_device.argtypes = [vp, ll, C.POINTER(C.c_uint32)]
@@ -479,6 +483,25 @@ class Lib:
                    "dc_med_sum_device")
         return np.float32(sm.value), np.float32(mx.value)
 
+    def med_shard_stats(self, x_ptr, n):
+        """A shard's double sum (an estimate of what it adds to the running float sum), its max (NaNs never
+        win) and its first element."""
+        sm, mx, x0 = C.c_double(0), C.c_float(0), C.c_float(0)
+        self.check(self.L.dc_med_shard_stats(C.c_void_p(x_ptr), n, C.byref(sm), C.byref(mx), C.byref(x0)),
+                   "dc_med_shard_stats")
+        return float(sm.value), np.float32(mx.value), np.float32(x0.value)
+
+    def med_shard_trans(self, x_ptr, n, s_est):
+        """A shard's whole-shard transducer for the binades of the window its running sum is estimated to
+        enter at s_est: (e_lo, units [MW, 2] int64, flags [MW] uint8), see include/dc_gpu.h."""
+        mw = int(self.L.dc_med_shard_binades())
+        e_lo = C.c_int(0)
+        units = (C.c_longlong * (2 * mw))()
+        flags = (C.c_ubyte * mw)()
+        self.check(self.L.dc_med_shard_trans(C.c_void_p(x_ptr), n, C.c_double(s_est), C.byref(e_lo), units, flags),
+                   "dc_med_shard_trans")
+        return int(e_lo.value), np.array(units[:], np.int64).reshape(mw, 2), np.array(flags[:], np.uint8)
+
     def type_from_max(self, mx):
         return int(self.L.dc_type_from_max(C.c_float(float(mx))))
 
@@ -641,26 +664,81 @@ def _bcast_scalar(v, src, dev, group=None, dtype=None):
     return t.cpu().numpy()[0]
 
 
+def med_apply_shard(e_lo, units, flags, s):
+    """The running float sum s after a shard whose whole-shard transducer (dc_med_shard_trans) is
+    (e_lo, units, flags), or None when the transducer does not cover s: s outside [2^-100, 3e38), s's
+    binade outside the window or marked bad, or the sum leaving its binade (k + units >= 2^24).  Exact:
+    s = k * 2^(E-150) with k in [2^23, 2^24) and the result is (k + units) * 2^(E-150)."""
+    s = np.float32(s)
+    if not (s >= np.float32(2.0 ** -100) and s < np.float32(3.0e38)):
+        return None
+    b = int(np.array([s], np.float32).view(np.uint32)[0])
+    E = (b >> 23) & 0xFF
+    w = E - int(e_lo)
+    if w < 0 or w >= len(flags) or int(flags[w]) & 4:
+        return None
+    k = (b & 0x7FFFFF) | 0x800000
+    k2 = k + int(units[w][k & 1])
+    if k2 >= 1 << 24:
+        return None
+    return np.float32(k2 * 2.0 ** (E - 150))
+
+
 def global_med(L, xs_ptr, n, dev, group=None):
     """med_dataset_float of the global array whose contiguous shard of n floats this rank holds (all
-    shards the same size): the exact left-to-right float sum is continued shard by shard (rank r starts
-    from the sum rank r-1 ended with, one broadcast per rank), the max is all-reduced.  Returns the
-    mean and type every rank agrees on -- those of the single-GPU med_dataset_float of the whole array."""
-    import numpy as _np
+    shards the same size), as an exscan over the ranks (impl/dataCompression.c:3593-3620 sums left to
+    right, so rank r's shard continues the sum rank r-1 ended with):
+      1. every rank: its shard's double sum, max and first value (one pass); one all_gather;
+      2. rank 0: its exact float sum from 0 (dc_med_sum_device); every other rank, in parallel: its
+         whole-shard binade transducer (dc_med_shard_trans) for the window around the double sum of the
+         shards before it; one all_gather;
+      3. every rank composes the same walk over the gathered records: a shard whose transducer covers the
+         incoming sum is applied exactly on the host; one that does not (the running sum crosses a binade
+         inside it -- at most about log2(world) of the ranks after 0) continues the exact sum itself
+         and broadcasts it.
+    The mean and type every rank returns are those of the single-GPU med_dataset_float of the whole array;
+    the max folds rank 0's x[0] with every shard's max (strict >, NaNs never win)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    s = _np.float32(0.0)
-    mx = _np.float32(0.0)
+    sm, mx, x0 = L.med_shard_stats(xs_ptr, n)
+    st = torch.tensor([sm, float(mx), float(x0)], dtype=torch.float64, device=dev)
+    parts = [torch.zeros_like(st) for _ in range(world)]
+    dist.all_gather(parts, st, group=group)
+    stats = [p.cpu().numpy() for p in parts]
+    gmax = np.float32(stats[0][2])
     for r in range(world):
-        if rank == r:
-            s, mx = L.med_sum_device(xs_ptr, n, s)
-        s = _np.float32(_bcast_scalar(float(s), r, dev, group))
-    m = torch.tensor([float(mx)], dtype=torch.float32, device=dev)
-    dist.all_reduce(m, op=dist.ReduceOp.MAX, group=group)
-    gmax = _np.float32(m.cpu().numpy()[0])
-    mean = _np.float32(s / _np.float32(world * n))
+        m = np.float32(stats[r][1])
+        if m > gmax:
+            gmax = m
+    mw = int(L.L.dc_med_shard_binades())
+    rec = np.zeros(2 + 3 * mw, np.int64)          # [s (rank 0, float bits) | e_lo] units[2 mw] flags[mw]
+    if rank == 0:
+        s0, _ = L.med_sum_device(xs_ptr, n, 0.0)
+        rec[0] = int(np.array([s0], np.float32).view(np.uint32)[0])
+    else:
+        s_est = 0.0
+        for r in range(rank):
+            s_est += float(stats[r][0])
+        e_lo, units, flags = L.med_shard_trans(xs_ptr, n, s_est)
+        rec[1] = e_lo
+        rec[2:2 + 2 * mw] = units.reshape(-1)
+        rec[2 + 2 * mw:] = flags
+    t = torch.from_numpy(rec).to(dev)
+    parts = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(parts, t, group=group)
+    recs = [p.cpu().numpy() for p in parts]
+    s = np.array([recs[0][0]], np.uint32).view(np.float32)[0]
+    for q in range(1, world):
+        r = recs[q]
+        s2 = med_apply_shard(r[1], r[2:2 + 2 * mw].reshape(mw, 2), r[2 + 2 * mw:], s)
+        if s2 is None:                            # rank q continues the exact sum itself
+            if rank == q:
+                s2, _ = L.med_sum_device(xs_ptr, n, s)
+            s2 = np.float32(_bcast_scalar(float(s2) if rank == q else 0.0, q, dev, group))
+        s = s2
+    mean = np.float32(s / np.float32(world * n))
     return mean, L.type_from_max(gmax)
 
 

@@ -134,6 +134,15 @@ int dc_med_device(const void* d_x, long long n, float* mean_out, int* type_out);
  * continued from s_init (0 on the first shard, else the sum the previous shard returned) and the max of
  * x; the global mean is sum / (float)n_total and the type dc_type_from_max(global max).  Synchronous. */
 int dc_med_sum_device(const void* d_x, long long n, float s_init, float* sum_out, float* max_out);
+/* The exscan form of the same (every rank in parallel, no chain of passes): a shard's double sum, its max
+ * (NaNs never win; the global max folds the first shard's x[0] with every shard's max, strict >) and x[0],
+ * and its whole-shard transducer for the dc_med_shard_binades() binades E = *e_lo + w of the window its
+ * running sum is estimated to enter at s_est (the double sums of the earlier shards): a sum k * 2^(E-150)
+ * entering with k in [2^23, 2^24) leaves as (k + units[2w + (k & 1)]) * 2^(E-150) when flags[w] & 4 is 0 and
+ * that stays below 2^24; flags[w] & 1 / & 2 are the end parities from start parity 0 / 1.  Synchronous. */
+int dc_med_shard_stats(const void* d_x, long long n, double* sum_out, float* max_out, float* first_out);
+int dc_med_shard_trans(const void* d_x, long long n, double s_est, int* e_lo, long long* units, unsigned char* flags);
+int dc_med_shard_binades(void);
 int dc_type_from_max(float mx);
 /* zlib-compatible CRC-32 of a device byte range. */
 int dc_crc32_device(const void* d_s, long long nbytes, uint32_t* crc_out);

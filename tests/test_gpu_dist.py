@@ -185,3 +185,53 @@ def test_device_step_world2(ct, n, kind):
     assert all(r[1] is True and r[2] is True for r in res), res
     if kind == "u10":
         assert not any(r[3] for r in res), res
+
+
+def _worker_med(rank, world, port, kind, n, q):
+    """dcamd.global_med on device shards (dc_med_shard_stats / dc_med_shard_trans / dc_med_sum_device)
+    against the oracle's med_dataset_float of the whole array."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import dcamd
+        from pyoracle import Oracle
+        from test_med_dist import _case
+        xs = _case(kind, world, n)
+        L = dcamd.Lib()
+        L.init(0)
+        calls = [0]
+        exact = L.med_sum_device
+
+        def counted(*a):
+            calls[0] += 1
+            return exact(*a)
+        L.med_sum_device = counted
+        dev = torch.device("cuda", 0)
+        xd = torch.from_numpy(xs[rank * n:(rank + 1) * n].copy()).to(dev)
+        mean, typ = dcamd.global_med(L, xd.data_ptr(), n, dev)
+        m_ref, t_ref = Oracle().med(xs)
+        ok = bool(np.array([mean], np.float32).view(np.uint32)[0] == np.array([m_ref], np.float32).view(np.uint32)[0]
+                  and typ == t_ref)
+        q.put((rank, ok, calls[0], float(mean), float(m_ref)))
+    except Exception as e:
+        q.put((rank, False, repr(e), None, None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind,world,n", [("u10", 4, 1 << 20), ("u10", 2, (1 << 21) + 5), ("neg", 2, 100000),
+                                          ("nan_cut", 2, 65536), ("zeros_head", 3, 50000)])
+def test_global_med_exscan_device(kind, world, n):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_med, args=(r, world, port, kind, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] is True for r in res), res
+    if kind == "u10" and world == 4:
+        assert sum(r[2] for r in res) < world, res
