@@ -680,15 +680,18 @@ __device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
 // wait timed out.
 // lw0 (optional): the first window as loaded into LDS before the tile's pack (lw0[q] = state s0 + q,
 // lb_dma below); a state it saw unpublished is polled and the window read again as usual.
+// vr (optional): the first window as loaded earlier into registers (vr[k] = lane's k-th state,
+// ld_relaxed(st + t - 1 - lane - 64 k), encode_pipe_kernel).
 template <int LB_K>
 __device__ __forceinline__ int enc_lookback(const uint64_t* __restrict__ st, long long t, uint32_t tag,
                                             unsigned long long& excl, uint32_t& stat, int start_bit,
-                                            const uint64_t* lw0 = nullptr, long long s0 = 0) {
+                                            const uint64_t* lw0 = nullptr, long long s0 = 0,
+                                            const uint64_t* vr = nullptr) {
     const int lane = threadIdx.x & 63;
     long long base = t - 1;
     excl = 0;
     const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
-    bool first = lw0 != nullptr;
+    bool first = lw0 != nullptr || vr != nullptr;
     for (;;) {
         uint64_t v[LB_K];
         int pinc;                                                         // first inclusive position (64 LB_K: none)
@@ -699,7 +702,7 @@ __device__ __forceinline__ int enc_lookback(const uint64_t* __restrict__ st, lon
 #pragma unroll
             for (int k = 0; k < LB_K; k++) {
                 const long long ti = base - (long long)(64 * k + lane);
-                const uint64_t w = first ? lw0[ti - s0] : ld_relaxed(p - 64 * k);
+                const uint64_t w = first ? (vr ? vr[k] : lw0[ti - s0]) : ld_relaxed(p - 64 * k);
                 v[k] = ti >= 0 ? w : st_word(tag, ST_INC, (unsigned long long)start_bit);   // (before tile 0)
             }
             first = false;
@@ -1120,6 +1123,337 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
 #undef E1STAMP
 }
 
+// ---- the persistent, software-pipelined single pass (mode 1 with DC_ENC_PIPE) ----
+// encode_fused_kernel's tile (tools/fused_stamps.py, 2^26 U10 CT7, r04): x loads + tokens 5.4 us, pack 2.3,
+// look-back 3.7, store 2.1 -- seven resident tiles per CU, each idling through two ~3 us memory round trips
+// (x, then the look-back) with its registers and LDS held.  Here a workgroup keeps two tiles in flight in
+// two LDS buffers and loops: while tile i makes its tokens and packs them, the look-back window of tile i-1
+// and the x granules of tile i+1 are in flight; then tile i-1 is stored.  Six barriers per tile:
+//   top       buffer b is free (its last tile was stored); x of tile i is in registers
+//   transpose (wave-local) ; wave 0 requests tile i-1's look-back window and predecessor tail, lane 0 the
+//             ticket of tile i+2
+//   A         tokens of tile i into buffer b
+//   B         x of tile i+1 requested; tokens back into registers; tile i's aggregate and tail published
+//   C         pack tile i into buffer b
+//   D         wave 0: tile i's wave boundary words; tile i-1's look-back evaluated (its window has been in
+//             flight through the tokens and the pack)
+//   E         tile i-1 stored from buffer b ^ 1
+// Tiles come from a ticket counter: a drawn tile's predecessors are held by running workgroups, each of
+// which publishes a tile's aggregate before it waits on anything, so any grid size and any residency make
+// progress.  Every workgroup draws until its first failing ticket; the launch's last draw (ticket
+// ntiles + tile workgroups - 1) resets the counter to 0 for the next encode.
+#ifndef DC_ENC_PIPE
+#define DC_ENC_PIPE 0                   // (DC_ENC_PIPE=1 in the environment selects it at run time)
+#endif
+#ifndef DC_PIPE_WAVES
+#define DC_PIPE_WAVES 4                 // workgroups per CU (two 16.6 KB buffers each)
+#endif
+#ifndef DC_PIPE_STATIC
+#define DC_PIPE_STATIC 0                // (A/B) tiles by workgroup index, every workgroup resident, no ticket
+#endif
+#ifndef DC_PIPE_XTOP
+#define DC_PIPE_XTOP 1                  // the next tile's x requested right after the transpose (0: after the tokens)
+#endif
+constexpr int EP_BUF = E3_WORDS;
+
+// x granules of tile t (load_tile_x's layout) and the three floats before each wave's first (the halo),
+// every load unconditional (buffer resources: a granule or float outside the array reads 0), so a wave's
+// count of memory instructions after them is fixed and the wait for them is exact.  has = false (no next
+// tile): every load is out of range.
+__device__ __forceinline__ void pipe_load_x(f32x4 (&f)[ENC_K / 4], float (&hw)[3], const float* __restrict__ x,
+                                            long long n, long long idx0, long long tbase, bool has, int lane, int wid) {
+    const long long m = has ? min(n - tbase, (long long)ENC_TILE) : 0ll;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x + (has ? tbase : 0)), (short)0, (int)((m + 3) / 4 * 16), 0x00020000);
+#pragma unroll
+    for (int q = 0; q < ENC_K / 4; q++)
+        f[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, 4 * (1024 * wid + 4 * (lane + 64 * q)), 0, DC_PACK_NT ? 2 : 0);
+    // the halo: floats tbase + 1024 wid - k (k = 1..3) exist when inside [-min(3, idx0 + tbase), m) of the tile
+    const int hc = has ? (int)min(3ll, idx0 + tbase) : 0;
+    const __amdgpu_buffer_rsrc_t rh =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x + (has ? tbase : 0) - hc), (short)0, (int)(4 * (m + hc)), 0x00020000);
+#pragma unroll
+    for (int k = 1; k <= 3; k++)
+        hw[k - 1] = __builtin_amdgcn_raw_buffer_load_b32(rh, 4 * (1024 * wid - k + hc), 0, 0);
+}
+
+// wave 0: the exclusive bit offset of tile t (look-back; vr: its first window, requested earlier, or null),
+// its predecessor's tail (tl0: requested earlier, or 0) -> s_G, s_tp, s_ok; the encode's total at the last tile
+__device__ __forceinline__ void pipe_offset(const uint64_t* __restrict__ st, const uint64_t* __restrict__ tl, long long t,
+                                            uint32_t Tt, uint32_t tag, uint32_t epoch, int start_bit, long long n,
+                                            unsigned ntiles, const uint64_t* vr, uint64_t tl0, unsigned* __restrict__ err,
+                                            unsigned long long* __restrict__ total_bits,
+                                            unsigned long long* __restrict__ total_bits2, unsigned long long& s_G,
+                                            uint32_t& s_tp, uint32_t& s_ok) {
+    const int lane = threadIdx.x & 63;
+    unsigned long long G = (unsigned long long)start_bit;
+    uint32_t lbst = 0;
+    int bad = 0;
+    if (t > 0) bad = enc_lookback<DC_LB_KS>(st, t, tag, G, lbst, start_bit, nullptr, 0, vr);
+    if (lane == 0) {
+        uint32_t tp = 0;
+        if (t > 0 && !bad) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            uint64_t v = tl0;
+            while ((v >> 32) != (uint64_t)epoch) {
+                v = ld_relaxed(tl + t - 1);
+                if ((v >> 32) == (uint64_t)epoch) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > LB_WAIT) { bad = 1; break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            tp = (uint32_t)v;
+        }
+        // (the guard of encode_fused_kernel: a tile's bits end within the stream's capacity)
+        if (!bad && G + Tt > (unsigned long long)start_bit + 32ull * (unsigned long long)min(n, (t + 1) * ENC_TILE)) bad = 2;
+        if (bad) atomicOr(err, bad == 2 ? 2u : 4u);
+        else if (t == (long long)ntiles - 1) {
+            *total_bits = G + Tt;
+            if (total_bits2) *total_bits2 = G + Tt;
+        }
+        s_G = G;
+        s_tp = tp;
+        s_ok = bad ? 0u : 1u;
+    }
+}
+
+// waves 1-3: tile t's words (bit buffer sp, Tt bits) from the one holding its first bit, PIPE_NS buffer
+// stores per thread whatever the tile's length (words past it are out of the resource's range and dropped):
+// a fixed count of memory instructions, so the next tile's x loads (issued before) are waited for exactly
+constexpr int PIPE_NS = (E3_WORDS + 1 + 191) / 192;
+__device__ __forceinline__ void pipe_store(uint32_t* __restrict__ out, const uint32_t* sp, uint32_t Tt, long long t,
+                                           unsigned ntiles, unsigned long long Gt, uint32_t tp0, bool ok) {
+    const uint32_t sh = (uint32_t)(Gt & 31ull);
+    const long long W0 = (long long)(Gt >> 5);
+    const int nw = ok ? (int)((long long)((Gt + Tt) >> 5) - W0) + ((t == (long long)ntiles - 1 && ((Gt + Tt) & 31ull)) ? 1 : 0) : 0;
+    const int tw = (int)((Tt + 31u) >> 5);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(out + (ok ? W0 : 0), (short)0, 4 * nw, 0x00020000);
+    const int t0 = max((int)threadIdx.x - 64, 0);
+#pragma unroll
+    for (int j = 0; j < PIPE_NS; j++) {
+        const int i = t0 + 192 * j;
+        const int ic = min(i, EP_BUF - 1);
+        const uint32_t c = i < tw ? sp[ic] : 0u;                           // (stale past the tile's bits)
+        const uint32_t pv = i ? sp[max(ic - 1, 0)] : tp0;
+        const uint32_t w = sh ? __builtin_amdgcn_alignbit(pv, c, sh) : c;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bswap32(w), ro, 4 * i, 0, DC_PACK_NT ? 2 : 0);
+        if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);          // (four at a time: bounded live ranges)
+    }
+}
+
+template <int CT>
+__global__ __launch_bounds__(ENC_TPB, DC_PIPE_WAVES) void encode_pipe_kernel(
+    const float* __restrict__ x, long long n, long long idx0, Params P, uint32_t* __restrict__ out,
+    uint64_t* __restrict__ st, uint64_t* __restrict__ tl, unsigned ntiles, int start_bit,
+    unsigned long long* __restrict__ total_bits, unsigned long long* __restrict__ total_bits2, uint32_t epoch,
+    unsigned* __restrict__ err, unsigned* __restrict__ ticket, unsigned ndraw) {
+    static_assert(ENC_K == 16 && ENC_TPB == 256, "16 consecutive floats per thread, 4 waves per tile");
+    __shared__ __attribute__((aligned(16))) uint32_t sbuf[2][EP_BUF];
+    __shared__ uint32_t s_w[4], s_hw[4], s_hi[4], s_tw[4], s_ti[4];
+    __shared__ uint32_t s_T[2];
+    __shared__ unsigned s_nx, s_k0;
+    __shared__ unsigned long long s_G;
+    __shared__ uint32_t s_tp, s_ok;
+    __shared__ uint16_t tab[512];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t tag = epoch & ST_TAGM;
+    if (blockIdx.x == 0) {                                            // the scanner (dispatched first)
+        enc_scanner(st, ntiles, tag, start_bit, err, s_hw, s_hi, s_tw);
+        return;
+    }
+    build_enc_tab<CT>(tab, P, tid, ENC_TPB);
+    if (DC_PIPE_STATIC) {                                             // (A/B: tile = workgroup + k * grid)
+        if (tid == 0) { s_k0 = blockIdx.x - 1; s_nx = blockIdx.x - 1 + (gridDim.x - 1); }
+    } else if (tid == 0) {
+        unsigned k0 = atomicAdd(ticket, 1u), k1 = ntiles;
+        if (k0 == ndraw - 1) atomicExch(ticket, 0u);
+        if (k0 < ntiles) {
+            k1 = atomicAdd(ticket, 1u);
+            if (k1 == ndraw - 1) atomicExch(ticket, 0u);
+        }
+        s_k0 = k0;
+        s_nx = k1;
+    }
+    __syncthreads();
+    long long cur = (long long)s_k0;
+    if (cur >= (long long)ntiles) return;
+    f32x4 f[ENC_K / 4];
+    float hw[3];
+    pipe_load_x(f, hw, x, n, idx0, cur * ENC_TILE, true, lane, wid);
+    pipe_store(out, sbuf[0], 0u, 0, ntiles, 0ull, 0u, false);         // (no stores: the loop's count)
+    long long prev = -1;
+    int b = 0;
+    for (;;) {
+        __syncthreads();                                              // top: buffer b free, s_nx current
+        const long long nxt = (long long)s_nx;
+        const bool hasn = nxt < (long long)ntiles;
+        uint32_t* sb = sbuf[b];
+        const long long tbase = cur * ENC_TILE;
+        const long long base = tbase + (long long)ENC_K * tid;
+        const bool full = tbase + ENC_TILE <= n;
+        // ---- transpose tile cur (wave-local staging in buffer b) and its history
+        float h[ENC_K + 3];
+        {
+            float* stg = reinterpret_cast<float*>(sb) + wid * E3_STG;
+            f32x4 u[ENC_K / 4];
+#pragma unroll
+            for (int half = 0; half < 2; half++) {
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    const int m = lane + 64 * q;
+                    *reinterpret_cast<f32x4*>(stg + 4 * m + 4 * (m >> 2)) = f[2 * half + q];
+                }
+                __builtin_amdgcn_wave_barrier();
+                if ((lane >> 5) == half)
+#pragma unroll
+                    for (int q = 0; q < ENC_K / 4; q++) u[q] = *reinterpret_cast<const f32x4*>(stg + 20 * (lane & 31) + 4 * q);
+                __builtin_amdgcn_wave_barrier();
+            }
+#pragma unroll
+            for (int q = 0; q < ENC_K / 4; q++) {
+                h[3 + 4 * q] = u[q].x; h[4 + 4 * q] = u[q].y; h[5 + 4 * q] = u[q].z; h[6 + 4 * q] = u[q].w;
+            }
+            h[2] = wave_shr1(h[3 + ENC_K - 1], hw[0]);
+            h[1] = wave_shr1(h[3 + ENC_K - 2], hw[1]);
+            h[0] = wave_shr1(h[3 + ENC_K - 3], hw[2]);
+        }
+        // ---- the next tile's x (in flight through this whole tile), then wave 0: the ticket after it, tile
+        // prev's look-back window and its predecessor's tail (positions before tile 0 read the pad in front)
+        if (DC_PIPE_XTOP) pipe_load_x(f, hw, x, n, idx0, hasn ? nxt * ENC_TILE : 0ll, hasn, lane, wid);
+        uint64_t lbv[DC_LB_KS];
+        uint64_t tl0 = 0ull;
+        unsigned nk = (unsigned)ntiles;
+        if (wid == 0) {
+            const uint64_t* p = st + (prev - 1 - lane);
+#pragma unroll
+            for (int k = 0; k < DC_LB_KS; k++) lbv[k] = ld_relaxed(p - 64 * k);
+            tl0 = ld_relaxed(tl + prev - 1);
+            if (DC_PIPE_STATIC) nk = (unsigned)min((long long)ntiles, nxt + (long long)(gridDim.x - 1));
+            else if (lane == 0 && hasn) nk = atomicAdd(ticket, 1u);
+        }
+        __syncthreads();                                              // A: every wave's transpose is done
+        // ---- the tokens of tile cur: values to buffer b, lengths packed in lp
+        uint32_t lp[ENC_K / 4], mysum;
+        {
+            bool neg1 = false;
+            if (full && idx0 + tbase >= 3) {
+                mysum = make_tokens16<CT, true>(h, P, tab, 0, ENC_K, sb + tid, lp, neg1);
+            } else {
+                const int rem = (int)min(max(n - base, 0ll), (long long)ENC_K);
+                const int g3 = (int)min(max(3 - (idx0 + base), 0ll), (long long)ENC_K);
+#pragma unroll
+                for (int j = 0; j < ENC_K; j++) h[3 + j] = j < rem ? h[3 + j] : 0.0f;
+                mysum = make_tokens16<CT, false>(h, P, tab, g3, rem, sb + tid, lp, neg1);
+            }
+            if (CT != 6 && __any(neg1) && lane == 0) atomicOr(err, 1u);
+        }
+        const uint32_t inc = wave_scan_incl(mysum);
+        if (lane == 63) s_w[wid] = inc;
+        __syncthreads();                                              // B
+        if (!DC_PIPE_XTOP) pipe_load_x(f, hw, x, n, idx0, hasn ? nxt * ENC_TILE : 0ll, hasn, lane, wid);
+        uint32_t tv[ENC_K];
+#pragma unroll
+        for (int j = 0; j < ENC_K; j++) tv[j] = sb[ENC_TPB * j + tid];
+        uint32_t wpre = 0, T = 0;
+#pragma unroll
+        for (int w = 0; w < ENC_TPB / 64; w++) {
+            if (w < wid) wpre += s_w[w];
+            T += s_w[w];
+        }
+        if (tid == 0) {
+            st_relaxed(st + cur, st_word(tag, ST_AGG, T));
+            s_T[b] = T;
+        }
+        if (tid == ENC_TPB - 1 && cur + 1 < (long long)ntiles) {
+            uint64_t acc = 0;
+#pragma unroll
+            for (int j = 0; j < ENC_K; j++) acc = (acc << ((lp[j >> 2] >> (8 * (j & 3))) & 0xFFu)) | tv[j];
+            st_relaxed(tl + cur, ((uint64_t)epoch << 32) | ((uint32_t)acc & 0x7FFFFFFFu));
+        }
+        const uint32_t off = wpre + inc - mysum;
+        __syncthreads();                                              // C: every thread has its tokens back
+        // ---- pack tile cur into buffer b (as encode_fused_kernel)
+        if (full) {
+            uint32_t wi = off >> 5, nb = off & 31u, headw = 0u;
+            const uint32_t hi = wi;
+            uint64_t acc = 0;
+            bool have = false;
+#pragma unroll
+            for (int j = 0; j < ENC_K; j++) {
+                const uint32_t len = (lp[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                acc |= (uint64_t)tv[j] << ((64u - nb - len) & 63u);
+                nb += len;
+                if (nb >= 32u) {
+                    const uint32_t w = (uint32_t)(acc >> 32);
+                    if (have) sb[wi] = w;
+                    else headw = w;
+                    have = true;
+                    wi++;
+                    acc <<= 32;
+                    nb -= 32u;
+                }
+            }
+            const uint32_t tailw = (uint32_t)(acc >> 32);
+            const uint32_t pt = wave_shr1_u(tailw, 0u);
+            if (lane == 0) { s_hw[wid] = headw; s_hi[wid] = hi; }
+            else sb[hi] = headw | pt;
+            if (lane == 63) { s_tw[wid] = tailw; s_ti[wid] = nb ? wi : 0xFFFFFFFFu; }
+        } else {
+            for (int i = tid; i < E3_WORDS / 4; i += ENC_TPB) reinterpret_cast<uint4*>(sb)[i] = make_uint4(0u, 0u, 0u, 0u);
+            __syncthreads();
+            uint32_t o = off;
+#pragma unroll
+            for (int j = 0; j < ENC_K; j++) {
+                const uint32_t lj = (lp[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                if (lj) {
+                    const uint64_t v = (uint64_t)tv[j] << ((64u - (o & 31u) - lj) & 63u);
+                    atomicOr(&sb[o >> 5], (uint32_t)(v >> 32));
+                    if ((o & 31u) + lj > 32u) atomicOr(&sb[(o >> 5) + 1], (uint32_t)v);
+                }
+                o += lj;
+            }
+            if (lane == 0) s_hi[wid] = 0xFFFFFFFFu;
+            if (lane == 63) s_ti[wid] = 0xFFFFFFFFu;
+        }
+        __syncthreads();                                              // D
+        // ---- wave 0: tile cur's boundary words; tile prev's offset (its window has been in flight through
+        // the tokens and the pack)
+        if (wid == 0) {
+            if (lane < 4) {
+                const uint32_t hi = s_hi[lane];
+                if (hi != 0xFFFFFFFFu) {
+                    uint32_t w = s_hw[lane];
+                    if (lane > 0 && s_ti[lane - 1] == hi) w |= s_tw[lane - 1];
+                    sb[hi] = w;
+                }
+                if (lane == 3 && s_ti[3] != 0xFFFFFFFFu) sb[s_ti[3]] = s_tw[3];
+            }
+            if (prev >= 0)
+                pipe_offset(st, tl, prev, s_T[b ^ 1], tag, epoch, start_bit, n, ntiles, lbv, tl0, err, total_bits,
+                            total_bits2, s_G, s_tp, s_ok);
+            if (lane == 0 && hasn) {
+                if (!DC_PIPE_STATIC && nk == ndraw - 1) atomicExch(ticket, 0u);
+                s_nx = nk;                                            // (read after the next top barrier)
+            }
+        }
+        __syncthreads();                                              // E
+        // ---- waves 1-3: store tile prev (wave 0 issues the same count with an empty range)
+        pipe_store(out, sbuf[b ^ 1], s_T[b ^ 1], prev, ntiles, s_G, s_tp, wid > 0 && prev >= 0 && s_ok);
+        prev = cur;
+        b ^= 1;
+        if (!hasn) break;
+        cur = nxt;
+    }
+    // ---- the workgroup's last tile (prev, in buffer b ^ 1): look-back and store
+    __syncthreads();
+    if (wid == 0) {
+        const uint64_t tl0 = lane == 0 ? ld_relaxed(tl + prev - 1) : 0ull;
+        pipe_offset(st, tl, prev, s_T[b ^ 1], tag, epoch, start_bit, n, ntiles, nullptr, tl0, err, total_bits,
+                    total_bits2, s_G, s_tp, s_ok);
+    }
+    __syncthreads();
+    pipe_store(out, sbuf[b ^ 1], s_T[b ^ 1], prev, ntiles, s_G, s_tp, wid > 0 && s_ok != 0);
+}
+
 // ------------------------------------------------------------------------------------------------
 #define DC_ENC_DISPATCH(KER, ...)                                                                  \
     switch (P->ct) {                                                                               \
@@ -1161,6 +1495,23 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
         uint64_t* st = desc + ((desc_words_multi(ntiles) + 1) & ~1ll) + LB_PAD;   // 16-byte aligned (lb_dma)
         static int scan = -1;                                            // DC_ENC_SCAN=0: chained look-back
         if (scan < 0) scan = (getenv("DC_ENC_SCAN") && *getenv("DC_ENC_SCAN") == '0') ? 0 : 1;
+        static int pipe = -1, cus = 0;                                   // DC_ENC_PIPE=0: one tile per workgroup
+        if (pipe < 0) {
+            const char* e = getenv("DC_ENC_PIPE");
+            pipe = e ? (*e != '0') : DC_ENC_PIPE;
+            int dev = 0;
+            if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+                cus = 256;
+        }
+        if (pipe && scan && flag) {
+            // persistent workgroups drawing tiles from a ticket counter (flag word 1088: its own 256-byte
+            // line past the pack's 1024 flags, zeroed at init and reset by each launch's last draw)
+            const unsigned g = (unsigned)min((long long)ntiles, (long long)DC_PIPE_WAVES * cus - (DC_PIPE_STATIC ? 1 : 0));
+            DC_ENC_DISPATCH(encode_pipe_kernel, dim3(g + 1), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, st,
+                            st + ntiles, ntiles, start_bit, total_bits, total_bits2, epoch, err, flag + 1088, ntiles + g);
+            dc_mark_phase(1, stream);
+            return hipGetLastError() == hipSuccess ? 0 : -1;
+        }
         DC_ENC_DISPATCH(encode_fused_kernel, dim3(grid + scan), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, st,
                         st + ntiles, ntiles, start_bit, total_bits, total_bits2, epoch, err, dbg, scan);
         dc_mark_phase(1, stream);

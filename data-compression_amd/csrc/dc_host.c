@@ -225,8 +225,9 @@ int dc_init(int device) {
     HIPCHK(hipMalloc((void**)&G.d_total, 64));
     HIPCHK(hipMalloc((void**)&G.d_enc_err, 64));
     HIPCHK(hipMemset(G.d_enc_err, 0, 64));
-    HIPCHK(hipMalloc((void**)&G.d_enc_flag, 4096));          /* a flag per 2048 tiles: up to 2^33 floats */
-    HIPCHK(hipMemset(G.d_enc_flag, 0, 4096));
+    /* a flag per 2048 tiles (up to 2^33 floats) + the single pass's tile ticket (word 1088) */
+    HIPCHK(hipMalloc((void**)&G.d_enc_flag, 8192));
+    HIPCHK(hipMemset(G.d_enc_flag, 0, 8192));
     G.enc_epoch = 0;
     HIPCHK(hipMalloc((void**)&G.part_v, DC_MIN_PARTS * sizeof(float)));
     HIPCHK(hipMalloc((void**)&G.part_i, DC_MIN_PARTS * sizeof(long long)));

@@ -210,6 +210,7 @@ def test_back_to_back_encodes_2p26(dc, oracle):
     same = True
     for _ in range(48):
         st.zero_()
+        torch.cuda.synchronize()          # (the library stream is non-blocking: no order with torch's)
         dc.encode_device(7, dx.data_ptr(), n, st.data_ptr(), type_=t, mask17=m17)
         dc.synchronize()
         same &= bool(torch.equal(st[:nb], first[:nb]))
