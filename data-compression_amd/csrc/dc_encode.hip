@@ -863,6 +863,9 @@ __device__ void enc_scanner(uint64_t* __restrict__ st, unsigned ntiles, uint32_t
 #ifndef DC_FUSED_WAVES
 #define DC_FUSED_WAVES 7
 #endif
+#ifndef DC_STORE_U
+#define DC_STORE_U 1                    // (A/B) words per thread per store round: 4 and 8 measured equal, off
+#endif
 template <int CT>
 __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
     const float* __restrict__ x, long long n, long long idx0, Params P, uint32_t* __restrict__ out,
@@ -1109,6 +1112,26 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
     const long long W0 = (long long)(Gt >> 5);
     const int nw = (int)((long long)((Gt + T) >> 5) - W0) + ((tile == ntiles - 1 && ((Gt + T) & 31ull)) ? 1 : 0);
     const int tw = (int)((T + 31u) >> 5);                                  // buffer words holding tile bits
+#if DC_STORE_U > 1
+    // DC_STORE_U words per thread per round: their LDS reads are in flight together (one word per round
+    // waited on one LDS round trip each)
+    for (int i0 = tid; i0 < nw; i0 += DC_STORE_U * ENC_TPB) {
+        uint32_t wv[DC_STORE_U];
+#pragma unroll
+        for (int u = 0; u < DC_STORE_U; u++) {
+            const int i = i0 + u * ENC_TPB;
+            const int ic = min(i, E3_WORDS - 1);
+            const uint32_t cur = i < tw ? sb[ic] : 0u;                     // (stale past the tile's bits)
+            const uint32_t prev = i ? sb[ic - 1] : tp0;
+            wv[u] = sh ? __builtin_amdgcn_alignbit(prev, cur, sh) : cur;
+        }
+#pragma unroll
+        for (int u = 0; u < DC_STORE_U; u++) {
+            const int i = i0 + u * ENC_TPB;
+            if (i < nw) __builtin_nontemporal_store(__builtin_bswap32(wv[u]), out + W0 + i);
+        }
+    }
+#else
     for (int i = tid; i < nw; i += ENC_TPB) {
         const uint32_t cur = i < tw ? sb[i] : 0u;                          // (stale past the tile's bits)
         const uint32_t prev = i ? sb[i - 1] : tp0;
@@ -1119,6 +1142,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
         out[W0 + i] = __builtin_bswap32(w);
 #endif
     }
+#endif
     E1STAMP(5);
 #undef E1STAMP
 }
@@ -1245,8 +1269,11 @@ __global__ __launch_bounds__(ENC_TPB, DC_PIPE_WAVES) void encode_pipe_kernel(
     const float* __restrict__ x, long long n, long long idx0, Params P, uint32_t* __restrict__ out,
     uint64_t* __restrict__ st, uint64_t* __restrict__ tl, unsigned ntiles, int start_bit,
     unsigned long long* __restrict__ total_bits, unsigned long long* __restrict__ total_bits2, uint32_t epoch,
-    unsigned* __restrict__ err, unsigned* __restrict__ ticket, unsigned ndraw) {
+    unsigned* __restrict__ err, unsigned* __restrict__ ticket, unsigned ndraw, unsigned long long* __restrict__ dbg) {
     static_assert(ENC_K == 16 && ENC_TPB == 256, "16 consecutive floats per thread, 4 waves per tile");
+    // (DC_DEBUG_STAMPS: per tile, s_memrealtime at the top, after barriers A..E and after the stores of the
+    // following iteration, by thread 0)
+#define EPSTAMP(t, ph) do { if (dbg && tid == 0 && (t) >= 0 && (t) < 16384) dbg[(t) * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); } while (0)
     __shared__ __attribute__((aligned(16))) uint32_t sbuf[2][EP_BUF];
     __shared__ uint32_t s_w[4], s_hw[4], s_hi[4], s_tw[4], s_ti[4];
     __shared__ uint32_t s_T[2];
@@ -1284,6 +1311,8 @@ __global__ __launch_bounds__(ENC_TPB, DC_PIPE_WAVES) void encode_pipe_kernel(
     int b = 0;
     for (;;) {
         __syncthreads();                                              // top: buffer b free, s_nx current
+        EPSTAMP(cur, 0);
+        if (dbg && tid == 0 && cur < 16384) dbg[cur * 8 + 7] = blockIdx.x;
         const long long nxt = (long long)s_nx;
         const bool hasn = nxt < (long long)ntiles;
         uint32_t* sb = sbuf[b];
@@ -1331,6 +1360,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_PIPE_WAVES) void encode_pipe_kernel(
             else if (lane == 0 && hasn) nk = atomicAdd(ticket, 1u);
         }
         __syncthreads();                                              // A: every wave's transpose is done
+        EPSTAMP(cur, 1);
         // ---- the tokens of tile cur: values to buffer b, lengths packed in lp
         uint32_t lp[ENC_K / 4], mysum;
         {
@@ -1349,6 +1379,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_PIPE_WAVES) void encode_pipe_kernel(
         const uint32_t inc = wave_scan_incl(mysum);
         if (lane == 63) s_w[wid] = inc;
         __syncthreads();                                              // B
+        EPSTAMP(cur, 2);
         if (!DC_PIPE_XTOP) pipe_load_x(f, hw, x, n, idx0, hasn ? nxt * ENC_TILE : 0ll, hasn, lane, wid);
         uint32_t tv[ENC_K];
 #pragma unroll
@@ -1371,6 +1402,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_PIPE_WAVES) void encode_pipe_kernel(
         }
         const uint32_t off = wpre + inc - mysum;
         __syncthreads();                                              // C: every thread has its tokens back
+        EPSTAMP(cur, 3);
         // ---- pack tile cur into buffer b (as encode_fused_kernel)
         if (full) {
             uint32_t wi = off >> 5, nb = off & 31u, headw = 0u;
@@ -1415,6 +1447,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_PIPE_WAVES) void encode_pipe_kernel(
             if (lane == 63) s_ti[wid] = 0xFFFFFFFFu;
         }
         __syncthreads();                                              // D
+        EPSTAMP(cur, 4);
         // ---- wave 0: tile cur's boundary words; tile prev's offset (its window has been in flight through
         // the tokens and the pack)
         if (wid == 0) {
@@ -1436,8 +1469,10 @@ __global__ __launch_bounds__(ENC_TPB, DC_PIPE_WAVES) void encode_pipe_kernel(
             }
         }
         __syncthreads();                                              // E
+        EPSTAMP(cur, 5);
         // ---- waves 1-3: store tile prev (wave 0 issues the same count with an empty range)
         pipe_store(out, sbuf[b ^ 1], s_T[b ^ 1], prev, ntiles, s_G, s_tp, wid > 0 && prev >= 0 && s_ok);
+        EPSTAMP(cur, 6);
         prev = cur;
         b ^= 1;
         if (!hasn) break;
@@ -1452,6 +1487,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_PIPE_WAVES) void encode_pipe_kernel(
     }
     __syncthreads();
     pipe_store(out, sbuf[b ^ 1], s_T[b ^ 1], prev, ntiles, s_G, s_tp, wid > 0 && s_ok != 0);
+#undef EPSTAMP
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1508,7 +1544,8 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
             // line past the pack's 1024 flags, zeroed at init and reset by each launch's last draw)
             const unsigned g = (unsigned)min((long long)ntiles, (long long)DC_PIPE_WAVES * cus - (DC_PIPE_STATIC ? 1 : 0));
             DC_ENC_DISPATCH(encode_pipe_kernel, dim3(g + 1), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, st,
-                            st + ntiles, ntiles, start_bit, total_bits, total_bits2, epoch, err, flag + 1088, ntiles + g);
+                            st + ntiles, ntiles, start_bit, total_bits, total_bits2, epoch, err, flag + 1088, ntiles + g,
+                            dbg);
             dc_mark_phase(1, stream);
             return hipGetLastError() == hipSuccess ? 0 : -1;
         }
