@@ -623,6 +623,9 @@ __device__ __forceinline__ uint32_t xpow8n(unsigned long long n, const uint32_t*
 #ifndef DC_CRC_NIB
 #define DC_CRC_NIB 1
 #endif
+#ifndef DC_CRC_DIAG
+#define DC_CRC_DIAG 0                   // (diagnostics: 1 = loads without the table step, 2 = table steps without loads)
+#endif
 #ifndef DC_CRC_STAGE
 #define DC_CRC_STAGE 0                  // (staging full blocks through LDS: 66 -> 71 us per pass, off)
 #endif
@@ -671,14 +674,17 @@ __global__ __launch_bounds__(256) void crc_blocks_kernel(const uint8_t* __restri
             uint4 q[CRC_RUN / 16];
 #pragma unroll
             for (int i = 0; i < CRC_RUN / 16; i++)
-                q[i] = staged ? *reinterpret_cast<const uint4*>(&stg[t * 36 + 4 * i]) : p4[i];
+                q[i] = DC_CRC_DIAG == 2 ? make_uint4((uint32_t)st + i, (uint32_t)b, 3u * i, 7u)   // (diagnostic: no loads)
+                                        : staged ? *reinterpret_cast<const uint4*>(&stg[t * 36 + 4 * i]) : p4[i];
 #pragma unroll
             for (int i = 0; i < CRC_RUN / 16; i++) {
                 const uint32_t w[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const uint32_t c = r ^ w[j];
-                    if (DC_CRC_NIB) {
+                    if (DC_CRC_DIAG == 1) {                  // (diagnostic: loads only, no table step)
+                        r = (c << 1) ^ (c >> 31);
+                    } else if (DC_CRC_NIB) {
                         r = (nib[0 * 16 + (c & 15u)] ^ nib[1 * 16 + ((c >> 4) & 15u)]) ^
                             (nib[2 * 16 + ((c >> 8) & 15u)] ^ nib[3 * 16 + ((c >> 12) & 15u)]) ^
                             ((nib[4 * 16 + ((c >> 16) & 15u)] ^ nib[5 * 16 + ((c >> 20) & 15u)]) ^
@@ -746,6 +752,73 @@ __global__ __launch_bounds__(256) void crc_final_kernel(const uint32_t* __restri
         uint32_t R = red[0];
         if (F.nblk > 0) R = multmodp(F.kl, R) ^ part[F.nblk - 1];
         // zlib: crc32(init, buf) = ~(raw(buf) ^ shift(~init, n))
+        *out = ~(R ^ multmodp(F.xn, ~init));
+    }
+}
+
+// DC_CRC_FIN2 (default): the same combine on 1024 threads with table-driven constant multiplies.  A product
+// a * K mod P is linear in a: with B[i] = (bit i alone) * K = K x^(31 - i) (B[31] = K, each lower one the
+// next times x: a shift and a conditional xor), the four byte tables T[j][v] = XOR of B[8 j + k] over the set
+// bits k of v give a * K = T[0][a & 255] ^ T[1][a >> 8 & 255] ^ T[2][a >> 16 & 255] ^ T[3][a >> 24]: four LDS
+// reads instead of 32 dependent shift/xor steps.  Tables for Kb and the ten tree levels (45 KB of LDS) are
+// built in the kernel (11 lanes compute the bases, every thread 11 entries).
+#ifndef DC_CRC_FIN2
+#define DC_CRC_FIN2 1
+#endif
+constexpr int CF2_T = 1024, CF2_L = 10;
+struct CrcFin2 {
+    uint32_t kc[1 + CF2_L];     // kc[0] = Kb = x^(8 CRC_BLK); kc[1 + l] = x^(8 CRC_BLK per 2^l)
+    uint32_t kl, xn;
+    long long nblk, per, pad;
+};
+__device__ __forceinline__ uint32_t mul_tab(const uint32_t (*T)[256], uint32_t a) {
+    return (T[0][a & 255u] ^ T[1][(a >> 8) & 255u]) ^ (T[2][(a >> 16) & 255u] ^ T[3][a >> 24]);
+}
+__global__ __launch_bounds__(CF2_T) void crc_final2_kernel(const uint32_t* __restrict__ part, CrcFin2 F, uint32_t init,
+                                                           uint32_t* __restrict__ out) {
+    __shared__ uint32_t T[1 + CF2_L][4][256];
+    __shared__ uint32_t B[1 + CF2_L][32];
+    __shared__ uint32_t red[CF2_T];
+    const int t = threadIdx.x;
+    if (t < 1 + CF2_L) {
+        uint32_t b = F.kc[t];
+        B[t][31] = b;
+        for (int i = 30; i >= 0; i--) {
+            b = (b & 1u) ? (b >> 1) ^ CRC_POLY : b >> 1;
+            B[t][i] = b;
+        }
+    }
+    __syncthreads();
+    for (int e = t; e < (1 + CF2_L) * 1024; e += CF2_T) {
+        const int c = e >> 10, j = (e >> 8) & 3, v = e & 255;
+        uint32_t x = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if ((v >> k) & 1) x ^= B[c][8 * j + k];
+        T[c][j][v] = x;
+    }
+    __syncthreads();
+    uint32_t r = 0;
+    const long long m = F.nblk > 0 ? F.nblk - 1 : 0;                 // full blocks
+    for (long long i = 0; i < F.per; i++) {
+        const long long b = (long long)t * F.per + i - F.pad;
+        r = mul_tab(T[0], r) ^ (b >= 0 && b < m ? part[b] : 0u);
+    }
+    red[t] = r;
+    __syncthreads();
+#pragma unroll
+    for (int l = 0; l < CF2_L; l++) {
+        const int w = 1 << l;
+        uint32_t v = 0;
+        const bool act = (t & (2 * w - 1)) == 0;
+        if (act) v = mul_tab(T[1 + l], red[t]) ^ red[t + w];
+        __syncthreads();
+        if (act) red[t] = v;
+        __syncthreads();
+    }
+    if (t == 0) {
+        uint32_t R = red[0];
+        if (F.nblk > 0) R = multmodp(F.kl, R) ^ part[F.nblk - 1];
         *out = ~(R ^ multmodp(F.xn, ~init));
     }
 }
@@ -902,6 +975,20 @@ extern "C" int dc_launch_crc32(const uint8_t* s, long long nbytes, const uint32_
         long long g = nblk > 4096 ? 4096 : nblk;
         hipLaunchKernelGGL(crc_blocks_kernel, dim3((unsigned)g), dim3(256), 0, st, s, nbytes, d_tab, d_tab + 1024,
                            d_x2n, d_parts);
+    }
+    if (DC_CRC_FIN2) {
+        CrcFin2 F2;
+        F2.nblk = nbytes > 0 ? nblk : 0;
+        const long long m2 = F2.nblk > 0 ? F2.nblk - 1 : 0;
+        F2.per = m2 > 0 ? (m2 + CF2_T - 1) / CF2_T : 0;
+        F2.pad = CF2_T * F2.per - m2;
+        F2.kc[0] = h_xpow8n((unsigned long long)CRC_BLK);
+        uint32_t kp = h_xpow8n((unsigned long long)CRC_BLK * (unsigned long long)F2.per);
+        for (int l = 0; l < CF2_L; l++) { F2.kc[1 + l] = kp; kp = h_mult(kp, kp); }
+        F2.kl = h_xpow8n((unsigned long long)(nbytes - m2 * CRC_BLK));
+        F2.xn = h_xpow8n((unsigned long long)nbytes);
+        hipLaunchKernelGGL(crc_final2_kernel, dim3(1), dim3(CF2_T), 0, st, d_parts, F2, init, d_out);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     CrcFin F;
     F.nblk = nbytes > 0 ? nblk : 0;
