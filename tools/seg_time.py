@@ -1,0 +1,38 @@
+"""Diagnostic (not a test): decode time (parse3 + decode3) of a 2^k U10 CT7 stream per forced segment length."""
+import os, sys
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "data-compression_amd"))
+import torch, dcamd
+L = dcamd.Lib(); L.init(0); L.set_bound(1e-3)
+lg = int(sys.argv[1]) if len(sys.argv) > 1 else 26
+ct = int(sys.argv[2]) if len(sys.argv) > 2 else 7
+n = 1 << lg
+x = torch.from_numpy(dcamd.gen_u10(n)).cuda()
+cap = L.stream_capacity(n)
+st = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+torch.cuda.synchronize()
+mean, t = L.med_device(x.data_ptr(), n)
+m17 = int(np.array([mean], np.float32).view(np.uint32)[0] >> 15)
+L.encode_device(ct, x.data_ptr(), n, st.data_ptr(), type_=t, mask17=m17)
+nbits = L.encode_result()
+nb = (nbits + 7) // 8
+ls = torch.cuda.ExternalStream(L.L.dc_get_stream())
+ref = None
+for seg in (16, 8, 16, 8):
+    L.set_decode3_seg(seg)
+    out = torch.empty(n, dtype=torch.float32, device="cuda")
+    for _ in range(3):
+        L.decode_device(ct, st.data_ptr(), nb, n, out.data_ptr(), type_=t, mask17=m17, max_bytes=cap)
+        L.decode_finish()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(ls)
+    for _ in range(20):
+        L.decode_device(ct, st.data_ptr(), nb, n, out.data_ptr(), type_=t, mask17=m17, max_bytes=cap)
+    e1.record(ls)
+    L.decode_finish()
+    torch.cuda.synchronize()
+    v3 = L.L.dc_last_decode_was_v3()
+    if ref is None:
+        ref = out.clone()
+    print(f"seg {seg}: decode {e0.elapsed_time(e1) * 1000 / 20:.1f} us per step, v3 {v3}, same {bool(torch.equal(out, ref))}", flush=True)
