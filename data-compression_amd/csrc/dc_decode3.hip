@@ -918,7 +918,13 @@ extern "C" int dc_decode3_seg(long long max_chunks, int B, int ct) {
     const int forced = seg_forced();
     if (forced) return forced;
     if (B > 12) return D3_SEG;
-    return (max_chunks <= 1000000ll && (ct == 5 || ct == 7)) ? 4 : (max_chunks <= 2500000ll ? 8 : D3_SEG);
+    if (max_chunks <= 1000000ll && (ct == 5 || ct == 7)) return 4;
+    // 8-chunk segments: a job exit that a repair moves after it was published declines the stream, and the
+    // chance grows with the job count.  U10 at the default bound (tools/seg_time.py): CT11 declined from 2^24
+    // floats (its 32-bit tokens resynchronise slowly), CT6 from 2^25; CT5 / CT7 never up to 2^26
+    if (ct == 11) return D3_SEG;
+    if (ct == 6) return max_chunks <= 1100000ll ? 8 : D3_SEG;
+    return max_chunks <= 2500000ll ? 8 : D3_SEG;
 }
 
 // DC_DEC3_DEBUG=1: wait for every kernel (at most 2 s each) and report one that does not finish

@@ -177,3 +177,25 @@ def test_decode3_segment_lengths(v3, oracle, seg, kind, n, ct):
             assert v3.last_decode_was_v3(), "an ordinary stream left the segment decoder"
     finally:
         v3.set_decode3_seg(old)
+
+
+@pytest.mark.parametrize("ct,lg", [(11, 24), (6, 24), (6, 25), (5, 24), (7, 24)])
+def test_default_segment_length_mid_sizes(v3, oracle, ct, lg):
+    """The default segment length (dc_decode3_seg) keeps mid-size U10 streams in the segment decoder:
+    8-chunk segments declined CT11 from 2^24 floats and CT6 from 2^25 (a job exit moved after it was
+    published), so those take 16-chunk segments; device stream, decode against the oracle's."""
+    import torch
+    v3.set_bound(1e-3)
+    n = 1 << lg
+    _, xs = oracle.to_small(oracle.gen_u10(n))
+    t, m17 = oracle.type_mask(xs)
+    s, nb, _ = oracle.compress(ct, xs, 1e-3, t, m17)
+    spec, got = oracle.decompress(ct, s, n, 1e-3, t, m17)
+    assert got == n
+    d_s = torch.from_numpy(np.concatenate([s, np.zeros(64, np.uint8)])).cuda()
+    out = torch.empty(n, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    v3.decode_device(ct, d_s.data_ptr(), nb, n, out.data_ptr(), type_=t, mask17=m17, max_bytes=d_s.numel())
+    v3.decode_finish()
+    assert v3.last_decode_was_v3(), "the stream left the segment decoder"
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), spec.view(np.uint32))

@@ -19,7 +19,8 @@ nbits = L.encode_result()
 nb = (nbits + 7) // 8
 ls = torch.cuda.ExternalStream(L.L.dc_get_stream())
 ref = None
-for seg in (16, 8, 16, 8):
+segs = [int(v) for v in sys.argv[3].split(",")] if len(sys.argv) > 3 else [16, 8, 16, 8]
+for seg in segs:
     L.set_decode3_seg(seg)
     out = torch.empty(n, dtype=torch.float32, device="cuda")
     for _ in range(3):
@@ -30,9 +31,12 @@ for seg in (16, 8, 16, 8):
     for _ in range(20):
         L.decode_device(ct, st.data_ptr(), nb, n, out.data_ptr(), type_=t, mask17=m17, max_bytes=cap)
     e1.record(ls)
+    stv = L.decode_status()
+    L.decode_status_clear()
+    L.decode_device(ct, st.data_ptr(), nb, n, out.data_ptr(), type_=t, mask17=m17, max_bytes=cap)
     L.decode_finish()
     torch.cuda.synchronize()
     v3 = L.L.dc_last_decode_was_v3()
     if ref is None:
         ref = out.clone()
-    print(f"seg {seg}: decode {e0.elapsed_time(e1) * 1000 / 20:.1f} us per step, v3 {v3}, same {bool(torch.equal(out, ref))}", flush=True)
+    print(f"2^{lg} ct{ct} seg {seg}: decode {e0.elapsed_time(e1) * 1000 / 20:.1f} us per step, fast-path status 0x{stv:x}, v3 {v3}, same {bool(torch.equal(out, ref))}", flush=True)
