@@ -358,8 +358,11 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
                   });
         const int X = r.pos - 256 * seg;                                 // entry of the next segment
         // the job's exit: 8- and 16-chunk segments publish it right after the main walk (a repair that
-        // moves it is rare enough to decline the stream for), 4-chunk segments after the in-job repairs
-        constexpr bool EARLY_EXIT = seg >= 8 && DC_EXIT_EARLY;
+        // moves it is rare enough to decline the stream for), 4-chunk segments after the in-job repairs;
+        // CT6 always after them (its long tokens at small bounds resynchronise slowly: U10 at 1e-6 declined
+        // at every size, `tools/seg_time.py`; late publication costs ~1 us at 2^26, 3-5 us for CT11, which
+        // keeps the early one)
+        constexpr bool EARLY_EXIT = seg >= 8 && DC_EXIT_EARLY && CT != 6;
         if (EARLY_EXIT && lane == 63) st_relaxed(&D3.pexit[job], ((uint64_t)epoch << 32) | (uint32_t)X);
         P3_T(t1);
         P3_ADD(0, t1 - t0);

@@ -179,18 +179,20 @@ def test_decode3_segment_lengths(v3, oracle, seg, kind, n, ct):
         v3.set_decode3_seg(old)
 
 
-@pytest.mark.parametrize("ct,lg", [(11, 24), (6, 24), (6, 25), (5, 24), (7, 24)])
-def test_default_segment_length_mid_sizes(v3, oracle, ct, lg):
-    """The default segment length (dc_decode3_seg) keeps mid-size U10 streams in the segment decoder:
-    8-chunk segments declined CT11 from 2^24 floats and CT6 from 2^25 (a job exit moved after it was
-    published), so those take 16-chunk segments; device stream, decode against the oracle's."""
+@pytest.mark.parametrize("ct,lg,bound", [(11, 24, 1e-3), (6, 24, 1e-3), (6, 25, 1e-3), (5, 24, 1e-3),
+                                         (7, 24, 1e-3), (6, 20, 1e-6), (6, 24, 1e-6), (11, 22, 1e-6)])
+def test_default_segment_length_mid_sizes(v3, oracle, ct, lg, bound):
+    """The default segment length (dc_decode3_seg) and exit publication keep mid-size U10 streams in the
+    segment decoder: 8-chunk segments declined CT11 from 2^24 floats and CT6 from 2^25, and CT6 at a bound
+    of 1e-6 declined at every size (a job exit moved after it was published), so those take 16-chunk
+    segments and CT6 publishes after its in-job repairs; device stream, decode against the oracle's."""
     import torch
-    v3.set_bound(1e-3)
+    v3.set_bound(bound)
     n = 1 << lg
     _, xs = oracle.to_small(oracle.gen_u10(n))
     t, m17 = oracle.type_mask(xs)
-    s, nb, _ = oracle.compress(ct, xs, 1e-3, t, m17)
-    spec, got = oracle.decompress(ct, s, n, 1e-3, t, m17)
+    s, nb, _ = oracle.compress(ct, xs, bound, t, m17)
+    spec, got = oracle.decompress(ct, s, n, bound, t, m17)
     assert got == n
     d_s = torch.from_numpy(np.concatenate([s, np.zeros(64, np.uint8)])).cuda()
     out = torch.empty(n, dtype=torch.float32, device="cuda")

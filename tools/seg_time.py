@@ -4,7 +4,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "data-compression_amd"))
 import torch, dcamd
-L = dcamd.Lib(); L.init(0); L.set_bound(1e-3)
+L = dcamd.Lib(); L.init(0)
+L.set_bound(float(sys.argv[4]) if len(sys.argv) > 4 else 1e-3)
 lg = int(sys.argv[1]) if len(sys.argv) > 1 else 26
 ct = int(sys.argv[2]) if len(sys.argv) > 2 else 7
 n = 1 << lg
@@ -39,4 +40,11 @@ for seg in segs:
     v3 = L.L.dc_last_decode_was_v3()
     if ref is None:
         ref = out.clone()
-    print(f"2^{lg} ct{ct} seg {seg}: decode {e0.elapsed_time(e1) * 1000 / 20:.1f} us per step, fast-path status 0x{stv:x}, v3 {v3}, same {bool(torch.equal(out, ref))}", flush=True)
+    import time
+    t0 = time.perf_counter()
+    for _ in range(5):
+        L.decode_device(ct, st.data_ptr(), nb, n, out.data_ptr(), type_=t, mask17=m17, max_bytes=cap)
+        L.decode_finish()
+    full = (time.perf_counter() - t0) / 5 * 1e3
+    print(f"   complete decode incl. any slow path (host-synchronised): {full:.3f} ms", flush=True)
+    print(f"2^{lg} ct{ct} bound {L.get_bound() if hasattr(L, 'get_bound') else ''} seg {seg}: decode {e0.elapsed_time(e1) * 1000 / 20:.1f} us per step, fast-path status 0x{stv:x}, v3 {v3}, same {bool(torch.equal(out, ref))}", flush=True)
