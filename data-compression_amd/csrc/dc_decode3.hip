@@ -54,6 +54,11 @@ constexpr int D3_SEG = 16;             // chunks per parse segment (4 region lin
 constexpr int D3_RING = 16;            // ring words per lane (four 128-bit phases; a power of two: the fetch wraps)
 constexpr int D3_CAP = 1024 + 16;      // decode job output buffer (floats per wave)
 constexpr uint32_t D3_DECLINE = 512u;
+#ifndef D3_MAX_ROUNDS
+#define D3_MAX_ROUNDS 8                 // repair rounds of a parse job before the stream is declined (64: a
+                                        // stream that never resynchronises, e.g. a noisy ramp, spent ~1 ms
+                                        // per decode in them; U10 at 1e-3 / 1e-6 never needs more than 8)
+#endif
 #ifdef DC_DEC3_PROF
 constexpr unsigned long long D3_LINK_WAIT = 200000; // (the profiling build's stamps slow the walks: 2 ms)
 #else
@@ -406,7 +411,7 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
             bad = chk && ecur != xin;
         }
         while (__any(bad)) {
-            if (++rounds > 64) { if (lane == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK); break; }
+            if (++rounds > D3_MAX_ROUNDS) { if (lane == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK); break; }
             bool live = bad;
             P3_T(tr0);
             const int nl = run_lines<true>(r, rs, G.nbytes, gw0, 1, seg / 4 + 1, lim, bad ? xin : 0, bad, tl,

@@ -9,7 +9,18 @@ L.set_bound(float(sys.argv[4]) if len(sys.argv) > 4 else 1e-3)
 lg = int(sys.argv[1]) if len(sys.argv) > 1 else 26
 ct = int(sys.argv[2]) if len(sys.argv) > 2 else 7
 n = 1 << lg
-x = torch.from_numpy(dcamd.gen_u10(n)).cuda()
+kind = sys.argv[5] if len(sys.argv) > 5 else "u10"
+if kind == "u10":
+    xh = dcamd.gen_u10(n)
+elif kind == "sine":
+    i = np.arange(n, dtype=np.float64)
+    xh = (np.sin(i * 1e-3) * 50.0 + np.sin(i * 0.37) * 0.5).astype(np.float32)
+elif kind == "normal":
+    xh = np.random.default_rng(1).standard_normal(n).astype(np.float32)
+else:                                                  # ramp with noise
+    xh = (np.arange(n, dtype=np.float64) * 1e-4 + np.random.default_rng(2).random(n) * 1e-2).astype(np.float32)
+xh = xh - xh.min()                                     # (toSmallDataset)
+x = torch.from_numpy(np.ascontiguousarray(xh, np.float32)).cuda()
 cap = L.stream_capacity(n)
 st = torch.zeros(cap, dtype=torch.uint8, device="cuda")
 torch.cuda.synchronize()
@@ -47,4 +58,4 @@ for seg in segs:
         L.decode_finish()
     full = (time.perf_counter() - t0) / 5 * 1e3
     print(f"   complete decode incl. any slow path (host-synchronised): {full:.3f} ms", flush=True)
-    print(f"2^{lg} ct{ct} bound {L.get_bound() if hasattr(L, 'get_bound') else ''} seg {seg}: decode {e0.elapsed_time(e1) * 1000 / 20:.1f} us per step, fast-path status 0x{stv:x}, v3 {v3}, same {bool(torch.equal(out, ref))}", flush=True)
+    print(f"{kind} 2^{lg} ct{ct} bound {L.get_bound() if hasattr(L, 'get_bound') else ''} seg {seg}: decode {e0.elapsed_time(e1) * 1000 / 20:.1f} us per step, fast-path status 0x{stv:x}, v3 {v3}, same {bool(torch.equal(out, ref))}", flush=True)
