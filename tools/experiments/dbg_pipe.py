@@ -1,7 +1,7 @@
 """Diagnostic (not a test): back-to-back encodes of 2^26 U10 CT7, where do repeats differ from the first."""
 import os, sys
 import numpy as np
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "data-compression_amd"))
 import torch, dcamd
 L = dcamd.Lib(); L.init(0); L.set_bound(1e-3)
