@@ -31,6 +31,16 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "data-compression_amd"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
+GOLDEN_HASHES = os.path.join(ROOT, "tests", "golden", "bench_hashes.json")
+
+
+def golden_entry(ct, kind, log2n, bound, world):
+    """The oracle's hashes for this workload (tests/golden/make_bench_hashes.py), or None."""
+    try:
+        g = json.load(open(GOLDEN_HASHES))
+    except (OSError, ValueError):
+        return None
+    return g.get(f"ct{ct}_{kind}_2^{log2n}_{bound:g}_w{world}")
 
 
 def parse():
@@ -630,7 +640,39 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
     if ber > 0:                                       # the CT9 launches between encode and decode, per step
         ct9["phase_ms"] = {nm: float(np.mean([p[i].elapsed_time(p[i + 1]) for p in phs]))
                            for i, nm in enumerate(ct9["phases"])}
-    res = {"nbits": int(nbits), "nbytes": int(nbytes), "wall": wall, "enc_ms": enc_ms, "dec_ms": dec_ms,
+    # ---- self-check: poison the stream and the output, run one more step, and compare device hashes of
+    # both with the oracle's (tests/golden/bench_hashes.json): a step that skipped work would leave poison
+    stream.fill_(0xA5)
+    out.view(torch.int32).fill_(-1)
+    if ber > 0:
+        rcv.fill_(0x5A)
+    torch.cuda.synchronize()
+    step()
+    L.synchronize()
+    chk_bits = L.encode_result()
+    if L.decode_status():
+        L.decode_finish()
+    torch.cuda.synchronize()
+    chk_bytes = (chk_bits + 7) // 8
+    sc = {"stream_hash": f"{L.hash_device(stream.data_ptr(), chk_bytes):016x}",
+          "out_hash": f"{L.hash_device(out.data_ptr(), 4 * n):016x}", "nbits": int(chk_bits)}
+    if ber > 0:
+        sc["received_hash"] = f"{L.hash_device(rcv.data_ptr(), chk_bytes):016x}"
+    g = golden_entry(ct, W["kind"], W["log2n"], W["bound"], C.world)
+    if g is not None and C.world > 1:
+        g = dict(g["ranks"][C.rank], type=g["type"], mask17=g["mask17"])
+    if g is None:
+        sc["ok"] = None
+        sc["golden"] = "none for this workload (tests/golden/make_bench_hashes.py)"
+    else:
+        ok = (int(g["nbits"]) == chk_bits and int(g["stream"]) == int(sc["stream_hash"], 16) and
+              int(g["out"]) == int(sc["out_hash"], 16) and g["type"] == typ and g["mask17"] == f"{mask17:05x}")
+        if ber > 0:
+            ok &= int(g["stream"]) == int(sc["received_hash"], 16)
+        sc["ok"] = bool(ok)
+        sc["golden"] = ("tests/golden/bench_hashes.json: the oracle's stream and decode of this workload"
+                        + (f" (rank {C.rank}'s shard)" if C.world > 1 else ""))
+    res = {"nbits": int(nbits), "nbytes": int(nbytes), "wall": wall, "enc_ms": enc_ms, "dec_ms": dec_ms, "self_check": sc,
            "kavg": kavg, "status": int(status | warm_status), "warm_status": int(warm_status), "resends": timed_resends,
            "slow_path_timed": slow[0], "v3": bool(L.L.dc_last_decode_launched_v3()),
            "runs": bool(L.L.dc_last_decode_launched_runs()),
@@ -703,23 +745,21 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
     return res
 
 
-def copy_bandwidth(dev, n, reps=10):
-    """Achievable HBM rate on this GPU: a device-to-device copy of n floats (torch copy_, one kernel),
-    read + written bytes over its HIP-event time (the practical ceiling a streaming kernel meets)."""
+COPY_VARIANTS = ["4 x 16 B per lane in flight, default policy", "4 x 16 B per lane, nontemporal",
+                 "8 x 16 B per lane, default policy", "8 x 16 B per lane, nontemporal"]
+
+
+def copy_bandwidth(L, dev, n, reps=10):
+    """Achievable HBM rate on this GPU: the best of four hand-written streaming copies (dc_copy_rate_device:
+    16-byte buffer loads and stores, the guide's float4 copy) of n floats, read + written bytes over the
+    average HIP-event launch time on the library stream."""
     import torch
     a = torch.ones(n, dtype=torch.float32, device=dev)
     b = torch.empty_like(a)
-    for _ in range(3):
-        b.copy_(a)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        b.copy_(a)
-    e1.record()
     torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / reps
+    gbs, v = L.copy_rate(a.data_ptr(), b.data_ptr(), 4 * n, reps)
     del a, b
-    return 8.0 * n / (ms * 1e-3) / 1e9
+    return gbs, COPY_VARIANTS[v]
 
 
 def kernel_table(ct, n, nbytes, kavg, v3=True, enc_mode=1, runs=False):
@@ -791,7 +831,8 @@ def side_config(C, ct, kind, log2n, steps, warmup, bound, ber=0.0):
     W = prepare(C, ct, kind, log2n, bound)
     R = run_codec(C, W, steps, warmup, ber=ber)
     out = line_for(C, W, R, steps)
-    out.update({"ct": ct, "input": kind, "floats": W["n"], "type": W["type"], "mask17": f"{W['mask17']:05x}"})
+    out.update({"ct": ct, "input": kind, "floats": W["n"], "type": W["type"], "mask17": f"{W['mask17']:05x}",
+                "self_check": R["self_check"]["ok"]})
     if ber > 0:
         out.update({"ber": ber, "flips_per_step": int(R["nbits"] * ber), "resends": R["resends"],
                     "detected_all": R["resends"] == steps and bool(R["ct9"].get("acks_ok"))})
@@ -826,7 +867,7 @@ def main():
         sys.exit(1)
     kernels = kernel_table(ct, n, nbytes, R["kavg"], R["v3"], R.get("enc_mode", 1), R.get("runs", False))
     dname = main_line["dominant"]["kernel"]
-    achievable = copy_bandwidth(C.dev, n)
+    achievable, copy_how = copy_bandwidth(C.L, C.dev, n)
     traffic, traffic_src, ktraffic = None, None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if os.path.exists(pmc):
@@ -878,7 +919,8 @@ def main():
                      "algorithmic_bytes_per_launch": int(kernels[dname][1]),
                      "avg_launch_ms": main_line["dominant"]["avg_launch_ms"],
                      "achievable": round(achievable, 1),
-                     "achievable_source": f"device copy of 2^{args.log2n} floats (torch copy_), read + written bytes",
+                     "achievable_source": f"hand-written streaming copy of 2^{args.log2n} floats (dc_copy_rate_device, best "
+                                          f"variant: {copy_how}), read + written bytes",
                      "frac_of_achievable": round(main_line["dominant"]["achieved_GBs"] / achievable, 4)},
         "kernels_ms": main_line["kernels_ms"],
         "kernels_traffic": ktraffic,
@@ -887,6 +929,8 @@ def main():
         "pipeline_roofline_frac": round((8.0 * n + 2 * nbytes) / ((R["enc_ms"] + R["dec_ms"]) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         "decoder_fast_path": R["status"] == 0,
         "slow_path_in_timed_step": bool(R["slow_path_timed"]),
+        "self_check": all_ranks_ok(C, R["self_check"]["ok"]),
+        "self_check_detail": R["self_check"],
     }
     if "pipelined" in R:
         res["pipelined"] = R["pipelined"]
@@ -917,8 +961,26 @@ def main():
         res["cpu_baseline"] = cpu_baseline(ct, args.bound, 1 << args.cpu_log2n, args.input)
     if C.rank == 0:
         print(json.dumps(res), flush=True)
+    bad = [nm for nm, ok in [("main", res["self_check"])] + [(f"sweep {k}", v.get("self_check")) for k, v in
+                                                               res.get("sweep", {}).items()]
+           + [(k, v.get("self_check")) for k, v in res.get("configs", {}).items()]
+           + [("end_to_end", res.get("end_to_end", {}).get("self_check"))] if ok is False]
     if C.dist is not None:
         C.dist.destroy_process_group()
+    if bad:
+        sys.exit(f"bench.py: self-check failed ({', '.join(bad)}): the hashes of the last step's stream / decode "
+                 f"differ from the oracle's (tests/golden/bench_hashes.json)")
+
+
+def all_ranks_ok(C, ok):
+    """True / False / None (no golden) over every rank: False if any rank failed."""
+    if C.dist is None:
+        return ok
+    import torch
+    t = torch.tensor([2.0 if ok is None else (1.0 if ok else 0.0)], dtype=torch.float64, device=C.dev)
+    C.dist.all_reduce(t, op=C.dist.ReduceOp.MIN)
+    v = float(t[0])
+    return False if v < 0.5 else (True if v < 1.5 else None)
 
 
 def e2e_run(C, W, steps, warmup):
@@ -968,9 +1030,25 @@ def e2e_run(C, W, steps, warmup):
     if any(st.values()):
         print(f"bench.py: end-to-end status words {st} after the timed steps", file=sys.stderr)
         sys.exit(1)
+    # self-check: poison the merged global stream and the decoded shard, one more step, device hashes against
+    # the oracle's global stream and its decode's slice for this rank (tests/golden/bench_hashes.json)
+    glob.fill_(0xA5)
+    out.view(torch.int32).fill_(-1)
+    torch.cuda.synchronize()
+    step()
+    L.synchronize()
+    torch.cuda.synchronize()
     total = int(d_total.item())
+    gh = L.hash_device(glob.data_ptr(), (total + 7) // 8)
+    oh = L.hash_device(out.data_ptr(), 4 * n)
+    g = golden_entry(ct, W["kind"], W["log2n"], W["bound"], C.world)
+    ok = None if g is None else (int(g["nbits"]) == total and int(g["stream"]) == gh and int(g["e2e_outs"][C.rank]) == oh)
+    ok = all_ranks_ok(C, ok)
     return {"value": round(C.world * 4.0 * n / (wall / steps) / 1e9, 3), "ms_per_step": round(wall / steps * 1e3, 4),
             "global_stream_bytes": (total + 7) // 8, "slot_bytes": slot[0],
+            "self_check": ok, "global_stream_hash": f"{gh:016x}",
+            "self_check_golden": ("tests/golden/bench_hashes.json: the oracle's stream of the whole global array and "
+                                  "its decode, every rank's slice" if g is not None else "none for this workload"),
             "how": "encode at start bit 0 (device bit count) + all-gather of the bit counts and of the shards "
                    "(slots from the warm-up's largest) + one merge kernel (device exscan, shifted shards, "
                    "OR-ed shared words) into the single global stream on every rank + segment-decoder shard "

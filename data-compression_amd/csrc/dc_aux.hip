@@ -1196,6 +1196,78 @@ extern "C" int dc_launch_ham_syndrome(const uint8_t* s, long long nbytes, unsign
 }
 
 // ------------------------------------------------------------------------------------------------
+// bench.py's self-check: an order-dependent hash of a byte buffer, sum over its 32-bit words (little-endian,
+// bytes past nbytes zero) of splitmix64(i << 32 | w_i) mod 2^64 -- additive, so any grid computes it, and
+// tests/golden/make_bench_hashes.py computes the same over the oracle's streams and decodes.
+__global__ __launch_bounds__(256) void hash_words_kernel(const uint32_t* __restrict__ p, long long nbytes,
+                                                         unsigned long long* __restrict__ out) {
+    const long long nw = (nbytes + 3) >> 2;
+    unsigned long long h = 0;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nw; i += (long long)gridDim.x * 256) {
+        uint32_t w = p[i];
+        const long long rem = nbytes - 4 * i;
+        if (rem < 4) w &= (1u << (8 * rem)) - 1u;
+        h += splitmix64(((unsigned long long)i << 32) | w);
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) h += __shfl_xor(h, d, 64);
+    if ((threadIdx.x & 63) == 0 && h) atomicAdd(out, h);
+}
+extern "C" int dc_launch_hash_words(const void* p, long long nbytes, unsigned long long* d_out, hipStream_t st) {
+    (void)hipMemsetAsync(d_out, 0, 8, st);
+    if (nbytes <= 0) return hipGetLastError() == hipSuccess ? 0 : -1;
+    long long g = ((nbytes + 3) / 4 + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(hash_words_kernel, dim3((unsigned)g), dim3(256), 0, st, (const uint32_t*)p, nbytes, d_out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// bench.py's achievable HBM rate: a streaming copy, U 16-byte buffer loads per lane in flight before their
+// stores (the guide's float4 copy reaches 6.29 TB/s), every workgroup a contiguous run of 256 U x 16 B per
+// round; NT: both streams past the caches.  Bytes beyond the last whole 16-byte group are not copied.
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void stream_copy_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                          long long n16) {
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, 0x7FFFFFFF, 0x00020000);
+    const long long per = 256ll * U;
+    for (long long b = (long long)blockIdx.x * per; b < n16; b += (long long)gridDim.x * per) {
+        // (buffers up to 2 GiB: the bench copies at most 1 GiB)
+        v4u v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const long long i = b + 256 * u + threadIdx.x;
+            v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, i < n16 ? (int)(16 * i) : 0x7FFFFFF0, 0, NT ? 2 : 0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const long long i = b + 256 * u + threadIdx.x;
+            __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, i < n16 ? (int)(16 * i) : 0x7FFFFFF0, 0, NT ? 2 : 0);
+        }
+    }
+}
+// variant 0..3: (U, NT) = (4, no), (4, yes), (8, no), (8, yes); grid = 8 workgroups per CU
+extern "C" int dc_launch_stream_copy(const void* src, void* dst, long long bytes, int variant, hipStream_t st) {
+    const long long n16 = bytes / 16;
+    if (n16 <= 0 || bytes > 0x7FFFFF00ll) return -2;
+    int dev = 0, ncu = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const dim3 g((unsigned)(8 * ncu)), b(256);
+    const uint8_t* s = (const uint8_t*)src;
+    uint8_t* d = (uint8_t*)dst;
+    switch (variant) {
+        case 0: hipLaunchKernelGGL(HIP_KERNEL_NAME(stream_copy_kernel<4, false>), g, b, 0, st, s, d, n16); break;
+        case 1: hipLaunchKernelGGL(HIP_KERNEL_NAME(stream_copy_kernel<4, true>), g, b, 0, st, s, d, n16); break;
+        case 2: hipLaunchKernelGGL(HIP_KERNEL_NAME(stream_copy_kernel<8, false>), g, b, 0, st, s, d, n16); break;
+        case 3: hipLaunchKernelGGL(HIP_KERNEL_NAME(stream_copy_kernel<8, true>), g, b, 0, st, s, d, n16); break;
+        default: return -2;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ------------------------------------------------------------------------------------------------
 // Per-kernel timing hooks (bench.py's roofline): when enabled, the launchers record HIP events on
 // their stream between kernels; event set s holds marks 0..3 (encode: start, after count, -, after pack)
 // and 4..7 (decode: start, after parse, after tile fix + scan (chunk-map decoder only), after decode).  dc_decode_finish's slow

@@ -53,6 +53,8 @@ constexpr int D3_SEG = 16;             // chunks per parse segment (4 region lin
 
 constexpr int D3_RING = 16;            // ring words per lane (four 128-bit phases; a power of two: the fetch wraps)
 constexpr int D3_CAP = 1024 + 16;      // decode job output buffer (floats per wave)
+constexpr int D3_CAP_DENSE = 2048 + 32; // the dense instantiation's (< ~16 bits per value, e.g. CT7 at 1e-2: 3
+                                        // workgroups per CU by LDS instead of 4; dc_launch_decode3's `dense`)
 constexpr uint32_t D3_DECLINE = 512u;
 #ifndef D3_MAX_ROUNDS
 #define D3_MAX_ROUNDS 8                 // repair rounds of a parse job before the stream is declined (64: a
@@ -591,13 +593,13 @@ __device__ __forceinline__ Pre3 prefetch3(__amdgpu_buffer_rsrc_t rr, __amdgpu_bu
 }
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return wave_total(v); }
 
-template <int CT, int SEG>
+template <int CT, int SEG, int CAP>
 __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict__ s, Params P, Dec3Bufs D3,
                                                      const unsigned long long* dev_nbits, unsigned long long host_nbits,
                                                      float* __restrict__ out, long long num, uint32_t epoch) {
     __shared__ Lut3 T;
     __shared__ uint32_t stg[4][12 * 64];
-    __shared__ __attribute__((aligned(16))) float obuf[4][D3_CAP];
+    __shared__ __attribute__((aligned(16))) float obuf[4][CAP];
     build_lut3<CT>(T, P, threadIdx.x, 256);
     __syncthreads();
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -661,7 +663,7 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
         P3_ADD(8, u1 - u0);
         // (no `continue` after a lane-conditional store here: the structurizer then peeled the loop head
         // for lanes 1..63 with lane 0 inactive, and their readfirstlane claimed job 0 again, forever)
-        const bool fits = al + Tn <= D3_CAP;
+        const bool fits = al + Tn <= CAP;
         if (!fits) atomicOr(D3.err, D3_DECLINE | D3_WHY_DENSE);        // every lane: OR is idempotent
         bool sent = false;
         if (fits) {
@@ -695,7 +697,7 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
                             if (t < need || t - need < pend || (g == 0 && t < 3)) {
                                 pend = t + 1;                                // needs the previous chunk's values
                                 // a prediction among the stream's first 3 (a shard's: its incoming values)
-                                sent |= g == 0 && t < 3 && !D3.shard;
+                                sent |= g == 0 && t < 3 && D3.shard != 1;
                                 v = 0u;
                             } else {
                                 const float pv = predict_value(need, ob[o - 1], ob[o - 2], ob[o - 3]);
@@ -728,7 +730,7 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
                     h[k - 1] = i >= al ? ob[i] : (job > 0 ? prev_job_value(D3, job, al - i, epoch) : 0.0f);
                 }
                 float b1 = h[0], b2 = h[1], b3 = h[2];
-                if (D3.shard && g == 0) {
+                if (D3.shard == 1 && g == 0) {
                     // a shard's first chunk: its prefix waits for the values before the shard (zeros here,
                     // re-decoded by shard3_fix_kernel).  Values after the prefix never read it; if the
                     // prefix reaches the chunk's last three (read by the next chunk), hand the shard over
@@ -771,9 +773,9 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
         bool sv = false;
         const float4* ob4 = reinterpret_cast<const float4*>(ob);
 #pragma unroll
-        for (int i = 0; i < (D3_CAP + 3) / 4 / 64 + 1; i++) {
+        for (int i = 0; i < (CAP + 3) / 4 / 64 + 1; i++) {
             const int q = lane + 64 * i;
-            const float4 v = ob4[min(q, D3_CAP / 4 - 1)];
+            const float4 v = ob4[min(q, CAP / 4 - 1)];
             const long long gi = gi0 + 4 * q;
             const bool full = fits && q < Q && 4 * q >= al && 4 * q + 4 <= span && gi + 4 <= num;
             if (chk_all && q < Q)
@@ -792,7 +794,7 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
             const long long gi = gi0 + idx;
             const bool qfull = 4 * qe >= al && 4 * qe + 4 <= span && gi0 + 4 * qe + 4 <= num;
             const bool ok = fits && lane < 8 && !qfull && idx >= al && idx < span && gi < num;
-            const float v = ob[min(max(idx, 0), D3_CAP - 1)];
+            const float v = ob[min(max(idx, 0), CAP - 1)];
             (void)ok;
 #ifndef DC_DEC3_NOSTORE
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ro, ok ? (int)(4 * gi) : D3_OOB, 0, DC_DEC3_NT ? 2 : 0);
@@ -816,7 +818,7 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
         asm volatile("" ::: "memory");
         const u32x4 z4 = {0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int i = 0; i < (D3_CAP + 3) / 4 / 64 + 1; i++)
+        for (int i = 0; i < (CAP + 3) / 4 / 64 + 1; i++)
             __builtin_amdgcn_raw_buffer_store_b128(z4, ro, D3_OOB - 64 * (i + 1), 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(0u, ro, D3_OOB, 0, 0);
         for (;;) {
@@ -845,11 +847,14 @@ __global__ __launch_bounds__(64) void shard3_fix_kernel(const uint8_t* __restric
     if (np <= 0) return;
     const __amdgpu_buffer_rsrc_t rs = stream_rsrc(s, D3.capw);
     float b1 = hin[0], b2 = hin[1], b3 = hin[2];
-    uint4 w = load_w4(rs, 1ll << 40, 0);           // (the prefix lies in the chunk's first 288 bits)
+    // (the prefix lies in the chunk's first 288 bits; finish4 takes the byte count as an int, so the stream's
+    // readable capacity bounds it -- 1 << 40 truncated to 0 and zeroed every word)
+    const long long nb = D3.capw * 4;
+    uint4 w = load_w4(rs, nb, 0);
     uint32_t win[12] = {w.x, w.y, w.z, w.w};
-    w = load_w4(rs, 1ll << 40, 4);
+    w = load_w4(rs, nb, 4);
     win[4] = w.x; win[5] = w.y; win[6] = w.z; win[7] = w.w;
-    w = load_w4(rs, 1ll << 40, 8);
+    w = load_w4(rs, nb, 8);
     win[8] = w.x; win[9] = w.y; win[10] = w.z; win[11] = w.w;
     int pos = 0;
     bool sent = false;
@@ -888,6 +893,33 @@ __global__ __launch_bounds__(64) void shard3_fix_kernel(const uint8_t* __restric
         case 1116: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<11, 16>), __VA_ARGS__); break;             \
         default: return -2;                                                                          \
     }
+
+// decode3_kernel<CT, SEG, CAP>: the kernel of a (CT, segment length) for a job buffer of CAP values
+template <int CAP>
+static const void* decode3_fn(int ct, int seg) {
+#define D3F(C)                                                                                       \
+    (seg == 4 ? (const void*)decode3_kernel<C, 4, CAP> : seg == 8 ? (const void*)decode3_kernel<C, 8, CAP> \
+                                                       : (const void*)decode3_kernel<C, 16, CAP>)
+    return ct == 5 ? D3F(5) : ct == 6 ? D3F(6) : ct == 7 ? D3F(7) : D3F(11);
+#undef D3F
+}
+template <int CAP>
+static int launch_decode3_cap(int ct, int seg, int grid, hipStream_t st, const uint8_t* s, const Params& P,
+                              const Dec3Bufs& D3, const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                              float* out, long long num, uint32_t epoch) {
+#define D3C(CTV, SEGV)                                                                              \
+    case CTV * 100 + SEGV:                                                                           \
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(decode3_kernel<CTV, SEGV, CAP>), dim3(grid), dim3(256), 0, st, s, P, D3, \
+                           dev_nbits, host_nbits, out, num, epoch);                                  \
+        break;
+    switch (ct * 100 + seg) {
+        D3C(5, 4) D3C(6, 4) D3C(7, 4) D3C(11, 4) D3C(5, 8) D3C(6, 8) D3C(7, 8) D3C(11, 8)
+        D3C(5, 16) D3C(6, 16) D3C(7, 16) D3C(11, 16)
+        default: return -2;
+    }
+#undef D3C
+    return 0;
+}
 
 static int resident3(const void* f, int threads) {
     int dev = 0, ncu = 256, per = 0;
@@ -977,42 +1009,51 @@ static void dbg_dump(const Dec3Bufs* D3) {
 
 extern "C" int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
                                  const Params* P, const Dec3Bufs* D3, float* out, long long num, uint32_t epoch,
-                                 hipStream_t st) {
-    // resident grids per (CT, segment length) instantiation: every job of a call must be resident at once
-    // (parse3's link wait, decode3's history wait), so each grid is sized from its own kernel's occupancy
-    static int gp[3][12], gd[3][12];
+                                 int dense, hipStream_t st) {
+    // resident grids per (CT, segment length, buffer) instantiation: every job of a call must be resident at
+    // once (parse3's link wait, decode3's history wait), so each grid is sized from its own kernel's occupancy
+    static int gp[3][12], gd[2][3][12];
     const int ci = (P->ct > 0 && P->ct < 12) ? P->ct : 0;
     if (D3->seg != 4 && D3->seg != 8 && D3->seg != 16) return -2;
-    const int si = D3->seg == 16 ? 1 : (D3->seg == 4 ? 2 : 0);
+    if (P->ct != 5 && P->ct != 6 && P->ct != 7 && P->ct != 11) return -2;
+    const int si = D3->seg == 16 ? 1 : (D3->seg == 4 ? 2 : 0), di = dense ? 1 : 0;
     if (!gp[si][ci]) {
         const void* fp;
-        const void* fd;
 #define DC_PICK3(KER, SEGV) (P->ct == 5 ? (const void*)KER<5, SEGV> : P->ct == 6 ? (const void*)KER<6, SEGV>   \
                              : P->ct == 7 ? (const void*)KER<7, SEGV> : (const void*)KER<11, SEGV>)
-        if (si == 1) {
-            fp = DC_PICK3(parse3_kernel, 16);
-            fd = DC_PICK3(decode3_kernel, 16);
-        } else if (si == 2) {
-            fp = DC_PICK3(parse3_kernel, 4);
-            fd = DC_PICK3(decode3_kernel, 4);
-        } else {
-            fp = DC_PICK3(parse3_kernel, 8);
-            fd = DC_PICK3(decode3_kernel, 8);
-        }
+        if (si == 1) fp = DC_PICK3(parse3_kernel, 16);
+        else if (si == 2) fp = DC_PICK3(parse3_kernel, 4);
+        else fp = DC_PICK3(parse3_kernel, 8);
 #undef DC_PICK3
         gp[si][ci] = resident3(fp, 64);
-        gd[si][ci] = resident3(fd, 256);
     }
+    if (!gd[di][si][ci])
+        gd[di][si][ci] = resident3(dense ? decode3_fn<D3_CAP_DENSE>(P->ct, D3->seg) : decode3_fn<D3_CAP>(P->ct, D3->seg), 256);
     const long long maxseg = (D3->max_chunks + D3->seg - 1) / D3->seg;
     const long long maxpj = (maxseg + 63) / 64, maxdj = (D3->max_chunks + 63) / 64;
-    const int g1 = (int)std::max<long long>(1, std::min<long long>(maxpj, gp[si][ci]));
-    const int g3 = (int)std::max<long long>(1, std::min<long long>((maxdj + 3) / 4, gd[si][ci]));
+    int g1 = (int)std::max<long long>(1, std::min<long long>(maxpj, gp[si][ci]));
+    int g3 = (int)std::max<long long>(1, std::min<long long>((maxdj + 3) / 4, gd[di][si][ci]));
+    {   // (experiments, DESIGN section 9: the occupancy a fused parse + decode launch would leave each phase)
+        // DC_P3_PER_CU / DC_D3_PER_CU cap the resident parse waves / decode workgroups per CU
+        static int p3cap = -1, d3cap = -1, ncu = 256;
+        if (p3cap < 0) {
+            const char* a = getenv("DC_P3_PER_CU");
+            const char* b = getenv("DC_D3_PER_CU");
+            p3cap = a ? atoi(a) : 0;
+            d3cap = b ? atoi(b) : 0;
+            int dev = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        }
+        if (p3cap > 0) g1 = std::min(g1, p3cap * ncu);
+        if (d3cap > 0) g3 = std::min(g3, d3cap * ncu);
+    }
     dc_mark_phase(4, st);
     DC_DISPATCH_3(P->ct, D3->seg, parse3_kernel, dim3(g1), dim3(64), 0, st, s, *P, *D3, dev_nbits, host_nbits, num, epoch);
     dbg_wait("parse3_kernel", st);
     dc_mark_phase(5, st);                       // (no mark 6: decode3's slot starts at mark 5)
-    DC_DISPATCH_3(P->ct, D3->seg, decode3_kernel, dim3(g3), dim3(256), 0, st, s, *P, *D3, dev_nbits, host_nbits, out, num,
-                  epoch);
+    if (dense) launch_decode3_cap<D3_CAP_DENSE>(P->ct, D3->seg, g3, st, s, *P, *D3, dev_nbits, host_nbits, out, num, epoch);
+    else launch_decode3_cap<D3_CAP>(P->ct, D3->seg, g3, st, s, *P, *D3, dev_nbits, host_nbits, out, num, epoch);
     dbg_wait("decode3_kernel", st);
     if (getenv("DC_DEC3_DEBUG") && hipStreamQuery(st) != hipSuccess) dbg_dump(D3);
     dc_mark_phase(7, st);

@@ -49,6 +49,8 @@ typedef struct {
         unsigned long long* tot; hipStream_t st; int valid;
     } last_enc;
     int enc_retries;                 /* encodes re-run wait-free (dc_encode_retries) */
+    int enc_outstanding;             /* single-pass encodes issued since the error word was last checked clean
+                                        or cleared: a timeout is retried only when it is the only one */
     /* decoder */
     DecBufs D;
     void* dec_pool;
@@ -71,7 +73,9 @@ typedef struct {
     int dec3_used;                   /* the pending decode ran the segment decoder */
     int dec3_last;                   /* the last finished decode's values came from it */
     int dec3_launched;               /* the last dc_decode_device launched it (it may decline later) */
-    int dec3_skip_once;              /* the next dc_decode_device takes the small-stream decoder (halo planes) */
+    int dec3_dense;                  /* ... with the dense job buffer (dc_launch_decode3's `dense`) */
+    int dense_key;                   /* ct * 256 + bound exponent of the last stream found dense (+1; 0: none):
+                                        later decodes with the same parameters start with the dense buffer */
     int halo_async;                  /* dc_halo_decode_device without dc_decode_finish (dc_set_halo_async) */
     int runs_used;                   /* the pending decode ran the small-stream decoder (dc_decode_runs.hip) */
     int runs_last;                   /* the last finished decode's values came from it */
@@ -412,6 +416,7 @@ static int encode_on(hipStream_t st, int ct, const void* d_x, long long n, long 
     G.last_enc.x = (const float*)d_x; G.last_enc.n = n; G.last_enc.idx0 = idx0; G.last_enc.P = P;
     G.last_enc.out = (uint32_t*)d_out; G.last_enc.start_bit = start_bit; G.last_enc.tot = tot; G.last_enc.st = st;
     G.last_enc.valid = 1;
+    G.enc_outstanding++;
     return DC_OK;
 }
 
@@ -437,11 +442,12 @@ int dc_encode_bits_device(int ct, const void* d_x, long long n, long long idx0, 
         HIPCHK(hipMalloc((void**)&G.enc_desc, cap * sizeof(uint64_t)));
         G.enc_desc_cap = cap;
     }
-    HIPCHK(hipMemsetAsync(G.d_enc_err, 0, 4, ENC_ST));
-    if (dc_launch_encode_bits((const float*)d_x, n, idx0, &P, G.enc_desc, G.d_total, G.d_enc_err, ENC_ST))
+    /* (its own error word: the single-pass encodes' word keeps what they left) */
+    HIPCHK(hipMemsetAsync(G.d_enc_err + 8, 0, 4, ENC_ST));
+    if (dc_launch_encode_bits((const float*)d_x, n, idx0, &P, G.enc_desc, G.d_total, G.d_enc_err + 8, ENC_ST))
         return seterr(DC_ERR_HIP, "encode launch failed");
     HIPCHK(hipMemcpyAsync(&G.h_scratch[0], G.d_total, 8, hipMemcpyDeviceToHost, ENC_ST));
-    HIPCHK(hipMemcpyAsync(&G.h_scratch[1], G.d_enc_err, 4, hipMemcpyDeviceToHost, ENC_ST));
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[1], G.d_enc_err + 8, 4, hipMemcpyDeviceToHost, ENC_ST));
     HIPCHK(hipStreamSynchronize(ENC_ST));
     if (G.h_scratch[1] & 1u) return seterr(DC_ERR_INPUT, "input contains -1.0f (the reference's history sentinel)");
     *bits_out = G.h_scratch[0];
@@ -462,6 +468,7 @@ static int encode_retry(hipStream_t st) {
                          G.d_enc_err, NULL, 3, st))
         return seterr(DC_ERR_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
     G.enc_retries++;
+    G.enc_outstanding = 1;
     return DC_OK;
 }
 int dc_encode_retries(void) { return G.enc_retries; }
@@ -486,6 +493,14 @@ int dc_encode_result(unsigned long long* total_bits) {
     HIPCHK(hipMemcpyAsync(&G.h_scratch[1], G.d_enc_err, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     unsigned err = (unsigned)(G.h_scratch[1] & 0xFFFFFFFFu);
+    if ((err & 4u) && G.enc_outstanding > 1) {
+        /* the error word is OR-ed over every encode since it was last checked: the one that timed out may be
+           an earlier one, whose stream a later launch has already consumed -- re-running the last encode
+           would not repair it, so report it and leave the word set (dc_encode_clear_status clears it) */
+        return seterr(DC_ERR_HIP, "a look-back wait timed out in one of the %d encodes issued since the encoder's "
+                                  "error word was last checked (err=%u): their streams may lack tiles",
+                      G.enc_outstanding, err);
+    }
     if ((err & 4u) && !(err & 1u) && G.last_enc.valid) {
         /* a single-pass tile waited past its bound for a predecessor (a workgroup not resident: another
            process on the GPU) and stored nothing: encode again with the wait-free three-launch variant */
@@ -498,12 +513,25 @@ int dc_encode_result(unsigned long long* total_bits) {
     }
     if (err) {
         HIPCHK(hipMemsetAsync(G.d_enc_err, 0, 4, st));
+        G.enc_outstanding = 0;
         if (err & 1u)
             return seterr(DC_ERR_INPUT, "input contains -1.0f, the reference encoder's empty-history sentinel "
                                         "(impl/dataCompression.c:2032); CT5/7/11 inputs must be >= 0 (toSmallDataset_float)");
         return seterr(DC_ERR_HIP, "encoder tile offsets inconsistent, nothing stored (err=%u)", err);
     }
+    G.enc_outstanding = 0;                       /* every encode so far checked clean */
     if (total_bits) *total_bits = G.h_scratch[0];
+    return DC_OK;
+}
+
+/* clear the single-pass encoder's error word (after dc_encode_result reported a timeout among several
+   outstanding encodes) */
+int dc_encode_clear_status(void) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    hipStream_t st = G.last_enc_st ? G.last_enc_st : G.st;
+    HIPCHK(hipMemsetAsync(G.d_enc_err, 0, 4, st));
+    G.enc_outstanding = 0;
     return DC_OK;
 }
 
@@ -597,6 +625,7 @@ static int dec3_ensure(long long max_chunks, int B, int ct) {
     if (max_chunks > G.dec3_cap) {
         if (G.dec3_pool) HIPCHK(hipFree(G.dec3_pool));
         G.dec3_pool = NULL;
+        G.sh3_ok = 0;                         /* a pending shard fix would read the freed spend/rec */
         const long long C = max_chunks + 4096;
         const long long DJ = C / 64 + 64, PJ = C / (64 * 4) + 64;
         size_t sz[6], off = 0, tot = 0;
@@ -671,8 +700,15 @@ long long dc_set_decode3_min_bytes(long long v) {
 #define DEC_ROUNDS 3
 #define DEC_FIX_ITERS 3
 
+/* halo: a Himeno halo plane (dc_halo_decode_device): the small-stream decoder up to its chunk limit */
+static int decode_device_h(int ct, const void* d_stream, long long nbytes, const unsigned long long* d_nbits,
+                           long long max_bytes, long long num, int type, uint32_t mask17, void* d_out, int halo);
 int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsigned long long* d_nbits,
                      long long max_bytes, long long num, int type, uint32_t mask17, void* d_out) {
+    return decode_device_h(ct, d_stream, nbytes, d_nbits, max_bytes, num, type, mask17, d_out, 0);
+}
+static int decode_device_h(int ct, const void* d_stream, long long nbytes, const unsigned long long* d_nbits,
+                           long long max_bytes, long long num, int type, uint32_t mask17, void* d_out, int halo) {
     int rc = ensure_init();
     if (rc) return rc;
     if (!valid_ct(ct)) return seterr(DC_ERR_ARG, "unsupported CT %d", ct);
@@ -694,11 +730,12 @@ int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsig
     /* the segment decoder reads whole 16-byte groups through a buffer resource (32-bit byte range): every
        stream byte must lie in one inside max_bytes, and max_bytes and the output below 2 GiB */
     const long long need16 = nbytes >= 0 ? (nbytes + 15) / 16 * 16 : 0;
-    const int halo = G.dec3_skip_once;
-    G.dec3_skip_once = 0;
     const long long mc256 = (max_bytes * 8 + 255) / 256 + 1;
-    G.runs_used = !G.D.shard && num >= 1 && mc256 <= dc_decode_runs_max_chunks() + 8 && m3 != 0 &&
-                  (halo || max_bytes <= runs_max_bytes());
+    /* -1 in either knob (DC_DEC3=0 / dc_set_decode3_min_bytes(-1), dc_set_runs_max_bytes(-1)) keeps every
+       stream, halo planes included, off the small-stream decoder; 0 forces the segment decoder */
+    const long long rmax = runs_max_bytes();
+    G.runs_used = !G.D.shard && num >= 1 && mc256 <= dc_decode_runs_max_chunks() + 8 && m3 > 0 && rmax >= 0 &&
+                  (halo || max_bytes <= rmax);
     G.dec3_used = !halo && !G.runs_used && m3 >= 0 && max_bytes >= m3 && max_bytes >= 16 && max_bytes >= need16 && max_bytes < (1ll << 31) && num < (1ll << 29) && !G.D.shard &&
                   !((uintptr_t)d_stream & 15u) && !((uintptr_t)d_out & 15u);
     G.dec3_launched = G.dec3_used;
@@ -714,8 +751,13 @@ int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsig
         if ((rc = dec3_ensure((max_bytes * 8 + 255) / 256 + 1, P.B, ct))) return rc;
         G.D3.err = G.D.err;
         G.D3.capw = max_bytes / 16 * 4;
+        /* a decode job holds 64 chunks (16384 bits): streams of fewer than ~16 bits per value overflow the
+           1040-value job buffer, so a stream known to be that dense (its length given, or the last stream of
+           these parameters was) takes the 2080-value instantiation */
+        G.dec3_dense = (nbytes >= 0 && nbytes * 8 < 18 * num && (ct == 6 || nbytes * 8 >= 6 * num)) ||
+                       G.dense_key == ct * 256 + P.B + 1;                /* (not runs mode: < 6 bits per value) */
         if (dc_launch_decode3((const uint8_t*)d_stream, G.dec_dnbits, G.dec_hnbits, &P, &G.D3, (float*)d_out, num,
-                              G.dec_epoch, G.st))
+                              G.dec_epoch, G.dec3_dense, G.st))
             return seterr(DC_ERR_HIP, "decode launch failed: %s", hipGetErrorString(hipGetLastError()));
     } else if (DV(dc_launch_decode_fast)((const uint8_t*)d_stream, G.dec_dnbits, G.dec_hnbits, max_chunks, &P, &G.D,
                                          (float*)d_out, num, G.dec_epoch, G.st))
@@ -738,7 +780,7 @@ int dc_decode_device(int ct, const void* d_stream, long long nbytes, const unsig
    three values are here; a stream the segment decoder declines sets the status word (dc_decode_status),
    and the caller decodes the shard again on the chunk-map path (dc_decode_shard_device). */
 int dc_decode_shard3_device(int ct, const void* d_stream, const unsigned long long* d_nbits, long long max_bytes,
-                            long long num, int type, uint32_t mask17, void* d_out) {
+                            long long num, int type, uint32_t mask17, void* d_out, int has_history) {
     int rc = ensure_init();
     if (rc) return rc;
     if (!valid_ct(ct)) return seterr(DC_ERR_ARG, "unsupported CT %d", ct);
@@ -754,9 +796,9 @@ int dc_decode_shard3_device(int ct, const void* d_stream, const unsigned long lo
     if ((rc = dec3_ensure((max_bytes * 8 + 255) / 256 + 1, P.B, ct))) return rc;
     G.D3.err = G.D.err;
     G.D3.capw = max_bytes / 16 * 4;
-    G.D3.shard = 1;
+    G.D3.shard = has_history ? 1 : 2;            /* 2: the first shard, no values before it */
     const int lrc = dc_launch_decode3((const uint8_t*)d_stream, d_nbits, 0ull, &P, &G.D3, (float*)d_out, num,
-                                      G.dec_epoch, G.st);
+                                      G.dec_epoch, 0, G.st);
     G.D3.shard = 0;
     if (lrc) return seterr(DC_ERR_HIP, "shard decode launch failed: %s", hipGetErrorString(hipGetLastError()));
     G.sh3_s = (const uint8_t*)d_stream;
@@ -830,6 +872,7 @@ int dc_decode_status(unsigned* status_out) {
 int dc_decode_status_clear(void) {
     int rc = ensure_init();
     if (rc) return rc;
+    if (!G.D.err) return DC_OK;                  /* (no decode yet) */
     HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
     G.dec_pending = 0;
     G.dec_queued = 0;
@@ -862,6 +905,21 @@ static int decode_finish_body(void) {
         HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
         return seterr(DC_ERR_STREAM, "decoder status 0x%x over %d queued decodes: an earlier decode left the fast "
                                      "path and was not completed (call dc_decode_finish after each decode)", err, queued);
+    }
+    if ((err & 512u) && (err & 8192u) && !(err & (1024u | 2048u | 4096u | 16384u | 65536u)) && G.dec_pending &&
+        G.dec3_used && !G.runs_used && !G.dec3_dense && !G.dec_shard) {
+        /* only a job denser than the 1040-value buffer declined: decode again with the dense instantiation
+           (2080 values per job), and start later decodes of these parameters with it */
+        if (getenv("DC_DEBUG_ERR")) fprintf(stderr, "[dcamd] dense stream (status 0x%x): dense segment decoder\n", err);
+        HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
+        if ((rc = dec_next_epoch())) return rc;
+        G.dense_key = G.dec_P.ct * 256 + G.dec_P.B + 1;
+        G.dec3_dense = 1;
+        if (dc_launch_decode3(G.dec_s, G.dec_dnbits, G.dec_hnbits, &G.dec_P, &G.D3, G.dec_out, G.dec_num, G.dec_epoch, 1,
+                              G.st))
+            return seterr(DC_ERR_HIP, "decode launch failed");
+        rc = read_dec_err(&err);
+        if (rc) return rc;
     }
     G.dec3_last = G.dec3_used && !G.runs_used && !(err & 512u);
     G.runs_last = G.dec3_used && G.runs_used && !(err & 512u);
@@ -1058,8 +1116,7 @@ int dc_halo_decode_device(int ct, const void* d_stream, long long nbytes, const 
     const long long cap = nbytes >= 0 ? nbytes : (long long)dc_stream_capacity(n);
     /* a plane is a runs-mode stream (copy runs), which the segment decoder declines: straight to the
        chunk-map decoder */
-    G.dec3_skip_once = 1;
-    if ((rc = dc_decode_device(ct, d_stream, nbytes, d_bits, cap, n, type, mask17, G.halo_a))) return rc;
+    if ((rc = decode_device_h(ct, d_stream, nbytes, d_bits, cap, n, type, mask17, G.halo_a, 1))) return rc;
     /* async (dc_set_halo_async): no host read here -- the caller reads dc_decode_status() after its steps
        and decodes a plane again synchronously if it is not 0 */
     if (!G.halo_async && (rc = dc_decode_finish())) return rc;
@@ -1205,6 +1262,49 @@ int dc_crc32_device(const void* d_s, long long nbytes, uint32_t* crc_out) {
         HIPCHK(hipStreamSynchronize(G.st));
         *crc_out = h;
     }
+    return DC_OK;
+}
+
+int dc_hash_device(const void* d_buf, long long nbytes, unsigned long long* hash_out) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (nbytes < 0 || ((uintptr_t)d_buf & 3u)) return seterr(DC_ERR_ARG, "hash: nbytes < 0 or buffer not 4-byte aligned");
+    if (dc_launch_hash_words(d_buf, nbytes, (unsigned long long*)G.d_crc + 1, G.st))
+        return seterr(DC_ERR_HIP, "hash launch failed");
+    unsigned long long h = 0;
+    HIPCHK(hipMemcpyAsync(&h, (unsigned long long*)G.d_crc + 1, 8, hipMemcpyDeviceToHost, G.st));
+    HIPCHK(hipStreamSynchronize(G.st));
+    if (hash_out) *hash_out = h;
+    return DC_OK;
+}
+
+int dc_copy_rate_device(const void* d_src, void* d_dst, long long bytes, int reps, double* gbs_out, int* variant_out) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (bytes < 16 || (bytes & 15) || bytes > 0x7FFFFF00ll || reps < 1 || (((uintptr_t)d_src | (uintptr_t)d_dst) & 15u))
+        return seterr(DC_ERR_ARG, "copy rate: 16-byte aligned buffers, bytes a multiple of 16 below 2 GiB");
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    double best = 0.0;
+    int bv = 0;
+    for (int v = 0; v < 4; v++) {
+        for (int w = 0; w < 2; w++)                  /* warm-up */
+            if (dc_launch_stream_copy(d_src, d_dst, bytes, v, G.st)) return seterr(DC_ERR_HIP, "copy launch failed");
+        HIPCHK(hipEventRecord(e0, G.st));
+        for (int r = 0; r < reps; r++)
+            if (dc_launch_stream_copy(d_src, d_dst, bytes, v, G.st)) return seterr(DC_ERR_HIP, "copy launch failed");
+        HIPCHK(hipEventRecord(e1, G.st));
+        HIPCHK(hipEventSynchronize(e1));
+        float ms = 0.0f;
+        HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+        const double gbs = ms > 0.0f ? 2.0 * (double)bytes * reps / (ms * 1e-3) / 1e9 : 0.0;
+        if (gbs > best) { best = gbs; bv = v; }
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (gbs_out) *gbs_out = best;
+    if (variant_out) *variant_out = bv;
     return DC_OK;
 }
 
@@ -1614,13 +1714,13 @@ int dc_ct1_encode_device(const void* d_x, long long n, void* d_raw, void* d_code
     if (n == 0) { if (nraw_out) *nraw_out = 0; return DC_OK; }
     uint32_t* traw; unsigned long long* rawoff; uint8_t* carr;
     if ((rc = c1_scratch(n, &traw, &rawoff, &carr))) return rc;
-    HIPCHK(hipMemsetAsync(G.d_enc_err, 0, 4, G.st));
+    HIPCHK(hipMemsetAsync(G.d_enc_err + 12, 0, 4, G.st));
     if (dc_launch_ct1_encode((const float*)d_x, n, thr_le(absErrBound), traw, rawoff, (float*)d_raw, (char*)d_codes,
-                             (int*)d_pos1, G.d_enc_err, G.st))
+                             (int*)d_pos1, G.d_enc_err + 12, G.st))
         return seterr(DC_ERR_HIP, "ct1 encode launch failed");
     const long long nt = dc_ct1_tiles(n);
     HIPCHK(hipMemcpyAsync(&G.h_scratch[0], rawoff + nt, 8, hipMemcpyDeviceToHost, G.st));
-    HIPCHK(hipMemcpyAsync(&G.h_scratch[1], G.d_enc_err, 4, hipMemcpyDeviceToHost, G.st));
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[1], G.d_enc_err + 12, 4, hipMemcpyDeviceToHost, G.st));
     HIPCHK(hipStreamSynchronize(G.st));
     if (G.h_scratch[1] & 1u) return seterr(DC_ERR_INPUT, "input contains -1.0f (the reference's history sentinel)");
     if (nraw_out) *nraw_out = (long long)G.h_scratch[0];
@@ -1634,11 +1734,11 @@ int dc_ct1_decode_device(const void* d_raw, long long nraw, const void* d_codes,
     if (num <= 0) return DC_OK;
     uint32_t* traw; unsigned long long* rawoff; uint8_t* carr;
     if ((rc = c1_scratch(num, &traw, &rawoff, &carr))) return rc;
-    HIPCHK(hipMemsetAsync(G.d_enc_err, 0, 4, G.st));
+    HIPCHK(hipMemsetAsync(G.d_enc_err + 12, 0, 4, G.st));
     if (dc_launch_ct1_decode((const float*)d_raw, nraw, (const char*)d_codes, (const int*)d_pos1, ncodes, num, carr, traw,
-                             rawoff, (float*)d_out, G.d_enc_err, G.st))
+                             rawoff, (float*)d_out, G.d_enc_err + 12, G.st))
         return seterr(DC_ERR_HIP, "ct1 decode launch failed");
-    HIPCHK(hipMemcpyAsync(&G.h_scratch[1], G.d_enc_err, 4, hipMemcpyDeviceToHost, G.st));
+    HIPCHK(hipMemcpyAsync(&G.h_scratch[1], G.d_enc_err + 12, 4, hipMemcpyDeviceToHost, G.st));
     HIPCHK(hipStreamSynchronize(G.st));
     if (G.h_scratch[1] & 4u) return seterr(DC_ERR_STREAM, "ct1 codes out of range or raw array too short");
     return DC_OK;

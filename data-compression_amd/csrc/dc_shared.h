@@ -86,7 +86,9 @@ typedef struct Dec3Bufs {
     int shard;                     /* 1: the stream is a shard of a longer one (dc_decode_shard3_device):
                                       predictions among its first tokens read the three values before
                                       it, which come later -- decoded as pending, fixed by
-                                      dc_decode_shard3_fix */
+                                      dc_decode_shard3_fix; 2: the first such shard (no values before it:
+                                      a prediction among its first three tokens declines, as for a
+                                      whole stream) */
     uint32_t* spend;               /* [0] tokens of the shard's first chunk that wait for those values */
 } Dec3Bufs;
 
@@ -126,9 +128,10 @@ int dc_launch_decode_fast(const uint8_t* s, const unsigned long long* dev_nbits,
                           long long num, uint32_t epoch, dc_hip_stream st);
 int dc_launch_decode_serial(const uint8_t* s, const DC_NS Params* P, const DC_NS DecBufs* D, float* out,
                             long long num, dc_hip_stream st);
+/* dense = 1: the decode3 instantiation with a 2080-value job buffer (streams of < ~16 bits per value) */
 int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
                       const DC_NS Params* P, const DC_NS Dec3Bufs* D3, float* out, long long num, uint32_t epoch,
-                      dc_hip_stream st);
+                      int dense, dc_hip_stream st);
 int dc_launch_merge_shards(const uint8_t* g, long long P, int world, const unsigned long long* counts, uint8_t* out,
                            long long out_bytes, unsigned long long* total_out, unsigned* err, long long max_bytes,
                            dc_hip_stream st);
@@ -210,6 +213,8 @@ int dc_launch_shard_fix_s(const uint8_t* s, const DC_NS Params* P, const DC_NS D
 int dc_launch_plane_gather(const float* p, int mj, int mk, int ijk, int v, int A, int B, float* out, dc_hip_stream st);
 int dc_launch_plane_scatter(const float* x, const float* d_min, float* p, int mj, int mk, int ijk, int v, int A, int B,
                             dc_hip_stream st);
+int dc_launch_hash_words(const void* p, long long nbytes, unsigned long long* d_out, hipStream_t st);
+int dc_launch_stream_copy(const void* src, void* dst, long long bytes, int variant, hipStream_t st);
 int dc_launch_flip_bits(uint8_t* s, unsigned long long nbits, long long count, unsigned long long seed,
                         dc_hip_stream st);
 int dc_launch_crc_resend(const uint32_t* crc, const uint8_t* src, uint8_t* dst, long long nbytes, int copy,

@@ -39,13 +39,13 @@ EXT_SYMBOLS = [
     "dc_get_abs_error_bound", "dc_stream_capacity", "dc_encode_device", "dc_encode_result",
     "dc_decode_device", "dc_decode_finish", "dc_to_small_device", "dc_med_device", "dc_crc32_device",
     "dc_decode_chunk_bits_value", "dc_ct1_encode_device", "dc_ct1_decode_device", "dc_encode_bits_device",
-    "dc_crc32_device_async", "dc_flip_bits_device", "dc_decode_shard_device", "dc_decode_shard_fix",
+    "dc_crc32_device_async", "dc_hash_device", "dc_copy_rate_device", "dc_flip_bits_device", "dc_decode_shard_device", "dc_decode_shard_fix",
     "dc_halo_encode_device", "dc_halo_decode_device",
     "dc64_stream_capacity", "dc64_encode_device", "dc64_encode_result", "dc64_decode_device", "dc64_decode_finish",
     "dc64_last_decode_flags", "dc64_to_small_device", "dc64_med_device", "dc_set_encode_stream",
     "dc_decode_status", "dc_abi_status", "dc_med_sum_device", "dc_type_from_max", "dc_set_small_chunk_max_bytes",
     "dc_set_decode3_min_bytes", "dc_set_decode3_seg", "dc_last_decode_was_v3", "dc_last_decode_launched_v3",
-    "dc_encode_status", "dc_encode_mode", "dc_encode_retries", "dc_crc_resend_device",
+    "dc_encode_status", "dc_encode_clear_status", "dc_encode_mode", "dc_encode_retries", "dc_crc_resend_device",
     "dc_merge_shards_device", "dc_merge_status", "dc_decode_shard3_device", "dc_decode_shard3_fix",
     "dc_decode_status_clear", "dc_set_runs_max_bytes", "dc_last_decode_was_runs",
     "dc_last_decode_launched_runs", "dc_set_halo_async", "dc_med_shard_stats", "dc_med_shard_trans",
@@ -86,7 +86,7 @@ class Lib:
         L.dc_decode_shard_fix.argtypes = [vp]
         L.dc_merge_shards_device.argtypes = [vp, ll, C.c_int, vp, vp, ll, vp]
         L.dc_merge_status.argtypes = [C.POINTER(C.c_uint), C.c_int]
-        L.dc_decode_shard3_device.argtypes = [C.c_int, vp, vp, ll, ll, C.c_int, u32, vp]
+        L.dc_decode_shard3_device.argtypes = [C.c_int, vp, vp, ll, ll, C.c_int, u32, vp, C.c_int]
         L.dc_decode_shard3_fix.argtypes = [vp]
         L.dc_to_small_device.argtypes = [vp, ll, vp, C.POINTER(C.c_float)]
         L.dc_med_device.argtypes = [vp, ll, C.POINTER(C.c_float), C.POINTER(C.c_int)]
@@ -97,6 +97,8 @@ class Lib:
         L.dc_type_from_max.argtypes = [C.c_float]
         L.dc_decode_status.argtypes = [C.POINTER(C.c_uint)]
         L.dc_crc32_device.argtypes = [vp, ll, C.POINTER(C.c_uint32)]
+        L.dc_hash_device.argtypes = [vp, ll, C.POINTER(C.c_ulonglong)]
+        L.dc_copy_rate_device.argtypes = [vp, vp, ll, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int)]
         L.dc_decode_chunk_bits_value.restype = ll
         L.dc_set_small_chunk_max_bytes.argtypes = [ll]
         L.dc_set_small_chunk_max_bytes.restype = ll
@@ -424,9 +426,10 @@ class Lib:
         self.check(self.L.dc_merge_status(C.byref(v), 1 if reset else 0), "dc_merge_status")
         return v.value
 
-    def decode_shard3_device(self, ct, s_ptr, nbits_ptr, max_bytes, num, out_ptr, type_=0, mask17=0):
+    def decode_shard3_device(self, ct, s_ptr, nbits_ptr, max_bytes, num, out_ptr, type_=0, mask17=0, has_history=1):
         """A shard encoded at start bit 0 through the segment decoder, its first predictions pending."""
-        self.check(self.L.dc_decode_shard3_device(ct, s_ptr, nbits_ptr, max_bytes, num, type_, mask17, out_ptr),
+        self.check(self.L.dc_decode_shard3_device(ct, s_ptr, nbits_ptr, max_bytes, num, type_, mask17, out_ptr,
+                                                  1 if has_history else 0),
                    "dc_decode_shard3_device")
 
     def decode_shard3_fix(self, hin_ptr):
@@ -512,6 +515,18 @@ class Lib:
         m, t = C.c_float(0), C.c_int(0)
         self.check(self.L.dc_med_device(x_ptr, n, C.byref(m), C.byref(t)), "dc_med_device")
         return np.float32(m.value), t.value
+
+    def hash_device(self, ptr, nbytes):
+        """dc_hash_device: sum of splitmix64(i << 32 | w_i) over the range's 32-bit words (hash_words below)."""
+        v = C.c_ulonglong(0)
+        self.check(self.L.dc_hash_device(ptr, nbytes, C.byref(v)), "dc_hash_device")
+        return int(v.value)
+
+    def copy_rate(self, src_ptr, dst_ptr, nbytes, reps=10):
+        """dc_copy_rate_device: (GB/s read + written, variant) of the best hand-written streaming copy."""
+        g, v = C.c_double(0), C.c_int(0)
+        self.check(self.L.dc_copy_rate_device(src_ptr, dst_ptr, nbytes, reps, C.byref(g), C.byref(v)), "dc_copy_rate_device")
+        return float(g.value), int(v.value)
 
     def crc32_device(self, s_ptr, nbytes):
         v = C.c_uint32(0)
@@ -862,7 +877,8 @@ def decode_sharded_device(L, ct, local, d_count, max_bytes, num, out, type_=0, m
     import torch
     rank = dist.get_rank(group)
     dev = out.device
-    L.decode_shard3_device(ct, local.data_ptr(), d_count.data_ptr(), max_bytes, num, out.data_ptr(), type_, mask17)
+    L.decode_shard3_device(ct, local.data_ptr(), d_count.data_ptr(), max_bytes, num, out.data_ptr(), type_, mask17,
+                           has_history=rank > 0)
     cur, ls = torch.cuda.current_stream(dev), _lib_stream(L, dev)
     _after(ls, cur)
     hin = exchange_history(out[num - 3:num].flip(0).contiguous(), group)
@@ -872,6 +888,31 @@ def decode_sharded_device(L, ct, local, d_count, max_bytes, num, out, type_=0, m
         L.decode_shard3_fix(hin.data_ptr())
         hin.record_stream(ls)
     return out
+
+
+def hash_words(buf, nbytes=None):
+    """Host twin of dc_hash_device: sum over the 32-bit little-endian words w_i of the first nbytes bytes
+    (zero-padded) of splitmix64(i << 32 | w_i) mod 2^64."""
+    b = np.frombuffer(memoryview(buf).cast("B"), np.uint8) if not isinstance(buf, np.ndarray) else buf.view(np.uint8).reshape(-1)
+    nbytes = b.size if nbytes is None else int(nbytes)
+    b = b[:nbytes]
+    nw = (nbytes + 3) // 4
+    h = np.uint64(0)
+    blk = 1 << 24
+    with np.errstate(over="ignore"):
+        for w0 in range(0, nw, blk):
+            w1 = min(nw, w0 + blk)
+            chunk = b[4 * w0:4 * w1]
+            if chunk.size < 4 * (w1 - w0):
+                chunk = np.concatenate([chunk, np.zeros(4 * (w1 - w0) - chunk.size, np.uint8)])
+            w = chunk.view("<u4").astype(np.uint64)
+            z = (np.arange(w0, w1, dtype=np.uint64) << np.uint64(32)) | w
+            z = z + np.uint64(0x9E3779B97F4A7C15)
+            z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+            z = z ^ (z >> np.uint64(31))
+            h = h + np.sum(z, dtype=np.uint64)
+    return int(h)
 
 
 def gen_u10(n, seed=42, offset=0):

@@ -57,8 +57,11 @@ int dc_encode_bits_device(int ct, const void* d_x, long long n, long long idx0, 
 /* Wait for the last encode and return start_bit + bits written (host value). */
 int dc_encode_result(unsigned long long* total_bits);
 /* the encoder's error word, read as is (bit 0: a -1.0f input; 2: an offset outside the stream; 4: a
-   single-pass look-back timed out -- dc_encode_result then re-encodes wait-free); synchronous */
+   single-pass look-back timed out -- dc_encode_result then re-encodes wait-free when that encode is the
+   only one issued since the word was last checked, and reports an error otherwise); synchronous */
 int dc_encode_status(unsigned* status_out);
+/* clear that word (after dc_encode_result reported a timeout among several outstanding encodes) */
+int dc_encode_clear_status(void);
 /* encoder variant of the last encode: 1 single pass, 2 count + pack, 3 count + scan + pack */
 int dc_encode_mode(void);
 /* encodes re-run wait-free after a look-back timeout (process lifetime) */
@@ -102,12 +105,14 @@ int dc_decode_shard_fix(const float* d_hin);
  * dc_decode_shard3_device: decode one such shard (its own encoded buffer, bit count on the device) with
  *   the segment decoder; predictions among its first tokens wait for the previous shard's last three
  *   values: dc_decode_shard3_fix(d_hin) decodes them once they are on the device (b1 = x[-1], b2, b3).
+ *   has_history 0 marks the first shard (nothing before it): a prediction among its first three tokens
+ *   then declines it, as for a whole stream.
  *   A shard the segment decoder declines sets dc_decode_status (decode it with dc_decode_shard_device). */
 int dc_merge_shards_device(const void* d_gathered, long long slot_bytes, int world, const unsigned long long* d_counts,
                            void* d_out, long long out_bytes, unsigned long long* d_total);
 int dc_merge_status(unsigned* status_out, int reset);
 int dc_decode_shard3_device(int ct, const void* d_stream, const unsigned long long* d_nbits, long long max_bytes,
-                            long long num, int type, uint32_t mask17, void* d_out);
+                            long long num, int type, uint32_t mask17, void* d_out, int has_history);
 int dc_decode_shard3_fix(const float* d_hin);
 int dc_decode_status_clear(void);           /* clear the decoder status word (after a declined shard) */
 
@@ -148,6 +153,16 @@ int dc_type_from_max(float mx);
 int dc_crc32_device(const void* d_s, long long nbytes, uint32_t* crc_out);
 /* The same, asynchronous on the library stream, result to device memory d_crc (one uint32). */
 int dc_crc32_device_async(const void* d_s, long long nbytes, uint32_t* d_crc);
+/* A 64-bit hash of a device byte range: the sum over its 32-bit little-endian words w_i (bytes past nbytes
+ * zero) of splitmix64(i << 32 | w_i) mod 2^64 (bench.py's self-check against hashes of the oracle's
+ * output, tests/golden/make_bench_hashes.py).  Synchronous. */
+int dc_hash_device(const void* d_buf, long long nbytes, unsigned long long* hash_out);
+/* The achievable HBM rate of this GPU: a hand-written streaming copy (16-byte buffer loads and stores,
+ * 4 or 8 in flight per lane, default or nontemporal policy: 4 variants) of `bytes` (a multiple of 16,
+ * < 2 GiB) from d_src to d_dst, `reps` launches per variant timed with HIP events on the library stream;
+ * *gbs_out = the best variant's (read + written bytes) / average launch time, in GB/s; *variant_out its
+ * index.  Synchronous. */
+int dc_copy_rate_device(const void* d_src, void* d_dst, long long bytes, int reps, double* gbs_out, int* variant_out);
 /* BER fault injection (CT8/CT9 flow): flip `count` bits of the stream at positions
  * splitmix64(seed + i) mod nbits (MSB-first in each byte, as bit_flip).  The stream buffer must be
  * 4-byte aligned and padded to whole words.  Asynchronous. */

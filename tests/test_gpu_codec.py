@@ -471,3 +471,57 @@ def _halo_plane_case(dc, oracle, ct, size, ijk, v, noise):
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
 
 
+
+
+@pytest.mark.parametrize("bound", BOUNDS)
+@pytest.mark.parametrize("ct", CTS)
+def test_decoder_golden_chunk_map_forced(dc, oracle, bound, ct):
+    """The chunk-map decoder is the fallback of every decline: with both knobs at -1 (segment decoder off,
+    small-stream decoder off) every golden stream goes straight to it and must still equal the grammar
+    decoder (-1 is honoured by both knobs, halo planes included)."""
+    g = golden(bound)
+    dc.set_bound(bound)
+    m3 = dc.L.dc_set_decode3_min_bytes(-1)
+    rm = dc.L.dc_set_runs_max_bytes(-1)
+    try:
+        for case in CASES:
+            s = g[f"{case}/ct{ct}/stream"]
+            n = g[f"{case}/input"].size
+            t, m17 = _prep(g, case)
+            out = dc.decompress(ct, s, n, t, m17)
+            assert not dc.L.dc_last_decode_launched_v3() and not dc.L.dc_last_decode_launched_runs()
+            spec, _ = oracle.decompress(ct, s, n, bound, t, m17)
+            assert np.array_equal(out.view(np.uint32), spec.view(np.uint32)), case
+    finally:
+        dc.L.dc_set_decode3_min_bytes(m3)
+        dc.L.dc_set_runs_max_bytes(rm)
+
+
+@pytest.mark.parametrize("nbytes", [0, 1, 3, 4, 5, 4096, 65537, (1 << 22) + 7])
+def test_hash_device_matches_host(dc, nbytes):
+    """dc_hash_device (bench.py's self-check) equals its host twin dcamd.hash_words on ragged lengths: bytes
+    past nbytes do not count."""
+    import torch
+    import dcamd
+    rng = np.random.RandomState(nbytes & 0xFFFF)
+    h = rng.randint(0, 256, size=nbytes + 9, dtype=np.uint8)
+    d = torch.from_numpy(h).cuda()
+    torch.cuda.synchronize()
+    assert dc.hash_device(d.data_ptr(), nbytes) == dcamd.hash_words(h, nbytes)
+    if nbytes:
+        h2 = h.copy()
+        h2[nbytes - 1] ^= 1
+        assert dcamd.hash_words(h2, nbytes) != dcamd.hash_words(h, nbytes)
+
+
+def test_copy_rate_device(dc):
+    """dc_copy_rate_device (bench.py's achievable ceiling): every variant copies the buffer exactly and the
+    best rate is a plausible HBM rate."""
+    import torch
+    n = 1 << 24
+    a = torch.arange(n, dtype=torch.int32, device="cuda")
+    b = torch.zeros_like(a)
+    torch.cuda.synchronize()
+    gbs, v = dc.copy_rate(a.data_ptr(), b.data_ptr(), 4 * n, 3)
+    assert torch.equal(a, b)
+    assert 0 <= v < 4 and 500.0 < gbs < 8000.0

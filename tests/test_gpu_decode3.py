@@ -201,3 +201,41 @@ def test_default_segment_length_mid_sizes(v3, oracle, ct, lg, bound):
     v3.decode_finish()
     assert v3.last_decode_was_v3(), "the stream left the segment decoder"
     assert np.array_equal(out.cpu().numpy().view(np.uint32), spec.view(np.uint32))
+
+
+@pytest.mark.parametrize("ct", [5, 7])
+@pytest.mark.parametrize("lg", [20, 24])
+def test_decode3_dense_streams(v3, oracle, ct, lg):
+    """Dense streams (CT7 at a bound of 1e-2: fewer than ~16 bits per value, more values per 64-chunk decode
+    job than the 1040-value buffer) stay on the segment decoder: the dense instantiation (2080 values per
+    job) takes them -- from the device path (bit count on the device: first decode declines DENSE and is
+    redone dense inside dc_decode_finish, later ones start dense) and from the host ABI (length known)."""
+    import torch
+    v3.set_bound(1e-2)
+    try:
+        n = 1 << lg
+        _, xs = oracle.to_small(oracle.gen_u10(n))
+        t, m17 = oracle.type_mask(xs)
+        s, nb, _ = oracle.compress(ct, xs, 1e-2, t, m17)
+        ref, _ = oracle.decompress(ct, s, n, 1e-2, t, m17)
+        out = v3.decompress(ct, s, n, t, m17)                     # host ABI: nbytes known
+        assert np.array_equal(out.view(np.uint32), ref.view(np.uint32))
+        assert v3.L.dc_last_decode_was_v3()
+        dx = torch.from_numpy(xs).cuda()
+        cap = v3.stream_capacity(n)
+        st = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+        d_nbits = torch.zeros(1, dtype=torch.int64, device="cuda")
+        o = torch.empty(n, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        for _ in range(2):                                        # device path, twice (the hint sticks)
+            o.fill_(-7.0)
+            torch.cuda.synchronize()
+            v3.encode_device(ct, dx.data_ptr(), n, st.data_ptr(), type_=t, mask17=m17, total_ptr=d_nbits.data_ptr())
+            v3.decode_device(ct, st.data_ptr(), -1, n, o.data_ptr(), type_=t, mask17=m17, d_nbits=d_nbits.data_ptr(),
+                             max_bytes=cap)
+            v3.decode_finish()
+            assert v3.L.dc_last_decode_was_v3()
+            assert np.array_equal(o.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+        assert nb * 8 < 18 * n                                    # (the case is dense)
+    finally:
+        v3.set_bound(1e-3)

@@ -235,3 +235,45 @@ def test_global_med_exscan_device(kind, world, n):
     assert all(r[1] is True for r in res), res
     if kind == "u10" and world == 4:
         assert sum(r[2] for r in res) < world, res
+
+
+@pytest.mark.parametrize("ct", [5, 7, 11])
+def test_shard3_first_shard_declines_early_prediction(dc, oracle, ct):
+    """dc_decode_shard3_device(has_history=0) is the first shard: a prediction among its first three tokens
+    (possible only in a stream that is not a real start, e.g. a damaged one) declines it as it declines a
+    whole stream, instead of decoding from zero history.  With has_history=1 the same shard
+    decodes its pending prefix once the previous values arrive and equals the oracle's slice."""
+    dc.set_bound(1e-3)
+    n = 1 << 16
+    x = oracle.gen_u10(2 * n)
+    x[n - 40:n + 40] = x[n - 41]                  # a copy run across the cut: the shard starts with '101' codes
+    _, xs = oracle.to_small(x)
+    t, m17 = oracle.type_mask(xs)
+    buf = torch.zeros(n + 4, dtype=torch.float32, device="cuda")
+    buf[1:4] = torch.from_numpy(xs[n - 3:n].copy())
+    buf[4:] = torch.from_numpy(xs[n:].copy())
+    cap = dc.stream_capacity(n)
+    local = torch.zeros(cap + 64, dtype=torch.uint8, device="cuda")
+    d_count = torch.zeros(1, dtype=torch.int64, device="cuda")
+    out = torch.empty(n, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    dc.encode_device(ct, buf[4:].data_ptr(), n, local.data_ptr(), idx0=n, type_=t, mask17=m17, start_bit=0,
+                     total_ptr=d_count.data_ptr())
+    dc.encode_result()
+    mb = (cap + 64) // 16 * 16
+    dc.decode_status_clear()
+    dc.decode_shard3_device(ct, local.data_ptr(), d_count.data_ptr(), mb, n, out.data_ptr(), t, m17, has_history=0)
+    dc.synchronize()
+    st = dc.decode_status()
+    assert st & 512 and st & 16384, hex(st)
+    dc.decode_status_clear()
+    dc.decode_shard3_device(ct, local.data_ptr(), d_count.data_ptr(), mb, n, out.data_ptr(), t, m17, has_history=1)
+    s_all, _, _ = oracle.compress(ct, xs, 1e-3, t, m17)
+    dec_all, _ = oracle.decompress(ct, s_all, 2 * n, 1e-3, t, m17)
+    hin = torch.from_numpy(dec_all[n - 3:n][::-1].copy()).cuda()
+    torch.cuda.synchronize()
+    dc.decode_shard3_fix(hin.data_ptr())
+    dc.synchronize()
+    assert dc.decode_status() == 0
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), dec_all[n:].view(np.uint32))
+    dc.decode_status_clear()
