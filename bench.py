@@ -518,9 +518,12 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
 
     # CT9 flow (--ber): sender CRC, channel copy with floor(bits*BER) flipped bits, receiver CRC check, resend
     # of the clean stream on a mismatch, CRC check of the resent copy, decode of the received copy.  The
-    # checks and the resend run on the device (dc_crc_resend_device: no host round trip inside the step);
-    # the host reads each step's counters (resends, mismatches left) asynchronously as the protocol's ack
-    # and checks them after the loop.  The stream length is the warm-up's (same input every step).
+    # sender's CRC comes out of the encoder (dc_encode_crc_device: its tiles CRC the words they store), the
+    # receiver's check of the resent copy out of the resend copy itself (dc_crc_resend_crc_device): one CRC
+    # pass per step, the receiver's check of the damaged copy.  Checks and resend run on the device (no host
+    # round trip inside the step); the host reads each step's counters (resends, mismatches left)
+    # asynchronously as the protocol's ack and checks them after the loop.  The stream length is the
+    # warm-up's (same input every step).
     resends = [0]
     ct9 = {}
     if ber > 0:
@@ -531,8 +534,9 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
         seed = [1]
         acks = []
         ack_buf = torch.zeros((max(steps, warmup) + 1, 2), dtype=torch.int32, pin_memory=True)
-        CT9_PHASES = ["crc32 (sender)", "channel copy", "flip_bits_kernel", "crc32 (receiver)",
-                      "crc_resend_kernel (compare + resend copy)", "crc32 (resent copy)", "crc_resend_kernel (check)"]
+        CT9_PHASES = ["crcf_final_kernel (sender CRC: combine of the encoder's block CRCs)", "channel copy",
+                      "flip_bits_kernel", "crcf_blocks + crcf_final (receiver CRC, damaged copy)",
+                      "crcf_blocks + crcf_final (resend copy with its CRC + check)"]
 
         def step(ev=None, ph=None):                          # noqa: F811 -- the CT9 variant of the step
             def mark(i):
@@ -540,25 +544,19 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
                     ph[i].record(ext)
             if ev:
                 ev[0].record(ext)
-            L.encode_device(ct, xs.data_ptr(), n, stream.data_ptr(), idx0=idx0, type_=typ, mask17=mask17,
-                            total_ptr=d_nbits.data_ptr())
+            L.encode_crc_device(ct, xs.data_ptr(), n, stream.data_ptr(), d_nbits.data_ptr(), d_crc.data_ptr(),
+                                idx0=idx0, type_=typ, mask17=mask17)
             mark(0)
-            L.crc32_device_async(stream.data_ptr(), nbytes, d_crc.data_ptr())
-            mark(1)
             with torch.cuda.stream(ext):
                 rcv[:nbytes].copy_(stream[:nbytes])
-            mark(2)
+            mark(1)
             L.flip_bits_device(rcv.data_ptr(), nbits, nflip, seed[0])
             seed[0] += nflip
+            mark(2)
+            L.crc32_stream_device(rcv.data_ptr(), nbytes, d_crc.data_ptr() + 4)
             mark(3)
-            L.crc32_device_async(rcv.data_ptr(), nbytes, d_crc.data_ptr() + 4)
+            L.crc_resend_crc_device(d_crc.data_ptr(), stream.data_ptr(), rcv.data_ptr(), nbytes, d_cnt.data_ptr())
             mark(4)
-            L.crc_resend_device(d_crc.data_ptr(), stream.data_ptr(), rcv.data_ptr(), nbytes, 1, d_cnt.data_ptr())
-            mark(5)
-            L.crc32_device_async(rcv.data_ptr(), nbytes, d_crc.data_ptr() + 4)
-            mark(6)
-            L.crc_resend_device(d_crc.data_ptr(), stream.data_ptr(), rcv.data_ptr(), nbytes, 0, d_cnt.data_ptr())
-            mark(7)
             if ev:
                 ev[1].record(ext)
             L.decode_device(ct, rcv.data_ptr(), nbytes, n, out.data_ptr(), type_=typ, mask17=mask17, max_bytes=cap)
@@ -610,7 +608,7 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
     # ---- the same steps again with per-kernel HIP events, recorded by the library on its own stream
     # (dc_timing_enable, one event set per step): the kernel table and the roofline's launch duration
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
-    phs = [[torch.cuda.Event(enable_timing=True) for _ in range(8)] for _ in range(steps)] if ber > 0 else None
+    phs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(steps)] if ber > 0 else None
     L.L.dc_timing_enable(steps)
     torch.cuda.synchronize()
     L.synchronize()
@@ -638,8 +636,11 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
     L.L.dc_timing_enable(0)
     kavg = kms.mean(axis=0)
     if ber > 0:                                       # the CT9 launches between encode and decode, per step
-        ct9["phase_ms"] = {nm: float(np.mean([p[i].elapsed_time(p[i + 1]) for p in phs]))
-                           for i, nm in enumerate(ct9["phases"])}
+        ct9["phase_ms"] = {nm: float(np.mean([p[i - 1].elapsed_time(p[i]) for p in phs]))
+                           for i, nm in enumerate(ct9["phases"]) if i > 0}
+        # the sender's combine: the encode call's span less the encoder kernel's own (library event slot)
+        ct9["phase_ms"][ct9["phases"][0]] = max(0.0, float(np.mean([e[0].elapsed_time(p[0]) for e, p in zip(evs, phs)]))
+                                                - float(kavg[0]))
     # ---- self-check: poison the stream and the output, run one more step, and compare device hashes of
     # both with the oracle's (tests/golden/bench_hashes.json): a step that skipped work would leave poison
     stream.fill_(0xA5)
@@ -808,8 +809,7 @@ def line_for(C, W, R, steps):
     ms = R["wall"] / steps * 1e3
     kernels = kernel_table(W["ct"], n, nbytes, R["kavg"], R["v3"], R.get("enc_mode", 1), R.get("runs", False))
     for nm, ms_ in R.get("ct9", {}).get("phase_ms", {}).items():   # CT9: every launch of the step
-        kernels[nm] = (ms_, 2.0 * nbytes if "copy" in nm and "compare" not in nm else
-                       (2.0 * nbytes if "resend copy" in nm else (float(nbytes) if "crc32" in nm else 0.0)))
+        kernels[nm] = (ms_, 2.0 * nbytes if "copy" in nm else (float(nbytes) if "damaged copy" in nm else 0.0))
     dname = max(kernels, key=lambda k: kernels[k][0])
     dms, dbytes = kernels[dname]
     ach = dbytes / (dms * 1e-3) / 1e9 if dms > 0 else 0.0

@@ -13,7 +13,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <algorithm>
-#include "dc_shared.h"
+#include "dc_device.h"
 
 namespace dc {
 
@@ -849,6 +849,207 @@ static uint32_t h_xpow8n(unsigned long long n) {                      // x^(8n) 
         k++;
     }
     return p;
+}
+
+// ---------------------------------------------------------------- fused CRC-32 over 16 KiB blocks
+// (dc_device.h): producers XOR each block's raw CRC into blk[b]; crcf_final_kernel combines them.
+// crcf_blocks_kernel: the blocks of a byte range, one workgroup per block, a 64-byte group per thread (four
+// 16-byte loads, its raw CRC, then x^(8 * bytes after the group in the block) by one carry-less multiply);
+// dst != NULL copies the range while it passes (the CT9 resend: the receiver's CRC of the resent copy costs no
+// pass of its own).  Reads whole 16-byte groups: the buffer must be readable to nbytes rounded up to 16
+// (stream buffers of dc_stream_capacity are); bytes past nbytes count as zero, and dst gets zeros there.
+extern "C" long long dc_crcf_blocks(long long nbytes) { return crcf_nblk(nbytes); }
+
+__global__ __launch_bounds__(256) void crcf_blocks_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                          long long nbytes, const uint32_t* __restrict__ ctab,
+                                                          uint32_t* __restrict__ blk, const uint32_t* __restrict__ gate,
+                                                          unsigned* __restrict__ gate_count) {
+    if (gate && gate[0] == gate[1]) return;                 // (the CT9 resend: only after a mismatch)
+    if (gate_count && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(gate_count, 1u);
+    __shared__ uint32_t nib[128];
+    __shared__ uint32_t red[4];
+    const int t = threadIdx.x;
+    if (t < 128) nib[t] = ctab[CRCF_NIB + t];
+    const uint32_t kq = ctab[CRCF_KQ + 2 * (255 - t)];     // group t: 64 (255 - t) bytes before the block's end
+    __syncthreads();
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    const int rng = (int)min((nbytes + 15) / 16 * 16, 0x7FFFFF00ll);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), (short)0, rng, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, rng, 0x00020000);
+    const long long nblk = crcf_nblk(nbytes);
+    for (long long b = blockIdx.x; b < nblk; b += gridDim.x) {
+        const long long g0 = b * DC_CRCF_BLK + 64ll * t;         // (streams below 2 GiB)
+        v4u q[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) q[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(g0 + 16 * i), 0, 0);
+        uint32_t r = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const long long o = g0 + 16 * i;
+            if (o + 16 > nbytes) {                                  // the stream's last group: zeros past its end
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const long long rem = nbytes - (o + 4 * j);
+                    const uint32_t m = rem >= 4 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : (0xFFFFFFFFu >> (8 * (4 - rem))));
+                    q[i][j] &= m;
+                }
+            }
+            if (dst && o < nbytes) __builtin_amdgcn_raw_buffer_store_b128(q[i], rd, (int)o, 0, 0);
+            r = crcf_word(r, q[i].x, nib);
+            r = crcf_word(r, q[i].y, nib);
+            r = crcf_word(r, q[i].z, nib);
+            r = crcf_word(r, q[i].w, nib);
+        }
+        uint32_t v = r ? crcf_mult(kq, r) : 0u;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) v ^= __shfl_xor(v, d, 64);
+        if ((t & 63) == 0) red[t >> 6] = v;
+        __syncthreads();
+        if (t == 0) blk[b] = red[0] ^ red[1] ^ red[2] ^ red[3];
+        __syncthreads();
+    }
+}
+
+// blk[0..nblk) (nblk = the stream's 16 KiB blocks, every one taken as full) -> the stream's zlib CRC-32: thread
+// t folds `per` consecutive blocks by Horner with Kb = x^(8 16384) (table-driven constant multiplies as
+// crc_final2), a 10-level tree joins them; the last block's padding to 16 KiB (p bytes) is undone by x^(-8 16384)
+// x^(8 (16384 - p)), and zlib's init by ~0 x^(8 nbytes) -- both powers as lane products of x^(2^k).  The block
+// words are zeroed as they are read (the next producer XORs into zeros).
+struct CrcfFin {
+    uint32_t kc[1 + CF2_L];     // kc[0] = Kb; kc[1 + l] = Kb^(per 2^l)
+    uint32_t kinv;              // Kb^-1
+    long long per, nbytes;      // (nbytes: when d_nbits is NULL)
+};
+__global__ __launch_bounds__(CF2_T) void crcf_final_kernel(uint32_t* __restrict__ blk, CrcfFin F,
+                                                           const unsigned long long* __restrict__ d_nbits,
+                                                           const uint32_t* __restrict__ ctab, uint32_t* __restrict__ out,
+                                                           const uint32_t* __restrict__ ref, unsigned* __restrict__ count,
+                                                           const uint32_t* __restrict__ gate) {
+    if (gate && gate[0] == gate[1]) return;
+    __shared__ uint32_t T[1 + CF2_L][4][256];
+    __shared__ uint32_t B[1 + CF2_L][32];
+    __shared__ uint32_t red[CF2_T];
+    const int t = threadIdx.x;
+    const long long nbytes = d_nbits ? (long long)((*d_nbits + 7) >> 3) : F.nbytes;
+    const long long nblk = crcf_nblk(nbytes);
+    if (t < 1 + CF2_L) {
+        uint32_t b = F.kc[t];
+        B[t][31] = b;
+        for (int i = 30; i >= 0; i--) {
+            b = (b & 1u) ? (b >> 1) ^ CRC_POLY : b >> 1;
+            B[t][i] = b;
+        }
+    }
+    __syncthreads();
+    for (int e = t; e < (1 + CF2_L) * 1024; e += CF2_T) {
+        const int c = e >> 10, j = (e >> 8) & 3, v = e & 255;
+        uint32_t x = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if ((v >> k) & 1) x ^= B[c][8 * j + k];
+        T[c][j][v] = x;
+    }
+    __syncthreads();
+    uint32_t r = 0;
+    const long long pad = CF2_T * F.per - nblk;                      // leading zero blocks add nothing
+    for (long long i = 0; i < F.per; i++) {
+        const long long b = (long long)t * F.per + i - pad;
+        uint32_t v = 0;
+        if (b >= 0 && b < nblk) { v = blk[b]; blk[b] = 0u; }
+        r = mul_tab(T[0], r) ^ v;
+    }
+    red[t] = r;
+    __syncthreads();
+#pragma unroll
+    for (int l = 0; l < CF2_L; l++) {
+        const int w = 1 << l;
+        uint32_t v = 0;
+        const bool act = (t & (2 * w - 1)) == 0;
+        if (act) v = mul_tab(T[1 + l], red[t]) ^ red[t + w];
+        __syncthreads();
+        if (act) red[t] = v;
+        __syncthreads();
+    }
+    if (t < 64) {
+        // lanes 0..31: x^(8 m), m = 16384 - p (the last block's bytes); lanes 32..63: x^(8 nbytes)
+        const long long p = DC_CRCF_BLK * nblk - nbytes;
+        const unsigned long long e = t < 32 ? (unsigned long long)(p ? DC_CRCF_BLK - p : 0) : (unsigned long long)nbytes;
+        const int k = t & 31;
+        uint32_t f = ((e >> k) & 1ull) ? ctab[CRCF_X2N + k + 3] : CRCF_ONE;
+#pragma unroll
+        for (int d = 1; d < 32; d <<= 1) {
+            const uint32_t o = __shfl_down(f, d, 64);
+            if ((k & (2 * d - 1)) == 0) f = crcf_mult(f, o);
+        }
+        const uint32_t xn = __shfl(f, 32, 64);
+        if (t == 0) {
+            uint32_t R = red[0];
+            if (p) R = crcf_mult(crcf_mult(R, F.kinv), f);
+            const uint32_t crc = nbytes > 0 ? ~(R ^ crcf_mult(xn, 0xFFFFFFFFu)) : 0u;
+            *out = crc;
+            if (ref && count && crc != *ref) atomicAdd(count, 1u);
+        }
+    }
+}
+
+extern "C" int dc_launch_crcf_blocks(const uint8_t* src, uint8_t* dst, long long nbytes, const uint32_t* d_ctab,
+                                     uint32_t* blk, const uint32_t* gate, unsigned* gate_count, hipStream_t st) {
+    if (nbytes <= 0 || nbytes > 0x7FFFFF00ll - 64) return nbytes == 0 ? 0 : -2;
+    const long long nblk = crcf_nblk(nbytes);
+    int dev = 0, ncu = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const long long g = std::max<long long>(1, std::min<long long>(nblk, 8ll * ncu));
+    hipLaunchKernelGGL(crcf_blocks_kernel, dim3((unsigned)g), dim3(256), 0, st, src, dst, nbytes, d_ctab, blk, gate,
+                       gate_count);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int dc_launch_crcf_final(uint32_t* blk, long long max_bytes, long long nbytes, const unsigned long long* d_nbits,
+                                    const uint32_t* d_ctab, uint32_t* crc_out, const uint32_t* ref, unsigned* count,
+                                    const uint32_t* gate, hipStream_t st) {
+    static uint32_t kb = 0, kinv = 0;
+    if (!kb) {
+        kb = h_xpow8n((unsigned long long)DC_CRCF_BLK);
+        uint32_t a = kb, r = 0x80000000u;                                   // Kb^(2^32 - 2): the inverse
+        unsigned long long e = (1ull << 32) - 2;
+        while (e) {
+            if (e & 1) r = h_mult(r, a);
+            a = h_mult(a, a);
+            e >>= 1;
+        }
+        kinv = r;
+    }
+    CrcfFin F;
+    const long long maxblk = std::max<long long>(1, crcf_nblk(std::max(max_bytes, nbytes)));
+    F.per = (maxblk + CF2_T - 1) / CF2_T;
+    F.nbytes = nbytes;
+    F.kc[0] = kb;
+    uint32_t kp = h_xpow8n((unsigned long long)DC_CRCF_BLK * (unsigned long long)F.per);
+    for (int l = 0; l < CF2_L; l++) { F.kc[1 + l] = kp; kp = h_mult(kp, kp); }
+    F.kinv = kinv;
+    hipLaunchKernelGGL(crcf_final_kernel, dim3(1), dim3(CF2_T), 0, st, blk, F, d_nbits, d_ctab, crc_out, ref, count, gate);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// the DC_CRCF_WORDS table words of dc_device.h's fused CRC (nibble tables, 32-byte shifts, x^(2^k))
+extern "C" int dc_crcf_tables(uint32_t* h) {
+    uint32_t tab[4][256];
+    for (uint32_t i = 0; i < 256; i++) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c & 1) ? CRC_POLY ^ (c >> 1) : c >> 1;
+        tab[0][i] = c;
+    }
+    for (int k = 1; k < 4; k++)
+        for (int i = 0; i < 256; i++) tab[k][i] = (tab[k - 1][i] >> 8) ^ tab[0][tab[k - 1][i] & 0xFFu];
+    for (int t = 0; t < 128; t++) {
+        const int j = t >> 4, v = t & 15;
+        h[CRCF_NIB + t] = tab[3 - (j >> 1)][(j & 1) ? (v << 4) : v];
+    }
+    for (int i = 0; i < 512; i++) h[CRCF_KQ + i] = h_xpow8n(32ull * (unsigned long long)i);
+    uint32_t p = 1u << 30;                                                   // x^1
+    for (int k = 0; k < 40; k++) { h[CRCF_X2N + k] = p; p = h_mult(p, p); }
+    return 0;
 }
 
 // CT9 receiver check (the MPI_Bcast_bitwise_mask_crc protocol, impl/dataCompression.c:968-1090; the

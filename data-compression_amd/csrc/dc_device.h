@@ -425,6 +425,31 @@ __device__ __forceinline__ int run_same(uint32_t t, int pos, int tgt, int kmax) 
 // runs mode of a stream: below 6 bits per value it is mostly 3-bit codes (constant input: 3.0; Himeno
 // planes ~3.1; random data ~20), and the walks that find boundaries step whole runs and skip the
 // merge shortcut (period-3 paths in different phases never merge).  CT6 has no 3-bit codes.
+// ------------------------------------------------------------------------------------------------
+// Fused CRC-32 (zlib, reflected polynomial 0xEDB88320) over 16 KiB stream blocks (DC_CRCF_BLK).  CRC is linear
+// over GF(2): the raw CRC (init 0, no final xor) of a block is the XOR of its pieces' raw CRCs, each shifted by
+// x^(8 * bytes after it in the block), so pieces computed by different workgroups (encoder tiles, decoder jobs)
+// combine with an atomic XOR.  ctab (DC_CRCF_WORDS words, dc_crcf_tables): [CRCF_NIB] eight 16-entry nibble
+// tables (the byte table's entry of nibble j alone), [CRCF_KQ] kq[i] = x^(256 i) mod P (a shift by i 32-byte
+// units), [CRCF_X2N] x^(2^k) mod P, k < 40.
+constexpr int CRCF_NIB = 0, CRCF_KQ = 128, CRCF_X2N = 640;
+constexpr uint32_t CRCF_POLY = 0xEDB88320u, CRCF_ONE = 0x80000000u;
+__host__ __device__ inline long long crcf_nblk(long long nbytes) { return (nbytes + DC_CRCF_BLK - 1) / DC_CRCF_BLK; }
+__device__ __forceinline__ uint32_t crcf_word(uint32_t r, uint32_t w, const uint32_t* nib) {   // 4 bytes, LE
+    const uint32_t c = r ^ w;
+    return (nib[c & 15u] ^ nib[16 + ((c >> 4) & 15u)]) ^ (nib[32 + ((c >> 8) & 15u)] ^ nib[48 + ((c >> 12) & 15u)]) ^
+           ((nib[64 + ((c >> 16) & 15u)] ^ nib[80 + ((c >> 20) & 15u)]) ^ (nib[96 + ((c >> 24) & 15u)] ^ nib[112 + (c >> 28)]));
+}
+__device__ __forceinline__ uint32_t crcf_mult(uint32_t a, uint32_t b) {                       // a b mod P
+    uint32_t p = 0;
+#pragma unroll 8
+    for (int i = 31; i >= 0; i--) {
+        p ^= ((a >> i) & 1u) ? b : 0u;
+        b = (b >> 1) ^ ((b & 1u) ? CRCF_POLY : 0u);
+    }
+    return p;
+}
+
 __device__ __forceinline__ int runs_mode(int ct, unsigned long long nbits, long long num) {
     return ct != 6 && num > 0 && nbits < 6ull * (unsigned long long)num;
 }

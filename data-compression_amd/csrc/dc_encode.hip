@@ -866,12 +866,17 @@ __device__ void enc_scanner(uint64_t* __restrict__ st, unsigned ntiles, uint32_t
 #ifndef DC_STORE_U
 #define DC_STORE_U 1                    // (A/B) words per thread per store round: 4 and 8 measured equal, off
 #endif
-template <int CT>
+// CRC (dc_encode_crc_device, the CT9 sender): the raw CRC-32 of the words a tile stores is XOR-ed into the 16 KiB
+// block accumulators cblk (dc_device.h's fused CRC; crcf_final_kernel turns them into the stream's zlib CRC):
+// thread k takes the 16-word group q0 + k of the stream's word grid (q0 = the group of the tile's first word),
+// the tile's stored words in it and zeros for the rest, and shifts its raw CRC to the end of its block.
+template <int CT, bool CRC = false>
 __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
     const float* __restrict__ x, long long n, long long idx0, Params P, uint32_t* __restrict__ out,
     uint64_t* __restrict__ st, uint64_t* __restrict__ tl, unsigned ntiles, int start_bit,
     unsigned long long* __restrict__ total_bits, unsigned long long* __restrict__ total_bits2, uint32_t epoch,
-    unsigned* __restrict__ err, unsigned long long* __restrict__ dbg, int scan) {
+    unsigned* __restrict__ err, unsigned long long* __restrict__ dbg, int scan, const uint32_t* __restrict__ ctab,
+    uint32_t* __restrict__ cblk) {
     static_assert(ENC_K == 16 && ENC_TPB == 256, "16 consecutive floats per thread, 4 waves per tile");
     // (DC_DEBUG_STAMPS: phase stamps of the first 16384 tiles, s_memrealtime)
 #define E1STAMP(ph) do { if (dbg && threadIdx.x == 0 && tile < 16384) dbg[tile * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -883,6 +888,8 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
     __shared__ uint32_t s_tp, s_ok;
     __shared__ uint16_t tab[512];
     __shared__ __attribute__((aligned(16))) uint64_t lbw[128 * LB_DMA_N];   // the first look-back window
+    __shared__ uint32_t cnib[CRC ? 128 : 1];
+    __shared__ uint32_t cred[CRC ? 3 * 4 : 1];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t tag = epoch & ST_TAGM;
     if (scan && blockIdx.x == 0) {                                    // the scanner (dispatched first)
@@ -892,6 +899,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
     const unsigned tile = blockIdx.x - (scan ? 1u : 0u);
     E1STAMP(0);
     build_enc_tab<CT>(tab, P, tid, ENC_TPB);                          // (read after the barrier below)
+    if (CRC && tid < 128) cnib[tid] = ctab[CRCF_NIB + tid];
     const long long tbase = (long long)tile * ENC_TILE;
     const long long base = tbase + (long long)ENC_K * tid;
     const bool full = tbase + ENC_TILE <= n;
@@ -1143,6 +1151,45 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
 #endif
     }
 #endif
+    if constexpr (CRC) {
+        // the stored words by 16-word groups of the stream's word grid (a tile spans at most 258 groups and
+        // three 16 KiB blocks: its raw CRC pieces are XOR-ed per block)
+        const long long q0 = W0 >> 4;
+        const int ng = (int)(((W0 + nw + 15) >> 4) - q0);
+        const long long b0 = q0 >> 8;
+        uint32_t vb[3] = {0u, 0u, 0u};
+        for (int k = tid; k < ng; k += ENC_TPB) {
+            const long long q = q0 + k;
+            uint32_t r = 0;
+#pragma unroll 4
+            for (int u = 0; u < 16; u++) {
+                const int i = (int)(16 * q + u - W0);                      // the tile's word index
+                uint32_t wv = 0u;
+                if (i >= 0 && i < nw) {
+                    const uint32_t cur = i < tw ? sb[i] : 0u;
+                    const uint32_t prev = i ? sb[i - 1] : tp0;
+                    wv = __builtin_bswap32(sh ? __builtin_amdgcn_alignbit(prev, cur, sh) : cur);
+                }
+                r = crcf_word(r, wv, cnib);
+            }
+            const uint32_t v = r ? crcf_mult(ctab[CRCF_KQ + 2 * (255 - (int)(q & 255))], r) : 0u;
+            const int bi = (int)((q >> 8) - b0);
+            vb[0] ^= bi == 0 ? v : 0u;
+            vb[1] ^= bi == 1 ? v : 0u;
+            vb[2] ^= bi == 2 ? v : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) vb[j] ^= __shfl_xor(vb[j], d, 64);
+        }
+        if (lane == 0) { cred[wid] = vb[0]; cred[4 + wid] = vb[1]; cred[8 + wid] = vb[2]; }
+        __syncthreads();
+        if (tid < 3) {
+            const uint32_t v = cred[4 * tid] ^ cred[4 * tid + 1] ^ cred[4 * tid + 2] ^ cred[4 * tid + 3];
+            if (v) atomicXor(cblk + b0 + tid, v);
+        }
+    }
     E1STAMP(5);
 #undef E1STAMP
 }
@@ -1520,7 +1567,8 @@ extern "C" int dc_encode_mode(void) { return g_enc_mode_last; }
 // per-thread bit counts (u16)
 extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, const Params* P,
                                 uint32_t* out, uint64_t* desc, unsigned* flag, uint32_t epoch, int start_bit, unsigned long long* total_bits, unsigned long long* total_bits2,
-                                unsigned* err, unsigned long long* dbg, int mode, hipStream_t stream) {
+                                unsigned* err, unsigned long long* dbg, int mode, const uint32_t* crc_tab, uint32_t* crc_blk,
+                                hipStream_t stream) {
     if (n <= 0) return 0;
     if (mode == 0) mode = enc_mode_default();
     g_enc_mode_last = mode;
@@ -1539,6 +1587,22 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
             if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
                 cus = 256;
         }
+        if (crc_blk) {                       // (the CT9 sender: the stream's CRC pieces while the words are stored)
+            if (!scan || start_bit) return -2;
+            const dim3 gd(grid + 1), bd(ENC_TPB);
+            switch (P->ct) {
+#define DC_ENC_CRC(C)                                                                                \
+    case C:                                                                                          \
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(encode_fused_kernel<C, true>), gd, bd, 0, stream, x, n, idx0, *P, out, st, \
+                           st + ntiles, ntiles, start_bit, total_bits, total_bits2, epoch, err, dbg, 1, crc_tab, crc_blk); \
+        break;
+                DC_ENC_CRC(5) DC_ENC_CRC(6) DC_ENC_CRC(7) DC_ENC_CRC(11)
+#undef DC_ENC_CRC
+                default: return -2;
+            }
+            dc_mark_phase(1, stream);
+            return hipGetLastError() == hipSuccess ? 0 : -1;
+        }
         if (pipe && scan && flag) {
             // persistent workgroups drawing tiles from a ticket counter (flag word 1088: its own 256-byte
             // line past the pack's 1024 flags, zeroed at init and reset by each launch's last draw)
@@ -1550,7 +1614,7 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
             return hipGetLastError() == hipSuccess ? 0 : -1;
         }
         DC_ENC_DISPATCH(encode_fused_kernel, dim3(grid + scan), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, st,
-                        st + ntiles, ntiles, start_bit, total_bits, total_bits2, epoch, err, dbg, scan);
+                        st + ntiles, ntiles, start_bit, total_bits, total_bits2, epoch, err, dbg, scan, nullptr, nullptr);
         dc_mark_phase(1, stream);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }

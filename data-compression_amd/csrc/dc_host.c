@@ -47,6 +47,7 @@ typedef struct {
     struct {                         /* the last encode's launch, re-run wait-free after a look-back timeout */
         const float* x; long long n, idx0; Params P; uint32_t* out; int start_bit;
         unsigned long long* tot; hipStream_t st; int valid;
+        uint32_t* crc;               /* dc_encode_crc_device's CRC output (recomputed after a retry) */
     } last_enc;
     int enc_retries;                 /* encodes re-run wait-free (dc_encode_retries) */
     int enc_outstanding;             /* single-pass encodes issued since the error word was last checked clean
@@ -104,6 +105,9 @@ typedef struct {
     void* med_scr; size_t med_scr_cap;  /* exact mean: chunk transducers (dc_med_scratch_bytes) */
     int* d_i;                        /* [0] type */
     uint32_t* d_crctab; uint32_t* d_x2n; uint32_t* d_crcparts; long long crcparts_cap; uint32_t* d_crc;
+    uint32_t* d_crcf;                /* the fused CRC's tables (dc_crcf_tables) */
+    uint32_t* crcf_blk[3];           /* 16 KiB block accumulators: the encoder's, a stream's, the resend's */
+    long long crcf_cap[3];
     unsigned long long* d_ham;
     unsigned long long* d_ratio;     /* ratio estimators: [0] bits [1] -1.0 flag */
     /* CT1 byte-wise codec */
@@ -256,6 +260,12 @@ int dc_init(int device) {
         const unsigned long long run = (unsigned long long)dc_crc_run_bytes();
         for (int j = 0; j < 256; j++) tab[1024 + j] = h_xpow8n(run * (unsigned long long)j, x2n);
     }
+    {
+        uint32_t ct[DC_CRCF_WORDS];
+        dc_crcf_tables(ct);
+        HIPCHK(hipMalloc((void**)&G.d_crcf, sizeof ct));
+        HIPCHK(hipMemcpy(G.d_crcf, ct, sizeof ct, hipMemcpyHostToDevice));
+    }
     HIPCHK(hipMalloc((void**)&G.d_crctab, sizeof tab));
     HIPCHK(hipMalloc((void**)&G.d_x2n, sizeof x2n));
     HIPCHK(hipMemcpy(G.d_crctab, tab, sizeof tab, hipMemcpyHostToDevice));
@@ -351,7 +361,7 @@ size_t dc_stream_capacity(long long n) { return (size_t)((n * 32 + 7 + 31) / 32)
 
 /* ------------------------------------------------------------------------------------------ */
 static int encode_on(hipStream_t st, int ct, const void* d_x, long long n, long long idx0, int type, uint32_t mask17,
-                     int start_bit, void* d_out, unsigned long long* d_total_bits);
+                     int start_bit, void* d_out, unsigned long long* d_total_bits, uint32_t* crc_blk);
 
 /* public entry: on the encode stream (dc_set_encode_stream) after the work queued on the library stream */
 int dc_encode_device(int ct, const void* d_x, long long n, long long idx0, int type, uint32_t mask17,
@@ -362,7 +372,7 @@ int dc_encode_device(int ct, const void* d_x, long long n, long long idx0, int t
         HIPCHK(hipEventRecord(G.ev_enc, G.st));
         HIPCHK(hipStreamWaitEvent(G.enc_st, G.ev_enc, 0));
     }
-    return encode_on(ENC_ST, ct, d_x, n, idx0, type, mask17, start_bit, d_out, d_total_bits);
+    return encode_on(ENC_ST, ct, d_x, n, idx0, type, mask17, start_bit, d_out, d_total_bits, NULL);
 }
 
 /* internal callers (host ABI, halo path): always on the library stream */
@@ -372,11 +382,56 @@ static int encode_lib(int ct, const void* d_x, long long n, long long idx0, int 
         HIPCHK(hipEventRecord(G.ev_lib, G.enc_st));
         HIPCHK(hipStreamWaitEvent(G.st, G.ev_lib, 0));
     }
-    return encode_on(G.st, ct, d_x, n, idx0, type, mask17, start_bit, d_out, d_total_bits);
+    return encode_on(G.st, ct, d_x, n, idx0, type, mask17, start_bit, d_out, d_total_bits, NULL);
+}
+
+/* the fused CRC's block accumulators of slot k, for streams of up to max_bytes (zeroed when grown; each combine
+   launch zeroes the blocks it reads) */
+static uint32_t* crcf_slot(int k, long long max_bytes) {
+    const long long nb = dc_crcf_blocks(max_bytes) + 4;
+    if (nb > G.crcf_cap[k]) {
+        if (G.crcf_blk[k] && hipFree(G.crcf_blk[k]) != hipSuccess) return NULL;
+        G.crcf_blk[k] = NULL;
+        if (hipMalloc((void**)&G.crcf_blk[k], (size_t)nb * 4) != hipSuccess) return NULL;
+        if (hipMemset(G.crcf_blk[k], 0, (size_t)nb * 4) != hipSuccess) return NULL;
+        G.crcf_cap[k] = nb;
+    }
+    return G.crcf_blk[k];
+}
+
+/* CT9 sender: dc_encode_device at start bit 0, plus the zlib CRC-32 of the stream bytes into d_crc (device, one
+   uint32): the encoder's tiles XOR the raw CRCs of the words they store into 16 KiB block accumulators and one
+   combine launch follows -- no pass over the stream (dc_encode_result re-encodes wait-free after a look-back
+   timeout and then computes the CRC by a pass) */
+int dc_encode_crc_device(int ct, const void* d_x, long long n, long long idx0, int type, uint32_t mask17, void* d_out,
+                         unsigned long long* d_total_bits, uint32_t* d_crc) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (!d_crc || !d_total_bits) return seterr(DC_ERR_ARG, "encode crc: need d_total_bits and d_crc");
+    if (G.enc_st) {
+        HIPCHK(hipEventRecord(G.ev_enc, G.st));
+        HIPCHK(hipStreamWaitEvent(G.enc_st, G.ev_enc, 0));
+    }
+    const long long cap = (long long)dc_stream_capacity(n);
+    uint32_t* blk = crcf_slot(0, cap);
+    if (!blk) return seterr(DC_ERR_HIP, "crc block allocation failed");
+    if ((rc = encode_on(ENC_ST, ct, d_x, n, idx0, type, mask17, 0, d_out, d_total_bits, n > 0 ? blk : NULL))) return rc;
+    G.last_enc.crc = d_crc;
+    if (n > 0 && dc_encode_mode() != 1) {        /* (a multi-pass variant, DC_ENC_PASSES: a pass of its own) */
+        unsigned long long bits = 0;
+        HIPCHK(hipMemcpyAsync(&bits, d_total_bits, 8, hipMemcpyDeviceToHost, ENC_ST));
+        HIPCHK(hipStreamSynchronize(ENC_ST));
+        if (dc_launch_crcf_blocks((const uint8_t*)d_out, NULL, (long long)((bits + 7) / 8), G.d_crcf, blk, NULL, NULL, ENC_ST))
+            return seterr(DC_ERR_HIP, "crc launch failed");
+    }
+    if (dc_launch_crcf_final(blk, cap, n > 0 ? -1 : 0, n > 0 ? d_total_bits : NULL, G.d_crcf, d_crc, NULL, NULL, NULL,
+                             ENC_ST))
+        return seterr(DC_ERR_HIP, "crc launch failed");
+    return DC_OK;
 }
 
 static int encode_on(hipStream_t st, int ct, const void* d_x, long long n, long long idx0, int type, uint32_t mask17,
-                     int start_bit, void* d_out, unsigned long long* d_total_bits) {
+                     int start_bit, void* d_out, unsigned long long* d_total_bits, uint32_t* crc_blk) {
     if (!valid_ct(ct)) return seterr(DC_ERR_ARG, "unsupported CT %d", ct);
     if (start_bit < 0 || start_bit > 7 || n < 0) return seterr(DC_ERR_ARG, "bad start_bit/n");
     if (n > (1ll << 33)) return seterr(DC_ERR_ARG, "n above 2^33 floats");
@@ -411,11 +466,13 @@ static int encode_on(hipStream_t st, int ct, const void* d_x, long long n, long 
         G.enc_epoch = 1;
     }
     if (dc_launch_encode((const float*)d_x, n, idx0, &P, (uint32_t*)d_out, G.enc_desc, G.d_enc_flag, G.enc_epoch,
-                         start_bit, tot, tot != G.d_total ? G.d_total : NULL, G.d_enc_err, G.enc_dbg, 0, st))
+                         start_bit, tot, tot != G.d_total ? G.d_total : NULL, G.d_enc_err, G.enc_dbg, 0,
+                         crc_blk ? G.d_crcf : NULL, crc_blk, st))
         return seterr(DC_ERR_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
     G.last_enc.x = (const float*)d_x; G.last_enc.n = n; G.last_enc.idx0 = idx0; G.last_enc.P = P;
     G.last_enc.out = (uint32_t*)d_out; G.last_enc.start_bit = start_bit; G.last_enc.tot = tot; G.last_enc.st = st;
     G.last_enc.valid = 1;
+    G.last_enc.crc = NULL;
     G.enc_outstanding++;
     return DC_OK;
 }
@@ -465,7 +522,7 @@ static int encode_retry(hipStream_t st) {
     unsigned long long* tot = G.last_enc.tot;
     if (dc_launch_encode(G.last_enc.x, G.last_enc.n, G.last_enc.idx0, &G.last_enc.P, G.last_enc.out, G.enc_desc,
                          G.d_enc_flag, G.enc_epoch, G.last_enc.start_bit, tot, tot != G.d_total ? G.d_total : NULL,
-                         G.d_enc_err, NULL, 3, st))
+                         G.d_enc_err, NULL, 3, NULL, NULL, st))
         return seterr(DC_ERR_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
     G.enc_retries++;
     G.enc_outstanding = 1;
@@ -510,6 +567,13 @@ int dc_encode_result(unsigned long long* total_bits) {
         HIPCHK(hipMemcpyAsync(&G.h_scratch[1], G.d_enc_err, 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         err = (unsigned)(G.h_scratch[1] & 0xFFFFFFFFu);
+        if (!err && G.last_enc.crc) {             /* the retried stream's CRC, by a pass of its own */
+            const long long nb = (long long)((G.h_scratch[0] + 7) / 8);
+            uint32_t* blk = crcf_slot(0, nb);
+            if (!blk || dc_launch_crcf_blocks((const uint8_t*)G.last_enc.out, NULL, nb, G.d_crcf, blk, NULL, NULL, st) ||
+                dc_launch_crcf_final(blk, nb, nb, NULL, G.d_crcf, G.last_enc.crc, NULL, NULL, NULL, st))
+                return seterr(DC_ERR_HIP, "crc launch failed");
+        }
     }
     if (err) {
         HIPCHK(hipMemsetAsync(G.d_enc_err, 0, 4, st));
@@ -1305,6 +1369,33 @@ int dc_copy_rate_device(const void* d_src, void* d_dst, long long bytes, int rep
     (void)hipEventDestroy(e1);
     if (gbs_out) *gbs_out = best;
     if (variant_out) *variant_out = bv;
+    return DC_OK;
+}
+
+/* the fused-CRC forms (dc_gpu.h): a stream's CRC by the 16 KiB block kernel + one combine; the CT9 resend with
+   the receiver's CRC of the copy computed as it is written */
+int dc_crc32_stream_device(const void* d_s, long long nbytes, uint32_t* d_crc) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (nbytes < 0 || nbytes > 0x7FFFFF00ll - 64 || ((uintptr_t)d_s & 15u)) return seterr(DC_ERR_ARG, "crc: bad stream");
+    uint32_t* blk = crcf_slot(1, nbytes);
+    if (!blk) return seterr(DC_ERR_HIP, "crc block allocation failed");
+    if (dc_launch_crcf_blocks((const uint8_t*)d_s, NULL, nbytes, G.d_crcf, blk, NULL, NULL, G.st) ||
+        dc_launch_crcf_final(blk, nbytes, nbytes, NULL, G.d_crcf, d_crc, NULL, NULL, NULL, G.st))
+        return seterr(DC_ERR_HIP, "crc launch failed");
+    return DC_OK;
+}
+
+int dc_crc_resend_crc_device(uint32_t* d_crc2, const void* d_src, void* d_dst, long long nbytes, unsigned* d_count) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (nbytes < 0 || nbytes > 0x7FFFFF00ll - 64 || (((uintptr_t)d_src | (uintptr_t)d_dst) & 15u))
+        return seterr(DC_ERR_ARG, "resend: 16-byte aligned streams below 2 GiB");
+    uint32_t* blk = crcf_slot(2, nbytes);
+    if (!blk) return seterr(DC_ERR_HIP, "crc block allocation failed");
+    if (dc_launch_crcf_blocks((const uint8_t*)d_src, (uint8_t*)d_dst, nbytes, G.d_crcf, blk, d_crc2, d_count, G.st) ||
+        dc_launch_crcf_final(blk, nbytes, nbytes, NULL, G.d_crcf, d_crc2 + 1, d_crc2, d_count + 1, d_crc2, G.st))
+        return seterr(DC_ERR_HIP, "resend launch failed");
     return DC_OK;
 }
 

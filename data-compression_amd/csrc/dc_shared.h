@@ -105,7 +105,8 @@ typedef struct ihipStream_t* dc_hip_stream;
 int dc_launch_encode(const float* x, long long n, long long idx0, const DC_NS Params* P, uint32_t* out,
                      uint64_t* desc, unsigned* flag, uint32_t epoch, int start_bit,
                      unsigned long long* total_bits, unsigned long long* total_bits2, unsigned* err,
-                     unsigned long long* dbg, int mode, dc_hip_stream stream);
+                     unsigned long long* dbg, int mode, const uint32_t* crc_tab, uint32_t* crc_blk,
+                     dc_hip_stream stream);
 int dc_encode_mode(void);
 unsigned dc_encode_epoch_limit(void);
 long long dc_encode_group_count(long long n);
@@ -213,8 +214,21 @@ int dc_launch_shard_fix_s(const uint8_t* s, const DC_NS Params* P, const DC_NS D
 int dc_launch_plane_gather(const float* p, int mj, int mk, int ijk, int v, int A, int B, float* out, dc_hip_stream st);
 int dc_launch_plane_scatter(const float* x, const float* d_min, float* p, int mj, int mk, int ijk, int v, int A, int B,
                             dc_hip_stream st);
-int dc_launch_hash_words(const void* p, long long nbytes, unsigned long long* d_out, hipStream_t st);
-int dc_launch_stream_copy(const void* src, void* dst, long long bytes, int variant, hipStream_t st);
+int dc_launch_hash_words(const void* p, long long nbytes, unsigned long long* d_out, dc_hip_stream st);
+int dc_launch_stream_copy(const void* src, void* dst, long long bytes, int variant, dc_hip_stream st);
+/* fused CRC-32 (zlib) over 16 KiB stream blocks: per-block raw CRCs (XOR-accumulated by the producers, or by
+   dc_launch_crcf_blocks from a byte range, optionally copying it: the CT9 resend), then one combine launch
+   (crc_out = zlib CRC of the first nbytes / *d_nbits bits' bytes; blk zeroed for the next use; with ref: a
+   mismatch increments *count).  gate (optional, two CRCs): the blocks launch runs only when they differ. */
+#define DC_CRCF_BLK 16384
+#define DC_CRCF_WORDS 680
+long long dc_crcf_blocks(long long nbytes);
+int dc_crcf_tables(uint32_t* h_tab);        /* the DC_CRCF_WORDS table words (nibble tables, shifts, x^2^k) */
+int dc_launch_crcf_blocks(const uint8_t* src, uint8_t* dst, long long nbytes, const uint32_t* d_ctab, uint32_t* blk,
+                          const uint32_t* gate, unsigned* gate_count, dc_hip_stream st);
+int dc_launch_crcf_final(uint32_t* blk, long long max_bytes, long long nbytes, const unsigned long long* d_nbits,
+                         const uint32_t* d_ctab, uint32_t* crc_out, const uint32_t* ref, unsigned* count,
+                         const uint32_t* gate, dc_hip_stream st);
 int dc_launch_flip_bits(uint8_t* s, unsigned long long nbits, long long count, unsigned long long seed,
                         dc_hip_stream st);
 int dc_launch_crc_resend(const uint32_t* crc, const uint8_t* src, uint8_t* dst, long long nbytes, int copy,

@@ -39,7 +39,8 @@ EXT_SYMBOLS = [
     "dc_get_abs_error_bound", "dc_stream_capacity", "dc_encode_device", "dc_encode_result",
     "dc_decode_device", "dc_decode_finish", "dc_to_small_device", "dc_med_device", "dc_crc32_device",
     "dc_decode_chunk_bits_value", "dc_ct1_encode_device", "dc_ct1_decode_device", "dc_encode_bits_device",
-    "dc_crc32_device_async", "dc_hash_device", "dc_copy_rate_device", "dc_flip_bits_device", "dc_decode_shard_device", "dc_decode_shard_fix",
+    "dc_crc32_device_async", "dc_encode_crc_device", "dc_crc32_stream_device", "dc_crc_resend_crc_device",
+    "dc_hash_device", "dc_copy_rate_device", "dc_flip_bits_device", "dc_decode_shard_device", "dc_decode_shard_fix",
     "dc_halo_encode_device", "dc_halo_decode_device",
     "dc64_stream_capacity", "dc64_encode_device", "dc64_encode_result", "dc64_decode_device", "dc64_decode_finish",
     "dc64_last_decode_flags", "dc64_to_small_device", "dc64_med_device", "dc_set_encode_stream",
@@ -79,6 +80,9 @@ class Lib:
         L.dc_stream_capacity.argtypes = [ll]
         L.dc_stream_capacity.restype = C.c_size_t
         L.dc_encode_device.argtypes = [C.c_int, vp, ll, ll, C.c_int, u32, C.c_int, vp, vp]
+        L.dc_encode_crc_device.argtypes = [C.c_int, vp, ll, ll, C.c_int, u32, vp, vp, vp]
+        L.dc_crc32_stream_device.argtypes = [vp, ll, vp]
+        L.dc_crc_resend_crc_device.argtypes = [vp, vp, vp, ll, vp]
         L.dc_encode_result.argtypes = [C.POINTER(C.c_ulonglong)]
         L.dc_encode_bits_device.argtypes = [C.c_int, vp, ll, ll, C.c_int, u32, C.POINTER(C.c_ulonglong)]
         L.dc_decode_device.argtypes = [C.c_int, vp, ll, vp, ll, ll, C.c_int, u32, vp]
@@ -370,6 +374,18 @@ class Lib:
     def encode_device(self, ct, x_ptr, n, out_ptr, idx0=0, type_=0, mask17=0, start_bit=0, total_ptr=None):
         self.check(self.L.dc_encode_device(ct, x_ptr, n, idx0, type_, mask17, start_bit, out_ptr, total_ptr),
                    "dc_encode_device")
+
+    def encode_crc_device(self, ct, x_ptr, n, out_ptr, total_ptr, crc_ptr, idx0=0, type_=0, mask17=0):
+        """dc_encode_crc_device: the encode (start bit 0) plus the stream's zlib CRC-32 into *crc_ptr (device)."""
+        self.check(self.L.dc_encode_crc_device(ct, x_ptr, n, idx0, type_, mask17, out_ptr, total_ptr, crc_ptr),
+                   "dc_encode_crc_device")
+
+    def crc32_stream_device(self, s_ptr, nbytes, crc_ptr):
+        self.check(self.L.dc_crc32_stream_device(s_ptr, nbytes, crc_ptr), "dc_crc32_stream_device")
+
+    def crc_resend_crc_device(self, d_crc2_ptr, src_ptr, dst_ptr, nbytes, d_count_ptr):
+        self.check(self.L.dc_crc_resend_crc_device(d_crc2_ptr, src_ptr, dst_ptr, nbytes, d_count_ptr),
+                   "dc_crc_resend_crc_device")
 
     def encode_bits(self, ct, x_ptr, n, idx0=0, type_=0, mask17=0):
         v = C.c_ulonglong(0)

@@ -163,6 +163,18 @@ int dc_hash_device(const void* d_buf, long long nbytes, unsigned long long* hash
  * *gbs_out = the best variant's (read + written bytes) / average launch time, in GB/s; *variant_out its
  * index.  Synchronous. */
 int dc_copy_rate_device(const void* d_src, void* d_dst, long long bytes, int reps, double* gbs_out, int* variant_out);
+/* The CT9 flow without CRC passes of its own (fused CRC-32 over 16 KiB blocks; each a zlib crc32 of the stream
+ * bytes, written to device memory, asynchronous on the library stream):
+ * dc_encode_crc_device: dc_encode_device at start bit 0 (d_total_bits required) plus the stream's CRC into
+ *   *d_crc, computed by the encoder's tiles from the words they store, and one combine launch;
+ * dc_crc32_stream_device: a stream's CRC by one pass (16-byte aligned, readable to nbytes rounded up to 16);
+ * dc_crc_resend_crc_device: the receiver's check with the resend (d_crc2[0] sender's CRC, d_crc2[1] receiver's):
+ *   on a mismatch d_src is copied over d_dst (d_count[0] += 1) and the copy's CRC, computed as it is written,
+ *   replaces d_crc2[1]; a mismatch left after that increments d_count[1]. */
+int dc_encode_crc_device(int ct, const void* d_x, long long n, long long idx0, int type, uint32_t mask17, void* d_out,
+                         unsigned long long* d_total_bits, uint32_t* d_crc);
+int dc_crc32_stream_device(const void* d_s, long long nbytes, uint32_t* d_crc);
+int dc_crc_resend_crc_device(uint32_t* d_crc2, const void* d_src, void* d_dst, long long nbytes, unsigned* d_count);
 /* BER fault injection (CT8/CT9 flow): flip `count` bits of the stream at positions
  * splitmix64(seed + i) mod nbits (MSB-first in each byte, as bit_flip).  The stream buffer must be
  * 4-byte aligned and padded to whole words.  Asynchronous. */

@@ -525,3 +525,72 @@ def test_copy_rate_device(dc):
     gbs, v = dc.copy_rate(a.data_ptr(), b.data_ptr(), 4 * n, 3)
     assert torch.equal(a, b)
     assert 0 <= v < 4 and 500.0 < gbs < 8000.0
+
+
+@pytest.mark.parametrize("nbytes", [0, 1, 15, 16, 17, 4095, 16383, 16384, 16385, 40000, (1 << 20) + 7, 3 * 16384 * 1024 + 5])
+def test_crc32_stream_device_zlib(dc, nbytes):
+    """The fused CRC's block kernel + combine (dc_crc32_stream_device) equals zlib on ragged lengths (bytes past
+    nbytes, here nonzero, do not count)."""
+    import zlib
+    import torch
+    rng = np.random.RandomState(nbytes & 0xFFFF)
+    h = rng.randint(0, 256, size=nbytes + 64, dtype=np.uint8)
+    d = torch.from_numpy(h).cuda()
+    c = torch.zeros(4, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    dc.crc32_stream_device(d.data_ptr(), nbytes, c.data_ptr())
+    dc.synchronize()
+    assert (int(c[0].item()) & 0xFFFFFFFF) == zlib.crc32(h[:nbytes].tobytes())
+
+
+@pytest.mark.parametrize("ct", [5, 6, 7, 11])
+@pytest.mark.parametrize("n", [1, 5, 4096, 4097, 70001, (1 << 20) + 5])
+def test_encode_crc_device(dc, oracle, ct, n):
+    """dc_encode_crc_device: the stream equals the plain encode's (and the oracle's), and the CRC its tiles build
+    from the words they store equals zlib's CRC-32 of the stream bytes."""
+    import zlib
+    import torch
+    dc.set_bound(1e-3)
+    _, xs = oracle.to_small(oracle.gen_u10(n))
+    t, m17 = oracle.type_mask(xs)
+    dx = torch.from_numpy(xs).cuda()
+    cap = dc.stream_capacity(n)
+    st = torch.full((cap,), 0x5A, dtype=torch.uint8, device="cuda")
+    nb = torch.zeros(1, dtype=torch.int64, device="cuda")
+    c = torch.zeros(4, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    for _ in range(2):                                   # (twice: the block accumulators are reused)
+        dc.encode_crc_device(ct, dx.data_ptr(), n, st.data_ptr(), nb.data_ptr(), c.data_ptr(), type_=t, mask17=m17)
+        bits = dc.encode_result()
+        nbytes = (bits + 7) // 8
+        s = st[:nbytes].cpu().numpy()
+        so, nbo, _ = oracle.compress(ct, xs, 1e-3, t, m17)
+        assert nbo == nbytes and np.array_equal(s, so)
+        assert (int(c[0].item()) & 0xFFFFFFFF) == zlib.crc32(s.tobytes())
+
+
+def test_crc_resend_crc_device(dc):
+    """The CT9 resend with the receiver's CRC of the copy computed as it is written: a damaged copy is replaced
+    (count[0] = 1), the copy's CRC equals the sender's (count[1] = 0); an intact copy is left alone."""
+    import zlib
+    import torch
+    nbytes = 5 * 16384 + 77
+    h = np.random.RandomState(7).randint(0, 256, size=nbytes + 64, dtype=np.uint8)
+    src = torch.from_numpy(h).cuda()
+    dst = src.clone()
+    dst[12345] ^= 4
+    crc2 = torch.zeros(2, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(2, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    dc.crc32_stream_device(src.data_ptr(), nbytes, crc2.data_ptr())
+    dc.crc32_stream_device(dst.data_ptr(), nbytes, crc2.data_ptr() + 4)
+    dc.synchronize()
+    assert int(crc2[0].item()) != int(crc2[1].item())
+    dc.crc_resend_crc_device(crc2.data_ptr(), src.data_ptr(), dst.data_ptr(), nbytes, cnt.data_ptr())
+    dc.synchronize()
+    assert cnt.tolist() == [1, 0]
+    assert torch.equal(dst[:nbytes], src[:nbytes])
+    assert (int(crc2[1].item()) & 0xFFFFFFFF) == zlib.crc32(h[:nbytes].tobytes())
+    dc.crc_resend_crc_device(crc2.data_ptr(), src.data_ptr(), dst.data_ptr(), nbytes, cnt.data_ptr())
+    dc.synchronize()
+    assert cnt.tolist() == [1, 0]
