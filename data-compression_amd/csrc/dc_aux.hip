@@ -183,7 +183,8 @@ struct MedScratch {
     int* elo;                                              // [nch] first candidate binade
     typename MedFP<T>::D* Td;                              // [nch * MW * 2] units added from parity 0 / 1
     uint8_t* F;                                            // [nch * MW] end parity 0 | end parity 1 << 1 | bad << 2
-    uint8_t* Z;                                            // [nch] 1: every element is +0 / -0
+    uint8_t* Z;                                            // [nch] 1: every element is +0 / -0; 2: some element
+                                                           // is negative or NaN (no transducer takes the chunk)
 };
 
 template <typename T>
@@ -210,6 +211,15 @@ __host__ __device__ inline MedScratch<T> med_scratch(void* base, long long nch) 
 template <typename T>
 __device__ __forceinline__ void load_chunk(const T* __restrict__ x, long long n, long long c, T* v) {
     const long long e0 = c * MC + (long long)threadIdx.x * MC_PER;
+    if (sizeof(T) == 4 && e0 + MC_PER <= n && (reinterpret_cast<uintptr_t>(x) & 15u) == 0) {
+        // (a whole thread's run: two 16-byte loads instead of eight guarded 4-byte ones)
+        const float4* p = reinterpret_cast<const float4*>(x + e0);
+        const float4 a = p[0], b = p[1];
+        const float f[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int i = 0; i < MC_PER; i++) v[i] = (T)f[i];
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < MC_PER; i++) v[i] = e0 + i < n ? x[e0 + i] : (T)0;
 }
@@ -225,15 +235,17 @@ __global__ __launch_bounds__(MC_T) void med_chunk_sum_kernel(const T* __restrict
     const long long e0 = c * MC + (long long)threadIdx.x * MC_PER;
     double sm = 0.0;
     T mx = -INFINITY;
-    bool nz = false;
+    bool nz = false, ng = false;
 #pragma unroll
     for (int i = 0; i < MC_PER; i++)
         if (e0 + i < n) {
             sm += (double)v[i];
             mx = v[i] > mx ? v[i] : mx;                          // NaNs never win (as the reference's >)
             nz |= (FP::bits(v[i]) << 1) != 0;
+            ng |= !(v[i] >= (T)0);                               // negative or NaN
         }
     const bool anynz = __syncthreads_or(nz);
+    const bool anyng = __syncthreads_or(ng);
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
         sm += __shfl_xor(sm, d, 64);
@@ -248,7 +260,7 @@ __global__ __launch_bounds__(MC_T) void med_chunk_sum_kernel(const T* __restrict
         for (int w = 0; w < MC_T / 64; w++) { t += ws[w]; m = wm[w] > m ? wm[w] : m; }
         M.csum[c] = isfinite(t) ? t : 0.0;
         M.cmax[c] = m;
-        M.Z[c] = anynz ? 0 : 1;
+        M.Z[c] = (uint8_t)((anynz ? 0 : 1) | (anyng ? 2 : 0));
     }
 }
 
@@ -261,7 +273,14 @@ __global__ __launch_bounds__(1024) void med_chunk_scan_kernel(MedScratch<T> M, l
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const long long per = (nch + 1023) / 1024, c0 = tid * per, c1 = min(nch, c0 + per);
     double sm = 0.0;
-    for (long long c = c0; c < c1; c++) sm += M.csum[c];
+    // (eight independent loads in flight per round: one dependent load after another took ~60 us at 2^26)
+    for (long long cb = c0; cb < c1; cb += 8) {
+        double t[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) t[i] = cb + i < c1 ? M.csum[cb + i] : 0.0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) sm += t[i];
+    }
     double inc = sm;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -272,37 +291,63 @@ __global__ __launch_bounds__(1024) void med_chunk_scan_kernel(MedScratch<T> M, l
     __syncthreads();
     double run = (double)s_init + inc - sm;
     for (int w = 0; w < wid; w++) run += wt[w];
-    for (long long c = c0; c < c1; c++) {
-        const T est = (T)fmin(fmax(run, 0.0), (double)FP::smax());
-        M.elo[c] = FP::expo(est) - 4;
-        run += M.csum[c];
+    for (long long cb = c0; cb < c1; cb += 8) {
+        double t[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) t[i] = cb + i < c1 ? M.csum[cb + i] : 0.0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            if (cb + i < c1) {
+                const T est = (T)fmin(fmax(run, 0.0), (double)FP::smax());
+                M.elo[cb + i] = FP::expo(est) - 4;
+                run += t[i];
+            }
+        }
     }
 }
 
-// transducer of one thread's elements for binade E (k's parity p in, units added / parity out)
-template <typename T>
+// transducer of one thread's elements for binade E (k's parity p in, units added / parity out).  Only a tie
+// (x/u exactly halfway) depends on the parity: before the first tie the two paths (start parity 0 / 1) add the
+// same units and differ in parity by 1 (X = the XOR of the units' low bits); the first tie rounds each to even
+// (its bit differs between the paths), and from then on both paths are one.  So the common units S, the first
+// tie's two bits and one parity are tracked, instead of both paths element by element.
+template <typename T, int N = MC_PER>
 __device__ __forceinline__ void trans_elems(const T* v, int cnt, int E, typename MedFP<T>::D& d0,
                                             typename MedFP<T>::D& d1, int& p0, int& p1, bool& bad) {
     typedef MedFP<T> FP;
     typedef typename FP::D D;
     const T scale = FP::pow2(FP::BIAS + FP::M - E);                 // 1/u
     const T lim = FP::pow2(E + 1 - FP::BIAS);                       // the binade's top
-    d0 = 0; d1 = 0; p0 = 0; p1 = 1; bad = false;
+    D S = 0;
+    int X = 0, e0 = 0, e1 = 0;
+    bool tied = false;
+    bad = false;
 #pragma unroll
-    for (int i = 0; i < MC_PER; i++) {
+    for (int i = 0; i < N; i++) {
         if (i < cnt) {
-            bad |= !(v[i] >= (T)0) || !(v[i] < lim);              // negative, NaN, inf or >= the binade's top
-            const T q = FP::mul(v[i], scale);                     // exact: power-of-two scaling
+            const bool ok = v[i] >= (T)0 && v[i] < lim;           // not negative, NaN, inf or >= the binade's top
+            bad |= !ok;
+            const T q = FP::mul(ok ? v[i] : (T)0, scale);         // exact: power-of-two scaling, < 2^(M+1)
             const T fq = floor(q);
             const T fr = FP::sub(q, fq);
             const D fl = (D)fq;
-            const int up = fr > (T)0.5 ? 1 : 0, tie = fr == (T)0.5 ? 1 : 0;
-            const D r0 = fl + up + (tie & (int)((p0 + fl) & 1));
-            const D r1 = fl + up + (tie & (int)((p1 + fl) & 1));
-            d0 = min(d0 + r0, FP::SAT); d1 = min(d1 + r1, FP::SAT);   // >= 2^(M+1) leaves the binade anyway
-            p0 = (int)((p0 + r0) & 1); p1 = (int)((p1 + r1) & 1);
+            if (__builtin_expect(fr == (T)0.5, 0)) {              // a tie: round the path's k + fl to even
+                const int b = (X ^ (int)(fl & 1)) & 1;
+                if (!tied) { e0 = b; e1 = b ^ 1; tied = true; } else S += b;
+                S += fl;
+                X = 0;
+            } else {
+                const D r = fl + (fr > (T)0.5 ? 1 : 0);
+                S += r;
+                X ^= (int)(r & 1);
+            }
         }
     }
+    // (a thread's MC_PER units stay far below the type's range; compose() saturates the sums)
+    d0 = min(S + e0, FP::SAT);
+    d1 = min(S + e1, FP::SAT);
+    p0 = X;
+    p1 = tied ? X : X ^ 1;
 }
 
 // f then g (f earlier): start parity p -> f's units + g's units from f's end parity
@@ -326,13 +371,22 @@ __global__ __launch_bounds__(MC_T) void med_chunk_trans_kernel(const T* __restri
     const long long e0 = c * MC + (long long)tid * MC_PER;
     const int cnt = (int)max(0ll, min((long long)MC_PER, n - e0));
     const int elo = M.elo[c];
+    const T cmax = M.cmax[c];
+    const bool negnan = (M.Z[c] & 2) != 0;
 #pragma unroll
     for (int w = 0; w < MW; w++) {
         const int E = elo + w;
         D d0 = 0, d1 = 0;
         int p0 = 0, p1 = 1;
         bool bad = E < FP::EMIN || E > FP::EMAX;                      // 1/u or the binade top not a number
-        if (!bad) trans_elems<T>(v, cnt, E, d0, d1, p0, p1, bad);
+        if (!bad && negnan) {
+            bad = true;                                                // (no transducer for any binade)
+        } else if (!bad && cmax < FP::pow2(E - FP::BIAS - FP::M - 1)) {
+            // every element below u/2 (and none negative or NaN): nothing added, parity kept -- the
+            // transducer of a stalled sum, computed for free (uniform branch)
+        } else if (!bad) {
+            trans_elems<T>(v, cnt, E, d0, d1, p0, p1, bad);
+        }
         // ordered reduction over the wave: lane i absorbs lane i + d (its successor block)
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -361,6 +415,54 @@ __global__ __launch_bounds__(MC_T) void med_chunk_trans_kernel(const T* __restri
     }
 }
 
+// a transducer as the compose kernel scans them: units from start parity 0 / 1, end parities, and the first
+// thread (of the scan) whose piece no transducer takes
+template <typename D>
+struct MTr {
+    D a0, a1;
+    int q0, q1, fb;
+};
+template <typename D>
+__device__ __forceinline__ MTr<D> mtr_then(const MTr<D>& f, const MTr<D>& g, D sat) {     // f, then g
+    MTr<D> r = f;
+    compose(r.a0, r.a1, r.q0, r.q1, g.a0, g.a1, g.q0, g.q1, sat);
+    r.fb = min(f.fb, g.fb);
+    return r;
+}
+template <typename D>
+__device__ __forceinline__ MTr<D> mtr_shfl_up(const MTr<D>& v, int d) {
+    MTr<D> o;
+    o.a0 = __shfl_up(v.a0, d, 64); o.a1 = __shfl_up(v.a1, d, 64);
+    o.q0 = __shfl_up(v.q0, d, 64); o.q1 = __shfl_up(v.q1, d, 64); o.fb = __shfl_up(v.fb, d, 64);
+    return o;
+}
+// inclusive scan of MX_T transducers in thread order (wave scans by shuffles, one LDS round for the 16 wave
+// totals: 3 barriers, where a Hillis-Steele scan through LDS took 10)
+template <typename D>
+__device__ __forceinline__ MTr<D> mtr_block_scan(MTr<D> v, MTr<D>* wt, D sat) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const MTr<D> o = mtr_shfl_up(v, d);
+        if (lane >= d) v = mtr_then(o, v, sat);
+    }
+    if (lane == 63) wt[wid] = v;
+    __syncthreads();
+    if (wid == 0) {
+        MTr<D> t = lane < MX_T / 64 ? wt[lane] : MTr<D>{0, 0, 0, 1, MX_T};
+#pragma unroll
+        for (int d = 1; d < MX_T / 64; d <<= 1) {
+            const MTr<D> o = mtr_shfl_up(t, d);
+            if (lane >= d) t = mtr_then(o, t, sat);
+        }
+        if (lane < MX_T / 64) wt[MX_T / 64 + lane] = t;       // inclusive over the waves
+    }
+    __syncthreads();
+    if (wid > 0) v = mtr_then(wt[MX_T / 64 + wid - 1], v, sat);
+    __syncthreads();                                        // (wt is rewritten by the next scan)
+    return v;
+}
+
 template <typename T>
 __global__ __launch_bounds__(MX_T) void med_compose_kernel(const T* __restrict__ x, long long n, T s_init,
                                                            MedScratch<T> M, T* __restrict__ out_mean,
@@ -370,12 +472,11 @@ __global__ __launch_bounds__(MX_T) void med_compose_kernel(const T* __restrict__
     typedef typename FP::D D;
     typedef typename FP::U U;
     __shared__ T buf[MC];
-    __shared__ D sa[2][2][MX_T];                            // [buffer][start parity] units
-    __shared__ unsigned char sq[2][2][MX_T];                // [buffer][start parity] end parity
-    __shared__ int sb[2][MX_T];                             // first invalid chunk (inclusive min)
+    __shared__ D sa[2][MX_T];                               // [start parity] inclusive units
+    __shared__ MTr<D> wt[2 * (MX_T / 64)];
     __shared__ T s_sum;
     __shared__ long long s_c;
-    __shared__ int s_first;
+    __shared__ int s_first, s_i;
     __shared__ T smx[MX_T / 64];
     const int tid = threadIdx.x;
     const long long nch = (n + MC - 1) / MC;
@@ -389,7 +490,7 @@ __global__ __launch_bounds__(MX_T) void med_compose_kernel(const T* __restrict__
         if (FP::bits(sv) == 0) {                            // +0 + (+-0) = +0: skip runs of zero chunks
             if (tid == 0) s_first = MX_T;
             __syncthreads();
-            if (c + tid < nch && !M.Z[c + tid]) atomicMin(&s_first, tid);
+            if (c + tid < nch && !(M.Z[c + tid] & 1)) atomicMin(&s_first, tid);
             __syncthreads();
             const int f = s_first;
             __syncthreads();
@@ -419,36 +520,19 @@ __global__ __launch_bounds__(MX_T) void med_compose_kernel(const T* __restrict__
                     fb = (f & 4) ? tid : MX_T;
                 }
             }
-            int cur = 0;
-            sa[0][0][tid] = a0; sa[0][1][tid] = a1; sq[0][0][tid] = (unsigned char)q0; sq[0][1][tid] = (unsigned char)q1;
-            sb[0][tid] = fb;
-            __syncthreads();
-            for (int dd = 1; dd < MX_T; dd <<= 1) {          // inclusive scan: F_t = f_0 then ... then f_t
-                D b0 = sa[cur][0][tid], b1 = sa[cur][1][tid];
-                int e0 = sq[cur][0][tid], e1 = sq[cur][1][tid];
-                int bb = sb[cur][tid];
-                if (tid >= dd) {
-                    D p0 = sa[cur][0][tid - dd], p1 = sa[cur][1][tid - dd];
-                    int r0 = sq[cur][0][tid - dd], r1 = sq[cur][1][tid - dd];
-                    compose(p0, p1, r0, r1, b0, b1, e0, e1, FP::SAT);
-                    b0 = p0; b1 = p1; e0 = r0; e1 = r1;
-                    bb = min(bb, sb[cur][tid - dd]);
-                }
-                sa[cur ^ 1][0][tid] = b0; sa[cur ^ 1][1][tid] = b1;
-                sq[cur ^ 1][0][tid] = (unsigned char)e0; sq[cur ^ 1][1][tid] = (unsigned char)e1;
-                sb[cur ^ 1][tid] = bb;
-                cur ^= 1;
-                __syncthreads();
-            }
-            const D kend = k0 + sa[cur][par][tid];
-            const bool leave = kend >= (D(1) << (FP::M + 1)) || sb[cur][tid] <= tid;
+            // inclusive scan: F_t = f_0 then ... then f_t
+            const MTr<D> inc = mtr_block_scan<D>(MTr<D>{a0, a1, q0, q1, fb}, wt, FP::SAT);
+            sa[0][tid] = inc.a0;
+            sa[1][tid] = inc.a1;
+            const D kend = k0 + (par ? inc.a1 : inc.a0);
+            const bool leave = kend >= (D(1) << (FP::M + 1)) || inc.fb <= tid;
             if (tid == 0) s_first = MX_T;
             __syncthreads();
             if (leave) atomicMin(&s_first, tid);
             __syncthreads();
             const int f = min(s_first, cnt);
             if (tid == 0) {
-                const D kf = f == 0 ? k0 : k0 + sa[cur][par][f - 1];
+                const D kf = f == 0 ? k0 : k0 + sa[par][f - 1];
                 s_sum = FP::mul((T)kf, FP::pow2(E - FP::BIAS - FP::M));   // k * u, exact
                 s_c = c + f;
             }
@@ -456,16 +540,81 @@ __global__ __launch_bounds__(MX_T) void med_compose_kernel(const T* __restrict__
             __syncthreads();
         }
         if (serial) {
+            // chunk cs element by element -- in parallel while the sum stays in a binade: two elements per
+            // thread, their transducers scanned; the thread whose piece leaves the binade (or that holds an
+            // element no transducer takes) adds its two elements exactly, and the rest of the chunk goes on in
+            // the new binade.  A sum that is not a positive normal, or a chunk that needs more than 8 such
+            // rounds, is finished by one lane, exactly as the reference.
             const long long cs = s_c;
             const int m = (int)min((long long)MC, n - cs * MC);
             for (int i = tid; i < m; i += MX_T) buf[i] = x[cs * MC + i];
+            if (tid == 0) s_i = 0;
             __syncthreads();
-            if (tid == 0) {
-                T s2 = s_sum;
-                for (int i = 0; i < m; i++) s2 = FP::add(s2, buf[i]);
-                s_sum = s2;
-                s_c = cs + 1;
+            for (int it = 0;; it++) {
+                const int i0 = s_i;
+                if (i0 >= m) break;
+                const T s0 = s_sum;
+                if (FP::bits(s0) == 0) {                            // +0 + (+-0) = +0: up to the first other
+                    if (tid == 0) s_first = MC;
+                    __syncthreads();
+                    for (int i = i0 + tid; i < m; i += MX_T)
+                        if ((FP::bits(buf[i]) << 1) != 0) atomicMin(&s_first, i);
+                    __syncthreads();
+                    if (tid == 0) {
+                        const int fz = s_first;
+                        if (fz < m) { s_sum = FP::add(s0, buf[fz]); s_i = fz + 1; }
+                        else s_i = m;
+                    }
+                    __syncthreads();
+                    continue;
+                }
+                if (!(s0 >= FP::smin() && s0 < FP::smax()) || it >= 8) {
+                    if (tid == 0) {
+                        T s2 = s0;
+                        for (int i = i0; i < m; i++) s2 = FP::add(s2, buf[i]);
+                        s_sum = s2;
+                        s_i = m;
+                    }
+                    __syncthreads();
+                    break;
+                }
+                const U sb2 = FP::bits(s0);
+                const int E = FP::expo(s0);
+                const D k0 = (D)((sb2 & ((U(1) << FP::M) - 1)) | (U(1) << FP::M));
+                const int par = (int)(k0 & 1);
+                const int j = i0 + 2 * tid;
+                const int cnt2 = max(0, min(2, m - j));
+                T v2[2] = {cnt2 > 0 ? buf[j] : (T)0, cnt2 > 1 ? buf[j + 1] : (T)0};
+                D a0 = 0, a1 = 0;
+                int q0 = 0, q1 = 1;
+                bool bad = false;
+                if (cnt2 > 0) trans_elems<T, 2>(v2, cnt2, E, a0, a1, q0, q1, bad);
+                const MTr<D> inc = mtr_block_scan<D>(MTr<D>{a0, a1, q0, q1, bad ? tid : MX_T}, wt, FP::SAT);
+                sa[0][tid] = inc.a0;
+                sa[1][tid] = inc.a1;
+                const int nth = (m - i0 + 1) / 2;                   // threads holding elements
+                const bool leave = tid < nth && (k0 + (par ? inc.a1 : inc.a0) >= (D(1) << (FP::M + 1)) || inc.fb <= tid);
+                if (tid == 0) s_first = MX_T;
+                __syncthreads();
+                if (leave) atomicMin(&s_first, tid);
+                __syncthreads();
+                const int f = s_first;
+                if (tid == 0) {
+                    const T u = FP::pow2(E - FP::BIAS - FP::M);
+                    if (f >= nth) {                                 // the rest of the chunk stays in the binade
+                        s_sum = FP::mul((T)(k0 + sa[par][nth - 1]), u);
+                        s_i = m;
+                    } else {                                        // thread f's two elements, exactly
+                        T s2 = FP::mul((T)(f == 0 ? k0 : k0 + sa[par][f - 1]), u);
+                        const int jf = i0 + 2 * f;
+                        for (int i = jf; i < min(m, jf + 2); i++) s2 = FP::add(s2, buf[i]);
+                        s_sum = s2;
+                        s_i = min(m, jf + 2);
+                    }
+                }
+                __syncthreads();
             }
+            if (tid == 0) s_c = cs + 1;
             __syncthreads();
         }
     }
