@@ -1007,11 +1007,9 @@ static void dbg_dump(const Dec3Bufs* D3) {
     (void)hipStreamDestroy(s2);
 }
 
-extern "C" int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
-                                 const Params* P, const Dec3Bufs* D3, float* out, long long num, uint32_t epoch,
-                                 int dense, hipStream_t st) {
-    // resident grids per (CT, segment length, buffer) instantiation: every job of a call must be resident at
-    // once (parse3's link wait, decode3's history wait), so each grid is sized from its own kernel's occupancy
+// resident grids per (CT, segment length, buffer) instantiation: every job of a call must be resident at once
+// (parse3's link wait, decode3's history wait), so each grid is sized from its own kernel's occupancy
+static int decode3_grids(const Params* P, const Dec3Bufs* D3, int dense, int* g1_out, int* g3_out) {
     static int gp[3][12], gd[2][3][12];
     const int ci = (P->ct > 0 && P->ct < 12) ? P->ct : 0;
     if (D3->seg != 4 && D3->seg != 8 && D3->seg != 16) return -2;
@@ -1048,6 +1046,16 @@ extern "C" int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev
         if (p3cap > 0) g1 = std::min(g1, p3cap * ncu);
         if (d3cap > 0) g3 = std::min(g3, d3cap * ncu);
     }
+    *g1_out = g1;
+    *g3_out = g3;
+    return 0;
+}
+
+extern "C" int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                                 const Params* P, const Dec3Bufs* D3, float* out, long long num, uint32_t epoch,
+                                 int dense, hipStream_t st) {
+    int g1 = 0, g3 = 0;
+    if (decode3_grids(P, D3, dense, &g1, &g3)) return -2;
     dc_mark_phase(4, st);
     DC_DISPATCH_3(P->ct, D3->seg, parse3_kernel, dim3(g1), dim3(64), 0, st, s, *P, *D3, dev_nbits, host_nbits, num, epoch);
     dbg_wait("parse3_kernel", st);
@@ -1058,6 +1066,17 @@ extern "C" int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev
     if (getenv("DC_DEC3_DEBUG") && hipStreamQuery(st) != hipSuccess) dbg_dump(D3);
     dc_mark_phase(7, st);
     dc_mark_next_set();
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// decode3 alone, after a parse that filled rec / rel / ptot another way (dc_launch_maps_parse)
+extern "C" int dc_launch_decode3_values(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                                        const Params* P, const Dec3Bufs* D3, float* out, long long num, uint32_t epoch,
+                                        int dense, hipStream_t st) {
+    int g1 = 0, g3 = 0;
+    if (decode3_grids(P, D3, dense, &g1, &g3)) return -2;
+    if (dense) launch_decode3_cap<D3_CAP_DENSE>(P->ct, D3->seg, g3, st, s, *P, *D3, dev_nbits, host_nbits, out, num, epoch);
+    else launch_decode3_cap<D3_CAP>(P->ct, D3->seg, g3, st, s, *P, *D3, dev_nbits, host_nbits, out, num, epoch);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

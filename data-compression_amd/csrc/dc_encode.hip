@@ -866,6 +866,13 @@ __device__ void enc_scanner(uint64_t* __restrict__ st, unsigned ntiles, uint32_t
 #ifndef DC_STORE_U
 #define DC_STORE_U 1                    // (A/B) words per thread per store round: 4 and 8 measured equal, off
 #endif
+// After the pack only wave 0 has work left that needs the tile's offset (the look-back, then the stores):
+// waves 1-3 end there, and their registers and wave slots take the next tile's waves while wave 0 waits for
+// its look-back round trip (the workgroup's LDS is held until wave 0 ends: 9 tiles per CU by LDS, 7 by
+// registers with every wave resident)
+#ifndef DC_ENC_EARLY_EXIT
+#define DC_ENC_EARLY_EXIT 1
+#endif
 // CRC (dc_encode_crc_device, the CT9 sender): the raw CRC-32 of the words a tile stores is XOR-ed into the 16 KiB
 // block accumulators cblk (dc_device.h's fused CRC; crcf_final_kernel turns them into the stream's zlib CRC):
 // thread k takes the 16-word group q0 + k of the stream's word grid (q0 = the group of the tile's first word),
@@ -1032,6 +1039,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
         if (lane == 63) s_ti[wid] = 0xFFFFFFFFu;
     }
     __syncthreads();
+    if (DC_ENC_EARLY_EXIT && wid != 0) return;                            // (no barrier after this one)
     // ---- wave 0: the waves' boundary words, then the look-back for the tile's offset
     if (wid == 0) {
         // the predecessor's last bits are requested before the look-back (published with its aggregate,
@@ -1111,7 +1119,8 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
             }
         }
     }
-    __syncthreads();
+    if (DC_ENC_EARLY_EXIT) __builtin_amdgcn_wave_barrier();               // (lane 0's LDS words, same wave)
+    else __syncthreads();
     if (!s_ok) return;                                                    // no offset: nothing stored
     // ---- store the words from the one holding the tile's first bit to its last full one
     const unsigned long long Gt = s_G;
@@ -1140,7 +1149,8 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
         }
     }
 #else
-    for (int i = tid; i < nw; i += ENC_TPB) {
+    constexpr int SW = DC_ENC_EARLY_EXIT ? 64 : ENC_TPB;                    // the storing threads
+    for (int i = DC_ENC_EARLY_EXIT ? lane : tid; i < nw; i += SW) {
         const uint32_t cur = i < tw ? sb[i] : 0u;                          // (stale past the tile's bits)
         const uint32_t prev = i ? sb[i - 1] : tp0;
         const uint32_t w = sh ? __builtin_amdgcn_alignbit(prev, cur, sh) : cur;
@@ -1158,7 +1168,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
         const int ng = (int)(((W0 + nw + 15) >> 4) - q0);
         const long long b0 = q0 >> 8;
         uint32_t vb[3] = {0u, 0u, 0u};
-        for (int k = tid; k < ng; k += ENC_TPB) {
+        for (int k = DC_ENC_EARLY_EXIT ? lane : tid; k < ng; k += SW) {
             const long long q = q0 + k;
             uint32_t r = 0;
 #pragma unroll 4
@@ -1183,11 +1193,18 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
 #pragma unroll
             for (int d = 32; d >= 1; d >>= 1) vb[j] ^= __shfl_xor(vb[j], d, 64);
         }
-        if (lane == 0) { cred[wid] = vb[0]; cred[4 + wid] = vb[1]; cred[8 + wid] = vb[2]; }
-        __syncthreads();
-        if (tid < 3) {
-            const uint32_t v = cred[4 * tid] ^ cred[4 * tid + 1] ^ cred[4 * tid + 2] ^ cred[4 * tid + 3];
-            if (v) atomicXor(cblk + b0 + tid, v);
+        if (DC_ENC_EARLY_EXIT) {
+            if (lane < 3) {
+                const uint32_t v = lane == 0 ? vb[0] : (lane == 1 ? vb[1] : vb[2]);
+                if (v) atomicXor(cblk + b0 + lane, v);
+            }
+        } else {
+            if (lane == 0) { cred[wid] = vb[0]; cred[4 + wid] = vb[1]; cred[8 + wid] = vb[2]; }
+            __syncthreads();
+            if (tid < 3) {
+                const uint32_t v = cred[4 * tid] ^ cred[4 * tid + 1] ^ cred[4 * tid + 2] ^ cred[4 * tid + 3];
+                if (v) atomicXor(cblk + b0 + tid, v);
+            }
         }
     }
     E1STAMP(5);

@@ -77,6 +77,9 @@ typedef struct {
     int dec3_dense;                  /* ... with the dense job buffer (dc_launch_decode3's `dense`) */
     int dense_key;                   /* ct * 256 + bound exponent of the last stream found dense (+1; 0: none):
                                         later decodes with the same parameters start with the dense buffer */
+    int dec3_maps;                   /* the pending segment decode parsed by entry -> exit maps */
+    int maps_key;                    /* as dense_key, for streams whose parse paths did not meet */
+    void* maps_scr; size_t maps_scr_cap;
     int halo_async;                  /* dc_halo_decode_device without dc_decode_finish (dc_set_halo_async) */
     int runs_used;                   /* the pending decode ran the small-stream decoder (dc_decode_runs.hip) */
     int runs_last;                   /* the last finished decode's values came from it */
@@ -732,6 +735,7 @@ static long long dec3_min_bytes(void) {
 }
 /* < -1: the default; -1 disables the segment decoder; returns the previous value */
 int dc_last_decode_was_v3(void) { return G.dec3_last; }
+int dc_last_decode_used_maps(void) { return G.dec3_last && G.dec3_maps; }
 int dc_last_decode_was_runs(void) { return G.runs_last; }
 int dc_set_halo_async(int on) {
     const int old = G.halo_async;
@@ -763,6 +767,33 @@ long long dc_set_decode3_min_bytes(long long v) {
 
 #define DEC_ROUNDS 3
 #define DEC_FIX_ITERS 3
+
+/* tests: every segment decode parsed by maps (DC_DEC3_MAPS=1 or dc_set_decode3_maps(1)) */
+static int g_maps_force = -1;
+static int maps_forced(void) {
+    if (g_maps_force < 0) g_maps_force = (getenv("DC_DEC3_MAPS") && *getenv("DC_DEC3_MAPS") == '1') ? 1 : 0;
+    return g_maps_force;
+}
+int dc_set_decode3_maps(int on) {
+    const int old = maps_forced();
+    g_maps_force = on ? 1 : 0;
+    return old;
+}
+/* the segment decoder's launch for the pending decode: parse3 + decode3, or the maps parse + decode3
+   (G.dec3_maps), with the job buffer G.dec3_dense picks */
+static int dec3_launch(const uint8_t* s, const Params* P, float* out, long long num) {
+    if (G.dec3_maps) {
+        const size_t need = (size_t)dc_maps_scratch_bytes(G.D3.max_chunks);
+        if (grow(&G.maps_scr, &G.maps_scr_cap, need)) return DC_ERR_HIP;
+        if (dc_launch_maps_parse(s, G.dec_dnbits, G.dec_hnbits, P, &G.D3, num, G.maps_scr, G.st) ||
+            dc_launch_decode3_values(s, G.dec_dnbits, G.dec_hnbits, P, &G.D3, out, num, G.dec_epoch, G.dec3_dense, G.st))
+            return seterr(DC_ERR_HIP, "decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+        return DC_OK;
+    }
+    if (dc_launch_decode3(s, G.dec_dnbits, G.dec_hnbits, P, &G.D3, out, num, G.dec_epoch, G.dec3_dense, G.st))
+        return seterr(DC_ERR_HIP, "decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+    return DC_OK;
+}
 
 /* halo: a Himeno halo plane (dc_halo_decode_device): the small-stream decoder up to its chunk limit */
 static int decode_device_h(int ct, const void* d_stream, long long nbytes, const unsigned long long* d_nbits,
@@ -820,9 +851,9 @@ static int decode_device_h(int ct, const void* d_stream, long long nbytes, const
            these parameters was) takes the 2080-value instantiation */
         G.dec3_dense = (nbytes >= 0 && nbytes * 8 < 18 * num && (ct == 6 || nbytes * 8 >= 6 * num)) ||
                        G.dense_key == ct * 256 + P.B + 1;                /* (not runs mode: < 6 bits per value) */
-        if (dc_launch_decode3((const uint8_t*)d_stream, G.dec_dnbits, G.dec_hnbits, &P, &G.D3, (float*)d_out, num,
-                              G.dec_epoch, G.dec3_dense, G.st))
-            return seterr(DC_ERR_HIP, "decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+        /* a stream of these parameters whose parse paths did not meet last time: the maps parse at once */
+        G.dec3_maps = G.maps_key == ct * 256 + P.B + 1 || maps_forced();
+        if ((rc = dec3_launch((const uint8_t*)d_stream, &P, (float*)d_out, num))) return rc;
     } else if (DV(dc_launch_decode_fast)((const uint8_t*)d_stream, G.dec_dnbits, G.dec_hnbits, max_chunks, &P, &G.D,
                                          (float*)d_out, num, G.dec_epoch, G.st))
         return seterr(DC_ERR_HIP, "decode launch failed: %s", hipGetErrorString(hipGetLastError()));
@@ -970,18 +1001,25 @@ static int decode_finish_body(void) {
         return seterr(DC_ERR_STREAM, "decoder status 0x%x over %d queued decodes: an earlier decode left the fast "
                                      "path and was not completed (call dc_decode_finish after each decode)", err, queued);
     }
-    if ((err & 512u) && (err & 8192u) && !(err & (1024u | 2048u | 4096u | 16384u | 65536u)) && G.dec_pending &&
-        G.dec3_used && !G.runs_used && !G.dec3_dense && !G.dec_shard) {
-        /* only a job denser than the 1040-value buffer declined: decode again with the dense instantiation
-           (2080 values per job), and start later decodes of these parameters with it */
-        if (getenv("DC_DEBUG_ERR")) fprintf(stderr, "[dcamd] dense stream (status 0x%x): dense segment decoder\n", err);
+    /* segment-decoder declines it recovers from itself: a job denser than the 1040-value buffer (the 2080-value
+       instantiation) and parse paths that did not meet (the maps parse); each is remembered per (CT, bound),
+       so later decodes of such streams start with it */
+    for (int r = 0; r < 2; r++) {
+        if (!((err & 512u) && G.dec_pending && G.dec3_used && !G.runs_used && !G.dec_shard)) break;
+        if (err & (1024u | 4096u | 16384u | 65536u)) break;       /* runs mode, short, sentinel, shard: other paths */
+        const int want_maps = G.dec3_maps || (err & 2048u) != 0;
+        const int want_dense = G.dec3_dense || (err & 8192u) != 0;
+        if (want_maps == G.dec3_maps && want_dense == G.dec3_dense) break;
+        if (getenv("DC_DEBUG_ERR"))
+            fprintf(stderr, "[dcamd] segment decoder declined (status 0x%x): again with%s%s\n", err,
+                    want_maps ? " the maps parse" : "", want_dense ? " the dense job buffer" : "");
         HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
         if ((rc = dec_next_epoch())) return rc;
-        G.dense_key = G.dec_P.ct * 256 + G.dec_P.B + 1;
-        G.dec3_dense = 1;
-        if (dc_launch_decode3(G.dec_s, G.dec_dnbits, G.dec_hnbits, &G.dec_P, &G.D3, G.dec_out, G.dec_num, G.dec_epoch, 1,
-                              G.st))
-            return seterr(DC_ERR_HIP, "decode launch failed");
+        if (want_dense) G.dense_key = G.dec_P.ct * 256 + G.dec_P.B + 1;
+        if (want_maps) G.maps_key = G.dec_P.ct * 256 + G.dec_P.B + 1;
+        G.dec3_dense = want_dense;
+        G.dec3_maps = want_maps;
+        if ((rc = dec3_launch(G.dec_s, &G.dec_P, G.dec_out, G.dec_num))) return rc;
         rc = read_dec_err(&err);
         if (rc) return rc;
     }

@@ -142,6 +142,15 @@ int dc_launch_decode_runs(const uint8_t* s, const unsigned long long* dev_nbits,
                           long long max_chunks, const DC_NS Params* P, uint8_t* maps, unsigned* err, float* out,
                           long long num, dc_hip_stream st);
 long long dc_decode_runs_max_chunks(void);
+/* the maps parse of streams whose token paths merge slowly (dc_decode_maps.hip): fills D3's rec / rel / ptot
+   as parse3 would, for dc_launch_decode3_values; scratch: dc_maps_scratch_bytes(max_chunks) bytes */
+long long dc_maps_scratch_bytes(long long max_chunks);
+int dc_launch_maps_parse(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                         const DC_NS Params* P, const DC_NS Dec3Bufs* D3, long long num, void* scratch,
+                         dc_hip_stream st);
+int dc_launch_decode3_values(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                             const DC_NS Params* P, const DC_NS Dec3Bufs* D3, float* out, long long num, uint32_t epoch,
+                             int dense, dc_hip_stream st);
 size_t dc_decode_runs_scratch_bytes(void);
 int dc_decode3_seg(long long max_chunks, int B, int ct);
 long long dc_ct1_tiles(long long n);

@@ -223,6 +223,11 @@ long long dc_set_decode3_min_bytes(long long min_bytes);
 int dc_set_decode3_seg(int seg);
 /* 1 if the last decode's values came from the segment decoder (after dc_decode_finish). */
 int dc_last_decode_was_v3(void);
+/* 1: the last finished decode's values came from the segment decoder after the maps parse (a stream whose
+ * parse paths merge slowly: noisy ramps, smooth data at small bounds, CT11 without 3-bit codes) */
+int dc_last_decode_used_maps(void);
+/* tests: 1 = parse every segment decode by maps (returns the previous setting) */
+int dc_set_decode3_maps(int on);
 /* Streams of at most this capacity (bytes) decode with the small-stream decoder (dc_decode_runs.hip: chunk
  * entry maps composed by a scan, one workgroup), unless dc_set_decode3_min_bytes(0) forces the segment
  * decoder; Himeno halo planes take it whatever their capacity (< -1: the default, 16 KiB + 256: 2^12 floats; -1:

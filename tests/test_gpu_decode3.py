@@ -239,3 +239,62 @@ def test_decode3_dense_streams(v3, oracle, ct, lg):
         assert nb * 8 < 18 * n                                    # (the case is dense)
     finally:
         v3.set_bound(1e-3)
+
+
+@pytest.fixture
+def v3maps(dc):
+    old = dc.set_decode3_min_bytes(0)
+    oldm = dc.L.dc_set_decode3_maps(1)             # every stream parsed by entry -> exit maps
+    yield dc
+    dc.L.dc_set_decode3_maps(oldm)
+    dc.set_decode3_min_bytes(old)
+
+
+@pytest.mark.parametrize("bound", BOUNDS)
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("ct", CTS)
+def test_maps_parse_golden(v3maps, oracle, bound, case, ct):
+    """The maps parse (dc_decode_maps.hip) in place of parse3 on every golden stream: the segment decoder's values
+    from its records equal the grammar decoder (runs-mode streams decline to the other decoders as before)."""
+    g = golden(bound)
+    v3maps.set_bound(bound)
+    s = g[f"{case}/ct{ct}/stream"]
+    n = g[f"{case}/input"].size
+    t, m17 = int(g[f"{case}/type"]), int(g[f"{case}/mask17"])
+    out = v3maps.decompress(ct, s, n, t, m17)
+    spec, _ = oracle.decompress(ct, s, n, bound, t, m17)
+    assert np.array_equal(out.view(np.uint32), spec.view(np.uint32))
+
+
+def _slow_sync(kind, n):
+    i = np.arange(n, dtype=np.float64)
+    if kind == "sine":
+        x = np.sin(i * 1e-3) * 50.0 + np.sin(i * 0.37) * 0.5
+    elif kind == "normal":
+        x = np.random.default_rng(1).standard_normal(n)
+    else:                                          # a noisy ramp
+        x = i * 1e-4 + np.random.default_rng(2).random(n) * 1e-2
+    x = x.astype(np.float32)
+    return x - x.min()
+
+
+@pytest.mark.parametrize("ct,kind,bound", [(7, "ramp", 1e-3), (5, "ramp", 1e-3), (7, "sine", 1e-5), (5, "sine", 1e-5),
+                                           (11, "normal", 1e-3), (6, "sine", 1e-5)])
+@pytest.mark.parametrize("lg", [16, 20])
+def test_slow_sync_streams(v3, oracle, ct, kind, bound, lg):
+    """Streams whose parse paths merge slowly (tools/experiments/sync_kinds.py: 20-200 kbit) stay on the segment
+    decoder: parse3 declines them (paths not met) and dc_decode_finish parses them by maps; the values equal the
+    grammar decoder.  Decoded twice: the second decode of the same parameters starts with the maps parse."""
+    v3.set_bound(bound)
+    try:
+        n = 1 << lg
+        xs = _slow_sync(kind, n)
+        t, m17 = oracle.type_mask(xs)
+        s, nb, _ = oracle.compress(ct, xs, bound, t, m17)
+        ref, _ = oracle.decompress(ct, s, n, bound, t, m17)
+        for _ in range(2):
+            out = v3.decompress(ct, s, n, t, m17)
+            assert np.array_equal(out.view(np.uint32), ref.view(np.uint32))
+            assert v3.L.dc_last_decode_was_v3()
+    finally:
+        v3.set_bound(1e-3)
