@@ -188,6 +188,7 @@ def halo_bench(args):
             L.halo_decode_device(ct, rs.data_ptr(), (rb + 7) // 8, 0, 0, 0, rmins.data_ptr() + 4 * i,
                                  q.data_ptr(), (mi, mj, mk), 3, kk, (imax, jmax, kmax))
 
+    torch.cuda.synchronize()                        # (the fills above run on torch's stream)
     for _ in range(max(args.warmup, 1)):
         step()
     L.synchronize()
@@ -222,6 +223,7 @@ def halo_bench(args):
             sn = torch.zeros(cap, dtype=torch.uint8, device=dev)
             bn = torch.zeros(1, dtype=torch.int64, device=dev)
             mnn = torch.zeros(1, dtype=torch.float32, device=dev)
+            torch.cuda.synchronize()
             L.halo_encode_device(ct, pn.data_ptr(), (mi, mj, mk), 3, planes[h], (imax, jmax, kmax), sn.data_ptr(),
                                  bn.data_ptr(), mnn.data_ptr())
             L.synchronize()
@@ -1002,14 +1004,30 @@ def e2e_run(C, W, steps, warmup):
     idx0 = C.rank * n
     slot = [(cap + 8 + 3) // 4 * 4]
 
+    dbg = [bool(os.environ.get("DC_BENCH_DEBUG"))]
+
+    def show(what):
+        if dbg[0]:
+            L.synchronize()
+            torch.cuda.synchronize()
+            print(f"e2e rank {C.rank} {what}: count {int(d_count.item())} total {int(d_total.item())} enc "
+                  f"{L.encode_status()} dec {L.decode_status()}", file=sys.stderr, flush=True)
+
     def step():
         L.encode_device(ct, xs.data_ptr(), n, local.data_ptr(), idx0=idx0, type_=typ, mask17=mask17, start_bit=0,
                         total_ptr=d_count.data_ptr())
+        show("after encode")
         dcamd.gather_stream_device(L, local, d_count, slot[0], glob, d_total)
+        show("after gather")
         dcamd.decode_sharded_device(L, ct, local, d_count, (cap + 64) // 16 * 16, n, out, typ, mask17)
+        show("after decode")
 
+    # the zero fills above are queued on torch's stream, the steps on the library's: without this a fill
+    # could land after the first encode wrote its bit count (seen with two ranks sharing one GPU)
+    torch.cuda.synchronize()
     for _ in range(max(warmup, 1)):
         step()
+    dbg[0] = False
     L.synchronize()
     torch.cuda.synchronize()
     # the slot for the timed steps: the warm-up's largest shard (a real run takes the previous step's)

@@ -714,14 +714,27 @@ __global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict_
         }
         P3_T(u3);
         P3_ADD(10, u3 - u2);
-        // ---- pending prefixes, lane by lane in stream order (rare)
+        // ---- pending prefixes, in rounds: a lane re-decodes its prefix once no lane before it still holds an
+        // unresolved prefix that reaches its three history values (U: the furthest end of those prefixes) --
+        // usually every pending lane in the first round (a noisy ramp has ~40% of its chunks start with a
+        // prediction; lane by lane, that serial loop was 80% of its decode)
         unsigned long long pm = __ballot(pend > 0);
         P3_ADD(14, __popcll(pm));
         P3_ADD(15, Tn);
         while (pm) {
-            const int Lp = __ffsll((long long)pm) - 1;
-            pm &= pm - 1;
-            if (lane == Lp) {
+            const bool mine = ((pm >> lane) & 1ull) != 0ull;
+            int U = mine ? o0 + pend : -(1 << 30);
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {                          // inclusive max over lanes <= this one
+                const int u = __shfl_up(U, d, 64);
+                if (lane >= d) U = max(U, u);
+            }
+            U = __shfl_up(U, 1, 64);                                      // exclusive
+            if (lane == 0) U = -(1 << 30);
+            const bool go = mine && U <= max(o0 - 3, al);
+            pm &= ~__ballot(go);
+            __builtin_amdgcn_wave_barrier();
+            if (go) {
                 float h[3];
 #pragma unroll
                 for (int k = 1; k <= 3; k++) {

@@ -9,17 +9,18 @@
 // repairs then chain over many segments and it declines the stream (status 512 | 2048).  Those streams were
 // decoded by the chunk-map decoder, ~5 ms at 2^24 values.  Here, with no walk longer than a group:
 //
-// maps_group_kernel   256-bit chunks, 32 lanes per chunk: lane e walks the chunk from entry bit e (a token
-//                     starts on one of a chunk's first 32 bits) -> the chunk's entry -> exit map; 8 chunks a
-//                     group, whose map (the 8 maps composed) goes to gmap.  (The walk of impl/dataCompression.c's
-//                     grammar, as runs_map_kernel.)
+// maps_group_kernel   256-bit chunks, 32 lanes per chunk: every bit's next token start (a 512-entry length
+//                     table on the token's top 9 bits) into LDS, then lane e steps from entry bit e (a token
+//                     starts on one of a chunk's first 32 bits) through that table -> the chunk's entry -> exit
+//                     map and token count; 8 chunks a group, whose map (the 8 maps composed) goes to gmap and,
+//                     for each of its 32 entries, its chunks' records (entry | tokens << 8) to gtab.
 // maps_scan_kernel    1024 group maps per workgroup: an inclusive scan of the maps inside each wave (register
 //                     maps, four-entry v_perm lookups), the 16 wave totals composed; either every map's entry
 //                     from the block's entry (ent_in), or the block's total map (a first pass: the block maps,
 //                     scanned by the same kernel on one workgroup to get every block's entry).
-// maps_rec_kernel     lane = group: its 8 chunks walked once from the group's entry -> parse3's records (entry,
-//                     tokens per chunk), each decode job's first token relative to its parse job and the parse
-//                     jobs' totals -- exactly the rec / rel / ptot decode3_kernel reads.
+// maps_rec_kernel     lane = group: the gtab row of the group's entry -> parse3's records (entry, tokens per
+//                     chunk), each decode job's first token relative to its parse job and the parse jobs'
+//                     totals -- exactly the rec / rel / ptot decode3_kernel reads.
 // decode3_kernel then decodes the values as after parse3.  Every walk is bounded by its group, so the path
 // never has to meet: the maps are exact whatever the stream.
 #include "dc_device.h"
@@ -38,42 +39,71 @@ __device__ __forceinline__ uint32_t mp_word(const uint8_t* __restrict__ s, long 
     return v;
 }
 
+// (a grid of at most MP_GRID workgroups, each looping over groups: the next group's stream words are loaded while
+// the current one is walked -- one workgroup per group spent most of its life waiting for its first load)
+constexpr int MP_GRID = 4096;
 template <int CT>
 __global__ __launch_bounds__(256) void maps_group_kernel(const uint8_t* __restrict__ s, Params P,
                                                          const unsigned long long* dev_nbits, unsigned long long host_nbits,
-                                                         uint8_t* __restrict__ gmap, long long num, long long max_chunks,
-                                                         unsigned* __restrict__ err) {
+                                                         uint8_t* __restrict__ gmap, uint4* __restrict__ gtab, long long ngr,
+                                                         long long num, long long max_chunks, unsigned* __restrict__ err) {
     __shared__ uint32_t w[MP_G][10];
-    __shared__ uint8_t gx[MP_G][32];
+    __shared__ uint8_t tl[512];
+    __shared__ uint16_t nx[MP_G][256];                           // the next token's start from every bit
+    __shared__ uint8_t gx[MP_G][32], gc[MP_G][32];
     const unsigned long long nbits = dev_nbits ? *dev_nbits : host_nbits;
     const long long nch = (long long)((nbits + 255) >> 8), nbytes = (long long)((nbits + 7) >> 3);
-    const long long g0 = (long long)blockIdx.x * MP_G;
     const int h = threadIdx.x >> 5, e = threadIdx.x & 31;
     // a runs-mode stream (decode3 would take it for zero runs, which only parse3 checks) or one longer than
     // the buffers: declined to the chunk-map decoder, as parse3 declines it (status 512 | 1024)
     if (blockIdx.x == 0 && threadIdx.x == 0 && (nch > max_chunks || runs_mode(CT, nbits, num))) atomicOr(err, 512u | 1024u);
-    if (g0 >= nch) {                                             // (past the stream's end: the identity)
-        if (h == 0) gmap[blockIdx.x * 32 + e] = (uint8_t)e;
-        return;
+    build_lut_len<CT>(tl, P, threadIdx.x, 256);
+    long long gi = blockIdx.x;
+    uint32_t wv = 0u;
+    {
+        const long long c = gi * MP_G + h;
+        if (e < 10 && c < nch) wv = mp_word(s, nbytes, 8 * c + e);
     }
-    const long long c = g0 + h;
-    if (e < 10) w[h][e] = c < nch ? mp_word(s, nbytes, 8 * c + e) : 0u;
-    __syncthreads();
-    const int lim = c < nch ? (int)min(256ll, (long long)nbits - 256 * c) : 0;
-    int pos = e;
-    while (pos < lim) {
-        const int wi = pos >> 5, sh = pos & 31;
-        const uint32_t t = sh ? __builtin_amdgcn_alignbit(w[h][wi], w[h][wi + 1], 32 - sh) : w[h][wi];
-        if (CT != 6 && (int)t < 0) pos += 3 * run3i(t, pos, lim);
-        else pos += token_len_bf<CT>(t, P);
-    }
-    gx[h][e] = c < nch ? (uint8_t)((pos - 256) & 31) : (uint8_t)e;   // (identity past the stream's end)
-    __syncthreads();
-    if (h == 0) {
-        int x = e;
+    for (; gi < ngr; gi += gridDim.x) {
+        const long long c = gi * MP_G + h;
+        __syncthreads();                                         // (the previous group's LDS reads are done)
+        if (e < 10) w[h][e] = wv;
+        {
+            const long long cn = (gi + gridDim.x) * MP_G + h;
+            wv = (e < 10 && cn < nch) ? mp_word(s, nbytes, 8 * cn + e) : 0u;
+        }
+        if (gi * MP_G >= nch) {                                  // (past the stream's end: the identity)
+            if (h == 0) gmap[gi * 32 + e] = (uint8_t)e;
+            continue;
+        }
+        __syncthreads();
+        // every bit's next token start (8 independent table lookups per lane instead of a token decode per
+        // step of each of the 32 walks)
 #pragma unroll
-        for (int j = 0; j < MP_G; j++) x = gx[j][x];
-        gmap[blockIdx.x * 32 + e] = (uint8_t)x;
+        for (int k = 0; k < 8; k++) {
+            const int p = e + 32 * k;
+            const uint32_t t = e ? __builtin_amdgcn_alignbit(w[h][k], w[h][k + 1], 32 - e) : w[h][k];
+            nx[h][p] = (uint16_t)(p + tl[t >> 23]);
+        }
+        __syncthreads();
+        const int lim = c < nch ? (int)min(256ll, (long long)nbits - 256 * c) : 0;
+        int pos = e, cnt = 0;
+        while (pos < lim) { pos = nx[h][pos]; cnt++; }             // (tokens starting before lim)
+        gx[h][e] = c < nch ? (uint8_t)((pos - 256) & 31) : (uint8_t)e;   // (identity past the stream's end)
+        gc[h][e] = (uint8_t)cnt;
+        __syncthreads();
+        if (h == 0) {
+            // from group entry e: the group's exit, and its chunks' records (entry | tokens << 8) for maps_rec_kernel
+            int x = e;
+            uint32_t r[MP_G / 2] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int j = 0; j < MP_G; j++) {
+                r[j >> 1] |= ((uint32_t)x | ((uint32_t)gc[j][x] << 8)) << (16 * (j & 1));
+                x = gx[j][x];
+            }
+            gmap[gi * 32 + e] = (uint8_t)x;
+            gtab[gi * 32 + e] = make_uint4(r[0], r[1], r[2], r[3]);
+        }
     }
 }
 
@@ -177,56 +207,27 @@ __global__ __launch_bounds__(MP_B) void maps_scan_kernel(const uint8_t* __restri
     (void)own;
 }
 
-// lane = group: its chunks from the group's entry -> rec (entry | tokens << 8), the tokens of each decode job
-// (64 chunks = 8 groups) and of each parse job (seg decode jobs): rel[decode job] = tokens before it in its
-// parse job, ptot[parse job]
-template <int CT>
-__global__ __launch_bounds__(MP_B) void maps_rec_kernel(const uint8_t* __restrict__ s, Params P,
-                                                       const unsigned long long* dev_nbits, unsigned long long host_nbits,
-                                                       const uint8_t* __restrict__ gent, Dec3Bufs D3) {
+// lane = group: its chunks' records (entry | tokens << 8) for the group's entry, from the group kernel's table ->
+// rec, the tokens of each decode job (64 chunks = 8 groups) and of each parse job (seg decode jobs): rel[decode
+// job] = tokens before it in its parse job, ptot[parse job]
+__global__ __launch_bounds__(MP_B) void maps_rec_kernel(const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                                                       const uint8_t* __restrict__ gent, const uint4* __restrict__ gtab,
+                                                       Dec3Bufs D3) {
     __shared__ uint32_t djt[MP_B / 8];                           // tokens per decode job
     const unsigned long long nbits = dev_nbits ? *dev_nbits : host_nbits;
-    const long long nch = (long long)((nbits + 255) >> 8), nbytes = (long long)((nbits + 7) >> 3);
+    const long long nch = (long long)((nbits + 255) >> 8);
     const long long g = (long long)blockIdx.x * MP_B + threadIdx.x, c0 = g * MP_G;
     if ((long long)blockIdx.x * MP_B * MP_G >= nch) return;
     uint32_t tot = 0;
     if (c0 < nch) {
-        long long pos = c0 * 256 + gent[g];
-        uint32_t w0 = mp_word(s, nbytes, pos >> 5), w1 = mp_word(s, nbytes, (pos >> 5) + 1);
-        long long wi = pos >> 5;
-        uint32_t rec[MP_G / 2];
-#pragma unroll
-        for (int j = 0; j < MP_G / 2; j++) rec[j] = 0u;
-#pragma unroll
-        for (int j = 0; j < MP_G; j++) {
-            const long long c = c0 + j;
-            uint32_t cnt = 0, ent = (uint32_t)(pos - 256 * c) & 31u;
-            const long long lim = min(256 * (c + 1), (long long)nbits);
-            while (pos < lim) {
-                if ((pos >> 5) != wi) {                          // the window follows pos
-                    const long long nw = pos >> 5;
-                    w0 = nw == wi + 1 ? w1 : mp_word(s, nbytes, nw);
-                    w1 = mp_word(s, nbytes, nw + 1);
-                    wi = nw;
-                }
-                const int sh = (int)(pos & 31);
-                const uint32_t t = sh ? __builtin_amdgcn_alignbit(w0, w1, 32 - sh) : w0;
-                if (CT != 6 && (int)t < 0) {
-                    const int k = run3i(t, 0, (int)min(32ll, lim - pos));       // (tokens starting before lim)
-                    pos += 3 * k;
-                    cnt += (uint32_t)k;
-                } else {
-                    pos += token_len_bf<CT>(t, P);
-                    cnt++;
-                }
-            }
-            if (c < nch) rec[j >> 1] |= (ent | (cnt << 8)) << (16 * (j & 1));
-            tot += cnt;
-        }
+        const uint4 q = gtab[g * 32 + (gent[g] & 31u)];
+        const uint32_t rec[MP_G / 2] = {q.x, q.y, q.z, q.w};
         uint32_t* r32 = reinterpret_cast<uint32_t*>(D3.rec);
 #pragma unroll
-        for (int j = 0; j < MP_G / 2; j++)
-            if (c0 + 2 * j < nch) r32[(c0 >> 1) + j] = rec[j];
+        for (int j = 0; j < MP_G / 2; j++) {
+            tot += ((rec[j] >> 8) & 0xFFu) + (rec[j] >> 24);
+            if (c0 + 2 * j < nch) r32[(c0 >> 1) + j] = c0 + 2 * j + 1 < nch ? rec[j] : rec[j] & 0xFFFFu;
+        }
     }
     // decode jobs: 8 consecutive lanes
     uint32_t v = tot;
@@ -250,7 +251,7 @@ __global__ __launch_bounds__(MP_B) void maps_rec_kernel(const uint8_t* __restric
 // scratch bytes of the maps parse for streams of up to max_chunks 256-bit chunks
 extern "C" long long dc_maps_scratch_bytes(long long max_chunks) {
     const long long ngr = (max_chunks + MP_G - 1) / MP_G + MP_B, nb = ngr / MP_B + 8;
-    return ngr * 32 + ngr + nb * 32 + nb + 64;
+    return ngr * 32 + ngr + nb * 32 + nb + 64 + 16 + ngr * 32 * 16;
 }
 
 extern "C" int dc_launch_maps_parse(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
@@ -262,34 +263,30 @@ extern "C" int dc_launch_maps_parse(const uint8_t* s, const unsigned long long* 
     uint8_t* bmap = gent + ngr + MP_B;
     uint8_t* bent = bmap + (nb + 8) * 32;
     long long* cnt = reinterpret_cast<long long*>(((uintptr_t)(bent + nb + 8) + 7) & ~(uintptr_t)7);
+    uint4* gtab = reinterpret_cast<uint4*>(((uintptr_t)(cnt + 2) + 15) & ~(uintptr_t)15);   // [group][entry]
     // the group and block counts of this stream (its length may be on the device): one tiny kernel would do;
     // the scans take their counts from device memory, written here from the capacity (groups past the
     // stream's end have identity maps and are never read)
     const long long hc[2] = {ngr, nb};
     if (hipMemcpyAsync(cnt, hc, sizeof hc, hipMemcpyHostToDevice, st) != hipSuccess) return -1;
-    const dim3 gg((unsigned)ngr), gb((unsigned)nb);
+    const dim3 gg((unsigned)min(ngr, (long long)MP_GRID)), gb((unsigned)nb);
     switch (P->ct) {
 #define DC_MAPS_CASE(C)                                                                                          \
     case C:                                                                                                      \
-        hipLaunchKernelGGL(maps_group_kernel<C>, gg, dim3(256), 0, st, s, *P, dev_nbits, host_nbits, gmap, num,  \
-                           D3->max_chunks, D3->err);                                                             \
+        hipLaunchKernelGGL(maps_group_kernel<C>, gg, dim3(256), 0, st, s, *P, dev_nbits, host_nbits, gmap, gtab, \
+                           ngr, num, D3->max_chunks, D3->err);                                                      \
         break;
         DC_MAPS_CASE(5) DC_MAPS_CASE(6) DC_MAPS_CASE(7) DC_MAPS_CASE(11)
         default: return -2;
     }
     hipLaunchKernelGGL(maps_scan_kernel<1>, gb, dim3(MP_B), 0, st, gmap, cnt, nullptr, nullptr, bmap);
-    hipLaunchKernelGGL(maps_scan_kernel<MP_TOPK>, dim3(1), dim3(MP_B), 0, st, bmap, cnt + 1, nullptr, bent, nullptr);
+    if (nb <= MP_B)                                              // (the block maps: one per thread)
+        hipLaunchKernelGGL(maps_scan_kernel<1>, dim3(1), dim3(MP_B), 0, st, bmap, cnt + 1, nullptr, bent, nullptr);
+    else
+        hipLaunchKernelGGL(maps_scan_kernel<MP_TOPK>, dim3(1), dim3(MP_B), 0, st, bmap, cnt + 1, nullptr, bent, nullptr);
     hipLaunchKernelGGL(maps_scan_kernel<1>, gb, dim3(MP_B), 0, st, gmap, cnt, bent, gent, nullptr);
-    switch (P->ct) {
 #undef DC_MAPS_CASE
-#define DC_MAPS_CASE(C)                                                                                          \
-    case C:                                                                                                      \
-        hipLaunchKernelGGL(maps_rec_kernel<C>, gb, dim3(MP_B), 0, st, s, *P, dev_nbits, host_nbits, gent, *D3);  \
-        break;
-        DC_MAPS_CASE(5) DC_MAPS_CASE(6) DC_MAPS_CASE(7) DC_MAPS_CASE(11)
-#undef DC_MAPS_CASE
-        default: return -2;
-    }
+    hipLaunchKernelGGL(maps_rec_kernel, gb, dim3(MP_B), 0, st, dev_nbits, host_nbits, gent, gtab, *D3);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

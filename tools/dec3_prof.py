@@ -1,5 +1,6 @@
 """Section timing of the segment decoder (DC_DEC3_PROF build): where do parse3/decode3 spend their cycles?
-Usage on the GPU box: DCAMD_LIB=data-compression_amd/lib_p/libdcamd.so python3 tools/dec3_prof.py [ct] [log2n]"""
+Usage on the GPU box: DCAMD_LIB=data-compression_amd/lib_p/libdcamd.so python3 tools/dec3_prof.py [ct] [log2n] [bound]
+[kind: u10 | ramp | sine | normal (the slowly-synchronising streams of tools/experiments/sync_kinds.py)] [maps]"""
 import ctypes
 import os
 import sys
@@ -26,7 +27,21 @@ def main():
     L = dcamd.Lib()
     L.init(0)
     C = types.SimpleNamespace(L=L, dev=dev, rank=0, dist=None, dcamd=dcamd)
-    W = bench.prepare(C, ct, "u10", log2n, bound)
+    kind = sys.argv[4] if len(sys.argv) > 4 else "u10"
+    if len(sys.argv) > 5 and sys.argv[5] == "maps":
+        L.L.dc_set_decode3_maps(1)
+    if kind == "u10":
+        W = bench.prepare(C, ct, "u10", log2n, bound)
+    else:
+        n = 1 << log2n
+        i = np.arange(n, dtype=np.float64)
+        xh = {"sine": lambda: np.sin(i * 1e-3) * 50.0 + np.sin(i * 0.37) * 0.5,
+              "normal": lambda: np.random.default_rng(1).standard_normal(n),
+              "ramp": lambda: i * 1e-4 + np.random.default_rng(2).random(n) * 1e-2}[kind]().astype(np.float32)
+        xs = torch.from_numpy(xh - xh.min()).to(dev)
+        L.set_bound(bound)
+        mean, t = L.med_device(xs.data_ptr(), n)
+        W = {"n": n, "xs": xs, "type": t, "mask17": int(np.array([mean], np.float32).view(np.uint32)[0] >> 15)}
     n = W["n"]
     cap = L.stream_capacity(n)
     stream = torch.empty(cap, dtype=torch.uint8, device=dev)
@@ -55,7 +70,7 @@ def main():
     p = [v / reps for v in buf]
     nbits = int(d_nbits.item())
     print(f"ct {ct} n 2^{log2n} bound {bound} stream {nbits / 8e6:.1f} MB ({nbits / n:.2f} bits/value) "
-          f"v3 {L.last_decode_was_v3()} wall {wall * 1e3:.3f} ms/decode")
+          f"v3 {L.last_decode_was_v3()} maps {L.L.dc_last_decode_used_maps()} wall {wall * 1e3:.3f} ms/decode")
     pj, dj = max(p[5], 1), max(p[13], 1)
     print(f"parse: jobs {p[5]:.0f} tokens {p[4]:.0f} repair rounds {p[3]:.0f}")
     print(f"  per job (kcycles): main {p[0] / pj / 1e3:.1f} link wait {p[1] / pj / 1e3:.1f} repair {p[2] / pj / 1e3:.1f}")

@@ -49,6 +49,7 @@ for seg in segs:
     L.decode_finish()
     torch.cuda.synchronize()
     v3 = L.L.dc_last_decode_was_v3()
+    maps = L.L.dc_last_decode_used_maps()
     if ref is None:
         ref = out.clone()
     import time
@@ -58,4 +59,4 @@ for seg in segs:
         L.decode_finish()
     full = (time.perf_counter() - t0) / 5 * 1e3
     print(f"   complete decode incl. any slow path (host-synchronised): {full:.3f} ms", flush=True)
-    print(f"{kind} 2^{lg} ct{ct} bound {L.get_bound() if hasattr(L, 'get_bound') else ''} seg {seg}: decode {e0.elapsed_time(e1) * 1000 / 20:.1f} us per step, fast-path status 0x{stv:x}, v3 {v3}, same {bool(torch.equal(out, ref))}", flush=True)
+    print(f"{kind} 2^{lg} ct{ct} bound {L.get_bound() if hasattr(L, 'get_bound') else ''} seg {seg}: decode {e0.elapsed_time(e1) * 1000 / 20:.1f} us per step, fast-path status 0x{stv:x}, v3 {v3}, maps {maps}, same {bool(torch.equal(out, ref))}", flush=True)
