@@ -114,22 +114,34 @@ __global__ __launch_bounds__(256) void sub_min_kernel(const float* __restrict__ 
 // 2-state transducer for a given binade: start parity -> (units added, end parity).
 //   med_chunk_sum   : per chunk its double sum and max (all CUs)
 //   med_chunk_scan  : one workgroup: exclusive scan of the double chunk sums = an estimate of the
-//                     running sum at every chunk, whose binade E_est picks the chunk's window of
-//                     MW candidate binades [E_est - 4, E_est + 1] (the float sum stalls below the real
-//                     one, never far above it)
-//   med_chunk_trans : per chunk and candidate binade the transducer (all CUs; one pass over x)
+//                     running sum at every chunk, whose binade E_est centres the chunk's window of
+//                     candidate binades
+//   med_chunk_trans : per chunk and candidate binade the transducer (one wave per chunk, 32 elements per
+//                     lane; one pass over x)
 //   med_compose     : one workgroup: from s_init, blocks of 1024 chunks are composed with a block scan
 //                     while the running sum stays in its binade and each chunk has a valid transducer
 //                     for it; a chunk where the sum leaves the binade, or that holds an element the
 //                     transducer cannot take (negative, NaN, too large, the binade not in its window),
-//                     or a sum below SMIN, is added element by element by one lane, exactly like the
-//                     reference.  At 2^26 U10: about 25 such chunks (the binade crossings).
+//                     or a sum below SMIN, is added element by element, exactly like the reference.
+//                     At 2^26 U10: about 25 such chunks (the binade crossings).  The chunk records come
+//                     from an LDS ring refilled ahead of the blocks (a block that restarts after a
+//                     crossing finds them there instead of waiting for its loads again).
+// Windows: the narrow one, [E_est - 1, E_est + 1], is tried first (the float sum's binade at every chunk
+// boundary lies there for U10, ramps, sines, normals, ones and small uniforms up to 2^26: a stalling sum falls
+// one binade behind the double estimate, a rounding-up one one ahead); a compose that meets more than
+// MED_MISS_MAX chunks outside it stops and raises the scratch flag, and the host runs the wide window
+// [E_est - 4, E_est + 1] from the start (dc_launch_med_wide).  The multi-GPU shard records (med_shard_kernel)
+// use the wide window.
 // The same kernels run med_dataset_double (:3564-3590) with u = 2^(E-1075) and k < 2^53 (MedFP<double>).
 constexpr int MC = 2048;                                   // elements per chunk
-constexpr int MW = 6;                                      // candidate binades per chunk
-constexpr int MC_T = 256;                                  // threads of the chunk kernels (8 elements each)
+constexpr int MW = 6;                                      // candidate binades per chunk, wide window
+constexpr int MWN = 3;                                     // narrow window
+constexpr int MC_T = 256;                                  // threads of the chunk-sum kernel (8 elements each)
 constexpr int MC_PER = MC / MC_T;
-constexpr int MX_T = 1024;                                 // compose workgroup
+constexpr int MT_PER = MC / 64;                            // transducer kernel: elements per lane
+constexpr int MX_T = 1024;                                 // chunks per compose block; med_shard workgroup
+constexpr int MED_MISS_MAX = 16;                           // narrow-window misses before the wide pass
+template <int W> __host__ __device__ constexpr int med_wlo() { return W == MW ? -4 : -1; }
 
 // float / double: the running sum's binade E (biased exponent), k = s/u in [2^M, 2^(M+1)), u = 2^(E-bias-M)
 template <typename T> struct MedFP;
@@ -180,11 +192,15 @@ template <typename T>
 struct MedScratch {
     double* csum;                                          // [nch] chunk sums (an estimate only)
     T* cmax;                                               // [nch] chunk max (NaN-skipping)
-    int* elo;                                              // [nch] first candidate binade
+    int* eest;                                             // [nch] E_est: the estimated running sum's binade
     typename MedFP<T>::D* Td;                              // [nch * MW * 2] units added from parity 0 / 1
     uint8_t* F;                                            // [nch * MW] end parity 0 | end parity 1 << 1 | bad << 2
     uint8_t* Z;                                            // [nch] 1: every element is +0 / -0; 2: some element
                                                            // is negative or NaN (no transducer takes the chunk)
+    long long* rec;                                        // med_shard_kernel's 21-word record
+    unsigned* flag;                                        // 1: the narrow window missed, the wide pass runs
+    long long* res;                                        // right after flag's word: mean, type, sum, max (bits)
+                                                           // -- the host reads flag + results in one copy
 };
 
 template <typename T>
@@ -202,9 +218,12 @@ __host__ __device__ inline MedScratch<T> med_scratch(void* base, long long nch) 
     m.csum = (double*)b; b += nch * 8;
     m.Td = (typename MedFP<T>::D*)b; b += nch * MW * 2 * (long long)sizeof(typename MedFP<T>::D);
     m.cmax = (T*)b; b += nch * (long long)sizeof(T);
-    m.elo = (int*)b; b += nch * 4;
+    m.eest = (int*)b; b += nch * 4;
     m.F = (uint8_t*)b; b += nch * MW;
-    m.Z = (uint8_t*)b;
+    m.Z = (uint8_t*)b; b += nch;
+    m.rec = (long long*)(((uintptr_t)b + 7) & ~(uintptr_t)7);
+    m.flag = (unsigned*)(m.rec + 24);
+    m.res = m.rec + 25;
     return m;
 }
 
@@ -224,12 +243,38 @@ __device__ __forceinline__ void load_chunk(const T* __restrict__ x, long long n,
     for (int i = 0; i < MC_PER; i++) v[i] = e0 + i < n ? x[e0 + i] : (T)0;
 }
 
+// a lane's run of N consecutive elements from e0 (16-byte loads when whole and aligned)
+template <typename T, int N>
+__device__ __forceinline__ void load_run(const T* __restrict__ x, long long n, long long e0, T* v) {
+    if (e0 + N <= n && (reinterpret_cast<uintptr_t>(x) & 15u) == 0) {
+        if (sizeof(T) == 4) {
+            const float4* p = reinterpret_cast<const float4*>(x + e0);
+#pragma unroll
+            for (int q = 0; q < N / 4; q++) {
+                const float4 a = p[q];
+                v[4 * q] = (T)a.x; v[4 * q + 1] = (T)a.y; v[4 * q + 2] = (T)a.z; v[4 * q + 3] = (T)a.w;
+            }
+        } else {
+            const double2* p = reinterpret_cast<const double2*>(x + e0);
+#pragma unroll
+            for (int q = 0; q < N / 2; q++) {
+                const double2 a = p[q];
+                v[2 * q] = (T)a.x; v[2 * q + 1] = (T)a.y;
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < N; i++) v[i] = e0 + i < n ? x[e0 + i] : (T)0;
+}
+
 template <typename T>
 __global__ __launch_bounds__(MC_T) void med_chunk_sum_kernel(const T* __restrict__ x, long long n, MedScratch<T> M) {
     typedef MedFP<T> FP;
     __shared__ double ws[MC_T / 64];
     __shared__ T wm[MC_T / 64];
     const long long c = blockIdx.x;
+    if (c == 0 && threadIdx.x == 0) *M.flag = 0u;           // (the narrow pass has not missed yet)
     T v[MC_PER];
     load_chunk(x, n, c, v);
     const long long e0 = c * MC + (long long)threadIdx.x * MC_PER;
@@ -264,45 +309,66 @@ __global__ __launch_bounds__(MC_T) void med_chunk_sum_kernel(const T* __restrict
     }
 }
 
-// exclusive scan of the chunk sums -> an estimate of the running sum at every chunk; its binade
-// E_est opens the chunk's window [E_est - 4, E_est + 1] (the float sum stalls below the real one)
+// exclusive scan of the chunk sums -> an estimate of the running sum at every chunk and its binade E_est.
+// Tiles of 8192 chunks: coalesced loads into LDS (the next tile's loads issued before this tile's scan), 8
+// consecutive chunks per thread, a block scan, the binades back through LDS and out coalesced (runs of
+// 32 chunks per thread, loaded in batches, took 37-54 us at 2^26: every load instruction spread over 64 lines).
+constexpr int MS_T = 8192;
 template <typename T>
 __global__ __launch_bounds__(1024) void med_chunk_scan_kernel(MedScratch<T> M, long long nch, T s_init) {
     typedef MedFP<T> FP;
+    __shared__ double tile[MS_T];
     __shared__ double wt[16];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const long long per = (nch + 1023) / 1024, c0 = tid * per, c1 = min(nch, c0 + per);
-    double sm = 0.0;
-    // (eight independent loads in flight per round: one dependent load after another took ~60 us at 2^26)
-    for (long long cb = c0; cb < c1; cb += 8) {
-        double t[8];
+    int* etile = reinterpret_cast<int*>(tile);              // (the binades overwrite the sums they came from)
+    double carry = (double)s_init;
+    double nx[MS_T / 1024];
 #pragma unroll
-        for (int i = 0; i < 8; i++) t[i] = cb + i < c1 ? M.csum[cb + i] : 0.0;
-#pragma unroll
-        for (int i = 0; i < 8; i++) sm += t[i];
+    for (int j = 0; j < MS_T / 1024; j++) {
+        const long long i = tid + 1024ll * j;
+        nx[j] = i < nch ? M.csum[i] : 0.0;
     }
-    double inc = sm;
+    for (long long base = 0; base < nch; base += MS_T) {
+        const int cnt = (int)min((long long)MS_T, nch - base);
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const double u = __shfl_up(inc, d, 64);
-        if (lane >= d) inc += u;
-    }
-    if (lane == 63) wt[wid] = inc;
-    __syncthreads();
-    double run = (double)s_init + inc - sm;
-    for (int w = 0; w < wid; w++) run += wt[w];
-    for (long long cb = c0; cb < c1; cb += 8) {
-        double t[8];
+        for (int j = 0; j < MS_T / 1024; j++) tile[tid + 1024 * j] = nx[j];
 #pragma unroll
-        for (int i = 0; i < 8; i++) t[i] = cb + i < c1 ? M.csum[cb + i] : 0.0;
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            if (cb + i < c1) {
-                const T est = (T)fmin(fmax(run, 0.0), (double)FP::smax());
-                M.elo[cb + i] = FP::expo(est) - 4;
-                run += t[i];
-            }
+        for (int j = 0; j < MS_T / 1024; j++) {             // (the next tile's sums, in flight meanwhile)
+            const long long i = base + MS_T + tid + 1024ll * j;
+            nx[j] = i < nch ? M.csum[i] : 0.0;
         }
+        __syncthreads();
+        double v[8], sm = 0.0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) { v[j] = tile[8 * tid + j]; sm += v[j]; }
+        double inc = sm;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const double u = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += u;
+        }
+        if (lane == 63) wt[wid] = inc;
+        __syncthreads();                                    // (every thread's sums read: tile is rewritten below)
+        double run = carry + inc - sm, tot = 0.0;
+#pragma unroll
+        for (int w = 0; w < 16; w++) { run += w < wid ? wt[w] : 0.0; tot += wt[w]; }
+        int e[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const T est = (T)fmin(fmax(run, 0.0), (double)FP::smax());
+            e[j] = FP::expo(est);
+            run += v[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) etile[8 * tid + j] = e[j];
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < MS_T / 1024; j++) {
+            const int i = tid + 1024 * j;
+            if (i < cnt) M.eest[base + i] = etile[i];
+        }
+        carry += tot;
+        __syncthreads();                                    // (etile read before the next tile's sums land)
     }
 }
 
@@ -313,7 +379,7 @@ __global__ __launch_bounds__(1024) void med_chunk_scan_kernel(MedScratch<T> M, l
 // tie's two bits and one parity are tracked, instead of both paths element by element.
 template <typename T, int N = MC_PER>
 __device__ __forceinline__ void trans_elems(const T* v, int cnt, int E, typename MedFP<T>::D& d0,
-                                            typename MedFP<T>::D& d1, int& p0, int& p1, bool& bad) {
+                                            typename MedFP<T>::D& d1, int& p0, int& p1, bool& bad, int first = 0) {
     typedef MedFP<T> FP;
     typedef typename FP::D D;
     const T scale = FP::pow2(FP::BIAS + FP::M - E);                 // 1/u
@@ -324,7 +390,7 @@ __device__ __forceinline__ void trans_elems(const T* v, int cnt, int E, typename
     bad = false;
 #pragma unroll
     for (int i = 0; i < N; i++) {
-        if (i < cnt) {
+        if (i >= first && i < cnt) {
             const bool ok = v[i] >= (T)0 && v[i] < lim;           // not negative, NaN, inf or >= the binade's top
             bad |= !ok;
             const T q = FP::mul(ok ? v[i] : (T)0, scale);         // exact: power-of-two scaling, < 2^(M+1)
@@ -343,7 +409,7 @@ __device__ __forceinline__ void trans_elems(const T* v, int cnt, int E, typename
             }
         }
     }
-    // (a thread's MC_PER units stay far below the type's range; compose() saturates the sums)
+    // (a thread's units stay far below the type's range; compose() saturates the sums)
     d0 = min(S + e0, FP::SAT);
     d1 = min(S + e1, FP::SAT);
     p0 = X;
@@ -358,60 +424,54 @@ __device__ __forceinline__ void compose(D& a0, D& a1, int& q0, int& q1, D b0, D 
     a0 = n0; a1 = n1; q0 = m0; q1 = m1;
 }
 
-template <typename T>
-__global__ __launch_bounds__(MC_T) void med_chunk_trans_kernel(const T* __restrict__ x, long long n, MedScratch<T> M) {
+// one wave per chunk (grid-stride: a gated launch whose flag is clear ends at once), lane = 32 consecutive
+// elements; the W binades [E_est + wlo, E_est + wlo + W) -> Td / F slots 0..W-1
+template <typename T, int W>
+__global__ __launch_bounds__(256) void med_chunk_trans_kernel(const T* __restrict__ x, long long n, MedScratch<T> M,
+                                                             int gated) {
     typedef MedFP<T> FP;
     typedef typename FP::D D;
-    __shared__ D sd[MW][MC_T / 64][2];
-    __shared__ int sf[MW][MC_T / 64];
-    const long long c = blockIdx.x;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    T v[MC_PER];
-    load_chunk(x, n, c, v);
-    const long long e0 = c * MC + (long long)tid * MC_PER;
-    const int cnt = (int)max(0ll, min((long long)MC_PER, n - e0));
-    const int elo = M.elo[c];
-    const T cmax = M.cmax[c];
-    const bool negnan = (M.Z[c] & 2) != 0;
+    if (gated && __hip_atomic_load(M.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+    const int lane = threadIdx.x & 63;
+    const long long nch = (n + MC - 1) / MC, nw = (long long)gridDim.x * 4;
+    for (long long c = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); c < nch; c += nw) {
+        T v[MT_PER];
+        const long long e0 = c * MC + (long long)lane * MT_PER;
+        load_run<T, MT_PER>(x, n, e0, v);
+        const int cnt = (int)max(0ll, min((long long)MT_PER, n - e0));
+        const int elo = M.eest[c] + med_wlo<W>();
+        const T cmax = M.cmax[c];
+        const bool negnan = (M.Z[c] & 2) != 0;
 #pragma unroll
-    for (int w = 0; w < MW; w++) {
-        const int E = elo + w;
-        D d0 = 0, d1 = 0;
-        int p0 = 0, p1 = 1;
-        bool bad = E < FP::EMIN || E > FP::EMAX;                      // 1/u or the binade top not a number
-        if (!bad && negnan) {
-            bad = true;                                                // (no transducer for any binade)
-        } else if (!bad && cmax < FP::pow2(E - FP::BIAS - FP::M - 1)) {
-            // every element below u/2 (and none negative or NaN): nothing added, parity kept -- the
-            // transducer of a stalled sum, computed for free (uniform branch)
-        } else if (!bad) {
-            trans_elems<T>(v, cnt, E, d0, d1, p0, p1, bad);
-        }
-        // ordered reduction over the wave: lane i absorbs lane i + d (its successor block)
+        for (int w = 0; w < W; w++) {
+            const int E = elo + w;
+            D d0 = 0, d1 = 0;
+            int p0 = 0, p1 = 1;
+            bool bad = E < FP::EMIN || E > FP::EMAX;                  // 1/u or the binade top not a number
+            if (!bad && negnan) {
+                bad = true;                                            // (no transducer for any binade)
+            } else if (!bad && cmax < FP::pow2(E - FP::BIAS - FP::M - 1)) {
+                // every element below u/2 (and none negative or NaN): nothing added, parity kept -- the
+                // transducer of a stalled sum, computed for free (uniform branch)
+            } else if (!bad) {
+                trans_elems<T, MT_PER>(v, cnt, E, d0, d1, p0, p1, bad);
+            }
+            // ordered reduction over the wave: lane i absorbs lane i + d (its successor block)
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const D b0 = __shfl_down(d0, d, 64), b1 = __shfl_down(d1, d, 64);
-            const int f = __shfl_down(p0 | (p1 << 1) | ((int)bad << 2), d, 64);
-            if ((lane & (2 * d - 1)) == 0) {
-                compose(d0, d1, p0, p1, b0, b1, f & 1, (f >> 1) & 1, FP::SAT);
-                bad |= (f & 4) != 0;
+            for (int d = 1; d < 64; d <<= 1) {
+                const D b0 = __shfl_down(d0, d, 64), b1 = __shfl_down(d1, d, 64);
+                const int f = __shfl_down(p0 | (p1 << 1) | ((int)bad << 2), d, 64);
+                if ((lane & (2 * d - 1)) == 0) {
+                    compose(d0, d1, p0, p1, b0, b1, f & 1, (f >> 1) & 1, FP::SAT);
+                    bad |= (f & 4) != 0;
+                }
+            }
+            if (lane == 0) {
+                M.Td[(c * MW + w) * 2] = d0;
+                M.Td[(c * MW + w) * 2 + 1] = d1;
+                M.F[c * MW + w] = (uint8_t)(p0 | (p1 << 1) | (bad ? 4 : 0));
             }
         }
-        if (lane == 0) { sd[w][wid][0] = d0; sd[w][wid][1] = d1; sf[w][wid] = p0 | (p1 << 1) | ((int)bad << 2); }
-    }
-    __syncthreads();
-    if (tid < MW) {
-        const int w = tid;
-        D a0 = sd[w][0][0], a1 = sd[w][0][1];
-        int q0 = sf[w][0] & 1, q1 = (sf[w][0] >> 1) & 1;
-        bool bad = (sf[w][0] & 4) != 0;
-        for (int k = 1; k < MC_T / 64; k++) {
-            compose(a0, a1, q0, q1, sd[w][k][0], sd[w][k][1], sf[w][k] & 1, (sf[w][k] >> 1) & 1, FP::SAT);
-            bad |= (sf[w][k] & 4) != 0;
-        }
-        M.Td[(c * MW + w) * 2] = a0;
-        M.Td[(c * MW + w) * 2 + 1] = a1;
-        M.F[c * MW + w] = (uint8_t)(q0 | (q1 << 1) | (bad ? 4 : 0));
     }
 }
 
@@ -436,8 +496,27 @@ __device__ __forceinline__ MTr<D> mtr_shfl_up(const MTr<D>& v, int d) {
     o.q0 = __shfl_up(v.q0, d, 64); o.q1 = __shfl_up(v.q1, d, 64); o.fb = __shfl_up(v.fb, d, 64);
     return o;
 }
-// inclusive scan of MX_T transducers in thread order (wave scans by shuffles, one LDS round for the 16 wave
-// totals: 3 barriers, where a Hillis-Steele scan through LDS took 10)
+// the compose kernel's LDS ring of chunk records (window's first binade, units, flags): as many chunks as fit
+// in ~128 KB (4096 for float's narrow window, 2048 for its wide one and double's narrow, 1024 for double's wide)
+template <typename T, int W>
+struct MedRing {
+    typedef typename MedFP<T>::D D;
+    static constexpr int BYTES = 4 + W * (2 * (int)sizeof(D) + 1);
+    static constexpr int R = BYTES * 4096 <= 128 * 1024 ? 4096 : (BYTES * 2048 <= 120 * 1024 ? 2048 : 1024);
+};
+
+// (DC_MED_PROF builds: thread 0's s_memrealtime per section and counts -> rec[32..47], dc_med_prof_read)
+#ifdef DC_MED_PROF
+#define MPF_T(v) const unsigned long long v = __builtin_amdgcn_s_memrealtime()
+#define MPF_ADD(i, x) (mpf[i] += (unsigned long long)(x))
+#else
+#define MPF_T(v) do {} while (0)
+#define MPF_ADD(i, x) do {} while (0)
+#endif
+
+// inclusive scan of MXC_T transducers in thread order (wave scans by shuffles, one LDS round for the 16 wave
+// totals: 3 barriers) -- only for a round with a tie somewhere (else plain prefix sums of the units)
+constexpr int MXC_T = 1024;                                // compose workgroup
 template <typename D>
 __device__ __forceinline__ MTr<D> mtr_block_scan(MTr<D> v, MTr<D>* wt, D sat) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -449,189 +528,471 @@ __device__ __forceinline__ MTr<D> mtr_block_scan(MTr<D> v, MTr<D>* wt, D sat) {
     if (lane == 63) wt[wid] = v;
     __syncthreads();
     if (wid == 0) {
-        MTr<D> t = lane < MX_T / 64 ? wt[lane] : MTr<D>{0, 0, 0, 1, MX_T};
+        MTr<D> t = lane < MXC_T / 64 ? wt[lane] : MTr<D>{0, 0, 0, 1, 1 << 30};
 #pragma unroll
-        for (int d = 1; d < MX_T / 64; d <<= 1) {
+        for (int d = 1; d < MXC_T / 64; d <<= 1) {
             const MTr<D> o = mtr_shfl_up(t, d);
             if (lane >= d) t = mtr_then(o, t, sat);
         }
-        if (lane < MX_T / 64) wt[MX_T / 64 + lane] = t;       // inclusive over the waves
+        if (lane < MXC_T / 64) wt[MXC_T / 64 + lane] = t;     // inclusive over the waves
     }
     __syncthreads();
-    if (wid > 0) v = mtr_then(wt[MX_T / 64 + wid - 1], v, sat);
+    if (wid > 0) v = mtr_then(wt[MXC_T / 64 + wid - 1], v, sat);
     __syncthreads();                                        // (wt is rewritten by the next scan)
     return v;
 }
 
+// k + x/u rounded as fl(s + x) rounds it, ties to even on the result (x >= 0 below the binade's top)
 template <typename T>
-__global__ __launch_bounds__(MX_T) void med_compose_kernel(const T* __restrict__ x, long long n, T s_init,
+__device__ __forceinline__ typename MedFP<T>::D med_units(T xv, T scale, typename MedFP<T>::D k) {
+    typedef typename MedFP<T>::D D;
+    const T q = MedFP<T>::mul(xv, scale);
+    const T fq = floor(q);
+    const T fr = MedFP<T>::sub(q, fq);
+    const D fl = (D)fq;
+    return fl + (fr > (T)0.5 ? 1 : (fr == (T)0.5 ? (D)((k + fl) & 1) : 0));
+}
+
+// Per-wave records of one round, exchanged through LDS between the round's two barriers
+template <typename T>
+struct MedRound {
+    typedef typename MedFP<T>::D D;
+    unsigned long long wt[MXC_T / 64];                      // wave totals of the clamped units
+    int wtie[MXC_T / 64];                                   // the wave's first stopping lane (64: none)
+    int wtf[MXC_T / 64];                                    // a tie among the wave's pieces
+    int wl[MXC_T / 64];                                     // the wave's first leaving piece (1 << 30: none)
+    D wk[MXC_T / 64];                                       // k before it
+    T wv[MXC_T / 64];                                       // (elements: its value)
+    int wy[MXC_T / 64];                                     // (chunks: 1 when it had no transducer for E)
+};
+
+// One round of the composition over MXC_T threads, each holding P pieces (chunks or elements) with units d0[j] /
+// d1[j] from an even / odd k (equal but for a tie), stop[j] (no transducer), tie = some piece of the thread's is a
+// tie.  From k0 (binade top TOP): the first piece (thread-major index) where the running k leaves the binade or
+// that stops, k before it, the piece's value (v) and why -- or none (returns 1 << 30) and the k after all.  Two
+// barriers when no thread has a tie (plain prefix sums of the units, DPP wave scans), the transducer block scan
+// otherwise.  Every thread returns the same values.
+template <typename T, int P>
+__device__ __forceinline__ int med_round(const typename MedFP<T>::D (&d0)[P], const typename MedFP<T>::D (&d1)[P],
+                                         const bool (&stop)[P], const bool (&live)[P], const T (&v)[P], const int (&why)[P],
+                                         bool tie, typename MedFP<T>::D k0, MedRound<T>& X, MTr<typename MedFP<T>::D>* wt,
+                                         typename MedFP<T>::D& k_out, T& v_out, int& why_out,
+                                         unsigned long long* pf = nullptr) {
+    typedef MedFP<T> FP;
+    typedef typename FP::D D;
+    constexpr D TOP = D(1) << (FP::M + 1);
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+#ifdef DC_MED_PROF
+#define MRS(i) do { if (pf && tid == 0) { const unsigned long long tt = __builtin_amdgcn_s_memrealtime(); pf[i] += tt - pf[7]; pf[7] = tt; } } while (0)
+    if (pf && tid == 0) pf[7] = __builtin_amdgcn_s_memrealtime();
+#else
+#define MRS(i) do {} while (0)
+#endif
+    // the thread's pieces as one transducer (up to its first stop)
+    D a0 = 0, a1 = 0;
+    int q0 = 0, q1 = 1;
+    bool st = false;
+#pragma unroll
+    for (int j = 0; j < P; j++) {
+        if (live[j] && !st) {
+            if (stop[j]) st = true;
+            else compose(a0, a1, q0, q1, d0[j], d1[j], (int)(d0[j] & 1), (int)((d1[j] + 1) & 1), FP::SAT);
+        }
+    }
+    MRS(0);
+    // the fast path's wave scan, and the wave's tie / stop flags, before the first barrier: a tie anywhere
+    // then selects the transducer scan (the flags travel with the wave totals -- __syncthreads_or cost ~0.8 us)
+    const D uc = min(a0, TOP);
+    unsigned long long incw;
+    if (sizeof(D) == 4 && P <= 4) {
+        incw = wave_scan_incl((uint32_t)uc);                // (64 x 4 x 2^24 pieces clamped: < 2^32)
+    } else {
+        incw = (unsigned long long)uc;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const unsigned long long o = __shfl_up(incw, d, 64);
+            if (lane >= d) incw += o;
+        }
+    }
+    const unsigned long long stb = __ballot(st), tb = __ballot(tie);
+    if (lane == 63) X.wt[wid] = incw;
+    if (lane == 0) { X.wtie[wid] = stb ? (int)(__ffsll((long long)stb) - 1) : 64; X.wtf[wid] = tb != 0; }
+    MRS(1);
+    __syncthreads();
+    MRS(2);
+    // lanes 0..15 hold the 16 waves' records: prefix over waves by shuffles, read out with readlane
+    constexpr int NW = MXC_T / 64;
+    const int lw = lane & (NW - 1);
+    unsigned long long wv = X.wt[lw];
+    const int wst = X.wtie[lw], wtf = X.wtf[lw];
+    const bool anytie = __ballot(lane < NW && wtf != 0) != 0;
+    D k;
+    bool before_ok;                                         // no earlier thread stops (its k is exact)
+    if (!anytie) {
+        unsigned long long woff;
+        if (sizeof(D) == 4) {
+            // (wave totals clamped to TOP: a wave adding that much leaves the binade by itself; 16 x 2^24 < 2^32,
+            // so one DPP scan of 32-bit lanes instead of 64-bit shuffles through LDS)
+            const uint32_t wp = wave_scan_incl(lane < NW ? (uint32_t)min(wv, (unsigned long long)TOP) : 0u);
+            woff = wid > 0 ? (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)wp, wid - 1) : 0ull;
+        } else {
+            unsigned long long wp = lane < NW ? wv : 0ull;  // inclusive over waves 0..lane
+#pragma unroll
+            for (int d = 1; d < NW; d <<= 1) {
+                const unsigned long long o = __shfl_up(wp, d, 64);
+                if (lane >= d) wp += o;
+            }
+            woff = wid > 0 ? ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)wp, wid - 1) |
+                              ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(wp >> 32), wid - 1) << 32))
+                           : 0ull;
+        }
+        const unsigned long long sbm = __ballot(lane < NW && lane < wid && wst < 64);   // an earlier wave stops
+        const int fsl = __builtin_amdgcn_readlane(wst, wid);
+        before_ok = sbm == 0 && lane <= fsl;
+        const unsigned long long kx = (unsigned long long)k0 + woff + incw - (unsigned long long)uc;
+        k = (D)min(kx, (unsigned long long)TOP);
+        MRS(3);
+    } else {
+        const MTr<D> inc = mtr_block_scan<D>(MTr<D>{a0, a1, q0, q1, st ? tid : (1 << 30)}, wt, FP::SAT);
+        // exclusive: the previous thread's inclusive
+        MTr<D> ex = mtr_shfl_up(inc, 1);
+        if (lane == 0) {
+            if (wid > 0) ex = wt[MXC_T / 64 + wid - 1];
+            else ex = MTr<D>{0, 0, 0, 1, 1 << 30};
+        }
+        const int par = (int)(k0 & 1);
+        k = min(k0 + (par ? ex.a1 : ex.a0), TOP);
+        before_ok = ex.fb == (1 << 30);
+        __syncthreads();                                    // (wt of the scan read)
+        MRS(3);
+    }
+    MRS(4);
+    // walk the thread's pieces from its exact k: the first that stops or leaves
+    int lj = P;
+    if (before_ok && k < TOP) {
+#pragma unroll
+        for (int j = 0; j < P; j++) {
+            if (lj == P && live[j]) {
+                if (stop[j]) lj = j;
+                else {
+                    const D d = (k & 1) ? d1[j] : d0[j];
+                    if (k + d >= TOP) lj = j;
+                    else k += d;
+                }
+            }
+        }
+    } else if (before_ok) {
+        lj = 0;                                             // (k >= TOP at the thread's start: cannot happen
+    }                                                       //  without an earlier leave, kept for safety)
+    const unsigned long long bl = __ballot(lj < P);
+    if (bl) {
+        const int L = __ffsll((long long)bl) - 1;
+        if (lane == L) {
+            X.wl[wid] = tid * P + lj;
+            X.wk[wid] = k;
+            T xv = v[0];
+            int y = why[0];
+#pragma unroll
+            for (int j = 1; j < P; j++) { xv = j == lj ? v[j] : xv; y = j == lj ? why[j] : y; }
+            X.wv[wid] = xv;
+            X.wy[wid] = y;
+        }
+    } else if (lane == 63) {
+        X.wl[wid] = 1 << 30;
+        X.wk[wid] = k;                                      // (the wave's last thread: k after it)
+    }
+    MRS(5);
+    __syncthreads();
+    // the first wave with a leaving piece (wl ascends with the wave), else the last wave's k
+    const int wlv = X.wl[lw];
+    const unsigned long long bw = __ballot(lane < NW && wlv < (1 << 30));
+    const int fw = bw ? __ffsll((long long)bw) - 1 : NW - 1;
+    const int f = bw ? __builtin_amdgcn_readlane(wlv, fw) : (1 << 30);
+    k_out = X.wk[fw];
+    v_out = X.wv[fw];
+    why_out = X.wy[fw];
+    MRS(6);
+#undef MRS
+    return f;
+}
+
+// The composition: one workgroup of 1024 threads.  A block of 1024 x CPT chunks (CPT consecutive chunks per
+// thread, their records from the LDS ring) is one med_round; a chunk where the sum leaves its binade is added
+// two elements per thread, each round adding the leaving element by one exact float add.  Every thread keeps the
+// running sum and position in registers (the rounds return the same values everywhere): two barriers per round.
+template <typename T, int W>
+__global__ __launch_bounds__(MXC_T) void med_compose_kernel(const T* __restrict__ x, long long n, T s_init,
                                                            MedScratch<T> M, T* __restrict__ out_mean,
                                                            int* __restrict__ out_type, T* __restrict__ out_sum,
-                                                           T* __restrict__ out_max) {
+                                                           T* __restrict__ out_max, int gated) {
     typedef MedFP<T> FP;
     typedef typename FP::D D;
     typedef typename FP::U U;
-    __shared__ T buf[MC];
-    __shared__ D sa[2][MX_T];                               // [start parity] inclusive units
-    __shared__ MTr<D> wt[2 * (MX_T / 64)];
-    __shared__ T s_sum;
-    __shared__ long long s_c;
-    __shared__ int s_first, s_i;
-    __shared__ T smx[MX_T / 64];
-    const int tid = threadIdx.x;
+    constexpr int R = MedRing<T, W>::R;
+    constexpr int CPT = R >= 4096 ? 2 : 1;                  // chunks per thread in a block
+    constexpr int BLK = MXC_T * CPT;
+    __shared__ T buf[MC];                                   // (a chunk added by one lane)
+    __shared__ int r_lo[R];                                 // ring slot: the chunk's first window binade
+    __shared__ D r_a[R][W][2];                              // units from parity 0 / 1 per window binade
+    __shared__ uint8_t r_f[R][W];                           // end parities | bad << 2
+    __shared__ MedRound<T> X;
+    __shared__ MTr<D> wt[2 * (MXC_T / 64)];
+    __shared__ T s_one;
+    __shared__ T smx[MXC_T / 64];
+#ifdef DC_MED_PROF
+    __shared__ unsigned long long s_pf[8];
+    if (threadIdx.x < 8) s_pf[threadIdx.x] = 0;
+    unsigned long long* pf = s_pf;
+#else
+    unsigned long long* pf = nullptr;
+#endif
+    if (gated && __hip_atomic_load(M.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const long long nch = (n + MC - 1) / MC;
-    if (tid == 0) { s_sum = s_init; s_c = 0; }
-    __syncthreads();
-    while (true) {
-        const long long c = s_c;
-        if (c >= nch) break;
-        const T sv = s_sum;
-        if (sv != sv) break;                                // NaN + anything stays NaN
-        if (FP::bits(sv) == 0) {                            // +0 + (+-0) = +0: skip runs of zero chunks
-            if (tid == 0) s_first = MX_T;
-            __syncthreads();
-            if (c + tid < nch && !(M.Z[c + tid] & 1)) atomicMin(&s_first, tid);
-            __syncthreads();
-            const int f = s_first;
-            __syncthreads();
-            if (f > 0) {
-                if (tid == 0) s_c = min(nch, c + (long long)f);
-                __syncthreads();
-                continue;
+#ifdef DC_MED_PROF
+    unsigned long long mpf[16] = {0};
+#endif
+    T s = s_init;
+    long long c = 0, lo = -(long long)R;
+    int miss = 0;
+    bool aborted = false;
+    while (c < nch && s == s) {                             // (NaN + anything stays NaN)
+        MPF_T(t0);
+        if (FP::bits(s) == 0) {                             // +0 + (+-0) = +0: skip runs of zero chunks
+            __syncthreads();                                // (X of the last round read everywhere)
+            int jz = 1 << 30;
+            for (int j = 0; j < CPT; j++) {
+                const long long ch = c + (long long)tid * CPT + j;
+                if (jz == (1 << 30) && ch < nch && !(M.Z[ch] & 1)) jz = tid * CPT + j;
             }
+            const unsigned long long bz = __ballot(jz < (1 << 30));
+            if (lane == 0) X.wl[wid] = bz ? __builtin_amdgcn_readlane(jz, __ffsll((long long)bz) - 1) : (1 << 30);
+            __syncthreads();
+            int f = 1 << 30;
+            for (int w = 0; w < MXC_T / 64; w++) f = min(f, X.wl[w]);
+            __syncthreads();
+            MPF_ADD(0, 1);
+            if (f == (1 << 30)) { c = min(nch, c + (long long)BLK); continue; }
+            c += f;
         }
         bool serial = true;
-        if (sv >= FP::smin() && sv < FP::smax()) {
-            const U sbits = FP::bits(sv);
-            const int E = FP::expo(sv);
+        if (s >= FP::smin() && s < FP::smax()) {
+            const int cnt = (int)min((long long)BLK, nch - c);
+            if (c + cnt > lo + R) {                         // the ring: chunks [c, c + R)
+                const long long from = max(lo + R, c), to = min(c + R, nch);
+                // (every load of the thread's R / MXC_T chunks issued before the LDS stores: one round trip)
+                constexpr int RPT = R / MXC_T;
+                int e_[RPT];
+                D a_[RPT][W][2];
+                uint8_t f_[RPT][W];
+#pragma unroll
+                for (int q = 0; q < RPT; q++) {
+                    const long long ch = from + tid + (long long)q * MXC_T;
+                    const long long chc = ch < to ? ch : from;  // (a valid address; not stored)
+                    e_[q] = M.eest[chc];
+#pragma unroll
+                    for (int w = 0; w < W; w++) {
+                        a_[q][w][0] = M.Td[(chc * MW + w) * 2];
+                        a_[q][w][1] = M.Td[(chc * MW + w) * 2 + 1];
+                        f_[q][w] = M.F[chc * MW + w];
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < RPT; q++) {
+                    const long long ch = from + tid + (long long)q * MXC_T;
+                    if (ch < to) {
+                        const int sl = (int)(ch % R);
+                        r_lo[sl] = e_[q] + med_wlo<W>();
+#pragma unroll
+                        for (int w = 0; w < W; w++) {
+                            r_a[sl][w][0] = a_[q][w][0];
+                            r_a[sl][w][1] = a_[q][w][1];
+                            r_f[sl][w] = f_[q][w];
+                        }
+                    }
+                }
+                __syncthreads();
+                lo = c;
+                MPF_ADD(2, 1);
+            }
+            MPF_T(t1);
+            MPF_ADD(3, t1 - t0);
+            MPF_ADD(1, 1);
+            const U sbits = FP::bits(s);
+            const int E = FP::expo(s);
             const D k0 = (D)((sbits & ((U(1) << FP::M) - 1)) | (U(1) << FP::M));
-            const int par = (int)(k0 & 1);
-            const long long cc = c + tid;
-            const int cnt = (int)min((long long)MX_T, nch - c);
-            D a0 = 0, a1 = 0;
-            int q0 = 0, q1 = 1, fb = tid;
-            if (tid < cnt) {
-                const int w = E - M.elo[cc];
-                if (w >= 0 && w < MW) {
-                    a0 = M.Td[(cc * MW + w) * 2];
-                    a1 = M.Td[(cc * MW + w) * 2 + 1];
-                    const int f = M.F[cc * MW + w];
-                    q0 = f & 1; q1 = (f >> 1) & 1;
-                    fb = (f & 4) ? tid : MX_T;
+            D d0[CPT], d1[CPT];
+            bool stop[CPT], live[CPT], tie = false;
+            T vv[CPT];
+            int why[CPT];
+#pragma unroll
+            for (int j = 0; j < CPT; j++) {
+                const int t = tid * CPT + j;
+                d0[j] = 0; d1[j] = 0; stop[j] = false; live[j] = t < cnt; vv[j] = (T)0; why[j] = 0;
+                if (live[j]) {
+                    const int sl = (int)((c + t) % R);
+                    const int w = E - r_lo[sl];
+                    if (w >= 0 && w < W) {
+                        const int fl = r_f[sl][w];
+                        d0[j] = r_a[sl][w][0];
+                        d1[j] = r_a[sl][w][1];
+                        // (d0 from an even k, d1 from an odd one; no tie: equal, and the end parities follow)
+                        if (fl & 4) stop[j] = true;
+                        else tie |= !(d0[j] == d1[j] && (fl & 1) == (int)(d0[j] & 1) && ((fl >> 1) & 1) == (int)((d1[j] + 1) & 1));
+                    } else {
+                        stop[j] = true;
+                        why[j] = 1;
+                    }
                 }
             }
-            // inclusive scan: F_t = f_0 then ... then f_t
-            const MTr<D> inc = mtr_block_scan<D>(MTr<D>{a0, a1, q0, q1, fb}, wt, FP::SAT);
-            sa[0][tid] = inc.a0;
-            sa[1][tid] = inc.a1;
-            const D kend = k0 + (par ? inc.a1 : inc.a0);
-            const bool leave = kend >= (D(1) << (FP::M + 1)) || inc.fb <= tid;
-            if (tid == 0) s_first = MX_T;
-            __syncthreads();
-            if (leave) atomicMin(&s_first, tid);
-            __syncthreads();
-            const int f = min(s_first, cnt);
-            if (tid == 0) {
-                const D kf = f == 0 ? k0 : k0 + sa[par][f - 1];
-                s_sum = FP::mul((T)kf, FP::pow2(E - FP::BIAS - FP::M));   // k * u, exact
-                s_c = c + f;
-            }
-            serial = f < cnt;                                 // chunk c + f is added element by element
-            __syncthreads();
+            D kf;
+            T xv;
+            int y;
+            int f = med_round<T, CPT>(d0, d1, stop, live, vv, why, tie, k0, X, wt, kf, xv, y, pf);
+            if (f >= cnt) f = cnt;
+            else if (y == 1) miss++;
+            s = FP::mul((T)kf, FP::pow2(E - FP::BIAS - FP::M));   // k * u, exact
+            c += f;
+            serial = f < cnt;
+            MPF_T(t2);
+            MPF_ADD(4, t2 - t1);
+            if (W < MW && miss > MED_MISS_MAX) { aborted = true; break; }   // the narrow window keeps missing
         }
-        if (serial) {
-            // chunk cs element by element -- in parallel while the sum stays in a binade: two elements per
-            // thread, their transducers scanned; the thread whose piece leaves the binade (or that holds an
-            // element no transducer takes) adds its two elements exactly, and the rest of the chunk goes on in
-            // the new binade.  A sum that is not a positive normal, or a chunk that needs more than 8 such
-            // rounds, is finished by one lane, exactly as the reference.
-            const long long cs = s_c;
-            const int m = (int)min((long long)MC, n - cs * MC);
-            for (int i = tid; i < m; i += MX_T) buf[i] = x[cs * MC + i];
-            if (tid == 0) s_i = 0;
-            __syncthreads();
-            for (int it = 0;; it++) {
-                const int i0 = s_i;
-                if (i0 >= m) break;
-                const T s0 = s_sum;
-                if (FP::bits(s0) == 0) {                            // +0 + (+-0) = +0: up to the first other
-                    if (tid == 0) s_first = MC;
-                    __syncthreads();
-                    for (int i = i0 + tid; i < m; i += MX_T)
-                        if ((FP::bits(buf[i]) << 1) != 0) atomicMin(&s_first, i);
-                    __syncthreads();
-                    if (tid == 0) {
-                        const int fz = s_first;
-                        if (fz < m) { s_sum = FP::add(s0, buf[fz]); s_i = fz + 1; }
-                        else s_i = m;
-                    }
-                    __syncthreads();
-                    continue;
+        if (!serial) continue;
+        // chunk c element by element, two per thread: while the sum stays in a binade, the elements' units are
+        // scanned and the first element that leaves it (or that no transducer takes) is added by one exact float
+        // add; a sum that is not a positive normal, or a chunk that needs more than 8 such rounds, is finished by
+        // one lane, exactly as the reference.
+        MPF_T(t3);
+        MPF_ADD(5, 1);
+        const int m = (int)min((long long)MC, n - c * MC);
+        T v2[2];
+        {
+            const long long e = c * MC + 2ll * tid;
+            v2[0] = 2 * tid < m ? x[e] : (T)0;
+            v2[1] = 2 * tid + 1 < m ? x[e + 1] : (T)0;
+        }
+        int i0 = 0;
+        for (int it = 0; i0 < m; it++) {
+            MPF_ADD(7, 1);
+            if (FP::bits(s) == 0) {                         // +0 + (+-0) = +0: up to the first other element
+                __syncthreads();                            // (X of the last round read everywhere)
+                int jz = 1 << 30;
+                T zv = (T)0;
+                for (int j = 1; j >= 0; j--)
+                    if (2 * tid + j >= i0 && 2 * tid + j < m && (FP::bits(v2[j]) << 1) != 0) { jz = 2 * tid + j; zv = v2[j]; }
+                const unsigned long long bz = __ballot(jz < (1 << 30));
+                if (bz) {
+                    const int L = __ffsll((long long)bz) - 1;
+                    if (lane == L) { X.wl[wid] = jz; X.wv[wid] = zv; }
+                } else if (lane == 0) {
+                    X.wl[wid] = 1 << 30;
                 }
-                if (!(s0 >= FP::smin() && s0 < FP::smax()) || it >= 8) {
-                    if (tid == 0) {
-                        T s2 = s0;
-                        for (int i = i0; i < m; i++) s2 = FP::add(s2, buf[i]);
-                        s_sum = s2;
-                        s_i = m;
-                    }
-                    __syncthreads();
-                    break;
-                }
-                const U sb2 = FP::bits(s0);
-                const int E = FP::expo(s0);
-                const D k0 = (D)((sb2 & ((U(1) << FP::M) - 1)) | (U(1) << FP::M));
-                const int par = (int)(k0 & 1);
-                const int j = i0 + 2 * tid;
-                const int cnt2 = max(0, min(2, m - j));
-                T v2[2] = {cnt2 > 0 ? buf[j] : (T)0, cnt2 > 1 ? buf[j + 1] : (T)0};
-                D a0 = 0, a1 = 0;
-                int q0 = 0, q1 = 1;
-                bool bad = false;
-                if (cnt2 > 0) trans_elems<T, 2>(v2, cnt2, E, a0, a1, q0, q1, bad);
-                const MTr<D> inc = mtr_block_scan<D>(MTr<D>{a0, a1, q0, q1, bad ? tid : MX_T}, wt, FP::SAT);
-                sa[0][tid] = inc.a0;
-                sa[1][tid] = inc.a1;
-                const int nth = (m - i0 + 1) / 2;                   // threads holding elements
-                const bool leave = tid < nth && (k0 + (par ? inc.a1 : inc.a0) >= (D(1) << (FP::M + 1)) || inc.fb <= tid);
-                if (tid == 0) s_first = MX_T;
                 __syncthreads();
-                if (leave) atomicMin(&s_first, tid);
+                int f = 1 << 30, fw = 0;
+                for (int w = MXC_T / 64 - 1; w >= 0; w--) if (X.wl[w] <= f) { f = X.wl[w]; fw = w; }
+                const T fv = X.wv[fw];
                 __syncthreads();
-                const int f = s_first;
+                if (f == (1 << 30)) { i0 = m; break; }
+                s = FP::add(s, fv);
+                i0 = f + 1;
+                continue;
+            }
+            if (!(s >= FP::smin() && s < FP::smax()) || it >= 8) {
+                MPF_ADD(8, 1);
+                MPF_ADD(9, m - i0);
+                if (2 * tid < m) buf[2 * tid] = v2[0];
+                if (2 * tid + 1 < m) buf[2 * tid + 1] = v2[1];
+                __syncthreads();
                 if (tid == 0) {
-                    const T u = FP::pow2(E - FP::BIAS - FP::M);
-                    if (f >= nth) {                                 // the rest of the chunk stays in the binade
-                        s_sum = FP::mul((T)(k0 + sa[par][nth - 1]), u);
-                        s_i = m;
-                    } else {                                        // thread f's two elements, exactly
-                        T s2 = FP::mul((T)(f == 0 ? k0 : k0 + sa[par][f - 1]), u);
-                        const int jf = i0 + 2 * f;
-                        for (int i = jf; i < min(m, jf + 2); i++) s2 = FP::add(s2, buf[i]);
-                        s_sum = s2;
-                        s_i = min(m, jf + 2);
+                    T s2 = s;
+                    int i = i0;
+                    for (; i + 16 <= m; i += 16) {          // (16 LDS reads in flight, then the adds)
+                        T b16[16];
+#pragma unroll
+                        for (int k2 = 0; k2 < 16; k2++) b16[k2] = buf[i + k2];
+#pragma unroll
+                        for (int k2 = 0; k2 < 16; k2++) s2 = FP::add(s2, b16[k2]);
                     }
+                    for (; i < m; i++) s2 = FP::add(s2, buf[i]);
+                    s_one = s2;
                 }
                 __syncthreads();
+                s = s_one;
+                __syncthreads();
+                i0 = m;
+                break;
             }
-            if (tid == 0) s_c = cs + 1;
-            __syncthreads();
+            const U sb2 = FP::bits(s);
+            const int E = FP::expo(s);
+            const D k0 = (D)((sb2 & ((U(1) << FP::M) - 1)) | (U(1) << FP::M));
+            const T scale = FP::pow2(FP::BIAS + FP::M - E), lim = FP::pow2(E + 1 - FP::BIAS);
+            D d0[2], d1[2];
+            bool stop[2], live[2], tie = false;
+            int why[2] = {0, 0};
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const int e = 2 * tid + j;
+                live[j] = e >= i0 && e < m;
+                stop[j] = false; d0[j] = 0; d1[j] = 0;
+                if (live[j]) {
+                    if (!(v2[j] >= (T)0 && v2[j] < lim)) stop[j] = true;
+                    else {
+                        d0[j] = med_units<T>(v2[j], scale, (D)0);   // from an even k
+                        d1[j] = med_units<T>(v2[j], scale, (D)1);   // from an odd one
+                        tie |= d0[j] != d1[j];
+                    }
+                }
+            }
+            D kf;
+            T xv;
+            int y;
+            const int f = med_round<T, 2>(d0, d1, stop, live, v2, why, tie, k0, X, wt, kf, xv, y, pf);
+            const T u = FP::pow2(E - FP::BIAS - FP::M);
+            if (f >= (1 << 30)) {                           // the rest of the chunk stays in the binade
+                s = FP::mul((T)kf, u);
+                i0 = m;
+                break;
+            }
+            s = FP::add(FP::mul((T)kf, u), xv);             // the leaving element, exactly
+            i0 = f + 1;
         }
+        c += 1;
+        MPF_T(t4);
+        MPF_ADD(10, t4 - t3);
+    }
+#ifdef DC_MED_PROF
+    if (tid == 0) {
+        for (int i = 0; i < 9; i++) M.rec[32 + i] = (long long)mpf[i];
+        mpf[10] = mpf[10];
+        M.rec[32 + 9] = (long long)mpf[10];
+        for (int i = 0; i < 6; i++) M.rec[32 + 10 + i] = (long long)s_pf[i + 1];   // med_round sections 1..6
+    }
+#endif
+    if (aborted) {                                          // (uniform: every thread holds the same state)
+        if (tid == 0) *M.flag = 1u;
+        return;
     }
     // max: x[0] folded with every chunk's max (strict >, as the reference's loop)
     T mx = -INFINITY;
-    for (long long c = tid; c < nch; c += MX_T) { const T v = M.cmax[c]; mx = v > mx ? v : mx; }
+    for (long long cc = tid; cc < nch; cc += MXC_T) { const T v = M.cmax[cc]; mx = v > mx ? v : mx; }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) { const T o = __shfl_xor(mx, d, 64); mx = o > mx ? o : mx; }
     if ((tid & 63) == 0) smx[tid >> 6] = mx;
     __syncthreads();
     if (tid == 0) {
         T mm = x[0];
-        for (int i = 0; i < MX_T / 64; i++) if (smx[i] > mm) mm = smx[i];
-        *out_type = FP::type(mm);
-        *out_mean = FP::mean(s_sum, n);
-        if (out_sum) *out_sum = s_sum;
+        for (int i = 0; i < MXC_T / 64; i++) if (smx[i] > mm) mm = smx[i];
+        const T mean = FP::mean(s, n);
+        const int ty = FP::type(mm);
+        *out_type = ty;
+        *out_mean = mean;
+        if (out_sum) *out_sum = s;
         if (out_max) *out_max = mm;
+        M.res[0] = (long long)FP::bits(mean);
+        M.res[1] = ty;
+        M.res[2] = (long long)FP::bits(s);
+        M.res[3] = (long long)FP::bits(mm);
     }
 }
 
@@ -640,8 +1001,8 @@ __global__ __launch_bounds__(MX_T) void med_compose_kernel(const T* __restrict__
 //   trans = 0: the shard's double sum (an estimate of what it adds), the max of its chunk maxes (NaNs
 //              never win) and x[0]; the global max folds the first shard's x[0] with every shard's max,
 //              strict >, as med_compose_kernel
-//   trans = 1: the whole shard as one transducer for each binade E of the first chunk's window
-//              [elo[0], elo[0] + MW): start parity -> (units added, end parity), "bad" where some chunk has
+//   trans = 1: the whole shard as one transducer for each binade E of the first chunk's wide window
+//              [E_est - 4, E_est + 2): start parity -> (units added, end parity), "bad" where some chunk has
 //              no transducer for E (E outside its window, or an element it cannot take).  A rank whose
 //              running sum enters in such a binade and stays in it (k + units < 2^24) ends at k + units
 //              without a pass of its own; composing these over the ranks is the exscan of global_med.
@@ -679,7 +1040,7 @@ __global__ __launch_bounds__(MX_T) void med_shard_kernel(const T* __restrict__ x
         }
         return;
     }
-    const int e0 = M.elo[0];
+    const int e0 = M.eest[0] + med_wlo<MW>();
 #pragma unroll 1
     for (int w = 0; w < MW; w++) {
         const int E = e0 + w;
@@ -687,7 +1048,7 @@ __global__ __launch_bounds__(MX_T) void med_shard_kernel(const T* __restrict__ x
         int q0 = 0, q1 = 1;
         bool bad = false;
         for (long long c = c0; c < c1; c++) {
-            const int wc = E - M.elo[c];
+            const int wc = E - (M.eest[c] + med_wlo<MW>());
             if (wc < 0 || wc >= MW) { bad = true; break; }
             const int f = M.F[c * MW + wc];
             compose(a0, a1, q0, q1, M.Td[(c * MW + wc) * 2], M.Td[(c * MW + wc) * 2 + 1], f & 1, (f >> 1) & 1, FP::SAT);
@@ -721,17 +1082,35 @@ __global__ __launch_bounds__(MX_T) void med_shard_kernel(const T* __restrict__ x
     }
 }
 
+// the transducer grid: one wave per chunk, at most 4096 workgroups of 4 (a gated launch that ends at once
+// costs ~3 us, not a full grid's dispatch)
+static inline unsigned med_trans_grid(long long nch) { return (unsigned)min((nch + 3) / 4, 4096ll); }
+
 template <typename T>
 static int launch_med(const T* x, long long n, T s_init, void* scratch, T* d_mean, int* d_type, T* d_sum, T* d_max,
-                      hipStream_t st) {
+                      int wide, hipStream_t st) {
     if (n <= 0) return 0;
     const long long nch = (n + MC - 1) / MC;
     const MedScratch<T> M = med_scratch<T>(scratch, nch);
-    hipLaunchKernelGGL(med_chunk_sum_kernel<T>, dim3((unsigned)nch), dim3(MC_T), 0, st, x, n, M);
-    hipLaunchKernelGGL(med_chunk_scan_kernel<T>, dim3(1), dim3(1024), 0, st, M, nch, s_init);
-    hipLaunchKernelGGL(med_chunk_trans_kernel<T>, dim3((unsigned)nch), dim3(MC_T), 0, st, x, n, M);
-    hipLaunchKernelGGL(med_compose_kernel<T>, dim3(1), dim3(MX_T), 0, st, x, n, s_init, M, d_mean, d_type, d_sum, d_max);
+    const unsigned tg = med_trans_grid(nch);
+    if (!wide) {
+        hipLaunchKernelGGL(med_chunk_sum_kernel<T>, dim3((unsigned)nch), dim3(MC_T), 0, st, x, n, M);
+        hipLaunchKernelGGL(med_chunk_scan_kernel<T>, dim3(1), dim3(1024), 0, st, M, nch, s_init);
+        hipLaunchKernelGGL((med_chunk_trans_kernel<T, MWN>), dim3(tg), dim3(256), 0, st, x, n, M, 0);
+        hipLaunchKernelGGL((med_compose_kernel<T, MWN>), dim3(1), dim3(MXC_T), 0, st, x, n, s_init, M, d_mean, d_type,
+                           d_sum, d_max, 0);
+    } else {                                                // (after the narrow compose raised the flag)
+        hipLaunchKernelGGL((med_chunk_trans_kernel<T, MW>), dim3(tg), dim3(256), 0, st, x, n, M, 0);
+        hipLaunchKernelGGL((med_compose_kernel<T, MW>), dim3(1), dim3(MXC_T), 0, st, x, n, s_init, M, d_mean, d_type,
+                           d_sum, d_max, 0);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// the narrow-window flag of a med scratch for n elements (1: run dc_launch_med*_wide)
+extern "C" unsigned* dc_med_flag_ptr(void* scratch, long long n, int is_double) {
+    const long long nch = (n + MC - 1) / MC;
+    return is_double ? med_scratch<double>(scratch, nch).flag : med_scratch<float>(scratch, nch).flag;
 }
 
 // ---------------------------------------------------------------- CRC-32 (zlib)
@@ -1287,7 +1666,11 @@ extern "C" int dc_launch_to_small(const float* x, long long n, float* y, float* 
 // (optional) the raw sum and max; scratch: dc_med_scratch_bytes(n) bytes of device memory
 extern "C" int dc_launch_med(const float* x, long long n, float s_init, void* scratch, float* d_mean, int* d_type,
                              float* d_sum, float* d_max, hipStream_t st) {
-    return launch_med<float>(x, n, s_init, scratch, d_mean, d_type, d_sum, d_max, st);
+    return launch_med<float>(x, n, s_init, scratch, d_mean, d_type, d_sum, d_max, 0, st);
+}
+extern "C" int dc_launch_med_wide(const float* x, long long n, float s_init, void* scratch, float* d_mean, int* d_type,
+                                  float* d_sum, float* d_max, hipStream_t st) {
+    return launch_med<float>(x, n, s_init, scratch, d_mean, d_type, d_sum, d_max, 1, st);
 }
 // a rank's shard (med_shard_kernel): trans = 0 its double sum and max; trans = 1 its whole-shard transducer,
 // the chunk windows opened from s_est (the estimated running sum the shard starts at).  The 21-word record
@@ -1297,13 +1680,13 @@ extern "C" int dc_launch_med_shard(const float* x, long long n, double s_est, in
     if (n <= 0) return -1;
     const long long nch = (n + MC - 1) / MC;
     const MedScratch<float> M = med_scratch<float>(scratch, nch);
-    long long* rec = (long long*)(((uintptr_t)(M.Z + nch) + 7) & ~(uintptr_t)7);
+    long long* rec = M.rec;
     *d_rec = rec;
     hipLaunchKernelGGL(med_chunk_sum_kernel<float>, dim3((unsigned)nch), dim3(MC_T), 0, st, x, n, M);
     if (trans) {
         const float se = (float)fmin(fmax(s_est, 0.0), 3.0e38);
         hipLaunchKernelGGL(med_chunk_scan_kernel<float>, dim3(1), dim3(1024), 0, st, M, nch, se);
-        hipLaunchKernelGGL(med_chunk_trans_kernel<float>, dim3((unsigned)nch), dim3(MC_T), 0, st, x, n, M);
+        hipLaunchKernelGGL((med_chunk_trans_kernel<float, MW>), dim3(med_trans_grid(nch)), dim3(256), 0, st, x, n, M, 0);
     }
     hipLaunchKernelGGL(med_shard_kernel<float>, dim3(1), dim3(MX_T), 0, st, x, nch, M, trans, rec);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -1311,8 +1694,9 @@ extern "C" int dc_launch_med_shard(const float* x, long long n, double s_est, in
 extern "C" int dc_med_shard_binades(void) { return MW; }
 
 // med_dataset_double (:3564-3590): the same on doubles (scratch: dc_med_scratch_bytes64(n))
-extern "C" int dc_launch_med64(const double* x, long long n, void* scratch, double* d_mean, int* d_type, hipStream_t st) {
-    return launch_med<double>(x, n, 0.0, scratch, d_mean, d_type, (double*)nullptr, (double*)nullptr, st);
+extern "C" int dc_launch_med64(const double* x, long long n, void* scratch, double* d_mean, int* d_type, int wide,
+                               hipStream_t st) {
+    return launch_med<double>(x, n, 0.0, scratch, d_mean, d_type, (double*)nullptr, (double*)nullptr, wide, st);
 }
 
 extern "C" long long dc_crc_parts(long long nbytes) { return (nbytes + CRC_BLK - 1) / CRC_BLK; }

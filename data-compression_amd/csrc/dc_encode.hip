@@ -866,12 +866,12 @@ __device__ void enc_scanner(uint64_t* __restrict__ st, unsigned ntiles, uint32_t
 #ifndef DC_STORE_U
 #define DC_STORE_U 1                    // (A/B) words per thread per store round: 4 and 8 measured equal, off
 #endif
-// After the pack only wave 0 has work left that needs the tile's offset (the look-back, then the stores):
-// waves 1-3 end there, and their registers and wave slots take the next tile's waves while wave 0 waits for
-// its look-back round trip (the workgroup's LDS is held until wave 0 ends: 9 tiles per CU by LDS, 7 by
-// registers with every wave resident)
+// (A/B, off) After the pack only wave 0 has work left that needs the tile's offset (the look-back, then the
+// stores): waves 1-3 may end there, their wave slots taking the next tile's waves while wave 0 waits for its
+// look-back round trip.  Measured r05: 148.7-150 us with vs 143.7-145.7 us without (one wave then stores the
+// whole tile; the next tile's waves find no free LDS: 9 tiles per CU by LDS, 7 by registers)
 #ifndef DC_ENC_EARLY_EXIT
-#define DC_ENC_EARLY_EXIT 1
+#define DC_ENC_EARLY_EXIT 0
 #endif
 // CRC (dc_encode_crc_device, the CT9 sender): the raw CRC-32 of the words a tile stores is XOR-ed into the 16 KiB
 // block accumulators cblk (dc_device.h's fused CRC; crcf_final_kernel turns them into the stream's zlib CRC):

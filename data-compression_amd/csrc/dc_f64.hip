@@ -1308,7 +1308,9 @@ extern "C" int dc64_to_small_device(const void* d_x, long long n, void* d_out, d
     return DC_OK;
 }
 
-extern "C" int dc_launch_med64(const double* x, long long n, void* scratch, double* d_mean, int* d_type, hipStream_t st);
+extern "C" int dc_launch_med64(const double* x, long long n, void* scratch, double* d_mean, int* d_type, int wide,
+                               hipStream_t st);
+extern "C" unsigned* dc_med_flag_ptr(void* scratch, long long n, int is_double);
 extern "C" long long dc_med_scratch_bytes64(long long n);
 
 // med_dataset_double (:3564-3590): the exact left-to-right double sum by the binade-transducer kernels of
@@ -1326,12 +1328,15 @@ extern "C" int dc64_med_device(const void* d_x, long long n, double* mean_out, i
         H64(hipMalloc(&C64.med_scr, need + need / 8));
         C64.med_cap = need + need / 8;
     }
-    if (dc_launch_med64((const double*)d_x, n, C64.med_scr, C64.d_f + 1, C64.d_i, st))
-        return dc_set_error(DC_ERR_HIP, "dc64_med_device: launch failed");
-    H64(hipMemcpyAsync(C64.h + 4, C64.d_f + 1, 8, hipMemcpyDeviceToHost, st));
-    H64(hipMemcpyAsync(C64.h + 5, C64.d_i, 4, hipMemcpyDeviceToHost, st));
-    H64(hipStreamSynchronize(st));
-    if (mean_out) memcpy(mean_out, C64.h + 4, 8);
-    if (type_out) *type_out = (int)(uint32_t)C64.h[5];
+    for (int wide = 0; wide < 2; wide++) {                // the narrow binade window, then the wide one if it missed
+        if (dc_launch_med64((const double*)d_x, n, C64.med_scr, C64.d_f + 1, C64.d_i, wide, st))
+            return dc_set_error(DC_ERR_HIP, "dc64_med_device: launch failed");
+        // flag, then mean, type (MedScratch.res): one copy
+        H64(hipMemcpyAsync(C64.h + 4, dc_med_flag_ptr(C64.med_scr, n, 1), 3 * 8, hipMemcpyDeviceToHost, st));
+        H64(hipStreamSynchronize(st));
+        if (!(uint32_t)C64.h[4] || wide) break;
+    }
+    if (mean_out) memcpy(mean_out, C64.h + 5, 8);
+    if (type_out) *type_out = (int)(uint32_t)C64.h[6];
     return DC_OK;
 }

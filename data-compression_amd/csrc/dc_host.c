@@ -106,6 +106,7 @@ typedef struct {
     float* part_v; long long* part_i;
     float* d_f;                      /* [0] min [1] mean */
     void* med_scr; size_t med_scr_cap;  /* exact mean: chunk transducers (dc_med_scratch_bytes) */
+    int med_wide;                        /* the last exact mean needed the wide binade window */
     int* d_i;                        /* [0] type */
     uint32_t* d_crctab; uint32_t* d_x2n; uint32_t* d_crcparts; long long crcparts_cap; uint32_t* d_crc;
     uint32_t* d_crcf;                /* the fused CRC's tables (dc_crcf_tables) */
@@ -1243,18 +1244,50 @@ int dc_to_small_device(const void* d_x, long long n, void* d_out, float* min_out
     return DC_OK;
 }
 
+
+
+/* DC_MED_WIDE=1: the exact mean goes straight to the wide binade window (tests compare both windows) */
+static int med_force_wide(void) {
+    const char* e = getenv("DC_MED_WIDE");
+    return e && *e == '1';
+}
+
+/* 1 when the last exact mean ran the wide binade window (the narrow one missed; dc_aux.hip) */
+int dc_med_last_wide(void) { return G.med_wide; }
+
+/* (DC_MED_PROF builds) the compose kernel's section counters of the last dc_med_device on n floats */
+int dc_med_prof_read(long long n, long long* out16) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (!G.med_scr || n <= 0) return seterr(DC_ERR_ARG, "no med scratch");
+    const long long nch = (n + 2047) / 2048;
+    const long long off = ((nch * (8 + 4 + 4 + 6 * 2 * 4 + 6 + 1) + 7) & ~7ll) + 32 * 8;
+    HIPCHK(hipMemcpy(out16, (char*)G.med_scr + off, 16 * 8, hipMemcpyDeviceToHost));
+    return DC_OK;
+}
+
 int dc_med_device(const void* d_x, long long n, float* mean_out, int* type_out) {
     int rc = ensure_init();
     if (rc) return rc;
     if (n <= 0) return seterr(DC_ERR_ARG, "empty input");
     if (grow(&G.med_scr, &G.med_scr_cap, (size_t)dc_med_scratch_bytes(n))) return DC_ERR_HIP;
-    if (dc_launch_med((const float*)d_x, n, 0.0f, G.med_scr, &G.d_f[1], &G.d_i[0], NULL, NULL, G.st))
-        return seterr(DC_ERR_HIP, "med launch failed");
     float m;
     int t;
-    HIPCHK(hipMemcpyAsync(&m, &G.d_f[1], 4, hipMemcpyDeviceToHost, G.st));
-    HIPCHK(hipMemcpyAsync(&t, &G.d_i[0], 4, hipMemcpyDeviceToHost, G.st));
-    HIPCHK(hipStreamSynchronize(G.st));
+    unsigned fl = 0;
+    for (int wide = med_force_wide(); wide < 2; wide++) {       /* the narrow window, then the wide one if it missed */
+        if ((wide ? dc_launch_med_wide : dc_launch_med)((const float*)d_x, n, 0.0f, G.med_scr, &G.d_f[1], &G.d_i[0],
+                                                         NULL, NULL, G.st))
+            return seterr(DC_ERR_HIP, "med launch failed");
+        /* flag, then mean, type, sum, max (dc_aux.hip MedScratch.res): one copy */
+        long long r[5];
+        HIPCHK(hipMemcpyAsync(r, dc_med_flag_ptr(G.med_scr, n, 0), sizeof r, hipMemcpyDeviceToHost, G.st));
+        HIPCHK(hipStreamSynchronize(G.st));
+        fl = (unsigned)r[0];
+        { const uint32_t b = (uint32_t)r[1]; memcpy(&m, &b, 4); }
+        t = (int)r[2];
+        G.med_wide = wide;
+        if (!fl || wide) break;
+    }
     if (mean_out) *mean_out = m;
     if (type_out) *type_out = t;
     return DC_OK;
@@ -1267,11 +1300,21 @@ int dc_med_sum_device(const void* d_x, long long n, float s_init, float* sum_out
     if (rc) return rc;
     if (n <= 0) return seterr(DC_ERR_ARG, "empty input");
     if (grow(&G.med_scr, &G.med_scr_cap, (size_t)dc_med_scratch_bytes(n))) return DC_ERR_HIP;
-    if (dc_launch_med((const float*)d_x, n, s_init, G.med_scr, &G.d_f[1], &G.d_i[0], &G.d_f[2], &G.d_f[3], G.st))
-        return seterr(DC_ERR_HIP, "med launch failed");
     float h[2];
-    HIPCHK(hipMemcpyAsync(h, &G.d_f[2], 8, hipMemcpyDeviceToHost, G.st));
-    HIPCHK(hipStreamSynchronize(G.st));
+    unsigned fl = 0;
+    for (int wide = med_force_wide(); wide < 2; wide++) {
+        if ((wide ? dc_launch_med_wide : dc_launch_med)((const float*)d_x, n, s_init, G.med_scr, &G.d_f[1], &G.d_i[0],
+                                                         &G.d_f[2], &G.d_f[3], G.st))
+            return seterr(DC_ERR_HIP, "med launch failed");
+        long long r[5];
+        HIPCHK(hipMemcpyAsync(r, dc_med_flag_ptr(G.med_scr, n, 0), sizeof r, hipMemcpyDeviceToHost, G.st));
+        HIPCHK(hipStreamSynchronize(G.st));
+        fl = (unsigned)r[0];
+        { const uint32_t b = (uint32_t)r[3]; memcpy(&h[0], &b, 4); }
+        { const uint32_t b = (uint32_t)r[4]; memcpy(&h[1], &b, 4); }
+        G.med_wide = wide;
+        if (!fl || wide) break;
+    }
     if (sum_out) *sum_out = h[0];
     if (max_out) *max_out = h[1];
     return DC_OK;

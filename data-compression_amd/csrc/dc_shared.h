@@ -201,6 +201,9 @@ int dc_launch_to_small(const float* x, long long n, float* y, float* part_v, lon
 #define DC_MIN_PARTS 2048                /* toSmallDataset: per-workgroup minima combined by min_final */
 int dc_launch_med(const float* x, long long n, float s_init, void* scratch, float* d_mean, int* d_type, float* d_sum,
                   float* d_max, dc_hip_stream st);
+int dc_launch_med_wide(const float* x, long long n, float s_init, void* scratch, float* d_mean, int* d_type,
+                       float* d_sum, float* d_max, dc_hip_stream st);
+unsigned* dc_med_flag_ptr(void* scratch, long long n, int is_double);
 int dc_launch_med_shard(const float* x, long long n, double s_est, int trans, void* scratch, long long** d_rec,
                         dc_hip_stream st);
 int dc_med_shard_binades(void);

@@ -135,6 +135,10 @@ int dc_set_halo_async(int on);
 /* Pre-passes on device data: toSmallDataset_float and med_dataset_float (exact). */
 int dc_to_small_device(const void* d_x, long long n, void* d_out, float* min_out);
 int dc_med_device(const void* d_x, long long n, float* mean_out, int* type_out);
+/* 1 when the last dc_med_device / dc_med_sum_device needed the wide binade window: the narrow window tried
+   first, [E_est - 1, E_est + 1] around the double estimate of the running sum, missed more than 16 chunks
+   (DC_MED_WIDE=1 in the environment goes to the wide window at once) */
+int dc_med_last_wide(void);
 /* Multi-GPU med_dataset_float over contiguous shards: the exact left-to-right float sum of x[0..n)
  * continued from s_init (0 on the first shard, else the sum the previous shard returned) and the max of
  * x; the global mean is sum / (float)n_total and the type dc_type_from_max(global max).  Synchronous. */

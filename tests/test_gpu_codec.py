@@ -317,6 +317,36 @@ def test_med_exact_parallel(dc, oracle, kind, n):
     assert t == ot
 
 
+@pytest.mark.parametrize("kind,n", [("u10", 1 << 22), ("ramp", 1 << 21), ("signed", 1 << 20), ("wide", 1 << 20),
+                                    ("zeros_u10", (1 << 20) + 77)])
+def test_med_windows(dc, oracle, kind, n, monkeypatch):
+    """The exact mean by the narrow binade window (tried first) and by the wide one (DC_MED_WIDE=1, or after
+    the narrow compose missed more than 16 chunks): the same serial sum bit for bit."""
+    import torch
+    rs = np.random.RandomState(n % 997)
+    if kind == "signed":
+        x = (rs.randn(n) * 3).astype(np.float32)
+    elif kind == "wide":
+        x = (rs.rand(n) * np.exp2(rs.randint(-30, 30, n))).astype(np.float32)
+    elif kind == "zeros_u10":
+        x = oracle.gen_u10(n)
+        x[: n // 3] = 0.0
+    else:
+        x = _inputs(oracle, kind, n)
+    d = torch.from_numpy(x).cuda()
+    torch.cuda.synchronize()
+    om, ot = oracle.med(x)
+    for force in ("0", "1"):
+        monkeypatch.setenv("DC_MED_WIDE", force)
+        mean, t = dc.med_device(d.data_ptr(), n)
+        assert np.array_equal(np.float32(mean).view(np.uint32), np.float32(om).view(np.uint32)), (force, mean, om)
+        assert t == ot
+        if force == "1":
+            assert dc.L.dc_med_last_wide() == 1
+        elif kind in ("u10", "ramp"):
+            assert dc.L.dc_med_last_wide() == 0          # the narrow window holds these sums
+
+
 @pytest.mark.parametrize("ber", [1e-6, 1e-4])
 def test_ct9_ber_flow(dc, oracle, ber):
     """CT9 (bitmask + CRC) with real bit flips: the sender's CRC-32 of the CT7
