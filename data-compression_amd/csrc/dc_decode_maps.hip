@@ -9,11 +9,11 @@
 // repairs then chain over many segments and it declines the stream (status 512 | 2048).  Those streams were
 // decoded by the chunk-map decoder, ~5 ms at 2^24 values.  Here, with no walk longer than a group:
 //
-// maps_group_kernel   256-bit chunks, 32 lanes per chunk: every bit's next token start (a 512-entry length
-//                     table on the token's top 9 bits) into LDS, then lane e steps from entry bit e (a token
-//                     starts on one of a chunk's first 32 bits) through that table -> the chunk's entry -> exit
-//                     map and token count; 8 chunks a group, whose map (the 8 maps composed) goes to gmap and,
-//                     for each of its 32 entries, its chunks' records (entry | tokens << 8) to gtab.
+// maps_group_kernel   256-bit chunks, 32 lanes per chunk: every bit's next token start into LDS, then lane e
+//                     steps from entry bit e (a token starts on one of a chunk's first 32 bits) through that
+//                     table -> the chunk's entry -> exit map and token count; 8 chunks a group (one wave), whose
+//                     map (the 8 maps composed) goes to gmap and, for each of its 32 entries, its chunks'
+//                     records (entry | tokens << 8) to gtab.
 // maps_scan_kernel    1024 group maps per workgroup: an inclusive scan of the maps inside each wave (register
 //                     maps, four-entry v_perm lookups), the 16 wave totals composed; either every map's entry
 //                     from the block's entry (ent_in), or the block's total map (a first pass: the block maps,
@@ -39,59 +39,76 @@ __device__ __forceinline__ uint32_t mp_word(const uint8_t* __restrict__ s, long 
     return v;
 }
 
-// (a grid of at most MP_GRID workgroups, each looping over groups: the next group's stream words are loaded while
-// the current one is walked -- one workgroup per group spent most of its life waiting for its first load)
-constexpr int MP_GRID = 4096;
+// One wave per group (a grid of at most MP_GRID waves, each looping over groups): the group's 66 stream words
+// (8 chunks + the lookahead) are loaded for the next group while the current one is walked; the wave takes its
+// 8 chunks two at a time (lanes 0-31 / 32-63), every bit's next token start computed in registers (the token's
+// length from its top 9 bits, token_len_bf) into a per-chunk LDS table, then lane e steps from entry bit e
+// through it.  No workgroup barrier: with four waves sharing a group and four barriers per group, waves waited
+// 72 % of their cycles (SQ counters, sine @1e-5 at 2^24: 463 us) and the table lookups of the lengths conflicted
+// on LDS banks.
+constexpr int MP_GRID = 8192;
+constexpr int MP_GWORDS = MP_G * 8 + 2;                  // a group's stream words with the last chunk's lookahead
 template <int CT>
-__global__ __launch_bounds__(256) void maps_group_kernel(const uint8_t* __restrict__ s, Params P,
-                                                         const unsigned long long* dev_nbits, unsigned long long host_nbits,
-                                                         uint8_t* __restrict__ gmap, uint4* __restrict__ gtab, long long ngr,
-                                                         long long num, long long max_chunks, unsigned* __restrict__ err) {
-    __shared__ uint32_t w[MP_G][10];
-    __shared__ uint8_t tl[512];
-    __shared__ uint16_t nx[MP_G][256];                           // the next token's start from every bit
+__global__ __launch_bounds__(64) void maps_group_kernel(const uint8_t* __restrict__ s, Params P,
+                                                        const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                                                        uint8_t* __restrict__ gmap, uint4* __restrict__ gtab, long long ngr,
+                                                        long long num, long long max_chunks, unsigned* __restrict__ err) {
+    __shared__ uint32_t gw[MP_GWORDS + 2];
+    __shared__ uint16_t nx[2][256];                              // the next token's start from every bit
     __shared__ uint8_t gx[MP_G][32], gc[MP_G][32];
     const unsigned long long nbits = dev_nbits ? *dev_nbits : host_nbits;
     const long long nch = (long long)((nbits + 255) >> 8), nbytes = (long long)((nbits + 7) >> 3);
-    const int h = threadIdx.x >> 5, e = threadIdx.x & 31;
+    const int lane = threadIdx.x, h = lane >> 5, e = lane & 31;
     // a runs-mode stream (decode3 would take it for zero runs, which only parse3 checks) or one longer than
     // the buffers: declined to the chunk-map decoder, as parse3 declines it (status 512 | 1024)
-    if (blockIdx.x == 0 && threadIdx.x == 0 && (nch > max_chunks || runs_mode(CT, nbits, num))) atomicOr(err, 512u | 1024u);
-    build_lut_len<CT>(tl, P, threadIdx.x, 256);
+    if (blockIdx.x == 0 && lane == 0 && (nch > max_chunks || runs_mode(CT, nbits, num))) atomicOr(err, 512u | 1024u);
     long long gi = blockIdx.x;
-    uint32_t wv = 0u;
+    uint32_t wa = 0u, wb = 0u;                                   // words lane and 64 + lane of the group
     {
-        const long long c = gi * MP_G + h;
-        if (e < 10 && c < nch) wv = mp_word(s, nbytes, 8 * c + e);
+        const long long w0 = gi * MP_G * 8;
+        if (gi * MP_G < nch) {
+            wa = mp_word(s, nbytes, w0 + lane);
+            if (lane < MP_GWORDS - 64) wb = mp_word(s, nbytes, w0 + 64 + lane);
+        }
     }
     for (; gi < ngr; gi += gridDim.x) {
-        const long long c = gi * MP_G + h;
-        __syncthreads();                                         // (the previous group's LDS reads are done)
-        if (e < 10) w[h][e] = wv;
-        {
-            const long long cn = (gi + gridDim.x) * MP_G + h;
-            wv = (e < 10 && cn < nch) ? mp_word(s, nbytes, 8 * cn + e) : 0u;
-        }
-        if (gi * MP_G >= nch) {                                  // (past the stream's end: the identity)
+        const long long g0 = gi * MP_G;
+        if (g0 >= nch) {                                         // (past the stream's end: the identity)
             if (h == 0) gmap[gi * 32 + e] = (uint8_t)e;
             continue;
         }
-        __syncthreads();
-        // every bit's next token start (8 independent table lookups per lane instead of a token decode per
-        // step of each of the 32 walks)
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const int p = e + 32 * k;
-            const uint32_t t = e ? __builtin_amdgcn_alignbit(w[h][k], w[h][k + 1], 32 - e) : w[h][k];
-            nx[h][p] = (uint16_t)(p + tl[t >> 23]);
+        __builtin_amdgcn_wave_barrier();                         // (the previous group's LDS reads are done)
+        gw[lane] = wa;
+        if (lane < MP_GWORDS - 64) gw[64 + lane] = wb;
+        {
+            const long long gn = gi + gridDim.x, w0 = gn * MP_G * 8;
+            wa = 0u; wb = 0u;
+            if (gn < ngr && gn * MP_G < nch) {
+                wa = mp_word(s, nbytes, w0 + lane);
+                if (lane < MP_GWORDS - 64) wb = mp_word(s, nbytes, w0 + 64 + lane);
+            }
         }
-        __syncthreads();
-        const int lim = c < nch ? (int)min(256ll, (long long)nbits - 256 * c) : 0;
-        int pos = e, cnt = 0;
-        while (pos < lim) { pos = nx[h][pos]; cnt++; }             // (tokens starting before lim)
-        gx[h][e] = c < nch ? (uint8_t)((pos - 256) & 31) : (uint8_t)e;   // (identity past the stream's end)
-        gc[h][e] = (uint8_t)cnt;
-        __syncthreads();
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+        for (int q = 0; q < MP_G / 2; q++) {
+            const int j = 2 * q + h;                             // the group's chunk this half-wave walks
+            const long long c = g0 + j;
+            // every bit's next token start (8 positions per lane, lengths in registers)
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int p = e + 32 * k;
+                const uint32_t w0 = gw[8 * j + k], w1 = gw[8 * j + k + 1];
+                const uint32_t t = e ? __builtin_amdgcn_alignbit(w0, w1, 32 - e) : w0;
+                nx[h][p] = (uint16_t)(p + token_len_bf<CT>(t, P));
+            }
+            __builtin_amdgcn_wave_barrier();
+            const int lim = c < nch ? (int)min(256ll, (long long)nbits - 256 * c) : 0;
+            int pos = e, cnt = 0;
+            while (pos < lim) { pos = nx[h][pos]; cnt++; }       // (tokens starting before lim)
+            gx[j][e] = c < nch ? (uint8_t)((pos - 256) & 31) : (uint8_t)e;   // (identity past the stream's end)
+            gc[j][e] = (uint8_t)cnt;
+            __builtin_amdgcn_wave_barrier();
+        }
         if (h == 0) {
             // from group entry e: the group's exit, and its chunks' records (entry | tokens << 8) for maps_rec_kernel
             int x = e;
@@ -273,7 +290,7 @@ extern "C" int dc_launch_maps_parse(const uint8_t* s, const unsigned long long* 
     switch (P->ct) {
 #define DC_MAPS_CASE(C)                                                                                          \
     case C:                                                                                                      \
-        hipLaunchKernelGGL(maps_group_kernel<C>, gg, dim3(256), 0, st, s, *P, dev_nbits, host_nbits, gmap, gtab, \
+        hipLaunchKernelGGL(maps_group_kernel<C>, gg, dim3(64), 0, st, s, *P, dev_nbits, host_nbits, gmap, gtab, \
                            ngr, num, D3->max_chunks, D3->err);                                                      \
         break;
         DC_MAPS_CASE(5) DC_MAPS_CASE(6) DC_MAPS_CASE(7) DC_MAPS_CASE(11)

@@ -1,8 +1,8 @@
-"""Print the headline numbers of a bench.py JSON line (the first line of the file)."""
+"""Print the headline numbers of a bench.py JSON line (the file's first line that starts with "{")."""
 import json
 import sys
 
-d = json.loads(open(sys.argv[1]).readline())
+d = json.loads(next(l for l in open(sys.argv[1]) if l.startswith("{")))   # (gloo prints before the line)
 rf = d.get("roofline", {})
 print(f"value {d['value']} GB/s, {d['ms_per_step']} ms/step, n_gpus {d['n_gpus']}, self_check {d.get('self_check')}, "
       f"fast_path {d.get('decoder_fast_path')}")
