@@ -542,9 +542,19 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
         seed = [1]
         acks = []
         ack_buf = torch.zeros((max(steps, warmup) + 1, 2), dtype=torch.int32, pin_memory=True)
-        CT9_PHASES = ["crcf_final_kernel (sender CRC: combine of the encoder's block CRCs)", "channel copy",
-                      "flip_bits_kernel", "crcf_blocks + crcf_final (receiver CRC, damaged copy)",
-                      "crcf_blocks + crcf_final (resend copy with its CRC + check)"]
+        CT9_PHASES = (["crcf_final_kernel (sender CRC: combine of the encoder's block CRCs)", "channel copy",
+                       "flip_bits_kernel", "crcf_blocks + crcf_final (receiver CRC, damaged copy)",
+                       "crc_blocks<copy> + crc_final2 (resend copy with its CRC + check)"]
+                      if os.environ.get("DC_CT9_FUSED", "0") == "1" else
+                      ["crc_blocks + crc_final2 (sender CRC pass)", "channel copy", "flip_bits_kernel",
+                       "crc_blocks + crc_final2 (receiver CRC, damaged copy)",
+                       "crc_blocks<copy> + crc_final2 (resend copy with its CRC + check)"])
+
+        # DC_CT9_FUSED=1: the sender's CRC inside the encoder's tiles and the receiver's by the 16 KiB-block kernels
+        # (dc_encode_crc_device, dc_crc32_stream_device); default: separate 32 KiB-block CRC passes
+        # (dc_crc32_device_async), which measured faster.  The resend always copies and CRCs
+        # in one pass (dc_crc_resend_crc_device).
+        fused_crc = os.environ.get("DC_CT9_FUSED", "0") == "1"
 
         def step(ev=None, ph=None):                          # noqa: F811 -- the CT9 variant of the step
             def mark(i):
@@ -552,8 +562,13 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
                     ph[i].record(ext)
             if ev:
                 ev[0].record(ext)
-            L.encode_crc_device(ct, xs.data_ptr(), n, stream.data_ptr(), d_nbits.data_ptr(), d_crc.data_ptr(),
-                                idx0=idx0, type_=typ, mask17=mask17)
+            if fused_crc:
+                L.encode_crc_device(ct, xs.data_ptr(), n, stream.data_ptr(), d_nbits.data_ptr(), d_crc.data_ptr(),
+                                    idx0=idx0, type_=typ, mask17=mask17)
+            else:
+                L.encode_device(ct, xs.data_ptr(), n, stream.data_ptr(), idx0=idx0, type_=typ, mask17=mask17,
+                                total_ptr=d_nbits.data_ptr())
+                L.crc32_device_async(stream.data_ptr(), nbytes, d_crc.data_ptr())
             mark(0)
             with torch.cuda.stream(ext):
                 rcv[:nbytes].copy_(stream[:nbytes])
@@ -561,7 +576,10 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
             L.flip_bits_device(rcv.data_ptr(), nbits, nflip, seed[0])
             seed[0] += nflip
             mark(2)
-            L.crc32_stream_device(rcv.data_ptr(), nbytes, d_crc.data_ptr() + 4)
+            if fused_crc:
+                L.crc32_stream_device(rcv.data_ptr(), nbytes, d_crc.data_ptr() + 4)
+            else:
+                L.crc32_device_async(rcv.data_ptr(), nbytes, d_crc.data_ptr() + 4)
             mark(3)
             L.crc_resend_crc_device(d_crc.data_ptr(), stream.data_ptr(), rcv.data_ptr(), nbytes, d_cnt.data_ptr())
             mark(4)

@@ -1157,11 +1157,19 @@ __device__ __forceinline__ uint32_t xpow8n(unsigned long long n, const uint32_t*
 #ifndef DC_CRC_STAGE
 #define DC_CRC_STAGE 0                  // (staging full blocks through LDS: 66 -> 71 us per pass, off)
 #endif
+// COPY (the CT9 resend): only when the gate's two CRCs differ (the received copy was damaged), the run is also
+// written to dst -- the resent copy and its CRC in one pass -- and gate_count counts the resends
+template <bool COPY>
 __global__ __launch_bounds__(256) void crc_blocks_kernel(const uint8_t* __restrict__ s, long long nbytes,
                                                          const uint32_t* __restrict__ tab_g,
                                                          const uint32_t* __restrict__ kpow_g,
                                                          const uint32_t* __restrict__ x2n_g,
-                                                         uint32_t* __restrict__ part) {
+                                                         uint32_t* __restrict__ part, uint8_t* __restrict__ dst,
+                                                         const uint32_t* __restrict__ gate, unsigned* __restrict__ gate_count) {
+    if (COPY) {
+        if (gate[0] == gate[1]) return;
+        if (gate_count && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(gate_count, 1u);
+    }
     __shared__ uint32_t tab[DC_CRC_NIB ? 1 : 4][256];
     __shared__ uint32_t nib[8 * 16];
     __shared__ uint32_t x2n[32];
@@ -1169,7 +1177,10 @@ __global__ __launch_bounds__(256) void crc_blocks_kernel(const uint8_t* __restri
     // DC_CRC_STAGE: a full block is read with coalesced 16-byte loads (a wave instruction covers 1 KiB)
     // and handed to the lanes' 128-byte runs through LDS rows of 36 words (b128 reads conflict-free):
     // each lane loading its own run touched 64 lines per instruction (~2.6 TB/s)
-    __shared__ __attribute__((aligned(16))) uint32_t stg[DC_CRC_STAGE ? 256 * 36 : 4];
+    // (COPY stages too: the copy's stores then cover 1 KiB per wave instruction like its loads -- per-lane runs
+    // stored 64 lines per instruction and the resend took 97 us per 163 MB, about copy + CRC)
+    constexpr bool STAGE = DC_CRC_STAGE || COPY;
+    __shared__ __attribute__((aligned(16))) uint32_t stg[STAGE ? 256 * 36 : 4];
     const int t = threadIdx.x;
     for (int k = 0; k < (DC_CRC_NIB ? 1 : 4); k++) tab[k][t] = tab_g[k * 256 + t];
     if (t < 128) {                                   // nibble j of the word c: byte table 3 - j/2
@@ -1184,12 +1195,18 @@ __global__ __launch_bounds__(256) void crc_blocks_kernel(const uint8_t* __restri
     for (long long b = blockIdx.x; b < nblk; b += gridDim.x) {
         const long long st = b * CRC_BLK + (long long)t * CRC_RUN;
         uint32_t r = 0;
-        const bool staged = DC_CRC_STAGE && al && (b + 1) * CRC_BLK <= nbytes;     // (uniform: a full block)
+        const bool staged = STAGE && al && (b + 1) * CRC_BLK <= nbytes &&
+                            (!COPY || (reinterpret_cast<uintptr_t>(dst) & 15u) == 0);   // (uniform: a full block)
         if (staged) {
             const uint4* g4 = reinterpret_cast<const uint4*>(s + b * CRC_BLK);
             uint4 v[CRC_RUN / 16];
 #pragma unroll
             for (int i = 0; i < CRC_RUN / 16; i++) v[i] = g4[t + 256 * i];
+            if (COPY) {
+                uint4* d4 = reinterpret_cast<uint4*>(dst + b * CRC_BLK);
+#pragma unroll
+                for (int i = 0; i < CRC_RUN / 16; i++) d4[t + 256 * i] = v[i];
+            }
 #pragma unroll
             for (int i = 0; i < CRC_RUN / 16; i++) {
                 const int u = t + 256 * i;                      // 16-byte unit: run u / 8, piece u % 8
@@ -1197,13 +1214,18 @@ __global__ __launch_bounds__(256) void crc_blocks_kernel(const uint8_t* __restri
             }
             __syncthreads();
         }
-        if (al && st + CRC_RUN <= nbytes) {
+        if (al && st + CRC_RUN <= nbytes && (!COPY || (reinterpret_cast<uintptr_t>(dst) & 15u) == 0)) {
             const uint4* p4 = reinterpret_cast<const uint4*>(s + st);
             uint4 q[CRC_RUN / 16];
 #pragma unroll
             for (int i = 0; i < CRC_RUN / 16; i++)
                 q[i] = DC_CRC_DIAG == 2 ? make_uint4((uint32_t)st + i, (uint32_t)b, 3u * i, 7u)   // (diagnostic: no loads)
                                         : staged ? *reinterpret_cast<const uint4*>(&stg[t * 36 + 4 * i]) : p4[i];
+            if (COPY && !staged) {
+                uint4* d4 = reinterpret_cast<uint4*>(dst + st);
+#pragma unroll
+                for (int i = 0; i < CRC_RUN / 16; i++) d4[i] = q[i];
+            }
 #pragma unroll
             for (int i = 0; i < CRC_RUN / 16; i++) {
                 const uint32_t w[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
@@ -1223,7 +1245,11 @@ __global__ __launch_bounds__(256) void crc_blocks_kernel(const uint8_t* __restri
                 }
             }
         } else {
-            for (long long p = st; p < st + CRC_RUN && p < nbytes; p++) r = tab[0][(r ^ s[p]) & 0xFFu] ^ (r >> 8);
+            for (long long p = st; p < st + CRC_RUN && p < nbytes; p++) {
+                const uint8_t v = s[p];
+                if (COPY) dst[p] = v;
+                r = tab[0][(r ^ v) & 0xFFu] ^ (r >> 8);
+            }
         }
         const long long blen = min((long long)CRC_BLK, nbytes - b * CRC_BLK);
         uint32_t v;
@@ -1302,8 +1328,11 @@ struct CrcFin2 {
 __device__ __forceinline__ uint32_t mul_tab(const uint32_t (*T)[256], uint32_t a) {
     return (T[0][a & 255u] ^ T[1][(a >> 8) & 255u]) ^ (T[2][(a >> 16) & 255u] ^ T[3][a >> 24]);
 }
+// gate (the CT9 resend): only when its two CRCs differ; ref / count: a result != *ref counts in *count
 __global__ __launch_bounds__(CF2_T) void crc_final2_kernel(const uint32_t* __restrict__ part, CrcFin2 F, uint32_t init,
-                                                           uint32_t* __restrict__ out) {
+                                                           uint32_t* __restrict__ out, const uint32_t* __restrict__ gate,
+                                                           const uint32_t* __restrict__ ref, unsigned* __restrict__ count) {
+    if (gate && gate[0] == gate[1]) return;
     __shared__ uint32_t T[1 + CF2_L][4][256];
     __shared__ uint32_t B[1 + CF2_L][32];
     __shared__ uint32_t red[CF2_T];
@@ -1347,7 +1376,9 @@ __global__ __launch_bounds__(CF2_T) void crc_final2_kernel(const uint32_t* __res
     if (t == 0) {
         uint32_t R = red[0];
         if (F.nblk > 0) R = multmodp(F.kl, R) ^ part[F.nblk - 1];
-        *out = ~(R ^ multmodp(F.xn, ~init));
+        const uint32_t crc = ~(R ^ multmodp(F.xn, ~init));
+        *out = crc;
+        if (ref && count && crc != *ref) atomicAdd(count, 1u);
     }
 }
 
@@ -1702,13 +1733,21 @@ extern "C" int dc_launch_med64(const double* x, long long n, void* scratch, doub
 extern "C" long long dc_crc_parts(long long nbytes) { return (nbytes + CRC_BLK - 1) / CRC_BLK; }
 extern "C" int dc_crc_run_bytes(void) { return CRC_RUN; }
 
-extern "C" int dc_launch_crc32(const uint8_t* s, long long nbytes, const uint32_t* d_tab, const uint32_t* d_x2n,
-                               uint32_t* d_parts, uint32_t init, uint32_t* d_out, hipStream_t st) {
+static int launch_crc32(const uint8_t* s, long long nbytes, const uint32_t* d_tab, const uint32_t* d_x2n,
+                        uint32_t* d_parts, uint32_t init, uint32_t* d_out, uint8_t* dst, const uint32_t* gate,
+                        unsigned* count, hipStream_t st) {
     long long nblk = dc_crc_parts(nbytes);
     if (nbytes > 0) {                                     // d_tab: 4 slicing tables, then kpow[256]
         long long g = nblk > 4096 ? 4096 : nblk;
-        hipLaunchKernelGGL(crc_blocks_kernel, dim3((unsigned)g), dim3(256), 0, st, s, nbytes, d_tab, d_tab + 1024,
-                           d_x2n, d_parts);
+        if (gate)
+            hipLaunchKernelGGL(crc_blocks_kernel<true>, dim3((unsigned)g), dim3(256), 0, st, s, nbytes, d_tab,
+                               d_tab + 1024, d_x2n, d_parts, dst, gate, count);
+        else
+            hipLaunchKernelGGL(crc_blocks_kernel<false>, dim3((unsigned)g), dim3(256), 0, st, s, nbytes, d_tab,
+                               d_tab + 1024, d_x2n, d_parts, (uint8_t*)nullptr, (const uint32_t*)nullptr,
+                               (unsigned*)nullptr);
+    } else if (gate) {
+        return -2;                                        // (the resend of an empty stream: nothing to copy)
     }
     if (DC_CRC_FIN2) {
         CrcFin2 F2;
@@ -1721,9 +1760,11 @@ extern "C" int dc_launch_crc32(const uint8_t* s, long long nbytes, const uint32_
         for (int l = 0; l < CF2_L; l++) { F2.kc[1 + l] = kp; kp = h_mult(kp, kp); }
         F2.kl = h_xpow8n((unsigned long long)(nbytes - m2 * CRC_BLK));
         F2.xn = h_xpow8n((unsigned long long)nbytes);
-        hipLaunchKernelGGL(crc_final2_kernel, dim3(1), dim3(CF2_T), 0, st, d_parts, F2, init, d_out);
+        hipLaunchKernelGGL(crc_final2_kernel, dim3(1), dim3(CF2_T), 0, st, d_parts, F2, init, d_out, gate,
+                           gate ? gate : (const uint32_t*)nullptr, gate ? count + 1 : (unsigned*)nullptr);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
+    if (gate) return -2;                                  // (the resend form needs the 1024-thread combine)
     CrcFin F;
     F.nblk = nbytes > 0 ? nblk : 0;
     const long long m = F.nblk > 0 ? F.nblk - 1 : 0;
@@ -1737,6 +1778,18 @@ extern "C" int dc_launch_crc32(const uint8_t* s, long long nbytes, const uint32_
     (void)d_x2n;
     hipLaunchKernelGGL(crc_final_kernel, dim3(1), dim3(256), 0, st, d_parts, F, init, d_out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int dc_launch_crc32(const uint8_t* s, long long nbytes, const uint32_t* d_tab, const uint32_t* d_x2n,
+                               uint32_t* d_parts, uint32_t init, uint32_t* d_out, hipStream_t st) {
+    return launch_crc32(s, nbytes, d_tab, d_x2n, d_parts, init, d_out, nullptr, nullptr, nullptr, st);
+}
+// the CT9 resend in one pass: if crc2[0] != crc2[1] (sender's vs receiver's CRC), copy src -> dst computing the
+// copy's CRC into crc2[1], count the resend in count[0] and a copy whose CRC still differs in count[1]
+extern "C" int dc_launch_crc32_resend(const uint8_t* src, uint8_t* dst, long long nbytes, const uint32_t* d_tab,
+                                      const uint32_t* d_x2n, uint32_t* d_parts, uint32_t* crc2, unsigned* count,
+                                      hipStream_t st) {
+    return launch_crc32(src, nbytes, d_tab, d_x2n, d_parts, 0u, crc2 + 1, dst, crc2, count, st);
 }
 
 // Shard stream: bits [start_bit, start_bit + 8*nout) of s as nout bytes starting at bit 0 (MSB first),
