@@ -593,8 +593,13 @@ __device__ __forceinline__ Pre3 prefetch3(__amdgpu_buffer_rsrc_t rr, __amdgpu_bu
 }
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return wave_total(v); }
 
+// four waves per SIMD (<= 128 VGPRs): round 5's dense buffer template, shard flags and pending rounds had taken the
+// kernel to 129-145 VGPRs, three waves per SIMD, and decode3 from 97 to 115 us at 2^26 U10
+#ifndef DC_D3_MINW
+#define DC_D3_MINW 4
+#endif
 template <int CT, int SEG, int CAP>
-__global__ __launch_bounds__(256) void decode3_kernel(const uint8_t* __restrict__ s, Params P, Dec3Bufs D3,
+__global__ __launch_bounds__(256, DC_D3_MINW) void decode3_kernel(const uint8_t* __restrict__ s, Params P, Dec3Bufs D3,
                                                      const unsigned long long* dev_nbits, unsigned long long host_nbits,
                                                      float* __restrict__ out, long long num, uint32_t epoch) {
     __shared__ Lut3 T;
