@@ -546,14 +546,15 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
                        "flip_bits_kernel", "crcf_blocks + crcf_final (receiver CRC, damaged copy)",
                        "crc_blocks<copy> + crc_final2 (resend copy with its CRC + check)"]
                       if os.environ.get("DC_CT9_FUSED", "0") == "1" else
-                      ["crc_blocks + crc_final2 (sender CRC pass)", "channel copy", "flip_bits_kernel",
-                       "crc_blocks + crc_final2 (receiver CRC, damaged copy)",
+                      ["(encode call beyond its kernel)", "crc_blocks<copy> + crc_final2 (send: channel copy + sender CRC)",
+                       "flip_bits_kernel", "crc_blocks + crc_final2 (receiver CRC, damaged copy)",
                        "crc_blocks<copy> + crc_final2 (resend copy with its CRC + check)"])
 
-        # DC_CT9_FUSED=1: the sender's CRC inside the encoder's tiles and the receiver's by the 16 KiB-block kernels
-        # (dc_encode_crc_device, dc_crc32_stream_device); default: separate 32 KiB-block CRC passes
-        # (dc_crc32_device_async), which measured faster.  The resend always copies and CRCs
-        # in one pass (dc_crc_resend_crc_device).
+        # Default: the send copies the stream into the receiver's buffer and CRCs the bytes it sends in one pass
+        # (dc_crc32_copy_device), the receiver CRCs what arrived (dc_crc32_device_async), the resend copies and
+        # CRCs in one pass (dc_crc_resend_crc_device).  DC_CT9_FUSED=1: the sender's CRC inside the encoder's
+        # tiles and the receiver's by the 16 KiB-block kernels (dc_encode_crc_device, dc_crc32_stream_device),
+        # which measured slower.
         fused_crc = os.environ.get("DC_CT9_FUSED", "0") == "1"
 
         def step(ev=None, ph=None):                          # noqa: F811 -- the CT9 variant of the step
@@ -565,13 +566,15 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
             if fused_crc:
                 L.encode_crc_device(ct, xs.data_ptr(), n, stream.data_ptr(), d_nbits.data_ptr(), d_crc.data_ptr(),
                                     idx0=idx0, type_=typ, mask17=mask17)
+                mark(0)
+                with torch.cuda.stream(ext):
+                    rcv[:nbytes].copy_(stream[:nbytes])
             else:
                 L.encode_device(ct, xs.data_ptr(), n, stream.data_ptr(), idx0=idx0, type_=typ, mask17=mask17,
                                 total_ptr=d_nbits.data_ptr())
-                L.crc32_device_async(stream.data_ptr(), nbytes, d_crc.data_ptr())
-            mark(0)
-            with torch.cuda.stream(ext):
-                rcv[:nbytes].copy_(stream[:nbytes])
+                mark(0)
+                # the send: the channel copy, the sender's CRC of the bytes it sends computed in the same pass
+                L.crc32_copy_device(stream.data_ptr(), rcv.data_ptr(), nbytes, d_crc.data_ptr())
             mark(1)
             L.flip_bits_device(rcv.data_ptr(), nbits, nflip, seed[0])
             seed[0] += nflip

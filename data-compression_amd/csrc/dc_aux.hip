@@ -1166,7 +1166,7 @@ __global__ __launch_bounds__(256) void crc_blocks_kernel(const uint8_t* __restri
                                                          const uint32_t* __restrict__ x2n_g,
                                                          uint32_t* __restrict__ part, uint8_t* __restrict__ dst,
                                                          const uint32_t* __restrict__ gate, unsigned* __restrict__ gate_count) {
-    if (COPY) {
+    if (COPY && gate) {
         if (gate[0] == gate[1]) return;
         if (gate_count && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(gate_count, 1u);
     }
@@ -1739,7 +1739,7 @@ static int launch_crc32(const uint8_t* s, long long nbytes, const uint32_t* d_ta
     long long nblk = dc_crc_parts(nbytes);
     if (nbytes > 0) {                                     // d_tab: 4 slicing tables, then kpow[256]
         long long g = nblk > 4096 ? 4096 : nblk;
-        if (gate)
+        if (dst)
             hipLaunchKernelGGL(crc_blocks_kernel<true>, dim3((unsigned)g), dim3(256), 0, st, s, nbytes, d_tab,
                                d_tab + 1024, d_x2n, d_parts, dst, gate, count);
         else
@@ -1783,6 +1783,11 @@ static int launch_crc32(const uint8_t* s, long long nbytes, const uint32_t* d_ta
 extern "C" int dc_launch_crc32(const uint8_t* s, long long nbytes, const uint32_t* d_tab, const uint32_t* d_x2n,
                                uint32_t* d_parts, uint32_t init, uint32_t* d_out, hipStream_t st) {
     return launch_crc32(s, nbytes, d_tab, d_x2n, d_parts, init, d_out, nullptr, nullptr, nullptr, st);
+}
+// the CT9 send: src copied to dst (the channel) and the CRC of what is sent into *d_out, one pass
+extern "C" int dc_launch_crc32_copy(const uint8_t* src, uint8_t* dst, long long nbytes, const uint32_t* d_tab,
+                                    const uint32_t* d_x2n, uint32_t* d_parts, uint32_t* d_out, hipStream_t st) {
+    return launch_crc32(src, nbytes, d_tab, d_x2n, d_parts, 0u, d_out, dst, nullptr, nullptr, st);
 }
 // the CT9 resend in one pass: if crc2[0] != crc2[1] (sender's vs receiver's CRC), copy src -> dst computing the
 // copy's CRC into crc2[1], count the resend in count[0] and a copy whose CRC still differs in count[1]

@@ -1391,6 +1391,26 @@ int dc_crc_resend_device(const uint32_t* d_crc2, const void* d_src, void* d_dst,
     return DC_OK;
 }
 
+/* CT9 send: the stream copied to the receiver's buffer (the channel) with the CRC of the bytes sent computed in
+   the same pass (*d_crc, device) */
+int dc_crc32_copy_device(const void* d_src, void* d_dst, long long nbytes, uint32_t* d_crc) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (nbytes < 0 || nbytes > 0x7FFFFF00ll - 64 || (((uintptr_t)d_src | (uintptr_t)d_dst) & 15u))
+        return seterr(DC_ERR_ARG, "crc copy: 16-byte aligned streams below 2 GiB");
+    if (nbytes == 0) return crc_into(d_src, 0, d_crc);
+    const long long parts = dc_crc_parts(nbytes) + 1;
+    if (parts > G.crcparts_cap) {
+        if (G.d_crcparts) HIPCHK(hipFree(G.d_crcparts));
+        HIPCHK(hipMalloc((void**)&G.d_crcparts, parts * 4 + 1024));
+        G.crcparts_cap = parts;
+    }
+    if (dc_launch_crc32_copy((const uint8_t*)d_src, (uint8_t*)d_dst, nbytes, G.d_crctab, G.d_x2n, G.d_crcparts, d_crc,
+                             G.st))
+        return seterr(DC_ERR_HIP, "crc copy launch failed");
+    return DC_OK;
+}
+
 int dc_crc32_device_async(const void* d_s, long long nbytes, uint32_t* d_crc) {
     int rc = ensure_init();
     if (rc) return rc;

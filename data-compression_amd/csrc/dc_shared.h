@@ -217,6 +217,8 @@ long long dc_crc_parts(long long nbytes);
 int dc_crc_run_bytes(void);
 int dc_launch_crc32(const uint8_t* s, long long nbytes, const uint32_t* d_tab, const uint32_t* d_x2n,
                     uint32_t* d_parts, uint32_t init, uint32_t* d_out, dc_hip_stream st);
+int dc_launch_crc32_copy(const uint8_t* src, uint8_t* dst, long long nbytes, const uint32_t* d_tab,
+                         const uint32_t* d_x2n, uint32_t* d_parts, uint32_t* d_out, dc_hip_stream st);
 int dc_launch_crc32_resend(const uint8_t* src, uint8_t* dst, long long nbytes, const uint32_t* d_tab,
                            const uint32_t* d_x2n, uint32_t* d_parts, uint32_t* crc2, unsigned* count, dc_hip_stream st);
 int dc_launch_bit_shift_copy(const uint8_t* s, long long sbytes, unsigned long long start_bit, unsigned long long nbits,

@@ -39,7 +39,7 @@ EXT_SYMBOLS = [
     "dc_get_abs_error_bound", "dc_stream_capacity", "dc_encode_device", "dc_encode_result",
     "dc_decode_device", "dc_decode_finish", "dc_to_small_device", "dc_med_device", "dc_crc32_device",
     "dc_decode_chunk_bits_value", "dc_ct1_encode_device", "dc_ct1_decode_device", "dc_encode_bits_device",
-    "dc_crc32_device_async", "dc_encode_crc_device", "dc_crc32_stream_device", "dc_crc_resend_crc_device",
+    "dc_crc32_device_async", "dc_crc32_copy_device", "dc_encode_crc_device", "dc_crc32_stream_device", "dc_crc_resend_crc_device",
     "dc_hash_device", "dc_copy_rate_device", "dc_flip_bits_device", "dc_decode_shard_device", "dc_decode_shard_fix",
     "dc_halo_encode_device", "dc_halo_decode_device",
     "dc64_stream_capacity", "dc64_encode_device", "dc64_encode_result", "dc64_decode_device", "dc64_decode_finish",
@@ -379,6 +379,11 @@ class Lib:
         """dc_encode_crc_device: the encode (start bit 0) plus the stream's zlib CRC-32 into *crc_ptr (device)."""
         self.check(self.L.dc_encode_crc_device(ct, x_ptr, n, idx0, type_, mask17, out_ptr, total_ptr, crc_ptr),
                    "dc_encode_crc_device")
+
+    def crc32_copy_device(self, src_ptr, dst_ptr, nbytes, crc_ptr):
+        """dc_crc32_copy_device: the CT9 send -- src copied to dst with the CRC-32 of the bytes sent (device)."""
+        self.check(self.L.dc_crc32_copy_device(C.c_void_p(src_ptr), C.c_void_p(dst_ptr), C.c_longlong(nbytes),
+                                               C.c_void_p(crc_ptr)), "dc_crc32_copy_device")
 
     def crc32_stream_device(self, s_ptr, nbytes, crc_ptr):
         self.check(self.L.dc_crc32_stream_device(s_ptr, nbytes, crc_ptr), "dc_crc32_stream_device")

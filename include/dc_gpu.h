@@ -178,6 +178,9 @@ int dc_copy_rate_device(const void* d_src, void* d_dst, long long bytes, int rep
 int dc_encode_crc_device(int ct, const void* d_x, long long n, long long idx0, int type, uint32_t mask17, void* d_out,
                          unsigned long long* d_total_bits, uint32_t* d_crc);
 int dc_crc32_stream_device(const void* d_s, long long nbytes, uint32_t* d_crc);
+/* CT9 send: d_src copied to d_dst (the channel) and the zlib CRC-32 of the bytes sent into *d_crc (device), in one
+   pass (16-byte aligned, < 2 GiB) */
+int dc_crc32_copy_device(const void* d_src, void* d_dst, long long nbytes, uint32_t* d_crc);
 int dc_crc_resend_crc_device(uint32_t* d_crc2, const void* d_src, void* d_dst, long long nbytes, unsigned* d_count);
 /* BER fault injection (CT8/CT9 flow): flip `count` bits of the stream at positions
  * splitmix64(seed + i) mod nbits (MSB-first in each byte, as bit_flip).  The stream buffer must be

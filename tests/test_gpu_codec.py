@@ -624,3 +624,45 @@ def test_crc_resend_crc_device(dc):
     dc.crc_resend_crc_device(crc2.data_ptr(), src.data_ptr(), dst.data_ptr(), nbytes, cnt.data_ptr())
     dc.synchronize()
     assert cnt.tolist() == [1, 0]
+
+
+@pytest.mark.parametrize("nbytes", [1, 16, 4095, 32768, 32769, 65536 + 48, (1 << 20) + 7, 5 * (1 << 22) + 13])
+def test_crc32_copy_device(dc, nbytes):
+    """The CT9 send (dc_crc32_copy_device): the destination holds the source's bytes (and nothing past them
+    changes), the CRC is zlib's of the bytes sent -- full 32 KiB blocks staged, the last block by bytes."""
+    import zlib
+    import torch
+    rng = np.random.RandomState(nbytes & 0xFFFF)
+    h = rng.randint(0, 256, size=nbytes + 64, dtype=np.uint8)
+    src = torch.from_numpy(h).cuda()
+    dst = torch.full((nbytes + 64,), 0x5A, dtype=torch.uint8, device="cuda")
+    c = torch.zeros(4, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    dc.crc32_copy_device(src.data_ptr(), dst.data_ptr(), nbytes, c.data_ptr())
+    dc.synchronize()
+    assert (int(c[0].item()) & 0xFFFFFFFF) == zlib.crc32(h[:nbytes].tobytes())
+    assert torch.equal(dst[:nbytes], src[:nbytes])
+    assert bool((dst[nbytes:] == 0x5A).all())
+
+
+@pytest.mark.parametrize("nbytes", [3 * 32768 * 32 + 5, (1 << 22) + 1])
+def test_crc_resend_crc_device_large(dc, nbytes):
+    """The resend at sizes of many 32 KiB blocks with a ragged tail: replaced once, its CRC zlib's, gated after."""
+    import zlib
+    import torch
+    h = np.random.RandomState(11).randint(0, 256, size=nbytes + 64, dtype=np.uint8)
+    src = torch.from_numpy(h).cuda()
+    dst = src.clone()
+    dst[nbytes // 2] ^= 1
+    dst[nbytes - 1] ^= 128
+    crc2 = torch.zeros(2, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(2, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    dc.crc32_device_async(src.data_ptr(), nbytes, crc2.data_ptr())
+    dc.crc32_device_async(dst.data_ptr(), nbytes, crc2.data_ptr() + 4)
+    dc.crc_resend_crc_device(crc2.data_ptr(), src.data_ptr(), dst.data_ptr(), nbytes, cnt.data_ptr())
+    dc.synchronize()
+    assert cnt.tolist() == [1, 0]
+    assert torch.equal(dst[:nbytes], src[:nbytes])
+    assert (int(crc2[1].item()) & 0xFFFFFFFF) == zlib.crc32(h[:nbytes].tobytes())
+
