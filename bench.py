@@ -895,6 +895,8 @@ def main():
         print(f"bench.py: decoder status 0x{R['status']:x} in the timed steps (slow path not timed)", file=sys.stderr)
         sys.exit(1)
     kernels = kernel_table(ct, n, nbytes, R["kavg"], R["v3"], R.get("enc_mode", 1), R.get("runs", False))
+    for nm, ms_ in R.get("ct9", {}).get("phase_ms", {}).items():   # (as line_for: the CT9 launches too)
+        kernels[nm] = (ms_, 2.0 * nbytes if "copy" in nm else (float(nbytes) if "damaged copy" in nm else 0.0))
     dname = main_line["dominant"]["kernel"]
     achievable, copy_how = copy_bandwidth(C.L, C.dev, n)
     traffic, traffic_src, ktraffic = None, None, None
