@@ -564,6 +564,9 @@ struct MedRound {
     D wk[MXC_T / 64];                                       // k before it
     T wv[MXC_T / 64];                                       // (elements: its value)
     int wy[MXC_T / 64];                                     // (chunks: 1 when it had no transducer for E)
+    uint32_t wt2[MXC_T / 64];                               // (two-binade element rounds: the wave's units in E + 1,
+    int wb2[MXC_T / 64];                                    //  its last element E + 1 does not take (-1: none),
+    uint32_t wi2[MXC_T / 64];                               //  the E + 1 units through the leaving element)
 };
 
 // One round of the composition over MXC_T threads, each holding P pieces (chunks or elements) with units d0[j] /
@@ -572,12 +575,18 @@ struct MedRound {
 // that stops, k before it, the piece's value (v) and why -- or none (returns 1 << 30) and the k after all.  Two
 // barriers when no thread has a tie (plain prefix sums of the units, DPP wave scans), the transducer block scan
 // otherwise.  Every thread returns the same values.
-template <typename T, int P>
+//
+// TWO (float element rounds): e2 / bad2 are the pieces' units in binade E + 1 (no tie there) and whether E + 1
+// does not take them; two[0..3] return whether the E + 1 sums are usable (no tie in E, no wave total >= TOP),
+// the E + 1 units of all live pieces, those through the leaving piece, and the last piece E + 1 does not take
+// (-1: none) -- so that a sum crossing from E into E + 1 finishes the chunk in the same round (the caller checks).
+template <typename T, int P, bool TWO = false>
 __device__ __forceinline__ int med_round(const typename MedFP<T>::D (&d0)[P], const typename MedFP<T>::D (&d1)[P],
                                          const bool (&stop)[P], const bool (&live)[P], const T (&v)[P], const int (&why)[P],
                                          bool tie, typename MedFP<T>::D k0, MedRound<T>& X, MTr<typename MedFP<T>::D>* wt,
                                          typename MedFP<T>::D& k_out, T& v_out, int& why_out,
-                                         unsigned long long* pf = nullptr) {
+                                         unsigned long long* pf = nullptr, const uint32_t* e2 = nullptr,
+                                         const bool* bad2 = nullptr, uint32_t* two = nullptr) {
     typedef MedFP<T> FP;
     typedef typename FP::D D;
     constexpr D TOP = D(1) << (FP::M + 1);
@@ -615,6 +624,16 @@ __device__ __forceinline__ int med_round(const typename MedFP<T>::D (&d0)[P], co
         }
     }
     const unsigned long long stb = __ballot(st), tb = __ballot(tie);
+    uint32_t u2 = 0, incw2 = 0;
+    if (TWO) {
+        int myb = -1;
+#pragma unroll
+        for (int j = 0; j < P; j++) { u2 += e2[j]; myb = bad2[j] ? tid * P + j : myb; }
+        incw2 = wave_scan_incl(u2);                         // (P x 2^24 per thread, 64 threads: < 2^32)
+        const unsigned long long bb = __ballot(myb >= 0);
+        if (lane == 63) X.wt2[wid] = incw2;
+        if (lane == 0) X.wb2[wid] = bb ? __builtin_amdgcn_readlane(myb, 63 - __clzll((long long)bb)) : -1;
+    }
     if (lane == 63) X.wt[wid] = incw;
     if (lane == 0) { X.wtie[wid] = stb ? (int)(__ffsll((long long)stb) - 1) : 64; X.wtf[wid] = tb != 0; }
     MRS(1);
@@ -651,8 +670,21 @@ __device__ __forceinline__ int med_round(const typename MedFP<T>::D (&d0)[P], co
         before_ok = sbm == 0 && lane <= fsl;
         const unsigned long long kx = (unsigned long long)k0 + woff + incw - (unsigned long long)uc;
         k = (D)min(kx, (unsigned long long)TOP);
+        if (TWO) {
+            const uint32_t wv2 = X.wt2[lw];
+            const int wb2 = X.wb2[lw];
+            const bool big = __ballot(lane < NW && wv2 >= (uint32_t)TOP) != 0ull;
+            const uint32_t wp2 = wave_scan_incl(lane < NW ? min(wv2, (uint32_t)TOP) : 0u);
+            const unsigned long long bb2 = __ballot(lane < NW && wb2 >= 0);
+            two[0] = big ? 0u : 1u;
+            two[1] = (uint32_t)__builtin_amdgcn_readlane((int)wp2, NW - 1);
+            two[3] = bb2 ? (uint32_t)__builtin_amdgcn_readlane(wb2, 63 - __clzll((long long)bb2)) : 0xFFFFFFFFu;
+            // (the thread's exclusive E + 1 prefix)
+            u2 = (wid > 0 ? (uint32_t)__builtin_amdgcn_readlane((int)wp2, wid - 1) : 0u) + incw2 - u2;
+        }
         MRS(3);
     } else {
+        if (TWO) two[0] = 0u;
         const MTr<D> inc = mtr_block_scan<D>(MTr<D>{a0, a1, q0, q1, st ? tid : (1 << 30)}, wt, FP::SAT);
         // exclusive: the previous thread's inclusive
         MTr<D> ex = mtr_shfl_up(inc, 1);
@@ -696,6 +728,12 @@ __device__ __forceinline__ int med_round(const typename MedFP<T>::D (&d0)[P], co
             for (int j = 1; j < P; j++) { xv = j == lj ? v[j] : xv; y = j == lj ? why[j] : y; }
             X.wv[wid] = xv;
             X.wy[wid] = y;
+            if (TWO) {
+                uint32_t i2 = u2;
+#pragma unroll
+                for (int j = 0; j < P; j++) i2 += j <= lj ? e2[j] : 0u;
+                X.wi2[wid] = i2;
+            }
         }
     } else if (lane == 63) {
         X.wl[wid] = 1 << 30;
@@ -711,6 +749,7 @@ __device__ __forceinline__ int med_round(const typename MedFP<T>::D (&d0)[P], co
     k_out = X.wk[fw];
     v_out = X.wv[fw];
     why_out = X.wy[fw];
+    if (TWO) two[2] = X.wi2[fw];
     MRS(6);
 #undef MRS
     return f;
@@ -930,6 +969,12 @@ __global__ __launch_bounds__(MXC_T) void med_compose_kernel(const T* __restrict_
             D d0[2], d1[2];
             bool stop[2], live[2], tie = false;
             int why[2] = {0, 0};
+            // (float: the units in E + 1 too, so that a sum crossing into the next binade finishes the chunk in
+            //  this round when nothing after the crossing leaves E + 1 or ties there)
+            constexpr bool TW = sizeof(D) == 4;
+            uint32_t e2[2] = {0u, 0u}, two[4] = {0u, 0u, 0u, 0u};
+            bool bad2[2] = {false, false};
+            const bool e2ok = TW && E + 1 <= FP::EMAX;
 #pragma unroll
             for (int j = 0; j < 2; j++) {
                 const int e = 2 * tid + j;
@@ -942,12 +987,22 @@ __global__ __launch_bounds__(MXC_T) void med_compose_kernel(const T* __restrict_
                         d1[j] = med_units<T>(v2[j], scale, (D)1);   // from an odd one
                         tie |= d0[j] != d1[j];
                     }
+                    if (TW) {
+                        if (e2ok && v2[j] >= (T)0 && v2[j] < FP::mul(lim, (T)2)) {
+                            const T sc2 = FP::mul(scale, (T)0.5);
+                            const D a = med_units<T>(v2[j], sc2, (D)0), b = med_units<T>(v2[j], sc2, (D)1);
+                            e2[j] = (uint32_t)a;
+                            bad2[j] = a != b;
+                        } else {
+                            bad2[j] = true;
+                        }
+                    }
                 }
             }
             D kf;
             T xv;
             int y;
-            const int f = med_round<T, 2>(d0, d1, stop, live, v2, why, tie, k0, X, wt, kf, xv, y, pf);
+            const int f = med_round<T, 2, TW>(d0, d1, stop, live, v2, why, tie, k0, X, wt, kf, xv, y, pf, e2, bad2, two);
             const T u = FP::pow2(E - FP::BIAS - FP::M);
             if (f >= (1 << 30)) {                           // the rest of the chunk stays in the binade
                 s = FP::mul((T)kf, u);
@@ -956,6 +1011,18 @@ __global__ __launch_bounds__(MXC_T) void med_compose_kernel(const T* __restrict_
             }
             s = FP::add(FP::mul((T)kf, u), xv);             // the leaving element, exactly
             i0 = f + 1;
+            if (TW && two[0] && (int)two[3] <= f && s >= FP::smin() && s < FP::smax() && FP::expo(s) == E + 1) {
+                // the rest of the chunk in E + 1: k' + its units, if that stays below the binade's top
+                const U sb3 = FP::bits(s);
+                const D k2 = (D)((sb3 & ((U(1) << FP::M) - 1)) | (U(1) << FP::M));
+                const D ke = k2 + (D)(two[1] - two[2]);
+                if (ke < (D(1) << (FP::M + 1))) {
+                    s = FP::mul((T)ke, FP::mul(u, (T)2));
+                    i0 = m;
+                    MPF_ADD(6, 1);
+                    break;
+                }
+            }
         }
         c += 1;
         MPF_T(t4);

@@ -18,7 +18,7 @@ L.check(L.L.dc_med_prof_read(ctypes.c_longlong(n), buf), "prof")
 v = list(buf)
 t = lambda k: v[k] * 10 / 1e3
 print(f"2^{lg}: zero-skip rounds {v[0]}, block iterations {v[1]}, ring refills {v[2]}, serial chunks {v[5]}, "
-      f"element rounds {v[7]}, single-lane finishes {v[8]}")
+      f"element rounds {v[7]}, single-lane finishes {v[8]}, two-binade finishes {v[6]}")
 print(f"  us: iteration head+refill {t(3):.1f}, block rounds {t(4):.1f}, serial chunks {t(9):.1f}")
 print(f"  med_round sections (us, all rounds): syncthreads_or {t(10):.1f}, scan..barrier1 {t(11):.1f}, barrier1 {t(12):.1f}, "
       f"prefix {t(13):.1f}, walk+ballot {t(14):.1f}, barrier2+pick {t(15):.1f}")
