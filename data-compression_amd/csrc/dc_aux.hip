@@ -379,37 +379,33 @@ __global__ __launch_bounds__(1024) void med_chunk_scan_kernel(MedScratch<T> M, l
 // tie's two bits and one parity are tracked, instead of both paths element by element.
 template <typename T, int N = MC_PER>
 __device__ __forceinline__ void trans_elems(const T* v, int cnt, int E, typename MedFP<T>::D& d0,
-                                            typename MedFP<T>::D& d1, int& p0, int& p1, bool& bad, int first = 0) {
+                                            typename MedFP<T>::D& d1, int& p0, int& p1) {
+    // (every element is >= 0 and below the binade's top: the caller checked the chunk's max and flags)
     typedef MedFP<T> FP;
     typedef typename FP::D D;
     const T scale = FP::pow2(FP::BIAS + FP::M - E);                 // 1/u
-    const T lim = FP::pow2(E + 1 - FP::BIAS);                       // the binade's top
-    D S = 0;
-    int X = 0, e0 = 0, e1 = 0;
+    D S = 0, Sl = 0;                                                // units; units at the last tie
+    int e0 = 0, e1 = 0;
     bool tied = false;
-    bad = false;
 #pragma unroll
     for (int i = 0; i < N; i++) {
-        if (i >= first && i < cnt) {
-            const bool ok = v[i] >= (T)0 && v[i] < lim;           // not negative, NaN, inf or >= the binade's top
-            bad |= !ok;
-            const T q = FP::mul(ok ? v[i] : (T)0, scale);         // exact: power-of-two scaling, < 2^(M+1)
-            const T fq = floor(q);
-            const T fr = FP::sub(q, fq);
-            const D fl = (D)fq;
-            if (__builtin_expect(fr == (T)0.5, 0)) {              // a tie: round the path's k + fl to even
-                const int b = (X ^ (int)(fl & 1)) & 1;
+        if (i < cnt) {
+            const T q = FP::mul(v[i], scale);                     // exact: power-of-two scaling, < 2^(M+1)
+            const T rn = rint(q);                                   // nearest (a tie to even: decided below)
+            const T dq = FP::sub(q, rn);
+            if (__builtin_expect(dq == (T)0.5 || dq == (T)-0.5, 0)) {   // a tie: round the path's k + fl to even
+                const D fl = (D)floor(q);
+                const int b = ((int)((S - Sl) & 1) ^ (int)(fl & 1)) & 1;   // (S - Sl: the units since the last tie)
                 if (!tied) { e0 = b; e1 = b ^ 1; tied = true; } else S += b;
                 S += fl;
-                X = 0;
+                Sl = S;
             } else {
-                const D r = fl + (fr > (T)0.5 ? 1 : 0);
-                S += r;
-                X ^= (int)(r & 1);
+                S += (D)rn;
             }
         }
     }
     // (a thread's units stay far below the type's range; compose() saturates the sums)
+    const int X = (int)((S - Sl) & 1);
     d0 = min(S + e0, FP::SAT);
     d1 = min(S + e1, FP::SAT);
     p0 = X;
@@ -453,8 +449,10 @@ __global__ __launch_bounds__(256) void med_chunk_trans_kernel(const T* __restric
             } else if (!bad && cmax < FP::pow2(E - FP::BIAS - FP::M - 1)) {
                 // every element below u/2 (and none negative or NaN): nothing added, parity kept -- the
                 // transducer of a stalled sum, computed for free (uniform branch)
+            } else if (!bad && !(cmax < FP::pow2(E + 1 - FP::BIAS))) {
+                bad = true;                                            // an element at or above the binade's top
             } else if (!bad) {
-                trans_elems<T, MT_PER>(v, cnt, E, d0, d1, p0, p1, bad);
+                trans_elems<T, MT_PER>(v, cnt, E, d0, d1, p0, p1);
             }
             // ordered reduction over the wave: lane i absorbs lane i + d (its successor block)
 #pragma unroll
