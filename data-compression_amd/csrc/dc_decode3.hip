@@ -85,7 +85,11 @@ __device__ unsigned long long g_prof3[32];
             for (int i_ = 0; i_ < 16; i_++)                                                            \
                 if (p3a[i_]) atomicAdd(&g_prof3[i_], p3a[i_]);                                         \
     } while (0)
+#define P3_PARAM , unsigned long long* p3a
+#define P3_ARG , p3a
 #else
+#define P3_PARAM
+#define P3_ARG
 #define P3_DECL() do {} while (0)
 #define P3_T(v) do {} while (0)
 #define P3_ADD(i, val) do {} while (0)
@@ -287,10 +291,11 @@ __device__ __forceinline__ int run_lines(Ring3& r, __amdgpu_buffer_rsrc_t rs, lo
 // period-3 pattern 100100... (grid-stride over 32-bit words, MSB-first) and flags any difference;
 // decode3 then writes the zeros at streaming speed, or hands the stream to the chunk-map decoder.
 constexpr uint32_t D3_ZMISS = 32768u;
-__device__ __forceinline__ void zero_run_check(__amdgpu_buffer_rsrc_t rs, const Geo3& G, long long num, unsigned* err) {
+__device__ __forceinline__ void zero_run_check(__amdgpu_buffer_rsrc_t rs, const Geo3& G, long long num, unsigned* err,
+                                               unsigned flag = D3_ZMISS) {
     const unsigned long long need = 3ull * (unsigned long long)num;
     if (need > G.nbits) {                                     // fewer bits than num tokens: not this case
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err, D3_ZMISS);
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err, flag);
         return;
     }
     const long long nw = (long long)((need + 31) >> 5);
@@ -309,7 +314,168 @@ __device__ __forceinline__ void zero_run_check(__amdgpu_buffer_rsrc_t rs, const 
             bad |= ((v[i] ^ pat) & m) != 0u;
         }
     }
-    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(err, D3_ZMISS);
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(err, flag);
+}
+
+// One parse job (64 segments, lane = segment): the main walk, the links, the records, the token offsets.
+// Returns the job's token total (every lane).
+template <int CT, int SEG>
+__device__ __forceinline__ uint32_t parse3_job(Ring3& r, uint16_t* recs, const uint8_t* tl, const Geo3& G,
+                                               __amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t rrec,
+                                               const Dec3Bufs& D3, unsigned job, uint32_t epoch, int lane P3_PARAM) {
+    constexpr int seg = SEG;
+    constexpr int PL = CT == 6 ? DC_PARSE_PL6 : 1;              // pre-walk lines (1024 bits each)
+    const long long sidx = (long long)job * 64 + lane;              // this lane's segment
+    const long long sbit = sidx * seg * 256;
+    const bool act = sidx < G.nseg;
+    const int lim = act ? (int)min((long long)G.nbits - sbit, (long long)seg * 256 + 64) : -(1 << 30);
+    const long long gw0 = sbit >> 5;
+    const long long c0 = sidx * seg;                                   // first chunk of the segment
+    P3_T(t0);
+
+    // ---- main walk: the pre-walk line (1024 bits before the segment), then the segment's lines
+    uint32_t tot = 0;
+    int e0 = 0, ec = 0;
+    run_lines<false>(r, rs, G.nbytes, gw0, 1 - PL, seg / 4 + 1, lim, -1024 * PL, act, tl,
+              [&](int c, int kbase) {
+                  if (c == 0 && sidx == 0) r.init(0, kbase);             // the stream's first bit
+                  ec = r.pos - 256 * c;
+              },
+              [&](int c, int cnt) {
+                  if (c >= 0) {
+                      recs[c * 64 + lane] = (uint16_t)((uint32_t)(ec & 31) | ((uint32_t)cnt << 8));
+                      tot += (uint32_t)cnt;
+                      if (c == 0) e0 = ec;
+                  }
+              });
+    const int X = r.pos - 256 * seg;                                 // entry of the next segment
+    // the job's exit: 8- and 16-chunk segments publish it right after the main walk (a repair that
+    // moves it is rare enough to decline the stream for), 4-chunk segments after the in-job repairs;
+    // CT6 always after them (its long tokens at small bounds resynchronise slowly: U10 at 1e-6 declined
+    // at every size, `tools/seg_time.py`; late publication costs ~1 us at 2^26, 3-5 us for CT11, which
+    // keeps the early one)
+    constexpr bool EARLY_EXIT = seg >= 8 && DC_EXIT_EARLY && CT != 6;
+    if (EARLY_EXIT && lane == 63) st_relaxed(&D3.pexit[job], ((uint64_t)epoch << 32) | (uint32_t)X);
+    P3_T(t1);
+    P3_ADD(0, t1 - t0);
+    P3_ADD(4, act ? tot : 0u);
+
+    // ---- links within the job: a segment's first entry = the previous segment's exit.  A lane whose
+    // entry is not re-walks from that exit, rewriting its records until the path meets a recorded
+    // entry again; a path that reaches the segment end without meeting it moves the exit, and the
+    // successor is checked again (rounds; a moved exit of the last segment declines)
+    // (the link into the job: checked at once if the previous job has published its exit, else after
+    // the in-job links with a bounded wait)
+    int xin = __shfl_up(X, 1, 64), ecur = e0, Xcur = X, rounds = 0;
+    bool link0 = false;
+    if (lane == 0 && act && sidx > 0) {
+        const uint64_t v = ld_relaxed(&D3.pexit[job - 1]);
+        if ((v >> 32) == (uint64_t)epoch) { xin = (int)(uint32_t)v; link0 = true; }
+    }
+    bool bad = act && (lane > 0 || link0) && ecur != xin;
+    for (int pass = 0; pass < 2; pass++) {
+    if (pass == 1) {                            // the job's first link: wait (bounded) for the exit
+        // the job's exit, after the links within the job are repaired (a repair that reaches the end
+        // of the last segment moves it -- with 4-chunk segments not rare enough to decline the stream
+        // for): it depends on nothing outside the job, so no job waits for more than one main walk
+        // and one round of in-job repairs
+        if (!EARLY_EXIT && lane == 63) st_relaxed(&D3.pexit[job], ((uint64_t)epoch << 32) | (uint32_t)Xcur);
+        bool chk = false;
+        if (lane == 0 && act && sidx > 0 && !link0) {
+            // the previous job is resident (a lower workgroup, or this grid's previous round) and
+            // publishes its exit after its main walk (and in-job repairs, 4-chunk segments)
+            const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
+            P3_T(tw0);
+            uint64_t v;
+            while (((v = ld_relaxed(&D3.pexit[job - 1])) >> 32) != (uint64_t)epoch &&
+                   __builtin_amdgcn_s_memrealtime() - w0 < D3_LINK_WAIT)
+                __builtin_amdgcn_s_sleep(2);
+            if ((v >> 32) == (uint64_t)epoch) { xin = (int)(uint32_t)v; link0 = true; chk = true; }
+            else atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK);   // (never seen: the chunk-map decoder takes it)
+            P3_T(tw1);
+            P3_ADD(1, tw1 - tw0);
+        }
+        bad = chk && ecur != xin;
+    }
+    while (__any(bad)) {
+        if (++rounds > D3_MAX_ROUNDS) { if (lane == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK); break; }
+        bool live = bad;
+        P3_T(tr0);
+        const int nl = run_lines<true>(r, rs, G.nbytes, gw0, 1, seg / 4 + 1, lim, bad ? xin : 0, bad, tl,
+                  [&](int c, int) {
+                      const int old = (int)(recs[c * 64 + lane] & 31u);
+                      if (live && c > 0 && r.pos - 256 * c == old && 256 * c < lim) {
+                          live = false;                                 // met the recorded path
+                          r.pos = 1 << 30;
+                      }
+                      ec = r.pos - 256 * c;
+                  },
+                  [&](int c, int cnt) {
+                      if (live) {
+                          const uint32_t old = recs[c * 64 + lane];
+                          recs[c * 64 + lane] = (uint16_t)((uint32_t)(ec & 31) | ((uint32_t)cnt << 8));
+                          tot += (uint32_t)cnt - (old >> 8);
+                          if (c == 0) ecur = ec;
+                      }
+                  });
+        P3_T(tr1);
+        P3_ADD(6, tr1 - tr0);
+        P3_ADD(7, nl);
+        (void)nl;
+        const bool whole = 256 * seg < lim;                              // a successor segment exists
+        const int Xn = live ? r.pos - 256 * seg : Xcur;
+        const bool moved = live && whole && Xn != Xcur;
+        Xcur = Xn;
+        if (moved && lane == 63 && (pass == 1 || EARLY_EXIT)) atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK);   // (published)
+        const int xp = __shfl_up(Xcur, 1, 64);
+        const bool mp = __shfl_up((int)moved, 1, 64) != 0;
+        bad = lane >= 1 && act && mp && ecur != xp;
+        xin = bad ? xp : xin;
+    }
+    }
+    P3_T(t2);
+    P3_ADD(2, t2 - t1);
+    P3_MAX(16, t2 - t0);
+    P3_MAX(17, t1 - t0);
+    P3_MAX(18, t2 - t1);
+    P3_ADD(3, rounds);
+    P3_ADD(5, 1);
+
+    // ---- the segment's records: 32 bytes per lane, one contiguous 2 KB block per wave
+    if (act) {
+        uint32_t w[seg / 2];
+#pragma unroll
+        for (int i = 0; i < seg / 2; i++)
+            w[i] = (uint32_t)recs[(2 * i) * 64 + lane] | ((uint32_t)recs[(2 * i + 1) * 64 + lane] << 16);
+#pragma unroll
+        for (int i = 0; i < seg / 8; i++) {
+            const u32x4 v = {w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
+            __builtin_amdgcn_raw_buffer_store_b128(v, rrec, (int)(2 * c0 + 16 * i), 0, 0);
+        }
+        if constexpr (seg % 8 == 4) {                  // (4 chunks left: 4-chunk segments, the fused kernel's 20)
+            const u32x2 v = {w[seg / 2 - 2], w[seg / 2 - 1]};
+            __builtin_amdgcn_raw_buffer_store_b64(v, rrec, (int)(2 * c0 + 16 * (seg / 8)), 0, 0);
+        }
+    }
+
+    // ---- token offsets: the job's total and every decode job's first token relative to the job
+    const uint32_t inc = wave_incl_scan(tot, lane);
+    if (lane == 63) D3.ptot[job] = inc;
+    if constexpr (64 % seg == 0) {                     // decode jobs start on segment boundaries
+        if (((lane * seg) & 63) == 0) {
+            const long long dj = (long long)job * seg + (lane * seg) / 64;
+            if (dj * 64 < D3.max_chunks) D3.rel[dj] = inc - tot;
+        }
+    } else {                                           // (seg < 64: at most one decode job starts in a segment)
+        const int k = (int)((64 - ((lane * seg) & 63)) & 63);        // its chunk within the segment
+        if (k < seg) {
+            uint32_t pre = inc - tot;
+            for (int c = 0; c < k; c++) pre += (uint32_t)(recs[c * 64 + lane] >> 8);
+            const long long dj = ((long long)job * 64 * seg + (long long)lane * seg + k) / 64;
+            if (dj * 64 < D3.max_chunks) D3.rel[dj] = pre;
+        }
+    }
+    return (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
 }
 
 template <int CT, int SEG>
@@ -318,7 +484,6 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
                                                     long long num, uint32_t epoch) {
     constexpr int seg = SEG;
     static_assert(SEG == 4 || SEG % 8 == 0, "whole region lines; 8- or 16-byte record stores per lane");
-    constexpr int PL = CT == 6 ? DC_PARSE_PL6 : 1;              // pre-walk lines (1024 bits each)
     __shared__ uint32_t ring[D3_RING * 64];
     __shared__ uint16_t recs[seg * 64];                          // [chunk][lane]: the wave's records
     __shared__ uint8_t tl[512];
@@ -340,147 +505,7 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
     P3_DECL();
     // jobs by a fixed stride (a shared ticket counter serialised every wave on one L2 line)
     for (unsigned job = blockIdx.x; !decline && (long long)job < G.npjobs; job += gridDim.x) {
-        const long long sidx = (long long)job * 64 + lane;              // this lane's segment
-        const long long sbit = sidx * seg * 256;
-        const bool act = sidx < G.nseg;
-        const int lim = act ? (int)min((long long)G.nbits - sbit, (long long)seg * 256 + 64) : -(1 << 30);
-        const long long gw0 = sbit >> 5;
-        const long long c0 = sidx * seg;                                   // first chunk of the segment
-        P3_T(t0);
-
-        // ---- main walk: the pre-walk line (1024 bits before the segment), then the segment's lines
-        uint32_t tot = 0;
-        int e0 = 0, ec = 0;
-        run_lines<false>(r, rs, G.nbytes, gw0, 1 - PL, seg / 4 + 1, lim, -1024 * PL, act, tl,
-                  [&](int c, int kbase) {
-                      if (c == 0 && sidx == 0) r.init(0, kbase);             // the stream's first bit
-                      ec = r.pos - 256 * c;
-                  },
-                  [&](int c, int cnt) {
-                      if (c >= 0) {
-                          recs[c * 64 + lane] = (uint16_t)((uint32_t)(ec & 31) | ((uint32_t)cnt << 8));
-                          tot += (uint32_t)cnt;
-                          if (c == 0) e0 = ec;
-                      }
-                  });
-        const int X = r.pos - 256 * seg;                                 // entry of the next segment
-        // the job's exit: 8- and 16-chunk segments publish it right after the main walk (a repair that
-        // moves it is rare enough to decline the stream for), 4-chunk segments after the in-job repairs;
-        // CT6 always after them (its long tokens at small bounds resynchronise slowly: U10 at 1e-6 declined
-        // at every size, `tools/seg_time.py`; late publication costs ~1 us at 2^26, 3-5 us for CT11, which
-        // keeps the early one)
-        constexpr bool EARLY_EXIT = seg >= 8 && DC_EXIT_EARLY && CT != 6;
-        if (EARLY_EXIT && lane == 63) st_relaxed(&D3.pexit[job], ((uint64_t)epoch << 32) | (uint32_t)X);
-        P3_T(t1);
-        P3_ADD(0, t1 - t0);
-        P3_ADD(4, act ? tot : 0u);
-
-        // ---- links within the job: a segment's first entry = the previous segment's exit.  A lane whose
-        // entry is not re-walks from that exit, rewriting its records until the path meets a recorded
-        // entry again; a path that reaches the segment end without meeting it moves the exit, and the
-        // successor is checked again (rounds; a moved exit of the last segment declines)
-        // (the link into the job: checked at once if the previous job has published its exit, else after
-        // the in-job links with a bounded wait)
-        int xin = __shfl_up(X, 1, 64), ecur = e0, Xcur = X, rounds = 0;
-        bool link0 = false;
-        if (lane == 0 && act && sidx > 0) {
-            const uint64_t v = ld_relaxed(&D3.pexit[job - 1]);
-            if ((v >> 32) == (uint64_t)epoch) { xin = (int)(uint32_t)v; link0 = true; }
-        }
-        bool bad = act && (lane > 0 || link0) && ecur != xin;
-        for (int pass = 0; pass < 2; pass++) {
-        if (pass == 1) {                            // the job's first link: wait (bounded) for the exit
-            // the job's exit, after the links within the job are repaired (a repair that reaches the end
-            // of the last segment moves it -- with 4-chunk segments not rare enough to decline the stream
-            // for): it depends on nothing outside the job, so no job waits for more than one main walk
-            // and one round of in-job repairs
-            if (!EARLY_EXIT && lane == 63) st_relaxed(&D3.pexit[job], ((uint64_t)epoch << 32) | (uint32_t)Xcur);
-            bool chk = false;
-            if (lane == 0 && act && sidx > 0 && !link0) {
-                // the previous job is resident (a lower workgroup, or this grid's previous round) and
-                // publishes its exit after its main walk (and in-job repairs, 4-chunk segments)
-                const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
-                P3_T(tw0);
-                uint64_t v;
-                while (((v = ld_relaxed(&D3.pexit[job - 1])) >> 32) != (uint64_t)epoch &&
-                       __builtin_amdgcn_s_memrealtime() - w0 < D3_LINK_WAIT)
-                    __builtin_amdgcn_s_sleep(2);
-                if ((v >> 32) == (uint64_t)epoch) { xin = (int)(uint32_t)v; link0 = true; chk = true; }
-                else atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK);   // (never seen: the chunk-map decoder takes it)
-                P3_T(tw1);
-                P3_ADD(1, tw1 - tw0);
-            }
-            bad = chk && ecur != xin;
-        }
-        while (__any(bad)) {
-            if (++rounds > D3_MAX_ROUNDS) { if (lane == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK); break; }
-            bool live = bad;
-            P3_T(tr0);
-            const int nl = run_lines<true>(r, rs, G.nbytes, gw0, 1, seg / 4 + 1, lim, bad ? xin : 0, bad, tl,
-                      [&](int c, int) {
-                          const int old = (int)(recs[c * 64 + lane] & 31u);
-                          if (live && c > 0 && r.pos - 256 * c == old && 256 * c < lim) {
-                              live = false;                                 // met the recorded path
-                              r.pos = 1 << 30;
-                          }
-                          ec = r.pos - 256 * c;
-                      },
-                      [&](int c, int cnt) {
-                          if (live) {
-                              const uint32_t old = recs[c * 64 + lane];
-                              recs[c * 64 + lane] = (uint16_t)((uint32_t)(ec & 31) | ((uint32_t)cnt << 8));
-                              tot += (uint32_t)cnt - (old >> 8);
-                              if (c == 0) ecur = ec;
-                          }
-                      });
-            P3_T(tr1);
-            P3_ADD(6, tr1 - tr0);
-            P3_ADD(7, nl);
-            (void)nl;
-            const bool whole = 256 * seg < lim;                              // a successor segment exists
-            const int Xn = live ? r.pos - 256 * seg : Xcur;
-            const bool moved = live && whole && Xn != Xcur;
-            Xcur = Xn;
-            if (moved && lane == 63 && (pass == 1 || EARLY_EXIT)) atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK);   // (published)
-            const int xp = __shfl_up(Xcur, 1, 64);
-            const bool mp = __shfl_up((int)moved, 1, 64) != 0;
-            bad = lane >= 1 && act && mp && ecur != xp;
-            xin = bad ? xp : xin;
-        }
-        }
-        P3_T(t2);
-        P3_ADD(2, t2 - t1);
-        P3_MAX(16, t2 - t0);
-        P3_MAX(17, t1 - t0);
-        P3_MAX(18, t2 - t1);
-        P3_ADD(3, rounds);
-        P3_ADD(5, 1);
-
-        // ---- the segment's records: 32 bytes per lane, one contiguous 2 KB block per wave
-        if (act) {
-            uint32_t w[seg / 2];
-#pragma unroll
-            for (int i = 0; i < seg / 2; i++)
-                w[i] = (uint32_t)recs[(2 * i) * 64 + lane] | ((uint32_t)recs[(2 * i + 1) * 64 + lane] << 16);
-            if constexpr (seg == 4) {
-                const u32x2 v = {w[0], w[1]};
-                __builtin_amdgcn_raw_buffer_store_b64(v, rrec, (int)(2 * c0), 0, 0);
-            } else {
-#pragma unroll
-                for (int i = 0; i < seg / 8; i++) {
-                    const u32x4 v = {w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
-                    __builtin_amdgcn_raw_buffer_store_b128(v, rrec, (int)(2 * c0 + 16 * i), 0, 0);
-                }
-            }
-        }
-
-        // ---- token offsets: the job's total and every decode job's first token relative to the job
-        const uint32_t inc = wave_incl_scan(tot, lane);
-        if (lane == 63) D3.ptot[job] = inc;
-        if (((lane * seg) & 63) == 0) {
-            const long long dj = (long long)job * seg + (lane * seg) / 64;
-            if (dj * 64 < D3.max_chunks) D3.rel[dj] = inc - tot;
-        }
+        parse3_job<CT, SEG>(r, recs, tl, G, rs, rrec, D3, job, epoch, lane P3_ARG);
     }
     P3_FLUSH();
 }
@@ -593,6 +618,184 @@ __device__ __forceinline__ Pre3 prefetch3(__amdgpu_buffer_rsrc_t rr, __amdgpu_bu
 }
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return wave_total(v); }
 
+// One decode job (64 chunks, lane = chunk) whose first token is `base`: the walk into the wave's buffer, the
+// pending prefixes, the history granules, the float4 stores.
+template <int CT, int CAP>
+__device__ __forceinline__ void decode3_job(const Lut3& T, uint32_t* L, float* ob, const Geo3& G, __amdgpu_buffer_rsrc_t rs,
+                                            __amdgpu_buffer_rsrc_t ro, bool chk_all, const Dec3Bufs& D3, const Pre3& cur,
+                                            unsigned job, unsigned long long base, float* __restrict__ out, long long num,
+                                            uint32_t epoch, int lane P3_PARAM) {
+    P3_T(u0);
+    const long long g = (long long)job * 64 + lane;
+    const int e = (int)(cur.rc & 31u), n = (int)(cur.rc >> 8);
+    const uint32_t inc = wave_incl_scan((uint32_t)n, lane);
+    const int off = (int)inc - n;
+    const int Tn = (int)__builtin_amdgcn_readlane(inc, 63);
+    // the stream's last decode job: a stream with fewer tokens than num is left to the other decoder
+    // (it reads past the stream as the reference does)
+    if ((long long)job == G.ndjobs - 1 && (long long)(base + (unsigned long long)Tn) < num && lane == 0)
+        atomicOr(D3.err, D3_DECLINE | D3_WHY_SHORT);
+    const int al = (int)(base & 3ull);
+    P3_T(u1);
+    P3_ADD(8, u1 - u0);
+    // (no `continue` after a lane-conditional store here: the structurizer then peeled the loop head
+    // for lanes 1..63 with lane 0 inactive, and their readfirstlane claimed job 0 again, forever)
+    const bool fits = al + Tn <= CAP;
+    if (!fits) atomicOr(D3.err, D3_DECLINE | D3_WHY_DENSE);        // every lane: OR is idempotent
+    bool sent = false;
+    if (fits) {
+    {   // stage the chunk's 8 words + 4 words of the next chunk
+        const uint4 v0 = finish4(cur.v0, G.nbytes, 8 * g), v1 = finish4(cur.v1, G.nbytes, 8 * g + 4),
+                    v2 = finish4(cur.v2, G.nbytes, 8 * g + 8);
+        L[(0 << 6) + lane] = v0.x; L[(1 << 6) + lane] = v0.y; L[(2 << 6) + lane] = v0.z; L[(3 << 6) + lane] = v0.w;
+        L[(4 << 6) + lane] = v1.x; L[(5 << 6) + lane] = v1.y; L[(6 << 6) + lane] = v1.z; L[(7 << 6) + lane] = v1.w;
+        L[(8 << 6) + lane] = v2.x; L[(9 << 6) + lane] = v2.y; L[(10 << 6) + lane] = v2.z; L[(11 << 6) + lane] = v2.w;
+    }
+    P3_T(u2);
+    P3_ADD(9, u2 - u1);
+    const int o0 = al + off;
+    int pend = 0;
+    {
+        Rd3 r;
+        r.init(L, lane, e);
+        int o = o0;
+        for (int t = 0; t < n; t++) {
+            const uint32_t nx = r.fetch();
+            const uint32_t tk = r.peek();
+            const uint32_t idx = tk >> 23;
+            const uint32_t meta = T.meta[idx];
+            const uint2 kv = T.kv[idx];
+            uint32_t v = ((tk >> (meta & 31u)) & kv.x) | kv.y;
+            if (CT != 6) {
+                const uint32_t cc = tk >> 29;                            // 5..7: '101' '110' '111'
+                if (__builtin_expect(__any(cc >= 5u), 0)) {
+                    if (cc >= 5u) {
+                        const int need = (int)cc - 4;
+                        if (t < need || t - need < pend || (g == 0 && t < 3)) {
+                            pend = t + 1;                                // needs the previous chunk's values
+                            // a prediction among the stream's first 3 (a shard's: its incoming values)
+                            sent |= g == 0 && t < 3 && D3.shard != 1;
+                            v = 0u;
+                        } else {
+                            const float pv = predict_value(need, ob[o - 1], ob[o - 2], ob[o - 3]);
+                            v = __float_as_uint(pv);
+                            sent |= v == 0xBF800000u;
+                        }
+                    }
+                }
+            }
+            ob[o] = __uint_as_float(v);
+            o++;
+            r.step(nx, (int)(meta >> 8));
+        }
+    }
+    P3_T(u3);
+    P3_ADD(10, u3 - u2);
+    // ---- pending prefixes, in rounds: a lane re-decodes its prefix once no lane before it still holds an
+    // unresolved prefix that reaches its three history values (U: the furthest end of those prefixes) --
+    // usually every pending lane in the first round (a noisy ramp has ~40% of its chunks start with a
+    // prediction; lane by lane, that serial loop was 80% of its decode)
+    unsigned long long pm = __ballot(pend > 0);
+    P3_ADD(14, __popcll(pm));
+    P3_ADD(15, Tn);
+    while (pm) {
+        const bool mine = ((pm >> lane) & 1ull) != 0ull;
+        int U = mine ? o0 + pend : -(1 << 30);
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {                          // inclusive max over lanes <= this one
+            const int u = __shfl_up(U, d, 64);
+            if (lane >= d) U = max(U, u);
+        }
+        U = __shfl_up(U, 1, 64);                                      // exclusive
+        if (lane == 0) U = -(1 << 30);
+        const bool go = mine && U <= max(o0 - 3, al);
+        pm &= ~__ballot(go);
+        __builtin_amdgcn_wave_barrier();
+        if (go) {
+            float h[3];
+#pragma unroll
+            for (int k = 1; k <= 3; k++) {
+                const int i = o0 - k;
+                // (job 0 has no predecessor: a prediction among its first tokens declined above)
+                h[k - 1] = i >= al ? ob[i] : (job > 0 ? prev_job_value(D3, job, al - i, epoch) : 0.0f);
+            }
+            float b1 = h[0], b2 = h[1], b3 = h[2];
+            if (D3.shard == 1 && g == 0) {
+                // a shard's first chunk: its prefix waits for the values before the shard (zeros here,
+                // re-decoded by shard3_fix_kernel).  Values after the prefix never read it; if the
+                // prefix reaches the chunk's last three (read by the next chunk), hand the shard over
+                D3.spend[0] = (uint32_t)pend;
+                if (pend > n - 3) atomicOr(D3.err, D3_DECLINE | D3_WHY_SHARD);
+            }
+            Rd3 r;
+            r.init(L, lane, e);
+            for (int t = 0; t < pend; t++) {
+                const uint32_t nx = r.fetch();
+                const uint32_t tk = r.peek();
+                const uint32_t idx = tk >> 23;
+                const uint32_t meta = T.meta[idx];
+                const uint2 kv = T.kv[idx];
+                uint32_t v = ((tk >> (meta & 31u)) & kv.x) | kv.y;
+                const uint32_t cc = tk >> 29;
+                if (CT != 6 && cc >= 5u) {
+                    v = __float_as_uint(predict_value((int)cc - 4, b1, b2, b3));
+                    sent |= v == 0xBF800000u;
+                }
+                ob[o0 + t] = __uint_as_float(v);
+                b3 = b2; b2 = b1; b1 = __uint_as_float(v);
+                r.step(nx, (int)(meta >> 8));
+            }
+        }
+    }
+    P3_T(u4);
+    P3_ADD(11, u4 - u3);
+    // ---- publish the job's last three values (the next job's first chunk may need them)
+    if (lane < 3 && Tn >= 3)
+        st_relaxed(&D3.hist[(long long)job * 3 + lane], ((uint64_t)epoch << 32) | __float_as_uint(ob[al + Tn - 1 - lane]));
+    }
+    P3_T(u4s);
+    // ---- store: the job's values as whole float4s of the output's 16-byte grid (a fixed count of
+    // buffer stores, lanes outside the job writing past the range), the partial float4s at its two
+    // ends float by float (lanes 0..3: the first, 4..7: the last)
+    const int span = al + Tn;
+    const int Q = (span + 3) >> 2;
+    const long long gi0 = (long long)(base - (unsigned long long)al);
+    bool sv = false;
+    const float4* ob4 = reinterpret_cast<const float4*>(ob);
+#pragma unroll
+    for (int i = 0; i < (CAP + 3) / 4 / 64 + 1; i++) {
+        const int q = lane + 64 * i;
+        const float4 v = ob4[min(q, CAP / 4 - 1)];
+        const long long gi = gi0 + 4 * q;
+        const bool full = fits && q < Q && 4 * q >= al && 4 * q + 4 <= span && gi + 4 <= num;
+        if (chk_all && q < Q)
+            sv |= __float_as_uint(v.x) == 0xBF800000u || __float_as_uint(v.y) == 0xBF800000u ||
+                  __float_as_uint(v.z) == 0xBF800000u || __float_as_uint(v.w) == 0xBF800000u;
+        const u32x4 raw = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+#ifndef DC_DEC3_NOSTORE
+        __builtin_amdgcn_raw_buffer_store_b128(raw, ro, full ? (int)(4 * gi) : D3_OOB, 0, DC_DEC3_NT ? 2 : 0);
+#else                                   // (diagnostic build: the values are computed, never stored)
+        if (raw.x == 0x12345678u && full && gi == 0) out[0] = v.y + v.z + v.w;
+#endif
+    }
+    {
+        const int qe = lane < 4 ? 0 : Q - 1;
+        const int idx = 4 * qe + (lane & 3);
+        const long long gi = gi0 + idx;
+        const bool qfull = 4 * qe >= al && 4 * qe + 4 <= span && gi0 + 4 * qe + 4 <= num;
+        const bool ok = fits && lane < 8 && !qfull && idx >= al && idx < span && gi < num;
+        const float v = ob[min(max(idx, 0), CAP - 1)];
+        (void)ok;
+#ifndef DC_DEC3_NOSTORE
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ro, ok ? (int)(4 * gi) : D3_OOB, 0, DC_DEC3_NT ? 2 : 0);
+#endif
+    }
+    if (__any(sent || sv) && lane == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_SENT);
+    P3_T(u5);
+    P3_ADD(12, u5 - u4s);
+    P3_ADD(13, 1);
+}
+
 // four waves per SIMD (<= 128 VGPRs): round 5's dense buffer template, shard flags and pending rounds had taken the
 // kernel to 129-145 VGPRs, three waves per SIMD, and decode3 from 97 to 115 us at 2^26 U10
 #ifndef DC_D3_MINW
@@ -639,9 +842,6 @@ __global__ __launch_bounds__(256, DC_D3_MINW) void decode3_kernel(const uint8_t*
     unsigned long long pcar = 0;                    // first token of parse job plo
     long long plo = 0;
     auto process = [&](const Pre3& cur, unsigned job) {
-        P3_T(u0);
-        const long long g = (long long)job * 64 + lane;
-        const int e = (int)(cur.rc & 31u), n = (int)(cur.rc >> 8);
         const long long pj = (long long)(job / SEG);
         uint32_t wsum = wave_sum(cur.pt[0] + cur.pt[1] + cur.pt[2] + cur.pt[3]);
         for (long long k0 = plo + 256; k0 < pj; k0 += 256) {     // a window longer than one prefetch (rare)
@@ -656,172 +856,7 @@ __global__ __launch_bounds__(256, DC_D3_MINW) void decode3_kernel(const uint8_t*
         pcar += wsum;
         plo = pj;
         const unsigned long long base = pcar + cur.rl;
-        const uint32_t inc = wave_incl_scan((uint32_t)n, lane);
-        const int off = (int)inc - n;
-        const int Tn = (int)__builtin_amdgcn_readlane(inc, 63);
-        // the stream's last decode job: a stream with fewer tokens than num is left to the other decoder
-        // (it reads past the stream as the reference does)
-        if ((long long)job == G.ndjobs - 1 && (long long)(base + (unsigned long long)Tn) < num && lane == 0)
-            atomicOr(D3.err, D3_DECLINE | D3_WHY_SHORT);
-        const int al = (int)(base & 3ull);
-        P3_T(u1);
-        P3_ADD(8, u1 - u0);
-        // (no `continue` after a lane-conditional store here: the structurizer then peeled the loop head
-        // for lanes 1..63 with lane 0 inactive, and their readfirstlane claimed job 0 again, forever)
-        const bool fits = al + Tn <= CAP;
-        if (!fits) atomicOr(D3.err, D3_DECLINE | D3_WHY_DENSE);        // every lane: OR is idempotent
-        bool sent = false;
-        if (fits) {
-        {   // stage the chunk's 8 words + 4 words of the next chunk
-            const uint4 v0 = finish4(cur.v0, G.nbytes, 8 * g), v1 = finish4(cur.v1, G.nbytes, 8 * g + 4),
-                        v2 = finish4(cur.v2, G.nbytes, 8 * g + 8);
-            L[(0 << 6) + lane] = v0.x; L[(1 << 6) + lane] = v0.y; L[(2 << 6) + lane] = v0.z; L[(3 << 6) + lane] = v0.w;
-            L[(4 << 6) + lane] = v1.x; L[(5 << 6) + lane] = v1.y; L[(6 << 6) + lane] = v1.z; L[(7 << 6) + lane] = v1.w;
-            L[(8 << 6) + lane] = v2.x; L[(9 << 6) + lane] = v2.y; L[(10 << 6) + lane] = v2.z; L[(11 << 6) + lane] = v2.w;
-        }
-        P3_T(u2);
-        P3_ADD(9, u2 - u1);
-        const int o0 = al + off;
-        int pend = 0;
-        {
-            Rd3 r;
-            r.init(L, lane, e);
-            int o = o0;
-            for (int t = 0; t < n; t++) {
-                const uint32_t nx = r.fetch();
-                const uint32_t tk = r.peek();
-                const uint32_t idx = tk >> 23;
-                const uint32_t meta = T.meta[idx];
-                const uint2 kv = T.kv[idx];
-                uint32_t v = ((tk >> (meta & 31u)) & kv.x) | kv.y;
-                if (CT != 6) {
-                    const uint32_t cc = tk >> 29;                            // 5..7: '101' '110' '111'
-                    if (__builtin_expect(__any(cc >= 5u), 0)) {
-                        if (cc >= 5u) {
-                            const int need = (int)cc - 4;
-                            if (t < need || t - need < pend || (g == 0 && t < 3)) {
-                                pend = t + 1;                                // needs the previous chunk's values
-                                // a prediction among the stream's first 3 (a shard's: its incoming values)
-                                sent |= g == 0 && t < 3 && D3.shard != 1;
-                                v = 0u;
-                            } else {
-                                const float pv = predict_value(need, ob[o - 1], ob[o - 2], ob[o - 3]);
-                                v = __float_as_uint(pv);
-                                sent |= v == 0xBF800000u;
-                            }
-                        }
-                    }
-                }
-                ob[o] = __uint_as_float(v);
-                o++;
-                r.step(nx, (int)(meta >> 8));
-            }
-        }
-        P3_T(u3);
-        P3_ADD(10, u3 - u2);
-        // ---- pending prefixes, in rounds: a lane re-decodes its prefix once no lane before it still holds an
-        // unresolved prefix that reaches its three history values (U: the furthest end of those prefixes) --
-        // usually every pending lane in the first round (a noisy ramp has ~40% of its chunks start with a
-        // prediction; lane by lane, that serial loop was 80% of its decode)
-        unsigned long long pm = __ballot(pend > 0);
-        P3_ADD(14, __popcll(pm));
-        P3_ADD(15, Tn);
-        while (pm) {
-            const bool mine = ((pm >> lane) & 1ull) != 0ull;
-            int U = mine ? o0 + pend : -(1 << 30);
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {                          // inclusive max over lanes <= this one
-                const int u = __shfl_up(U, d, 64);
-                if (lane >= d) U = max(U, u);
-            }
-            U = __shfl_up(U, 1, 64);                                      // exclusive
-            if (lane == 0) U = -(1 << 30);
-            const bool go = mine && U <= max(o0 - 3, al);
-            pm &= ~__ballot(go);
-            __builtin_amdgcn_wave_barrier();
-            if (go) {
-                float h[3];
-#pragma unroll
-                for (int k = 1; k <= 3; k++) {
-                    const int i = o0 - k;
-                    // (job 0 has no predecessor: a prediction among its first tokens declined above)
-                    h[k - 1] = i >= al ? ob[i] : (job > 0 ? prev_job_value(D3, job, al - i, epoch) : 0.0f);
-                }
-                float b1 = h[0], b2 = h[1], b3 = h[2];
-                if (D3.shard == 1 && g == 0) {
-                    // a shard's first chunk: its prefix waits for the values before the shard (zeros here,
-                    // re-decoded by shard3_fix_kernel).  Values after the prefix never read it; if the
-                    // prefix reaches the chunk's last three (read by the next chunk), hand the shard over
-                    D3.spend[0] = (uint32_t)pend;
-                    if (pend > n - 3) atomicOr(D3.err, D3_DECLINE | D3_WHY_SHARD);
-                }
-                Rd3 r;
-                r.init(L, lane, e);
-                for (int t = 0; t < pend; t++) {
-                    const uint32_t nx = r.fetch();
-                    const uint32_t tk = r.peek();
-                    const uint32_t idx = tk >> 23;
-                    const uint32_t meta = T.meta[idx];
-                    const uint2 kv = T.kv[idx];
-                    uint32_t v = ((tk >> (meta & 31u)) & kv.x) | kv.y;
-                    const uint32_t cc = tk >> 29;
-                    if (CT != 6 && cc >= 5u) {
-                        v = __float_as_uint(predict_value((int)cc - 4, b1, b2, b3));
-                        sent |= v == 0xBF800000u;
-                    }
-                    ob[o0 + t] = __uint_as_float(v);
-                    b3 = b2; b2 = b1; b1 = __uint_as_float(v);
-                    r.step(nx, (int)(meta >> 8));
-                }
-            }
-        }
-        P3_T(u4);
-        P3_ADD(11, u4 - u3);
-        // ---- publish the job's last three values (the next job's first chunk may need them)
-        if (lane < 3 && Tn >= 3)
-            st_relaxed(&D3.hist[(long long)job * 3 + lane], ((uint64_t)epoch << 32) | __float_as_uint(ob[al + Tn - 1 - lane]));
-        }
-        P3_T(u4s);
-        // ---- store: the job's values as whole float4s of the output's 16-byte grid (a fixed count of
-        // buffer stores, lanes outside the job writing past the range), the partial float4s at its two
-        // ends float by float (lanes 0..3: the first, 4..7: the last)
-        const int span = al + Tn;
-        const int Q = (span + 3) >> 2;
-        const long long gi0 = (long long)(base - (unsigned long long)al);
-        bool sv = false;
-        const float4* ob4 = reinterpret_cast<const float4*>(ob);
-#pragma unroll
-        for (int i = 0; i < (CAP + 3) / 4 / 64 + 1; i++) {
-            const int q = lane + 64 * i;
-            const float4 v = ob4[min(q, CAP / 4 - 1)];
-            const long long gi = gi0 + 4 * q;
-            const bool full = fits && q < Q && 4 * q >= al && 4 * q + 4 <= span && gi + 4 <= num;
-            if (chk_all && q < Q)
-                sv |= __float_as_uint(v.x) == 0xBF800000u || __float_as_uint(v.y) == 0xBF800000u ||
-                      __float_as_uint(v.z) == 0xBF800000u || __float_as_uint(v.w) == 0xBF800000u;
-            const u32x4 raw = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
-#ifndef DC_DEC3_NOSTORE
-            __builtin_amdgcn_raw_buffer_store_b128(raw, ro, full ? (int)(4 * gi) : D3_OOB, 0, DC_DEC3_NT ? 2 : 0);
-#else                                   // (diagnostic build: the values are computed, never stored)
-            if (raw.x == 0x12345678u && full && gi == 0) out[0] = v.y + v.z + v.w;
-#endif
-        }
-        {
-            const int qe = lane < 4 ? 0 : Q - 1;
-            const int idx = 4 * qe + (lane & 3);
-            const long long gi = gi0 + idx;
-            const bool qfull = 4 * qe >= al && 4 * qe + 4 <= span && gi0 + 4 * qe + 4 <= num;
-            const bool ok = fits && lane < 8 && !qfull && idx >= al && idx < span && gi < num;
-            const float v = ob[min(max(idx, 0), CAP - 1)];
-            (void)ok;
-#ifndef DC_DEC3_NOSTORE
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ro, ok ? (int)(4 * gi) : D3_OOB, 0, DC_DEC3_NT ? 2 : 0);
-#endif
-        }
-        if (__any(sent || sv) && lane == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_SENT);
-        P3_T(u5);
-        P3_ADD(12, u5 - u4s);
-        P3_ADD(13, 1);
+        decode3_job<CT, CAP>(T, L, ob, G, rs, ro, chk_all, D3, cur, job, base, out, num, epoch, lane P3_ARG);
     };
     // two jobs per round, their inputs in two register sets: each job's loads are in flight during the
     // other's walk and stores (one set copied into the other would wait for the loads -- and for every
@@ -849,6 +884,132 @@ __global__ __launch_bounds__(256, DC_D3_MINW) void decode3_kernel(const uint8_t*
             job += stride;
             if ((long long)job >= G.ndjobs) break;
         }
+    }
+    P3_FLUSH();
+}
+
+// ------------------------------------------------------------------------------------------------
+// fused3_kernel (opt-in: DC_FUSED3=1; ordinary density, whole streams): parse and decode in one launch, the
+// prototype VERDICT r04 asked for.  A workgroup of 4 waves takes fused job J = parse jobs 4J..4J+3 (256 SEG
+// chunks): wave w parses job 4J+w exactly as parse3_kernel does (parse3_job), the workgroup publishes its token
+// total (ftag[J], epoch-tagged) and sums the totals of the fused jobs between its previous one and J (published
+// by the other workgroups after their parse; waited for, bounded) for the tokens before J; then the 4 waves
+// decode J's 4 SEG decode jobs (decode job 4 SEG J + 4i + w) exactly as decode3_kernel does (decode3_job),
+// their stream words and records fresh in the caches.  The parse rings and the decode buffers share one LDS
+// union, so the launch holds decode3's 4 workgroups per CU -- 16 waves, where parse3 alone holds 24: the host
+// takes the shortest segment (16, 20 or 32 chunks) whose parse jobs all fit in one round of resident waves, as
+// parse3's do (a second round of parse jobs runs after the first round's decode, alone).  `stamps` (or null):
+// per fused job the workgroup's s_memrealtime at its start, parse end, prefix known and decode end.
+__device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+template <int CT, int SEG, int CAP>
+__global__ __launch_bounds__(256, DC_D3_MINW) void fused3_kernel(const uint8_t* __restrict__ s, Params P, Dec3Bufs D3,
+                                                                const unsigned long long* dev_nbits,
+                                                                unsigned long long host_nbits, float* __restrict__ out,
+                                                                long long num, uint32_t epoch,
+                                                                unsigned long long* __restrict__ stamps) {
+    static_assert(SEG % 4 == 0 && SEG <= 64, "whole region lines; at most one decode job start per segment");
+    struct PS { uint32_t ring[4][D3_RING * 64]; uint16_t recs[4][SEG * 64]; };
+    struct DS { uint32_t stg[4][12 * 64]; float obuf[4][CAP]; };
+    union US { PS p; DS d; };
+    __shared__ __attribute__((aligned(16))) US U;
+    __shared__ Lut3 T;
+    __shared__ uint8_t tl[512];
+    __shared__ uint32_t sj[8];
+    build_lut_len<CT>(tl, P, threadIdx.x, 256);
+    build_lut3<CT>(T, P, threadIdx.x, 256);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const Geo3 G = geo3<SEG>(dev_nbits, host_nbits);
+    const __amdgpu_buffer_rsrc_t rs = stream_rsrc(s, D3.capw);
+    const __amdgpu_buffer_rsrc_t rrec =
+        __builtin_amdgcn_make_buffer_rsrc(D3.rec, (short)0, (int)min(2 * (D3.max_chunks + 4096), 0x7FFFFF00ll), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr = any_rsrc(D3.rec, 0x7FFFFF00), rl = any_rsrc(D3.rel, 0x7FFFFF00),
+                                 ro = any_rsrc(out, (int)(num * 4));
+    const bool over = G.nchunks > D3.max_chunks, runs = !over && runs_mode(CT, G.nbits, num);
+    if (over) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_RUNS);
+        return;
+    }
+    if (runs) {
+        // a runs-mode stream of nothing but '100' codes: zeros, written while every workgroup checks its part of
+        // the pattern -- a difference anywhere declines it, and the chunk-map decoder writes the output again
+        zero_run_check(rs, G, num, D3.err, D3_ZMISS | D3_DECLINE | D3_WHY_RUNS);
+        const u32x4 z4 = {0u, 0u, 0u, 0u};
+        for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; 4 * i < num; i += (long long)gridDim.x * blockDim.x)
+            if (4 * i + 4 <= num) __builtin_amdgcn_raw_buffer_store_b128(z4, ro, (int)(16 * i), 0, DC_DEC3_NT ? 2 : 0);
+            else for (long long j = 4 * i; j < num; j++) out[j] = 0.0f;
+        return;
+    }
+    __syncthreads();
+    const bool chk_all = (CT == 6 && P.B >= 23) || (CT == 7 && (P.mask17 >> 16) != 0u && P.mm == 23);
+    Ring3 r;
+    r.L = U.p.ring[w];
+    r.lc = (uint32_t)lane << 2;
+    P3_DECL();
+    const long long nfj = (G.npjobs + 3) / 4;
+    unsigned long long pcar = 0;                               // tokens before fused job jn
+    long long jn = 0;
+    for (long long J = blockIdx.x; J < nfj; J += gridDim.x) {
+        const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
+        // ---- parse: wave w takes parse job 4J + w
+        const long long pj = 4 * J + w;
+        uint32_t tot = 0;
+        if (pj < G.npjobs) tot = parse3_job<CT, SEG>(r, U.p.recs[w], tl, G, rs, rrec, D3, (unsigned)pj, epoch, lane P3_ARG);
+        if (lane == 0) sj[w] = tot;
+        __syncthreads();                                       // (records, rel and totals written; rings free)
+        const unsigned long long ts1 = __builtin_amdgcn_s_memrealtime();
+        // ---- the tokens before J: this workgroup's carry plus the fused jobs jn .. J-1 of the other workgroups
+        if (w == 0) {
+            const uint32_t ft = sj[0] + sj[1] + sj[2] + sj[3];
+            if (lane == 0) st_relaxed(&D3.ftag[J], ((uint64_t)epoch << 32) | ft);
+            unsigned long long acc = 0;
+            bool ok = true;
+            for (long long k = jn + lane; k < J; k += 64) {
+                const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
+                uint64_t v;
+                while (((v = ld_relaxed(&D3.ftag[k])) >> 32) != (uint64_t)epoch) {
+                    if (__builtin_amdgcn_s_memrealtime() - w0 > D3_LINK_WAIT) { ok = false; break; }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                acc += (uint32_t)v;
+            }
+            if (!ok) atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK);
+            pcar += wave_sum64(acc);
+            if (lane == 0) {
+                sj[4] = (uint32_t)pcar; sj[5] = (uint32_t)(pcar >> 32);
+                sj[6] = declined_now(D3) ? 1u : 0u;            // (no decode after a decline: its records are partial)
+            }
+            pcar += ft;
+        }
+        jn = J + 1;
+        __syncthreads();
+        const unsigned long long S0 = (unsigned long long)sj[4] | ((unsigned long long)sj[5] << 32);
+        const uint32_t pre[4] = {0u, sj[0], sj[0] + sj[1], sj[0] + sj[1] + sj[2]};
+        const unsigned long long ts2 = __builtin_amdgcn_s_memrealtime();
+        // ---- decode: decode jobs 64J + 4i + w (the job's successor is the next wave's, its predecessor the
+        // previous wave's: the history granules are published in step)
+        for (int i = 0; i < SEG && !sj[6]; i++) {
+            const long long dj = 4ll * SEG * J + 4 * i + w;
+            if (dj >= G.ndjobs) break;
+            const long long g = dj * 64 + lane;
+            Pre3 cur;
+            cur.rc = __builtin_amdgcn_raw_buffer_load_b16(rr, g < G.nchunks ? (int)(2 * g) : D3_OOB, 0, 0);
+            cur.rl = __builtin_amdgcn_raw_buffer_load_b32(rl, (int)(4 * dj), 0, 0);
+            cur.v0 = load_raw4(rs, 8 * g);
+            cur.v1 = load_raw4(rs, 8 * g + 4);
+            cur.v2 = load_raw4(rs, 8 * g + 8);
+            const unsigned long long base = S0 + pre[(4 * i + w) / SEG] + cur.rl;
+            decode3_job<CT, CAP>(T, U.d.stg[w], U.d.obuf[w], G, rs, ro, chk_all, D3, cur, (unsigned)dj, base, out, num,
+                                 epoch, lane P3_ARG);
+        }
+        const unsigned long long ts3 = __builtin_amdgcn_s_memrealtime();
+        if (stamps && threadIdx.x == 0) {
+            stamps[4 * J] = ts0; stamps[4 * J + 1] = ts1; stamps[4 * J + 2] = ts2; stamps[4 * J + 3] = ts3;
+        }
+        __syncthreads();                                       // (the decode buffers read: the next parse's rings)
     }
     P3_FLUSH();
 }
@@ -1069,11 +1230,106 @@ static int decode3_grids(const Params* P, const Dec3Bufs* D3, int dense, int* g1
     return 0;
 }
 
+// DC_FUSED3=1: fused3_kernel instead of parse3 + decode3 (16-chunk segments, ordinary density, whole streams);
+// DC_FUSED3_STAMPS=1 records its per-job phase stamps (dc_fused3_stamps)
+static unsigned long long* g_f3_stamps = nullptr;
+static long long g_f3_nfj = 0;
+static int g_f3_on = -1;
+static int fused3_on() {
+    if (g_f3_on < 0) { const char* e = getenv("DC_FUSED3"); g_f3_on = (e && *e == '1') ? 1 : 0; }
+    return g_f3_on;
+}
+// tests / experiments: 1 selects fused3_kernel, 0 the two launches; returns the previous setting
+extern "C" int dc_set_fused3(int on) {
+    const int old = fused3_on();
+    g_f3_on = on ? 1 : 0;
+    return old;
+}
+static int g_f3_seg = 0;
+static int launch_fused3(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                         const Params* P, const Dec3Bufs* D3, float* out, long long num, uint32_t epoch, hipStream_t st) {
+    const void* fp = P->ct == 5 ? (const void*)fused3_kernel<5, 16, D3_CAP> : P->ct == 6 ? (const void*)fused3_kernel<6, 16, D3_CAP>
+                   : P->ct == 7 ? (const void*)fused3_kernel<7, 16, D3_CAP> : (const void*)fused3_kernel<11, 16, D3_CAP>;
+    static int res[12];
+    const int ci = P->ct;
+    if (!res[ci]) res[ci] = resident3(fp, 256);             // (the same registers and LDS for every SEG)
+    // the segment length by a model of the launch (fused jobs in rounds of res[ci] workgroups; per round a job's
+    // parse ~2.35 us per 4 chunks walked -- the pre-walk line and the segment's lines -- its decode ~4.4 us per
+    // decode job and wave, ~10 us of prefix wait; measured at 2^26 U10) on the stream's chunks
+    // (its capacity when the length is on the device only); DC_FUSED3_SEG forces one
+    const long long nch = host_nbits ? (long long)((host_nbits + 255) / 256) : D3->max_chunks;
+    int seg = 16;
+    double best = 1e30;
+    for (int sg : {16, 20, 24, 32, 64}) {
+        const long long fj = (((nch + sg - 1) / sg + 63) / 64 + 3) / 4;
+        const double t = (double)((fj + res[ci] - 1) / res[ci]) * (2.35 * (sg / 4 + 1) * 4 + 4.4 * sg + 10.0);
+        if (t < best) { best = t; seg = sg; }
+    }
+    if (const char* e = getenv("DC_FUSED3_SEG")) {
+        const int f = atoi(e);
+        if (f == 16 || f == 20 || f == 24 || f == 32 || f == 64) seg = f;
+    }
+    g_f3_seg = seg;
+    const long long maxpj = ((D3->max_chunks + seg - 1) / seg + 63) / 64, nfj = (maxpj + 3) / 4;
+    const int grid = (int)std::max<long long>(1, std::min<long long>(nfj, res[ci]));
+    unsigned long long* stamps = nullptr;
+    if (getenv("DC_FUSED3_STAMPS")) {
+        if (nfj > g_f3_nfj) {
+            if (g_f3_stamps) (void)hipFree(g_f3_stamps);
+            if (hipMalloc((void**)&g_f3_stamps, (size_t)nfj * 4 * 8) != hipSuccess) return -1;
+            g_f3_nfj = nfj;
+        }
+        stamps = g_f3_stamps;
+        (void)hipMemsetAsync(stamps, 0, (size_t)g_f3_nfj * 4 * 8, st);
+    }
+#define F3L(C, S) hipLaunchKernelGGL(HIP_KERNEL_NAME(fused3_kernel<C, S, D3_CAP>), dim3(grid), dim3(256), 0, st, s, *P, \
+                                     *D3, dev_nbits, host_nbits, out, num, epoch, stamps)
+#define F3C(C)                                                                                       \
+    do {                                                                                             \
+        if (seg == 16) F3L(C, 16);                                                                   \
+        else if (seg == 20) F3L(C, 20);                                                              \
+        else if (seg == 24) F3L(C, 24);                                                              \
+        else if (seg == 32) F3L(C, 32);                                                              \
+        else F3L(C, 64);                                                                             \
+    } while (0)
+    switch (P->ct) {
+        case 5: F3C(5); break;
+        case 6: F3C(6); break;
+        case 7: F3C(7); break;
+        case 11: F3C(11); break;
+        default: return -2;
+    }
+#undef F3C
+#undef F3L
+    return 0;
+}
+// the stamps of the last fused launch (4 per fused job: start, parse end, prefix known, decode end; 100 MHz)
+extern "C" int dc_fused3_last_seg(void) { return g_f3_seg; }
+extern "C" long long dc_fused3_stamps(unsigned long long* out, long long max_jobs) {
+    if (!g_f3_stamps) return 0;
+    const long long n = std::min(max_jobs, g_f3_nfj);
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpy(out, g_f3_stamps, (size_t)n * 4 * 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return n;
+}
+
+static int g_f3_last = 0;
+extern "C" int dc_decode3_last_fused(void) { return g_f3_last; }
+extern "C" void dc_decode3_clear_fused(void) { g_f3_last = 0; }
 extern "C" int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
                                  const Params* P, const Dec3Bufs* D3, float* out, long long num, uint32_t epoch,
                                  int dense, hipStream_t st) {
     int g1 = 0, g3 = 0;
     if (decode3_grids(P, D3, dense, &g1, &g3)) return -2;
+    g_f3_last = fused3_on() && D3->seg == 16 && !dense && !D3->shard;
+    if (g_f3_last) {
+        dc_mark_phase(4, st);
+        if (launch_fused3(s, dev_nbits, host_nbits, P, D3, out, num, epoch, st)) return -2;
+        dbg_wait("fused3_kernel", st);
+        dc_mark_phase(7, st);
+        dc_mark_next_set();
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     dc_mark_phase(4, st);
     DC_DISPATCH_3(P->ct, D3->seg, parse3_kernel, dim3(g1), dim3(64), 0, st, s, *P, *D3, dev_nbits, host_nbits, num, epoch);
     dbg_wait("parse3_kernel", st);

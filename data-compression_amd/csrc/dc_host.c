@@ -678,6 +678,7 @@ static int dec_next_epoch(void) {
         if (G.dec3_pool) {
             HIPCHK(hipMemsetAsync(G.D3.pexit, 0, (size_t)(G.dec3_cap + 4096) / 256 * 8 + 64 * 8, G.st));
             HIPCHK(hipMemsetAsync(G.D3.hist, 0, (size_t)((G.dec3_cap + 4096) / 64 + 64) * 3 * 8, G.st));
+            HIPCHK(hipMemsetAsync(G.D3.ftag, 0, (size_t)((G.dec3_cap + 4096) / 256 + 64) * 8, G.st));
         }
         G.dec_epoch = 1;
     }
@@ -696,25 +697,27 @@ static int dec3_ensure(long long max_chunks, int B, int ct) {
         G.sh3_ok = 0;                         /* a pending shard fix would read the freed spend/rec */
         const long long C = max_chunks + 4096;
         const long long DJ = C / 64 + 64, PJ = C / (64 * 4) + 64;
-        size_t sz[6], off = 0, tot = 0;
+        size_t sz[7], off = 0, tot = 0;
         sz[0] = (size_t)C * 2;                /* rec */
         sz[1] = (size_t)DJ * 4;               /* rel */
         sz[2] = (size_t)PJ * 4;               /* ptot */
         sz[3] = (size_t)PJ * 8;               /* pexit */
         sz[4] = (size_t)DJ * 3 * 8;           /* hist */
         sz[5] = 256;                          /* spend */
-        for (int i = 0; i < 6; i++) tot += (sz[i] + 255) & ~(size_t)255;
+        sz[6] = (size_t)PJ * 8;               /* ftag */
+        for (int i = 0; i < 7; i++) tot += (sz[i] + 255) & ~(size_t)255;
         HIPCHK(hipMalloc(&G.dec3_pool, tot));
         HIPCHK(hipMemsetAsync(G.dec3_pool, 0, tot, G.st));
         char* b = (char*)G.dec3_pool;
-        void* ptr[6];
-        for (int i = 0; i < 6; i++) { ptr[i] = b + off; off += (sz[i] + 255) & ~(size_t)255; }
+        void* ptr[7];
+        for (int i = 0; i < 7; i++) { ptr[i] = b + off; off += (sz[i] + 255) & ~(size_t)255; }
         G.D3.rec = (uint16_t*)ptr[0];
         G.D3.rel = (uint32_t*)ptr[1];
         G.D3.ptot = (uint32_t*)ptr[2];
         G.D3.pexit = (uint64_t*)ptr[3];
         G.D3.hist = (uint64_t*)ptr[4];
         G.D3.spend = (uint32_t*)ptr[5];
+        G.D3.ftag = (uint64_t*)ptr[6];
         G.dec3_cap = max_chunks;
     }
     G.D3.max_chunks = max_chunks;
@@ -778,6 +781,7 @@ static int maps_forced(void) {
 int dc_set_decode3_maps(int on) {
     const int old = maps_forced();
     g_maps_force = on ? 1 : 0;
+    if (on < 0) { G.maps_key = 0; G.dense_key = 0; g_maps_force = 0; }   /* tests: forget the remembered streams */
     return old;
 }
 /* the segment decoder's launch for the pending decode: parse3 + decode3, or the maps parse + decode3
@@ -812,6 +816,7 @@ static int decode_device_h(int ct, const void* d_stream, long long nbytes, const
     if ((uintptr_t)d_stream & 3u) return seterr(DC_ERR_ARG, "stream must be 4-byte aligned");
     if (nbytes < 0 && !d_nbits) return seterr(DC_ERR_ARG, "need nbytes or d_nbits");
     if (max_bytes < nbytes) max_bytes = nbytes;
+    dc_decode3_clear_fused();             /* (set again by a fused segment-decoder launch) */
     /* small streams (a Himeno halo plane: 25 KB) decode with 256-bit chunks: 4x more lanes, 4x shorter walks */
     G.dec_small = max_bytes <= small_chunk_max_bytes();
     long long cb = DV(dc_decode_chunk_bits)();

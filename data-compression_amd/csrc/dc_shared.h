@@ -90,6 +90,7 @@ typedef struct Dec3Bufs {
                                       a prediction among its first three tokens declines, as for a
                                       whole stream) */
     uint32_t* spend;               /* [0] tokens of the shard's first chunk that wait for those values */
+    uint64_t* ftag;                /* [fused job = 4 parse jobs] epoch << 32 | tokens (fused3_kernel) */
 } Dec3Bufs;
 
 #ifdef __cplusplus
@@ -129,10 +130,14 @@ int dc_launch_decode_fast(const uint8_t* s, const unsigned long long* dev_nbits,
                           long long num, uint32_t epoch, dc_hip_stream st);
 int dc_launch_decode_serial(const uint8_t* s, const DC_NS Params* P, const DC_NS DecBufs* D, float* out,
                             long long num, dc_hip_stream st);
-/* dense = 1: the decode3 instantiation with a 2080-value job buffer (streams of < ~16 bits per value) */
+/* dense = 1: the decode3 instantiation with a 2080-value job buffer (streams of < ~16 bits per value);
+   the single-launch parse + decode (fused3_kernel) instead of parse3 + decode3 when it is switched on
+   (dc_set_fused3) and the stream qualifies (dc_decode3_last_fused() then says so) */
 int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
                       const DC_NS Params* P, const DC_NS Dec3Bufs* D3, float* out, long long num, uint32_t epoch,
                       int dense, dc_hip_stream st);
+int dc_decode3_last_fused(void);
+void dc_decode3_clear_fused(void);
 int dc_launch_merge_shards(const uint8_t* g, long long P, int world, const unsigned long long* counts, uint8_t* out,
                            long long out_bytes, unsigned long long* total_out, unsigned* err, long long max_bytes,
                            dc_hip_stream st);

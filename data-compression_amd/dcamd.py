@@ -45,7 +45,7 @@ EXT_SYMBOLS = [
     "dc64_stream_capacity", "dc64_encode_device", "dc64_encode_result", "dc64_decode_device", "dc64_decode_finish",
     "dc64_last_decode_flags", "dc64_to_small_device", "dc64_med_device", "dc_set_encode_stream",
     "dc_decode_status", "dc_abi_status", "dc_med_sum_device", "dc_type_from_max", "dc_set_small_chunk_max_bytes",
-    "dc_set_decode3_min_bytes", "dc_set_decode3_seg", "dc_last_decode_was_v3", "dc_last_decode_launched_v3",
+    "dc_set_decode3_min_bytes", "dc_set_decode3_seg", "dc_set_fused3", "dc_fused3_stamps", "dc_fused3_last_seg", "dc_decode3_last_fused", "dc_last_decode_was_v3", "dc_last_decode_launched_v3",
     "dc_encode_status", "dc_encode_clear_status", "dc_encode_mode", "dc_encode_retries", "dc_crc_resend_device",
     "dc_merge_shards_device", "dc_merge_status", "dc_decode_shard3_device", "dc_decode_shard3_fix",
     "dc_decode_status_clear", "dc_set_runs_max_bytes", "dc_last_decode_was_runs",
@@ -473,6 +473,27 @@ class Lib:
         """Force the segment decoder's parse segment length (4, 8 or 16 chunks; 0: by size); returns the
         previous setting."""
         return int(self.L.dc_set_decode3_seg(int(seg)))
+
+    def set_fused3(self, on):
+        """1: decode 16-chunk-segment streams with the single-launch parse + decode (fused3_kernel), 0: with
+        parse3 + decode3 (the default); returns the previous setting."""
+        return int(self.L.dc_set_fused3(int(on)))
+
+    def last_decode_fused(self):
+        """1 if the last segment-decoder launch was the fused parse + decode."""
+        return bool(self.L.dc_decode3_last_fused())
+
+    def fused3_last_seg(self):
+        """The segment length (chunks) of the last fused launch."""
+        return int(self.L.dc_fused3_last_seg())
+
+    def fused3_stamps(self, max_jobs):
+        """The last fused launch's stamps (DC_FUSED3_STAMPS set): an (n, 4) uint64 array of s_memrealtime
+        ticks per fused job (start, parse end, prefix known, decode end)."""
+        buf = np.zeros((int(max_jobs), 4), dtype=np.uint64)
+        self.L.dc_fused3_stamps.restype = C.c_longlong
+        n = int(self.L.dc_fused3_stamps(C.c_void_p(buf.ctypes.data), C.c_longlong(int(max_jobs))))
+        return buf[:max(n, 0)]
 
     def set_runs_max_bytes(self, v):
         """Streams of at most v bytes of capacity use the small-stream decoder (< -1: default 16 KiB + 256,

@@ -228,13 +228,24 @@ long long dc_set_decode3_min_bytes(long long min_bytes);
 /* The segment decoder's parse segment length in 256-bit chunks: 4, 8 or 16 forces one, 0 chooses by the
  * stream's capacity and bound (dc_decode3.hip dc_decode3_seg).  Returns the previous setting. */
 int dc_set_decode3_seg(int seg);
+/* Experiments: 1 decodes 16-chunk-segment streams with the single-launch parse + decode (fused3_kernel,
+ * DESIGN section 4b), 0 with parse3 + decode3 (the default; DC_FUSED3=1 sets it at start).  Returns the
+ * previous setting. */
+int dc_set_fused3(int on);
+/* The last fused launch's per-job stamps when DC_FUSED3_STAMPS is set (4 per fused job: start, parse end,
+ * prefix known, decode end; s_memrealtime, 100 MHz): the number of jobs copied, 0 when none were recorded. */
+long long dc_fused3_stamps(unsigned long long* out, long long max_jobs);
+/* The segment length (chunks) of the last fused launch: 16, 20, 24, 32 or 64 (0: none yet). */
+int dc_fused3_last_seg(void);
+/* 1 if the last segment-decoder launch was the fused one. */
+int dc_decode3_last_fused(void);
 /* 1 if the last decode's values came from the segment decoder (after dc_decode_finish). */
 int dc_last_decode_was_v3(void);
 /* 1: the last finished decode's values came from the segment decoder after the maps parse (a stream whose
  * parse paths merge slowly: noisy ramps, smooth data at small bounds, CT11 without 3-bit codes) */
 int dc_last_decode_used_maps(void);
 /* tests: 1 = parse every segment decode by maps (returns the previous setting) */
-int dc_set_decode3_maps(int on);
+int dc_set_decode3_maps(int on);   /* (-1: also forget the parameters remembered for the maps parse / dense buffer) */
 /* Streams of at most this capacity (bytes) decode with the small-stream decoder (dc_decode_runs.hip: chunk
  * entry maps composed by a scan, one workgroup), unless dc_set_decode3_min_bytes(0) forces the segment
  * decoder; Himeno halo planes take it whatever their capacity (< -1: the default, 16 KiB + 256: 2^12 floats; -1:
