@@ -705,7 +705,8 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
     res = {"nbits": int(nbits), "nbytes": int(nbytes), "wall": wall, "enc_ms": enc_ms, "dec_ms": dec_ms, "self_check": sc,
            "kavg": kavg, "status": int(status | warm_status), "warm_status": int(warm_status), "resends": timed_resends,
            "slow_path_timed": slow[0], "v3": bool(L.L.dc_last_decode_launched_v3()),
-           "runs": bool(L.L.dc_last_decode_launched_runs()),
+           "runs": bool(L.L.dc_last_decode_launched_runs()), "fused": bool(L.L.dc_decode3_last_fused()),
+           "fused_seg": int(L.L.dc_fused3_last_seg()),
            "enc_mode": int(L.L.dc_encode_mode()), "ct9": {k: v for k, v in ct9.items() if k in ("phase_ms", "acks_ok", "nflip")}}
 
     if pipelined and ber <= 0:
@@ -792,7 +793,7 @@ def copy_bandwidth(L, dev, n, reps=10):
     return gbs, COPY_VARIANTS[v]
 
 
-def kernel_table(ct, n, nbytes, kavg, v3=True, enc_mode=1, runs=False):
+def kernel_table(ct, n, nbytes, kavg, v3=True, enc_mode=1, runs=False, fused=False):
     """The timed launches of a step (library timing slots, HIP events on the library stream) and their
     algorithmic bytes: the encoder's count and pack launches (the pack's workgroup 0 scans the tile
     offsets), then the decoder's -- the segment decoder (parse3, whose jobs check the
@@ -814,6 +815,8 @@ def kernel_table(ct, n, nbytes, kavg, v3=True, enc_mode=1, runs=False):
     if runs:              # the small-stream decoder: chunk maps + one-workgroup scans, then the values
         kernels.update({f"runs_map_kernel<{ct}>+runs_scan_kernel<{ct}>": (k[3], 0.0 if fin else float(nbytes)),
                         f"runs_values_kernel<{ct}>": (k[5], 0.0 if fin else dec_b)})
+    elif v3 and fused:    # the single-launch parse + decode: the stream read once, the floats written
+        kernels.update({f"fused3_kernel<{ct}>": (k[3] + k[5], 0.0 if fin else dec_b)})
     elif v3:
         kernels.update({f"parse3_kernel<{ct}>": (k[3], 0.0 if fin else float(nbytes)),
                         f"decode3_kernel<{ct}>": (k[5], 0.0 if fin else dec_b)})
@@ -836,7 +839,8 @@ def line_for(C, W, R, steps):
     kernel (algorithmic bytes / its HIP-event duration on the library stream) and of the whole step."""
     n, nbytes = W["n"], R["nbytes"]
     ms = R["wall"] / steps * 1e3
-    kernels = kernel_table(W["ct"], n, nbytes, R["kavg"], R["v3"], R.get("enc_mode", 1), R.get("runs", False))
+    kernels = kernel_table(W["ct"], n, nbytes, R["kavg"], R["v3"], R.get("enc_mode", 1), R.get("runs", False),
+                           R.get("fused", False))
     for nm, ms_ in R.get("ct9", {}).get("phase_ms", {}).items():   # CT9: every launch of the step
         kernels[nm] = (ms_, 2.0 * nbytes if "copy" in nm else (float(nbytes) if "damaged copy" in nm else 0.0))
     dname = max(kernels, key=lambda k: kernels[k][0])
@@ -846,6 +850,7 @@ def line_for(C, W, R, steps):
     return {"value": round(C.world * 4.0 * n / (ms * 1e-3) / 1e9, 3), "ms_per_step": round(ms, 4),
             "stream_bytes": int(nbytes), "ratio": round(4.0 * n / max(nbytes, 1), 4), "fast_path": R["status"] == 0,
             "decoder_status": R["status"],
+            **({"fused_segment_chunks": R["fused_seg"]} if R.get("fused") else {}),
             "slow_path_in_timed_step": bool(R.get("slow_path_timed", False)),
             "dominant": {"kernel": dname, "avg_launch_ms": round(dms, 4), "achieved_GBs": round(ach, 1),
                          "frac": round(ach / HBM_PEAK_GBS, 4)},
@@ -894,7 +899,8 @@ def main():
         # warm-up on run it inside every timed step and are reported with fast_path false)
         print(f"bench.py: decoder status 0x{R['status']:x} in the timed steps (slow path not timed)", file=sys.stderr)
         sys.exit(1)
-    kernels = kernel_table(ct, n, nbytes, R["kavg"], R["v3"], R.get("enc_mode", 1), R.get("runs", False))
+    kernels = kernel_table(ct, n, nbytes, R["kavg"], R["v3"], R.get("enc_mode", 1), R.get("runs", False),
+                           R.get("fused", False))
     for nm, ms_ in R.get("ct9", {}).get("phase_ms", {}).items():   # (as line_for: the CT9 launches too)
         kernels[nm] = (ms_, 2.0 * nbytes if "copy" in nm else (float(nbytes) if "damaged copy" in nm else 0.0))
     dname = main_line["dominant"]["kernel"]

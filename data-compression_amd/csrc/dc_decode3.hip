@@ -461,18 +461,17 @@ __device__ __forceinline__ uint32_t parse3_job(Ring3& r, uint16_t* recs, const u
     // ---- token offsets: the job's total and every decode job's first token relative to the job
     const uint32_t inc = wave_incl_scan(tot, lane);
     if (lane == 63) D3.ptot[job] = inc;
+    auto put_rel = [&](long long dj, uint32_t v) {
+        if (dj * 64 < D3.max_chunks) D3.rel[dj] = v;
+    };
     if constexpr (64 % seg == 0) {                     // decode jobs start on segment boundaries
-        if (((lane * seg) & 63) == 0) {
-            const long long dj = (long long)job * seg + (lane * seg) / 64;
-            if (dj * 64 < D3.max_chunks) D3.rel[dj] = inc - tot;
-        }
+        if (((lane * seg) & 63) == 0) put_rel((long long)job * seg + (lane * seg) / 64, inc - tot);
     } else {                                           // (seg < 64: at most one decode job starts in a segment)
         const int k = (int)((64 - ((lane * seg) & 63)) & 63);        // its chunk within the segment
         if (k < seg) {
             uint32_t pre = inc - tot;
             for (int c = 0; c < k; c++) pre += (uint32_t)(recs[c * 64 + lane] >> 8);
-            const long long dj = ((long long)job * 64 * seg + (long long)lane * seg + k) / 64;
-            if (dj * 64 < D3.max_chunks) D3.rel[dj] = pre;
+            put_rel(((long long)job * 64 * seg + (long long)lane * seg + k) / 64, pre);
         }
     }
     return (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
@@ -1246,6 +1245,11 @@ extern "C" int dc_set_fused3(int on) {
     return old;
 }
 static int g_f3_seg = 0;
+static long long g_f3_hint_cap = -1, g_f3_hint_nch = 0;
+extern "C" void dc_decode3_size_hint(long long max_chunks, long long nchunks) {
+    g_f3_hint_cap = max_chunks;
+    g_f3_hint_nch = nchunks;
+}
 static int launch_fused3(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
                          const Params* P, const Dec3Bufs* D3, float* out, long long num, uint32_t epoch, hipStream_t st) {
     const void* fp = P->ct == 5 ? (const void*)fused3_kernel<5, 16, D3_CAP> : P->ct == 6 ? (const void*)fused3_kernel<6, 16, D3_CAP>
@@ -1257,7 +1261,10 @@ static int launch_fused3(const uint8_t* s, const unsigned long long* dev_nbits, 
     // parse ~2.35 us per 4 chunks walked -- the pre-walk line and the segment's lines -- its decode ~4.4 us per
     // decode job and wave, ~10 us of prefix wait; measured at 2^26 U10) on the stream's chunks
     // (its capacity when the length is on the device only); DC_FUSED3_SEG forces one
-    const long long nch = host_nbits ? (long long)((host_nbits + 255) / 256) : D3->max_chunks;
+    // (the length of the last stream of this capacity when this one's is on the device only: a stream decoded
+    // over and over, like the bench's, then gets the segment length of its own size)
+    const long long nch = host_nbits ? (long long)((host_nbits + 255) / 256)
+                        : (g_f3_hint_cap == D3->max_chunks && g_f3_hint_nch > 0 ? g_f3_hint_nch : D3->max_chunks);
     int seg = 16;
     double best = 1e30;
     for (int sg : {16, 20, 24, 32, 64}) {
@@ -1324,6 +1331,7 @@ extern "C" int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev
     g_f3_last = fused3_on() && D3->seg == 16 && !dense && !D3->shard;
     if (g_f3_last) {
         dc_mark_phase(4, st);
+        dc_mark_phase(5, st);                   // (the timing slots: an empty parse, the launch as decode's)
         if (launch_fused3(s, dev_nbits, host_nbits, P, D3, out, num, epoch, st)) return -2;
         dbg_wait("fused3_kernel", st);
         dc_mark_phase(7, st);

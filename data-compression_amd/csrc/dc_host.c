@@ -79,6 +79,7 @@ typedef struct {
                                         later decodes with the same parameters start with the dense buffer */
     int dec3_maps;                   /* the pending segment decode parsed by entry -> exit maps */
     int maps_key;                    /* as dense_key, for streams whose parse paths did not meet */
+    int dec3_fusedl;                 /* the pending segment decode's launch was the fused one */
     void* maps_scr; size_t maps_scr_cap;
     int halo_async;                  /* dc_halo_decode_device without dc_decode_finish (dc_set_halo_async) */
     int runs_used;                   /* the pending decode ran the small-stream decoder (dc_decode_runs.hip) */
@@ -797,6 +798,7 @@ static int dec3_launch(const uint8_t* s, const Params* P, float* out, long long 
     }
     if (dc_launch_decode3(s, G.dec_dnbits, G.dec_hnbits, P, &G.D3, out, num, G.dec_epoch, G.dec3_dense, G.st))
         return seterr(DC_ERR_HIP, "decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+    G.dec3_fusedl = dc_decode3_last_fused();
     return DC_OK;
 }
 
@@ -817,6 +819,7 @@ static int decode_device_h(int ct, const void* d_stream, long long nbytes, const
     if (nbytes < 0 && !d_nbits) return seterr(DC_ERR_ARG, "need nbytes or d_nbits");
     if (max_bytes < nbytes) max_bytes = nbytes;
     dc_decode3_clear_fused();             /* (set again by a fused segment-decoder launch) */
+    G.dec3_fusedl = 0;
     /* small streams (a Himeno halo plane: 25 KB) decode with 256-bit chunks: 4x more lanes, 4x shorter walks */
     G.dec_small = max_bytes <= small_chunk_max_bytes();
     long long cb = DV(dc_decode_chunk_bits)();
@@ -951,7 +954,12 @@ int dc_decode_shard3_fix(const float* d_hin) {
 static int read_dec_err(unsigned* err) {
     HIPCHK(hipMemcpyAsync(&G.h_scratch[2], G.D.err, 4, hipMemcpyDeviceToHost, G.st));
     HIPCHK(hipMemcpyAsync(&G.h_scratch[12], G.D.plan, sizeof(Plan), hipMemcpyDeviceToHost, G.st));
+    /* a fused segment decode of a stream whose length is on the device: the length, for the next launch's
+       segment length (dc_decode3_size_hint; the launch itself reads nothing back) */
+    const int hint = G.dec3_fusedl && G.dec_dnbits != NULL;
+    if (hint) HIPCHK(hipMemcpyAsync(&G.h_scratch[4], G.dec_dnbits, 8, hipMemcpyDeviceToHost, G.st));
     HIPCHK(hipStreamSynchronize(G.st));
+    if (hint) dc_decode3_size_hint(G.D3.max_chunks, (long long)((G.h_scratch[4] + 255) / 256));
     *err = (unsigned)(G.h_scratch[2] & 0xFFFFFFFFu);
     const Plan* pl = (const Plan*)&G.h_scratch[12];
     G.dec_nbits = pl->nbits;

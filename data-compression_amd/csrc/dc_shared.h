@@ -138,6 +138,8 @@ int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev_nbits, uns
                       int dense, dc_hip_stream st);
 int dc_decode3_last_fused(void);
 void dc_decode3_clear_fused(void);
+/* the chunks of the last fused decode of a stream of this capacity: the next launch's segment length */
+void dc_decode3_size_hint(long long max_chunks, long long nchunks);
 int dc_launch_merge_shards(const uint8_t* g, long long P, int world, const unsigned long long* counts, uint8_t* out,
                            long long out_bytes, unsigned long long* total_out, unsigned* err, long long max_bytes,
                            dc_hip_stream st);

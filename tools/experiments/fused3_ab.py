@@ -4,7 +4,8 @@ stream, 20 back-to-back decodes), bit-exactness against the two-launch output, a
 stamps (DC_FUSED3_STAMPS=1 must be set in the environment): per fused job the parse, prefix wait and decode
 times, and when the jobs' phases run on the device's timeline.
 
-usage: DC_FUSED3_STAMPS=1 python3 tools/experiments/fused3_ab.py [lg=26] [ct=7]"""
+usage: DC_FUSED3_STAMPS=1 python3 tools/experiments/fused3_ab.py [lg=26] [ct=7] [enc]   (enc: an encode before
+every decode, as the bench's step)"""
 import os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -31,6 +32,9 @@ ls = torch.cuda.ExternalStream(L.L.dc_get_stream())
 L.set_decode3_seg(16)
 
 
+ENC = "enc" in sys.argv[3:]          # re-encode before every decode (the bench's step: the stream fresh)
+
+
 def run(fused, K=20):
     L.set_fused3(fused)
     out = torch.empty(n, dtype=torch.float32, device="cuda")
@@ -39,12 +43,16 @@ def run(fused, K=20):
         L.decode_finish()
     torch.cuda.synchronize()
     L.decode_status_clear()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(ls)
-    for _ in range(K):
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    for k in range(K):
+        if ENC:
+            L.encode_device(ct, x.data_ptr(), n, st.data_ptr(), type_=t, mask17=m17)
+        ev[k][0].record(ls)
         L.decode_device(ct, st.data_ptr(), nb, n, out.data_ptr(), type_=t, mask17=m17, max_bytes=cap)
-    e1.record(ls)
+        ev[k][1].record(ls)
     torch.cuda.synchronize()
+    e0, e1 = ev[0][0], ev[-1][1]
+    per = float(np.mean([a.elapsed_time(b) for a, b in ev])) * 1000
     stv = L.decode_status()
     L.decode_status_clear()
     out.fill_(-7.0)
@@ -52,7 +60,7 @@ def run(fused, K=20):
     L.decode_device(ct, st.data_ptr(), nb, n, out.data_ptr(), type_=t, mask17=m17, max_bytes=cap)
     L.decode_finish()
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1) * 1000 / K, stv, L.L.dc_last_decode_was_v3(), out
+    return per, stv, L.L.dc_last_decode_was_v3(), out
 
 
 us2, s2, v2, ref = run(0)
