@@ -753,7 +753,8 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
             if pst == 0:
                 raise
         res["pipelined"] = {"value": round(C.world * 4.0 * n / (pw / steps) / 1e9, 3),
-                            "ms_per_step": round(pw / steps * 1e3, 4), "fast_path": pst == 0,
+                            "ms_per_step": round(pw / steps * 1e3, 4), "fast_path": pst == 0, "decoder_status": pst,
+                            "encoder_status": int(L.encode_status()),
                             "how": "encode of step k+1 on its own HIP stream overlaps the decode of step k (two "
                                    "stream buffers); every step encodes and decodes the whole block"}
     if check and C.rank == 0:

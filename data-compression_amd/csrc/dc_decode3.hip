@@ -61,11 +61,11 @@ constexpr uint32_t D3_DECLINE = 512u;
                                         // stream that never resynchronises, e.g. a noisy ramp, spent ~1 ms
                                         // per decode in them; U10 at 1e-3 / 1e-6 never needs more than 8)
 #endif
-#ifdef DC_DEC3_PROF
-constexpr unsigned long long D3_LINK_WAIT = 200000; // (the profiling build's stamps slow the walks: 2 ms)
-#else
-constexpr unsigned long long D3_LINK_WAIT = 20000;  // s_memrealtime ticks (100 MHz): 200 us
-#endif
+// s_memrealtime ticks (100 MHz): 2 ms.  Jobs are dispatched in order on each XCD but not across XCDs, so with
+// another kernel running beside (bench.py's pipelined pass: the next step's encode) a job's predecessor can
+// start more than 200 us after it -- the old bound declined such streams (status 0xa00 with 20-chunk
+// segments); the bound only guards against a wait that never ends, which has not been seen
+constexpr unsigned long long D3_LINK_WAIT = 200000;
 // why (diagnostic bits beside 512): 1024 runs mode / capacity, 2048 unresolved link, 4096 fewer tokens
 // than values, 8192 a job denser than its buffer, 16384 the history sentinel or an early prediction
 constexpr uint32_t D3_WHY_RUNS = 1024u, D3_WHY_LINK = 2048u, D3_WHY_SHORT = 4096u, D3_WHY_DENSE = 8192u,
@@ -482,7 +482,7 @@ __global__ __launch_bounds__(64) void parse3_kernel(const uint8_t* __restrict__ 
                                                     const unsigned long long* dev_nbits, unsigned long long host_nbits,
                                                     long long num, uint32_t epoch) {
     constexpr int seg = SEG;
-    static_assert(SEG == 4 || SEG % 8 == 0, "whole region lines; 8- or 16-byte record stores per lane");
+    static_assert(SEG % 4 == 0 && SEG <= 64, "whole region lines; at most one decode job start per segment");
     __shared__ uint32_t ring[D3_RING * 64];
     __shared__ uint16_t recs[seg * 64];                          // [chunk][lane]: the wave's records
     __shared__ uint8_t tl[512];
@@ -1069,6 +1069,14 @@ __global__ __launch_bounds__(64) void shard3_fix_kernel(const uint8_t* __restric
         case 616: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<6, 16>), __VA_ARGS__); break;               \
         case 716: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<7, 16>), __VA_ARGS__); break;               \
         case 1116: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<11, 16>), __VA_ARGS__); break;             \
+        case 520: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<5, 20>), __VA_ARGS__); break;               \
+        case 620: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<6, 20>), __VA_ARGS__); break;               \
+        case 720: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<7, 20>), __VA_ARGS__); break;               \
+        case 1120: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<11, 20>), __VA_ARGS__); break;             \
+        case 524: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<5, 24>), __VA_ARGS__); break;               \
+        case 624: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<6, 24>), __VA_ARGS__); break;               \
+        case 724: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<7, 24>), __VA_ARGS__); break;               \
+        case 1124: hipLaunchKernelGGL(HIP_KERNEL_NAME(KER<11, 24>), __VA_ARGS__); break;             \
         default: return -2;                                                                          \
     }
 
@@ -1077,7 +1085,8 @@ template <int CAP>
 static const void* decode3_fn(int ct, int seg) {
 #define D3F(C)                                                                                       \
     (seg == 4 ? (const void*)decode3_kernel<C, 4, CAP> : seg == 8 ? (const void*)decode3_kernel<C, 8, CAP> \
-                                                       : (const void*)decode3_kernel<C, 16, CAP>)
+     : seg == 20 ? (const void*)decode3_kernel<C, 20, CAP> : seg == 24 ? (const void*)decode3_kernel<C, 24, CAP> \
+                 : (const void*)decode3_kernel<C, 16, CAP>)
     return ct == 5 ? D3F(5) : ct == 6 ? D3F(6) : ct == 7 ? D3F(7) : D3F(11);
 #undef D3F
 }
@@ -1092,7 +1101,8 @@ static int launch_decode3_cap(int ct, int seg, int grid, hipStream_t st, const u
         break;
     switch (ct * 100 + seg) {
         D3C(5, 4) D3C(6, 4) D3C(7, 4) D3C(11, 4) D3C(5, 8) D3C(6, 8) D3C(7, 8) D3C(11, 8)
-        D3C(5, 16) D3C(6, 16) D3C(7, 16) D3C(11, 16)
+        D3C(5, 16) D3C(6, 16) D3C(7, 16) D3C(11, 16) D3C(5, 20) D3C(6, 20) D3C(7, 20) D3C(11, 20)
+        D3C(5, 24) D3C(6, 24) D3C(7, 24) D3C(11, 24)
         default: return -2;
     }
 #undef D3C
@@ -1117,19 +1127,20 @@ static int resident3(const void* f, int threads) {
 // side by side for longer, tools/sync_sim.py: 4% of 1024-bit pre-walks unsynchronised, 0.4% not met
 // within 4 chunks) takes 8 chunks or more; CT11 (32-bit verbatim tokens, a path
 // read out of phase stays out of phase until a 3-bit code realigns it) takes 8 or more.  The host sizes the scratch for
-// 4-chunk segments (DC_DEC3_SEG=4|8|16 forces one)
+// 4-chunk segments (DC_DEC3_SEG=4|8|16|20|24 forces one)
 static int g_seg_forced = -1;
 static int seg_forced() {
     if (g_seg_forced < 0) {
         const char* e = getenv("DC_DEC3_SEG");
-        g_seg_forced = (e && (atoi(e) == 4 || atoi(e) == 8 || atoi(e) == 16)) ? atoi(e) : 0;
+        const int f = e ? atoi(e) : 0;
+        g_seg_forced = (f == 4 || f == 8 || f == 16 || f == 20 || f == 24) ? f : 0;
     }
     return g_seg_forced;
 }
 // tests: force a segment length (4, 8 or 16; 0: by size); returns the previous setting
 extern "C" int dc_set_decode3_seg(int seg) {
     const int old = seg_forced();
-    g_seg_forced = (seg == 4 || seg == 8 || seg == 16) ? seg : 0;
+    g_seg_forced = (seg == 4 || seg == 8 || seg == 16 || seg == 20 || seg == 24) ? seg : 0;
     return old;
 }
 extern "C" int dc_decode3_seg(long long max_chunks, int B, int ct) {
@@ -1142,7 +1153,10 @@ extern "C" int dc_decode3_seg(long long max_chunks, int B, int ct) {
     // floats (its 32-bit tokens resynchronise slowly), CT6 from 2^25; CT5 / CT7 never up to 2^26
     if (ct == 11) return D3_SEG;
     if (ct == 6) return max_chunks <= 1100000ll ? 8 : D3_SEG;
-    return max_chunks <= 2500000ll ? 8 : D3_SEG;
+    // CT5 / CT7 above 2.5 M chunks of capacity: 20-chunk segments -- fewer parse waves than parse3's 24 per CU
+    // are resident (2^26 U10: 3971 jobs instead of 4964), each walks 20 % more bits but faster (parse3 88.6-89.1
+    // -> 83.3 us, bench 767-775 -> 782-786 GB/s, tools/gpu_seg_ab.sh; 24 chunks: 86.6-87.1 us)
+    return max_chunks <= 2500000ll ? 8 : 20;
 }
 
 // DC_DEC3_DEBUG=1: wait for every kernel (at most 2 s each) and report one that does not finish
@@ -1188,17 +1202,19 @@ static void dbg_dump(const Dec3Bufs* D3) {
 // resident grids per (CT, segment length, buffer) instantiation: every job of a call must be resident at once
 // (parse3's link wait, decode3's history wait), so each grid is sized from its own kernel's occupancy
 static int decode3_grids(const Params* P, const Dec3Bufs* D3, int dense, int* g1_out, int* g3_out) {
-    static int gp[3][12], gd[2][3][12];
+    static int gp[5][12], gd[2][5][12];
     const int ci = (P->ct > 0 && P->ct < 12) ? P->ct : 0;
-    if (D3->seg != 4 && D3->seg != 8 && D3->seg != 16) return -2;
+    if (D3->seg != 4 && D3->seg != 8 && D3->seg != 16 && D3->seg != 20 && D3->seg != 24) return -2;
     if (P->ct != 5 && P->ct != 6 && P->ct != 7 && P->ct != 11) return -2;
-    const int si = D3->seg == 16 ? 1 : (D3->seg == 4 ? 2 : 0), di = dense ? 1 : 0;
+    const int si = D3->seg == 16 ? 1 : D3->seg == 4 ? 2 : D3->seg == 20 ? 3 : D3->seg == 24 ? 4 : 0, di = dense ? 1 : 0;
     if (!gp[si][ci]) {
         const void* fp;
 #define DC_PICK3(KER, SEGV) (P->ct == 5 ? (const void*)KER<5, SEGV> : P->ct == 6 ? (const void*)KER<6, SEGV>   \
                              : P->ct == 7 ? (const void*)KER<7, SEGV> : (const void*)KER<11, SEGV>)
         if (si == 1) fp = DC_PICK3(parse3_kernel, 16);
         else if (si == 2) fp = DC_PICK3(parse3_kernel, 4);
+        else if (si == 3) fp = DC_PICK3(parse3_kernel, 20);
+        else if (si == 4) fp = DC_PICK3(parse3_kernel, 24);
         else fp = DC_PICK3(parse3_kernel, 8);
 #undef DC_PICK3
         gp[si][ci] = resident3(fp, 64);
@@ -1328,7 +1344,7 @@ extern "C" int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev
                                  int dense, hipStream_t st) {
     int g1 = 0, g3 = 0;
     if (decode3_grids(P, D3, dense, &g1, &g3)) return -2;
-    g_f3_last = fused3_on() && D3->seg == 16 && !dense && !D3->shard;
+    g_f3_last = fused3_on() && D3->seg >= 16 && !dense && !D3->shard;
     if (g_f3_last) {
         dc_mark_phase(4, st);
         dc_mark_phase(5, st);                   // (the timing slots: an empty parse, the launch as decode's)
@@ -1353,8 +1369,11 @@ extern "C" int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev
 
 // decode3 alone, after a parse that filled rec / rel / ptot another way (dc_launch_maps_parse)
 extern "C" int dc_launch_decode3_values(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
-                                        const Params* P, const Dec3Bufs* D3, float* out, long long num, uint32_t epoch,
+                                        const Params* P, const Dec3Bufs* D3in, float* out, long long num, uint32_t epoch,
                                         int dense, hipStream_t st) {
+    Dec3Bufs Dv = *D3in;
+    Dec3Bufs* D3 = &Dv;
+    Dv.seg = dc_maps_seg(D3in->seg);                   // (the maps parse's parse jobs)
     int g1 = 0, g3 = 0;
     if (decode3_grids(P, D3, dense, &g1, &g3)) return -2;
     if (dense) launch_decode3_cap<D3_CAP_DENSE>(P->ct, D3->seg, g3, st, s, *P, *D3, dev_nbits, host_nbits, out, num, epoch);

@@ -271,8 +271,15 @@ extern "C" long long dc_maps_scratch_bytes(long long max_chunks) {
     return ngr * 32 + ngr + nb * 32 + nb + 64 + 16 + ngr * 32 * 16;
 }
 
+// the parse-job length (decode jobs) the maps parse writes ptot / rel for: the segment decoder's when it divides a
+// scan workgroup's 128 decode jobs, else 16 (dc_launch_decode3_values decodes with the same)
+extern "C" int dc_maps_seg(int seg) { return (MP_B / 8) % seg == 0 ? seg : 16; }
+
 extern "C" int dc_launch_maps_parse(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
-                                    const Params* P, const Dec3Bufs* D3, long long num, void* scratch, hipStream_t st) {
+                                    const Params* P, const Dec3Bufs* D3in, long long num, void* scratch, hipStream_t st) {
+    Dec3Bufs Dv = *D3in;
+    const Dec3Bufs* D3 = &Dv;
+    Dv.seg = dc_maps_seg(D3in->seg);
     const long long ngr = (D3->max_chunks + MP_G - 1) / MP_G, nb = (ngr + MP_B - 1) / MP_B;
     if (nb > (long long)MP_TOPK * MP_B || (MP_B / 8) % D3->seg) return -2;
     uint8_t* gmap = (uint8_t*)scratch;

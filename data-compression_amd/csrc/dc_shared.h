@@ -137,6 +137,7 @@ int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev_nbits, uns
                       const DC_NS Params* P, const DC_NS Dec3Bufs* D3, float* out, long long num, uint32_t epoch,
                       int dense, dc_hip_stream st);
 int dc_decode3_last_fused(void);
+int dc_maps_seg(int seg);
 void dc_decode3_clear_fused(void);
 /* the chunks of the last fused decode of a stream of this capacity: the next launch's segment length */
 void dc_decode3_size_hint(long long max_chunks, long long nchunks);

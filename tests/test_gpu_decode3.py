@@ -155,13 +155,14 @@ def test_decode3_zero_runs(v3, oracle, ct, n, kind):
         assert not v3.last_decode_was_v3()
 
 
-@pytest.mark.parametrize("seg", [4, 8, 16])
+@pytest.mark.parametrize("seg", [4, 8, 16, 20, 24])
 @pytest.mark.parametrize("kind,n", [("u10", 1 << 20), ("u10", 12345), ("mixed", 500000), ("sparse", 400009),
                                     ("u10", 4097)])
 @pytest.mark.parametrize("ct", CTS)
 def test_decode3_segment_lengths(v3, oracle, seg, kind, n, ct):
-    """Every parse segment length (4, 8, 16 chunks: the pre-walk, the record stores, the jobs per parse
-    job) decodes exactly; ordinary streams stay in the segment decoder at each."""
+    """Every parse segment length (4, 8, 16, 20, 24 chunks: the pre-walk, the record stores, the jobs per parse
+    job, decode jobs starting inside a segment) decodes exactly; ordinary streams stay in the segment decoder at
+    each (the maps parse keeps 16-chunk parse jobs when the length does not divide 128 decode jobs)."""
     old = v3.set_decode3_seg(seg)
     try:
         v3.set_bound(1e-3)
