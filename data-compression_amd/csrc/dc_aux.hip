@@ -18,44 +18,47 @@
 namespace dc {
 
 // ---------------------------------------------------------------- toSmallDataset_float
-struct MinKey { float v; long long i; };
-
-__device__ __forceinline__ MinKey min_pick(MinKey a, MinKey b) {
-    const bool an = a.v != a.v, bn = b.v != b.v;        // NaN never wins (except as data[0])
-    if (an) return b;
-    if (bn) return a;
-    if (b.v < a.v) return b;
-    if (a.v < b.v) return a;
-    return a.i <= b.i ? a : b;                           // equal (incl. +0 == -0): first occurrence
-}
-
-// per-workgroup (min, first index) over x[1..n): float4 loads, grid-stride; min_pick is a total order
-// (value, then index), so the partials can be combined in any order
+// per-workgroup minimum of x[1..n) (NaN ignored: hardware minNum) and the index of the first zero (+0 or -0)
+// in it: the reference keeps data[0] unless a later value is strictly smaller, so equal values only matter for
+// zeros, where the first one's sign wins (min_final).  Four float4 loads of a thread in flight at once
+// (coalesced: q, q + S, q + 2S, q + 3S).  (r05: with a (value, index) total order per element the pass ran at
+// ~3.3 TB/s, issue-bound on the 64-bit index selects)
 __global__ __launch_bounds__(256) void min_partial_kernel(const float* __restrict__ x, long long n,
                                                           float* __restrict__ pv, long long* __restrict__ pi) {
     __shared__ float sv[256];
     __shared__ long long si[256];
-    MinKey m = {__int_as_float(0x7fc00000), (long long)1 << 62};
+    float mv = __int_as_float(0x7fc00000);
+    long long fz = (long long)1 << 62;
     const long long n4 = ((reinterpret_cast<uintptr_t>(x) & 15u) == 0) ? (n >> 2) : 0;
     const float4* x4 = reinterpret_cast<const float4*>(x);
-    for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (long long)gridDim.x * blockDim.x) {
-        const float4 v = x4[q];
-        const long long i = 4 * q;
-        if (i > 0) m = min_pick(m, MinKey{v.x, i});          // element 0 is the reference's start value
-        m = min_pick(m, MinKey{v.y, i + 1});
-        m = min_pick(m, MinKey{v.z, i + 2});
-        m = min_pick(m, MinKey{v.w, i + 3});
+    const long long S = (long long)gridDim.x * blockDim.x;
+    for (long long q0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; q0 < n4; q0 += 4 * S) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {                      // (past the end: NaN, which no minimum takes)
+            const float qn = __int_as_float(0x7fc00000);
+            v[u] = q0 + u * S < n4 ? x4[q0 + u * S] : make_float4(qn, qn, qn, qn);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const long long q = q0 + u * S;
+            const float a = q == 0 ? __int_as_float(0x7fc00000) : v[u].x;   // (element 0 is the start value)
+            mv = fminf(mv, fminf(fminf(a, v[u].y), fminf(v[u].z, v[u].w)));
+            const int k = a == 0.f ? 0 : v[u].y == 0.f ? 1 : v[u].z == 0.f ? 2 : v[u].w == 0.f ? 3 : 4;
+            if (k < 4 && q < n4) fz = min(fz, 4 * q + k);
+        }
     }
-    for (long long i = max(4 * n4, 1ll) + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (long long)gridDim.x * blockDim.x)
-        m = min_pick(m, MinKey{x[i], i});
-    sv[threadIdx.x] = m.v; si[threadIdx.x] = m.i;
+    for (long long i = max(4 * n4, 1ll) + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += S) {
+        const float a = x[i];
+        mv = fminf(mv, a);
+        if (a == 0.f) fz = min(fz, i);
+    }
+    sv[threadIdx.x] = mv; si[threadIdx.x] = fz;
     __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) {
-            MinKey a = {sv[threadIdx.x], si[threadIdx.x]}, b = {sv[threadIdx.x + s], si[threadIdx.x + s]};
-            const MinKey r = min_pick(a, b);
-            sv[threadIdx.x] = r.v; si[threadIdx.x] = r.i;
+    for (int st = 128; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st) {
+            sv[threadIdx.x] = fminf(sv[threadIdx.x], sv[threadIdx.x + st]);
+            si[threadIdx.x] = min(si[threadIdx.x], si[threadIdx.x + st]);
         }
         __syncthreads();
     }
@@ -67,27 +70,36 @@ __global__ __launch_bounds__(256) void min_final_kernel(const float* __restrict_
                                                         float* __restrict__ out_min) {
     __shared__ float sv[256];
     __shared__ long long si[256];
-    MinKey m = {__int_as_float(0x7fc00000), (long long)1 << 62};
-    for (int p = threadIdx.x; p < nparts; p += 256) m = min_pick(m, MinKey{pv[p], pi[p]});
-    sv[threadIdx.x] = m.v; si[threadIdx.x] = m.i;
+    float mv = __int_as_float(0x7fc00000);
+    long long fz = (long long)1 << 62;
+    for (int p = threadIdx.x; p < nparts; p += 256) { mv = fminf(mv, pv[p]); fz = min(fz, pi[p]); }
+    sv[threadIdx.x] = mv; si[threadIdx.x] = fz;
     __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) {
-            MinKey a = {sv[threadIdx.x], si[threadIdx.x]}, b = {sv[threadIdx.x + s], si[threadIdx.x + s]};
-            const MinKey r = min_pick(a, b);
-            sv[threadIdx.x] = r.v; si[threadIdx.x] = r.i;
+    for (int st = 128; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st) {
+            sv[threadIdx.x] = fminf(sv[threadIdx.x], sv[threadIdx.x + st]);
+            si[threadIdx.x] = min(si[threadIdx.x], si[threadIdx.x + st]);
         }
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        const float mv = sv[0];
+        const float m = sv[0];
         const float x0 = x[0];
         float r = x0;                                        // min = data[0]; later strictly smaller wins
-        if (!(mv != mv) && mv < x0) r = mv;
+        if (!(m != m) && m < x0) r = m == 0.f ? x[si[0]] : m;   // (a zero: the first one, with its sign)
         *out_min = r;
     }
 }
 
+// a - b as the reference's x86 build computes it (SSE subss): a NaN operand propagates quieted, the first one
+// when both are, and an invalid result (inf - inf) is the default NaN 0xFFC00000 -- the GPU's fsub returns
+// 0x7FC00000 in every case
+__device__ __forceinline__ float sub_x86(float a, float b) {
+    if (__builtin_expect(a != a, 0)) return __uint_as_float(__float_as_uint(a) | 0x00400000u);
+    if (__builtin_expect(b != b, 0)) return __uint_as_float(__float_as_uint(b) | 0x00400000u);
+    const float r = __fsub_rn(a, b);
+    return r != r ? __uint_as_float(0xFFC00000u) : r;
+}
 __global__ __launch_bounds__(256) void sub_min_kernel(const float* __restrict__ x, long long n,
                                                       const float* __restrict__ mn, float* __restrict__ y) {
     const float m = *mn;
@@ -97,12 +109,12 @@ __global__ __launch_bounds__(256) void sub_min_kernel(const float* __restrict__ 
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
          i += (long long)gridDim.x * blockDim.x) {
         float4 v = x4[i];
-        v.x = __fsub_rn(v.x, m); v.y = __fsub_rn(v.y, m); v.z = __fsub_rn(v.z, m); v.w = __fsub_rn(v.w, m);
+        v.x = sub_x86(v.x, m); v.y = sub_x86(v.y, m); v.z = sub_x86(v.z, m); v.w = sub_x86(v.w, m);
         y4[i] = v;
     }
     for (long long i = (n4 << 2) + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (long long)gridDim.x * blockDim.x)
-        y[i] = __fsub_rn(x[i], m);
+        y[i] = sub_x86(x[i], m);
 }
 
 // ---------------------------------------------------------------- med_dataset_float

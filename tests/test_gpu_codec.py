@@ -24,6 +24,42 @@ def test_prepasses_gpu(dc, bound, case):
     assert mean == g[f"{case}/mean"] and t == g[f"{case}/type"]
 
 
+@pytest.mark.parametrize("kind", ["pos_zero_first", "neg_zero_first", "zero_at_0", "neg_zero_at_0", "nan_at_0",
+                                  "nans", "inf", "neg", "all_nan_tail", "equal"])
+@pytest.mark.parametrize("n", [1, 2, 5, 4097, 1 << 20, (1 << 20) + 3])
+def test_to_small_edge_cases(dc, oracle, kind, n):
+    """toSmallDataset_float's minimum (impl/dataCompression.c: data[0], replaced only by a strictly smaller
+    value, NaNs never) bit for bit against the oracle: signed zeros (the first zero's sign wins when the
+    minimum is zero), NaN at data[0] and elsewhere, infinities, negatives, ragged sizes."""
+    rs = np.random.RandomState(n)
+    x = (rs.rand(n).astype(np.float32) * 10 + 1).astype(np.float32)
+    m = n // 2
+    if kind == "pos_zero_first" and n > 3:
+        x[m] = 0.0; x[m + 1:] = np.where(rs.rand(n - m - 1) < 0.01, np.float32(-0.0), x[m + 1:])
+    elif kind == "neg_zero_first" and n > 3:
+        x[m] = -0.0; x[m + 1:] = np.where(rs.rand(n - m - 1) < 0.01, np.float32(0.0), x[m + 1:])
+    elif kind == "zero_at_0":
+        x[0] = 0.0; x[1::7] = -0.0
+    elif kind == "neg_zero_at_0":
+        x[0] = -0.0; x[1::5] = 0.0
+    elif kind == "nan_at_0":
+        x[0] = np.nan; x[1::3] = -3.0
+    elif kind == "nans":
+        x[1::4] = np.nan; x[-1] = 0.5
+    elif kind == "inf":
+        x[::9] = np.inf; x[n // 3] = -np.inf
+    elif kind == "neg":
+        x -= 20.0; x[-1] = -100.0
+    elif kind == "all_nan_tail":
+        x[1:] = np.nan
+    elif kind == "equal":
+        x[:] = 2.5
+    mn, xs = dc.to_small(x)
+    omn, oxs = oracle.to_small(x)
+    assert np.float32(mn).view(np.uint32) == np.float32(omn).view(np.uint32)
+    assert np.array_equal(xs.view(np.uint32), oxs.view(np.uint32))
+
+
 @pytest.mark.parametrize("bound", BOUNDS)
 @pytest.mark.parametrize("case", CASES)
 @pytest.mark.parametrize("ct", CTS)
