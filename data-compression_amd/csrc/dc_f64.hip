@@ -970,10 +970,19 @@ __global__ void min_final(const double* __restrict__ x, const double* __restrict
     *dmin = (x0 != x0 || bi < 0) ? x0 : x[bi];
 }
 
+// a - b as the reference's x86 build computes it (SSE subsd): a NaN operand propagates quieted, the first one
+// when both are, and an invalid result (inf - inf) is the default NaN 0xFFF8000000000000
+__device__ __forceinline__ double sub_x86(double a, double b) {
+    const unsigned long long q = 0x0008000000000000ull;
+    if (__builtin_expect(a != a, 0)) return __longlong_as_double((long long)((unsigned long long)__double_as_longlong(a) | q));
+    if (__builtin_expect(b != b, 0)) return __longlong_as_double((long long)((unsigned long long)__double_as_longlong(b) | q));
+    const double r = __dsub_rn(a, b);
+    return r != r ? __longlong_as_double((long long)0xFFF8000000000000ull) : r;
+}
 __global__ void sub_min(const double* __restrict__ x, long long n, const double* __restrict__ dmin, double* __restrict__ y) {
     const double m = *dmin;
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
-        y[i] = __dsub_rn(x[i], m);
+        y[i] = sub_x86(x[i], m);
 }
 
 }  // namespace dc64

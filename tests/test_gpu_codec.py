@@ -25,7 +25,7 @@ def test_prepasses_gpu(dc, bound, case):
 
 
 @pytest.mark.parametrize("kind", ["pos_zero_first", "neg_zero_first", "zero_at_0", "neg_zero_at_0", "nan_at_0",
-                                  "nans", "inf", "neg", "all_nan_tail", "equal"])
+                                  "nans", "inf", "neg", "all_nan_tail", "equal", "snan"])
 @pytest.mark.parametrize("n", [1, 2, 5, 4097, 1 << 20, (1 << 20) + 3])
 def test_to_small_edge_cases(dc, oracle, kind, n):
     """toSmallDataset_float's minimum (impl/dataCompression.c: data[0], replaced only by a strictly smaller
@@ -54,6 +54,8 @@ def test_to_small_edge_cases(dc, oracle, kind, n):
         x[1:] = np.nan
     elif kind == "equal":
         x[:] = 2.5
+    elif kind == "snan":                                  # signalling NaNs with payloads: quieted, kept
+        x.view(np.uint32)[1::5] = np.uint32(0x7F800123)
     mn, xs = dc.to_small(x)
     omn, oxs = oracle.to_small(x)
     assert np.float32(mn).view(np.uint32) == np.float32(omn).view(np.uint32)

@@ -28,6 +28,32 @@ def test_prepasses64_gpu(dc, bound, case):
     assert mean == g[f"{case}/mean"] and t == g[f"{case}/type"]
 
 
+@pytest.mark.parametrize("kind", ["neg_zero_first", "zero_at_0", "nan_at_0", "nans", "inf", "snan"])
+@pytest.mark.parametrize("n", [1, 5, 4097, (1 << 18) + 3])
+def test_to_small64_edge_cases(dc, oracle, kind, n):
+    """toSmallDataset_double bit for bit against the oracle (x86): signed zeros, NaN at data[0] and elsewhere
+    (quieted payloads propagate through the subtraction), infinities (inf - inf: the default NaN)."""
+    rs = np.random.RandomState(n)
+    x = rs.rand(n) * 10 + 1
+    if kind == "neg_zero_first" and n > 3:
+        x[n // 2] = -0.0; x[n // 2 + 1::11] = 0.0
+    elif kind == "zero_at_0":
+        x[0] = 0.0; x[1::7] = -0.0
+    elif kind == "nan_at_0":
+        x[0] = np.nan; x[1::3] = -3.0
+    elif kind == "nans":
+        x[1::4] = np.nan; x[-1] = 0.5
+    elif kind == "inf":
+        x[::9] = np.inf; x[n // 3] = -np.inf
+    elif kind == "snan":
+        x[1::5] = np.nan
+        x.view(np.uint64)[1::5] = np.uint64(0x7FF0000000000123)
+    mn, xs = dc.to_small64(x)
+    omn, oxs = oracle.to_small64(x)
+    assert np.float64(mn).view(np.uint64) == np.float64(omn).view(np.uint64)
+    assert np.array_equal(xs.view(np.uint64), oxs.view(np.uint64))
+
+
 @pytest.mark.parametrize("bound", BOUNDS)
 @pytest.mark.parametrize("case", CASES64)
 @pytest.mark.parametrize("ct", CTS)
