@@ -542,20 +542,29 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
         seed = [1]
         acks = []
         ack_buf = torch.zeros((max(steps, warmup) + 1, 2), dtype=torch.int32, pin_memory=True)
-        CT9_PHASES = (["crcf_final_kernel (sender CRC: combine of the encoder's block CRCs)", "channel copy",
-                       "flip_bits_kernel", "crcf_blocks + crcf_final (receiver CRC, damaged copy)",
-                       "crc_blocks<copy> + crc_final2 (resend copy with its CRC + check)"]
-                      if os.environ.get("DC_CT9_FUSED", "0") == "1" else
-                      ["(encode call beyond its kernel)", "crc_blocks<copy> + crc_final2 (send: channel copy + sender CRC)",
-                       "flip_bits_kernel", "crc_blocks + crc_final2 (receiver CRC, damaged copy)",
-                       "crc_blocks<copy> + crc_final2 (resend copy with its CRC + check)"])
+        # DC_CT9_MODE: "send" (default) the encoder writes its stream into the receiver's buffer as well (the
+        # channel, dc_encode_send_device) and one pass CRCs both copies after the damage (dc_crc32_pair_device);
+        # "copy" the send as a copy pass that CRCs what it sends (dc_crc32_copy_device) and a receiver pass;
+        # "fused" (or DC_CT9_FUSED=1) the sender's CRC inside the encoder's tiles (slower)
+        ct9_mode = "fused" if os.environ.get("DC_CT9_FUSED", "0") == "1" else os.environ.get("DC_CT9_MODE", "copy")
+        CT9_PHASES = {
+            "fused": ["crcf_final_kernel (sender CRC: combine of the encoder's block CRCs)", "channel copy",
+                      "flip_bits_kernel", "crcf_blocks + crcf_final (receiver CRC, damaged copy)",
+                      "crc_blocks<copy> + crc_final2 (resend copy with its CRC + check)"],
+            "copy": ["(encode call beyond its kernel)", "crc_blocks<copy> + crc_final2 (send: channel copy + sender CRC)",
+                     "flip_bits_kernel", "crc_blocks + crc_final2 (receiver CRC, damaged copy)",
+                     "crc_blocks<copy> + crc_final2 (resend copy with its CRC + check)"],
+            "send": ["(encode call beyond its kernel: the encoder also writes the receiver's copy)", "(no send pass)",
+                     "flip_bits_kernel", "crc_blocks x2 + crc_final2 x2 (sender's and receiver's CRC, one pass)",
+                     "crc_blocks<copy> + crc_final2 (resend copy with its CRC + check)"]}[ct9_mode]
 
         # Default: the send copies the stream into the receiver's buffer and CRCs the bytes it sends in one pass
         # (dc_crc32_copy_device), the receiver CRCs what arrived (dc_crc32_device_async), the resend copies and
         # CRCs in one pass (dc_crc_resend_crc_device).  DC_CT9_FUSED=1: the sender's CRC inside the encoder's
         # tiles and the receiver's by the 16 KiB-block kernels (dc_encode_crc_device, dc_crc32_stream_device),
         # which measured slower.
-        fused_crc = os.environ.get("DC_CT9_FUSED", "0") == "1"
+        fused_crc = ct9_mode == "fused"
+        send_mode = ct9_mode == "send"
 
         def step(ev=None, ph=None):                          # noqa: F811 -- the CT9 variant of the step
             def mark(i):
@@ -569,6 +578,11 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
                 mark(0)
                 with torch.cuda.stream(ext):
                     rcv[:nbytes].copy_(stream[:nbytes])
+            elif send_mode:
+                # the send: the encoder writes the stream into the receiver's buffer too (no copy pass)
+                L.encode_send_device(ct, xs.data_ptr(), n, stream.data_ptr(), rcv.data_ptr(), d_nbits.data_ptr(),
+                                     idx0=idx0, type_=typ, mask17=mask17)
+                mark(0)
             else:
                 L.encode_device(ct, xs.data_ptr(), n, stream.data_ptr(), idx0=idx0, type_=typ, mask17=mask17,
                                 total_ptr=d_nbits.data_ptr())
@@ -581,6 +595,8 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
             mark(2)
             if fused_crc:
                 L.crc32_stream_device(rcv.data_ptr(), nbytes, d_crc.data_ptr() + 4)
+            elif send_mode:                                  # the sender's CRC and the receiver's, one pass
+                L.crc32_pair_device(stream.data_ptr(), rcv.data_ptr(), nbytes, d_crc.data_ptr(), d_crc.data_ptr() + 4)
             else:
                 L.crc32_device_async(rcv.data_ptr(), nbytes, d_crc.data_ptr() + 4)
             mark(3)
@@ -835,6 +851,16 @@ def kernel_table(ct, n, nbytes, kavg, v3=True, enc_mode=1, runs=False, fused=Fal
     return kernels
 
 
+def ct9_bytes(name, nbytes):
+    """Algorithmic bytes of a CT9 phase: a copy pass reads and writes the stream, a CRC pass reads it (the pair
+    pass both copies), the flips and the launch gaps nothing."""
+    if "damaged copy" in name:
+        return float(nbytes)
+    if "one pass" in name or "copy" in name:
+        return 2.0 * nbytes
+    return 0.0
+
+
 def line_for(C, W, R, steps):
     """Summary of one configuration: value (GB/s of input floats, all ranks), roofline of the dominant
     kernel (algorithmic bytes / its HIP-event duration on the library stream) and of the whole step."""
@@ -843,7 +869,7 @@ def line_for(C, W, R, steps):
     kernels = kernel_table(W["ct"], n, nbytes, R["kavg"], R["v3"], R.get("enc_mode", 1), R.get("runs", False),
                            R.get("fused", False))
     for nm, ms_ in R.get("ct9", {}).get("phase_ms", {}).items():   # CT9: every launch of the step
-        kernels[nm] = (ms_, 2.0 * nbytes if "copy" in nm else (float(nbytes) if "damaged copy" in nm else 0.0))
+        kernels[nm] = (ms_, ct9_bytes(nm, nbytes))
     dname = max(kernels, key=lambda k: kernels[k][0])
     dms, dbytes = kernels[dname]
     ach = dbytes / (dms * 1e-3) / 1e9 if dms > 0 else 0.0
@@ -903,7 +929,7 @@ def main():
     kernels = kernel_table(ct, n, nbytes, R["kavg"], R["v3"], R.get("enc_mode", 1), R.get("runs", False),
                            R.get("fused", False))
     for nm, ms_ in R.get("ct9", {}).get("phase_ms", {}).items():   # (as line_for: the CT9 launches too)
-        kernels[nm] = (ms_, 2.0 * nbytes if "copy" in nm else (float(nbytes) if "damaged copy" in nm else 0.0))
+        kernels[nm] = (ms_, ct9_bytes(nm, nbytes))
     dname = main_line["dominant"]["kernel"]
     achievable, copy_how = copy_bandwidth(C.L, C.dev, n)
     traffic, traffic_src, ktraffic = None, None, None

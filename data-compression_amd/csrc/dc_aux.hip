@@ -1236,13 +1236,17 @@ __device__ __forceinline__ uint32_t xpow8n(unsigned long long n, const uint32_t*
 #endif
 // COPY (the CT9 resend): only when the gate's two CRCs differ (the received copy was damaged), the run is also
 // written to dst -- the resent copy and its CRC in one pass -- and gate_count counts the resends
+// (blockIdx.y = 1: the second buffer s2 into part2 -- the CT9 pair pass, dc_crc32_pair_device)
 template <bool COPY>
-__global__ __launch_bounds__(256) void crc_blocks_kernel(const uint8_t* __restrict__ s, long long nbytes,
+__global__ __launch_bounds__(256) void crc_blocks_kernel(const uint8_t* __restrict__ s_in, long long nbytes,
                                                          const uint32_t* __restrict__ tab_g,
                                                          const uint32_t* __restrict__ kpow_g,
                                                          const uint32_t* __restrict__ x2n_g,
-                                                         uint32_t* __restrict__ part, uint8_t* __restrict__ dst,
-                                                         const uint32_t* __restrict__ gate, unsigned* __restrict__ gate_count) {
+                                                         uint32_t* __restrict__ part_in, uint8_t* __restrict__ dst,
+                                                         const uint32_t* __restrict__ gate, unsigned* __restrict__ gate_count,
+                                                         const uint8_t* __restrict__ s2, uint32_t* __restrict__ part2) {
+    const uint8_t* __restrict__ s = blockIdx.y ? s2 : s_in;
+    uint32_t* __restrict__ part = blockIdx.y ? part2 : part_in;
     if (COPY && gate) {
         if (gate[0] == gate[1]) return;
         if (gate_count && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(gate_count, 1u);
@@ -1406,10 +1410,14 @@ __device__ __forceinline__ uint32_t mul_tab(const uint32_t (*T)[256], uint32_t a
     return (T[0][a & 255u] ^ T[1][(a >> 8) & 255u]) ^ (T[2][(a >> 16) & 255u] ^ T[3][a >> 24]);
 }
 // gate (the CT9 resend): only when its two CRCs differ; ref / count: a result != *ref counts in *count
-__global__ __launch_bounds__(CF2_T) void crc_final2_kernel(const uint32_t* __restrict__ part, CrcFin2 F, uint32_t init,
-                                                           uint32_t* __restrict__ out, const uint32_t* __restrict__ gate,
-                                                           const uint32_t* __restrict__ ref, unsigned* __restrict__ count) {
+// (blockIdx.x = 1: the second buffer's blocks part2 into out2)
+__global__ __launch_bounds__(CF2_T) void crc_final2_kernel(const uint32_t* __restrict__ part_in, CrcFin2 F, uint32_t init,
+                                                           uint32_t* __restrict__ out_in, const uint32_t* __restrict__ gate,
+                                                           const uint32_t* __restrict__ ref, unsigned* __restrict__ count,
+                                                           const uint32_t* __restrict__ part2, uint32_t* __restrict__ out2) {
     if (gate && gate[0] == gate[1]) return;
+    const uint32_t* __restrict__ part = blockIdx.x ? part2 : part_in;
+    uint32_t* __restrict__ out = blockIdx.x ? out2 : out_in;
     __shared__ uint32_t T[1 + CF2_L][4][256];
     __shared__ uint32_t B[1 + CF2_L][32];
     __shared__ uint32_t red[CF2_T];
@@ -1810,19 +1818,21 @@ extern "C" int dc_launch_med64(const double* x, long long n, void* scratch, doub
 extern "C" long long dc_crc_parts(long long nbytes) { return (nbytes + CRC_BLK - 1) / CRC_BLK; }
 extern "C" int dc_crc_run_bytes(void) { return CRC_RUN; }
 
+// s2 / d_out2 (or null): a second buffer of the same length CRC-ed in the same two launches (parts after d_parts)
 static int launch_crc32(const uint8_t* s, long long nbytes, const uint32_t* d_tab, const uint32_t* d_x2n,
                         uint32_t* d_parts, uint32_t init, uint32_t* d_out, uint8_t* dst, const uint32_t* gate,
-                        unsigned* count, hipStream_t st) {
+                        unsigned* count, hipStream_t st, const uint8_t* s2 = nullptr, uint32_t* d_out2 = nullptr) {
     long long nblk = dc_crc_parts(nbytes);
+    uint32_t* parts2 = d_parts + nblk;
     if (nbytes > 0) {                                     // d_tab: 4 slicing tables, then kpow[256]
         long long g = nblk > 4096 ? 4096 : nblk;
         if (dst)
             hipLaunchKernelGGL(crc_blocks_kernel<true>, dim3((unsigned)g), dim3(256), 0, st, s, nbytes, d_tab,
-                               d_tab + 1024, d_x2n, d_parts, dst, gate, count);
+                               d_tab + 1024, d_x2n, d_parts, dst, gate, count, (const uint8_t*)nullptr, (uint32_t*)nullptr);
         else
-            hipLaunchKernelGGL(crc_blocks_kernel<false>, dim3((unsigned)g), dim3(256), 0, st, s, nbytes, d_tab,
+            hipLaunchKernelGGL(crc_blocks_kernel<false>, dim3((unsigned)g, s2 ? 2u : 1u), dim3(256), 0, st, s, nbytes, d_tab,
                                d_tab + 1024, d_x2n, d_parts, (uint8_t*)nullptr, (const uint32_t*)nullptr,
-                               (unsigned*)nullptr);
+                               (unsigned*)nullptr, s2, parts2);
     } else if (gate) {
         return -2;                                        // (the resend of an empty stream: nothing to copy)
     }
@@ -1837,11 +1847,12 @@ static int launch_crc32(const uint8_t* s, long long nbytes, const uint32_t* d_ta
         for (int l = 0; l < CF2_L; l++) { F2.kc[1 + l] = kp; kp = h_mult(kp, kp); }
         F2.kl = h_xpow8n((unsigned long long)(nbytes - m2 * CRC_BLK));
         F2.xn = h_xpow8n((unsigned long long)nbytes);
-        hipLaunchKernelGGL(crc_final2_kernel, dim3(1), dim3(CF2_T), 0, st, d_parts, F2, init, d_out, gate,
-                           gate ? gate : (const uint32_t*)nullptr, gate ? count + 1 : (unsigned*)nullptr);
+        hipLaunchKernelGGL(crc_final2_kernel, dim3(s2 ? 2 : 1), dim3(CF2_T), 0, st, d_parts, F2, init, d_out, gate,
+                           gate ? gate : (const uint32_t*)nullptr, gate ? count + 1 : (unsigned*)nullptr,
+                           (const uint32_t*)parts2, d_out2);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
-    if (gate) return -2;                                  // (the resend form needs the 1024-thread combine)
+    if (gate || s2) return -2;                            // (the resend and pair forms need the 1024-thread combine)
     CrcFin F;
     F.nblk = nbytes > 0 ? nblk : 0;
     const long long m = F.nblk > 0 ? F.nblk - 1 : 0;
@@ -1860,6 +1871,14 @@ static int launch_crc32(const uint8_t* s, long long nbytes, const uint32_t* d_ta
 extern "C" int dc_launch_crc32(const uint8_t* s, long long nbytes, const uint32_t* d_tab, const uint32_t* d_x2n,
                                uint32_t* d_parts, uint32_t init, uint32_t* d_out, hipStream_t st) {
     return launch_crc32(s, nbytes, d_tab, d_x2n, d_parts, init, d_out, nullptr, nullptr, nullptr, st);
+}
+// the CT9 checks after dc_encode_send_device: the sender's CRC of a and the receiver's of b (same length) in one
+// pass over both (parts: 2 dc_crc_parts(nbytes) words)
+extern "C" int dc_launch_crc32_pair(const uint8_t* a, const uint8_t* b, long long nbytes, const uint32_t* d_tab,
+                                    const uint32_t* d_x2n, uint32_t* d_parts, uint32_t* d_out_a, uint32_t* d_out_b,
+                                    hipStream_t st) {
+    if (nbytes <= 0) return -2;
+    return launch_crc32(a, nbytes, d_tab, d_x2n, d_parts, 0u, d_out_a, nullptr, nullptr, nullptr, st, b, d_out_b);
 }
 // the CT9 send: src copied to dst (the channel) and the CRC of what is sent into *d_out, one pass
 extern "C" int dc_launch_crc32_copy(const uint8_t* src, uint8_t* dst, long long nbytes, const uint32_t* d_tab,

@@ -402,7 +402,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
     uint64_t* __restrict__ toff, const uint32_t* __restrict__ tcnt, const uint32_t* __restrict__ tails,
     const uint16_t* __restrict__ psum16, unsigned ntiles, int start_bit, unsigned long long* __restrict__ total_bits,
     unsigned long long* __restrict__ total_bits2, unsigned* __restrict__ flag, uint32_t epoch,
-    unsigned* __restrict__ err, unsigned long long* __restrict__ dbg) {
+    unsigned* __restrict__ err, unsigned long long* __restrict__ dbg, uint32_t* __restrict__ mirror) {
     static_assert(ENC_K == 16 && ENC_TPB == 256, "16 consecutive floats per thread, 4 waves per tile");
 #define E3STAMP(ph) do { if (dbg && threadIdx.x == 0 && blockIdx.x < 8192) dbg[blockIdx.x * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); } while (0)
     E3STAMP(0);
@@ -613,6 +613,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
 #else
         out[W0 + i] = __builtin_bswap32(w);
 #endif
+        if (mirror) __builtin_nontemporal_store(__builtin_bswap32(w), mirror + W0 + i);
     }
     E3STAMP(4);
 #undef E3STAMP
@@ -883,7 +884,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
     uint64_t* __restrict__ st, uint64_t* __restrict__ tl, unsigned ntiles, int start_bit,
     unsigned long long* __restrict__ total_bits, unsigned long long* __restrict__ total_bits2, uint32_t epoch,
     unsigned* __restrict__ err, unsigned long long* __restrict__ dbg, int scan, const uint32_t* __restrict__ ctab,
-    uint32_t* __restrict__ cblk) {
+    uint32_t* __restrict__ cblk, uint32_t* __restrict__ mirror) {
     static_assert(ENC_K == 16 && ENC_TPB == 256, "16 consecutive floats per thread, 4 waves per tile");
     // (DC_DEBUG_STAMPS: phase stamps of the first 16384 tiles, s_memrealtime)
 #define E1STAMP(ph) do { if (dbg && threadIdx.x == 0 && tile < 16384) dbg[tile * 8 + (ph)] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -1146,6 +1147,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
         for (int u = 0; u < DC_STORE_U; u++) {
             const int i = i0 + u * ENC_TPB;
             if (i < nw) __builtin_nontemporal_store(__builtin_bswap32(wv[u]), out + W0 + i);
+            if (mirror && i < nw) __builtin_nontemporal_store(__builtin_bswap32(wv[u]), mirror + W0 + i);
         }
     }
 #else
@@ -1159,6 +1161,8 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
 #else
         out[W0 + i] = __builtin_bswap32(w);
 #endif
+        // (the CT9 send: the same words into the receiver's buffer, dc_encode_send_device)
+        if (mirror) __builtin_nontemporal_store(__builtin_bswap32(w), mirror + W0 + i);
     }
 #endif
     if constexpr (CRC) {
@@ -1582,6 +1586,11 @@ extern "C" int dc_encode_mode(void) { return g_enc_mode_last; }
 // mode 0: the default variant.  desc (dc_encode_desc_words): single pass -- tile states (u64) | tail
 // granules (u64); two/three launches -- tile offsets (u64) | tile bit counts (u32) | tile tails (u32) |
 // per-thread bit counts (u16)
+// the CT9 send (dc_encode_send_device): every launch of the next encodes also writes its stream words into this
+// buffer (the receiver's), nullptr otherwise
+static uint32_t* g_enc_mirror = nullptr;
+extern "C" void dc_set_encode_mirror(void* dst) { g_enc_mirror = (uint32_t*)dst; }
+
 extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, const Params* P,
                                 uint32_t* out, uint64_t* desc, unsigned* flag, uint32_t epoch, int start_bit, unsigned long long* total_bits, unsigned long long* total_bits2,
                                 unsigned* err, unsigned long long* dbg, int mode, const uint32_t* crc_tab, uint32_t* crc_blk,
@@ -1611,7 +1620,8 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
 #define DC_ENC_CRC(C)                                                                                \
     case C:                                                                                          \
         hipLaunchKernelGGL(HIP_KERNEL_NAME(encode_fused_kernel<C, true>), gd, bd, 0, stream, x, n, idx0, *P, out, st, \
-                           st + ntiles, ntiles, start_bit, total_bits, total_bits2, epoch, err, dbg, 1, crc_tab, crc_blk); \
+                           st + ntiles, ntiles, start_bit, total_bits, total_bits2, epoch, err, dbg, 1, crc_tab, crc_blk, \
+                           g_enc_mirror); \
         break;
                 DC_ENC_CRC(5) DC_ENC_CRC(6) DC_ENC_CRC(7) DC_ENC_CRC(11)
 #undef DC_ENC_CRC
@@ -1620,7 +1630,7 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
             dc_mark_phase(1, stream);
             return hipGetLastError() == hipSuccess ? 0 : -1;
         }
-        if (pipe && scan && flag) {
+        if (pipe && scan && flag && !g_enc_mirror) {
             // persistent workgroups drawing tiles from a ticket counter (flag word 1088: its own 256-byte
             // line past the pack's 1024 flags, zeroed at init and reset by each launch's last draw)
             const unsigned g = (unsigned)min((long long)ntiles, (long long)DC_PIPE_WAVES * cus - (DC_PIPE_STATIC ? 1 : 0));
@@ -1631,7 +1641,8 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
             return hipGetLastError() == hipSuccess ? 0 : -1;
         }
         DC_ENC_DISPATCH(encode_fused_kernel, dim3(grid + scan), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, st,
-                        st + ntiles, ntiles, start_bit, total_bits, total_bits2, epoch, err, dbg, scan, nullptr, nullptr);
+                        st + ntiles, ntiles, start_bit, total_bits, total_bits2, epoch, err, dbg, scan, nullptr, nullptr,
+                        g_enc_mirror);
         dc_mark_phase(1, stream);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
@@ -1648,7 +1659,7 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
         flag = nullptr;
     }
     DC_ENC_DISPATCH(encode_pack_kernel, dim3(ntiles), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, desc, tbits,
-                    tails, psum16, ntiles, start_bit, total_bits, total_bits2, flag, epoch, err, dbg);
+                    tails, psum16, ntiles, start_bit, total_bits, total_bits2, flag, epoch, err, dbg, g_enc_mirror);
     dc_mark_phase(3, stream);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -48,6 +48,7 @@ typedef struct {
         const float* x; long long n, idx0; Params P; uint32_t* out; int start_bit;
         unsigned long long* tot; hipStream_t st; int valid;
         uint32_t* crc;               /* dc_encode_crc_device's CRC output (recomputed after a retry) */
+        void* mirror;                /* dc_encode_send_device's receiver buffer (written again by a retry) */
     } last_enc;
     int enc_retries;                 /* encodes re-run wait-free (dc_encode_retries) */
     int enc_outstanding;             /* single-pass encodes issued since the error word was last checked clean
@@ -478,8 +479,27 @@ static int encode_on(hipStream_t st, int ct, const void* d_x, long long n, long 
     G.last_enc.out = (uint32_t*)d_out; G.last_enc.start_bit = start_bit; G.last_enc.tot = tot; G.last_enc.st = st;
     G.last_enc.valid = 1;
     G.last_enc.crc = NULL;
+    G.last_enc.mirror = NULL;
     G.enc_outstanding++;
     return DC_OK;
+}
+
+/* CT9 send: the encode, its stream words written into the receiver's buffer d_mirror as well (the channel) --
+   the sender keeps d_out for a resend; the CRCs come after (dc_crc32_pair_device) */
+int dc_encode_send_device(int ct, const void* d_x, long long n, long long idx0, int type, uint32_t mask17,
+                          void* d_out, void* d_mirror, unsigned long long* d_total_bits) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (!d_mirror || ((uintptr_t)d_mirror & 3u)) return seterr(DC_ERR_ARG, "send: the receiver's buffer must be 4-byte aligned");
+    if (G.enc_st) {
+        HIPCHK(hipEventRecord(G.ev_enc, G.st));
+        HIPCHK(hipStreamWaitEvent(G.enc_st, G.ev_enc, 0));
+    }
+    dc_set_encode_mirror(d_mirror);
+    rc = encode_on(ENC_ST, ct, d_x, n, idx0, type, mask17, 0, d_out, d_total_bits, NULL);
+    dc_set_encode_mirror(NULL);
+    if (!rc) G.last_enc.mirror = d_mirror;
+    return rc;
 }
 
 /* bits an encode of these n floats would produce (no stream written); synchronous */
@@ -525,10 +545,12 @@ static int encode_retry(hipStream_t st) {
         G.enc_epoch = 1;
     }
     unsigned long long* tot = G.last_enc.tot;
-    if (dc_launch_encode(G.last_enc.x, G.last_enc.n, G.last_enc.idx0, &G.last_enc.P, G.last_enc.out, G.enc_desc,
-                         G.d_enc_flag, G.enc_epoch, G.last_enc.start_bit, tot, tot != G.d_total ? G.d_total : NULL,
-                         G.d_enc_err, NULL, 3, NULL, NULL, st))
-        return seterr(DC_ERR_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
+    dc_set_encode_mirror(G.last_enc.mirror);
+    const int lrc = dc_launch_encode(G.last_enc.x, G.last_enc.n, G.last_enc.idx0, &G.last_enc.P, G.last_enc.out,
+                                     G.enc_desc, G.d_enc_flag, G.enc_epoch, G.last_enc.start_bit, tot,
+                                     tot != G.d_total ? G.d_total : NULL, G.d_enc_err, NULL, 3, NULL, NULL, st);
+    dc_set_encode_mirror(NULL);
+    if (lrc) return seterr(DC_ERR_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
     G.enc_retries++;
     G.enc_outstanding = 1;
     return DC_OK;
@@ -1401,6 +1423,29 @@ int dc_crc_resend_device(const uint32_t* d_crc2, const void* d_src, void* d_dst,
     if (copy && (((uintptr_t)d_src | (uintptr_t)d_dst) & 15u)) return seterr(DC_ERR_ARG, "streams must be 16-byte aligned");
     if (dc_launch_crc_resend(d_crc2, (const uint8_t*)d_src, (uint8_t*)d_dst, nbytes, copy, d_count, G.st))
         return seterr(DC_ERR_HIP, "resend launch failed");
+    return DC_OK;
+}
+
+/* CT9 checks after dc_encode_send_device: the sender's CRC of a and the receiver's CRC of b (nbytes each, device
+   results) in one pass over both */
+int dc_crc32_pair_device(const void* d_a, const void* d_b, long long nbytes, uint32_t* d_crc_a, uint32_t* d_crc_b) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (nbytes < 0 || nbytes > 0x7FFFFF00ll - 64 || (((uintptr_t)d_a | (uintptr_t)d_b) & 15u))
+        return seterr(DC_ERR_ARG, "crc pair: 16-byte aligned streams below 2 GiB");
+    if (nbytes == 0) {
+        if ((rc = crc_into(d_a, 0, d_crc_a))) return rc;
+        return crc_into(d_b, 0, d_crc_b);
+    }
+    const long long parts = 2 * dc_crc_parts(nbytes) + 1;
+    if (parts > G.crcparts_cap) {
+        if (G.d_crcparts) HIPCHK(hipFree(G.d_crcparts));
+        HIPCHK(hipMalloc((void**)&G.d_crcparts, parts * 4 + 1024));
+        G.crcparts_cap = parts;
+    }
+    if (dc_launch_crc32_pair((const uint8_t*)d_a, (const uint8_t*)d_b, nbytes, G.d_crctab, G.d_x2n, G.d_crcparts,
+                             d_crc_a, d_crc_b, G.st))
+        return seterr(DC_ERR_HIP, "crc pair launch failed");
     return DC_OK;
 }
 

@@ -138,6 +138,10 @@ int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev_nbits, uns
                       int dense, dc_hip_stream st);
 int dc_decode3_last_fused(void);
 int dc_maps_seg(int seg);
+void dc_set_encode_mirror(void* dst);
+int dc_launch_crc32_pair(const uint8_t* a, const uint8_t* b, long long nbytes, const uint32_t* d_tab,
+                         const uint32_t* d_x2n, uint32_t* d_parts, uint32_t* d_out_a, uint32_t* d_out_b,
+                         dc_hip_stream st);
 void dc_decode3_clear_fused(void);
 /* the chunks of the last fused decode of a stream of this capacity: the next launch's segment length */
 void dc_decode3_size_hint(long long max_chunks, long long nchunks);

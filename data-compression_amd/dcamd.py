@@ -39,7 +39,7 @@ EXT_SYMBOLS = [
     "dc_get_abs_error_bound", "dc_stream_capacity", "dc_encode_device", "dc_encode_result",
     "dc_decode_device", "dc_decode_finish", "dc_to_small_device", "dc_med_device", "dc_crc32_device",
     "dc_decode_chunk_bits_value", "dc_ct1_encode_device", "dc_ct1_decode_device", "dc_encode_bits_device",
-    "dc_crc32_device_async", "dc_crc32_copy_device", "dc_encode_crc_device", "dc_crc32_stream_device", "dc_crc_resend_crc_device",
+    "dc_crc32_device_async", "dc_crc32_copy_device", "dc_encode_send_device", "dc_crc32_pair_device", "dc_encode_crc_device", "dc_crc32_stream_device", "dc_crc_resend_crc_device",
     "dc_hash_device", "dc_copy_rate_device", "dc_flip_bits_device", "dc_decode_shard_device", "dc_decode_shard_fix",
     "dc_halo_encode_device", "dc_halo_decode_device",
     "dc64_stream_capacity", "dc64_encode_device", "dc64_encode_result", "dc64_decode_device", "dc64_decode_finish",
@@ -384,6 +384,19 @@ class Lib:
         """dc_crc32_copy_device: the CT9 send -- src copied to dst with the CRC-32 of the bytes sent (device)."""
         self.check(self.L.dc_crc32_copy_device(C.c_void_p(src_ptr), C.c_void_p(dst_ptr), C.c_longlong(nbytes),
                                                C.c_void_p(crc_ptr)), "dc_crc32_copy_device")
+
+    def encode_send_device(self, ct, x_ptr, n, out_ptr, mirror_ptr, total_ptr=None, idx0=0, type_=0, mask17=0):
+        """dc_encode_send_device: the encode (start bit 0) with its stream also written into the receiver's
+        buffer mirror_ptr -- the CT9 send without a copy pass."""
+        self.check(self.L.dc_encode_send_device(C.c_int(ct), C.c_void_p(x_ptr), C.c_longlong(n), C.c_longlong(idx0),
+                                                C.c_int(type_), C.c_uint32(mask17), C.c_void_p(out_ptr),
+                                                C.c_void_p(mirror_ptr), C.c_void_p(total_ptr)),
+                   "dc_encode_send_device")
+
+    def crc32_pair_device(self, a_ptr, b_ptr, nbytes, crc_a_ptr, crc_b_ptr):
+        """dc_crc32_pair_device: the CRC-32 of two equally long device buffers in one pass (device results)."""
+        self.check(self.L.dc_crc32_pair_device(C.c_void_p(a_ptr), C.c_void_p(b_ptr), C.c_longlong(nbytes),
+                                               C.c_void_p(crc_a_ptr), C.c_void_p(crc_b_ptr)), "dc_crc32_pair_device")
 
     def crc32_stream_device(self, s_ptr, nbytes, crc_ptr):
         self.check(self.L.dc_crc32_stream_device(s_ptr, nbytes, crc_ptr), "dc_crc32_stream_device")

@@ -178,6 +178,14 @@ int dc_copy_rate_device(const void* d_src, void* d_dst, long long bytes, int rep
 int dc_encode_crc_device(int ct, const void* d_x, long long n, long long idx0, int type, uint32_t mask17, void* d_out,
                          unsigned long long* d_total_bits, uint32_t* d_crc);
 int dc_crc32_stream_device(const void* d_s, long long nbytes, uint32_t* d_crc);
+/* CT9 send without a copy pass (replaces the reference's MPI send of the compressed buffer,
+ * impl/pingpong.c:260-289): the encode of dc_encode_device (start bit 0) with its stream words also written
+ * into the receiver's buffer d_mirror (4-byte aligned, the stream's capacity); the sender keeps d_out for a
+ * resend.  Then dc_crc32_pair_device gives the sender's CRC of d_out and the receiver's of d_mirror (after any
+ * channel damage) in one pass over both (16-byte aligned buffers, device results). */
+int dc_encode_send_device(int ct, const void* d_x, long long n, long long idx0, int type, uint32_t mask17,
+                          void* d_out, void* d_mirror, unsigned long long* d_total_bits);
+int dc_crc32_pair_device(const void* d_a, const void* d_b, long long nbytes, uint32_t* d_crc_a, uint32_t* d_crc_b);
 /* CT9 send: d_src copied to d_dst (the channel) and the zlib CRC-32 of the bytes sent into *d_crc (device), in one
    pass (16-byte aligned, < 2 GiB) */
 int dc_crc32_copy_device(const void* d_src, void* d_dst, long long nbytes, uint32_t* d_crc);

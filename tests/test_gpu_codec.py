@@ -683,6 +683,57 @@ def test_crc32_copy_device(dc, nbytes):
     assert bool((dst[nbytes:] == 0x5A).all())
 
 
+@pytest.mark.parametrize("nbytes", [1, 100, 32768, 32768 * 5 + 17, (1 << 22) + 3])
+def test_crc32_pair_device(dc, nbytes):
+    """The CT9 checks in one pass (dc_crc32_pair_device): both CRCs zlib's of their own buffer, the buffers
+    untouched -- one byte apart, and identical."""
+    import zlib
+    import torch
+    rng = np.random.RandomState(nbytes & 0xFFFF)
+    h = rng.randint(0, 256, size=nbytes + 64, dtype=np.uint8)
+    a = torch.from_numpy(h).cuda()
+    b = a.clone()
+    b[nbytes // 2] ^= 0x10
+    c = torch.zeros(4, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    dc.crc32_pair_device(a.data_ptr(), b.data_ptr(), nbytes, c.data_ptr(), c.data_ptr() + 4)
+    dc.synchronize()
+    hb = h.copy()
+    hb[nbytes // 2] ^= 0x10
+    assert (int(c[0].item()) & 0xFFFFFFFF) == zlib.crc32(h[:nbytes].tobytes())
+    assert (int(c[1].item()) & 0xFFFFFFFF) == zlib.crc32(hb[:nbytes].tobytes())
+    dc.crc32_pair_device(a.data_ptr(), a.data_ptr(), nbytes, c.data_ptr() + 8, c.data_ptr() + 12)
+    dc.synchronize()
+    assert int(c[2].item()) == int(c[3].item()) == int(c[0].item())
+
+
+@pytest.mark.parametrize("ct", [5, 6, 7, 11])
+@pytest.mark.parametrize("log2n", [12, 20, 24])
+def test_encode_send_device(dc, oracle, ct, log2n):
+    """The CT9 send without a copy pass (dc_encode_send_device): the receiver's buffer holds exactly the
+    sender's stream (the oracle's bytes), nothing past it written."""
+    import torch
+    n = 1 << log2n
+    dc.set_bound(1e-3)
+    _, xs = oracle.to_small(oracle.gen_u10(n))
+    t, m17 = oracle.type_mask(xs)
+    cap = dc.stream_capacity(n)
+    x = torch.from_numpy(xs).cuda()
+    st = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    rcv = torch.full((cap,), 0x5A, dtype=torch.uint8, device="cuda")
+    nbits = torch.zeros(1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    dc.encode_send_device(ct, x.data_ptr(), n, st.data_ptr(), rcv.data_ptr(), nbits.data_ptr(), type_=t, mask17=m17)
+    nb = (dc.encode_result() + 7) // 8
+    torch.cuda.synchronize()
+    s, onb, _ = oracle.compress(ct, xs, 1e-3, t, m17)
+    assert nb == onb
+    assert np.array_equal(st[:nb].cpu().numpy(), s)
+    assert torch.equal(rcv[:nb], st[:nb])
+    w = (nb + 3) // 4 * 4                                # (the last word's padding bytes are the stream's zeros)
+    assert bool((rcv[w:] == 0x5A).all())
+
+
 @pytest.mark.parametrize("nbytes", [3 * 32768 * 32 + 5, (1 << 22) + 1])
 def test_crc_resend_crc_device_large(dc, nbytes):
     """The resend at sizes of many 32 KiB blocks with a ragged tail: replaced once, its CRC zlib's, gated after."""
