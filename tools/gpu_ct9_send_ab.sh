@@ -12,3 +12,5 @@ for i in 1 2; do
     echo "$m run $i: $(grep -E '^value' gpurun_out/ct9s_${m}_$i.txt)"; grep -E '^kernels_ms' gpurun_out/ct9s_${m}_$i.txt
   done
 done
+timeout -k 10 300 python3 -u bench.py --no-extra --no-cpu > gpurun_out/ct9s_main.json 2> gpurun_out/ct9s_main.err || { tail -20 gpurun_out/ct9s_main.err; exit 1; }
+python3 tools/bench_summary.py gpurun_out/ct9s_main.json > gpurun_out/ct9s_main.txt; echo "headline: $(grep -E '^value' gpurun_out/ct9s_main.txt)"; grep -E '^kernels_ms' gpurun_out/ct9s_main.txt
