@@ -1825,7 +1825,9 @@ static int launch_crc32(const uint8_t* s, long long nbytes, const uint32_t* d_ta
     long long nblk = dc_crc_parts(nbytes);
     uint32_t* parts2 = d_parts + nblk;
     if (nbytes > 0) {                                     // d_tab: 4 slicing tables, then kpow[256]
-        long long g = nblk > 4096 ? 4096 : nblk;
+        static long long gcap = -1;                       // (A/B: DC_CRC_GRID caps the workgroups; 0 = one per block)
+        if (gcap < 0) { const char* e = getenv("DC_CRC_GRID"); gcap = e ? atoll(e) : 4096; }
+        long long g = (gcap > 0 && nblk > gcap) ? gcap : nblk;
         if (dst)
             hipLaunchKernelGGL(crc_blocks_kernel<true>, dim3((unsigned)g), dim3(256), 0, st, s, nbytes, d_tab,
                                d_tab + 1024, d_x2n, d_parts, dst, gate, count, (const uint8_t*)nullptr, (uint32_t*)nullptr);
