@@ -299,3 +299,34 @@ def test_slow_sync_streams(v3, oracle, ct, kind, bound, lg):
             assert v3.L.dc_last_decode_was_v3()
     finally:
         v3.set_bound(1e-3)
+
+
+@pytest.mark.parametrize("ct", [5, 7])
+def test_slow_sync_large_seg20(dc, oracle, ct):
+    """A noisy ramp large enough for 20-chunk parse segments (2^25 floats: > 2.5 M chunks of capacity) declines
+    parse3 and is parsed by maps, which keep 16-chunk parse jobs (dc_maps_seg) -- decode3 after them uses the
+    same; the values equal the grammar decoder's."""
+    import torch
+    dc.set_bound(1e-3)
+    n = 1 << 25
+    xs = _slow_sync("ramp", n)
+    t, m17 = oracle.type_mask(xs)
+    s, nb, _ = oracle.compress(ct, xs, 1e-3, t, m17)
+    ref, _ = oracle.decompress(ct, s, n, 1e-3, t, m17)
+    cap = dc.stream_capacity(n)
+    d_s = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    d_s[:nb] = torch.from_numpy(s).cuda()
+    out = torch.empty(n, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    for force in (0, 1):                              # as parse3 leaves it, then parsed by maps for certain
+        old = dc.L.dc_set_decode3_maps(force)
+        try:
+            out.fill_(-1.0)
+            dc.decode_device(ct, d_s.data_ptr(), nb, n, out.data_ptr(), type_=t, mask17=m17, max_bytes=cap)
+            dc.decode_finish()
+            assert dc.L.dc_last_decode_was_v3()
+            if force:
+                assert dc.L.dc_last_decode_used_maps()
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+        finally:
+            dc.L.dc_set_decode3_maps(old)
