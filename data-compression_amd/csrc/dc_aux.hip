@@ -778,7 +778,10 @@ __global__ __launch_bounds__(MXC_T) void med_compose_kernel(const T* __restrict_
     typedef typename FP::D D;
     typedef typename FP::U U;
     constexpr int R = MedRing<T, W>::R;
-    constexpr int CPT = R >= 4096 ? 2 : 1;                  // chunks per thread in a block
+#ifndef DC_MED_CPT
+#define DC_MED_CPT 2
+#endif
+    constexpr int CPT = R >= 4096 ? DC_MED_CPT : 1;         // chunks per thread in a block
     constexpr int BLK = MXC_T * CPT;
     __shared__ T buf[MC];                                   // (a chunk added by one lane)
     __shared__ int r_lo[R];                                 // ring slot: the chunk's first window binade
