@@ -46,23 +46,32 @@ __device__ __forceinline__ uint32_t mp_word(const uint8_t* __restrict__ s, long 
 // through it.  No workgroup barrier: with four waves sharing a group and four barriers per group, waves waited
 // 72 % of their cycles (SQ counters, sine @1e-5 at 2^24: 463 us) and the table lookups of the lengths conflicted
 // on LDS banks.
-constexpr int MP_GRID = 8192;
+#ifndef DC_MP_WPG
+#define DC_MP_WPG 1                      // waves per workgroup (independent: each its own groups and LDS)
+#endif
+constexpr int MP_GRID = DC_MP_WPG > 1 ? 12288 : 8192;   // waves (one-wave workgroups: at most 8 per SIMD)
 constexpr int MP_GWORDS = MP_G * 8 + 2;                  // a group's stream words with the last chunk's lookahead
 template <int CT>
-__global__ __launch_bounds__(64) void maps_group_kernel(const uint8_t* __restrict__ s, Params P,
+__global__ __launch_bounds__(64 * DC_MP_WPG) void maps_group_kernel(const uint8_t* __restrict__ s, Params P,
                                                         const unsigned long long* dev_nbits, unsigned long long host_nbits,
                                                         uint8_t* __restrict__ gmap, uint4* __restrict__ gtab, long long ngr,
                                                         long long num, long long max_chunks, unsigned* __restrict__ err) {
-    __shared__ uint32_t gw[MP_GWORDS + 2];
-    __shared__ uint16_t nx[2][256];                              // the next token's start from every bit
-    __shared__ uint8_t gx[MP_G][32], gc[MP_G][32];
+    __shared__ uint32_t gwa[DC_MP_WPG][MP_GWORDS + 2];
+    __shared__ uint16_t nxa[DC_MP_WPG][2][256];                 // the next token's start from every bit
+    __shared__ uint8_t gxa[DC_MP_WPG][MP_G][32], gca[DC_MP_WPG][MP_G][32];
+    const int wv = threadIdx.x >> 6;
+    uint32_t* gw = gwa[wv];
+    uint16_t (*nx)[256] = nxa[wv];
+    uint8_t (*gx)[32] = gxa[wv];
+    uint8_t (*gc)[32] = gca[wv];
     const unsigned long long nbits = dev_nbits ? *dev_nbits : host_nbits;
     const long long nch = (long long)((nbits + 255) >> 8), nbytes = (long long)((nbits + 7) >> 3);
-    const int lane = threadIdx.x, h = lane >> 5, e = lane & 31;
+    const int lane = threadIdx.x & 63, h = lane >> 5, e = lane & 31;
     // a runs-mode stream (decode3 would take it for zero runs, which only parse3 checks) or one longer than
     // the buffers: declined to the chunk-map decoder, as parse3 declines it (status 512 | 1024)
-    if (blockIdx.x == 0 && lane == 0 && (nch > max_chunks || runs_mode(CT, nbits, num))) atomicOr(err, 512u | 1024u);
-    long long gi = blockIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (nch > max_chunks || runs_mode(CT, nbits, num))) atomicOr(err, 512u | 1024u);
+    const long long gstride = (long long)gridDim.x * DC_MP_WPG;
+    long long gi = (long long)blockIdx.x * DC_MP_WPG + wv;
     uint32_t wa = 0u, wb = 0u;                                   // words lane and 64 + lane of the group
     {
         const long long w0 = gi * MP_G * 8;
@@ -71,7 +80,7 @@ __global__ __launch_bounds__(64) void maps_group_kernel(const uint8_t* __restric
             if (lane < MP_GWORDS - 64) wb = mp_word(s, nbytes, w0 + 64 + lane);
         }
     }
-    for (; gi < ngr; gi += gridDim.x) {
+    for (; gi < ngr; gi += gstride) {
         const long long g0 = gi * MP_G;
         if (g0 >= nch) {                                         // (past the stream's end: the identity)
             if (h == 0) gmap[gi * 32 + e] = (uint8_t)e;
@@ -81,7 +90,7 @@ __global__ __launch_bounds__(64) void maps_group_kernel(const uint8_t* __restric
         gw[lane] = wa;
         if (lane < MP_GWORDS - 64) gw[64 + lane] = wb;
         {
-            const long long gn = gi + gridDim.x, w0 = gn * MP_G * 8;
+            const long long gn = gi + gstride, w0 = gn * MP_G * 8;
             wa = 0u; wb = 0u;
             if (gn < ngr && gn * MP_G < nch) {
                 wa = mp_word(s, nbytes, w0 + lane);
@@ -293,11 +302,11 @@ extern "C" int dc_launch_maps_parse(const uint8_t* s, const unsigned long long* 
     // stream's end have identity maps and are never read)
     const long long hc[2] = {ngr, nb};
     if (hipMemcpyAsync(cnt, hc, sizeof hc, hipMemcpyHostToDevice, st) != hipSuccess) return -1;
-    const dim3 gg((unsigned)min(ngr, (long long)MP_GRID)), gb((unsigned)nb);
+    const dim3 gg((unsigned)((min(ngr, (long long)MP_GRID) + DC_MP_WPG - 1) / DC_MP_WPG)), gb((unsigned)nb);
     switch (P->ct) {
 #define DC_MAPS_CASE(C)                                                                                          \
     case C:                                                                                                      \
-        hipLaunchKernelGGL(maps_group_kernel<C>, gg, dim3(64), 0, st, s, *P, dev_nbits, host_nbits, gmap, gtab, \
+        hipLaunchKernelGGL(maps_group_kernel<C>, gg, dim3(64 * DC_MP_WPG), 0, st, s, *P, dev_nbits, host_nbits, gmap, gtab, \
                            ngr, num, D3->max_chunks, D3->err);                                                      \
         break;
         DC_MAPS_CASE(5) DC_MAPS_CASE(6) DC_MAPS_CASE(7) DC_MAPS_CASE(11)
