@@ -542,21 +542,27 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
         seed = [1]
         acks = []
         ack_buf = torch.zeros((max(steps, warmup) + 1, 2), dtype=torch.int32, pin_memory=True)
-        # DC_CT9_MODE: "send" (default) the encoder writes its stream into the receiver's buffer as well (the
-        # channel, dc_encode_send_device) and one pass CRCs both copies after the damage (dc_crc32_pair_device);
-        # "copy" the send as a copy pass that CRCs what it sends (dc_crc32_copy_device) and a receiver pass;
-        # "fused" (or DC_CT9_FUSED=1) the sender's CRC inside the encoder's tiles (slower)
+        # DC_CT9_MODE: "copy" (default) the send as a copy pass that CRCs what it sends (dc_crc32_copy_device) and
+        # a receiver pass; "send" the encoder writes its stream into the receiver's buffer as well (the channel,
+        # dc_encode_send_device) and one pass CRCs both copies after the damage (dc_crc32_pair_device);
+        # "fused" (or DC_CT9_FUSED=1) the sender's CRC inside the encoder's tiles (slower).
+        # Each phase carries its algorithmic bytes in stream sizes: a copy pass reads and writes the stream (2),
+        # a CRC pass reads it (1), the pair pass reads both copies (2), flips and launch gaps move nothing (0)
         ct9_mode = "fused" if os.environ.get("DC_CT9_FUSED", "0") == "1" else os.environ.get("DC_CT9_MODE", "copy")
         CT9_PHASES = {
-            "fused": ["crcf_final_kernel (sender CRC: combine of the encoder's block CRCs)", "channel copy",
-                      "flip_bits_kernel", "crcf_blocks + crcf_final (receiver CRC, damaged copy)",
-                      "crc_blocks<copy> + crc_final2 (resend copy with its CRC + check)"],
-            "copy": ["(encode call beyond its kernel)", "crc_blocks<copy> + crc_final2 (send: channel copy + sender CRC)",
-                     "flip_bits_kernel", "crc_blocks + crc_final2 (receiver CRC, damaged copy)",
-                     "crc_blocks<copy> + crc_final2 (resend copy with its CRC + check)"],
-            "send": ["(encode call beyond its kernel: the encoder also writes the receiver's copy)", "(no send pass)",
-                     "flip_bits_kernel", "crc_blocks x2 + crc_final2 x2 (sender's and receiver's CRC, one pass)",
-                     "crc_blocks<copy> + crc_final2 (resend copy with its CRC + check)"]}[ct9_mode]
+            "fused": [("crcf_final_kernel (sender CRC: combine of the encoder's block CRCs)", 0), ("channel copy", 2),
+                      ("flip_bits_kernel", 0), ("crcf_blocks + crcf_final (receiver CRC, damaged copy)", 1),
+                      ("crc_blocks<copy> + crc_final2 (resend copy with its CRC + check)", 2)],
+            "copy": [("(encode call beyond its kernel)", 0),
+                     ("crc_blocks<copy> + crc_final2 (send: channel copy + sender CRC)", 2),
+                     ("flip_bits_kernel", 0), ("crc_blocks + crc_final2 (receiver CRC, damaged copy)", 1),
+                     ("crc_blocks<copy> + crc_final2 (resend copy with its CRC + check)", 2)],
+            "send": [("(encode call beyond its kernel: the encoder also writes the receiver's copy)", 0),
+                     ("(no send pass)", 0), ("flip_bits_kernel", 0),
+                     ("crc_blocks x2 + crc_final2 x2 (sender's and receiver's CRC, one pass)", 2),
+                     ("crc_blocks<copy> + crc_final2 (resend copy with its CRC + check)", 2)]}[ct9_mode]
+        CT9_STREAMS = dict(CT9_PHASES)
+        CT9_PHASES = [nm for nm, _ in CT9_PHASES]
 
         # Default: the send copies the stream into the receiver's buffer and CRCs the bytes it sends in one pass
         # (dc_crc32_copy_device), the receiver CRCs what arrived (dc_crc32_device_async), the resend copies and
@@ -618,7 +624,7 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
         L.synchronize()
         d_cnt.zero_()
         acks.clear()
-        ct9 = {"d_cnt": d_cnt, "acks": acks, "phases": CT9_PHASES, "nflip": nflip}
+        ct9 = {"d_cnt": d_cnt, "acks": acks, "phases": CT9_PHASES, "streams": CT9_STREAMS, "nflip": nflip}
 
     # ---- timed region: barrier + sync on both sides, max over ranks, nothing but the steps (an event
     # record between launches costs a few microseconds of dispatch gap)
@@ -723,7 +729,7 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
            "slow_path_timed": slow[0], "v3": bool(L.L.dc_last_decode_launched_v3()),
            "runs": bool(L.L.dc_last_decode_launched_runs()), "fused": bool(L.L.dc_decode3_last_fused()),
            "fused_seg": int(L.L.dc_fused3_last_seg()),
-           "enc_mode": int(L.L.dc_encode_mode()), "ct9": {k: v for k, v in ct9.items() if k in ("phase_ms", "acks_ok", "nflip")}}
+           "enc_mode": int(L.L.dc_encode_mode()), "ct9": {k: v for k, v in ct9.items() if k in ("phase_ms", "acks_ok", "nflip", "streams")}}
 
     if pipelined and ber <= 0:
         # the same K steps pipelined (encode k+1 || decode k, two stream buffers), reported beside value
@@ -851,14 +857,10 @@ def kernel_table(ct, n, nbytes, kavg, v3=True, enc_mode=1, runs=False, fused=Fal
     return kernels
 
 
-def ct9_bytes(name, nbytes):
-    """Algorithmic bytes of a CT9 phase: a copy pass reads and writes the stream, a CRC pass reads it (the pair
-    pass both copies), the flips and the launch gaps nothing."""
-    if "damaged copy" in name:
-        return float(nbytes)
-    if "one pass" in name or "copy" in name:
-        return 2.0 * nbytes
-    return 0.0
+def ct9_bytes(name, nbytes, streams):
+    """Algorithmic bytes of a CT9 phase: its stream count (CT9_PHASES: a copy pass 2, a CRC pass 1, the pair pass
+    2, the flips and the launch gaps 0) times the stream's bytes."""
+    return float(streams.get(name, 0)) * nbytes
 
 
 def line_for(C, W, R, steps):
@@ -869,7 +871,7 @@ def line_for(C, W, R, steps):
     kernels = kernel_table(W["ct"], n, nbytes, R["kavg"], R["v3"], R.get("enc_mode", 1), R.get("runs", False),
                            R.get("fused", False))
     for nm, ms_ in R.get("ct9", {}).get("phase_ms", {}).items():   # CT9: every launch of the step
-        kernels[nm] = (ms_, ct9_bytes(nm, nbytes))
+        kernels[nm] = (ms_, ct9_bytes(nm, nbytes, R["ct9"].get("streams", {})))
     dname = max(kernels, key=lambda k: kernels[k][0])
     dms, dbytes = kernels[dname]
     ach = dbytes / (dms * 1e-3) / 1e9 if dms > 0 else 0.0
@@ -929,7 +931,7 @@ def main():
     kernels = kernel_table(ct, n, nbytes, R["kavg"], R["v3"], R.get("enc_mode", 1), R.get("runs", False),
                            R.get("fused", False))
     for nm, ms_ in R.get("ct9", {}).get("phase_ms", {}).items():   # (as line_for: the CT9 launches too)
-        kernels[nm] = (ms_, ct9_bytes(nm, nbytes))
+        kernels[nm] = (ms_, ct9_bytes(nm, nbytes, R["ct9"].get("streams", {})))
     dname = main_line["dominant"]["kernel"]
     achievable, copy_how = copy_bandwidth(C.L, C.dev, n)
     traffic, traffic_src, ktraffic = None, None, None

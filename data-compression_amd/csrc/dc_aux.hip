@@ -1173,13 +1173,18 @@ static int launch_med(const T* x, long long n, T s_init, void* scratch, T* d_mea
     const long long nch = (n + MC - 1) / MC;
     const MedScratch<T> M = med_scratch<T>(scratch, nch);
     const unsigned tg = med_trans_grid(nch);
-    if (!wide) {
+    // wide: 0 the narrow window; 1 the wide one after the narrow compose raised the flag (the chunk sums, max
+    // and binade estimates of that call are in the scratch); 2 the wide one on a fresh array (DC_MED_WIDE=1:
+    // the chunk sums and the estimate scan run first, nothing is taken from an earlier call's scratch)
+    if (wide != 1) {
         hipLaunchKernelGGL(med_chunk_sum_kernel<T>, dim3((unsigned)nch), dim3(MC_T), 0, st, x, n, M);
         hipLaunchKernelGGL(med_chunk_scan_kernel<T>, dim3(1), dim3(1024), 0, st, M, nch, s_init);
+    }
+    if (!wide) {
         hipLaunchKernelGGL((med_chunk_trans_kernel<T, MWN>), dim3(tg), dim3(256), 0, st, x, n, M, 0);
         hipLaunchKernelGGL((med_compose_kernel<T, MWN>), dim3(1), dim3(MXC_T), 0, st, x, n, s_init, M, d_mean, d_type,
                            d_sum, d_max, 0);
-    } else {                                                // (after the narrow compose raised the flag)
+    } else {
         hipLaunchKernelGGL((med_chunk_trans_kernel<T, MW>), dim3(tg), dim3(256), 0, st, x, n, M, 0);
         hipLaunchKernelGGL((med_compose_kernel<T, MW>), dim3(1), dim3(MXC_T), 0, st, x, n, s_init, M, d_mean, d_type,
                            d_sum, d_max, 0);
@@ -1787,9 +1792,10 @@ extern "C" int dc_launch_med(const float* x, long long n, float s_init, void* sc
                              float* d_sum, float* d_max, hipStream_t st) {
     return launch_med<float>(x, n, s_init, scratch, d_mean, d_type, d_sum, d_max, 0, st);
 }
+// fresh = 1: the array was not just run through dc_launch_med (its chunk sums are not in the scratch)
 extern "C" int dc_launch_med_wide(const float* x, long long n, float s_init, void* scratch, float* d_mean, int* d_type,
-                                  float* d_sum, float* d_max, hipStream_t st) {
-    return launch_med<float>(x, n, s_init, scratch, d_mean, d_type, d_sum, d_max, 1, st);
+                                  float* d_sum, float* d_max, int fresh, hipStream_t st) {
+    return launch_med<float>(x, n, s_init, scratch, d_mean, d_type, d_sum, d_max, fresh ? 2 : 1, st);
 }
 // a rank's shard (med_shard_kernel): trans = 0 its double sum and max; trans = 1 its whole-shard transducer,
 // the chunk windows opened from s_est (the estimated running sum the shard starts at).  The 21-word record

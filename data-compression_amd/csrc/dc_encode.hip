@@ -1570,6 +1570,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_PIPE_WAVES) void encode_pipe_kernel(
 
 static long long desc_words_multi(long long nt);
 static int g_enc_mode_last = 0;
+static int g_enc_crc_fused = 0;                 // 1: the last launch computed the fused CRC pieces
 // encoder variant: 1 = single pass (default), 2 = count + pack (the pack's workgroup 0 scans the tile
 // counts, the other tiles wait for its flag), 3 = count + scan launch + pack (no wait anywhere: the
 // fallback after a single-pass timeout).  DC_ENC_PASSES=2|3 selects the others.
@@ -1582,6 +1583,7 @@ static int enc_mode_default(void) {
     return m;
 }
 extern "C" int dc_encode_mode(void) { return g_enc_mode_last; }
+extern "C" int dc_encode_crc_fused_last(void) { return g_enc_crc_fused; }
 
 // mode 0: the default variant.  desc (dc_encode_desc_words): single pass -- tile states (u64) | tail
 // granules (u64); two/three launches -- tile offsets (u64) | tile bit counts (u32) | tile tails (u32) |
@@ -1598,6 +1600,7 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
     if (n <= 0) return 0;
     if (mode == 0) mode = enc_mode_default();
     g_enc_mode_last = mode;
+    g_enc_crc_fused = 0;
     const unsigned ntiles = (unsigned)((n + ENC_TILE - 1) / ENC_TILE);
     if (mode == 1) {
         const int grid = (int)ntiles;
@@ -1613,8 +1616,11 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
             if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
                 cus = 256;
         }
-        if (crc_blk) {                       // (the CT9 sender: the stream's CRC pieces while the words are stored)
-            if (!scan || start_bit) return -2;
+        g_enc_crc_fused = 0;
+        // (the CT9 sender: the stream's CRC pieces while the words are stored; the chained look-back variant
+        // has no fused CRC: it encodes plainly and the host takes a CRC pass, dc_encode_crc_fused_last)
+        if (crc_blk && scan && !start_bit) {
+            g_enc_crc_fused = 1;
             const dim3 gd(grid + 1), bd(ENC_TPB);
             switch (P->ct) {
 #define DC_ENC_CRC(C)                                                                                \

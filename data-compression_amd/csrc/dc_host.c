@@ -423,7 +423,7 @@ int dc_encode_crc_device(int ct, const void* d_x, long long n, long long idx0, i
     if (!blk) return seterr(DC_ERR_HIP, "crc block allocation failed");
     if ((rc = encode_on(ENC_ST, ct, d_x, n, idx0, type, mask17, 0, d_out, d_total_bits, n > 0 ? blk : NULL))) return rc;
     G.last_enc.crc = d_crc;
-    if (n > 0 && dc_encode_mode() != 1) {        /* (a multi-pass variant, DC_ENC_PASSES: a pass of its own) */
+    if (n > 0 && !dc_encode_crc_fused_last()) {  /* (a multi-pass or chained look-back variant: a pass of its own) */
         unsigned long long bits = 0;
         HIPCHK(hipMemcpyAsync(&bits, d_total_bits, 8, hipMemcpyDeviceToHost, ENC_ST));
         HIPCHK(hipStreamSynchronize(ENC_ST));
@@ -536,6 +536,17 @@ int dc_encode_bits_device(int ct, const void* d_x, long long n, long long idx0, 
     return DC_OK;
 }
 
+/* after an encode error that is reported, not repaired: the fused CRC's slot-0 block accumulators may hold
+   pieces of tiles past the bits the combine read (it zeroes only those), so clear the whole slot; the
+   receiver's buffer and CRC of that encode are forgotten (a later retry must not write into them) */
+static int enc_forget_failed(hipStream_t st) {
+    if (G.crcf_blk[0] && G.crcf_cap[0] > 0) HIPCHK(hipMemsetAsync(G.crcf_blk[0], 0, (size_t)G.crcf_cap[0] * 4, st));
+    G.last_enc.mirror = NULL;
+    G.last_enc.crc = NULL;
+    G.last_enc.valid = 0;
+    return DC_OK;
+}
+
 /* re-run the last encode with no wait between workgroups (count, scan launch, pack) */
 static int encode_retry(hipStream_t st) {
     HIPCHK(hipMemsetAsync(G.d_enc_err, 0, 4, st));
@@ -581,6 +592,7 @@ int dc_encode_result(unsigned long long* total_bits) {
         /* the error word is OR-ed over every encode since it was last checked: the one that timed out may be
            an earlier one, whose stream a later launch has already consumed -- re-running the last encode
            would not repair it, so report it and leave the word set (dc_encode_clear_status clears it) */
+        if ((rc = enc_forget_failed(st))) return rc;
         return seterr(DC_ERR_HIP, "a look-back wait timed out in one of the %d encodes issued since the encoder's "
                                   "error word was last checked (err=%u): their streams may lack tiles",
                       G.enc_outstanding, err);
@@ -605,6 +617,7 @@ int dc_encode_result(unsigned long long* total_bits) {
     if (err) {
         HIPCHK(hipMemsetAsync(G.d_enc_err, 0, 4, st));
         G.enc_outstanding = 0;
+        if ((rc = enc_forget_failed(st))) return rc;
         if (err & 1u)
             return seterr(DC_ERR_INPUT, "input contains -1.0f, the reference encoder's empty-history sentinel "
                                         "(impl/dataCompression.c:2032); CT5/7/11 inputs must be >= 0 (toSmallDataset_float)");
@@ -623,7 +636,7 @@ int dc_encode_clear_status(void) {
     hipStream_t st = G.last_enc_st ? G.last_enc_st : G.st;
     HIPCHK(hipMemsetAsync(G.d_enc_err, 0, 4, st));
     G.enc_outstanding = 0;
-    return DC_OK;
+    return enc_forget_failed(st);
 }
 
 /* ------------------------------------------------------------------------------------------ */
@@ -1309,9 +1322,10 @@ int dc_med_device(const void* d_x, long long n, float* mean_out, int* type_out) 
     float m;
     int t;
     unsigned fl = 0;
-    for (int wide = med_force_wide(); wide < 2; wide++) {       /* the narrow window, then the wide one if it missed */
-        if ((wide ? dc_launch_med_wide : dc_launch_med)((const float*)d_x, n, 0.0f, G.med_scr, &G.d_f[1], &G.d_i[0],
-                                                         NULL, NULL, G.st))
+    const int forced = med_force_wide();
+    for (int wide = forced; wide < 2; wide++) {       /* the narrow window, then the wide one if it missed */
+        if (wide ? dc_launch_med_wide((const float*)d_x, n, 0.0f, G.med_scr, &G.d_f[1], &G.d_i[0], NULL, NULL, forced, G.st)
+                 : dc_launch_med((const float*)d_x, n, 0.0f, G.med_scr, &G.d_f[1], &G.d_i[0], NULL, NULL, G.st))
             return seterr(DC_ERR_HIP, "med launch failed");
         /* flag, then mean, type, sum, max (dc_aux.hip MedScratch.res): one copy */
         long long r[5];
@@ -1337,9 +1351,11 @@ int dc_med_sum_device(const void* d_x, long long n, float s_init, float* sum_out
     if (grow(&G.med_scr, &G.med_scr_cap, (size_t)dc_med_scratch_bytes(n))) return DC_ERR_HIP;
     float h[2];
     unsigned fl = 0;
-    for (int wide = med_force_wide(); wide < 2; wide++) {
-        if ((wide ? dc_launch_med_wide : dc_launch_med)((const float*)d_x, n, s_init, G.med_scr, &G.d_f[1], &G.d_i[0],
-                                                         &G.d_f[2], &G.d_f[3], G.st))
+    const int forced = med_force_wide();
+    for (int wide = forced; wide < 2; wide++) {
+        if (wide ? dc_launch_med_wide((const float*)d_x, n, s_init, G.med_scr, &G.d_f[1], &G.d_i[0], &G.d_f[2], &G.d_f[3],
+                                      forced, G.st)
+                 : dc_launch_med((const float*)d_x, n, s_init, G.med_scr, &G.d_f[1], &G.d_i[0], &G.d_f[2], &G.d_f[3], G.st))
             return seterr(DC_ERR_HIP, "med launch failed");
         long long r[5];
         HIPCHK(hipMemcpyAsync(r, dc_med_flag_ptr(G.med_scr, n, 0), sizeof r, hipMemcpyDeviceToHost, G.st));

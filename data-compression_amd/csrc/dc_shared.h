@@ -109,6 +109,7 @@ int dc_launch_encode(const float* x, long long n, long long idx0, const DC_NS Pa
                      unsigned long long* dbg, int mode, const uint32_t* crc_tab, uint32_t* crc_blk,
                      dc_hip_stream stream);
 int dc_encode_mode(void);
+int dc_encode_crc_fused_last(void);      /* 1: the last encode launch computed the fused CRC pieces */
 unsigned dc_encode_epoch_limit(void);
 long long dc_encode_group_count(long long n);
 long long dc_encode_tile_count(long long n);
@@ -214,7 +215,7 @@ int dc_launch_to_small(const float* x, long long n, float* y, float* part_v, lon
 int dc_launch_med(const float* x, long long n, float s_init, void* scratch, float* d_mean, int* d_type, float* d_sum,
                   float* d_max, dc_hip_stream st);
 int dc_launch_med_wide(const float* x, long long n, float s_init, void* scratch, float* d_mean, int* d_type,
-                       float* d_sum, float* d_max, dc_hip_stream st);
+                       float* d_sum, float* d_max, int fresh, dc_hip_stream st);
 unsigned* dc_med_flag_ptr(void* scratch, long long n, int is_double);
 int dc_launch_med_shard(const float* x, long long n, double s_est, int trans, void* scratch, long long** d_rec,
                         dc_hip_stream st);

@@ -385,6 +385,28 @@ def test_med_windows(dc, oracle, kind, n, monkeypatch):
             assert dc.L.dc_med_last_wide() == 0          # the narrow window holds these sums
 
 
+@pytest.mark.parametrize("n", [5000, 1 << 20])
+def test_med_wide_fresh(dc, oracle, n, monkeypatch):
+    """DC_MED_WIDE=1 on the FIRST call for an array: the wide window must compute its own chunk
+    sums and binade estimates, not take those an earlier call on other data left in the scratch.  The
+    previous call here runs on a different array (other values, other size), then the forced-wide call on
+    a new one; both equal the serial sums."""
+    import torch
+    rs = np.random.RandomState(n % 101)
+    prev = (rs.rand(3 * n + 7) * 1e4).astype(np.float32)         # other binades, other chunk count
+    x = oracle.gen_u10(n)
+    dp = torch.from_numpy(prev).cuda()
+    dx = torch.from_numpy(x).cuda()
+    torch.cuda.synchronize()
+    monkeypatch.setenv("DC_MED_WIDE", "1")
+    for arr, d in ((prev, dp), (x, dx), (prev, dp)):
+        om, ot = oracle.med(arr)
+        mean, t = dc.med_device(d.data_ptr(), len(arr))
+        assert np.float32(mean).view(np.uint32) == np.float32(om).view(np.uint32), (len(arr), mean, om)
+        assert t == ot
+        assert dc.L.dc_med_last_wide() == 1
+
+
 @pytest.mark.parametrize("ber", [1e-6, 1e-4])
 def test_ct9_ber_flow(dc, oracle, ber):
     """CT9 (bitmask + CRC) with real bit flips: the sender's CRC-32 of the CT7

@@ -15,7 +15,12 @@ HIPCC = "/opt/rocm/bin/hipcc"
 
 FLOORS = {
     "dc_encode.hip": {r"encode_fused_kernelILi7ELb0E": 7},
-    "dc_decode3.hip": {r"parse3_kernelILi7ELi16E": 6, r"decode3_kernelILi7ELi16ELi1040E": 4},
+    # every segment length the hot paths run (16: CT6 / CT11 and mid sizes; 20: CT5/CT7 above 2.5 M chunks, the
+    # headline bench), and the dense-job decode3 instance
+    # headline bench), and the dense-job decode3 instance.  parse3<7,20> holds 5 waves per SIMD (its 20-chunk
+    # segments: 3971 jobs at 2^26 = 3.9 per SIMD, all resident in one round)
+    "dc_decode3.hip": {r"parse3_kernelILi7ELi16E": 6, r"parse3_kernelILi7ELi20E": 5,
+                       r"decode3_kernelILi7ELi(16|20)ELi1040E": 4, r"parse3_kernelILi6ELi16E": 6},
 }
 
 
