@@ -1054,9 +1054,9 @@ def e2e_run(C, W, steps, warmup):
     """End-to-end multi-GPU step, device-side: each rank encodes its shard at start bit 0 with
     its global index (bit count left on the device), the bit counts and the shards are all-gathered (RCCL
     over xGMI; slots sized from the warm-up's largest shard), one merge kernel scans the counts and lays
-    the shards into the single global stream on every rank, and each rank decodes its own shard with the
-    segment decoder, its first predictions fixed after a 12-byte all-gather of the previous shard's last
-    values.  No host read inside the timed steps; the status words are checked after them."""
+    the shards into the single global stream on every rank, and each rank cuts its shard out of that
+    received stream and decodes it with the segment decoder, its first predictions fixed after a 12-byte
+    all-gather of the previous shard's last values.  No host read inside the timed steps; the status words are checked after them."""
     import torch
     L, dev, dcamd = C.L, C.dev, C.dcamd
     n, ct, typ, mask17, xs = W["n"], W["ct"], W["type"], W["mask17"], W["xs"]
@@ -1066,6 +1066,8 @@ def e2e_run(C, W, steps, warmup):
     glob = torch.zeros((C.world * cap + 64) // 4 * 4, dtype=torch.uint8, device=dev)
     d_count = torch.zeros(1, dtype=torch.int64, device=dev)
     d_total = torch.zeros(1, dtype=torch.int64, device=dev)
+    recv = torch.zeros(cap + 64, dtype=torch.uint8, device=dev)       # this rank's shard cut out of the received
+    d_rbits = torch.zeros(1, dtype=torch.int64, device=dev)           # global stream
     idx0 = C.rank * n
     slot = [(cap + 8 + 3) // 4 * 4]
 
@@ -1082,9 +1084,10 @@ def e2e_run(C, W, steps, warmup):
         L.encode_device(ct, xs.data_ptr(), n, local.data_ptr(), idx0=idx0, type_=typ, mask17=mask17, start_bit=0,
                         total_ptr=d_count.data_ptr())
         show("after encode")
-        dcamd.gather_stream_device(L, local, d_count, slot[0], glob, d_total)
+        counts = dcamd.gather_stream_device(L, local, d_count, slot[0], glob, d_total)
         show("after gather")
-        dcamd.decode_sharded_device(L, ct, local, d_count, (cap + 64) // 16 * 16, n, out, typ, mask17)
+        dcamd.decode_sharded_device(L, ct, local, d_count, (cap + 64) // 16 * 16, n, out, typ, mask17,
+                                    received=(glob, counts, recv, d_rbits))
         show("after decode")
 
     # the zero fills above are queued on torch's stream, the steps on the library's: without this a fill
@@ -1116,6 +1119,7 @@ def e2e_run(C, W, steps, warmup):
     # self-check: poison the merged global stream and the decoded shard, one more step, device hashes against
     # the oracle's global stream and its decode's slice for this rank (tests/golden/bench_hashes.json)
     glob.fill_(0xA5)
+    recv.fill_(0x5A)
     out.view(torch.int32).fill_(-1)
     torch.cuda.synchronize()
     step()
@@ -1134,9 +1138,10 @@ def e2e_run(C, W, steps, warmup):
                                   "its decode, every rank's slice" if g is not None else "none for this workload"),
             "how": "encode at start bit 0 (device bit count) + all-gather of the bit counts and of the shards "
                    "(slots from the warm-up's largest) + one merge kernel (device exscan, shifted shards, "
-                   "OR-ed shared words) into the single global stream on every rank + segment-decoder shard "
-                   "decode with a 12-byte all-gather of the previous shard's last values and a one-wave "
-                   "prefix fix; no host read inside the timed steps"}
+                   "OR-ed shared words) into the single global stream on every rank + each rank's shard cut "
+                   "out of that received stream (extract kernel) and decoded by the segment decoder with a "
+                   "12-byte all-gather of the previous shard's last values and a one-wave prefix fix; no host "
+                   "read inside the timed steps"}
 
 
 if __name__ == "__main__":

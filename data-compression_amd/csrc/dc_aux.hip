@@ -2014,6 +2014,58 @@ extern "C" int dc_launch_merge_shards(const uint8_t* g, long long P, int world, 
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// The receiver's side of the all-gather: shard `rank` cut out of the merged global stream (the bytes that
+// arrived, not the rank's own encode) to bit 0 of d, its bit count to *nbits_out -- what
+// dc_decode_shard3_device then decodes.  Every workgroup scans the counts itself (no host read); thread =
+// one 32-bit output word, v_alignbit of the two global words it spans, the bits past the shard cleared.
+// err |= 4: the shard does not fit d or lies outside the global buffer (nothing written then).
+__global__ __launch_bounds__(256) void extract_shard_kernel(const uint32_t* __restrict__ g, long long g_bytes,
+                                                            const unsigned long long* __restrict__ counts, int rank,
+                                                            uint32_t* __restrict__ d, long long d_bytes,
+                                                            unsigned long long* __restrict__ nbits_out,
+                                                            unsigned* __restrict__ err) {
+    __shared__ unsigned long long s_start, s_cnt;
+    __shared__ int bad;
+    if (threadIdx.x == 0) {
+        unsigned long long acc = 0;
+        for (int r = 0; r < rank; r++) acc += counts[r];
+        const unsigned long long cnt = counts[rank];
+        s_start = acc;
+        s_cnt = cnt;
+        const int b = ((long long)((cnt + 31) / 32) * 4 > d_bytes || (long long)((acc + cnt + 31) / 32) * 4 > g_bytes) ? 4 : 0;
+        bad = b;
+        if (blockIdx.x == 0) {
+            *nbits_out = b ? 0ull : cnt;
+            if (b) atomicOr(err, (unsigned)b);
+        }
+    }
+    __syncthreads();
+    if (bad) return;
+    const unsigned long long S = s_start, cnt = s_cnt;
+    const long long nw = (long long)((cnt + 31) / 32), gw = g_bytes / 4;
+    const int sh = (int)(S & 31ull);
+    for (long long w = (long long)blockIdx.x * 256 + threadIdx.x; w < nw; w += (long long)gridDim.x * 256) {
+        const long long i = (long long)(S >> 5) + w;
+        const uint32_t a = __builtin_bswap32(g[i]);
+        const uint32_t b = i + 1 < gw ? __builtin_bswap32(g[i + 1]) : 0u;
+        uint32_t v = sh ? __builtin_amdgcn_alignbit(a, b, 32 - sh) : a;
+        const long long left = (long long)cnt - 32 * w;                   // shard bits from this word's top
+        if (left < 32) v &= ~(0xFFFFFFFFu >> left);
+        d[w] = __builtin_bswap32(v);
+    }
+}
+
+extern "C" int dc_launch_extract_shard(const uint8_t* g, long long g_bytes, const unsigned long long* counts, int rank,
+                                       uint8_t* d, long long d_bytes, unsigned long long* nbits_out, unsigned* err,
+                                       hipStream_t st) {
+    if (rank < 0 || ((uintptr_t)g & 3) || ((uintptr_t)d & 3)) return -2;
+    long long grid = (d_bytes / 4 + 255) / 256 + 1;
+    if (grid > 8192) grid = 8192;
+    hipLaunchKernelGGL(extract_shard_kernel, dim3((unsigned)grid), dim3(256), 0, st, reinterpret_cast<const uint32_t*>(g),
+                       g_bytes, counts, rank, reinterpret_cast<uint32_t*>(d), d_bytes, nbits_out, err);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // Himeno halo planes: the plane ijk = 1/2/3 at index v of a [mi][mj][mk] float array in
 // the order of transform_3d_array_to_1d_array (impl/dataCompression.c:3741-3775), gathered into a
 // contiguous array; and the decoded plane + min scattered back (impl/himenoBMTxps.c:699-706).

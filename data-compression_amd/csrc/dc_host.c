@@ -965,7 +965,23 @@ int dc_merge_shards_device(const void* d_gathered, long long slot_bytes, int wor
     return DC_OK;
 }
 
-/* 1: a shard longer than its slot, 2: the global stream longer than the output (sticky; reset = 1 clears) */
+/* the receiver's side: shard `rank` of the merged global stream d_global (g_bytes of buffer, the shards' bit
+   counts d_counts as merged) to bit 0 of d_out (out_bytes of room), its bit count to d_nbits; no host read.
+   A shard that does not fit sets bit 4 of dc_merge_status */
+int dc_extract_shard_device(const void* d_global, long long g_bytes, const unsigned long long* d_counts, int rank,
+                            void* d_out, long long out_bytes, unsigned long long* d_nbits) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (!d_global || !d_counts || !d_out || !d_nbits || rank < 0 || ((uintptr_t)d_global & 3u) || ((uintptr_t)d_out & 3u))
+        return seterr(DC_ERR_ARG, "extract: bad buffers (4-byte aligned)");
+    if (dc_launch_extract_shard((const uint8_t*)d_global, g_bytes, d_counts, rank, (uint8_t*)d_out, out_bytes, d_nbits,
+                                G.d_enc_err + 4, G.st))
+        return seterr(DC_ERR_HIP, "extract launch failed");
+    return DC_OK;
+}
+
+/* 1: a shard longer than its slot, 2: the global stream longer than the output, 4: an extracted shard that did
+   not fit (sticky; reset = 1 clears) */
 int dc_merge_status(unsigned* status_out, int reset) {
     int rc = ensure_init();
     if (rc) return rc;

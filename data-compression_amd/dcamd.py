@@ -47,7 +47,7 @@ EXT_SYMBOLS = [
     "dc_decode_status", "dc_abi_status", "dc_med_sum_device", "dc_type_from_max", "dc_set_small_chunk_max_bytes",
     "dc_set_decode3_min_bytes", "dc_set_decode3_seg", "dc_set_fused3", "dc_fused3_stamps", "dc_fused3_last_seg", "dc_decode3_last_fused", "dc_last_decode_was_v3", "dc_last_decode_launched_v3",
     "dc_encode_status", "dc_encode_clear_status", "dc_encode_mode", "dc_encode_retries", "dc_crc_resend_device",
-    "dc_merge_shards_device", "dc_merge_status", "dc_decode_shard3_device", "dc_decode_shard3_fix",
+    "dc_merge_shards_device", "dc_merge_status", "dc_extract_shard_device", "dc_decode_shard3_device", "dc_decode_shard3_fix",
     "dc_decode_status_clear", "dc_set_runs_max_bytes", "dc_last_decode_was_runs",
     "dc_last_decode_launched_runs", "dc_last_decode_used_maps", "dc_med_last_wide", "dc_set_decode3_maps", "dc_set_halo_async", "dc_med_shard_stats", "dc_med_shard_trans",
     "dc_med_shard_binades",
@@ -90,6 +90,7 @@ class Lib:
         L.dc_decode_shard_fix.argtypes = [vp]
         L.dc_merge_shards_device.argtypes = [vp, ll, C.c_int, vp, vp, ll, vp]
         L.dc_merge_status.argtypes = [C.POINTER(C.c_uint), C.c_int]
+        L.dc_extract_shard_device.argtypes = [vp, ll, vp, C.c_int, vp, ll, vp]
         L.dc_decode_shard3_device.argtypes = [C.c_int, vp, vp, ll, ll, C.c_int, u32, vp, C.c_int]
         L.dc_decode_shard3_fix.argtypes = [vp]
         L.dc_to_small_device.argtypes = [vp, ll, vp, C.POINTER(C.c_float)]
@@ -454,6 +455,10 @@ class Lib:
         and its device bit count (dc_gpu.h); no host read."""
         self.check(self.L.dc_merge_shards_device(gathered_ptr, slot_bytes, world, counts_ptr, out_ptr, out_bytes,
                                                  total_ptr), "dc_merge_shards_device")
+
+    def extract_shard_device(self, global_ptr, global_bytes, counts_ptr, rank, out_ptr, out_bytes, nbits_ptr):
+        self.check(self.L.dc_extract_shard_device(global_ptr, global_bytes, counts_ptr, rank, out_ptr, out_bytes,
+                                                  nbits_ptr), "dc_extract_shard_device")
 
     def merge_status(self, reset=False):
         v = C.c_uint(0)
@@ -923,15 +928,25 @@ def gather_stream_device(L, local, d_count, slot_bytes, out, d_total, group=None
     return counts
 
 
-def decode_sharded_device(L, ct, local, d_count, max_bytes, num, out, type_=0, mask17=0, group=None):
-    """Decode this rank's shard from its own encoded buffer (start bit 0, bit count on the device) with the
-    segment decoder; its first predictions wait for the previous rank's last three values, which arrive
-    by one all-gather of 12 bytes per rank, and a one-wave fix decodes them (dc_decode_shard3_fix).  No
-    host read: L.decode_status() after the steps tells whether every shard stayed on this path."""
+def decode_sharded_device(L, ct, local, d_count, max_bytes, num, out, type_=0, mask17=0, group=None, received=None):
+    """Decode this rank's shard (start bit 0, bit count on the device) with the segment decoder; its first
+    predictions wait for the previous rank's last three values, which arrive by one all-gather of 12 bytes
+    per rank, and a one-wave fix decodes them (dc_decode_shard3_fix).  No host read: L.decode_status() after
+    the steps tells whether every shard stayed on this path.
+
+    received = (glob, counts, buf, d_nbits): the shard is cut out of the merged global stream `glob` (the bytes
+    that arrived: gather_stream_device's output, `counts` the all-gathered bit counts it returned) into `buf`
+    (bit 0, count to d_nbits; dc_extract_shard_device) and decoded from there, as a receiver decodes what it
+    received (impl/himenoBMTxps.c:696-697); otherwise from the rank's own encode `local` / d_count."""
     import torch.distributed as dist
     import torch
     rank = dist.get_rank(group)
     dev = out.device
+    if received is not None:
+        glob, counts, buf, d_nbits = received
+        L.extract_shard_device(glob.data_ptr(), glob.numel(), counts.data_ptr(), rank, buf.data_ptr(), buf.numel(),
+                               d_nbits.data_ptr())
+        local, d_count = buf, d_nbits
     L.decode_shard3_device(ct, local.data_ptr(), d_count.data_ptr(), max_bytes, num, out.data_ptr(), type_, mask17,
                            has_history=rank > 0)
     cur, ls = torch.cuda.current_stream(dev), _lib_stream(L, dev)

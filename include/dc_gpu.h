@@ -111,6 +111,12 @@ int dc_decode_shard_fix(const float* d_hin);
 int dc_merge_shards_device(const void* d_gathered, long long slot_bytes, int world, const unsigned long long* d_counts,
                            void* d_out, long long out_bytes, unsigned long long* d_total);
 int dc_merge_status(unsigned* status_out, int reset);
+/* dc_extract_shard_device: the receiver's side of the all-gather -- shard `rank` cut out of the merged global
+ *   stream d_global (g_bytes of buffer; d_counts the shards' bit counts, as given to the merge) to bit 0 of
+ *   d_out (out_bytes of room, 4-byte aligned), its bit count to *d_nbits: the bytes that arrived, ready for
+ *   dc_decode_shard3_device.  A shard that does not fit sets dc_merge_status bit 4 (nothing written). */
+int dc_extract_shard_device(const void* d_global, long long g_bytes, const unsigned long long* d_counts, int rank,
+                            void* d_out, long long out_bytes, unsigned long long* d_nbits);
 int dc_decode_shard3_device(int ct, const void* d_stream, const unsigned long long* d_nbits, long long max_bytes,
                             long long num, int type, uint32_t mask17, void* d_out, int has_history);
 int dc_decode_shard3_fix(const float* d_hin);

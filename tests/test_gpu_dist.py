@@ -77,15 +77,19 @@ def _worker(rank, world, port, ct, n, kind, q):
         dist.destroy_process_group()
 
 
-def _worker_device(rank, world, port, ct, n, kind, q):
+def _worker_device(rank, world, port, ct, n, kind, q, backend="gloo", received=True):
     """The device-side step (bench.py e2e): encode at start bit 0 with the global index, device bit count;
     gather_stream_device (all-gathered counts and shards, one merge kernel); decode_sharded_device (the
-    segment decoder on the rank's own shard, 12-byte exchange, one-wave prefix fix).  No host read until
-    the checks.  A shard the segment decoder declines (a prediction chain through its whole first chunk)
-    is decoded again on the host-synchronised path from the gathered stream."""
+    segment decoder on the rank's shard -- cut out of the received global stream when `received`, else its
+    own encode -- 12-byte exchange, one-wave prefix fix).  No host read until the checks.  A shard the
+    segment decoder declines (a prediction chain through its whole first chunk) is decoded again on the
+    host-synchronised path from the gathered stream.  backend "nccl" (world 1 on the one GPU of a box):
+    the collectives run through RCCL on device tensors, the branch the driver's multi-GPU bench takes."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     try:
         import dcamd
         from pyoracle import Oracle
@@ -117,11 +121,20 @@ def _worker_device(rank, world, port, ct, n, kind, q):
         slot = (cap + 8 + 3) // 4 * 4
         glob = torch.zeros((world * cap + 64) // 4 * 4, dtype=torch.uint8, device=dev)
         d_total = torch.zeros(1, dtype=torch.int64, device=dev)
-        dcamd.gather_stream_device(L, local, d_count, slot, glob, d_total)
+        counts_d = dcamd.gather_stream_device(L, local, d_count, slot, glob, d_total)
         out = torch.empty(n, dtype=torch.float32, device=dev)
-        dcamd.decode_sharded_device(L, ct, local, d_count, (cap + 64) // 16 * 16, n, out, t, m17)
+        rx = None
+        if received:                           # decode the received bytes: poison the rank's own encode first
+            L.synchronize()
+            local.fill_(0xA5)
+            torch.cuda.synchronize()
+            rx = (glob, counts_d, torch.zeros(cap + 64, dtype=torch.uint8, device=dev),
+                  torch.zeros(1, dtype=torch.int64, device=dev))
+        dcamd.decode_sharded_device(L, ct, local, d_count, (cap + 64) // 16 * 16, n, out, t, m17, received=rx)
         L.synchronize()
         torch.cuda.synchronize()
+        if received:
+            assert int(rx[3].item()) == int(d_count.item()), (int(rx[3].item()), int(d_count.item()))
         st_enc, st_merge, st_dec = L.encode_status(), L.merge_status(reset=True), L.decode_status()
         tot = int(d_total.item())
         fallback = st_dec != 0
@@ -132,7 +145,11 @@ def _worker_device(rank, world, port, ct, n, kind, q):
             dist.all_gather(counts, torch.tensor([bits], dtype=torch.int64))
             starts, _ = dcamd.shard_offsets([int(c[0]) for c in counts])
             g = glob[:(tot + 7) // 8]
-            dcamd.decode_sharded(L, ct, g, g.numel(), starts[rank], bits, n, out, t, m17)
+            if world == 1:
+                L.decode_device(ct, g.data_ptr(), g.numel(), n, out.data_ptr(), t, m17)
+                L.decode_finish()
+            else:
+                dcamd.decode_sharded(L, ct, g, g.numel(), starts[rank], bits, n, out, t, m17)
             torch.cuda.synchronize()
         s_all, nb_all, pos_all = O.compress(ct, xs, 1e-3, t, m17)
         dec_all, _ = O.decompress(ct, s_all, N, 1e-3, t, m17)
@@ -168,15 +185,20 @@ def test_sharded_encode_gather_decode_world2(ct, n, kind):
     assert all(r[1] is True and r[2] is True for r in res), res
 
 
-@pytest.mark.parametrize("ct,n,kind", [(7, (1 << 18) + 5, "u10"), (5, 100003, "chain"), (6, 65536, "u10"),
-                                       (11, 40001, "u10"), (7, 300007, "chain"), (7, 1 << 20, "u10")])
-def test_device_step_world2(ct, n, kind):
+@pytest.mark.parametrize("ct,n,kind,received", [(7, (1 << 18) + 5, "u10", True), (5, 100003, "chain", True),
+                                                (6, 65536, "u10", True), (11, 40001, "u10", True),
+                                                (7, 300007, "chain", True), (7, 1 << 20, "u10", True),
+                                                (7, (1 << 18) + 5, "u10", False)])
+def test_device_step_world2(ct, n, kind, received):
     """The device-side multi-GPU step against the oracle's single stream and its decode; ordinary shards
-    stay on the device path (no fallback)."""
+    stay on the device path (no fallback).  received: every rank decodes its shard cut out of the merged
+    global stream, its own encode poisoned before the decode (the step must decode what
+    arrived)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_device, args=(r, 2, port, ct, n, kind, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker_device, args=(r, 2, port, ct, n, kind, q, "gloo", received))
+             for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in procs]
@@ -185,6 +207,25 @@ def test_device_step_world2(ct, n, kind):
     assert all(r[1] is True and r[2] is True for r in res), res
     if kind == "u10":
         assert not any(r[3] for r in res), res
+
+
+@pytest.mark.parametrize("ct,n,kind", [(7, (1 << 20) + 3, "u10"), (5, 100003, "chain"), (6, 65536, "u10")])
+def test_device_step_rccl_world1(ct, n, kind):
+    """The RCCL branch of the device-side step, executed (it had only ever run as gloo on host
+    copies): a world-size-1 `nccl` process group on the box's one GPU, so gather_stream_device's two
+    all_gather_into_tensor calls, the merge, the extract of the received shard, decode_sharded_device and
+    exchange_history's all_gather all run on device tensors through RCCL; stream and decode against the
+    oracle."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    p = ctx.Process(target=_worker_device, args=(0, 1, port, ct, n, kind, q, "nccl", True))
+    p.start()
+    res = q.get(timeout=240)
+    p.join(timeout=60)
+    assert res[1] is True and res[2] is True, res
+    if kind == "u10":
+        assert not res[3], res
 
 
 def _worker_med(rank, world, port, kind, n, q):
