@@ -1009,7 +1009,16 @@ def main():
                                      f"{args.input.upper()} 2^{args.log2n} float32 per GPU, absErrorBound={args.bound:g}")
         res["config"].update({"ber": args.ber, "flips_per_step": int(R["nbits"] * args.ber), "resends": R["resends"],
                               "detected_all": R["resends"] == args.steps and bool(R["ct9"].get("acks_ok"))})
-    if C.world > 1 and not args.no_e2e:
+    if C.world > 1 and args.ber > 0:
+        # config 5 across GPUs: the CT9 stream travels to the partner rank and back (the headline of --ber at N > 1);
+        # the per-rank flow with a local channel copy stays beside it
+        res["local_channel"] = {"value": res["value"], "ms_per_step": res["ms_per_step"]}
+        X = ct9_pairs_run(C, W, args.steps, args.warmup, args.ber)
+        res["ct9_exchange"] = X
+        res["value"], res["ms_per_step"] = X["value"], X["ms_per_step"]
+        res["config"]["detected_all"] = bool(X["detected_all"])
+        res["config"]["parallelism"] = f"pairs{C.world}"
+    elif C.world > 1 and not args.no_e2e:
         res["end_to_end"] = e2e_run(C, W, args.steps, args.warmup)
     del W
     if C.world == 1 and not args.no_extra and args.ber <= 0:
@@ -1031,7 +1040,8 @@ def main():
     bad = [nm for nm, ok in [("main", res["self_check"])] + [(f"sweep {k}", v.get("self_check")) for k, v in
                                                                res.get("sweep", {}).items()]
            + [(k, v.get("self_check")) for k, v in res.get("configs", {}).items()]
-           + [("end_to_end", res.get("end_to_end", {}).get("self_check"))] if ok is False]
+           + [("end_to_end", res.get("end_to_end", {}).get("self_check")),
+              ("ct9_exchange", res.get("ct9_exchange", {}).get("self_check"))] if ok is False]
     if C.dist is not None:
         C.dist.destroy_process_group()
     if bad:
@@ -1048,6 +1058,101 @@ def all_ranks_ok(C, ok):
     C.dist.all_reduce(t, op=C.dist.ReduceOp.MIN)
     v = float(t[0])
     return False if v < 0.5 else (True if v < 1.5 else None)
+
+
+def ct9_pairs_run(C, W, steps, warmup, ber):
+    """BASELINE config 5 across GPUs (CT9 = CT7 stream + CRC-32 at a bit-error rate): the
+    ranks pair up (dcamd.ct9_partner: 0-1, 2-3, ...) and every step each rank encodes its shard, CRCs its
+    stream and sends stream + [CRC, bits] to its partner over torch.distributed point-to-point (RCCL over xGMI
+    on device tensors), while receiving the partner's; the channel flips floor(bits * BER) bits of what
+    arrived, the receiver CRCs it and answers with an ack; a rejected stream is sent again and checked again
+    (impl/pingpong.c:280-289 sender, :408-447 receiver); then each rank decodes the copy it RECEIVED.  The acks
+    are read on the host every round (the reference's blocking MPI_Recv of crc_ok).  value = all ranks'
+    floats / max-over-ranks step time (each rank encodes n floats and decodes n)."""
+    import torch
+    L, dev, dcamd = C.L, C.dev, C.dcamd
+    n, ct, typ, mask17, xs = W["n"], W["ct"], W["type"], W["mask17"], W["xs"]
+    cap = L.stream_capacity(n)
+    stream = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    rcv = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    out = torch.empty(n, dtype=torch.float32, device=dev)
+    d_nbits = torch.zeros(1, dtype=torch.int64, device=dev)
+    idx0 = C.rank * n
+    partner = dcamd.ct9_partner(C.rank, C.world)
+    ops = dcamd.LibCT9(L)
+    torch.cuda.synchronize()
+    L.encode_device(ct, xs.data_ptr(), n, stream.data_ptr(), idx0=idx0, type_=typ, mask17=mask17,
+                    total_ptr=d_nbits.data_ptr())
+    nbits = L.encode_result()
+    nbytes = (nbits + 7) // 8
+    nbits_rx = dcamd.ct9_sizes(nbits, partner, dev)
+    nbytes_rx = (nbits_rx + 7) // 8
+    meta_tx = torch.zeros(2, dtype=torch.int64, device=dev)
+    meta_tx[1] = nbits
+    meta_rx = torch.zeros(2, dtype=torch.int64, device=dev)
+    crc_rx = torch.zeros(1, dtype=torch.int64, device=dev)
+    ack = torch.zeros(2, dtype=torch.int64, device=dev)
+    nflip = int(nbits_rx * ber)
+    seed = [1 + 1000003 * C.rank]
+    log = []
+
+    def step():
+        L.encode_device(ct, xs.data_ptr(), n, stream.data_ptr(), idx0=idx0, type_=typ, mask17=mask17,
+                        total_ptr=d_nbits.data_ptr())
+        r = dcamd.ct9_exchange(ops, stream, nbytes, meta_tx, rcv, nbytes_rx, nbits_rx, meta_rx, crc_rx, ack, partner,
+                               nflip, seed[0])
+        seed[0] += nflip
+        L.decode_device(ct, rcv.data_ptr(), nbytes_rx, n, out.data_ptr(), type_=typ, mask17=mask17, max_bytes=cap)
+        log.append(r)
+
+    for _ in range(max(warmup, 1)):
+        step()
+        L.decode_finish()
+    L.synchronize()
+    log.clear()
+    C.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    L.synchronize()
+    torch.cuda.synchronize()
+    wall = C.max_over_ranks(time.perf_counter() - t0)
+    st = {"encode": L.encode_status(), "decode": L.decode_status()}
+    if any(st.values()):
+        print(f"bench.py: CT9 exchange status words {st} after the timed steps", file=sys.stderr)
+        sys.exit(1)
+    # every round detected its damaged copy (nflip > 0: the first check fails, the resent copy passes)
+    detected = all(ok and (rx == 1 if nflip > 0 else rx == 0) and rounds == (2 if nflip > 0 else 1)
+                   for rounds, _, rx, ok in log) and len(log) == steps
+    detected = all_ranks_ok(C, detected)
+    # self-check: the received copy and its decode, poisoned first, against the oracle's stream and decode of
+    # the PARTNER's shard
+    rcv.fill_(0x5A)
+    out.view(torch.int32).fill_(-1)
+    torch.cuda.synchronize()
+    step()
+    L.synchronize()
+    if L.decode_status():
+        L.decode_finish()
+    torch.cuda.synchronize()
+    rh = L.hash_device(rcv.data_ptr(), nbytes_rx)
+    oh = L.hash_device(out.data_ptr(), 4 * n)
+    g = golden_entry(ct, W["kind"], W["log2n"], W["bound"], C.world)
+    if g is not None and C.world > 1:
+        g = g["ranks"][partner]
+    ok = None if g is None else (int(g["nbits"]) == nbits_rx and int(g["stream"]) == rh and int(g["out"]) == oh)
+    ok = all_ranks_ok(C, ok)
+    return {"value": round(C.world * 4.0 * n / (wall / steps) / 1e9, 3), "ms_per_step": round(wall / steps * 1e3, 4),
+            "partner": partner, "stream_bytes_sent": int(nbytes), "flips_per_step": nflip,
+            "resends_per_step": float(np.mean([r[2] for r in log])) if log else 0.0, "detected_all": detected,
+            "self_check": ok, "received_hash": f"{rh:016x}",
+            "self_check_golden": ("tests/golden/bench_hashes.json: the oracle's stream and decode of the partner's "
+                                  "shard" if g is not None else "none for this workload"),
+            "how": "pairs (0-1, 2-3, ...): encode + CRC-32 of the own stream, stream + [CRC, bits] to the partner and "
+                   "the partner's received (torch.distributed P2P: RCCL over xGMI), BER flips on the received copy, "
+                   "receiver CRC + ack back, the rejected stream resent and re-checked, decode of the received "
+                   "copy; acks read on the host each round"}
 
 
 def e2e_run(C, W, steps, warmup):

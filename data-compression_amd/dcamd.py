@@ -731,6 +731,134 @@ def halo_exchange(streams, nbits, mins, down, up, group=None):
     return out
 
 
+# ---- CT9 between ranks (BASELINE config 5 across GPUs) ---------------------------
+def ct9_partner(rank, world):
+    """Rank pairs (0,1), (2,3), ...: each rank sends its stream to its partner and receives the partner's
+    (the ping and the pong of impl/pingpong.c at once).  An odd world's last rank is its own partner: its
+    channel is a local copy."""
+    p = rank ^ 1
+    return p if p < world else rank
+
+
+class LibCT9:
+    """The device operations of a CT9 round (ct9_exchange) on the library's HIP stream: the CRC-32 of a
+    stream (dc_crc32_device_async: zlib's CRC = the reference's do_crc32, impl/dataCompression.c:5524) into
+    the low 4 bytes of an int64 device slot, and floor(bits * BER) bit flips (dc_flip_bits_device, the
+    channel's damage).  to_torch / to_lib order torch's current stream (where the collectives run) and the
+    library's."""
+
+    def __init__(self, L):
+        self.L = L
+
+    def crc(self, buf, nbytes, dst):
+        self.L.crc32_device_async(buf.data_ptr(), nbytes, dst.data_ptr())
+
+    def flip(self, buf, nbits, count, seed):
+        if count > 0:
+            self.L.flip_bits_device(buf.data_ptr(), nbits, count, seed)
+
+    def to_torch(self, dev):
+        import torch
+        _after(_lib_stream(self.L, dev), torch.cuda.current_stream(dev))
+
+    def to_lib(self, dev):
+        import torch
+        _after(torch.cuda.current_stream(dev), _lib_stream(self.L, dev))
+
+
+def _p2p(ops_spec, group, host):
+    """Run [(isend|irecv, tensor, peer, tag)] as one batch; gloo moves host copies of device tensors."""
+    import torch.distributed as dist
+    if not ops_spec:
+        return
+    ops, back = [], []
+    for kind, t, peer, tag in ops_spec:
+        if host and t.device.type == "cuda":
+            h = t.cpu() if kind == "send" else t.new_empty(t.shape, device="cpu")
+            if kind == "recv":
+                back.append((t, h))
+            t = h
+        ops.append(dist.P2POp(dist.isend if kind == "send" else dist.irecv, t, peer, group=group, tag=tag))
+    for w in dist.batch_isend_irecv(ops):
+        w.wait()
+    for t, h in back:
+        t.copy_(h)
+
+
+def ct9_exchange(ops, stream, nbytes_tx, meta_tx, rcv, nbytes_rx, nbits_rx, meta_rx, crc_rx, ack, partner, nflip,
+                 seed, group=None, max_rounds=4):
+    """One CT9 round with the partner rank (impl/pingpong.c: sender :280-289, receiver :408-447), both directions
+    at once, over torch.distributed point-to-point (RCCL on device tensors; gloo on host copies):
+      sender    meta_tx = [CRC-32 of its stream, its bit count]; sends the stream bytes and meta_tx;
+      receiver  receives them into rcv / meta_rx, the channel flips nflip bits of rcv (seeded), CRCs what
+                arrived and answers ack = 1 when the CRC (or the bit count) differs -- 'n' in the reference;
+      both      read the two acks on the host (the reference's blocking MPI_Recv of crc_ok); a rejected
+                stream is sent again (the reference repeats the round: ping_pong_count--), the receiver
+                CRCs the new copy and answers again, until both acks are 0 or max_rounds.
+    The stream sizes are known on both sides beforehand (the reference's receiver passes the same byte
+    count: both ranks compressed the same data; here ct9_sizes exchanges them once).  meta_tx / meta_rx /
+    crc_rx: int64 tensors of 2 / 2 / 1 (CRC in the low 4 bytes; crc_rx's upper bytes zero), ack int64[2]
+    (device).  The decode of rcv is the caller's.  Returns (rounds, resent_tx, resent_rx, ok)."""
+    import torch.distributed as dist
+    dev = stream.device
+    cuda = dev.type == "cuda"
+    host = cuda and dist.get_backend(group) == "gloo"
+    me = dist.get_rank(group)
+    ops.crc(stream, nbytes_tx, meta_tx)                     # the sender's CRC of what it sends
+    if cuda:
+        ops.to_torch(dev)
+    if partner == me:                                       # the local channel
+        rcv[:nbytes_rx].copy_(stream[:nbytes_tx])
+        meta_rx.copy_(meta_tx)
+    else:
+        _p2p([("send", stream[:nbytes_tx], partner, 0), ("send", meta_tx, partner, 1),
+              ("recv", rcv[:nbytes_rx], partner, 0), ("recv", meta_rx, partner, 1)], group, host)
+    if cuda:
+        ops.to_lib(dev)
+    ops.flip(rcv, nbits_rx, nflip, seed)                    # the channel's damage
+    resent_tx = resent_rx = 0
+    for rnd in range(max_rounds):
+        ops.crc(rcv, nbytes_rx, crc_rx)                     # the receiver's check of what arrived
+        if cuda:
+            ops.to_torch(dev)
+        ack[0] = ((crc_rx[0] & 0xFFFFFFFF) != (meta_rx[0] & 0xFFFFFFFF)) | (meta_rx[1] != nbits_rx)
+        if partner == me:
+            ack[1] = ack[0]
+        else:
+            _p2p([("send", ack[0:1], partner, 2), ("recv", ack[1:2], partner, 2)], group, host)
+        a = ack.cpu()                                       # [my verdict on its stream, its verdict on mine]
+        rej_rx, rej_tx = int(a[0]), int(a[1])
+        if not rej_rx and not rej_tx:
+            return rnd + 1, resent_tx, resent_rx, True
+        if partner == me:
+            rcv[:nbytes_rx].copy_(stream[:nbytes_tx])
+        else:
+            spec = []
+            if rej_tx:
+                spec.append(("send", stream[:nbytes_tx], partner, 3))
+            if rej_rx:
+                spec.append(("recv", rcv[:nbytes_rx], partner, 3))
+            _p2p(spec, group, host)
+        resent_tx += rej_tx
+        resent_rx += rej_rx
+        if cuda:
+            ops.to_lib(dev)
+    return max_rounds, resent_tx, resent_rx, False
+
+
+def ct9_sizes(nbits_tx, partner, dev, group=None):
+    """The partner's stream bit count (exchanged once, before the rounds)."""
+    import torch
+    import torch.distributed as dist
+    if partner == dist.get_rank(group):
+        return int(nbits_tx)
+    host = dev.type == "cuda" and dist.get_backend(group) == "gloo"
+    t = torch.tensor([int(nbits_tx)], dtype=torch.int64, device=dev)
+    r = torch.zeros(1, dtype=torch.int64, device=dev)
+    _p2p([("send", t, partner, 9), ("recv", r, partner, 9)], group, host)
+    return int(r.item())
+
+
 def _bcast_scalar(v, src, dev, group=None, dtype=None):
     import torch
     import torch.distributed as dist

@@ -182,3 +182,79 @@ def test_halo_exchange(world, empty):
     for p in procs:
         p.join(timeout=60)
     assert all(r[1] for r in res), res
+
+
+class _NpCT9:
+    """Host stand-in for dcamd.LibCT9 (zlib's CRC-32 = the reference's do_crc32; the flips at
+    dcamd.flip_positions, as dc_flip_bits_device places them)."""
+
+    def crc(self, buf, nbytes, dst):
+        import zlib
+        dst[0] = zlib.crc32(buf[:nbytes].numpy().tobytes())
+
+    def flip(self, buf, nbits, count, seed):
+        import dcamd
+        for p in dcamd.flip_positions(nbits, count, seed):
+            buf[p // 8] ^= 0x80 >> (p % 8)
+
+
+def _ct9_worker(rank, world, port, nflip, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import dcamd
+        from pyoracle import Oracle
+        O = Oracle()
+        n = 5000 + 777 * rank                          # shards of different lengths: different stream sizes
+        x = O.gen_u10(n) + np.float32(rank)
+        _, xs = O.to_small(x)
+        t, m17 = O.type_mask(xs)
+        s, nb, pos = O.compress(7, xs, 1e-3, t, m17)
+        nbits = _bits_of(nb, pos)
+        partner = dcamd.ct9_partner(rank, world)
+        stream = torch.zeros(nb + 64, dtype=torch.uint8)
+        stream[:nb] = torch.from_numpy(s)
+        nbits_rx = dcamd.ct9_sizes(nbits, partner, stream.device)
+        nb_rx = (nbits_rx + 7) // 8
+        rcv = torch.zeros(nb_rx + 64, dtype=torch.uint8)
+        meta_tx = torch.zeros(2, dtype=torch.int64)
+        meta_tx[1] = nbits
+        meta_rx, crc_rx, ack = (torch.zeros(2, dtype=torch.int64), torch.zeros(1, dtype=torch.int64),
+                                torch.zeros(2, dtype=torch.int64))
+        res = dcamd.ct9_exchange(_NpCT9(), stream, nb, meta_tx, rcv, nb_rx, nbits_rx, meta_rx, crc_rx, ack, partner,
+                                 nflip, 7 + rank)
+        # what arrived is the partner's stream exactly (after the resend), and decodes as the partner's data
+        xp = O.gen_u10(5000 + 777 * partner) + np.float32(partner)
+        _, xps = O.to_small(xp)
+        tp, mp_ = O.type_mask(xps)
+        sp, nbp, _ = O.compress(7, xps, 1e-3, tp, mp_)
+        same = bool(nb_rx == nbp and np.array_equal(rcv[:nb_rx].numpy(), sp))
+        q.put((rank, partner, res, same))
+    except Exception as e:
+        q.put((rank, None, repr(e), False))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,nflip", [(2, 3), (2, 0), (3, 2), (4, 1)])
+def test_ct9_exchange(world, nflip):
+    """BASELINE config 5 across ranks, the protocol on host tensors (gloo): rank pairs swap CT7 streams with
+    their CRC-32, the receiver's copy is damaged by nflip bit flips, the CRC check rejects it, the sender
+    resends and the second check passes; the partner's stream arrives bit-exact.  An odd world's last rank is
+    its own partner (local channel)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ct9_worker, args=(r, world, port, nflip, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for rank, partner, r, same in res:
+        assert partner == (rank ^ 1 if (rank ^ 1) < world else rank), res
+        rounds, resent_tx, resent_rx, ok = r
+        assert ok and same, res
+        assert rounds == (2 if nflip else 1) and resent_rx == (1 if nflip else 0), res
+        assert resent_tx == (1 if nflip else 0), res

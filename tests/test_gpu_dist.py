@@ -228,6 +228,95 @@ def test_device_step_rccl_world1(ct, n, kind):
         assert not res[3], res
 
 
+def _shard_stream(O, xs, r, n, ct, t, m17):
+    """The oracle's stream of shard r (its elements' tokens with the 3 values before it as history): the
+    stream of xs[r n - 3, (r+1) n) without its first three tokens (tests/golden/make_bench_hashes.py)."""
+    if r == 0:
+        s, nb, pos = O.compress(ct, xs[:n], 1e-3, t, m17)
+        return s, _bits_of(nb, pos)
+    full, fb, fp = O.compress(ct, xs[r * n - 3:(r + 1) * n], 1e-3, t, m17)
+    _, hb, hp = O.compress(ct, xs[r * n - 3:r * n], 1e-3, t, m17)
+    b, m = _bits_of(hb, hp), _bits_of(fb, fp) - _bits_of(hb, hp)
+    bits = np.unpackbits(full[b // 8:(b + m + 7) // 8])[b % 8:b % 8 + m]
+    return np.packbits(bits), m
+
+
+def _worker_ct9(rank, world, port, n, ber, q):
+    """Config 5 across ranks on the device (bench.py ct9_pairs_run's round): encode the shard, CRC-32, stream +
+    [CRC, bits] to the partner, the channel's flips on what arrived, receiver CRC + ack, resend, decode of
+    the RECEIVED copy -- against the oracle's stream and decode of the partner's shard."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import dcamd
+        from pyoracle import Oracle
+        L = dcamd.Lib()
+        L.init(0)
+        L.set_bound(1e-3)
+        O = Oracle()
+        ct = 7
+        x = O.gen_u10(world * n)
+        _, xs = O.to_small(x)
+        t, m17 = O.type_mask(xs)
+        dev = torch.device("cuda", 0)
+        lo = rank * n
+        buf = torch.zeros(n + 4, dtype=torch.float32, device=dev)
+        halo = xs[max(lo - 3, 0):lo]
+        if halo.size:
+            buf[4 - halo.size:4] = torch.from_numpy(halo.copy())
+        buf[4:] = torch.from_numpy(xs[lo:lo + n].copy())
+        xd = buf[4:]
+        cap = L.stream_capacity(n)
+        stream = torch.zeros(cap, dtype=torch.uint8, device=dev)
+        rcv = torch.zeros(cap, dtype=torch.uint8, device=dev)
+        out = torch.empty(n, dtype=torch.float32, device=dev)
+        torch.cuda.synchronize()
+        L.encode_device(ct, xd.data_ptr(), n, stream.data_ptr(), idx0=lo, type_=t, mask17=m17)
+        nbits = L.encode_result()
+        partner = dcamd.ct9_partner(rank, world)
+        nbits_rx = dcamd.ct9_sizes(nbits, partner, dev)
+        meta_tx = torch.zeros(2, dtype=torch.int64, device=dev)
+        meta_tx[1] = nbits
+        meta_rx, crc_rx, ack = (torch.zeros(2, dtype=torch.int64, device=dev), torch.zeros(1, dtype=torch.int64, device=dev),
+                                torch.zeros(2, dtype=torch.int64, device=dev))
+        nflip = int(nbits_rx * ber)
+        res = dcamd.ct9_exchange(dcamd.LibCT9(L), stream, (nbits + 7) // 8, meta_tx, rcv, (nbits_rx + 7) // 8, nbits_rx,
+                                 meta_rx, crc_rx, ack, partner, nflip, 11 + rank)
+        L.decode_device(ct, rcv.data_ptr(), (nbits_rx + 7) // 8, n, out.data_ptr(), type_=t, mask17=m17, max_bytes=cap)
+        L.decode_finish()
+        torch.cuda.synchronize()
+        sp, mp_ = _shard_stream(O, xs, partner, n, ct, t, m17)
+        dp, _ = O.decompress(ct, sp, n, 1e-3, t, m17)
+        nb = (nbits_rx + 7) // 8
+        ok_stream = bool(mp_ == nbits_rx and np.array_equal(rcv[:nb].cpu().numpy(), sp[:nb]))
+        ok_dec = bool(np.array_equal(out.cpu().numpy().view(np.uint32), dp.view(np.uint32)))
+        q.put((rank, ok_stream, ok_dec, res, nflip))
+    except Exception as e:
+        q.put((rank, False, repr(e), None, None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,ber", [(2, (1 << 20) + 5, 1e-6), (2, 300007, 1e-4), (3, 100003, 1e-5)])
+def test_ct9_exchange_device(world, n, ber):
+    """BASELINE config 5 across ranks, on the GPU (ranks share cuda:0 over gloo): every received copy is
+    damaged, detected by the CRC-32 check, resent, and the received stream and its decode equal the oracle's
+    for the partner's shard bit for bit (an odd world's last rank keeps a local channel)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_ct9, args=(r, world, port, n, ber, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok_s, ok_d, r, nflip in res:
+        assert ok_s is True and ok_d is True, res
+        assert nflip > 0 and r[3] and r[0] == 2 and r[2] == 1, res
+
+
 def _worker_med(rank, world, port, kind, n, q):
     """dcamd.global_med on device shards (dc_med_shard_stats / dc_med_shard_trans / dc_med_sum_device)
     against the oracle's med_dataset_float of the whole array."""
