@@ -318,8 +318,15 @@ __device__ __forceinline__ void zero_run_check(__amdgpu_buffer_rsrc_t rs, const 
 }
 
 // One parse job (64 segments, lane = segment): the main walk, the links, the records, the token offsets.
-// Returns the job's token total (every lane).
-template <int CT, int SEG>
+// Returns the job's token total (every lane).  PUB (fused3d_kernel): the records and the decode jobs' offsets
+// are read by other CUs in the same launch, so they are stored sc1 (write-through, MI355X_MICROARCH.md
+// "Valid forms"), the offsets into frel's per-fused-job rows
+template <int SEG>
+__device__ __forceinline__ long long frel_index(long long dj) {
+    constexpr long long JPF = 4 * SEG, RELP = (4 * SEG + 31) & ~31;
+    return (dj / JPF) * RELP + dj % JPF;
+}
+template <int CT, int SEG, bool PUB = false>
 __device__ __forceinline__ uint32_t parse3_job(Ring3& r, uint16_t* recs, const uint8_t* tl, const Geo3& G,
                                                __amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t rrec,
                                                const Dec3Bufs& D3, unsigned job, uint32_t epoch, int lane P3_PARAM) {
@@ -450,11 +457,11 @@ __device__ __forceinline__ uint32_t parse3_job(Ring3& r, uint16_t* recs, const u
 #pragma unroll
         for (int i = 0; i < seg / 8; i++) {
             const u32x4 v = {w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
-            __builtin_amdgcn_raw_buffer_store_b128(v, rrec, (int)(2 * c0 + 16 * i), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rrec, (int)(2 * c0 + 16 * i), 0, PUB ? 16 : 0);
         }
         if constexpr (seg % 8 == 4) {                  // (4 chunks left: 4-chunk segments, the fused kernel's 20)
             const u32x2 v = {w[seg / 2 - 2], w[seg / 2 - 1]};
-            __builtin_amdgcn_raw_buffer_store_b64(v, rrec, (int)(2 * c0 + 16 * (seg / 8)), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(v, rrec, (int)(2 * c0 + 16 * (seg / 8)), 0, PUB ? 16 : 0);
         }
     }
 
@@ -462,7 +469,10 @@ __device__ __forceinline__ uint32_t parse3_job(Ring3& r, uint16_t* recs, const u
     const uint32_t inc = wave_incl_scan(tot, lane);
     if (lane == 63) D3.ptot[job] = inc;
     auto put_rel = [&](long long dj, uint32_t v) {
-        if (dj * 64 < D3.max_chunks) D3.rel[dj] = v;
+        if (dj * 64 < D3.max_chunks) {
+            if constexpr (PUB) __hip_atomic_store(&D3.frel[frel_index<SEG>(dj)], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else D3.rel[dj] = v;
+        }
     };
     if constexpr (64 % seg == 0) {                     // decode jobs start on segment boundaries
         if (((lane * seg) & 63) == 0) put_rel((long long)job * seg + (lane * seg) / 64, inc - tot);
@@ -1013,6 +1023,212 @@ __global__ __launch_bounds__(256, DC_D3_MINW) void fused3_kernel(const uint8_t* 
     P3_FLUSH();
 }
 
+// ------------------------------------------------------------------------------------------------
+// fused3d_kernel (DC_FUSED3=2): fused3_kernel's parse, then the decode jobs split between the parsing workgroup
+// and every other wave.  Round 5's fused3 lost its single stream read to scheduling: every workgroup decoded its
+// own fused job, so a workgroup whose parse ended late decoded late, and the launch ended in a 45-us tail with
+// fewer and fewer workgroups decoding (r05_fused3.txt: parse 46-75 us, decode 65-98 us per workgroup).  Here:
+//   parse   workgroup J parses fused job J (4 parse jobs, one per wave; J += gridDim.x when one round does not
+//           hold them) and publishes its records, the decode jobs' offsets (frel) and {its token total (ftag[J]),
+//           the tokens before its parse jobs 1..3 (fsub[J])} -- records and offsets stored sc1, every storing
+//           wave drained, one lane's sc1 granules behind the workgroup barrier (MI355X_MICROARCH.md "Valid
+//           forms", first row);
+//   static  the first DC_F3D_STATIC quarters of J's rounds of 4 decode jobs are decoded by J's own waves
+//           (jobs 4 i + w, as fused3_kernel: the records and stream words its parse just read);
+//   dynamic the remaining rounds of every fused job are tickets (one round's 4 jobs) in 8 queues (queue q: the
+//           fused jobs J = q mod 8, in order; a wave starts at its workgroup's queue blockIdx % 8 -- the blocks
+//           of one XCD -- and moves on to the others when it runs dry), so the launch ends with every wave busy.
+// A wave keeps the tokens before its last fused job and adds the totals in between (polled, epoch-tagged).
+// 8 queue heads (the guide's dequeue: one returning atomic per ticket; one head saturates near 88 per us).  The
+// launch's last wave (a done counter) zeroes the heads.  First measured with every round dynamic (r06): 210 vs
+// 195 us for parse3 + decode3 -- every wave waited for the slowest parse and paid ~2 round trips per ticket.
+constexpr int F3D_B = 4;                            // decode jobs per ticket (~4 us each at 2^26)
+#ifndef DC_F3D_STATIC
+#define DC_F3D_STATIC 3                             // quarters of a fused job's decode rounds its own workgroup takes
+#endif
+constexpr int F3D_QW = 32;                          // words between queue heads (a 128-B line each)
+template <int CT, int SEG, int CAP>
+__global__ __launch_bounds__(256, DC_D3_MINW) void fused3d_kernel(const uint8_t* __restrict__ s, Params P, Dec3Bufs D3,
+                                                                 const unsigned long long* dev_nbits,
+                                                                 unsigned long long host_nbits, float* __restrict__ out,
+                                                                 long long num, uint32_t epoch,
+                                                                 unsigned long long* __restrict__ stamps, int sq) {
+    static_assert(SEG % 4 == 0 && SEG <= 64 && F3D_B == 4, "whole region lines; a ticket = one round's 4 jobs");
+    // SR of a fused job's SEG rounds of 4 decode jobs are decoded by its own workgroup, the rest handed out
+    constexpr int JPF = 4 * SEG;
+    const int SR = SEG * sq / 4, TPF = SEG - SR;
+    struct PS { uint32_t ring[4][D3_RING * 64]; uint16_t recs[4][SEG * 64]; };
+    struct DS { uint32_t stg[4][12 * 64]; float obuf[4][CAP]; };
+    union US { PS p; DS d; };
+    __shared__ __attribute__((aligned(16))) US U;
+    __shared__ Lut3 T;
+    __shared__ uint8_t tl[512];
+    __shared__ uint32_t sj[4];
+    build_lut_len<CT>(tl, P, threadIdx.x, 256);
+    build_lut3<CT>(T, P, threadIdx.x, 256);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const Geo3 G = geo3<SEG>(dev_nbits, host_nbits);
+    const __amdgpu_buffer_rsrc_t rs = stream_rsrc(s, D3.capw);
+    const __amdgpu_buffer_rsrc_t rrec =
+        __builtin_amdgcn_make_buffer_rsrc(D3.rec, (short)0, (int)min(2 * (D3.max_chunks + 4096), 0x7FFFFF00ll), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsub = any_rsrc(D3.fsub, 0x7FFFFF00), ro = any_rsrc(out, (int)(num * 4));
+    const bool over = G.nchunks > D3.max_chunks, runs = !over && runs_mode(CT, G.nbits, num);
+    if (over) {                                                // (no ticket drawn: the heads stay zero)
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_RUNS);
+        return;
+    }
+    if (runs) {
+        zero_run_check(rs, G, num, D3.err, D3_ZMISS | D3_DECLINE | D3_WHY_RUNS);
+        const u32x4 z4 = {0u, 0u, 0u, 0u};
+        for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; 4 * i < num; i += (long long)gridDim.x * blockDim.x)
+            if (4 * i + 4 <= num) __builtin_amdgcn_raw_buffer_store_b128(z4, ro, (int)(16 * i), 0, DC_DEC3_NT ? 2 : 0);
+            else for (long long j = 4 * i; j < num; j++) out[j] = 0.0f;
+        return;
+    }
+    __syncthreads();
+    const bool chk_all = (CT == 6 && P.B >= 23) || (CT == 7 && (P.mask17 >> 16) != 0u && P.mm == 23);
+    Ring3 r;
+    r.L = U.p.ring[w];
+    r.lc = (uint32_t)lane << 2;
+    P3_DECL();
+    const long long nfj = (G.npjobs + 3) / 4;
+    const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
+    // ---- parse: fused jobs J = blockIdx.x, + gridDim.x, ... (one round when the grid holds them all), wave w
+    // taking parse job 4J + w; a parse waits only for its predecessor's exit, which a lower workgroup of the
+    // same round (or the previous round) publishes after its main walk: no wait on any decode
+    for (long long J = blockIdx.x; J < nfj; J += gridDim.x) {
+        const long long pj = 4 * J + w;
+        uint32_t tot = 0;
+        if (pj < G.npjobs)
+            tot = parse3_job<CT, SEG, true>(r, U.p.recs[w], tl, G, rs, rrec, D3, (unsigned)pj, epoch, lane P3_ARG);
+        if (lane == 0) sj[w] = tot;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this wave's records and offsets have left
+        __syncthreads();                                       // (after the last: the rings become decode buffers)
+        if (threadIdx.x == 0) {
+            const uint32_t c1 = sj[0], c2 = c1 + sj[1], c3 = c2 + sj[2];
+            const u32x4 v = {epoch, c1, c2, c3};
+            __builtin_amdgcn_raw_buffer_store_b128(v, rsub, (int)(16 * J), 0, 16);   // sc1 granule
+            st_relaxed(&D3.ftag[J], ((uint64_t)epoch << 32) | (c3 + sj[3]));
+        }
+        __syncthreads();                                       // (sj is rewritten by the next round)
+    }
+    const unsigned long long ts1 = __builtin_amdgcn_s_memrealtime();
+    // ---- the tokens before fused job J (polled totals; a wave keeps the sum for its last fused job Jc)
+    long long Jc = 0;
+    unsigned long long pc = 0;
+    bool bad = false;
+    auto prefix_to = [&](long long J2) {
+        if (J2 < Jc) { Jc = 0; pc = 0; }
+        if (J2 > Jc) {
+            unsigned long long acc = 0;
+            for (long long k = Jc + lane; k < J2; k += 64) {
+                const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
+                uint64_t v;
+                while (((v = ld_relaxed(&D3.ftag[k])) >> 32) != (uint64_t)epoch) {
+                    if (__builtin_amdgcn_s_memrealtime() - w0 > D3_LINK_WAIT) { bad = true; break; }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                acc += (uint32_t)v;
+            }
+            pc += wave_sum64(acc);
+            Jc = J2;
+        }
+    };
+    // the tokens before each parse job of J2 (lane 0 polls J2's granule), wave-uniform
+    auto subs = [&](long long J2, uint32_t (&c)[4]) {
+        uint32_t c1 = 0, c2 = 0, c3 = 0;
+        if (lane == 0) {
+            const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
+            u32x4 v;
+            while ((v = __builtin_amdgcn_raw_buffer_load_b128(rsub, (int)(16 * J2), 0, 16)).x != epoch) {
+                if (__builtin_amdgcn_s_memrealtime() - w0 > D3_LINK_WAIT) { bad = true; break; }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            c1 = v.y; c2 = v.z; c3 = v.w;
+        }
+        c[0] = 0u;
+        c[1] = (uint32_t)__builtin_amdgcn_readfirstlane((int)c1);
+        c[2] = (uint32_t)__builtin_amdgcn_readfirstlane((int)c2);
+        c[3] = (uint32_t)__builtin_amdgcn_readfirstlane((int)c3);
+    };
+    auto job = [&](long long J2, long long dj, const uint32_t (&c)[4]) {
+        const long long g = dj * 64 + lane;
+        Pre3 cur;
+        cur.rc = __builtin_amdgcn_raw_buffer_load_b16(rrec, g < G.nchunks ? (int)(2 * g) : D3_OOB, 0, 16);
+        cur.rl = __hip_atomic_load(&D3.frel[frel_index<SEG>(dj)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        cur.v0 = load_raw4(rs, 8 * g);
+        cur.v1 = load_raw4(rs, 8 * g + 4);
+        cur.v2 = load_raw4(rs, 8 * g + 8);
+        const int pi = (int)((dj - JPF * J2) / SEG);
+        const unsigned long long base = pc + (pi == 0 ? 0u : pi == 1 ? c[1] : pi == 2 ? c[2] : c[3]) + cur.rl;
+        decode3_job<CT, CAP>(T, U.d.stg[w], U.d.obuf[w], G, rs, ro, chk_all, D3, cur, (unsigned)dj, base, out, num,
+                             epoch, lane P3_ARG);
+    };
+    // ---- static part: the workgroup's own fused jobs, decode jobs 4 i + w of rounds i < SR, as fused3_kernel
+    // (their records and stream words fresh from this workgroup's parse, no ticket)
+    for (long long J2 = blockIdx.x; J2 < nfj && !bad; J2 += gridDim.x) {
+        prefix_to(J2);
+        uint32_t c[4];
+        subs(J2, c);
+        if (__any(bad)) { bad = true; break; }
+        for (int i = 0; i < SR; i++) {
+            const long long dj = JPF * J2 + 4 * i + w;
+            if (dj >= G.ndjobs) break;
+            job(J2, dj, c);
+        }
+    }
+    // ---- dynamic part: the rounds i >= SR of every fused job, as tickets of F3D_B decode jobs (one round's
+    // four); queue q holds the fused jobs q, q + 8, ... (TPF tickets each)
+    auto ntk = [&](int q) -> unsigned { return q < nfj ? (unsigned)(((nfj - q + 7) / 8) * TPF) : 0u; };
+    auto deq = [&](int q) -> unsigned {
+        unsigned t = 0;
+        if (lane == 0) t = __hip_atomic_fetch_add(&D3.fq[F3D_QW * q], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return (unsigned)__builtin_amdgcn_readfirstlane((int)t);
+    };
+    unsigned qdone = 0;
+    int q = (int)(blockIdx.x & 7);
+    unsigned t = deq(q);
+    bad = __any(bad);
+    while (!bad) {
+        if (t >= ntk(q)) {                                     // queue q has run dry: the next one
+            qdone |= 1u << q;
+            if (qdone == 0xFFu) break;
+            do { q = (q + 1) & 7; } while ((qdone >> q) & 1u);
+            t = deq(q);
+            continue;
+        }
+        const long long J2 = q + 8ll * (t / TPF);
+        const long long dj0 = JPF * J2 + 4ll * SR + (long long)F3D_B * (t % TPF);
+        const unsigned tn = deq(q);                            // the next ticket
+        prefix_to(J2);
+        uint32_t c[4];
+        subs(J2, c);
+        bad = __any(bad);
+        if (bad) break;
+        for (int b = 0; b < F3D_B; b++) {
+            const long long dj = dj0 + b;
+            if (dj >= G.ndjobs) break;
+            job(J2, dj, c);
+        }
+        t = tn;
+    }
+    if (bad && lane == 0) atomicOr(D3.err, D3_DECLINE | D3_WHY_LINK);
+    if (stamps && lane == 0) {                                 // per wave: start, parse end, decode end
+        stamps[16 * blockIdx.x + 4 * w] = ts0; stamps[16 * blockIdx.x + 4 * w + 1] = ts1;
+        stamps[16 * blockIdx.x + 4 * w + 2] = __builtin_amdgcn_s_memrealtime();
+    }
+    // ---- the launch's last wave zeroes the queue heads for the next launch (every wave of the grid gets here
+    // once, after its last draw)
+    if (lane == 0) {
+        const unsigned d = __hip_atomic_fetch_add(&D3.fq[F3D_QW * 8], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (d == 4u * gridDim.x - 1u) {
+#pragma unroll
+            for (int k = 0; k <= 8; k++) __hip_atomic_store(&D3.fq[F3D_QW * k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    P3_FLUSH();
+}
+
 // A shard's first pending tokens (D3.spend[0] of its first chunk, which starts at stream bit 0), decoded
 // again from the three values before the shard (hin: b1, b2, b3 = the previous shard's last three values,
 // last first), one token after another as impl/dataCompression.c:1900-2027 reads them.
@@ -1251,13 +1467,14 @@ static unsigned long long* g_f3_stamps = nullptr;
 static long long g_f3_nfj = 0;
 static int g_f3_on = -1;
 static int fused3_on() {
-    if (g_f3_on < 0) { const char* e = getenv("DC_FUSED3"); g_f3_on = (e && *e == '1') ? 1 : 0; }
+    if (g_f3_on < 0) { const char* e = getenv("DC_FUSED3"); g_f3_on = (e && (*e == '1' || *e == '2')) ? *e - '0' : 0; }
     return g_f3_on;
 }
-// tests / experiments: 1 selects fused3_kernel, 0 the two launches; returns the previous setting
+// tests / experiments: 1 selects fused3_kernel, 2 fused3d_kernel (dynamic decode jobs), 0 the two launches;
+// returns the previous setting
 extern "C" int dc_set_fused3(int on) {
     const int old = fused3_on();
-    g_f3_on = on ? 1 : 0;
+    g_f3_on = (on == 1 || on == 2) ? on : 0;
     return old;
 }
 static int g_f3_seg = 0;
@@ -1267,10 +1484,14 @@ extern "C" void dc_decode3_size_hint(long long max_chunks, long long nchunks) {
     g_f3_hint_nch = nchunks;
 }
 static int launch_fused3(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
-                         const Params* P, const Dec3Bufs* D3, float* out, long long num, uint32_t epoch, hipStream_t st) {
-    const void* fp = P->ct == 5 ? (const void*)fused3_kernel<5, 16, D3_CAP> : P->ct == 6 ? (const void*)fused3_kernel<6, 16, D3_CAP>
-                   : P->ct == 7 ? (const void*)fused3_kernel<7, 16, D3_CAP> : (const void*)fused3_kernel<11, 16, D3_CAP>;
-    static int res[12];
+                         const Params* P, const Dec3Bufs* D3, float* out, long long num, uint32_t epoch, int dyn,
+                         hipStream_t st) {
+    const void* fp = dyn ? (P->ct == 5 ? (const void*)fused3d_kernel<5, 16, D3_CAP> : P->ct == 6 ? (const void*)fused3d_kernel<6, 16, D3_CAP>
+                            : P->ct == 7 ? (const void*)fused3d_kernel<7, 16, D3_CAP> : (const void*)fused3d_kernel<11, 16, D3_CAP>)
+                         : (P->ct == 5 ? (const void*)fused3_kernel<5, 16, D3_CAP> : P->ct == 6 ? (const void*)fused3_kernel<6, 16, D3_CAP>
+                            : P->ct == 7 ? (const void*)fused3_kernel<7, 16, D3_CAP> : (const void*)fused3_kernel<11, 16, D3_CAP>);
+    static int resv[2][12];
+    int* res = resv[dyn ? 1 : 0];
     const int ci = P->ct;
     if (!res[ci]) res[ci] = resident3(fp, 256);             // (the same registers and LDS for every SEG)
     // the segment length by a model of the launch (fused jobs in rounds of res[ci] workgroups; per round a job's
@@ -1285,7 +1506,10 @@ static int launch_fused3(const uint8_t* s, const unsigned long long* dev_nbits, 
     double best = 1e30;
     for (int sg : {16, 20, 24, 32, 64}) {
         const long long fj = (((nch + sg - 1) / sg + 63) / 64 + 3) / 4;
-        const double t = (double)((fj + res[ci] - 1) / res[ci]) * (2.35 * (sg / 4 + 1) * 4 + 4.4 * sg + 10.0);
+        // (dynamic decode: the decode work is spread over every wave, so the shortest segment whose parse is one
+        // round wins -- the parse walk is the part no other workgroup can take over)
+        const double t = dyn ? (fj <= res[ci] ? (double)sg : 1e6 + sg)
+                             : (double)((fj + res[ci] - 1) / res[ci]) * (2.35 * (sg / 4 + 1) * 4 + 4.4 * sg + 10.0);
         if (t < best) { best = t; seg = sg; }
     }
     if (const char* e = getenv("DC_FUSED3_SEG")) {
@@ -1295,18 +1519,28 @@ static int launch_fused3(const uint8_t* s, const unsigned long long* dev_nbits, 
     g_f3_seg = seg;
     const long long maxpj = ((D3->max_chunks + seg - 1) / seg + 63) / 64, nfj = (maxpj + 3) / 4;
     const int grid = (int)std::max<long long>(1, std::min<long long>(nfj, res[ci]));
+    static int sq = -1;                                    // fused3d: quarters of the rounds decoded statically
+    if (sq < 0) {
+        const char* e = getenv("DC_F3D_STATIC");
+        sq = (e && *e >= '0' && *e <= '4') ? *e - '0' : DC_F3D_STATIC;
+    }
     unsigned long long* stamps = nullptr;
-    if (getenv("DC_FUSED3_STAMPS")) {
-        if (nfj > g_f3_nfj) {
+    if (getenv("DC_FUSED3_STAMPS")) {                      // (fused3d: 16 words per workgroup, 4 per wave)
+        const long long nst = dyn ? 4 * (long long)grid : nfj;
+        if (nst > g_f3_nfj) {
             if (g_f3_stamps) (void)hipFree(g_f3_stamps);
-            if (hipMalloc((void**)&g_f3_stamps, (size_t)nfj * 4 * 8) != hipSuccess) return -1;
-            g_f3_nfj = nfj;
+            if (hipMalloc((void**)&g_f3_stamps, (size_t)nst * 4 * 8) != hipSuccess) return -1;
+            g_f3_nfj = nst;
         }
         stamps = g_f3_stamps;
         (void)hipMemsetAsync(stamps, 0, (size_t)g_f3_nfj * 4 * 8, st);
     }
-#define F3L(C, S) hipLaunchKernelGGL(HIP_KERNEL_NAME(fused3_kernel<C, S, D3_CAP>), dim3(grid), dim3(256), 0, st, s, *P, \
-                                     *D3, dev_nbits, host_nbits, out, num, epoch, stamps)
+#define F3L(C, S) do {                                                                               \
+        if (dyn) hipLaunchKernelGGL(HIP_KERNEL_NAME(fused3d_kernel<C, S, D3_CAP>), dim3(grid), dim3(256), 0, st, s, \
+                                    *P, *D3, dev_nbits, host_nbits, out, num, epoch, stamps, sq);    \
+        else hipLaunchKernelGGL(HIP_KERNEL_NAME(fused3_kernel<C, S, D3_CAP>), dim3(grid), dim3(256), 0, st, s, *P, \
+                                *D3, dev_nbits, host_nbits, out, num, epoch, stamps);                \
+    } while (0)
 #define F3C(C)                                                                                       \
     do {                                                                                             \
         if (seg == 16) F3L(C, 16);                                                                   \
@@ -1348,7 +1582,7 @@ extern "C" int dc_launch_decode3(const uint8_t* s, const unsigned long long* dev
     if (g_f3_last) {
         dc_mark_phase(4, st);
         dc_mark_phase(5, st);                   // (the timing slots: an empty parse, the launch as decode's)
-        if (launch_fused3(s, dev_nbits, host_nbits, P, D3, out, num, epoch, st)) return -2;
+        if (launch_fused3(s, dev_nbits, host_nbits, P, D3, out, num, epoch, fused3_on() == 2, st)) return -2;
         dbg_wait("fused3_kernel", st);
         dc_mark_phase(7, st);
         dc_mark_next_set();

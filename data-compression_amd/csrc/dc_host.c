@@ -715,6 +715,7 @@ static int dec_next_epoch(void) {
             HIPCHK(hipMemsetAsync(G.D3.pexit, 0, (size_t)(G.dec3_cap + 4096) / 256 * 8 + 64 * 8, G.st));
             HIPCHK(hipMemsetAsync(G.D3.hist, 0, (size_t)((G.dec3_cap + 4096) / 64 + 64) * 3 * 8, G.st));
             HIPCHK(hipMemsetAsync(G.D3.ftag, 0, (size_t)((G.dec3_cap + 4096) / 256 + 64) * 8, G.st));
+            HIPCHK(hipMemsetAsync(G.D3.fsub, 0, (size_t)((G.dec3_cap + 4096) / 256 + 64) * 16, G.st));
         }
         G.dec_epoch = 1;
     }
@@ -733,7 +734,7 @@ static int dec3_ensure(long long max_chunks, int B, int ct) {
         G.sh3_ok = 0;                         /* a pending shard fix would read the freed spend/rec */
         const long long C = max_chunks + 4096;
         const long long DJ = C / 64 + 64, PJ = C / (64 * 4) + 64;
-        size_t sz[7], off = 0, tot = 0;
+        size_t sz[10], off = 0, tot = 0;
         sz[0] = (size_t)C * 2;                /* rec */
         sz[1] = (size_t)DJ * 4;               /* rel */
         sz[2] = (size_t)PJ * 4;               /* ptot */
@@ -741,12 +742,15 @@ static int dec3_ensure(long long max_chunks, int B, int ct) {
         sz[4] = (size_t)DJ * 3 * 8;           /* hist */
         sz[5] = 256;                          /* spend */
         sz[6] = (size_t)PJ * 8;               /* ftag */
-        for (int i = 0; i < 7; i++) tot += (sz[i] + 255) & ~(size_t)255;
+        sz[7] = (size_t)DJ * 4 * 2 + 4096;    /* frel (fused jobs of >= 16-chunk segments: < 1.5x rel) */
+        sz[8] = (size_t)PJ * 16;              /* fsub */
+        sz[9] = 4096;                         /* fq */
+        for (int i = 0; i < 10; i++) tot += (sz[i] + 255) & ~(size_t)255;
         HIPCHK(hipMalloc(&G.dec3_pool, tot));
         HIPCHK(hipMemsetAsync(G.dec3_pool, 0, tot, G.st));
         char* b = (char*)G.dec3_pool;
-        void* ptr[7];
-        for (int i = 0; i < 7; i++) { ptr[i] = b + off; off += (sz[i] + 255) & ~(size_t)255; }
+        void* ptr[10];
+        for (int i = 0; i < 10; i++) { ptr[i] = b + off; off += (sz[i] + 255) & ~(size_t)255; }
         G.D3.rec = (uint16_t*)ptr[0];
         G.D3.rel = (uint32_t*)ptr[1];
         G.D3.ptot = (uint32_t*)ptr[2];
@@ -754,6 +758,9 @@ static int dec3_ensure(long long max_chunks, int B, int ct) {
         G.D3.hist = (uint64_t*)ptr[4];
         G.D3.spend = (uint32_t*)ptr[5];
         G.D3.ftag = (uint64_t*)ptr[6];
+        G.D3.frel = (uint32_t*)ptr[7];
+        G.D3.fsub = (uint32_t*)ptr[8];
+        G.D3.fq = (unsigned*)ptr[9];
         G.dec3_cap = max_chunks;
     }
     G.D3.max_chunks = max_chunks;

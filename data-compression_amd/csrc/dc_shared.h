@@ -91,6 +91,12 @@ typedef struct Dec3Bufs {
                                       whole stream) */
     uint32_t* spend;               /* [0] tokens of the shard's first chunk that wait for those values */
     uint64_t* ftag;                /* [fused job = 4 parse jobs] epoch << 32 | tokens (fused3_kernel) */
+    uint32_t* frel;                /* fused3d_kernel: rel by fused job, (4 SEG + 31) & ~31 words each (no
+                                      128-B line shared by two fused jobs: they are handed to other CUs) */
+    uint32_t* fsub;                /* fused3d_kernel: [fused job] 16-B granule {epoch, tokens before its parse
+                                      jobs 1, 2, 3} */
+    unsigned* fq;                  /* fused3d_kernel: 8 decode-job queue heads + a done counter, 128 B apart
+                                      (zero between launches: the launch's last wave resets them) */
 } Dec3Bufs;
 
 #ifdef __cplusplus

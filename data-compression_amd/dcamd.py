@@ -493,8 +493,9 @@ class Lib:
         return int(self.L.dc_set_decode3_seg(int(seg)))
 
     def set_fused3(self, on):
-        """1: decode 16-chunk-segment streams with the single-launch parse + decode (fused3_kernel), 0: with
-        parse3 + decode3 (the default); returns the previous setting."""
+        """1: decode 16-chunk-segment streams with the single-launch parse + decode (fused3_kernel), 2: its
+        dynamic form (fused3d_kernel, decode jobs from 8 queues), 0: with parse3 + decode3 (the default); returns
+        the previous setting."""
         return int(self.L.dc_set_fused3(int(on)))
 
     def last_decode_fused(self):

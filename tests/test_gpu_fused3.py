@@ -1,5 +1,6 @@
-"""GPU parity of the single-launch parse + decode (fused3_kernel, csrc/dc_decode3.hip):
-switched on (dc_set_fused3) for 16-chunk-segment streams, every segment length it can take (16, 20, 24, 32,
+"""GPU parity of the single-launch parse + decode (fused3_kernel, csrc/dc_decode3.hip) and of
+its dynamic form (fused3d_kernel: decode jobs handed out from 8 queues, records handed to other CUs in the launch;
+mode 2): switched on (dc_set_fused3) for 16-chunk-segment streams, every segment length it can take (16, 20, 24, 32,
 64 chunks) must decode bit for bit as the oracle's grammar decoder, from host and device bit counts, for the
 golden streams, ragged sizes, prediction-heavy streams and the zero-run streams it fills itself."""
 import os
@@ -15,11 +16,11 @@ CTS = [5, 6, 7, 11]
 SEGS = [16, 20, 24, 32, 64]
 
 
-@pytest.fixture
-def f3(dc):
+@pytest.fixture(params=[1, 2], ids=["static", "dynamic"])
+def f3(dc, request):
     old_min = dc.set_decode3_min_bytes(0)         # every stream through the segment decoder ...
     old_seg = dc.set_decode3_seg(16)               # ... with 16-chunk segments: the fused launch's streams
-    old_f = dc.set_fused3(1)
+    old_f = dc.set_fused3(request.param)
     dc.L.dc_set_decode3_maps(-1)                   # (no parameters remembered for the maps parse or dense buffer)
     yield dc
     dc.set_fused3(old_f)
@@ -118,13 +119,14 @@ def test_fused3_zero_runs(f3, oracle, ct, n, kind):
         assert not f3.last_decode_was_v3()
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("ct", CTS)
 @pytest.mark.parametrize("log2n", [22, 24])
-def test_fused3_device_chain(dc, oracle, ct, log2n):
+def test_fused3_device_chain(dc, oracle, ct, log2n, mode):
     """encode_device -> decode_device with the bit count on the device (the bench's path, default thresholds,
     the fused launch switched on; its segment length from the stream's capacity) equals the oracle."""
     import torch
-    old = dc.set_fused3(1)
+    old = dc.set_fused3(mode)
     try:
         n = 1 << log2n
         dc.set_bound(1e-3)
@@ -150,11 +152,13 @@ def test_fused3_device_chain(dc, oracle, ct, log2n):
         dc.set_fused3(old)
 
 
-def test_fused3_bench_size(dc, oracle):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_fused3_bench_size(dc, oracle, mode):
     """The bench's workload (CT7, U10 2^26, bound 1e-3, host bit count: the model picks the segment length)
-    through the fused launch, back to back twice (epochs), against the oracle."""
+    through the fused launch, back to back twice (epochs; fused3d: its queue heads reset between launches),
+    against the oracle."""
     import torch
-    old = dc.set_fused3(1)
+    old = dc.set_fused3(mode)
     try:
         n = 1 << 26
         dc.set_bound(1e-3)
@@ -165,7 +169,7 @@ def test_fused3_bench_size(dc, oracle):
         d_s = torch.from_numpy(np.concatenate([s, np.zeros(64, np.uint8)])).cuda()
         out = torch.empty(n, dtype=torch.float32, device="cuda")
         torch.cuda.synchronize()
-        for _ in range(2):
+        for _ in range(3):
             out.fill_(-1.0)
             dc.decode_device(7, d_s.data_ptr(), nb, n, out.data_ptr(), type_=t, mask17=m17, max_bytes=d_s.numel())
             dc.decode_finish()

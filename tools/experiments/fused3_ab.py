@@ -33,6 +33,9 @@ L.set_decode3_seg(16)
 
 
 ENC = "enc" in sys.argv[3:]          # re-encode before every decode (the bench's step: the stream fresh)
+MODE = 2 if "dyn" in sys.argv[3:] else 1   # dyn: fused3d_kernel (dynamic decode jobs)
+if "seg20" in sys.argv[3:]:
+    L.set_decode3_seg(20)
 
 
 def run(fused, K=20):
@@ -65,18 +68,26 @@ def run(fused, K=20):
 
 us2, s2, v2, ref = run(0)
 print(f"2^{lg} ct{ct}: parse3 + decode3 {us2:.1f} us per decode, status 0x{s2:x}, v3 {v2}", flush=True)
-us1, s1, v1, out = run(1)
-print(f"2^{lg} ct{ct}: fused3_kernel   {us1:.1f} us per decode, status 0x{s1:x}, v3 {v1}, "
+us1, s1, v1, out = run(MODE)
+print(f"2^{lg} ct{ct}: {'fused3d_kernel' if MODE == 2 else 'fused3_kernel'}   {us1:.1f} us per decode, status 0x{s1:x}, v3 {v1}, "
       f"bit-exact vs two launches {bool(torch.equal(out.view(torch.int32), ref.view(torch.int32)))}", flush=True)
 us2b, _, _, _ = run(0)
 print(f"2^{lg} ct{ct}: parse3 + decode3 again {us2b:.1f} us", flush=True)
 nfj = 1 << 20
-L.set_fused3(1)
+L.set_fused3(MODE)
 L.decode_device(ct, st.data_ptr(), nb, n, ref.data_ptr(), type_=t, mask17=m17, max_bytes=cap)
 L.decode_finish()
 S = L.fused3_stamps(nfj).astype(np.int64)
 L.set_fused3(0)
 print(f"fused segment length {L.L.dc_fused3_last_seg()} chunks", flush=True)
+if MODE == 2:                                     # per wave: start, parse end, decode end
+    S = S[S[:, 2] > 0]
+    t0 = S[:, 0].min()
+    par, dec, end = (S[:, 1] - S[:, 0]) * 0.01, (S[:, 2] - S[:, 1]) * 0.01, (S[:, 2] - t0) * 0.01
+    print(f"waves {len(S)}: parse {par.mean():.1f} us (min {par.min():.1f}, max {par.max():.1f}), decode "
+          f"{dec.mean():.1f} (min {dec.min():.1f}, max {dec.max():.1f}); wave end min {end.min():.1f} "
+          f"median {np.median(end):.1f} max {end.max():.1f} us", flush=True)
+    sys.exit(0)
 used = S[:, 3] > 0
 S = S[used]
 if len(S):
