@@ -413,12 +413,11 @@ class Ctx:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
-        # several ranks on one GPU (the gloo rehearsal): a tile of the single-pass encoder can wait past its 20 ms
-        # bound while another process holds the CUs, so the ranks encode with the wait-free three-launch
-        # variant (one process per GPU -- the real multi-GPU run -- keeps the single pass)
+        # several ranks on one GPU (the gloo rehearsal).  Until r05 they encoded with the wait-free three-launch
+        # variant: a single-pass tile could wait past its bound for a predecessor left undispatched behind another
+        # process's waiting waves.  Since r06 a tile computes a late predecessor's count itself (dc_encode.hip
+        # enc_lookback's help), so every rank keeps the single pass (DC_ENC_PASSES still selects another)
         self.shared_gpu = self.world > max(torch.cuda.device_count(), 1)
-        if self.shared_gpu:
-            os.environ.setdefault("DC_ENC_PASSES", "3")
         self.dist = None
         if self.world > 1:
             import torch.distributed as dist
@@ -979,7 +978,8 @@ def main():
                                f"absErrorBound={args.bound:g}", "floats_per_gpu": n, "ct": ct,
                    "stream_bytes": int(nbytes), "ratio": main_line["ratio"], "type": W["type"],
                    "mask17": f"{W['mask17']:05x}", "parallelism": f"dp{C.world}",
-                   "encoder": ("three-launch (ranks share a GPU)" if C.shared_gpu else "single pass")},
+                   "encoder": {1: "single pass", 2: "count + pack", 3: "three-launch"}.get(R.get("enc_mode", 1), "?")
+                              + (" (ranks share a GPU)" if C.shared_gpu else "")},
         "roofline": {"bound": "hbm", "kernel": dname, "achieved": main_line["dominant"]["achieved_GBs"],
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": main_line["dominant"]["frac"],
                      "traffic": traffic, "traffic_source": traffic_src,

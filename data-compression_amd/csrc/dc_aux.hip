@@ -2066,6 +2066,26 @@ extern "C" int dc_launch_extract_shard(const uint8_t* g, long long g_bytes, cons
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// Co-residency tests (dc_occupy_device): `blocks` workgroups of 256 threads, `lds` bytes of LDS each, that stay
+// resident for `ticks` of s_memrealtime (every wave leaves by then) -- a neighbour occupying CU slots while the
+// codec runs on another stream
+__global__ __launch_bounds__(256) void occupy_kernel(unsigned long long ticks, unsigned* __restrict__ sink) {
+    extern __shared__ uint32_t occ_lds[];
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned acc = threadIdx.x;
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) {
+        acc = acc * 1664525u + 1013904223u;
+        __builtin_amdgcn_s_sleep(8);
+    }
+    if (acc == 0x9E3779B9u) { occ_lds[0] = acc; sink[0] = occ_lds[threadIdx.x & 7]; }
+}
+extern "C" int dc_launch_occupy(double us, int blocks, int lds, unsigned* sink, hipStream_t st) {
+    if (blocks < 1 || us < 0.0 || us > 1.0e6 || lds < 0 || lds > 160 * 1024) return -2;
+    hipLaunchKernelGGL(occupy_kernel, dim3((unsigned)blocks), dim3(256), (size_t)lds, st,
+                       (unsigned long long)(us * 100.0), sink);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // Himeno halo planes: the plane ijk = 1/2/3 at index v of a [mi][mj][mk] float array in
 // the order of transform_3d_array_to_1d_array (impl/dataCompression.c:3741-3775), gathered into a
 // contiguous array; and the decoded plane + min scattered back (impl/himenoBMTxps.c:699-706).

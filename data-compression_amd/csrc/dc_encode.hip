@@ -608,7 +608,9 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
         const uint32_t cur = i < tw ? sb[i] : 0u;                      // (stale past the tile's bits)
         const uint32_t prev = i ? sb[i - 1] : tp0;
         const uint32_t w = sh ? __builtin_amdgcn_alignbit(prev, cur, sh) : cur;
-#if DC_PACK_NT
+#if defined(DC_ENC_DIAG_NOSTORE)
+        if (w == 0x9E3779B9u && i == 12345) out[W0 + i] = 0u;         // (diagnostic build: the words are made, not stored)
+#elif DC_PACK_NT
         __builtin_nontemporal_store(__builtin_bswap32(w), out + W0 + i);
 #else
         out[W0 + i] = __builtin_bswap32(w);
@@ -654,13 +656,28 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
 #define DC_LB_SLEEP 1
 #endif
 static_assert(DC_LB_K <= 8 && DC_LB_KS <= 8, "look-back windows read at most LB_PAD words before tile 0");
-static_assert(!DC_LB_DMA || DC_LB_KS <= 4, "the LDS window holds 256 predecessors");
+static_assert(!DC_LB_DMA || DC_LB_KS <= 8, "the LDS window holds at most 512 predecessors");
 constexpr long long LB_PAD = 512;                                 // readable words in front of the tile states
 constexpr int LB_KW = DC_LB_K;                                    // look-back: tiles per lane per round trip
 constexpr unsigned long long ST_VAL = (1ull << 40) - 1;
 constexpr unsigned long long ST_MASK = 3ull << 40, ST_AGG = 1ull << 40, ST_INC = 2ull << 40, ST_BAD = 3ull << 40;
 constexpr uint32_t ST_TAGM = (1u << 22) - 1;
 constexpr unsigned long long LB_WAIT = 2000000ull;                // s_memrealtime ticks (100 MHz): 20 ms
+// A wait gives up only when BOTH its wall time exceeds LB_WAIT AND the waiting lane has polled LB_POLLS times
+// (r06): the r05 rehearsal with three processes on one GPU ended with encoder status 4 although no tile can wait
+// for a later one -- a queue preempted by the other processes' queues (compute wave save / restore) stops every
+// wave of the launch, and the wall clock a restored wave reads then jumps past the bound.  A preempted wave does
+// not poll, so a count of polls (each >= 1 state round trip, ~1 us) measures the time it actually waited; a
+// true deadlock still ends after max(20 ms, LB_POLLS polls) and takes the exact three-launch fallback.
+constexpr unsigned LB_POLLS = 8192;
+struct WaitBound {
+    unsigned long long t0;
+    unsigned polls;
+    __device__ __forceinline__ void start() { t0 = __builtin_amdgcn_s_memrealtime(); polls = 0; }
+    __device__ __forceinline__ bool expired() {           // call once per poll
+        return ++polls >= LB_POLLS && __builtin_amdgcn_s_memrealtime() - t0 > LB_WAIT;
+    }
+};
 
 __device__ __forceinline__ uint64_t st_word(uint32_t tag, unsigned long long status, unsigned long long v) {
     return ((uint64_t)tag << 42) | status | (v & ST_VAL);
@@ -669,6 +686,49 @@ __device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
     return v;
+}
+
+// The help of a waiting tile (enc_lookback): tile ti's bit count computed by one wave from x (lane = 64 floats,
+// token_len_t: the length decision of make_token_t), and the tile's last 31 bits (its last 16 tokens, one lane)
+// -- exactly what the tile itself publishes.
+template <int CT>
+__device__ unsigned long long help_tile_bits(const float* __restrict__ x, long long n, long long idx0, const Params& P,
+                                             const uint16_t* tab, long long ti) {
+    const int lane = threadIdx.x & 63;
+    const long long e0 = ti * ENC_TILE + 64ll * lane;
+    float b[3];
+#pragma unroll
+    for (int k = 1; k <= 3; k++) {
+        const long long e = e0 - k;
+        b[k - 1] = (e < n && e >= -3 && idx0 + e >= 0) ? x[e] : 0.0f;
+    }
+    float b1 = b[0], b2 = b[1], b3 = b[2];
+    unsigned long long bits = 0;
+    for (int j = 0; j < 64; j++) {
+        const long long e = e0 + j;
+        if (e >= n) break;
+        const float v = x[e];
+        bits += (unsigned)token_len_t<CT>(v, b1, b2, b3, idx0 + e >= 3, P, tab);
+        b3 = b2; b2 = b1; b1 = v;
+    }
+    return wave_sum64(bits);
+}
+template <int CT>
+__device__ uint32_t help_tile_tail(const float* __restrict__ x, long long idx0, const Params& P, const uint16_t* tab,
+                                   long long ti) {                        // (a full tile: ti + 1 < ntiles)
+    const long long e0 = (ti + 1) * ENC_TILE - ENC_K;
+    float b1 = x[e0 - 1], b2 = x[e0 - 2], b3 = x[e0 - 3];
+    unsigned long long acc = 0;
+    for (int j = 0; j < ENC_K; j++) {
+        const long long e = e0 + j;
+        const float v = x[e];
+        uint32_t tv;
+        int len;
+        make_token_t<CT>(v, b1, b2, b3, idx0 + e >= 3, P, tab, tv, len);
+        acc = (acc << len) | tv;
+        b3 = b2; b2 = b1; b1 = v;
+    }
+    return (uint32_t)acc & 0x7FFFFFFFu;
 }
 
 // exclusive bit offset of tile t >= 1 (one whole wave; wave-uniform result).  Position p = 64 k + l of the
@@ -683,15 +743,29 @@ __device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
 // lb_dma below); a state it saw unpublished is polled and the window read again as usual.
 // vr (optional): the first window as loaded earlier into registers (vr[k] = lane's k-th state,
 // ld_relaxed(st + t - 1 - lane - 64 k), encode_pipe_kernel).
-template <int LB_K>
+// help (r06): a callable help(ti) -> the bit count of tile ti, computed by this wave from x, or ~0 for no help.
+// A state still unpublished after HELP_POLLS polls is computed and published (CAS from the value seen) by the
+// waiting tile itself: its forward progress then depends on no other workgroup being scheduled -- with other
+// processes' look-back kernels on the same GPU, a predecessor's workgroup can stay undispatched on its XCD
+// behind their waiting waves while this one holds a slot of another XCD (r05f: three ranks on one GPU, encoder
+// status 4).  The value is the one the owner publishes, so a late owner's store is harmless.
+#ifndef DC_HELP_POLLS
+#define DC_HELP_POLLS 256                       // (tests build 0: every unpublished state helped at once)
+#endif
+constexpr unsigned HELP_POLLS = DC_HELP_POLLS;
+struct NoHelp {
+    __device__ __forceinline__ unsigned long long operator()(long long) const { return ~0ull; }
+};
+template <int LB_K, class Help = NoHelp>
 __device__ __forceinline__ int enc_lookback(const uint64_t* __restrict__ st, long long t, uint32_t tag,
                                             unsigned long long& excl, uint32_t& stat, int start_bit,
                                             const uint64_t* lw0 = nullptr, long long s0 = 0,
-                                            const uint64_t* vr = nullptr) {
+                                            const uint64_t* vr = nullptr, Help help = Help()) {
     const int lane = threadIdx.x & 63;
     long long base = t - 1;
     excl = 0;
-    const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
+    WaitBound wb;
+    wb.start();
     bool first = lw0 != nullptr || vr != nullptr;
     for (;;) {
         uint64_t v[LB_K];
@@ -721,17 +795,28 @@ __device__ __forceinline__ int enc_lookback(const uint64_t* __restrict__ st, lon
             // past it)
             if (pinv >= pinc) break;
             stat++;
+            bool gone = false, stuck = false;
+            uint64_t seen = 0;
+            const long long ti = base - pinv;
             if (lane == (pinv & 63)) {                                    // its lane polls it alone
-                const long long ti = base - pinv;
-                for (;;) {
+                for (unsigned k = 0;; k++) {
                     const uint64_t w = ld_relaxed(st + ti);
                     if ((uint32_t)(w >> 42) == tag && (w & ST_MASK) != 0) break;
-                    if (__builtin_amdgcn_s_memrealtime() - w0 > LB_WAIT) break;
+                    if (k >= HELP_POLLS) { stuck = true; seen = w; break; }
+                    if (wb.expired()) { gone = true; break; }
                     stat += 1u << 16;
                     __builtin_amdgcn_s_sleep(DC_LB_SLEEP);
                 }
             }
-            if (__builtin_amdgcn_s_memrealtime() - w0 > LB_WAIT) return 1;
+            if (__any(gone)) return 1;
+            if (__any(stuck)) {                                           // compute the late tile's count here
+                const unsigned long long b = help(ti);
+                if (b != ~0ull && lane == (pinv & 63))
+                    atomicCAS(reinterpret_cast<unsigned long long*>(const_cast<uint64_t*>(st + ti)),
+                              (unsigned long long)seen, (unsigned long long)st_word(tag, ST_AGG, b));
+                stat += 1u << 28;
+                if (b == ~0ull && wb.expired()) return 1;
+            }
         }
         unsigned long long s = 0;
         bool bad = false;
@@ -754,9 +839,9 @@ __device__ __forceinline__ int enc_lookback(const uint64_t* __restrict__ st, lon
 // ~3 us round trip of state loads under the stream then overlaps the pack.  Lane l of load m brings
 // states s0 + 128 m + 2 l, +1 (16 bytes); s0 is even (16-byte aligned: st is) and the three loads cover
 // the 256 states base - 255 .. base.  Positions before tile 0 read LB_PAD words in front of st.
-constexpr int LB_DMA_N = 3;
+constexpr int LB_DMA_N = DC_LB_KS / 2 + 1;                        // 128 states per load (+1: s0 rounded down)
 __device__ __forceinline__ long long lb_dma(const uint64_t* __restrict__ st, long long base, uint64_t* lw) {
-    const long long s0 = (base - 256) & ~1ll;
+    const long long s0 = (base - 64 * DC_LB_KS) & ~1ll;
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int m = 0; m < LB_DMA_N; m++)
@@ -767,11 +852,114 @@ __device__ __forceinline__ long long lb_dma(const uint64_t* __restrict__ st, lon
 #ifndef DC_TOK_SB
 #define DC_TOK_SB 0                     // (experiments: tokens the scheduler may interleave)
 #endif
+// (r06) the tokens without the LDS table and with ONE wave-uniform prediction branch per 16 tokens: the table
+// read + wait + branch of make_token_t made each thread's 16 tokens one dependent chain (16 x ~150 cycles of
+// LDS latency, a branch between tokens; the ISA showed ds_read_u16 -> s_waitcnt lgkmcnt(1) -> s_cbranch per
+// token); here the raw length is arithmetic (tab[i9] = 32 - l9 | len << 8, l9 = clamp(E + rawadd, 9, 32)) and
+// the 16 tokens are independent until the rare prediction fix-up.  Measured r06 (CT7 2^26): encoder 150.8-151.4
+// vs 144-145 us with the table form: the extra VALU cost more than the chain (7 waves per SIMD hide the LDS
+// latency) -- off.  DC_TOK_ALU=2: the table read kept, one prediction branch per group: 149-152 vs 145-146 us
+// (tools/experiments/enc_time.py) -- off as well.
+#ifndef DC_TOK_ALU
+#define DC_TOK_ALU 0
+#endif
+#ifndef DC_TOK_G
+#define DC_TOK_G 4
+#endif
+template <int CT>
+__device__ __forceinline__ void raw_token_alu(float x, const Params& P, const uint16_t* tab, uint32_t& val, int& len) {
+    const uint32_t u = __float_as_uint(x);
+    if (CT == 11) { val = u; len = 32; return; }
+    const uint32_t i9 = u >> 23;
+#if DC_TOK_ALU == 2                                       // (the table read, grouped: one wait per group)
+    const uint32_t e = tab[i9];
+    uint32_t v = u >> (e & 31u);
+    int l = (int)(e >> 8);
+    if (CT == 7) {
+        const bool f0 = (u >> 15) == P.mask17;
+        v ^= f0 ? P.K0 : (i9 == (P.mask17 >> 8) ? P.K1 : 0u);
+        l = f0 ? P.lm0 : l;
+    }
+    val = v;
+    len = l;
+#else
+    const int l9 = min(max((int)(i9 & 0xFFu) + P.rawadd, 9), 32);
+    uint32_t v = u >> (uint32_t)(32 - l9);
+    int l = l9;
+    if (CT == 7) {
+        const bool f1 = i9 == (P.mask17 >> 8);
+        const bool f0 = (u >> 15) == P.mask17;
+        l = f0 ? P.lm0 : (f1 ? P.lm1 : l9);
+        v ^= f0 ? P.K0 : (f1 ? P.K1 : 0u);
+    }
+    val = v;
+    len = l;
+#endif
+}
+// |b1 - x| etc. of make_token_t: the predictor distances, and whether a prediction is taken
+__device__ __forceinline__ void pred_dists(float x, float b1, float b2, float b3, float& d1, float& d2, float& d3) {
+    const float p2 = __fsub_rn(__fmul_rn(2.0f, b1), b2);
+    const float p3 = __fadd_rn(__fsub_rn(__fmul_rn(3.0f, b1), __fmul_rn(3.0f, b2)), b3);
+    d1 = fabsf(__fsub_rn(b1, x));
+    d2 = fabsf(__fsub_rn(p2, x));
+    d3 = fabsf(__fsub_rn(p3, x));
+}
+template <int CT, bool FAST>
+__device__ __forceinline__ uint32_t make_tokens16_alu(const float* h, const Params& P, const uint16_t* tab, int g3, int rem,
+                                                      uint32_t* tvs,
+                                                      uint32_t (&lp)[ENC_K / 4], bool& neg1) {
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < ENC_K / 4; q++) lp[q] = 0u;
+    // groups of DC_TOK_G tokens: independent work to cover the VALU latencies, and each group's rare prediction
+    // fix-up right after it, so that a float's history dies with its group (one fix-up after all 16 kept the 19
+    // history floats live and spilled ~40 VGPRs at 7 workgroups per CU)
+#pragma unroll
+    for (int g0 = 0; g0 < ENC_K; g0 += DC_TOK_G) {
+        uint32_t prm = 0;                                                // the group's tokens that take a prediction
+#pragma unroll
+        for (int j = g0; j < g0 + DC_TOK_G; j++) {
+            const float x = h[3 + j];
+            uint32_t v;
+            int len;
+            raw_token_alu<CT>(x, P, tab, v, len);
+            if (CT != 6) {
+                float d1, d2, d3;
+                pred_dists(x, h[2 + j], h[1 + j], h[j], d1, d2, d3);
+                const bool pr = (FAST ? true : j >= g3) && d1 == d1 && fminf(fminf(d1, d2), d3) <= P.thr_le;
+                const bool z = fabsf(x) <= P.thr_lt;
+                prm |= (pr && !z) ? 1u << j : 0u;
+                v = z ? 4u : v;
+                len = (pr || z) ? 3 : len;
+                neg1 |= x == -1.0f;                                      // the reference's sentinel
+            }
+            if (!FAST) len = j < rem ? len : 0;                          // past the end: no token
+            tvs[ENC_TPB * j] = v;
+            lp[j >> 2] |= (uint32_t)len << (8 * (j & 3));
+            sum += (uint32_t)len;
+        }
+        if (CT != 6 && __builtin_expect(__any(prm != 0u), 0)) {         // (rare in ordinary data)
+#pragma unroll
+            for (int j = g0; j < g0 + DC_TOK_G; j++) {
+                if ((prm >> j) & 1u) {
+                    float d1, d2, d3;
+                    pred_dists(h[3 + j], h[2 + j], h[1 + j], h[j], d1, d2, d3);
+                    const float d12 = fminf(d1, d2);
+                    tvs[ENC_TPB * j] = d3 < d12 ? 7u : (d2 < d1 ? 6u : 5u);
+                }
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return sum;
+}
+
 // the 16 tokens of a thread: values to tvs[256 j], lengths packed 4 per word in lp, their sum.  Not FAST: the
 // thread's elements j >= rem are past the end (no token), those j < g3 precede global index 3 (no prediction)
 template <int CT, bool FAST>
 __device__ __forceinline__ uint32_t make_tokens16(const float* h, const Params& P, const uint16_t* tab, int g3, int rem,
                                                   uint32_t* tvs, uint32_t (&lp)[ENC_K / 4], bool& neg1) {
+    if (DC_TOK_ALU) return make_tokens16_alu<CT, FAST>(h, P, tab, g3, rem, tvs, lp, neg1);
     uint32_t sum = 0;
 #pragma unroll
     for (int q = 0; q < ENC_K / 4; q++) lp[q] = 0u;
@@ -804,7 +992,8 @@ __device__ void enc_scanner(uint64_t* __restrict__ st, unsigned ntiles, uint32_t
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     unsigned long long carry = (unsigned long long)start_bit;
     unsigned F = 0;
-    unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    WaitBound wb;
+    wb.start();
     while (F < ntiles) {
         uint64_t v[4];
         int kb = 4;                                                       // the thread's first state not ready
@@ -849,9 +1038,9 @@ __device__ void enc_scanner(uint64_t* __restrict__ st, unsigned ntiles, uint32_t
         carry += tot;
         F += p;
         if (p) {
-            t0 = __builtin_amdgcn_s_memrealtime();
+            wb.start();
         } else {
-            if (__builtin_amdgcn_s_memrealtime() - t0 > LB_WAIT) { if (tid == 0) atomicOr(err, 4u); return; }
+            if (wb.expired()) { if (tid == 0) atomicOr(err, 4u); return; }
             __builtin_amdgcn_s_sleep(2);
         }
         __syncthreads();                                                  // the LDS words are rewritten
@@ -928,6 +1117,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
                 *reinterpret_cast<f32x4*>(stg + 4 * m + 4 * (m >> 2)) = f[2 * half + q];
             }
             __builtin_amdgcn_wave_barrier();
+            if (half == 0) E1STAMP(7);                                    // (stamps: wave 0's first x granules here)
             if ((lane >> 5) == half)
 #pragma unroll
                 for (int q = 0; q < ENC_K / 4; q++) u[q] = *reinterpret_cast<const f32x4*>(stg + 20 * (lane & 31) + 4 * q);
@@ -1061,12 +1251,13 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
         int bad = 0;
         if (scan && DC_SCAN_POLL) {                                      // (A/B: wait for the scanner itself)
             if (lane == 0) {
-                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                WaitBound wb;
+                wb.start();
                 uint64_t v;
                 for (;;) {
                     v = ld_relaxed(st + tile);
                     if ((uint32_t)(v >> 42) == tag && (v & ST_MASK) == ST_INC) break;
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > LB_WAIT) { bad = 1; break; }
+                    if (wb.expired()) { bad = 1; break; }
                     lbst += 1u << 16;
                     __builtin_amdgcn_s_sleep(DC_LB_SLEEP);
                 }
@@ -1077,27 +1268,43 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
             // behind this tile's own neighbours (which started with it): a look-back over DC_LB_KS x 64
             // predecessors in one round trip mostly meets one (waiting for the scanner to reach this tile
             // itself cost ~4 us per tile)
+#ifdef DC_ENC_DIAG_NOLB
+            if (false) {
+#else
             if (tile > 0) {
+#endif
                 if (DC_LB_DMA) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the window's LDS writes landed
                     bad = enc_lookback<DC_LB_KS>(st, tile, tag, G, lbst, start_bit, lbw, lb_s0);
                 } else {
-                    bad = enc_lookback<DC_LB_KS>(st, tile, tag, G, lbst, start_bit);
+                    bad = enc_lookback<DC_LB_KS>(st, tile, tag, G, lbst, start_bit, nullptr, 0, nullptr,
+                                                 [&](long long ti) { return help_tile_bits<CT>(x, n, idx0, P, tab, ti); });
                 }
             }
         } else if (tile > 0) {
             bad = enc_lookback<LB_KW>(st, tile, tag, G, lbst, start_bit);
         }
         E1STAMP(4);
+#ifdef DC_ENC_DIAG_NOLB
+        // (diagnostic build: no look-back -- an in-bounds but wrong offset, 20 bits per float -- to time the rest)
+        G = (unsigned long long)start_bit + 20ull * (unsigned long long)tbase;
+        bad = 0;
+#endif
         if (lane == 0) {
             uint32_t tp = 0;
             if (tile > 0 && !bad) {                                       // the predecessor's last bits
-                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                WaitBound wb;
+                wb.start();
                 uint64_t v = tl0;
-                while ((v >> 32) != (uint64_t)epoch) {
+                for (unsigned k = 0; (v >> 32) != (uint64_t)epoch; k++) {
                     v = ld_relaxed(tl + tile - 1);
                     if ((v >> 32) == (uint64_t)epoch) break;
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > LB_WAIT) { bad = 1; break; }
+                    if (k == HELP_POLLS) {                                // the predecessor is late: its tail here
+                        v = ((uint64_t)epoch << 32) | help_tile_tail<CT>(x, idx0, P, tab, (long long)tile - 1);
+                        st_relaxed(tl + tile - 1, v);
+                        break;
+                    }
+                    if (wb.expired()) { bad = 1; break; }
                     __builtin_amdgcn_s_sleep(1);
                 }
                 tp = (uint32_t)v;
@@ -1116,7 +1323,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
             s_ok = bad ? 0u : 1u;
             if (dbg && tile < 16384) {
                 dbg[tile * 8 + 6] = lbst;
-                dbg[tile * 8 + 7] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & 7u;   // HW_REG_XCC_ID
+                // (slot 7: wave 0's x arrival, E1STAMP(7) above)
             }
         }
     }
@@ -1156,7 +1363,9 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
         const uint32_t cur = i < tw ? sb[i] : 0u;                          // (stale past the tile's bits)
         const uint32_t prev = i ? sb[i - 1] : tp0;
         const uint32_t w = sh ? __builtin_amdgcn_alignbit(prev, cur, sh) : cur;
-#if DC_PACK_NT
+#if defined(DC_ENC_DIAG_NOSTORE)
+        if (w == 0x9E3779B9u && i == 12345) out[W0 + i] = 0u;         // (diagnostic build: the words are made, not stored)
+#elif DC_PACK_NT
         __builtin_nontemporal_store(__builtin_bswap32(w), out + W0 + i);
 #else
         out[W0 + i] = __builtin_bswap32(w);
@@ -1285,12 +1494,13 @@ __device__ __forceinline__ void pipe_offset(const uint64_t* __restrict__ st, con
     if (lane == 0) {
         uint32_t tp = 0;
         if (t > 0 && !bad) {
-            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            WaitBound wb;
+            wb.start();
             uint64_t v = tl0;
             while ((v >> 32) != (uint64_t)epoch) {
                 v = ld_relaxed(tl + t - 1);
                 if ((v >> 32) == (uint64_t)epoch) break;
-                if (__builtin_amdgcn_s_memrealtime() - t0 > LB_WAIT) { bad = 1; break; }
+                if (wb.expired()) { bad = 1; break; }
                 __builtin_amdgcn_s_sleep(1);
             }
             tp = (uint32_t)v;

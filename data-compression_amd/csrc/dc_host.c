@@ -1540,6 +1540,21 @@ int dc_hash_device(const void* d_buf, long long nbytes, unsigned long long* hash
     return DC_OK;
 }
 
+/* co-residency tests: `blocks` workgroups (256 threads, lds bytes of LDS each) resident for `us` microseconds on
+   `stream` (NULL: a stream of the library's own, not the codec's) -- asynchronous */
+int dc_occupy_device(void* stream, double us, int blocks, int lds) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    static hipStream_t own = NULL;
+    if (!stream) {
+        if (!own) HIPCHK(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
+        stream = own;
+    }
+    if (dc_launch_occupy(us, blocks, lds, G.d_enc_err + 12, (hipStream_t)stream))   /* (a word nothing reads) */
+        return seterr(DC_ERR_ARG, "occupy: blocks >= 1, 0 <= us <= 1e6, lds <= 160 KiB");
+    return DC_OK;
+}
+
 int dc_copy_rate_device(const void* d_src, void* d_dst, long long bytes, int reps, double* gbs_out, int* variant_out) {
     int rc = ensure_init();
     if (rc) return rc;

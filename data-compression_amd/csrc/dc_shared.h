@@ -155,6 +155,7 @@ void dc_decode3_size_hint(long long max_chunks, long long nchunks);
 int dc_launch_merge_shards(const uint8_t* g, long long P, int world, const unsigned long long* counts, uint8_t* out,
                            long long out_bytes, unsigned long long* total_out, unsigned* err, long long max_bytes,
                            dc_hip_stream st);
+int dc_launch_occupy(double us, int blocks, int lds, unsigned* sink, dc_hip_stream st);
 int dc_launch_extract_shard(const uint8_t* g, long long g_bytes, const unsigned long long* counts, int rank, uint8_t* d,
                             long long d_bytes, unsigned long long* nbits_out, unsigned* err, dc_hip_stream st);
 int dc_launch_shard3_fix(const uint8_t* s, const DC_NS Params* P, const DC_NS Dec3Bufs* D3, const float* hin,

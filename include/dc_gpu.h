@@ -173,6 +173,10 @@ int dc_hash_device(const void* d_buf, long long nbytes, unsigned long long* hash
  * *gbs_out = the best variant's (read + written bytes) / average launch time, in GB/s; *variant_out its
  * index.  Synchronous. */
 int dc_copy_rate_device(const void* d_src, void* d_dst, long long bytes, int reps, double* gbs_out, int* variant_out);
+/* Co-residency tests: `blocks` workgroups of 256 threads with `lds` bytes of LDS each that stay resident for `us`
+ * microseconds on `stream` (NULL: a stream of the library's own, not the codec's), so that the codec can be
+ * run while other work holds CU slots.  Asynchronous. */
+int dc_occupy_device(void* stream, double us, int blocks, int lds);
 /* The CT9 flow without CRC passes of its own (fused CRC-32 over 16 KiB blocks; each a zlib crc32 of the stream
  * bytes, written to device memory, asynchronous on the library stream):
  * dc_encode_crc_device: dc_encode_device at start bit 0 (d_total_bits required) plus the stream's CRC into

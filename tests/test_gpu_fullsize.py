@@ -219,3 +219,33 @@ def test_back_to_back_encodes_2p26(dc, oracle):
     assert same
     del dx, st, first
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("per_cu,lds,log2n", [(1, 0, 22), (4, 0, 24), (2, 65536, 24), (6, 0, 22)])
+def test_encode_beside_occupying_kernel(dc, oracle, per_cu, lds, log2n):
+    """The single-pass encoder while another kernel holds CU slots on a second stream of the same process
+    (forward progress under co-residency).  Its tiles wait only for lower tiles, which in-order
+    dispatch has made resident, so the neighbour slows it but cannot wedge it; a wait that did reach its bound
+    (20 ms AND 8192 polls: dc_encode.hip WaitBound) would have taken the exact three-launch fallback.  Either way
+    the stream equals the oracle's, and the encoder's error word is clear after dc_encode_result."""
+    import torch
+    n = 1 << log2n
+    dc.set_bound(1e-3)
+    _, xs = oracle.to_small(_u10(oracle, n))
+    t, m17 = oracle.type_mask(xs)
+    dx = torch.from_numpy(xs).cuda()
+    cap = dc.stream_capacity(n)
+    st = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    retries0 = int(dc.L.dc_encode_retries())
+    side = torch.cuda.Stream()
+    for _ in range(3):
+        dc.occupy_device(side.cuda_stream, 4000.0, per_cu * 256, lds)    # 4 ms beside each encode
+        dc.encode_device(7, dx.data_ptr(), n, st.data_ptr(), type_=t, mask17=m17)
+        nbits = dc.encode_result()
+        assert dc.encode_status() == 0
+    torch.cuda.synchronize()
+    so, nbo, _ = oracle.compress(7, xs, 1e-3, t, m17)
+    assert (nbits + 7) // 8 == nbo
+    assert np.array_equal(st[:nbo].cpu().numpy(), so)
+    print(f"encoder fallbacks beside the neighbour: {int(dc.L.dc_encode_retries()) - retries0}")

@@ -25,9 +25,15 @@ a = a[ok]
 idx = np.nonzero(ok)[0]
 t0 = a[:, 0].min()
 d = np.diff(a[:, :6], axis=1) / 100.0
+xa = (a[:, 7] - a[:, 0]) / 100.0                 # wave 0's first x granules arrived (slot 7)
+print(f"x arrival    mean {xa.mean():8.2f} us  p50 {np.median(xa):8.2f}  p90 {np.percentile(xa, 90):8.2f}  max {xa.max():8.2f}")
 for i, nm in enumerate(["load+tokens", "scan", "tv+pack", "look-back", "tail+store"]):
     print(f"{nm:12s} mean {d[:, i].mean():8.2f} us  p50 {np.median(d[:, i]):8.2f}  p90 {np.percentile(d[:, i], 90):8.2f}  max {d[:, i].max():8.2f}")
 print("tiles", len(a), "span us", (a[:, 5].max() - t0) / 100.0)
+life = (a[:, 5] - a[:, 0]) / 100.0
+st_ = (a[:, 0] - t0) / 100.0
+print(f"lifetime mean {life.mean():.2f} us p50 {np.median(life):.2f}; starts: last {st_.max():.1f} us; "
+      f"tiles started in the first 5 us {(st_ < 5).sum()}")
 win = a[:, 6] & 0xFFFF; spins = a[:, 6] >> 16
 print("look-back windows mean %.2f max %d; spins mean %.2f p90 %.0f max %d" % (win.mean(), win.max(), spins.mean(), np.percentile(spins, 90), spins.max()))
 xcc = a[:, 7]
