@@ -416,7 +416,8 @@ class Ctx:
         # several ranks on one GPU (the gloo rehearsal).  Until r05 they encoded with the wait-free three-launch
         # variant: a single-pass tile could wait past its bound for a predecessor left undispatched behind another
         # process's waiting waves.  Since r06 a tile computes a late predecessor's count itself (dc_encode.hip
-        # enc_lookback's help), so every rank keeps the single pass (DC_ENC_PASSES still selects another)
+        # enc_lookback's help: the helping instantiation, selected below), so every rank keeps the single pass
+        # (DC_ENC_PASSES still selects another)
         self.shared_gpu = self.world > max(torch.cuda.device_count(), 1)
         self.dist = None
         if self.world > 1:
@@ -431,6 +432,8 @@ class Ctx:
         self.dcamd = dcamd
         self.L = dcamd.Lib()
         self.L.init(self.local)
+        if self.shared_gpu:             # ranks share a GPU: the encoder's helping instantiation
+            self.L.L.dc_set_encode_help(1)
 
     def barrier(self):
         if self.dist is not None:

@@ -692,7 +692,7 @@ __device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
 // token_len_t: the length decision of make_token_t), and the tile's last 31 bits (its last 16 tokens, one lane)
 // -- exactly what the tile itself publishes.
 template <int CT>
-__device__ unsigned long long help_tile_bits(const float* __restrict__ x, long long n, long long idx0, const Params& P,
+__device__ __forceinline__ unsigned long long help_tile_bits(const float* __restrict__ x, long long n, long long idx0, const Params& P,
                                              const uint16_t* tab, long long ti) {
     const int lane = threadIdx.x & 63;
     const long long e0 = ti * ENC_TILE + 64ll * lane;
@@ -714,7 +714,7 @@ __device__ unsigned long long help_tile_bits(const float* __restrict__ x, long l
     return wave_sum64(bits);
 }
 template <int CT>
-__device__ uint32_t help_tile_tail(const float* __restrict__ x, long long idx0, const Params& P, const uint16_t* tab,
+__device__ __forceinline__ uint32_t help_tile_tail(const float* __restrict__ x, long long idx0, const Params& P, const uint16_t* tab,
                                    long long ti) {                        // (a full tile: ti + 1 < ntiles)
     const long long e0 = (ti + 1) * ENC_TILE - ENC_K;
     float b1 = x[e0 - 1], b2 = x[e0 - 2], b3 = x[e0 - 3];
@@ -749,6 +749,10 @@ __device__ uint32_t help_tile_tail(const float* __restrict__ x, long long idx0, 
 // processes' look-back kernels on the same GPU, a predecessor's workgroup can stay undispatched on its XCD
 // behind their waiting waves while this one holds a slot of another XCD (r05f: three ranks on one GPU, encoder
 // status 4).  The value is the one the owner publishes, so a late owner's store is harmless.
+// The help is compiled into its own instantiation (encode_fused_kernel<CT, CRC, true>, chosen by
+// dc_set_encode_help / DC_ENC_HELP=1): never triggered, it still cost the hot path 7 us (tiles helping) and 12 us
+// (the scanner helping) at 2^26 -- more spilled SGPRs in the token code -- and one process per GPU (the real
+// multi-GPU run) does not need it: dispatch there is in order per XCD and only this launch holds the slots.
 #ifndef DC_HELP_POLLS
 #define DC_HELP_POLLS 256                       // (tests build 0: every unpublished state helped at once)
 #endif
@@ -987,11 +991,54 @@ __device__ __forceinline__ uint32_t make_tokens16(const float* h, const Params& 
 // stores their inclusive states; F moves past them.  A tile then needs ONE poll of its own state instead
 // of a look-back: the chained look-back cost ~3 state round trips (~4.5 us) per tile, as each tile's
 // predecessors were looking back at the same time.
+// (r06) The scanner's help: a tile whose aggregate is still unpublished after HELP_POLLS scanner rounds is
+// counted by the scanner workgroup itself (256 threads x 16 floats, token_len_t) and published -- its aggregate
+// (CAS from the value seen) and, for the successor's first word, its tail granule.  The values are the ones the
+// tile publishes, so a late tile's own stores are harmless.  With it a tile's look-back depends on no other
+// workgroup being dispatched: with other processes' look-back kernels on the GPU a predecessor can stay
+// undispatched on its XCD behind their waiting waves (r05f: three ranks on one GPU, encoder status 4).
+template <int CT>
+__device__ void scanner_help(uint64_t* __restrict__ st, uint64_t* __restrict__ tl, unsigned F, unsigned ntiles,
+                             uint32_t tag, uint32_t epoch, uint64_t seen, const float* __restrict__ x, long long n,
+                             long long idx0, const Params& P, const uint16_t* tab, unsigned long long* s_red) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const long long e0 = (long long)F * ENC_TILE + (long long)ENC_K * tid;
+    float b[3];
+#pragma unroll
+    for (int k = 1; k <= 3; k++) {
+        const long long e = e0 - k;
+        b[k - 1] = (e < n && e >= -3 && idx0 + e >= 0) ? x[e] : 0.0f;
+    }
+    float b1 = b[0], b2 = b[1], b3 = b[2];
+    unsigned long long bits = 0;
+    for (int j = 0; j < ENC_K; j++) {
+        const long long e = e0 + j;
+        if (e >= n) break;
+        const float v = x[e];
+        bits += (unsigned)token_len_t<CT>(v, b1, b2, b3, idx0 + e >= 3, P, tab);
+        b3 = b2; b2 = b1; b1 = v;
+    }
+    bits = wave_sum64(bits);
+    if (lane == 0) s_red[wid] = bits;
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned long long T = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+        atomicCAS(reinterpret_cast<unsigned long long*>(st + F), (unsigned long long)seen,
+                  (unsigned long long)st_word(tag, ST_AGG, T));
+        if (F + 1 < ntiles && (ld_relaxed(tl + F) >> 32) != (uint64_t)epoch)
+            st_relaxed(tl + F, ((uint64_t)epoch << 32) | help_tile_tail<CT>(x, idx0, P, tab, (long long)F));
+    }
+    __syncthreads();
+}
+
+template <int CT, bool HELP>
 __device__ void enc_scanner(uint64_t* __restrict__ st, unsigned ntiles, uint32_t tag, int start_bit,
-                            unsigned* __restrict__ err, uint32_t* s_gap, uint32_t* s_kb, uint32_t* s_tot) {
+                            unsigned* __restrict__ err, uint32_t* s_gap, uint32_t* s_kb, uint32_t* s_tot,
+                            uint64_t* __restrict__ tl, uint32_t epoch, const float* __restrict__ x, long long n,
+                            long long idx0, const Params& P, const uint16_t* tab, unsigned long long* s_red) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     unsigned long long carry = (unsigned long long)start_bit;
-    unsigned F = 0;
+    unsigned F = 0, idle = 0;
     WaitBound wb;
     wb.start();
     while (F < ntiles) {
@@ -1039,7 +1086,16 @@ __device__ void enc_scanner(uint64_t* __restrict__ st, unsigned ntiles, uint32_t
         F += p;
         if (p) {
             wb.start();
+            idle = 0;
         } else {
+            if (HELP && ++idle >= HELP_POLLS) {                          // tile F is late: count it here
+                __syncthreads();                                          // (s_gap / s_kb read above)
+                const uint64_t seen = ld_relaxed(st + F);
+                const bool pub = (uint32_t)(seen >> 42) == tag && (seen & ST_MASK) == ST_AGG;
+                if (!pub) scanner_help<CT>(st, tl, F, ntiles, tag, epoch, seen, x, n, idx0, P, tab, s_red);
+                idle = 0;
+                continue;
+            }
             if (wb.expired()) { if (tid == 0) atomicOr(err, 4u); return; }
             __builtin_amdgcn_s_sleep(2);
         }
@@ -1056,6 +1112,10 @@ __device__ void enc_scanner(uint64_t* __restrict__ st, unsigned ntiles, uint32_t
 #ifndef DC_STORE_U
 #define DC_STORE_U 1                    // (A/B) words per thread per store round: 4 and 8 measured equal, off
 #endif
+#ifndef DC_STORE_Q
+#define DC_STORE_Q 1                    // (r06) 16-byte quads of the stream's grid per thread
+#endif
+typedef unsigned u32x4q __attribute__((ext_vector_type(4)));
 // (A/B, off) After the pack only wave 0 has work left that needs the tile's offset (the look-back, then the
 // stores): waves 1-3 may end there, their wave slots taking the next tile's waves while wave 0 waits for its
 // look-back round trip.  Measured r05: 148.7-150 us with vs 143.7-145.7 us without (one wave then stores the
@@ -1067,7 +1127,7 @@ __device__ void enc_scanner(uint64_t* __restrict__ st, unsigned ntiles, uint32_t
 // block accumulators cblk (dc_device.h's fused CRC; crcf_final_kernel turns them into the stream's zlib CRC):
 // thread k takes the 16-word group q0 + k of the stream's word grid (q0 = the group of the tile's first word),
 // the tile's stored words in it and zeros for the rest, and shifts its raw CRC to the end of its block.
-template <int CT, bool CRC = false>
+template <int CT, bool CRC = false, bool HELP = false>
 __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
     const float* __restrict__ x, long long n, long long idx0, Params P, uint32_t* __restrict__ out,
     uint64_t* __restrict__ st, uint64_t* __restrict__ tl, unsigned ntiles, int start_bit,
@@ -1090,7 +1150,10 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t tag = epoch & ST_TAGM;
     if (scan && blockIdx.x == 0) {                                    // the scanner (dispatched first)
-        enc_scanner(st, ntiles, tag, start_bit, err, s_hw, s_hi, s_tw);
+        __shared__ unsigned long long s_red[4];
+        build_enc_tab<CT>(tab, P, tid, ENC_TPB);                      // (its help counts late tiles)
+        __syncthreads();
+        enc_scanner<CT, HELP>(st, ntiles, tag, start_bit, err, s_hw, s_hi, s_tw, tl, epoch, x, n, idx0, P, tab, s_red);
         return;
     }
     const unsigned tile = blockIdx.x - (scan ? 1u : 0u);
@@ -1277,8 +1340,11 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the window's LDS writes landed
                     bad = enc_lookback<DC_LB_KS>(st, tile, tag, G, lbst, start_bit, lbw, lb_s0);
                 } else {
-                    bad = enc_lookback<DC_LB_KS>(st, tile, tag, G, lbst, start_bit, nullptr, 0, nullptr,
-                                                 [&](long long ti) { return help_tile_bits<CT>(x, n, idx0, P, tab, ti); });
+                    if constexpr (HELP)
+                        bad = enc_lookback<DC_LB_KS>(st, tile, tag, G, lbst, start_bit, nullptr, 0, nullptr,
+                                                     [&](long long ti) { return help_tile_bits<CT>(x, n, idx0, P, tab, ti); });
+                    else
+                        bad = enc_lookback<DC_LB_KS>(st, tile, tag, G, lbst, start_bit);
                 }
             }
         } else if (tile > 0) {
@@ -1299,7 +1365,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
                 for (unsigned k = 0; (v >> 32) != (uint64_t)epoch; k++) {
                     v = ld_relaxed(tl + tile - 1);
                     if ((v >> 32) == (uint64_t)epoch) break;
-                    if (k == HELP_POLLS) {                                // the predecessor is late: its tail here
+                    if (HELP && k == HELP_POLLS) {                        // the predecessor is late: its tail here
                         v = ((uint64_t)epoch << 32) | help_tile_tail<CT>(x, idx0, P, tab, (long long)tile - 1);
                         st_relaxed(tl + tile - 1, v);
                         break;
@@ -1337,6 +1403,41 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
     const long long W0 = (long long)(Gt >> 5);
     const int nw = (int)((long long)((Gt + T) >> 5) - W0) + ((tile == ntiles - 1 && ((Gt + T) & 31ull)) ? 1 : 0);
     const int tw = (int)((T + 31u) >> 5);                                  // buffer words holding tile bits
+    constexpr int SW = DC_ENC_EARLY_EXIT ? 64 : ENC_TPB;                    // the storing threads
+#if DC_STORE_Q
+    // (r06) the stream's 16-byte grid: thread k takes quad Q0 + k (Q0 = W0 / 4): its 4 words from 5 buffer words
+    // (v_alignbit by sh, 0 keeps the word), one 16-byte store when the quad lies inside the tile's word range,
+    // word stores at the two ends.  The word loop spent ~10 VALU per word (two LDS reads, a select, 64-bit
+    // addresses, loop control): the encoder is VALU-bound (SQ: VALU instructions x 4 cycles ~ the kernel time)
+    if (!CRC && !mirror) {
+        const long long Q0 = W0 >> 2;
+        const int nq = (int)(((W0 + nw + 3) >> 2) - Q0);
+        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(out + 4 * Q0, (short)0, nq * 16, 0x00020000);
+        for (int k = tid; k < nq; k += ENC_TPB) {
+            const int i0 = (int)(4 * (Q0 + k) - W0);                      // the quad's first word in the tile (>= -3)
+            uint32_t b[5];
+#pragma unroll
+            for (int m = 0; m < 5; m++) {
+                const int i = i0 - 1 + m;
+                b[m] = (i >= 0 && i < tw) ? sb[i] : (i == -1 ? tp0 : 0u);
+            }
+            u32x4q q;
+            q.x = __builtin_bswap32(__builtin_amdgcn_alignbit(b[0], b[1], sh));
+            q.y = __builtin_bswap32(__builtin_amdgcn_alignbit(b[1], b[2], sh));
+            q.z = __builtin_bswap32(__builtin_amdgcn_alignbit(b[2], b[3], sh));
+            q.w = __builtin_bswap32(__builtin_amdgcn_alignbit(b[3], b[4], sh));
+            if (i0 >= 0 && i0 + 4 <= nw) {
+                __builtin_amdgcn_raw_buffer_store_b128(q, ro, 16 * k, 0, DC_PACK_NT ? 2 : 0);
+            } else {
+                const uint32_t qv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                for (int m = 0; m < 4; m++)
+                    if (i0 + m >= 0 && i0 + m < nw) __builtin_amdgcn_raw_buffer_store_b32(qv[m], ro, 16 * k + 4 * m, 0, DC_PACK_NT ? 2 : 0);
+            }
+        }
+    } else
+#endif
+    {
 #if DC_STORE_U > 1
     // DC_STORE_U words per thread per round: their LDS reads are in flight together (one word per round
     // waited on one LDS round trip each)
@@ -1358,7 +1459,6 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
         }
     }
 #else
-    constexpr int SW = DC_ENC_EARLY_EXIT ? 64 : ENC_TPB;                    // the storing threads
     for (int i = DC_ENC_EARLY_EXIT ? lane : tid; i < nw; i += SW) {
         const uint32_t cur = i < tw ? sb[i] : 0u;                          // (stale past the tile's bits)
         const uint32_t prev = i ? sb[i - 1] : tp0;
@@ -1374,6 +1474,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
         if (mirror) __builtin_nontemporal_store(__builtin_bswap32(w), mirror + W0 + i);
     }
 #endif
+    }
     if constexpr (CRC) {
         // the stored words by 16-word groups of the stream's word grid (a tile spans at most 258 groups and
         // three 16 KiB blocks: its raw CRC pieces are XOR-ed per block)
@@ -1562,7 +1663,10 @@ __global__ __launch_bounds__(ENC_TPB, DC_PIPE_WAVES) void encode_pipe_kernel(
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t tag = epoch & ST_TAGM;
     if (blockIdx.x == 0) {                                            // the scanner (dispatched first)
-        enc_scanner(st, ntiles, tag, start_bit, err, s_hw, s_hi, s_tw);
+        __shared__ unsigned long long s_red[4];
+        build_enc_tab<CT>(tab, P, tid, ENC_TPB);
+        __syncthreads();
+        enc_scanner<CT, false>(st, ntiles, tag, start_bit, err, s_hw, s_hi, s_tw, tl, epoch, x, n, idx0, P, tab, s_red);
         return;
     }
     build_enc_tab<CT>(tab, P, tid, ENC_TPB);
@@ -1781,6 +1885,12 @@ __global__ __launch_bounds__(ENC_TPB, DC_PIPE_WAVES) void encode_pipe_kernel(
 static long long desc_words_multi(long long nt);
 static int g_enc_mode_last = 0;
 static int g_enc_crc_fused = 0;                 // 1: the last launch computed the fused CRC pieces
+static int g_enc_help = -1;                     // the helping instantiation (DC_ENC_HELP=1 / dc_set_encode_help)
+extern "C" int dc_set_encode_help(int on) {
+    const int old = g_enc_help < 0 ? 0 : g_enc_help;
+    g_enc_help = on ? 1 : 0;
+    return old;
+}
 // encoder variant: 1 = single pass (default), 2 = count + pack (the pack's workgroup 0 scans the tile
 // counts, the other tiles wait for its flag), 3 = count + scan launch + pack (no wait anywhere: the
 // fallback after a single-pass timeout).  DC_ENC_PASSES=2|3 selects the others.
@@ -1811,6 +1921,7 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
     if (mode == 0) mode = enc_mode_default();
     g_enc_mode_last = mode;
     g_enc_crc_fused = 0;
+    if (g_enc_help < 0) g_enc_help = (getenv("DC_ENC_HELP") && *getenv("DC_ENC_HELP") == '1') ? 1 : 0;
     const unsigned ntiles = (unsigned)((n + ENC_TILE - 1) / ENC_TILE);
     if (mode == 1) {
         const int grid = (int)ntiles;
@@ -1856,9 +1967,23 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
             dc_mark_phase(1, stream);
             return hipGetLastError() == hipSuccess ? 0 : -1;
         }
-        DC_ENC_DISPATCH(encode_fused_kernel, dim3(grid + scan), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, st,
-                        st + ntiles, ntiles, start_bit, total_bits, total_bits2, epoch, err, dbg, scan, nullptr, nullptr,
-                        g_enc_mirror);
+        if (g_enc_help) {                    // (ranks sharing a GPU: tiles and scanner compute late tiles' counts)
+            switch (P->ct) {
+#define DC_ENC_HELPK(C)                                                                              \
+    case C:                                                                                          \
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(encode_fused_kernel<C, false, true>), dim3(grid + scan), dim3(ENC_TPB), 0, \
+                           stream, x, n, idx0, *P, out, st, st + ntiles, ntiles, start_bit, total_bits, total_bits2, \
+                           epoch, err, dbg, scan, nullptr, nullptr, g_enc_mirror);                   \
+        break;
+                DC_ENC_HELPK(5) DC_ENC_HELPK(6) DC_ENC_HELPK(7) DC_ENC_HELPK(11)
+#undef DC_ENC_HELPK
+                default: return -2;
+            }
+        } else {
+            DC_ENC_DISPATCH(encode_fused_kernel, dim3(grid + scan), dim3(ENC_TPB), 0, stream, x, n, idx0, *P, out, st,
+                            st + ntiles, ntiles, start_bit, total_bits, total_bits2, epoch, err, dbg, scan, nullptr,
+                            nullptr, g_enc_mirror);
+        }
         dc_mark_phase(1, stream);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }

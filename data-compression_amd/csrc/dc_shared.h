@@ -116,6 +116,7 @@ int dc_launch_encode(const float* x, long long n, long long idx0, const DC_NS Pa
                      dc_hip_stream stream);
 int dc_encode_mode(void);
 int dc_encode_crc_fused_last(void);      /* 1: the last encode launch computed the fused CRC pieces */
+int dc_set_encode_help(int on);
 unsigned dc_encode_epoch_limit(void);
 long long dc_encode_group_count(long long n);
 long long dc_encode_tile_count(long long n);

@@ -47,7 +47,7 @@ EXT_SYMBOLS = [
     "dc_decode_status", "dc_abi_status", "dc_med_sum_device", "dc_type_from_max", "dc_set_small_chunk_max_bytes",
     "dc_set_decode3_min_bytes", "dc_set_decode3_seg", "dc_set_fused3", "dc_fused3_stamps", "dc_fused3_last_seg", "dc_decode3_last_fused", "dc_last_decode_was_v3", "dc_last_decode_launched_v3",
     "dc_encode_status", "dc_encode_clear_status", "dc_encode_mode", "dc_encode_retries", "dc_crc_resend_device",
-    "dc_merge_shards_device", "dc_merge_status", "dc_extract_shard_device", "dc_occupy_device", "dc_decode_shard3_device", "dc_decode_shard3_fix",
+    "dc_merge_shards_device", "dc_merge_status", "dc_extract_shard_device", "dc_occupy_device", "dc_set_encode_help", "dc_decode_shard3_device", "dc_decode_shard3_fix",
     "dc_decode_status_clear", "dc_set_runs_max_bytes", "dc_last_decode_was_runs",
     "dc_last_decode_launched_runs", "dc_last_decode_used_maps", "dc_med_last_wide", "dc_set_decode3_maps", "dc_set_halo_async", "dc_med_shard_stats", "dc_med_shard_trans",
     "dc_med_shard_binades",

@@ -173,6 +173,11 @@ int dc_hash_device(const void* d_buf, long long nbytes, unsigned long long* hash
  * *gbs_out = the best variant's (read + written bytes) / average launch time, in GB/s; *variant_out its
  * index.  Synchronous. */
 int dc_copy_rate_device(const void* d_src, void* d_dst, long long bytes, int reps, double* gbs_out, int* variant_out);
+/* The single-pass encoder's tiles wait for lower tiles.  With one process per GPU that is safe (dispatch is in
+ * order per XCD).  Where several processes run look-back kernels on one GPU, a predecessor can stay undispatched
+ * behind their waiting waves: on = 1 selects the helping instantiation, whose waiting tiles (and scanner) compute
+ * a late predecessor's count and tail themselves (also DC_ENC_HELP=1).  Returns the previous setting. */
+int dc_set_encode_help(int on);
 /* Co-residency tests: `blocks` workgroups of 256 threads with `lds` bytes of LDS each that stay resident for `us`
  * microseconds on `stream` (NULL: a stream of the library's own, not the codec's), so that the codec can be
  * run while other work holds CU slots.  Asynchronous. */

@@ -221,8 +221,9 @@ def test_back_to_back_encodes_2p26(dc, oracle):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("help_", [0, 1])
 @pytest.mark.parametrize("per_cu,lds,log2n", [(1, 0, 22), (4, 0, 24), (2, 65536, 24), (6, 0, 22)])
-def test_encode_beside_occupying_kernel(dc, oracle, per_cu, lds, log2n):
+def test_encode_beside_occupying_kernel(dc, oracle, per_cu, lds, log2n, help_):
     """The single-pass encoder while another kernel holds CU slots on a second stream of the same process
     (forward progress under co-residency).  Its tiles wait only for lower tiles, which in-order
     dispatch has made resident, so the neighbour slows it but cannot wedge it; a wait that did reach its bound
@@ -239,11 +240,15 @@ def test_encode_beside_occupying_kernel(dc, oracle, per_cu, lds, log2n):
     torch.cuda.synchronize()
     retries0 = int(dc.L.dc_encode_retries())
     side = torch.cuda.Stream()
-    for _ in range(3):
-        dc.occupy_device(side.cuda_stream, 4000.0, per_cu * 256, lds)    # 4 ms beside each encode
-        dc.encode_device(7, dx.data_ptr(), n, st.data_ptr(), type_=t, mask17=m17)
-        nbits = dc.encode_result()
-        assert dc.encode_status() == 0
+    old = dc.L.dc_set_encode_help(help_)            # (1: the helping instantiation, as ranks sharing a GPU run)
+    try:
+        for _ in range(3):
+            dc.occupy_device(side.cuda_stream, 4000.0, per_cu * 256, lds)    # 4 ms beside each encode
+            dc.encode_device(7, dx.data_ptr(), n, st.data_ptr(), type_=t, mask17=m17)
+            nbits = dc.encode_result()
+            assert dc.encode_status() == 0
+    finally:
+        dc.L.dc_set_encode_help(old)
     torch.cuda.synchronize()
     so, nbo, _ = oracle.compress(7, xs, 1e-3, t, m17)
     assert (nbits + 7) // 8 == nbo
