@@ -646,6 +646,10 @@ __global__ __launch_bounds__(ENC_TPB, DC_PACK_STG2 ? 8 : 1) void encode_pack_ker
 #ifndef DC_LB_DMA
 #define DC_LB_DMA 0                     // the first window into LDS before the pack (lb_dma): 194 vs 147 us, off
 #endif
+#ifndef DC_LB_EARLY
+#define DC_LB_EARLY 0                   // (r06, A/B, off) the first window requested into registers before the pack:
+                                        // 156-159 vs 142-143 us (K = 1), 164-165 (K = 2)
+#endif
 #ifndef DC_LB_K
 #define DC_LB_K 8
 #endif
@@ -958,11 +962,95 @@ __device__ __forceinline__ uint32_t make_tokens16_alu(const float* h, const Para
     return sum;
 }
 
+// (r06) Fewer VALU per token: the encoder is VALU-issue bound (SQ r05l: 1201 VALU per wave x 4 cycles, 7 waves per
+// SIMD ~ the launch), and the ISA of make_tokens16 spent ~36 VALU per token, ~6 of them spilling compare masks
+// to VGPR lanes (v_writelane / v_readlane: the length selects were sunk below the loop).  Here:
+//  * the predictor distances of two tokens per packed instruction (v_pk_add_f32 / v_pk_mul_f32; 3 b computed once
+//    per float), no FMA contraction (-ffp-contract=off), the same IEEE operations as make_token_t;
+//  * no d1 == d1 test: d1 = |b1 - x| is NaN only when x or b1 is NaN or x = b1 = +-inf, and then d2 and d3 are NaN
+//    too (p2 = 2 b1 - b2 and p3 = 3 b1 - 3 b2 + b3 are NaN or an infinity of b1's sign), so min(d1, d2, d3) is NaN
+//    and the threshold compare is false either way;
+//  * each token's value and length forced into VGPRs where they are made (no mask lives past its token);
+//  * the length sum from the packed length bytes (v_sad_u8), not one add per token.
+#ifndef DC_ENC_V2
+#define DC_ENC_V2 0                     // (A/B, off) bit 0: make_tokens16_v2; bit 1: the OR pack (below)
+#endif
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <int CT, bool FAST>
+__device__ __forceinline__ uint32_t make_tokens16_v2(const float* h, const Params& P, const uint16_t* tab, int g3, int rem,
+                                                     uint32_t* tvs, uint32_t (&lp)[ENC_K / 4], bool& neg1) {
+#pragma unroll
+    for (int q = 0; q < ENC_K / 4; q++) lp[q] = 0u;
+    float dm[ENC_K];
+    if (CT != 6) {
+        float t3[ENC_K + 2];                                             // 3 h[k], k < 18 (b1 and b2 of every token)
+#pragma unroll
+        for (int k = 0; k < ENC_K + 2; k += 2) {
+            const f32x2 a = {h[k], h[k + 1]};
+            const f32x2 m = a * 3.0f;
+            t3[k] = m.x; t3[k + 1] = m.y;
+        }
+#pragma unroll
+        for (int j = 0; j < ENC_K; j += 2) {
+            const f32x2 x = {h[3 + j], h[4 + j]}, b1 = {h[2 + j], h[3 + j]}, b2 = {h[1 + j], h[2 + j]},
+                        b3 = {h[j], h[1 + j]}, c1 = {t3[2 + j], t3[3 + j]}, c2 = {t3[1 + j], t3[2 + j]};
+            const f32x2 p2 = (b1 + b1) - b2;                             // __fmul_rn(2, b1) is exact: b1 + b1
+            const f32x2 p3 = (c1 - c2) + b3;
+            const f32x2 d1 = b1 - x, d2 = p2 - x, d3 = p3 - x;
+            dm[j] = fminf(fminf(fabsf(d1.x), fabsf(d2.x)), fabsf(d3.x));
+            dm[j + 1] = fminf(fminf(fabsf(d1.y), fabsf(d2.y)), fabsf(d3.y));
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < ENC_K; j++) {
+        const float xf = h[3 + j];
+        const uint32_t u = __float_as_uint(xf);
+        uint32_t v;
+        int l;
+        if (CT == 11) {
+            v = u; l = 32;
+        } else {
+            const uint32_t i9 = u >> 23;
+            const uint32_t e = tab[i9];
+            v = u >> (e & 31u);
+            l = (int)(e >> 8);
+            if (CT == 7) {
+                const bool f0 = (u >> 15) == P.mask17;
+                v ^= f0 ? P.K0 : (i9 == (P.mask17 >> 8) ? P.K1 : 0u);
+                l = f0 ? P.lm0 : l;
+            }
+        }
+        if (CT != 6) {
+            const bool pr = (FAST ? true : j >= g3) && dm[j] <= P.thr_le;
+            const bool z = fabsf(xf) <= P.thr_lt;
+            if (__builtin_expect(__any(pr), 0)) {                        // (rare in ordinary data) the predicted code
+                float d1, d2, d3;
+                pred_dists(xf, h[2 + j], h[1 + j], h[j], d1, d2, d3);
+                const float d12 = fminf(d1, d2);
+                const uint32_t code = d3 < d12 ? 7u : (d2 < d1 ? 6u : 5u);
+                v = pr ? code : v;
+            }
+            v = z ? 4u : v;
+            l = (pr || z) ? 3 : l;
+            neg1 |= xf == -1.0f;                                         // the reference's sentinel
+        }
+        if (!FAST) l = j < rem ? l : 0;                                  // past the end: no token
+        asm volatile("" : "+v"(v), "+v"(l));                             // made here: no compare mask outlives it
+        tvs[ENC_TPB * j] = v;
+        lp[j >> 2] |= (uint32_t)l << (8 * (j & 3));
+    }
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < ENC_K / 4; q++) sum = __builtin_amdgcn_sad_u8(lp[q], 0u, sum);
+    return sum;
+}
+
 // the 16 tokens of a thread: values to tvs[256 j], lengths packed 4 per word in lp, their sum.  Not FAST: the
 // thread's elements j >= rem are past the end (no token), those j < g3 precede global index 3 (no prediction)
 template <int CT, bool FAST>
 __device__ __forceinline__ uint32_t make_tokens16(const float* h, const Params& P, const uint16_t* tab, int g3, int rem,
                                                   uint32_t* tvs, uint32_t (&lp)[ENC_K / 4], bool& neg1) {
+    if (DC_ENC_V2 & 1) return make_tokens16_v2<CT, FAST>(h, P, tab, g3, rem, tvs, lp, neg1);
     if (DC_TOK_ALU) return make_tokens16_alu<CT, FAST>(h, P, tab, g3, rem, tvs, lp, neg1);
     uint32_t sum = 0;
 #pragma unroll
@@ -1245,11 +1333,45 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
     const uint32_t off = wpre + inc - mysum;                              // the thread's first tile bit
     long long lb_s0 = 0;
     if (DC_LB_DMA && scan && !DC_SCAN_POLL && wid == 0 && tile > 0) lb_s0 = lb_dma(st, (long long)tile - 1, lbw);
+    // (r06, DC_LB_EARLY = K > 0) wave 0 requests the first look-back window (K x 64 states) into registers here,
+    // before the pack: the barriers wait only for LDS (lgkmcnt), so the state round trip overlaps the pack
+    uint64_t lbv[DC_LB_EARLY > 0 ? DC_LB_EARLY : 1];
+    if (DC_LB_EARLY && !HELP && !DC_LB_DMA && scan && !DC_SCAN_POLL && wid == 0 && tile > 0) {
+        const uint64_t* p = st + ((long long)tile - 1 - lane);
+#pragma unroll
+        for (int k = 0; k < (DC_LB_EARLY > 0 ? DC_LB_EARLY : 1); k++) lbv[k] = ld_relaxed(p - 64 * k);
+    }
     __syncthreads();                                                      // every thread has its tokens back
     // ---- pack, MSB-first.  Full tiles: every thread holds >= 48 bits, so a word is shared by at most
     // two neighbouring threads: each writes the words it completes, its first merged with the previous
     // lane's unfinished last one (DPP); a wave's first and last words are merged after the barrier
-    if (full) {
+    // (r06, DC_ENC_V2) Branch-free instead: the buffer is cleared and every token ORed into the (at most) two
+    // words it touches.  A token of l bits at tile bit o ends at e = (o & 31) + l < 64; with sh = (o + l) & 31
+    // (v_alignbit's own 5-bit shift), alignbit(0, v, sh) is its part of word o >> 5 when e >= 32 (and
+    // alignbit(v, 0, sh) its part of the next word), alignbit(v, 0, sh) its part of word o >> 5 when e < 32.
+    // ~8 VALU per token against ~17 for the register word assembly with its per-lane branches.
+    if ((DC_ENC_V2 & 2) && full) {
+        uint4* sb4 = reinterpret_cast<uint4*>(sb);
+#pragma unroll
+        for (int i = 0; i < ENC_TILE / 4 / ENC_TPB; i++) sb4[tid + ENC_TPB * i] = make_uint4(0u, 0u, 0u, 0u);
+        if (tid < (E3_WORDS - ENC_TILE) / 4) sb4[ENC_TILE / 4 + tid] = make_uint4(0u, 0u, 0u, 0u);
+        __syncthreads();
+        uint32_t o = off, a = (off >> 3) & ~3u;                           // the token's bit; its word's byte
+        char* sbc = reinterpret_cast<char*>(sb);
+#pragma unroll
+        for (int j = 0; j < ENC_K; j++) {
+            const uint32_t l = (lp[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            const uint32_t on = o + l, an = (on >> 3) & ~3u;
+            const uint32_t A = __builtin_amdgcn_alignbit(0u, tv[j], on), B = __builtin_amdgcn_alignbit(tv[j], 0u, on);
+            const bool big = an != a;
+            __hip_atomic_fetch_or(reinterpret_cast<uint32_t*>(sbc + a), big ? A : B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_or(reinterpret_cast<uint32_t*>(sbc + a + 4), big ? B : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            o = on;
+            a = an;
+        }
+        if (lane == 0) s_hi[wid] = 0xFFFFFFFFu;
+        if (lane == 63) s_ti[wid] = 0xFFFFFFFFu;
+    } else if (full) {
         uint32_t wi = off >> 5, nb = off & 31u, headw = 0u;
         const uint32_t hi = wi;
         uint64_t acc = 0;
@@ -1339,6 +1461,8 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
                 if (DC_LB_DMA) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the window's LDS writes landed
                     bad = enc_lookback<DC_LB_KS>(st, tile, tag, G, lbst, start_bit, lbw, lb_s0);
+                } else if (DC_LB_EARLY && !HELP) {
+                    bad = enc_lookback<(DC_LB_EARLY > 0 ? DC_LB_EARLY : 1)>(st, tile, tag, G, lbst, start_bit, nullptr, 0, lbv);
                 } else {
                     if constexpr (HELP)
                         bad = enc_lookback<DC_LB_KS>(st, tile, tag, G, lbst, start_bit, nullptr, 0, nullptr,
