@@ -890,6 +890,56 @@ def line_for(C, W, R, steps):
             "kernels_ms": {k: round(v[0], 4) for k, v in kernels.items()}}
 
 
+def prepass_chain(C, log2n, bound, reps=5):
+    """The bitmask chain's pre-passes + encode (impl/pingpong.c:148-209: toSmallDataset_float, med_dataset_float of
+    data_small, the mask, myCompress_bitwise_mask of data_small) on the raw U10 input in HBM, wall time per chain
+    (outside the bench's timed step, like the reference apps' pre-passes): `separate` = dc_to_small_device (x - min
+    written) + dc_med_device + dc_encode_device, `fused` = dc_prep_device (x - min never written) +
+    dc_encode_sub_device.  The fused chain's stream hash is checked against the oracle's for the main workload."""
+    import torch
+    L, dev = C.L, C.dev
+    L.set_bound(bound)
+    n = 1 << log2n
+    x = torch.from_numpy(gen_input("u10", n, 0)).to(dev)
+    y = torch.empty_like(x)
+    cap = L.stream_capacity(n)
+    s1 = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    s2 = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+
+    def mask(mean):
+        return int(np.array([mean], np.float32).view(np.uint32)[0] >> 15)
+
+    def separate():
+        mn = L.to_small_device(x.data_ptr(), n, y.data_ptr())
+        mean, t = L.med_device(y.data_ptr(), n)
+        L.encode_device(7, y.data_ptr(), n, s1.data_ptr(), type_=t, mask17=mask(mean))
+        return float(mn), float(mean), t, L.encode_result()
+
+    def fused():
+        mn, mean, t = L.prep_device(x.data_ptr(), n)
+        L.encode_sub_device(7, x.data_ptr(), n, mn, s2.data_ptr(), type_=t, mask17=mask(mean))
+        return float(mn), float(mean), t, L.encode_result()
+
+    out = {}
+    for name, f in (("separate", separate), ("fused", fused)):
+        f()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            r = f()
+        out[name] = (round((time.perf_counter() - t0) / reps * 1e3, 4), r)
+    bits = out["fused"][1][3]
+    g = golden_entry(7, "u10", log2n, bound, 1)
+    sh = L.hash_device(s2.data_ptr(), (bits + 7) // 8)
+    res = {"separate_ms": out["separate"][0], "fused_ms": out["fused"][0],
+           "same_results": out["separate"][1] == out["fused"][1] and bool(torch.equal(s1[:(bits + 7) // 8], s2[:(bits + 7) // 8])),
+           "self_check": None if g is None else (int(g["nbits"]) == bits and int(g["stream"]) == sh),
+           "workload": f"CT7 U10 2^{log2n} raw input, bound {bound:g}: min + mean of x - min + mask + encode"}
+    del x, y, s1, s2
+    torch.cuda.empty_cache()
+    return res
+
+
 def side_config(C, ct, kind, log2n, steps, warmup, bound, ber=0.0):
     """A BASELINE config / sweep point on this GPU (N=1): prepared, timed, summarised, freed."""
     import torch
@@ -1031,6 +1081,7 @@ def main():
         res["sweep"] = {}
         for lg in (14, 18, 22, 28):
             res["sweep"][f"2^{lg}"] = side_config(C, 7, "u10", lg, max(5, args.steps // 4), 2, args.bound)
+        res["prepass_chain"] = prepass_chain(C, 26, args.bound)
         res["configs"] = {
             "config2_ct6_u10_2^26": side_config(C, 6, "u10", 26, max(5, args.steps // 4), 2, args.bound),
             "config3_ct7_eq_2^28": side_config(C, 7, "eq", 28, max(5, args.steps // 4), 2, args.bound),
@@ -1043,6 +1094,7 @@ def main():
     bad = [nm for nm, ok in [("main", res["self_check"])] + [(f"sweep {k}", v.get("self_check")) for k, v in
                                                                res.get("sweep", {}).items()]
            + [(k, v.get("self_check")) for k, v in res.get("configs", {}).items()]
+           + [("prepass_chain", res.get("prepass_chain", {}).get("self_check"))]
            + [("end_to_end", res.get("end_to_end", {}).get("self_check")),
               ("ct9_exchange", res.get("ct9_exchange", {}).get("self_check"))] if ok is False]
     if C.dist is not None:

@@ -91,15 +91,7 @@ __global__ __launch_bounds__(256) void min_final_kernel(const float* __restrict_
     }
 }
 
-// a - b as the reference's x86 build computes it (SSE subss): a NaN operand propagates quieted, the first one
-// when both are, and an invalid result (inf - inf) is the default NaN 0xFFC00000 -- the GPU's fsub returns
-// 0x7FC00000 in every case
-__device__ __forceinline__ float sub_x86(float a, float b) {
-    if (__builtin_expect(a != a, 0)) return __uint_as_float(__float_as_uint(a) | 0x00400000u);
-    if (__builtin_expect(b != b, 0)) return __uint_as_float(__float_as_uint(b) | 0x00400000u);
-    const float r = __fsub_rn(a, b);
-    return r != r ? __uint_as_float(0xFFC00000u) : r;
-}
+// (sub_x86, the reference's x86 subtraction: dc_device.h)
 __global__ __launch_bounds__(256) void sub_min_kernel(const float* __restrict__ x, long long n,
                                                       const float* __restrict__ mn, float* __restrict__ y) {
     const float m = *mn;
@@ -115,6 +107,17 @@ __global__ __launch_bounds__(256) void sub_min_kernel(const float* __restrict__ 
     for (long long i = (n4 << 2) + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (long long)gridDim.x * blockDim.x)
         y[i] = sub_x86(x[i], m);
+}
+
+// y = x - m for a value m (dc_encode_sub_device's fallback: the variants that do not subtract while loading)
+__global__ __launch_bounds__(256) void sub_val_kernel(const float* __restrict__ x, long long n, float m, float* __restrict__ y) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        y[i] = sub_x86(x[i], m);
+}
+extern "C" int dc_launch_sub_value(const float* x, long long n, float m, float* y, hipStream_t st) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(sub_val_kernel, dim3((unsigned)min((n + 255) / 256, 8192ll)), dim3(256), 0, st, x, n, m, y);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // ---------------------------------------------------------------- med_dataset_float
@@ -321,6 +324,152 @@ __global__ __launch_bounds__(MC_T) void med_chunk_sum_kernel(const T* __restrict
     }
 }
 
+// ---- fused pre-passes (dc_prep_device, r06): toSmallDataset_float's minimum and med_dataset_float of x - min in
+// one read of x for the statistics, with x - min never written.  The chunk statistics of x - min
+// follow from those of x once the minimum m is known, for a FINITE m (the host falls back to the separate passes
+// otherwise): fl(x - m) >= 0 for every non-NaN x (m is the minimum), is NaN exactly where x is, and is monotone in x,
+// so its chunk max is fl(max x - m) and a chunk is all zeros exactly when its max equals m and it holds no NaN; the
+// double chunk sum only estimates the running sum's binade (the compose is exact whatever it is), so sum x - count m
+// serves.  med_chunk_stats_kernel: per chunk the double sum, the max and a NaN flag of x, and (min_partial's rule)
+// the minimum of x[1..n) in it and the index of its first zero; min_final_kernel then takes the minimum, and
+// med_sub_fix_kernel turns the statistics into those of x - m.
+__global__ __launch_bounds__(MC_T) void med_chunk_stats_kernel(const float* __restrict__ x, long long n, MedScratch<float> M,
+                                                               float* __restrict__ pv, long long* __restrict__ pi) {
+    __shared__ double ws[MC_T / 64];
+    __shared__ float wm[MC_T / 64], wn[MC_T / 64];
+    __shared__ long long wz[MC_T / 64];
+    const long long c = blockIdx.x;
+    if (c == 0 && threadIdx.x == 0) { *M.flag = 0u; M.res[4] = 0; }
+    float v[MC_PER];
+    load_chunk(x, n, c, v);
+    const long long e0 = c * MC + (long long)threadIdx.x * MC_PER;
+    double sm = 0.0;
+    float mx = -INFINITY, mn = __int_as_float(0x7fc00000);
+    long long fz = (long long)1 << 62;
+    bool nan = false;
+#pragma unroll
+    for (int i = 0; i < MC_PER; i++)
+        if (e0 + i < n) {
+            sm += (double)v[i];
+            mx = v[i] > mx ? v[i] : mx;                          // NaNs never win
+            nan |= v[i] != v[i];
+            if (e0 + i > 0) {                                    // (element 0 is the reference's start value)
+                mn = fminf(mn, v[i]);                            // NaN ignored (minNum)
+                if (v[i] == 0.f) fz = min(fz, e0 + i);
+            }
+        }
+    const bool anynan = __syncthreads_or(nan);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        sm += __shfl_xor(sm, d, 64);
+        const float o = __shfl_xor(mx, d, 64);
+        mx = o > mx ? o : mx;
+        mn = fminf(mn, __shfl_xor(mn, d, 64));
+        fz = min(fz, (long long)__shfl_xor(fz, d, 64));
+    }
+    if ((threadIdx.x & 63) == 0) { ws[threadIdx.x >> 6] = sm; wm[threadIdx.x >> 6] = mx; wn[threadIdx.x >> 6] = mn; wz[threadIdx.x >> 6] = fz; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        float m = -INFINITY, q = __int_as_float(0x7fc00000);
+        long long z = (long long)1 << 62;
+        for (int w = 0; w < MC_T / 64; w++) { t += ws[w]; m = wm[w] > m ? wm[w] : m; q = fminf(q, wn[w]); z = min(z, wz[w]); }
+        M.csum[c] = t;                                           // (of x: med_sub_fix_kernel turns them into x - m)
+        M.cmax[c] = m;
+        M.Z[c] = (uint8_t)(anynan ? 2 : 0);
+        pv[c] = q;
+        pi[c] = z;
+    }
+}
+
+// min_final_kernel and med_sub_fix_kernel in one workgroup of 1024 threads, every load of a thread's batch in flight
+// at once: the minimum from the nch chunk partials (one 256-thread pass over 32768 partials was 36 us of dependent
+// loads at 2^26), then the statistics of x - m
+constexpr int PF_T = 1024, PF_B = 8;
+__global__ __launch_bounds__(PF_T) void prep_min_fix_kernel(const float* __restrict__ x, long long n, MedScratch<float> M,
+                                                            const float* __restrict__ pv, const long long* __restrict__ pi,
+                                                            float* __restrict__ d_min) {
+    __shared__ float sv[PF_T / 64];
+    __shared__ long long si[PF_T / 64];
+    __shared__ float s_m;
+    const int tid = threadIdx.x;
+    const long long nch = (n + MC - 1) / MC;
+    float mv = __int_as_float(0x7fc00000);
+    long long fz = (long long)1 << 62;
+    for (long long b = 0; b < nch; b += (long long)PF_T * PF_B) {
+        float v[PF_B];
+        long long z[PF_B];
+#pragma unroll
+        for (int k = 0; k < PF_B; k++) {
+            const long long c = b + tid + (long long)k * PF_T;
+            v[k] = c < nch ? pv[c] : __int_as_float(0x7fc00000);
+            z[k] = c < nch ? pi[c] : (long long)1 << 62;
+        }
+#pragma unroll
+        for (int k = 0; k < PF_B; k++) { mv = fminf(mv, v[k]); fz = min(fz, z[k]); }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        mv = fminf(mv, __shfl_xor(mv, d, 64));
+        fz = min(fz, (long long)__shfl_xor(fz, d, 64));
+    }
+    if ((tid & 63) == 0) { sv[tid >> 6] = mv; si[tid >> 6] = fz; }
+    __syncthreads();
+    if (tid == 0) {
+        float m = __int_as_float(0x7fc00000);
+        long long z = (long long)1 << 62;
+        for (int w = 0; w < PF_T / 64; w++) { m = fminf(m, sv[w]); z = min(z, si[w]); }
+        const float x0 = x[0];
+        float r = x0;                                        // (min_final_kernel's rule)
+        if (!(m != m) && m < x0) r = m == 0.f ? x[z] : m;
+        *d_min = r;
+        s_m = r;
+        if (!isfinite(r)) M.res[4] = 1;
+    }
+    __syncthreads();
+    const float m = s_m;
+    if (!isfinite(m)) return;
+    for (long long b = 0; b < nch; b += (long long)PF_T * PF_B) {
+        double t[PF_B];
+        float mx[PF_B];
+        uint8_t zz[PF_B];
+#pragma unroll
+        for (int k = 0; k < PF_B; k++) {
+            const long long c = min(b + tid + (long long)k * PF_T, nch - 1);
+            t[k] = M.csum[c]; mx[k] = M.cmax[c]; zz[k] = M.Z[c];
+        }
+#pragma unroll
+        for (int k = 0; k < PF_B; k++) {
+            const long long c = b + tid + (long long)k * PF_T;
+            if (c < nch) {
+                const long long cnt = min((long long)MC, n - c * MC);
+                M.csum[c] = isfinite(t[k]) ? t[k] - (double)cnt * (double)m : 0.0;
+                M.cmax[c] = mx[k] == -INFINITY ? mx[k] : sub_fin(mx[k], m);
+                M.Z[c] = (uint8_t)(zz[k] | (!(zz[k] & 2) && mx[k] == m ? 1 : 0));
+            }
+        }
+    }
+}
+
+// the statistics of x - m (m = *d_min): a non-finite m sets res[4] (the host then runs the separate passes)
+__global__ __launch_bounds__(256) void med_sub_fix_kernel(long long n, MedScratch<float> M, const float* __restrict__ d_min) {
+    const float m = *d_min;
+    const long long nch = (n + MC - 1) / MC;
+    if (!isfinite(m)) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) M.res[4] = 1;
+        return;
+    }
+    for (long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x; c < nch; c += (long long)gridDim.x * blockDim.x) {
+        const long long cnt = min((long long)MC, n - c * MC);
+        const double t = M.csum[c];
+        const float mx = M.cmax[c];
+        const uint8_t z = M.Z[c];
+        M.csum[c] = isfinite(t) ? t - (double)cnt * (double)m : 0.0;
+        M.cmax[c] = mx == -INFINITY ? mx : sub_fin(mx, m);    // (a chunk of NaNs only keeps -inf)
+        M.Z[c] = (uint8_t)(z | (!(z & 2) && mx == m ? 1 : 0));
+    }
+}
+
 // exclusive scan of the chunk sums -> an estimate of the running sum at every chunk and its binade E_est.
 // Tiles of 8192 chunks: coalesced loads into LDS (the next tile's loads issued before this tile's scan), 8
 // consecutive chunks per thread, a block scan, the binades back through LDS and out coalesced (runs of
@@ -436,7 +585,7 @@ __device__ __forceinline__ void compose(D& a0, D& a1, int& q0, int& q1, D b0, D 
 // elements; the W binades [E_est + wlo, E_est + wlo + W) -> Td / F slots 0..W-1
 template <typename T, int W>
 __global__ __launch_bounds__(256) void med_chunk_trans_kernel(const T* __restrict__ x, long long n, MedScratch<T> M,
-                                                             int gated) {
+                                                             int gated, const T* __restrict__ sub = nullptr) {
     typedef MedFP<T> FP;
     typedef typename FP::D D;
     if (gated && __hip_atomic_load(M.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
@@ -446,6 +595,11 @@ __global__ __launch_bounds__(256) void med_chunk_trans_kernel(const T* __restric
         T v[MT_PER];
         const long long e0 = c * MC + (long long)lane * MT_PER;
         load_run<T, MT_PER>(x, n, e0, v);
+        if (sub) {                                                  // (dc_prep_device: the elements of x - min)
+            const T m = *sub;
+#pragma unroll
+            for (int i = 0; i < MT_PER; i++) v[i] = sub_fin(v[i], m);
+        }
         const int cnt = (int)max(0ll, min((long long)MT_PER, n - e0));
         const int elo = M.eest[c] + med_wlo<W>();
         const T cmax = M.cmax[c];
@@ -773,7 +927,8 @@ template <typename T, int W>
 __global__ __launch_bounds__(MXC_T) void med_compose_kernel(const T* __restrict__ x, long long n, T s_init,
                                                            MedScratch<T> M, T* __restrict__ out_mean,
                                                            int* __restrict__ out_type, T* __restrict__ out_sum,
-                                                           T* __restrict__ out_max, int gated) {
+                                                           T* __restrict__ out_max, int gated,
+                                                           const T* __restrict__ sub = nullptr) {
     typedef MedFP<T> FP;
     typedef typename FP::D D;
     typedef typename FP::U U;
@@ -923,6 +1078,11 @@ __global__ __launch_bounds__(MXC_T) void med_compose_kernel(const T* __restrict_
             const long long e = c * MC + 2ll * tid;
             v2[0] = 2 * tid < m ? x[e] : (T)0;
             v2[1] = 2 * tid + 1 < m ? x[e + 1] : (T)0;
+            if (sub) {
+                const T mn = *sub;
+                if (2 * tid < m) v2[0] = sub_fin(v2[0], mn);
+                if (2 * tid + 1 < m) v2[1] = sub_fin(v2[1], mn);
+            }
         }
         int i0 = 0;
         for (int it = 0; i0 < m; it++) {
@@ -1061,7 +1221,7 @@ __global__ __launch_bounds__(MXC_T) void med_compose_kernel(const T* __restrict_
     if ((tid & 63) == 0) smx[tid >> 6] = mx;
     __syncthreads();
     if (tid == 0) {
-        T mm = x[0];
+        T mm = sub ? sub_fin(x[0], *sub) : x[0];
         for (int i = 0; i < MXC_T / 64; i++) if (smx[i] > mm) mm = smx[i];
         const T mean = FP::mean(s, n);
         const int ty = FP::type(mm);
@@ -1188,6 +1348,34 @@ static int launch_med(const T* x, long long n, T s_init, void* scratch, T* d_mea
         hipLaunchKernelGGL((med_chunk_trans_kernel<T, MW>), dim3(tg), dim3(256), 0, st, x, n, M, 0);
         hipLaunchKernelGGL((med_compose_kernel<T, MW>), dim3(1), dim3(MXC_T), 0, st, x, n, s_init, M, d_mean, d_type,
                            d_sum, d_max, 0);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// dc_prep_device's kernels: wide 0 -- statistics of x and the minimum (into *d_min), the statistics of x - m, the
+// binade estimates, the narrow window's transducers and compose; wide 1 -- the wide window after a narrow miss (the
+// statistics of that call are in the scratch).  pv / pi: nch partial minima.  The result words as dc_launch_med's,
+// plus res[4] = 1 when the minimum is not finite (nothing else is valid then)
+extern "C" int dc_launch_med_sub(const float* x, long long n, void* scratch, float* d_min, float* pv, long long* pi,
+                                 float* d_mean, int* d_type, int wide, hipStream_t st) {
+    if (n <= 0) return 0;
+    const long long nch = (n + MC - 1) / MC;
+    const MedScratch<float> M = med_scratch<float>(scratch, nch);
+    const unsigned tg = med_trans_grid(nch);
+    if (wide != 1) {                                     // (2: the wide window on a fresh array, DC_MED_WIDE=1)
+        hipLaunchKernelGGL(med_chunk_stats_kernel, dim3((unsigned)nch), dim3(MC_T), 0, st, x, n, M, pv, pi);
+        hipLaunchKernelGGL(prep_min_fix_kernel, dim3(1), dim3(PF_T), 0, st, x, n, M, (const float*)pv,
+                           (const long long*)pi, d_min);
+        hipLaunchKernelGGL(med_chunk_scan_kernel<float>, dim3(1), dim3(1024), 0, st, M, nch, 0.0f);
+    }
+    if (!wide) {
+        hipLaunchKernelGGL((med_chunk_trans_kernel<float, MWN>), dim3(tg), dim3(256), 0, st, x, n, M, 0, (const float*)d_min);
+        hipLaunchKernelGGL((med_compose_kernel<float, MWN>), dim3(1), dim3(MXC_T), 0, st, x, n, 0.0f, M, d_mean, d_type,
+                           (float*)nullptr, (float*)nullptr, 0, (const float*)d_min);
+    } else {
+        hipLaunchKernelGGL((med_chunk_trans_kernel<float, MW>), dim3(tg), dim3(256), 0, st, x, n, M, 0, (const float*)d_min);
+        hipLaunchKernelGGL((med_compose_kernel<float, MW>), dim3(1), dim3(MXC_T), 0, st, x, n, 0.0f, M, d_mean, d_type,
+                           (float*)nullptr, (float*)nullptr, 0, (const float*)d_min);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

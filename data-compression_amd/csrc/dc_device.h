@@ -512,6 +512,23 @@ __device__ __forceinline__ uint32_t wave_total(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_incl(v), 63);
 }
 
+// a - b as the reference's x86 build computes it (SSE subss): a NaN operand propagates quieted, the first one
+// when both are, and an invalid result (inf - inf) is the default NaN 0xFFC00000 -- the GPU's fsub returns
+// 0x7FC00000 in every case
+__device__ __forceinline__ float sub_x86(float a, float b) {
+    if (__builtin_expect(a != a, 0)) return __uint_as_float(__float_as_uint(a) | 0x00400000u);
+    if (__builtin_expect(b != b, 0)) return __uint_as_float(__float_as_uint(b) | 0x00400000u);
+    const float r = __fsub_rn(a, b);
+    return r != r ? __uint_as_float(0xFFC00000u) : r;
+}
+// the same for a FINITE b (the fused pre-passes subtract a finite minimum; their host falls back otherwise): the
+// result is NaN only when a is, and then it is a quieted
+__device__ __forceinline__ float sub_fin(float a, float b) {
+    const float r = __fsub_rn(a, b);
+    return a != a ? __uint_as_float(__float_as_uint(a) | 0x00400000u) : r;
+}
+__device__ __forceinline__ double sub_fin(double a, double b) { return __dsub_rn(a, b); }   // (float path only)
+
 __device__ __forceinline__ uint64_t ld_relaxed(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

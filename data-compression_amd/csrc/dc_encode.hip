@@ -1284,6 +1284,11 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
         for (int k = 1; k <= 3; k++) {
             const long long e = w0 - k;
             hw[k - 1] = (e < n && e >= -3 && idx0 + e >= 0) ? x[e] : 0.0f;
+            if (!CRC && !HELP && P.sub && e < n && e >= -3 && idx0 + e >= 0) hw[k - 1] = sub_fin(hw[k - 1], P.submin);
+        }
+        if (!CRC && !HELP && P.sub) {                                      // (dc_encode_sub_device: x - min)
+#pragma unroll
+            for (int j = 0; j < ENC_K; j++) h[3 + j] = sub_fin(h[3 + j], P.submin);
         }
         h[2] = wave_shr1(h[3 + ENC_K - 1], hw[0]);
         h[1] = wave_shr1(h[3 + ENC_K - 2], hw[1]);
@@ -2061,6 +2066,9 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
             if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
                 cus = 256;
         }
+        // (dc_encode_sub_device: only the plain single-pass instantiation subtracts the minimum while loading; for
+        // the others the host writes x - min first and encodes that)
+        if (P->sub && (crc_blk || !scan || (pipe && flag) || g_enc_help || g_enc_mirror)) return -3;
         g_enc_crc_fused = 0;
         // (the CT9 sender: the stream's CRC pieces while the words are stored; the chained look-back variant
         // has no fused CRC: it encodes plainly and the host takes a CRC pass, dc_encode_crc_fused_last)
@@ -2111,6 +2119,7 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
         dc_mark_phase(1, stream);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
+    if (P->sub) return -3;
     uint32_t* tbits = reinterpret_cast<uint32_t*>(desc + ntiles);
     uint32_t* tails = tbits + ntiles + (ntiles & 1u);
     uint16_t* psum16 = reinterpret_cast<uint16_t*>(tails + ntiles + (ntiles & 1u));

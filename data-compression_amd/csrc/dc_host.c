@@ -107,6 +107,9 @@ typedef struct {
     /* aux */
     float* part_v; long long* part_i;
     float* d_f;                      /* [0] min [1] mean */
+    void* prep_part; size_t prep_part_cap;  /* dc_prep_device: the chunks' partial minima (float) and first zeros (i64) */
+    void* sub_buf; size_t sub_buf_cap;      /* x - min written out: dc_prep_device / dc_encode_sub_device fallbacks */
+    const float* enc_sub;                   /* encode_on: the minimum to subtract while loading (NULL: none) */
     void* med_scr; size_t med_scr_cap;  /* exact mean: chunk transducers (dc_med_scratch_bytes) */
     int med_wide;                        /* the last exact mean needed the wide binade window */
     int* d_i;                        /* [0] type */
@@ -324,6 +327,7 @@ static float thr_le(double bound) {
 }
 
 static void make_params(Params* P, int ct, int type, uint32_t mask17) {
+    memset(P, 0, sizeof *P);                         /* (P->sub = 0: dc_encode_sub_device sets it) */
     P->ct = ct;
     P->B = bound_binary(absErrBound);
     P->thr_lt = thr_lt(absErrBound);
@@ -436,6 +440,23 @@ int dc_encode_crc_device(int ct, const void* d_x, long long n, long long idx0, i
     return DC_OK;
 }
 
+/* dc_launch_encode, and for an encode of x - min (P->sub) that the chosen variant cannot subtract while loading
+   (dc_launch_encode returns -3: the three-launch retry, the CRC / send / helping instantiations), x - min written
+   into sub_buf first and encoded from there */
+static int launch_enc(const float* x, long long n, long long idx0, const Params* P, uint32_t* out, uint64_t* desc,
+                      unsigned* flag, uint32_t epoch, int start_bit, unsigned long long* tb, unsigned long long* tb2,
+                      unsigned* err, unsigned long long* dbg, int mode, const uint32_t* ctab, uint32_t* cblk,
+                      hipStream_t st) {
+    const int r = dc_launch_encode(x, n, idx0, P, out, desc, flag, epoch, start_bit, tb, tb2, err, dbg, mode, ctab, cblk, st);
+    if (r != -3) return r;
+    if (grow(&G.sub_buf, &G.sub_buf_cap, (size_t)n * 4 + 64)) return -1;
+    if (dc_launch_sub_value(x, n, P->submin, (float*)G.sub_buf, st)) return -1;
+    Params Q = *P;
+    Q.sub = 0;
+    return dc_launch_encode((const float*)G.sub_buf, n, idx0, &Q, out, desc, flag, epoch, start_bit, tb, tb2, err, dbg,
+                            mode, ctab, cblk, st);
+}
+
 static int encode_on(hipStream_t st, int ct, const void* d_x, long long n, long long idx0, int type, uint32_t mask17,
                      int start_bit, void* d_out, unsigned long long* d_total_bits, uint32_t* crc_blk) {
     if (!valid_ct(ct)) return seterr(DC_ERR_ARG, "unsupported CT %d", ct);
@@ -445,6 +466,18 @@ static int encode_on(hipStream_t st, int ct, const void* d_x, long long n, long 
     if (((uintptr_t)d_x & 15u) || ((uintptr_t)d_out & 3u)) return seterr(DC_ERR_ARG, "misaligned device buffer");
     Params P;
     make_params(&P, ct, type, mask17);
+    if (G.enc_sub) {                                 /* dc_encode_sub_device */
+        if (idx0) return seterr(DC_ERR_ARG, "encode of x - min: idx0 must be 0");
+        P.sub = 1;
+        P.submin = *G.enc_sub;
+        if (!isfinite(P.submin)) {                   /* (the kernels' subtraction assumes a finite minimum) */
+            if (n > 0 && (grow(&G.sub_buf, &G.sub_buf_cap, (size_t)n * 4 + 64) ||
+                          dc_launch_sub_value((const float*)d_x, n, P.submin, (float*)G.sub_buf, st)))
+                return seterr(DC_ERR_HIP, "x - min launch failed");
+            d_x = G.sub_buf;
+            P.sub = 0;
+        }
+    }
     if (dc_encode_desc_words(n) + 8 > G.enc_desc_cap) {
         if (G.enc_desc) HIPCHK(hipFree(G.enc_desc));
         long long cap = dc_encode_desc_words(n) + 1024;
@@ -471,7 +504,7 @@ static int encode_on(hipStream_t st, int ct, const void* d_x, long long n, long 
         HIPCHK(hipMemsetAsync(G.d_enc_flag, 0, 4096, st));
         G.enc_epoch = 1;
     }
-    if (dc_launch_encode((const float*)d_x, n, idx0, &P, (uint32_t*)d_out, G.enc_desc, G.d_enc_flag, G.enc_epoch,
+    if (launch_enc((const float*)d_x, n, idx0, &P, (uint32_t*)d_out, G.enc_desc, G.d_enc_flag, G.enc_epoch,
                          start_bit, tot, tot != G.d_total ? G.d_total : NULL, G.d_enc_err, G.enc_dbg, 0,
                          crc_blk ? G.d_crcf : NULL, crc_blk, st))
         return seterr(DC_ERR_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
@@ -557,7 +590,7 @@ static int encode_retry(hipStream_t st) {
     }
     unsigned long long* tot = G.last_enc.tot;
     dc_set_encode_mirror(G.last_enc.mirror);
-    const int lrc = dc_launch_encode(G.last_enc.x, G.last_enc.n, G.last_enc.idx0, &G.last_enc.P, G.last_enc.out,
+    const int lrc = launch_enc(G.last_enc.x, G.last_enc.n, G.last_enc.idx0, &G.last_enc.P, G.last_enc.out,
                                      G.enc_desc, G.d_enc_flag, G.enc_epoch, G.last_enc.start_bit, tot,
                                      tot != G.d_total ? G.d_total : NULL, G.d_enc_err, NULL, 3, NULL, NULL, st);
     dc_set_encode_mirror(NULL);
@@ -1363,6 +1396,65 @@ int dc_med_device(const void* d_x, long long n, float* mean_out, int* type_out) 
     if (mean_out) *mean_out = m;
     if (type_out) *type_out = t;
     return DC_OK;
+}
+
+/* The reference's pre-passes for the bitmask codecs (impl/pingpong.c:148-206: min = toSmallDataset_float(data,
+ * &data_small); medium = med_dataset_float(data_small, &type)) on device data, fused: one read of x for
+ * the minimum and the chunk statistics, the exact mean of x - min from x itself; x - min is never written.  With
+ * dc_encode_sub_device the whole chain (min, mean, mask, encode of data_small) reads x three times and writes
+ * only the stream.  A non-finite minimum (NaN or infinite data[0] / data) takes the separate passes.  Synchronous. */
+int dc_prep_device(const void* d_x, long long n, float* min_out, float* mean_out, int* type_out) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (n <= 0) return seterr(DC_ERR_ARG, "empty input");
+    if (((uintptr_t)d_x & 15u)) return seterr(DC_ERR_ARG, "misaligned device buffer");
+    const long long nch = (n + 2047) / 2048;
+    if (grow(&G.med_scr, &G.med_scr_cap, (size_t)dc_med_scratch_bytes(n)) ||
+        grow(&G.prep_part, &G.prep_part_cap, (size_t)nch * 12 + 64))
+        return DC_ERR_HIP;
+    float* pv = (float*)G.prep_part;
+    long long* pi = (long long*)((char*)G.prep_part + (((size_t)nch * 4 + 15) & ~(size_t)15));
+    float mn = 0.0f, m = 0.0f;
+    int t = 0;
+    const int forced = med_force_wide();
+    for (int wide = forced; wide < 2; wide++) {     /* the narrow window, then the wide one if it missed */
+        if (dc_launch_med_sub((const float*)d_x, n, G.med_scr, &G.d_f[0], pv, pi, &G.d_f[1], &G.d_i[0],
+                              wide && forced ? 2 : wide, G.st))
+            return seterr(DC_ERR_HIP, "prep launch failed");
+        long long r[6];                              /* flag, mean, type, sum, max, minimum not finite */
+        HIPCHK(hipMemcpyAsync(r, dc_med_flag_ptr(G.med_scr, n, 0), sizeof r, hipMemcpyDeviceToHost, G.st));
+        HIPCHK(hipMemcpyAsync(&mn, &G.d_f[0], 4, hipMemcpyDeviceToHost, G.st));
+        HIPCHK(hipStreamSynchronize(G.st));
+        if (r[5]) {                                  /* the separate passes: x - min written out */
+            if (grow(&G.sub_buf, &G.sub_buf_cap, (size_t)n * 4 + 64)) return DC_ERR_HIP;
+            if ((rc = dc_to_small_device(d_x, n, G.sub_buf, &mn)) || (rc = dc_med_device(G.sub_buf, n, &m, &t))) return rc;
+            break;
+        }
+        { const uint32_t b = (uint32_t)r[1]; memcpy(&m, &b, 4); }
+        t = (int)r[2];
+        G.med_wide = wide;
+        if (!(unsigned)r[0]) break;
+    }
+    if (min_out) *min_out = mn;
+    if (mean_out) *mean_out = m;
+    if (type_out) *type_out = t;
+    return DC_OK;
+}
+
+/* dc_encode_device of x - min (the minimum dc_prep_device returned), x - min computed while loading: the stream is
+ * the one dc_encode_device makes from toSmallDataset_float's array.  Asynchronous, as dc_encode_device. */
+int dc_encode_sub_device(int ct, const void* d_x, long long n, float min, int type, uint32_t mask17, void* d_out,
+                         unsigned long long* d_total_bits) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (G.enc_st) {
+        HIPCHK(hipEventRecord(G.ev_enc, G.st));
+        HIPCHK(hipStreamWaitEvent(G.enc_st, G.ev_enc, 0));
+    }
+    G.enc_sub = &min;
+    rc = encode_on(ENC_ST, ct, d_x, n, 0, type, mask17, 0, d_out, d_total_bits, NULL);
+    G.enc_sub = NULL;
+    return rc;
 }
 
 /* multi-GPU med_dataset_float: the exact running float sum of x[0..n) continued from s_init (the sum

@@ -33,6 +33,10 @@ typedef struct Params {  /* per-call codec parameters, computed on the host */
        mask's): flag 1 token = v ^ K1 (length lm1), flag 0 token = v ^ K0 (length lm0) */
     uint32_t K0, K1;
     int lm1;
+    /* (dc_encode_sub_device) encode x - submin instead of x, the subtraction as the reference's x86 build makes it
+       (toSmallDataset_float); the single-pass encoder only, submin finite */
+    int sub;
+    float submin;
 } Params;
 
 typedef struct Plan {    /* device-resident sizes of the stream being decoded */
@@ -224,6 +228,9 @@ int dc_launch_to_small(const float* x, long long n, float* y, float* part_v, lon
 #define DC_MIN_PARTS 2048                /* toSmallDataset: per-workgroup minima combined by min_final */
 int dc_launch_med(const float* x, long long n, float s_init, void* scratch, float* d_mean, int* d_type, float* d_sum,
                   float* d_max, dc_hip_stream st);
+int dc_launch_med_sub(const float* x, long long n, void* scratch, float* d_min, float* pv, long long* pi, float* d_mean,
+                      int* d_type, int wide, hipStream_t st);
+int dc_launch_sub_value(const float* x, long long n, float m, float* y, hipStream_t st);
 int dc_launch_med_wide(const float* x, long long n, float s_init, void* scratch, float* d_mean, int* d_type,
                        float* d_sum, float* d_max, int fresh, dc_hip_stream st);
 unsigned* dc_med_flag_ptr(void* scratch, long long n, int is_double);

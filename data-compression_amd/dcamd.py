@@ -37,7 +37,7 @@ ABI_SYMBOLS = [
 EXT_SYMBOLS = [
     "dc_init", "dc_last_error", "dc_get_stream", "dc_synchronize", "dc_set_abs_error_bound",
     "dc_get_abs_error_bound", "dc_stream_capacity", "dc_encode_device", "dc_encode_result",
-    "dc_decode_device", "dc_decode_finish", "dc_to_small_device", "dc_med_device", "dc_crc32_device",
+    "dc_decode_device", "dc_decode_finish", "dc_to_small_device", "dc_med_device", "dc_prep_device", "dc_encode_sub_device", "dc_crc32_device",
     "dc_decode_chunk_bits_value", "dc_ct1_encode_device", "dc_ct1_decode_device", "dc_encode_bits_device",
     "dc_crc32_device_async", "dc_crc32_copy_device", "dc_encode_send_device", "dc_crc32_pair_device", "dc_encode_crc_device", "dc_crc32_stream_device", "dc_crc_resend_crc_device",
     "dc_hash_device", "dc_copy_rate_device", "dc_flip_bits_device", "dc_decode_shard_device", "dc_decode_shard_fix",
@@ -96,6 +96,8 @@ class Lib:
         L.dc_decode_shard3_fix.argtypes = [vp]
         L.dc_to_small_device.argtypes = [vp, ll, vp, C.POINTER(C.c_float)]
         L.dc_med_device.argtypes = [vp, ll, C.POINTER(C.c_float), C.POINTER(C.c_int)]
+        L.dc_prep_device.argtypes = [vp, ll, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_int)]
+        L.dc_encode_sub_device.argtypes = [C.c_int, vp, ll, C.c_float, C.c_int, u32, vp, vp]
         L.dc_med_sum_device.argtypes = [vp, ll, C.c_float, C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.dc_med_shard_stats.argtypes = [vp, ll, C.POINTER(C.c_double), C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.dc_med_shard_trans.argtypes = [vp, ll, C.c_double, C.POINTER(C.c_int), C.POINTER(C.c_longlong),
@@ -576,6 +578,24 @@ class Lib:
 
     def synchronize(self):
         self.check(self.L.dc_synchronize(), "dc_synchronize")
+
+    def to_small_device(self, x_ptr, n, out_ptr):
+        """dc_to_small_device: out = x - min (toSmallDataset_float on device data); returns the minimum."""
+        mn = C.c_float(0)
+        self.check(self.L.dc_to_small_device(x_ptr, n, out_ptr, C.byref(mn)), "dc_to_small_device")
+        return np.float32(mn.value)
+
+    def prep_device(self, x_ptr, n):
+        """dc_prep_device: (min, mean, type) = toSmallDataset_float's minimum and med_dataset_float of x - min, fused
+        (x - min never written)."""
+        mn, m, t = C.c_float(0), C.c_float(0), C.c_int(0)
+        self.check(self.L.dc_prep_device(x_ptr, n, C.byref(mn), C.byref(m), C.byref(t)), "dc_prep_device")
+        return np.float32(mn.value), np.float32(m.value), t.value
+
+    def encode_sub_device(self, ct, x_ptr, n, mn, out_ptr, type_=0, mask17=0, total_ptr=None):
+        """dc_encode_sub_device: the stream of x - mn (toSmallDataset_float's array), subtracted while loading."""
+        self.check(self.L.dc_encode_sub_device(ct, x_ptr, n, float(mn), type_, mask17, out_ptr, total_ptr),
+                   "dc_encode_sub_device")
 
     def med_device(self, x_ptr, n):
         m, t = C.c_float(0), C.c_int(0)

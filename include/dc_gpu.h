@@ -141,6 +141,16 @@ int dc_set_halo_async(int on);
 /* Pre-passes on device data: toSmallDataset_float and med_dataset_float (exact). */
 int dc_to_small_device(const void* d_x, long long n, void* d_out, float* min_out);
 int dc_med_device(const void* d_x, long long n, float* mean_out, int* type_out);
+/* The two pre-passes fused, for the bitmask chain of impl/pingpong.c:148-209 (toSmallDataset_float, then
+ * med_dataset_float of data_small): min_out = toSmallDataset_float's minimum of x, mean_out / type_out =
+ * med_dataset_float of x - min, without writing x - min (one read of x for the minimum and the chunk statistics,
+ * one for the transducers).  Synchronous.  Replaces dc_to_small_device + dc_med_device on the same data. */
+int dc_prep_device(const void* d_x, long long n, float* min_out, float* mean_out, int* type_out);
+/* dc_encode_device (idx0 = 0, start_bit = 0) of x - min, the subtraction made while loading x (the reference's x86
+ * subtraction, as toSmallDataset_float): the stream myCompress_bitwise* makes from data_small
+ * (impl/dataCompression.c:3543-3562 then :2030-2284), with no data_small array.  Asynchronous. */
+int dc_encode_sub_device(int ct, const void* d_x, long long n, float min, int type, uint32_t mask17, void* d_out,
+                         unsigned long long* d_total_bits);
 /* 1 when the last dc_med_device / dc_med_sum_device needed the wide binade window: the narrow window tried
    first, [E_est - 1, E_est + 1] around the double estimate of the running sum, missed more than 16 chunks
    (DC_MED_WIDE=1 in the environment goes to the wide window at once) */
