@@ -730,6 +730,7 @@ def run_codec(C, W, steps, warmup, pipelined=False, ber=0.0, check=False):
            "kavg": kavg, "status": int(status | warm_status), "warm_status": int(warm_status), "resends": timed_resends,
            "slow_path_timed": slow[0], "v3": bool(L.L.dc_last_decode_launched_v3()),
            "runs": bool(L.L.dc_last_decode_launched_runs()), "fused": bool(L.L.dc_decode3_last_fused()),
+           "tiny": bool(L.L.dc_last_decode_launched_tiny()),
            "fused_seg": int(L.L.dc_fused3_last_seg()),
            "enc_mode": int(L.L.dc_encode_mode()), "ct9": {k: v for k, v in ct9.items() if k in ("phase_ms", "acks_ok", "nflip", "streams")}}
 
@@ -818,7 +819,7 @@ def copy_bandwidth(L, dev, n, reps=10):
     return gbs, COPY_VARIANTS[v]
 
 
-def kernel_table(ct, n, nbytes, kavg, v3=True, enc_mode=1, runs=False, fused=False):
+def kernel_table(ct, n, nbytes, kavg, v3=True, enc_mode=1, runs=False, fused=False, tiny=False):
     """The timed launches of a step (library timing slots, HIP events on the library stream) and their
     algorithmic bytes: the encoder's count and pack launches (the pack's workgroup 0 scans the tile
     offsets), then the decoder's -- the segment decoder (parse3, whose jobs check the
@@ -837,7 +838,9 @@ def kernel_table(ct, n, nbytes, kavg, v3=True, enc_mode=1, runs=False, fused=Fal
             f"encode_count_kernel<{ct}>": (k[0], 4.0 * n),
             f"encode_pack_kernel<{ct}>": (k[2], 4.0 * n + nbytes),
         }
-    if runs:              # the small-stream decoder: chunk maps + one-workgroup scans, then the values
+    if tiny:              # the one-workgroup decoder of small streams: the stream read once, the floats written
+        kernels.update({f"tiny_decode_kernel<{ct}>": (k[3] + k[5], 0.0 if fin else dec_b)})
+    elif runs:            # the small-stream decoder: chunk maps + one-workgroup scans, then the values
         kernels.update({f"runs_map_kernel<{ct}>+runs_scan_kernel<{ct}>": (k[3], 0.0 if fin else float(nbytes)),
                         f"runs_values_kernel<{ct}>": (k[5], 0.0 if fin else dec_b)})
     elif v3 and fused:    # the single-launch parse + decode: the stream read once, the floats written
@@ -871,7 +874,7 @@ def line_for(C, W, R, steps):
     n, nbytes = W["n"], R["nbytes"]
     ms = R["wall"] / steps * 1e3
     kernels = kernel_table(W["ct"], n, nbytes, R["kavg"], R["v3"], R.get("enc_mode", 1), R.get("runs", False),
-                           R.get("fused", False))
+                           R.get("fused", False), R.get("tiny", False))
     for nm, ms_ in R.get("ct9", {}).get("phase_ms", {}).items():   # CT9: every launch of the step
         kernels[nm] = (ms_, ct9_bytes(nm, nbytes, R["ct9"].get("streams", {})))
     dname = max(kernels, key=lambda k: kernels[k][0])
@@ -981,7 +984,7 @@ def main():
         print(f"bench.py: decoder status 0x{R['status']:x} in the timed steps (slow path not timed)", file=sys.stderr)
         sys.exit(1)
     kernels = kernel_table(ct, n, nbytes, R["kavg"], R["v3"], R.get("enc_mode", 1), R.get("runs", False),
-                           R.get("fused", False))
+                           R.get("fused", False), R.get("tiny", False))
     for nm, ms_ in R.get("ct9", {}).get("phase_ms", {}).items():   # (as line_for: the CT9 launches too)
         kernels[nm] = (ms_, ct9_bytes(nm, nbytes, R["ct9"].get("streams", {})))
     dname = main_line["dominant"]["kernel"]

@@ -110,6 +110,10 @@ typedef struct {
     void* prep_part; size_t prep_part_cap;  /* dc_prep_device: the chunks' partial minima (float) and first zeros (i64) */
     void* sub_buf; size_t sub_buf_cap;      /* x - min written out: dc_prep_device / dc_encode_sub_device fallbacks */
     const float* enc_sub;                   /* encode_on: the minimum to subtract while loading (NULL: none) */
+    int tiny_used, tiny_last;               /* the pending decode went to / the last finished one stayed on the
+                                               one-workgroup decoder (dc_decode_tiny.hip) */
+    int tiny_key;                           /* ct * 256 + B + 1 of parameters whose small stream it declined */
+    long long dec_max_bytes;                /* the pending decode's readable stream bytes */
     void* med_scr; size_t med_scr_cap;  /* exact mean: chunk transducers (dc_med_scratch_bytes) */
     int med_wide;                        /* the last exact mean needed the wide binade window */
     int* d_i;                        /* [0] type */
@@ -813,6 +817,18 @@ static long long dec3_min_bytes(void) {
     }
     return g_dec3_min;
 }
+/* DC_TINY=0 (or dc_set_decode_tiny(0)): small streams stay on the segment decoder */
+static int g_tiny_on = -1;
+static int tiny_on(void) {
+    if (g_tiny_on < 0) g_tiny_on = (getenv("DC_TINY") && *getenv("DC_TINY") == '0') ? 0 : 1;
+    return g_tiny_on;
+}
+int dc_set_decode_tiny(int on) {
+    const int old = tiny_on();
+    g_tiny_on = on ? 1 : 0;
+    return old;
+}
+int dc_last_decode_was_tiny(void) { return G.tiny_last; }
 /* < -1: the default; -1 disables the segment decoder; returns the previous value */
 int dc_last_decode_was_v3(void) { return G.dec3_last; }
 int dc_last_decode_used_maps(void) { return G.dec3_last && G.dec3_maps; }
@@ -823,6 +839,7 @@ int dc_set_halo_async(int on) {
     return old;
 }
 int dc_last_decode_launched_runs(void) { return G.runs_used; }
+int dc_last_decode_launched_tiny(void) { return G.tiny_used; }
 /* streams of at most this capacity (bytes) use the small-stream decoder (dc_decode_runs.hip), unless the
    segment decoder is forced (dc_set_decode3_min_bytes(0)); halo planes use it up to its chunk limit */
 static long long g_runs_max = -2;
@@ -857,7 +874,7 @@ static int maps_forced(void) {
 int dc_set_decode3_maps(int on) {
     const int old = maps_forced();
     g_maps_force = on ? 1 : 0;
-    if (on < 0) { G.maps_key = 0; G.dense_key = 0; g_maps_force = 0; }   /* tests: forget the remembered streams */
+    if (on < 0) { G.maps_key = 0; G.dense_key = 0; G.tiny_key = 0; g_maps_force = 0; }   /* tests: forget the remembered streams */
     return old;
 }
 /* the segment decoder's launch for the pending decode: parse3 + decode3, or the maps parse + decode3
@@ -875,6 +892,24 @@ static int dec3_launch(const uint8_t* s, const Params* P, float* out, long long 
         return seterr(DC_ERR_HIP, "decode launch failed: %s", hipGetErrorString(hipGetLastError()));
     G.dec3_fusedl = dc_decode3_last_fused();
     return DC_OK;
+}
+
+/* the segment decoder for the pending decode's stream (also after the one-workgroup decoder declined it) */
+static int seg_decode_launch(const uint8_t* d_stream, long long nbytes, long long max_bytes, const Params* P,
+                             float* d_out, long long num) {
+    int rc;
+    const int ct = P->ct;
+    if ((rc = dec3_ensure((max_bytes * 8 + 255) / 256 + 1, P->B, ct))) return rc;
+    G.D3.err = G.D.err;
+    G.D3.capw = max_bytes / 16 * 4;
+    /* a decode job holds 64 chunks (16384 bits): streams of fewer than ~16 bits per value overflow the
+       1040-value job buffer, so a stream known to be that dense (its length given, or the last stream of
+       these parameters was) takes the 2080-value instantiation */
+    G.dec3_dense = (nbytes >= 0 && nbytes * 8 < 18 * num && (ct == 6 || nbytes * 8 >= 6 * num)) ||
+                   G.dense_key == ct * 256 + P->B + 1;                   /* (not runs mode: < 6 bits per value) */
+    /* a stream of these parameters whose parse paths did not meet last time: the maps parse at once */
+    G.dec3_maps = G.maps_key == ct * 256 + P->B + 1 || maps_forced();
+    return dec3_launch(d_stream, P, d_out, num);
 }
 
 /* halo: a Himeno halo plane (dc_halo_decode_device): the small-stream decoder up to its chunk limit */
@@ -917,27 +952,31 @@ static int decode_device_h(int ct, const void* d_stream, long long nbytes, const
                   (halo || max_bytes <= rmax);
     G.dec3_used = !halo && !G.runs_used && m3 >= 0 && max_bytes >= m3 && max_bytes >= 16 && max_bytes >= need16 && max_bytes < (1ll << 31) && num < (1ll << 29) && !G.D.shard &&
                   !((uintptr_t)d_stream & 15u) && !((uintptr_t)d_out & 15u);
+    /* (r06) streams of at most 2^14 values whose bits fit 2^19: the one-workgroup decoder (dc_decode_tiny.hip),
+       after the small-stream decoder's range; DC_TINY=0 disables it */
+    G.tiny_used = 0;
+    G.dec_max_bytes = max_bytes;
+    if (G.dec3_used && tiny_on() && num <= dc_tiny_max_values() && !((uintptr_t)d_out & 15u) &&
+        G.tiny_key != ct * 256 + P.B + 1) {
+        G.tiny_used = 1;
+        G.dec3_used = 0;
+    }
     G.dec3_launched = G.dec3_used;
     G.dec_dnbits = nbytes >= 0 ? NULL : d_nbits;
     G.dec_hnbits = nbytes >= 0 ? (unsigned long long)nbytes * 8ull : 0ull;
-    if (G.runs_used) {
+    if (G.tiny_used) {
+        if (dc_launch_decode_tiny((const uint8_t*)d_stream, max_bytes, G.dec_dnbits, G.dec_hnbits, &P, (float*)d_out,
+                                  num, G.D.err, G.st))
+            return seterr(DC_ERR_HIP, "decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+        G.dec3_used = 1;                  /* (a first decoder that may decline: dc_decode_finish falls back) */
+    } else if (G.runs_used) {
         if (!G.runs_maps) HIPCHK(hipMalloc((void**)&G.runs_maps, dc_decode_runs_scratch_bytes()));
         if (dc_launch_decode_runs((const uint8_t*)d_stream, G.dec_dnbits, G.dec_hnbits, mc256, &P, G.runs_maps, G.D.err,
                                   (float*)d_out, num, G.st))
             return seterr(DC_ERR_HIP, "decode launch failed: %s", hipGetErrorString(hipGetLastError()));
         G.dec3_used = 1;                  /* (a first decoder that may decline: dc_decode_finish falls back) */
     } else if (G.dec3_used) {
-        if ((rc = dec3_ensure((max_bytes * 8 + 255) / 256 + 1, P.B, ct))) return rc;
-        G.D3.err = G.D.err;
-        G.D3.capw = max_bytes / 16 * 4;
-        /* a decode job holds 64 chunks (16384 bits): streams of fewer than ~16 bits per value overflow the
-           1040-value job buffer, so a stream known to be that dense (its length given, or the last stream of
-           these parameters was) takes the 2080-value instantiation */
-        G.dec3_dense = (nbytes >= 0 && nbytes * 8 < 18 * num && (ct == 6 || nbytes * 8 >= 6 * num)) ||
-                       G.dense_key == ct * 256 + P.B + 1;                /* (not runs mode: < 6 bits per value) */
-        /* a stream of these parameters whose parse paths did not meet last time: the maps parse at once */
-        G.dec3_maps = G.maps_key == ct * 256 + P.B + 1 || maps_forced();
-        if ((rc = dec3_launch((const uint8_t*)d_stream, &P, (float*)d_out, num))) return rc;
+        if ((rc = seg_decode_launch((const uint8_t*)d_stream, nbytes, max_bytes, &P, (float*)d_out, num))) return rc;
     } else if (DV(dc_launch_decode_fast)((const uint8_t*)d_stream, G.dec_dnbits, G.dec_hnbits, max_chunks, &P, &G.D,
                                          (float*)d_out, num, G.dec_epoch, G.st))
         return seterr(DC_ERR_HIP, "decode launch failed: %s", hipGetErrorString(hipGetLastError()));
@@ -1106,11 +1145,26 @@ static int decode_finish_body(void) {
         return seterr(DC_ERR_STREAM, "decoder status 0x%x over %d queued decodes: an earlier decode left the fast "
                                      "path and was not completed (call dc_decode_finish after each decode)", err, queued);
     }
+    /* the one-workgroup decoder declined (link or pending chains past its rounds, e.g. CT11's slowly
+       resynchronising 32-bit tokens): the segment decoder, and for these parameters from the start next time;
+       a stream it declines for the sentinel or its length goes on below like any declined segment decode */
+    if ((err & 512u) && G.dec_pending && G.tiny_used && !(err & (4096u | 16384u))) {
+        if (getenv("DC_DEBUG_ERR")) fprintf(stderr, "[dcamd] one-workgroup decoder declined (status 0x%x)\n", err);
+        HIPCHK(hipMemsetAsync(G.D.err, 0, 4, G.st));
+        if ((rc = dec_next_epoch())) return rc;
+        G.tiny_key = G.dec_P.ct * 256 + G.dec_P.B + 1;
+        G.tiny_used = 0;
+        if ((rc = seg_decode_launch(G.dec_s, G.dec_hnbits ? (long long)(G.dec_hnbits / 8) : -1, G.dec_max_bytes,
+                                    &G.dec_P, G.dec_out, G.dec_num)))
+            return rc;
+        rc = read_dec_err(&err);
+        if (rc) return rc;
+    }
     /* segment-decoder declines it recovers from itself: a job denser than the 1040-value buffer (the 2080-value
        instantiation) and parse paths that did not meet (the maps parse); each is remembered per (CT, bound),
        so later decodes of such streams start with it */
     for (int r = 0; r < 2; r++) {
-        if (!((err & 512u) && G.dec_pending && G.dec3_used && !G.runs_used && !G.dec_shard)) break;
+        if (!((err & 512u) && G.dec_pending && G.dec3_used && !G.runs_used && !G.tiny_used && !G.dec_shard)) break;
         if (err & (1024u | 4096u | 16384u | 65536u)) break;       /* runs mode, short, sentinel, shard: other paths */
         const int want_maps = G.dec3_maps || (err & 2048u) != 0;
         const int want_dense = G.dec3_dense || (err & 8192u) != 0;
@@ -1128,7 +1182,8 @@ static int decode_finish_body(void) {
         rc = read_dec_err(&err);
         if (rc) return rc;
     }
-    G.dec3_last = G.dec3_used && !G.runs_used && !(err & 512u);
+    G.tiny_last = G.tiny_used && !(err & 512u);
+    G.dec3_last = G.dec3_used && !G.runs_used && !G.tiny_used && !(err & 512u);
     G.runs_last = G.dec3_used && G.runs_used && !(err & 512u);
     if ((err & 512u) && G.dec_pending && G.dec3_used) {
         /* the segment decoder declined the stream (runs mode, an unconverged repair, a dense job, the

@@ -165,6 +165,10 @@ int dc_launch_extract_shard(const uint8_t* g, long long g_bytes, const unsigned 
                             long long d_bytes, unsigned long long* nbits_out, unsigned* err, dc_hip_stream st);
 int dc_launch_shard3_fix(const uint8_t* s, const DC_NS Params* P, const DC_NS Dec3Bufs* D3, const float* hin,
                          float* out, long long num, dc_hip_stream st);
+int dc_launch_decode_tiny(const uint8_t* s, long long capb, const unsigned long long* dev_nbits,
+                          unsigned long long host_nbits, const DC_NS Params* P, float* out, long long num, unsigned* err,
+                          dc_hip_stream st);
+long long dc_tiny_max_values(void);
 int dc_launch_decode_runs(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
                           long long max_chunks, const DC_NS Params* P, uint8_t* maps, unsigned* err, float* out,
                           long long num, dc_hip_stream st);

@@ -286,6 +286,12 @@ int dc_set_decode3_maps(int on);   /* (-1: also forget the parameters remembered
 long long dc_set_runs_max_bytes(long long max_bytes);
 /* 1 if the last decode's values came from the small-stream decoder (after dc_decode_finish). */
 int dc_last_decode_was_runs(void);
+/* 1 when the last finished decode stayed on the one-workgroup decoder of small streams (at most 2^14 values, 2^19
+ * bits: dc_decode_tiny.hip); dc_set_decode_tiny(0) (or DC_TINY=0) keeps them on the segment decoder.  Returns the
+ * previous setting. */
+int dc_last_decode_was_tiny(void);
+int dc_last_decode_launched_tiny(void);
+int dc_set_decode_tiny(int on);
 int dc_last_decode_launched_runs(void);     /* 1: the last dc_decode_device launched it (it may decline) */
 /* 1: the last dc_decode_device launched the segment decoder (its values may still come from the chunk-map
  * decoder if it declined the stream: dc_last_decode_was_v3 after dc_decode_finish tells) */
