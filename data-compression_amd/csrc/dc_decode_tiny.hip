@@ -100,6 +100,16 @@ __device__ __forceinline__ int ty_walk(TyRd& r, int end, const uint16_t* meta, c
     return n;
 }
 
+#ifdef DC_TY_STAMPS                                // (diagnostic builds: phase stamps of the last launch)
+__device__ unsigned long long ty_stamps[16];
+#define TYS(k) do { if (threadIdx.x == 0) ty_stamps[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+extern "C" int dc_tiny_stamps(unsigned long long* h) {
+    return hipMemcpyFromSymbol(h, HIP_SYMBOL(ty_stamps), sizeof(ty_stamps), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#else
+#define TYS(k) do {} while (0)
+#endif
+
 template <int CT>
 __global__ __launch_bounds__(TY_T, 1) void tiny_decode_kernel(const uint8_t* __restrict__ s, long long capw,
                                                               const unsigned long long* dev_nbits,
@@ -112,6 +122,7 @@ __global__ __launch_bounds__(TY_T, 1) void tiny_decode_kernel(const uint8_t* __r
     __shared__ int X[TY_T];                        // exits (absolute bits); then the pending counts
     __shared__ uint32_t wsum[TY_T / 64];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    TYS(0);
     const unsigned long long nb64 = dev_nbits ? *dev_nbits : host_nbits;
     if (nb64 > (unsigned long long)TY_MAXBITS || num < 1 || num > TY_NUM) {      // (uniform)
         if (tid == 0) atomicOr(err, TY_DECLINE | TY_WHY_SHORT);
@@ -140,6 +151,7 @@ __global__ __launch_bounds__(TY_T, 1) void tiny_decode_kernel(const uint8_t* __r
         if (tid < 7) W[wix(TY_W - 7 + tid)] = 0u;
     }
     __syncthreads();
+    TYS(1);
     // ---- walk: entry, exit, count of segment tid
     const int sb = tid * TY_SEGB;
     const bool act = sb < nbits;
@@ -155,11 +167,18 @@ __global__ __launch_bounds__(TY_T, 1) void tiny_decode_kernel(const uint8_t* __r
     }
     X[tid] = x;
     __syncthreads();
+    TYS(2);
     // ---- links: a segment's entry must be its predecessor's exit
     for (int round = 0;; round++) {
         const int xin = tid > 0 ? X[tid - 1] : 0;
         const bool bad = act && tid > 0 && e != xin;
-        if (!__syncthreads_or(bad)) break;
+        if (!__syncthreads_or(bad)) {
+            TYS(8 + 0 * round);
+#ifdef DC_TY_STAMPS
+            if (tid == 0) ty_stamps[10] = round;
+#endif
+            break;
+        }
         if (round >= TY_ROUNDS) {
             if (tid == 0) atomicOr(err, TY_DECLINE | TY_WHY_RUNS);
             return;                                                                // (uniform)
@@ -183,6 +202,7 @@ __global__ __launch_bounds__(TY_T, 1) void tiny_decode_kernel(const uint8_t* __r
         pre += w < wid ? wsum[w] : 0u;
         tot += wsum[w];
     }
+    TYS(3);
     if ((long long)tot < num) {                                                    // (uniform)
         if (tid == 0) atomicOr(err, TY_DECLINE | TY_WHY_SHORT);
         return;
@@ -215,12 +235,18 @@ __global__ __launch_bounds__(TY_T, 1) void tiny_decode_kernel(const uint8_t* __r
         }
     }
     __syncthreads();                                                                // (X read by every thread)
+    TYS(4);
     X[tid] = pend;
     __syncthreads();
     // ---- pending prefixes, one link of a chain per round
     for (int round = 0;; round++) {
         const bool go = pend > 0 && (tid == 0 || X[tid - 1] == 0);
-        if (!__syncthreads_or(pend > 0)) break;
+        if (!__syncthreads_or(pend > 0)) {
+#ifdef DC_TY_STAMPS
+            if (tid == 0) ty_stamps[11] = round;
+#endif
+            break;
+        }
         if (round >= TY_ROUNDS) {
             if (tid == 0) atomicOr(err, TY_DECLINE | TY_WHY_RUNS);
             return;
@@ -251,12 +277,14 @@ __global__ __launch_bounds__(TY_T, 1) void tiny_decode_kernel(const uint8_t* __r
         if (tid == 0) atomicOr(err, TY_DECLINE | TY_WHY_SENT);
         return;
     }
+    TYS(5);
     // ---- store: whole float4s, then the tail
     const int n4 = (int)(num >> 2);
     float4* o4 = reinterpret_cast<float4*>(out);
     const float4* b4 = reinterpret_cast<const float4*>(OB);
     for (int q = tid; q < n4; q += TY_T) o4[q] = b4[q];
     if (tid < (int)(num & 3)) out[4 * n4 + tid] = OB[4 * n4 + tid];
+    TYS(6);
 }
 
 extern "C" long long dc_tiny_max_values(void) { return TY_NUM; }

@@ -817,10 +817,11 @@ static long long dec3_min_bytes(void) {
     }
     return g_dec3_min;
 }
-/* DC_TINY=0 (or dc_set_decode_tiny(0)): small streams stay on the segment decoder */
+/* DC_TINY=1 (or dc_set_decode_tiny(1)): small streams on the one-workgroup decoder -- opt-in: measured at parity
+   with the segment decoder at 2^14 (one CU's VALU issue bounds it) */
 static int g_tiny_on = -1;
 static int tiny_on(void) {
-    if (g_tiny_on < 0) g_tiny_on = (getenv("DC_TINY") && *getenv("DC_TINY") == '0') ? 0 : 1;
+    if (g_tiny_on < 0) g_tiny_on = (getenv("DC_TINY") && *getenv("DC_TINY") == '1') ? 1 : 0;
     return g_tiny_on;
 }
 int dc_set_decode_tiny(int on) {
@@ -953,7 +954,7 @@ static int decode_device_h(int ct, const void* d_stream, long long nbytes, const
     G.dec3_used = !halo && !G.runs_used && m3 >= 0 && max_bytes >= m3 && max_bytes >= 16 && max_bytes >= need16 && max_bytes < (1ll << 31) && num < (1ll << 29) && !G.D.shard &&
                   !((uintptr_t)d_stream & 15u) && !((uintptr_t)d_out & 15u);
     /* (r06) streams of at most 2^14 values whose bits fit 2^19: the one-workgroup decoder (dc_decode_tiny.hip),
-       after the small-stream decoder's range; DC_TINY=0 disables it */
+       after the small-stream decoder's range, when enabled (DC_TINY=1 / dc_set_decode_tiny(1)) */
     G.tiny_used = 0;
     G.dec_max_bytes = max_bytes;
     if (G.dec3_used && tiny_on() && num <= dc_tiny_max_values() && !((uintptr_t)d_out & 15u) &&

@@ -287,8 +287,7 @@ long long dc_set_runs_max_bytes(long long max_bytes);
 /* 1 if the last decode's values came from the small-stream decoder (after dc_decode_finish). */
 int dc_last_decode_was_runs(void);
 /* 1 when the last finished decode stayed on the one-workgroup decoder of small streams (at most 2^14 values, 2^19
- * bits: dc_decode_tiny.hip); dc_set_decode_tiny(0) (or DC_TINY=0) keeps them on the segment decoder.  Returns the
- * previous setting. */
+ * bits: dc_decode_tiny.hip).  Opt-in: dc_set_decode_tiny(1) (or DC_TINY=1); it returns the previous setting. */
 int dc_last_decode_was_tiny(void);
 int dc_last_decode_launched_tiny(void);
 int dc_set_decode_tiny(int on);

@@ -9,6 +9,14 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def tiny_on(dc):
+    """the one-workgroup decoder is opt-in (dc_set_decode_tiny(1)): on for these tests"""
+    prev = dc.L.dc_set_decode_tiny(1)
+    yield
+    dc.L.dc_set_decode_tiny(prev)
+
+
 def _x(oracle, kind, n):
     rs = np.random.RandomState(n % 977 + 1)
     if kind == "u10":
