@@ -44,6 +44,9 @@ namespace dc {
 #ifndef DC_EXIT_EARLY
 #define DC_EXIT_EARLY 1                 // 8/16-chunk segments: a job's exit published right after its main walk
 #endif
+#ifndef DC_P3_PW4
+#define DC_P3_PW4 1024
+#endif
 // pre-walk: 1024 bits (4 chunks, one region line) before every segment (DC_PARSE_PL6=2: 2048 for CT6 --
 // 12% instead of 94% of its jobs repair, but the longer walk cost more: config 2 parse3 98 vs 92 us)
 #ifndef DC_PARSE_PL6
@@ -343,7 +346,10 @@ __device__ __forceinline__ uint32_t parse3_job(Ring3& r, uint16_t* recs, const u
     // ---- main walk: the pre-walk line (1024 bits before the segment), then the segment's lines
     uint32_t tot = 0;
     int e0 = 0, ec = 0;
-    run_lines<false>(r, rs, G.nbytes, gw0, 1 - PL, seg / 4 + 1, lim, -1024 * PL, act, tl,
+    // (DC_P3_PW4: the pre-walk's bits for 4-chunk segments -- small streams, whose parse is one walk; the walk
+    // starts inside line 0, the phases before it step nothing)
+    constexpr int PW = (SEG == 4 && PL == 1) ? DC_P3_PW4 : 1024 * PL;
+    run_lines<false>(r, rs, G.nbytes, gw0, 1 - PL, seg / 4 + 1, lim, -PW, act, tl,
               [&](int c, int kbase) {
                   if (c == 0 && sidx == 0) r.init(0, kbase);             // the stream's first bit
                   ec = r.pos - 256 * c;
