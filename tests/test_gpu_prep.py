@@ -136,3 +136,46 @@ def test_encode_sub_other_variants(dc, oracle):
     finally:
         dc.L.dc_set_encode_help(prev)
     assert nb2 == nb1 and np.array_equal(s2, s1)
+
+
+def test_prep_chain_u10_2p26_vs_oracle(dc, oracle):
+    """The bench workload through the fused chain (raw U10 2^26 floats in HBM): minimum, mean, type and the stream of
+    x - min equal the oracle's separate passes (toSmallDataset_float, med_dataset_float, the CT7 encoder)."""
+    import torch
+    dc.set_bound(1e-3)
+    n = 1 << 26
+    x = oracle.gen_u10(n)
+    d = torch.from_numpy(x).cuda()
+    torch.cuda.synchronize()
+    mn, mean, t = dc.prep_device(d.data_ptr(), n)
+    omn, xs = oracle.to_small(x)
+    om, ot = oracle.med(xs)
+    assert np.float32(mn) == np.float32(omn) and np.float32(mean).view(np.uint32) == np.float32(om).view(np.uint32)
+    assert t == ot
+    m17 = oracle.mask17(mean)
+    s, nb, bits = _encode_sub(dc, d, n, mn, 7, t, m17)
+    del d
+    torch.cuda.empty_cache()
+    so, nbo, _ = oracle.compress(7, xs, 1e-3, t, m17)
+    assert nb == nbo == 162634383 and np.array_equal(s, so)
+
+
+def test_prep_chain_u10_2p28_vs_golden_hash(dc, oracle):
+    """2^28 raw floats (the sweep's largest size): the fused chain's stream has the oracle's bit count and hash
+    (tests/golden/bench_hashes.json, tests/golden/make_bench_hashes.py)"""
+    import json, os
+    import torch
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "bench_hashes.json")))["ct7_u10_2^28_0.001_w1"]
+    dc.set_bound(1e-3)
+    n = 1 << 28
+    d = torch.from_numpy(oracle.gen_u10(n)).cuda()
+    torch.cuda.synchronize()
+    mn, mean, t = dc.prep_device(d.data_ptr(), n)
+    m17 = oracle.mask17(mean)
+    st = torch.zeros(dc.stream_capacity(n), dtype=torch.uint8, device="cuda")
+    dc.encode_sub_device(7, d.data_ptr(), n, mn, st.data_ptr(), type_=t, mask17=m17)
+    bits = dc.encode_result()
+    h = dc.hash_device(st.data_ptr(), (bits + 7) // 8)
+    del d, st
+    torch.cuda.empty_cache()
+    assert bits == int(g["nbits"]) and h == int(g["stream"])
