@@ -2290,6 +2290,38 @@ __global__ __launch_bounds__(256) void plane_gather_kernel(const float* __restri
     for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long long)gridDim.x * 256)
         out[e] = p[plane_index(e / B, e % B, ijk, v, mj, mk)];
 }
+// (r06) the gather with toSmallDataset's minimum partials of the gathered plane (min_partial_kernel's rule: the
+// minimum of out[1..n), NaN ignored, and the index of its first zero) -- the halo encode then needs min_final and
+// the encoder, which subtracts the minimum while loading (Params.subp): three launches instead of six
+__global__ __launch_bounds__(256) void plane_gather_min_kernel(const float* __restrict__ p, int mj, int mk, int ijk, int v,
+                                                               int A, int B, float* __restrict__ out,
+                                                               float* __restrict__ pv, long long* __restrict__ pi) {
+    __shared__ float sv[4];
+    __shared__ long long si[4];
+    const long long n = (long long)A * B;
+    float mv = __int_as_float(0x7fc00000);
+    long long fz = (long long)1 << 62;
+    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+        const float a = p[plane_index(e / B, e % B, ijk, v, mj, mk)];
+        out[e] = a;
+        if (e > 0) {
+            mv = fminf(mv, a);
+            if (a == 0.f) fz = min(fz, e);
+        }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        mv = fminf(mv, __shfl_xor(mv, d, 64));
+        fz = min(fz, (long long)__shfl_xor(fz, d, 64));
+    }
+    if ((threadIdx.x & 63) == 0) { sv[threadIdx.x >> 6] = mv; si[threadIdx.x >> 6] = fz; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        pv[blockIdx.x] = fminf(fminf(sv[0], sv[1]), fminf(sv[2], sv[3]));
+        pi[blockIdx.x] = min(min(si[0], si[1]), min(si[2], si[3]));
+    }
+}
+
 __global__ __launch_bounds__(256) void plane_scatter_kernel(const float* __restrict__ x, const float* __restrict__ d_min,
                                                             float* __restrict__ p, int mj, int mk, int ijk, int v, int A,
                                                             int B) {
@@ -2305,6 +2337,26 @@ extern "C" int dc_launch_plane_gather(const float* p, int mj, int mk, int ijk, i
     long long g = (n + 255) / 256;
     if (g > 4096) g = 4096;
     hipLaunchKernelGGL(plane_gather_kernel, dim3((unsigned)g), dim3(256), 0, st, p, mj, mk, ijk, v, A, B, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+// the gathered plane and its minimum into d_min (toSmallDataset_float's minimum of the plane), two launches
+extern "C" int dc_launch_plane_gather_min(const float* p, int mj, int mk, int ijk, int v, int A, int B, float* out,
+                                          float* part_v, long long* part_i, float* d_min, hipStream_t st) {
+    const long long n = (long long)A * B;
+    if (n <= 0) return 0;
+    const int g = (int)std::min<long long>(DC_MIN_PARTS, std::max<long long>(1, (n + 1023) / 1024));
+    hipLaunchKernelGGL(plane_gather_min_kernel, dim3((unsigned)g), dim3(256), 0, st, p, mj, mk, ijk, v, A, B, out,
+                       part_v, part_i);
+    hipLaunchKernelGGL(min_final_kernel, dim3(1), dim3(256), 0, st, (const float*)out, (const float*)part_v,
+                       (const long long*)part_i, g, d_min);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+// y = x - *d_min (the reference's x86 subtraction)
+extern "C" int dc_launch_sub_ptr(const float* x, long long n, const float* d_min, float* y, hipStream_t st) {
+    if (n <= 0) return 0;
+    long long g = (n / 4 + 255) / 256;
+    g = std::max(1ll, std::min(g, 2048ll));
+    hipLaunchKernelGGL(sub_min_kernel, dim3((unsigned)g), dim3(256), 0, st, x, n, d_min, y);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 extern "C" int dc_launch_plane_scatter(const float* x, const float* d_min, float* p, int mj, int mk, int ijk, int v,

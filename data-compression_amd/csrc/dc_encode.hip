@@ -1284,11 +1284,22 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
         for (int k = 1; k <= 3; k++) {
             const long long e = w0 - k;
             hw[k - 1] = (e < n && e >= -3 && idx0 + e >= 0) ? x[e] : 0.0f;
-            if (!CRC && !HELP && P.sub && e < n && e >= -3 && idx0 + e >= 0) hw[k - 1] = sub_fin(hw[k - 1], P.submin);
         }
         if (!CRC && !HELP && P.sub) {                                      // (dc_encode_sub_device: x - min)
+            const float m = P.subp ? *P.subp : P.submin;
+            if (__builtin_expect(isfinite(m), 1)) {
 #pragma unroll
-            for (int j = 0; j < ENC_K; j++) h[3 + j] = sub_fin(h[3 + j], P.submin);
+                for (int j = 0; j < ENC_K; j++) h[3 + j] = sub_fin(h[3 + j], m);
+#pragma unroll
+                for (int k = 1; k <= 3; k++)
+                    if (w0 - k < n && w0 - k >= -3 && idx0 + w0 - k >= 0) hw[k - 1] = sub_fin(hw[k - 1], m);
+            } else {                                                       // (a NaN / infinite minimum)
+#pragma unroll
+                for (int j = 0; j < ENC_K; j++) h[3 + j] = sub_x86(h[3 + j], m);
+#pragma unroll
+                for (int k = 1; k <= 3; k++)
+                    if (w0 - k < n && w0 - k >= -3 && idx0 + w0 - k >= 0) hw[k - 1] = sub_x86(hw[k - 1], m);
+            }
         }
         h[2] = wave_shr1(h[3 + ENC_K - 1], hw[0]);
         h[1] = wave_shr1(h[3 + ENC_K - 2], hw[1]);

@@ -110,6 +110,8 @@ typedef struct {
     void* prep_part; size_t prep_part_cap;  /* dc_prep_device: the chunks' partial minima (float) and first zeros (i64) */
     void* sub_buf; size_t sub_buf_cap;      /* x - min written out: dc_prep_device / dc_encode_sub_device fallbacks */
     const float* enc_sub;                   /* encode_on: the minimum to subtract while loading (NULL: none) */
+    const float* enc_subp;                  /* encode_on: the same on the device (the halo path; NULL: none) */
+    int halo_unfused;                       /* 1: the halo encode's separate passes (dc_set_halo_unfused, A/B) */
     int tiny_used, tiny_last;               /* the pending decode went to / the last finished one stayed on the
                                                one-workgroup decoder (dc_decode_tiny.hip) */
     int tiny_key;                           /* ct * 256 + B + 1 of parameters whose small stream it declined */
@@ -454,7 +456,9 @@ static int launch_enc(const float* x, long long n, long long idx0, const Params*
     const int r = dc_launch_encode(x, n, idx0, P, out, desc, flag, epoch, start_bit, tb, tb2, err, dbg, mode, ctab, cblk, st);
     if (r != -3) return r;
     if (grow(&G.sub_buf, &G.sub_buf_cap, (size_t)n * 4 + 64)) return -1;
-    if (dc_launch_sub_value(x, n, P->submin, (float*)G.sub_buf, st)) return -1;
+    if (P->subp ? dc_launch_sub_ptr(x, n, P->subp, (float*)G.sub_buf, st)
+                : dc_launch_sub_value(x, n, P->submin, (float*)G.sub_buf, st))
+        return -1;
     Params Q = *P;
     Q.sub = 0;
     return dc_launch_encode((const float*)G.sub_buf, n, idx0, &Q, out, desc, flag, epoch, start_bit, tb, tb2, err, dbg,
@@ -470,7 +474,11 @@ static int encode_on(hipStream_t st, int ct, const void* d_x, long long n, long 
     if (((uintptr_t)d_x & 15u) || ((uintptr_t)d_out & 3u)) return seterr(DC_ERR_ARG, "misaligned device buffer");
     Params P;
     make_params(&P, ct, type, mask17);
-    if (G.enc_sub) {                                 /* dc_encode_sub_device */
+    if (G.enc_subp) {                                /* the halo path: the minimum on the device */
+        if (idx0) return seterr(DC_ERR_ARG, "encode of x - min: idx0 must be 0");
+        P.sub = 1;
+        P.subp = G.enc_subp;
+    } else if (G.enc_sub) {                          /* dc_encode_sub_device */
         if (idx0) return seterr(DC_ERR_ARG, "encode of x - min: idx0 must be 0");
         P.sub = 1;
         P.submin = *G.enc_sub;
@@ -834,6 +842,11 @@ int dc_last_decode_was_tiny(void) { return G.tiny_last; }
 int dc_last_decode_was_v3(void) { return G.dec3_last; }
 int dc_last_decode_used_maps(void) { return G.dec3_last && G.dec3_maps; }
 int dc_last_decode_was_runs(void) { return G.runs_last; }
+int dc_set_halo_unfused(int on) {
+    const int old = G.halo_unfused;
+    G.halo_unfused = on ? 1 : 0;
+    return old;
+}
 int dc_set_halo_async(int on) {
     const int old = G.halo_async;
     G.halo_async = on ? 1 : 0;
@@ -1349,6 +1362,25 @@ int dc_halo_encode_device(int ct, const void* d_p, int mi, int mj, int mk, int i
     if (n <= 0) return seterr(DC_ERR_ARG, "empty plane");
     if (grow(&G.halo_a, &G.halo_a_cap, (size_t)n * 4 + 64) || grow(&G.halo_b, &G.halo_b_cap, (size_t)n * 4 + 64))
         return DC_ERR_HIP;
+    if (!(ct == 7 && type <= 0) && !G.halo_unfused) {
+        /* (r06) the gather computes toSmallDataset's minimum partials, min_final writes the minimum where the caller
+           wants it, and the encoder subtracts it while loading (no x - min written, no copy of the minimum): three
+           launches instead of six */
+        float* dmin = d_min ? d_min : &G.d_f[0];
+        if (dc_launch_plane_gather_min((const float*)d_p, mj, mk, ijk, v, A, B, (float*)G.halo_a, G.part_v, G.part_i,
+                                       dmin, G.st))
+            return seterr(DC_ERR_HIP, "plane gather launch failed");
+        if (type_out) *type_out = type;
+        if (mask17_out) *mask17_out = mask17;
+        if (G.enc_st) {
+            HIPCHK(hipEventRecord(G.ev_lib, G.enc_st));
+            HIPCHK(hipStreamWaitEvent(G.st, G.ev_lib, 0));
+        }
+        G.enc_subp = dmin;
+        rc = encode_on(G.st, ct, G.halo_a, n, 0, type, mask17, 0, d_stream, d_bits, NULL);
+        G.enc_subp = NULL;
+        return rc;
+    }
     if (dc_launch_plane_gather((const float*)d_p, mj, mk, ijk, v, A, B, (float*)G.halo_a, G.st))
         return seterr(DC_ERR_HIP, "plane gather launch failed");
     if (dc_launch_to_small((const float*)G.halo_a, n, (float*)G.halo_b, G.part_v, G.part_i, &G.d_f[0], G.st))

@@ -37,6 +37,7 @@ typedef struct Params {  /* per-call codec parameters, computed on the host */
        (toSmallDataset_float); the single-pass encoder only, submin finite */
     int sub;
     float submin;
+    const float* subp;   /* (device) the minimum, when set: read by the kernel instead of submin (the halo path) */
 } Params;
 
 typedef struct Plan {    /* device-resident sizes of the stream being decoded */
@@ -234,6 +235,9 @@ int dc_launch_med(const float* x, long long n, float s_init, void* scratch, floa
                   float* d_max, dc_hip_stream st);
 int dc_launch_med_sub(const float* x, long long n, void* scratch, float* d_min, float* pv, long long* pi, float* d_mean,
                       int* d_type, int wide, hipStream_t st);
+int dc_launch_plane_gather_min(const float* p, int mj, int mk, int ijk, int v, int A, int B, float* out, float* part_v,
+                               long long* part_i, float* d_min, dc_hip_stream st);
+int dc_launch_sub_ptr(const float* x, long long n, const float* d_min, float* y, dc_hip_stream st);
 int dc_launch_sub_value(const float* x, long long n, float m, float* y, hipStream_t st);
 int dc_launch_med_wide(const float* x, long long n, float s_init, void* scratch, float* d_mean, int* d_type,
                        float* d_sum, float* d_max, int fresh, dc_hip_stream st);

@@ -37,7 +37,7 @@ ABI_SYMBOLS = [
 EXT_SYMBOLS = [
     "dc_init", "dc_last_error", "dc_get_stream", "dc_synchronize", "dc_set_abs_error_bound",
     "dc_get_abs_error_bound", "dc_stream_capacity", "dc_encode_device", "dc_encode_result",
-    "dc_decode_device", "dc_decode_finish", "dc_to_small_device", "dc_med_device", "dc_prep_device", "dc_encode_sub_device", "dc_last_decode_was_tiny", "dc_last_decode_launched_tiny", "dc_set_decode_tiny", "dc_crc32_device",
+    "dc_decode_device", "dc_decode_finish", "dc_to_small_device", "dc_med_device", "dc_prep_device", "dc_encode_sub_device", "dc_last_decode_was_tiny", "dc_set_halo_unfused", "dc_last_decode_launched_tiny", "dc_set_decode_tiny", "dc_crc32_device",
     "dc_decode_chunk_bits_value", "dc_ct1_encode_device", "dc_ct1_decode_device", "dc_encode_bits_device",
     "dc_crc32_device_async", "dc_crc32_copy_device", "dc_encode_send_device", "dc_crc32_pair_device", "dc_encode_crc_device", "dc_crc32_stream_device", "dc_crc_resend_crc_device",
     "dc_hash_device", "dc_copy_rate_device", "dc_flip_bits_device", "dc_decode_shard_device", "dc_decode_shard_fix",

@@ -137,6 +137,10 @@ int dc_halo_decode_device(int ct, const void* d_stream, long long nbytes, const 
  * dc_decode_status() reads 0 after the caller's steps; else decode it again with this off).  Returns the
  * previous setting. */
 int dc_set_halo_async(int on);
+/* 1: dc_halo_encode_device takes the separate passes (gather, toSmallDataset's three launches, a copy of the
+ * minimum, encode) instead of the fused ones (gather with the minimum's partials, min_final, an encode that subtracts
+ * the minimum while loading); the same stream and minimum.  Returns the previous setting. */
+int dc_set_halo_unfused(int on);
 
 /* Pre-passes on device data: toSmallDataset_float and med_dataset_float (exact). */
 int dc_to_small_device(const void* d_x, long long n, void* d_out, float* min_out);

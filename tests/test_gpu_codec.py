@@ -561,6 +561,60 @@ def _halo_plane_case(dc, oracle, ct, size, ijk, v, noise):
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
 
 
+@pytest.mark.parametrize("ct", [5, 6, 11])
+@pytest.mark.parametrize("kind", ["initmt", "noise", "negative", "zero_min", "nan", "inf"])
+@pytest.mark.parametrize("ijk,v", [(3, 1), (1, 255), (2, 7)])
+def test_halo_fused_vs_separate(dc, oracle, ct, kind, ijk, v):
+    """(r06) The halo encode's fused passes (the gather with toSmallDataset's minimum partials, min_final, the encoder
+    subtracting the minimum while loading) against its separate passes (dc_set_halo_unfused(1)) and the oracle:
+    the same minimum (bits), bit count and stream -- planes with negative values, a zero minimum, NaNs (quieted as
+    x86 does) and infinities (a NaN or infinite minimum takes the x86 subtraction in the encoder)."""
+    import torch
+    dc.set_bound(1e-3)
+    mi, mj, mk = 257, 257, 8
+    imax, jmax, kmax = 256, 256, 7
+    rs = np.random.RandomState(hash((kind, ijk, v)) % 1000)
+    ii = np.arange(mi, dtype=np.float32)[:, None, None]
+    p = (ii * ii / np.float32((imax - 1) * (imax - 1)) + np.zeros((mi, mj, mk), np.float32)).astype(np.float32)
+    if kind != "initmt":
+        p += (rs.rand(mi, mj, mk).astype(np.float32) * np.float32(0.01))
+    if kind == "negative":
+        p -= np.float32(3.5)
+    elif kind == "zero_min":
+        p[5, 3, :] = -0.0; p[7, 9, :] = 0.0; p[0, :, :] += np.float32(0.5); p[:, 0, :] += np.float32(0.5)
+    elif kind == "nan":
+        p[3::17, 5::13, :] = np.nan
+    elif kind == "inf":
+        p[2::19, :, :] = np.inf
+    A, B = {1: (jmax, kmax), 2: (imax, kmax), 3: (imax, jmax)}[ijk]
+    a, b = np.meshgrid(np.arange(A), np.arange(B), indexing="ij")
+    idx = {1: (v, a, b), 2: (a, v, b), 3: (a, b, v)}[ijk]
+    plane = p[idx].reshape(-1).copy()
+    n = A * B
+    omn, xs = oracle.to_small(plane)
+    dp = torch.from_numpy(p).cuda()
+    res = []
+    for unfused in (0, 1):
+        prev = dc.L.dc_set_halo_unfused(unfused)
+        try:
+            st = torch.zeros(dc.stream_capacity(n), dtype=torch.uint8, device="cuda")
+            bits = torch.zeros(1, dtype=torch.int64, device="cuda")
+            dmin = torch.zeros(1, dtype=torch.float32, device="cuda")
+            torch.cuda.synchronize()
+            dc.halo_encode_device(ct, dp.data_ptr(), (mi, mj, mk), ijk, v, (imax, jmax, kmax), st.data_ptr(),
+                                  bits.data_ptr(), dmin.data_ptr(), type_=0, mask17=0)
+            tb = dc.encode_result()
+            res.append((tb, st[:(tb + 7) // 8].cpu().numpy(), dmin.cpu().numpy().view(np.uint32)[0]))
+        finally:
+            dc.L.dc_set_halo_unfused(prev)
+    (b0, s0, m0), (b1, s1, m1) = res
+    assert m0 == m1 == np.float32(omn).view(np.uint32)
+    assert b0 == b1 and np.array_equal(s0, s1)
+    if ct != 6 or not np.isnan(xs).any():
+        so, nbo, _ = oracle.compress(ct, xs, 1e-3, 0, 0)
+        assert (b0 + 7) // 8 == nbo and np.array_equal(s0, so)
+
+
 
 
 @pytest.mark.parametrize("bound", BOUNDS)
