@@ -168,6 +168,13 @@ def halo_bench(args):
             L.halo_encode_device(ct, p.data_ptr(), (mi, mj, mk), 3, v, (imax, jmax, kmax), st[h].data_ptr(),
                                  bits.data_ptr() + 8 * h, mins.data_ptr() + 4 * h)
         if dist is None:
+            # both planes at once (each on its own stream: the decoders are one-workgroup scans); DC_HALO_PAIR=0
+            # decodes them one after the other
+            if os.environ.get("DC_HALO_PAIR", "1") != "0":
+                L.halo_decode2_device(ct, st[0].data_ptr(), st[1].data_ptr(), bits.data_ptr(), bits.data_ptr() + 8, 0, 0,
+                                      mins.data_ptr(), mins.data_ptr() + 4, q.data_ptr(), (mi, mj, mk), 3, planes[0],
+                                      planes[1], (imax, jmax, kmax))
+                return
             for h, v in enumerate(planes):
                 L.halo_decode_device(ct, st[h].data_ptr(), -1, bits.data_ptr() + 8 * h, 0, 0, mins.data_ptr() + 4 * h,
                                      q.data_ptr(), (mi, mj, mk), 3, v, (imax, jmax, kmax))

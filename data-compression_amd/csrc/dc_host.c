@@ -111,6 +111,10 @@ typedef struct {
     void* sub_buf; size_t sub_buf_cap;      /* x - min written out: dc_prep_device / dc_encode_sub_device fallbacks */
     const float* enc_sub;                   /* encode_on: the minimum to subtract while loading (NULL: none) */
     const float* enc_subp;                  /* encode_on: the same on the device (the halo path; NULL: none) */
+    hipStream_t st2;                        /* dc_halo_decode2_device: the second plane's stream */
+    hipEvent_t ev_h0, ev_h1;                /* its fork and join with the library stream */
+    void* halo_a2; size_t halo_a2_cap;      /* the second plane's values */
+    uint8_t* runs_maps2;                    /* the second plane's small-stream decoder scratch */
     int halo_unfused;                       /* 1: the halo encode's separate passes (dc_set_halo_unfused, A/B) */
     int tiny_used, tiny_last;               /* the pending decode went to / the last finished one stayed on the
                                                one-workgroup decoder (dc_decode_tiny.hip) */
@@ -1417,6 +1421,57 @@ int dc_halo_decode_device(int ct, const void* d_stream, long long nbytes, const 
     if (!G.halo_async && (rc = dc_decode_finish())) return rc;
     if (dc_launch_plane_scatter((const float*)G.halo_a, d_min, (float*)d_p, mj, mk, ijk, v, A, B, G.st))
         return seterr(DC_ERR_HIP, "plane scatter launch failed");
+    return DC_OK;
+}
+
+/* (r06) Two halo planes of one array (the two z-neighbours' planes of a Himeno step, impl/himenoBMTxps.c:696-706)
+   decoded at once: each plane's small-stream decode and scatter on its own stream -- the decoders are one-
+   workgroup scans, so two of them overlap on the GPU.  Asynchronous, as dc_halo_decode_device under
+   dc_set_halo_async(1): a stream the small-stream decoder declines sets the status word (dc_decode_status) and the
+   caller decodes that plane again with dc_halo_decode_device.  Planes it cannot take go one after the other. */
+int dc_halo_decode2_device(int ct, const void* s0, const void* s1, const unsigned long long* bits0,
+                           const unsigned long long* bits1, int type, uint32_t mask17, const float* dmin0,
+                           const float* dmin1, void* d_p, int mi, int mj, int mk, int ijk, int v0, int v1, int imax,
+                           int jmax, int kmax) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (!valid_ct(ct)) return seterr(DC_ERR_ARG, "unsupported CT %d", ct);
+    if (ct == 7 && (type < 1 || type > 7)) return seterr(DC_ERR_ARG, "CT7 type %d outside 1..7", type);
+    int A = 0, B = 0;
+    if ((rc = plane_dims(ijk, imax, jmax, kmax, &A, &B))) return rc;
+    const long long n = (long long)A * B;
+    const long long cap = (long long)dc_stream_capacity(n);
+    const long long mc256 = (cap * 8 + 255) / 256 + 1;
+    if (!bits0 || !bits1 || ((uintptr_t)s0 & 3u) || ((uintptr_t)s1 & 3u) || mc256 > dc_decode_runs_max_chunks() + 8 ||
+        runs_max_bytes() < 0 || dec3_min_bytes() <= 0 || !G.halo_async) {
+        if ((rc = dc_halo_decode_device(ct, s0, -1, bits0, type, mask17, dmin0, d_p, mi, mj, mk, ijk, v0, imax, jmax,
+                                        kmax)))
+            return rc;
+        return dc_halo_decode_device(ct, s1, -1, bits1, type, mask17, dmin1, d_p, mi, mj, mk, ijk, v1, imax, jmax, kmax);
+    }
+    if (!G.st2) {
+        HIPCHK(hipStreamCreateWithFlags(&G.st2, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&G.ev_h0, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&G.ev_h1, hipEventDisableTiming));
+    }
+    if (grow(&G.halo_a, &G.halo_a_cap, (size_t)n * 4 + 64) || grow(&G.halo_a2, &G.halo_a2_cap, (size_t)n * 4 + 64))
+        return DC_ERR_HIP;
+    if (!G.runs_maps) HIPCHK(hipMalloc((void**)&G.runs_maps, dc_decode_runs_scratch_bytes()));
+    if (!G.runs_maps2) HIPCHK(hipMalloc((void**)&G.runs_maps2, dc_decode_runs_scratch_bytes()));
+    if ((rc = dec_ensure((cap * 8 + 1023) / 1024 + 1))) return rc;     /* (the status word) */
+    Params P;
+    make_params(&P, ct, type, mask17);
+    HIPCHK(hipEventRecord(G.ev_h0, G.st));                            /* the second stream after the library's */
+    HIPCHK(hipStreamWaitEvent(G.st2, G.ev_h0, 0));
+    if (dc_launch_decode_runs((const uint8_t*)s0, bits0, 0ull, mc256, &P, G.runs_maps, G.D.err, (float*)G.halo_a, n,
+                              G.st) ||
+        dc_launch_plane_scatter((const float*)G.halo_a, dmin0, (float*)d_p, mj, mk, ijk, v0, A, B, G.st) ||
+        dc_launch_decode_runs((const uint8_t*)s1, bits1, 0ull, mc256, &P, G.runs_maps2, G.D.err, (float*)G.halo_a2, n,
+                              G.st2) ||
+        dc_launch_plane_scatter((const float*)G.halo_a2, dmin1, (float*)d_p, mj, mk, ijk, v1, A, B, G.st2))
+        return seterr(DC_ERR_HIP, "halo decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+    HIPCHK(hipEventRecord(G.ev_h1, G.st2));                           /* the library stream after both */
+    HIPCHK(hipStreamWaitEvent(G.st, G.ev_h1, 0));
     return DC_OK;
 }
 

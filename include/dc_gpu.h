@@ -141,6 +141,13 @@ int dc_set_halo_async(int on);
  * minimum, encode) instead of the fused ones (gather with the minimum's partials, min_final, an encode that subtracts
  * the minimum while loading); the same stream and minimum.  Returns the previous setting. */
 int dc_set_halo_unfused(int on);
+/* Two planes of one array decoded at once (each on its own stream; asynchronous, dc_set_halo_async(1) required,
+ * else the planes go one after the other): the two z-neighbour planes of a Himeno step.  A plane the small-stream
+ * decoder declines sets dc_decode_status(); decode it again with dc_halo_decode_device. */
+int dc_halo_decode2_device(int ct, const void* s0, const void* s1, const unsigned long long* bits0,
+                           const unsigned long long* bits1, int type, uint32_t mask17, const float* dmin0,
+                           const float* dmin1, void* d_p, int mi, int mj, int mk, int ijk, int v0, int v1, int imax,
+                           int jmax, int kmax);
 
 /* Pre-passes on device data: toSmallDataset_float and med_dataset_float (exact). */
 int dc_to_small_device(const void* d_x, long long n, void* d_out, float* min_out);

@@ -561,6 +561,60 @@ def _halo_plane_case(dc, oracle, ct, size, ijk, v, noise):
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
 
 
+@pytest.mark.parametrize("ct", [5, 6, 7, 11])
+@pytest.mark.parametrize("noise", [False, True])
+def test_halo_decode2_pair(dc, oracle, ct, noise):
+    """(r06) two planes decoded at once on two streams (dc_halo_decode2_device) write the same values into p as two
+    dc_halo_decode_device calls (async halo mode, as the bench's step)"""
+    import torch
+    dc.set_bound(1e-3)
+    mi, mj, mk = 257, 257, 8
+    imax, jmax, kmax = 256, 256, 7
+    ii = np.arange(mi, dtype=np.float32)[:, None, None]
+    kk = np.arange(mk, dtype=np.float32)[None, None, :]
+    p = (ii * ii / np.float32((imax - 1) * (imax - 1)) + np.float32(0.01) * kk + np.zeros((mi, mj, mk), np.float32))
+    if noise:
+        p = p + np.random.RandomState(3).rand(mi, mj, mk).astype(np.float32) * np.float32(0.01)
+    p = p.astype(np.float32)
+    dp = torch.from_numpy(p).cuda()
+    n = imax * jmax
+    st = [torch.zeros(dc.stream_capacity(n), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    bits = torch.zeros(2, dtype=torch.int64, device="cuda")
+    mins = torch.zeros(2, dtype=torch.float32, device="cuda")
+    planes = [1, kmax - 2]
+    torch.cuda.synchronize()
+    ty = [0, 0]
+    m17 = [0, 0]
+    for h, v in enumerate(planes):
+        ty[h], m17[h] = dc.halo_encode_device(ct, dp.data_ptr(), (mi, mj, mk), 3, v, (imax, jmax, kmax),
+                                              st[h].data_ptr(), bits.data_ptr() + 8 * h, mins.data_ptr() + 4 * h)
+        dc.encode_result()
+    if ct == 7 and (ty[0], m17[0]) != (ty[1], m17[1]):
+        pytest.skip("CT7: the two planes have different masks (one decode2 call takes one)")
+    q1 = torch.zeros_like(dp)
+    q2 = torch.zeros_like(dp)
+    prev = dc.L.dc_set_halo_async(1)
+    try:
+        for h, v in enumerate(planes):
+            dc.halo_decode_device(ct, st[h].data_ptr(), -1, bits.data_ptr() + 8 * h, ty[h], m17[h],
+                                  mins.data_ptr() + 4 * h, q1.data_ptr(), (mi, mj, mk), 3, v, (imax, jmax, kmax))
+        dc.halo_decode2_device(ct, st[0].data_ptr(), st[1].data_ptr(), bits.data_ptr(), bits.data_ptr() + 8, ty[0],
+                               m17[0], mins.data_ptr(), mins.data_ptr() + 4, q2.data_ptr(), (mi, mj, mk), 3, planes[0],
+                               planes[1], (imax, jmax, kmax))
+        dc.synchronize()
+        status = dc.decode_status()
+    finally:
+        dc.L.dc_set_halo_async(prev)
+    assert status == 0, hex(status)
+    assert torch.equal(q1, q2)
+    for h, v in enumerate(planes):                        # and against the oracle's decode + min
+        k = (int(bits[h]) + 7) // 8
+        s = st[h][:k].cpu().numpy()
+        dec, _ = oracle.decompress(ct, s, n, 1e-3, ty[h], m17[h])
+        want = (dec + mins[h].cpu().numpy()).astype(np.float32)
+        assert np.array_equal(q2[:imax, :jmax, v].cpu().numpy().reshape(-1).view(np.uint32), want.view(np.uint32))
+
+
 @pytest.mark.parametrize("ct", [5, 6, 11])
 @pytest.mark.parametrize("kind", ["initmt", "noise", "negative", "zero_min", "nan", "inf"])
 @pytest.mark.parametrize("ijk,v", [(3, 1), (1, 255), (2, 7)])
