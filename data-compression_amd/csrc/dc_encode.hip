@@ -1215,7 +1215,9 @@ typedef unsigned u32x4q __attribute__((ext_vector_type(4)));
 // block accumulators cblk (dc_device.h's fused CRC; crcf_final_kernel turns them into the stream's zlib CRC):
 // thread k takes the 16-word group q0 + k of the stream's word grid (q0 = the group of the tile's first word),
 // the tile's stored words in it and zeros for the rest, and shifts its raw CRC to the end of its block.
-template <int CT, bool CRC = false, bool HELP = false>
+// SUB (r06): x - min made while loading (dc_encode_sub_device, the halo path) -- its own instantiation, so that the
+// default one holds no code for it
+template <int CT, bool CRC = false, bool HELP = false, bool SUB = false>
 __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
     const float* __restrict__ x, long long n, long long idx0, Params P, uint32_t* __restrict__ out,
     uint64_t* __restrict__ st, uint64_t* __restrict__ tl, unsigned ntiles, int start_bit,
@@ -1285,7 +1287,7 @@ __global__ __launch_bounds__(ENC_TPB, DC_FUSED_WAVES) void encode_fused_kernel(
             const long long e = w0 - k;
             hw[k - 1] = (e < n && e >= -3 && idx0 + e >= 0) ? x[e] : 0.0f;
         }
-        if (!CRC && !HELP && P.sub) {                                      // (dc_encode_sub_device: x - min)
+        if (SUB) {                                                         // (dc_encode_sub_device: x - min)
             const float m = P.subp ? *P.subp : P.submin;
             if (__builtin_expect(isfinite(m), 1)) {
 #pragma unroll
@@ -2120,6 +2122,18 @@ extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, con
         break;
                 DC_ENC_HELPK(5) DC_ENC_HELPK(6) DC_ENC_HELPK(7) DC_ENC_HELPK(11)
 #undef DC_ENC_HELPK
+                default: return -2;
+            }
+        } else if (P->sub) {                 // (x - min made while loading)
+            switch (P->ct) {
+#define DC_ENC_SUBK(C)                                                                               \
+    case C:                                                                                          \
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(encode_fused_kernel<C, false, false, true>), dim3(grid + scan), dim3(ENC_TPB), \
+                           0, stream, x, n, idx0, *P, out, st, st + ntiles, ntiles, start_bit, total_bits, total_bits2, \
+                           epoch, err, dbg, scan, nullptr, nullptr, g_enc_mirror);                   \
+        break;
+                DC_ENC_SUBK(5) DC_ENC_SUBK(6) DC_ENC_SUBK(7) DC_ENC_SUBK(11)
+#undef DC_ENC_SUBK
                 default: return -2;
             }
         } else {
