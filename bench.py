@@ -163,14 +163,22 @@ def halo_bench(args):
     # no host read inside a step: the planes' decoder status is read after the timed steps
     L.L.dc_set_halo_async(1)
 
+    pair = os.environ.get("DC_HALO_PAIR", "1") != "0"            # decode both planes at once
+    epair = os.environ.get("DC_HALO_EPAIR", "1") != "0"          # encode both planes at once
+
     def step():
-        for h, v in enumerate(planes):
-            L.halo_encode_device(ct, p.data_ptr(), (mi, mj, mk), 3, v, (imax, jmax, kmax), st[h].data_ptr(),
-                                 bits.data_ptr() + 8 * h, mins.data_ptr() + 4 * h)
+        if epair:                                   # both planes at once (two streams, DC_HALO_EPAIR=0: one by one)
+            L.halo_encode2_device(ct, p.data_ptr(), (mi, mj, mk), 3, planes[0], planes[1], (imax, jmax, kmax),
+                                  st[0].data_ptr(), st[1].data_ptr(), bits.data_ptr(), bits.data_ptr() + 8,
+                                  mins.data_ptr(), mins.data_ptr() + 4)
+        else:
+            for h, v in enumerate(planes):
+                L.halo_encode_device(ct, p.data_ptr(), (mi, mj, mk), 3, v, (imax, jmax, kmax), st[h].data_ptr(),
+                                     bits.data_ptr() + 8 * h, mins.data_ptr() + 4 * h)
         if dist is None:
             # both planes at once (each on its own stream: the decoders are one-workgroup scans); DC_HALO_PAIR=0
             # decodes them one after the other
-            if os.environ.get("DC_HALO_PAIR", "1") != "0":
+            if pair:
                 L.halo_decode2_device(ct, st[0].data_ptr(), st[1].data_ptr(), bits.data_ptr(), bits.data_ptr() + 8, 0, 0,
                                       mins.data_ptr(), mins.data_ptr() + 4, q.data_ptr(), (mi, mj, mk), 3, planes[0],
                                       planes[1], (imax, jmax, kmax))

@@ -2054,6 +2054,15 @@ extern "C" int dc_encode_crc_fused_last(void) { return g_enc_crc_fused; }
 // buffer (the receiver's), nullptr otherwise
 static uint32_t* g_enc_mirror = nullptr;
 extern "C" void dc_set_encode_mirror(void* dst) { g_enc_mirror = (uint32_t*)dst; }
+// 1 when an encode takes the plain single-pass instantiation (no pipe, chained look-back, helping or multi-pass
+// variant is selected): dc_halo_encode2_device runs two such encodes side by side with their own scratch
+extern "C" int dc_encode_plain(void) {
+    if (g_enc_help < 0) g_enc_help = (getenv("DC_ENC_HELP") && *getenv("DC_ENC_HELP") == '1') ? 1 : 0;
+    const char* sc = getenv("DC_ENC_SCAN");
+    const char* pp = getenv("DC_ENC_PIPE");
+    return enc_mode_default() == 1 && !g_enc_help && !(sc && *sc == '0') && !(pp ? (*pp != '0') : DC_ENC_PIPE) &&
+           !g_enc_mirror;
+}
 
 extern "C" int dc_launch_encode(const float* x, long long n, long long idx0, const Params* P,
                                 uint32_t* out, uint64_t* desc, unsigned* flag, uint32_t epoch, int start_bit, unsigned long long* total_bits, unsigned long long* total_bits2,

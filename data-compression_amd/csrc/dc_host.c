@@ -113,7 +113,11 @@ typedef struct {
     const float* enc_subp;                  /* encode_on: the same on the device (the halo path; NULL: none) */
     hipStream_t st2;                        /* dc_halo_decode2_device: the second plane's stream */
     hipEvent_t ev_h0, ev_h1;                /* its fork and join with the library stream */
-    void* halo_a2; size_t halo_a2_cap;      /* the second plane's values */
+    void* halo_a2; size_t halo_a2_cap;      /* the second plane's values (decode2) / gathered floats (encode2) */
+    float* part_v2; long long* part_i2;     /* encode2: the second plane's minimum partials */
+    uint64_t* enc_desc2; long long enc_desc2_cap;   /* encode2: the second encode's tile states */
+    unsigned* d_enc_flag2;                  /* encode2: its flags */
+    uint32_t enc_epoch2;                    /* encode2: its epoch */
     uint8_t* runs_maps2;                    /* the second plane's small-stream decoder scratch */
     int halo_unfused;                       /* 1: the halo encode's separate passes (dc_set_halo_unfused, A/B) */
     int tiny_used, tiny_last;               /* the pending decode went to / the last finished one stayed on the
@@ -854,6 +858,12 @@ int dc_set_halo_unfused(int on) {
 int dc_set_halo_async(int on) {
     const int old = G.halo_async;
     G.halo_async = on ? 1 : 0;
+    /* leaving async mode: the caller has read the status of its planes itself (dc_decode_status), so the queued
+       count of those decodes must not make the next decode's dc_decode_finish report them as never completed */
+    if (old && !G.halo_async) {
+        G.dec_queued = 0;
+        G.dec_pending = 0;
+    }
     return old;
 }
 int dc_last_decode_launched_runs(void) { return G.runs_used; }
@@ -1424,6 +1434,78 @@ int dc_halo_decode_device(int ct, const void* d_stream, long long nbytes, const 
     return DC_OK;
 }
 
+/* (r06) Two halo planes of one array encoded at once (impl/himenoBMTxps.c:644-690: a rank compresses its two z-halo
+   planes every iteration): plane v0 as dc_halo_encode_device on the library stream, plane v1 on a second stream with
+   its own gathered floats, minimum partials and encoder scratch -- each encode of 65,536 floats is a few small
+   launches, so the two overlap.  The fused path only (not CT7 with type <= 0, which needs the mean); otherwise, or
+   when the encoder runs a non-default variant, the planes go one after the other. */
+static int halo_streams(void) {
+    if (!G.st2) {
+        HIPCHK(hipStreamCreateWithFlags(&G.st2, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&G.ev_h0, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&G.ev_h1, hipEventDisableTiming));
+    }
+    return DC_OK;
+}
+int dc_halo_encode2_device(int ct, const void* d_p, int mi, int mj, int mk, int ijk, int v0, int v1, int imax, int jmax,
+                           int kmax, int type, uint32_t mask17, void* s0, void* s1, unsigned long long* bits0,
+                           unsigned long long* bits1, float* dmin0, float* dmin1) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    int A = 0, B = 0;
+    if ((rc = plane_dims(ijk, imax, jmax, kmax, &A, &B))) return rc;
+    const long long n = (long long)A * B;
+    if (!valid_ct(ct) || (ct == 7 && type <= 0) || G.halo_unfused || !dc_encode_plain() || !bits1 || !dmin1 || n <= 0 ||
+        v1 < 0 || (ijk == 1 && v1 >= mi) || (ijk == 2 && v1 >= mj) || (ijk == 3 && v1 >= mk) ||
+        ((uintptr_t)s1 & 3u) || A > (ijk == 1 ? mj : mi) || B > (ijk == 3 ? mj : mk)) {
+        if ((rc = dc_halo_encode_device(ct, d_p, mi, mj, mk, ijk, v0, imax, jmax, kmax, type, mask17, s0, bits0, dmin0,
+                                        NULL, NULL)))
+            return rc;
+        return dc_halo_encode_device(ct, d_p, mi, mj, mk, ijk, v1, imax, jmax, kmax, type, mask17, s1, bits1, dmin1,
+                                     NULL, NULL);
+    }
+    if ((rc = halo_streams())) return rc;
+    if (grow(&G.halo_a2, &G.halo_a2_cap, (size_t)n * 4 + 64)) return DC_ERR_HIP;
+    if (!G.part_v2) {
+        HIPCHK(hipMalloc((void**)&G.part_v2, DC_MIN_PARTS * sizeof(float)));
+        HIPCHK(hipMalloc((void**)&G.part_i2, DC_MIN_PARTS * sizeof(long long)));
+        HIPCHK(hipMalloc((void**)&G.d_enc_flag2, 8192));
+        HIPCHK(hipMemset(G.d_enc_flag2, 0, 8192));
+    }
+    if (dc_encode_desc_words(n) + 8 > G.enc_desc2_cap) {
+        if (G.enc_desc2) HIPCHK(hipFree(G.enc_desc2));
+        const long long cap = dc_encode_desc_words(n) + 1024;
+        HIPCHK(hipMalloc((void**)&G.enc_desc2, cap * sizeof(uint64_t)));
+        HIPCHK(hipMemset(G.enc_desc2, 0, cap * sizeof(uint64_t)));
+        G.enc_desc2_cap = cap;
+        G.enc_epoch2 = 0;
+    }
+    HIPCHK(hipEventRecord(G.ev_h0, G.st));                            /* the second stream after the library's */
+    HIPCHK(hipStreamWaitEvent(G.st2, G.ev_h0, 0));
+    if ((rc = dc_halo_encode_device(ct, d_p, mi, mj, mk, ijk, v0, imax, jmax, kmax, type, mask17, s0, bits0, dmin0, NULL,
+                                    NULL)))
+        return rc;
+    if (dc_launch_plane_gather_min((const float*)d_p, mj, mk, ijk, v1, A, B, (float*)G.halo_a2, G.part_v2, G.part_i2,
+                                   dmin1, G.st2))
+        return seterr(DC_ERR_HIP, "plane gather launch failed");
+    Params P;
+    make_params(&P, ct, type, mask17);
+    P.sub = 1;
+    P.subp = dmin1;
+    if (++G.enc_epoch2 >= dc_encode_epoch_limit() || G.enc_epoch2 == 1) {
+        HIPCHK(hipMemsetAsync(G.enc_desc2, 0, (size_t)G.enc_desc2_cap * sizeof(uint64_t), G.st2));
+        HIPCHK(hipMemsetAsync(G.d_enc_flag2, 0, 4096, G.st2));
+        G.enc_epoch2 = 1;
+    }
+    if (dc_launch_encode((const float*)G.halo_a2, n, 0, &P, (uint32_t*)s1, G.enc_desc2, G.d_enc_flag2, G.enc_epoch2, 0,
+                         bits1, NULL, G.d_enc_err, NULL, 0, NULL, NULL, G.st2))
+        return seterr(DC_ERR_HIP, "encode launch failed: %s", hipGetErrorString(hipGetLastError()));
+    G.enc_outstanding++;                             /* (a timeout in either encode is reported, not re-run) */
+    HIPCHK(hipEventRecord(G.ev_h1, G.st2));                           /* the library stream after both */
+    HIPCHK(hipStreamWaitEvent(G.st, G.ev_h1, 0));
+    return DC_OK;
+}
+
 /* (r06) Two halo planes of one array (the two z-neighbours' planes of a Himeno step, impl/himenoBMTxps.c:696-706)
    decoded at once: each plane's small-stream decode and scatter on its own stream -- the decoders are one-
    workgroup scans, so two of them overlap on the GPU.  Asynchronous, as dc_halo_decode_device under
@@ -1449,11 +1531,7 @@ int dc_halo_decode2_device(int ct, const void* s0, const void* s1, const unsigne
             return rc;
         return dc_halo_decode_device(ct, s1, -1, bits1, type, mask17, dmin1, d_p, mi, mj, mk, ijk, v1, imax, jmax, kmax);
     }
-    if (!G.st2) {
-        HIPCHK(hipStreamCreateWithFlags(&G.st2, hipStreamNonBlocking));
-        HIPCHK(hipEventCreateWithFlags(&G.ev_h0, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&G.ev_h1, hipEventDisableTiming));
-    }
+    if ((rc = halo_streams())) return rc;
     if (grow(&G.halo_a, &G.halo_a_cap, (size_t)n * 4 + 64) || grow(&G.halo_a2, &G.halo_a2_cap, (size_t)n * 4 + 64))
         return DC_ERR_HIP;
     if (!G.runs_maps) HIPCHK(hipMalloc((void**)&G.runs_maps, dc_decode_runs_scratch_bytes()));

@@ -237,6 +237,7 @@ int dc_launch_med_sub(const float* x, long long n, void* scratch, float* d_min, 
                       int* d_type, int wide, hipStream_t st);
 int dc_launch_plane_gather_min(const float* p, int mj, int mk, int ijk, int v, int A, int B, float* out, float* part_v,
                                long long* part_i, float* d_min, dc_hip_stream st);
+int dc_encode_plain(void);
 int dc_launch_sub_ptr(const float* x, long long n, const float* d_min, float* y, dc_hip_stream st);
 int dc_launch_sub_value(const float* x, long long n, float m, float* y, hipStream_t st);
 int dc_launch_med_wide(const float* x, long long n, float s_init, void* scratch, float* d_mean, int* d_type,

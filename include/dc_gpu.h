@@ -141,6 +141,11 @@ int dc_set_halo_async(int on);
  * minimum, encode) instead of the fused ones (gather with the minimum's partials, min_final, an encode that subtracts
  * the minimum while loading); the same stream and minimum.  Returns the previous setting. */
 int dc_set_halo_unfused(int on);
+/* Two planes of one array encoded at once (each on its own stream with its own scratch; the fused path only --
+ * otherwise one after the other): streams, bit counts and minima as two dc_halo_encode_device calls. */
+int dc_halo_encode2_device(int ct, const void* d_p, int mi, int mj, int mk, int ijk, int v0, int v1, int imax, int jmax,
+                           int kmax, int type, uint32_t mask17, void* s0, void* s1, unsigned long long* bits0,
+                           unsigned long long* bits1, float* dmin0, float* dmin1);
 /* Two planes of one array decoded at once (each on its own stream; asynchronous, dc_set_halo_async(1) required,
  * else the planes go one after the other): the two z-neighbour planes of a Himeno step.  A plane the small-stream
  * decoder declines sets dc_decode_status(); decode it again with dc_halo_decode_device. */

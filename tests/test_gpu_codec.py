@@ -615,6 +615,44 @@ def test_halo_decode2_pair(dc, oracle, ct, noise):
         assert np.array_equal(q2[:imax, :jmax, v].cpu().numpy().reshape(-1).view(np.uint32), want.view(np.uint32))
 
 
+@pytest.mark.parametrize("ct", [5, 6, 7, 11])
+@pytest.mark.parametrize("ijk,v0,v1", [(3, 1, 5), (1, 1, 255), (2, 7, 100)])
+def test_halo_encode2_pair(dc, oracle, ct, ijk, v0, v1):
+    """(r06) two planes encoded at once on two streams (dc_halo_encode2_device): the same bit counts, streams and
+    minima as two dc_halo_encode_device calls"""
+    import torch
+    dc.set_bound(1e-3)
+    mi, mj, mk = 257, 257, 8
+    imax, jmax, kmax = 256, 256, 7
+    rs = np.random.RandomState(ct * 100 + ijk)
+    p = (rs.rand(mi, mj, mk).astype(np.float32) * np.float32(3) - np.float32(1)).astype(np.float32)
+    dp = torch.from_numpy(p).cuda()
+    A, B = {1: (jmax, kmax), 2: (imax, kmax), 3: (imax, jmax)}[ijk]
+    n = A * B
+    t, m17 = (3, 0x0813f) if ct == 7 else (0, 0)           # (CT7 with a given mask: the fused path)
+    outs = []
+    for pairwise in (False, True):
+        st = [torch.zeros(dc.stream_capacity(n), dtype=torch.uint8, device="cuda") for _ in range(2)]
+        bits = torch.zeros(2, dtype=torch.int64, device="cuda")
+        mins = torch.zeros(2, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        if pairwise:
+            dc.halo_encode2_device(ct, dp.data_ptr(), (mi, mj, mk), ijk, v0, v1, (imax, jmax, kmax), st[0].data_ptr(),
+                                   st[1].data_ptr(), bits.data_ptr(), bits.data_ptr() + 8, mins.data_ptr(),
+                                   mins.data_ptr() + 4, type_=t, mask17=m17)
+        else:
+            for h, v in enumerate((v0, v1)):
+                dc.halo_encode_device(ct, dp.data_ptr(), (mi, mj, mk), ijk, v, (imax, jmax, kmax), st[h].data_ptr(),
+                                      bits.data_ptr() + 8 * h, mins.data_ptr() + 4 * h, type_=t, mask17=m17)
+        dc.synchronize()
+        assert dc.encode_status() == 0
+        b = bits.cpu().tolist()
+        outs.append((b, [st[h][:(b[h] + 7) // 8].cpu().numpy() for h in range(2)], mins.cpu().numpy().view(np.uint32)))
+    (b0, s0, m0), (b1, s1, m1) = outs
+    assert b0 == b1 and np.array_equal(m0, m1)
+    assert all(np.array_equal(x, y) for x, y in zip(s0, s1))
+
+
 @pytest.mark.parametrize("ct", [5, 6, 11])
 @pytest.mark.parametrize("kind", ["initmt", "noise", "negative", "zero_min", "nan", "inf"])
 @pytest.mark.parametrize("ijk,v", [(3, 1), (1, 255), (2, 7)])
