@@ -164,10 +164,13 @@ def halo_bench(args):
     L.L.dc_set_halo_async(1)
 
     pair = os.environ.get("DC_HALO_PAIR", "1") != "0"            # decode both planes at once
-    epair = os.environ.get("DC_HALO_EPAIR", "1") != "0"          # encode both planes at once
+    # one rank: the step recorded once into a HIP graph and replayed (DC_HALO_GRAPH=0: call by call); the planes
+    # encoded at once on two streams (DC_HALO_EPAIR) pays inside the graph, not call by call
+    use_graph = dist is None and os.environ.get("DC_HALO_GRAPH", "1") != "0"
+    epair = os.environ.get("DC_HALO_EPAIR", "1" if use_graph else "0") == "1"
 
     def step():
-        if epair:                                   # both planes at once (two streams, DC_HALO_EPAIR=0: one by one)
+        if epair:                                   # both planes at once (two streams)
             L.halo_encode2_device(ct, p.data_ptr(), (mi, mj, mk), 3, planes[0], planes[1], (imax, jmax, kmax),
                                   st[0].data_ptr(), st[1].data_ptr(), bits.data_ptr(), bits.data_ptr() + 8,
                                   mins.data_ptr(), mins.data_ptr() + 4)
@@ -207,22 +210,44 @@ def halo_bench(args):
     for _ in range(max(args.warmup, 1)):
         step()
     L.synchronize()
+    graph = None
+    if use_graph:
+        L.capture_begin()
+        step()
+        graph = L.capture_end()
+        for _ in range(max(args.warmup, 1)):
+            L.graph_launch(graph)
+        L.synchronize()
+    run = (lambda: L.graph_launch(graph)) if graph is not None else step
     nbytes = [(int(b) + 7) // 8 for b in bits.cpu()]
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        run()
     L.synchronize()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     dstat = L.decode_status()
+    estat = L.encode_status()
     L.L.dc_set_halo_async(0)
-    if dstat != 0:
-        print(f"bench.py: halo decoder status 0x{dstat:x} after the timed steps", file=sys.stderr)
+    if graph is not None:
+        L.graph_destroy(graph)
+    if dstat != 0 or estat != 0:
+        print(f"bench.py: halo decoder status 0x{dstat:x}, encoder status 0x{estat:x} after the timed steps",
+              file=sys.stderr)
         sys.exit(1)
     xcheck = None
+    if dist is None:                                # the last (replayed) step's output = the calls issued directly
+        got = (bits.clone(), mins.clone(), [s.clone() for s in st], q[:, :, planes].clone())
+        L.L.dc_set_halo_async(1)
+        step()
+        L.synchronize()
+        L.L.dc_set_halo_async(0)
+        xcheck = (torch.equal(got[0], bits) and torch.equal(got[1].view(torch.int32), mins.view(torch.int32)) and
+                  all(torch.equal(a, b) for a, b in zip(got[2], st)) and
+                  torch.equal(got[3].view(torch.int32), q[:, :, planes].view(torch.int32)))
     if dist is not None:
         # the plane received from up must be up's plane k = 1 and the one from down down's plane
         # k = kmax - 2 (each rank's field differs): encoded here from the neighbour's field, the same
@@ -269,6 +294,7 @@ def halo_bench(args):
                                   "plane gather + toSmallDataset + encode, decode + min scatter", "ct": ct,
                       "plane_floats": n, "stream_bytes": nbytes, "ratio": round(4.0 * n / max(nbytes[0], 1), 3),
                       "parallelism": f"dp{world}",
+                      "launch": "one HIP graph per step" if graph is not None else "call by call",
                       "exchange": ("none (one rank: each plane decoded locally)" if dist is None else
                                    "z-neighbour exchange inside the timed step: sizes + min, then the stream bytes "
                                    f"(torch.distributed P2P, {dist.get_backend()}); rank 0 received {xfer} bytes"),

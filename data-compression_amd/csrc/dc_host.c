@@ -120,6 +120,9 @@ typedef struct {
     uint32_t enc_epoch2;                    /* encode2: its epoch */
     uint8_t* runs_maps2;                    /* the second plane's small-stream decoder scratch */
     int halo_unfused;                       /* 1: the halo encode's separate passes (dc_set_halo_unfused, A/B) */
+    int capturing;                          /* between dc_capture_begin and dc_capture_end */
+    int capture_bad;                        /* a call inside the capture that a replay cannot repeat */
+    char capture_why[160];
     int tiny_used, tiny_last;               /* the pending decode went to / the last finished one stayed on the
                                                one-workgroup decoder (dc_decode_tiny.hip) */
     int tiny_key;                           /* ct * 256 + B + 1 of parameters whose small stream it declined */
@@ -519,7 +522,12 @@ static int encode_on(hipStream_t st, int ct, const void* d_x, long long n, long 
     }
     /* the kernel writes the total to both (no copy node per encode).  Epochs tag the tile states and flags:
        when they wrap, every old tag is cleared (a state of an old encode must never read as published) */
-    if (++G.enc_epoch >= dc_encode_epoch_limit() || G.enc_epoch == 1) {
+    if (G.capturing) {
+        /* a graph replays the same epoch each time: the tile states this encode reads are cleared in the graph */
+        HIPCHK(hipMemsetAsync(G.enc_desc, 0, (size_t)(dc_encode_desc_words(n) + 8) * sizeof(uint64_t), st));
+        HIPCHK(hipMemsetAsync(G.d_enc_flag, 0, 4096, st));
+        G.enc_epoch = 1;
+    } else if (++G.enc_epoch >= dc_encode_epoch_limit() || G.enc_epoch == 1) {
         HIPCHK(hipMemsetAsync(G.enc_desc, 0, (size_t)G.enc_desc_cap * sizeof(uint64_t), st));
         HIPCHK(hipMemsetAsync(G.d_enc_flag, 0, 4096, st));
         G.enc_epoch = 1;
@@ -990,6 +998,13 @@ static int decode_device_h(int ct, const void* d_stream, long long nbytes, const
         G.dec3_used = 0;
     }
     G.dec3_launched = G.dec3_used;
+    /* inside a capture only the small-stream decoder of an async halo plane: the other decoders tag their flags
+       with a host epoch a replay would repeat, and a synchronous halo decode reads the status on the host */
+    if (G.capturing && !(halo && G.halo_async && G.runs_used)) {
+        G.capture_bad = 1;
+        snprintf(G.capture_why, sizeof G.capture_why, "a decode other than an async halo plane's small-stream decode");
+        return seterr(DC_ERR_ARG, "decode not capturable (only async halo planes on the small-stream decoder)");
+    }
     G.dec_dnbits = nbytes >= 0 ? NULL : d_nbits;
     G.dec_hnbits = nbytes >= 0 ? (unsigned long long)nbytes * 8ull : 0ull;
     if (G.tiny_used) {
@@ -1492,7 +1507,11 @@ int dc_halo_encode2_device(int ct, const void* d_p, int mi, int mj, int mk, int 
     make_params(&P, ct, type, mask17);
     P.sub = 1;
     P.subp = dmin1;
-    if (++G.enc_epoch2 >= dc_encode_epoch_limit() || G.enc_epoch2 == 1) {
+    if (G.capturing) {                          /* (as encode_on: the graph clears what this encode reads) */
+        HIPCHK(hipMemsetAsync(G.enc_desc2, 0, (size_t)(dc_encode_desc_words(n) + 8) * sizeof(uint64_t), G.st2));
+        HIPCHK(hipMemsetAsync(G.d_enc_flag2, 0, 4096, G.st2));
+        G.enc_epoch2 = 1;
+    } else if (++G.enc_epoch2 >= dc_encode_epoch_limit() || G.enc_epoch2 == 1) {
         HIPCHK(hipMemsetAsync(G.enc_desc2, 0, (size_t)G.enc_desc2_cap * sizeof(uint64_t), G.st2));
         HIPCHK(hipMemsetAsync(G.d_enc_flag2, 0, 4096, G.st2));
         G.enc_epoch2 = 1;
@@ -1550,6 +1569,70 @@ int dc_halo_decode2_device(int ct, const void* s0, const void* s1, const unsigne
         return seterr(DC_ERR_HIP, "halo decode launch failed: %s", hipGetErrorString(hipGetLastError()));
     HIPCHK(hipEventRecord(G.ev_h1, G.st2));                           /* the library stream after both */
     HIPCHK(hipStreamWaitEvent(G.st, G.ev_h1, 0));
+    return DC_OK;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* (r06) HIP graphs.  A Himeno halo step is ~14 small launches (per plane: gather + minimum, min_final, the encoder;
+   the small-stream decoder's three kernels and the scatter) whose GPU work is a few microseconds each, so a step
+   issued call by call is bound by the host's launch rate.  dc_capture_begin .. dc_capture_end records the library
+   calls in between (the library stream and the second halo stream, forked and joined by events) into a graph;
+   dc_graph_launch replays it with one launch.  A replay reads the same device pointers (the caller rewrites the
+   data in place between replays) and repeats the same work: encodes clear the tile states they read inside the
+   graph, and only decodes with no host epoch or host read (async halo planes on the small-stream decoder) may be
+   recorded -- any other call fails and makes dc_capture_end fail. */
+int dc_capture_begin(void) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (G.capturing) return seterr(DC_ERR_ARG, "a capture is already open");
+    if ((rc = halo_streams())) return rc;
+    HIPCHK(hipStreamBeginCapture(G.st, hipStreamCaptureModeRelaxed));
+    G.capturing = 1;
+    G.capture_bad = 0;
+    G.capture_why[0] = 0;
+    return DC_OK;
+}
+
+int dc_capture_end(void** graph_out) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (!G.capturing) return seterr(DC_ERR_ARG, "no capture open");
+    if (graph_out) *graph_out = NULL;
+    hipGraph_t g = NULL;
+    const hipError_t e = hipStreamEndCapture(G.st, &g);
+    G.capturing = 0;
+    /* replays tag tile states with epoch 1: the next direct encodes start a fresh epoch cycle (a full clear) */
+    G.enc_epoch = 0;
+    G.enc_epoch2 = 0;
+    if (e != hipSuccess || !g) {
+        (void)hipGetLastError();
+        return seterr(DC_ERR_HIP, "stream capture failed: %s", hipGetErrorString(e));
+    }
+    if (G.capture_bad) {
+        hipGraphDestroy(g);
+        G.capture_bad = 0;
+        return seterr(DC_ERR_ARG, "capture discarded: %s was called inside it", G.capture_why);
+    }
+    hipGraphExec_t ex = NULL;
+    const hipError_t ei = hipGraphInstantiate(&ex, g, NULL, NULL, 0);
+    hipGraphDestroy(g);
+    if (ei != hipSuccess) return seterr(DC_ERR_HIP, "graph instantiate failed: %s", hipGetErrorString(ei));
+    if (graph_out) *graph_out = (void*)ex;
+    else hipGraphExecDestroy(ex);
+    return DC_OK;
+}
+
+int dc_graph_launch(void* graph) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    if (!graph) return seterr(DC_ERR_ARG, "null graph");
+    if (G.capturing) return seterr(DC_ERR_ARG, "graph launch inside a capture");
+    HIPCHK(hipGraphLaunch((hipGraphExec_t)graph, G.st));
+    return DC_OK;
+}
+
+int dc_graph_destroy(void* graph) {
+    if (graph) HIPCHK(hipGraphExecDestroy((hipGraphExec_t)graph));
     return DC_OK;
 }
 

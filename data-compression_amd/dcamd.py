@@ -37,7 +37,7 @@ ABI_SYMBOLS = [
 EXT_SYMBOLS = [
     "dc_init", "dc_last_error", "dc_get_stream", "dc_synchronize", "dc_set_abs_error_bound",
     "dc_get_abs_error_bound", "dc_stream_capacity", "dc_encode_device", "dc_encode_result",
-    "dc_decode_device", "dc_decode_finish", "dc_to_small_device", "dc_med_device", "dc_prep_device", "dc_encode_sub_device", "dc_last_decode_was_tiny", "dc_set_halo_unfused", "dc_halo_decode2_device", "dc_halo_encode2_device", "dc_last_decode_launched_tiny", "dc_set_decode_tiny", "dc_crc32_device",
+    "dc_decode_device", "dc_decode_finish", "dc_to_small_device", "dc_med_device", "dc_prep_device", "dc_encode_sub_device", "dc_last_decode_was_tiny", "dc_set_halo_unfused", "dc_halo_decode2_device", "dc_halo_encode2_device", "dc_capture_begin", "dc_capture_end", "dc_graph_launch", "dc_graph_destroy", "dc_last_decode_launched_tiny", "dc_set_decode_tiny", "dc_crc32_device",
     "dc_decode_chunk_bits_value", "dc_ct1_encode_device", "dc_ct1_decode_device", "dc_encode_bits_device",
     "dc_crc32_device_async", "dc_crc32_copy_device", "dc_encode_send_device", "dc_crc32_pair_device", "dc_encode_crc_device", "dc_crc32_stream_device", "dc_crc_resend_crc_device",
     "dc_hash_device", "dc_copy_rate_device", "dc_flip_bits_device", "dc_decode_shard_device", "dc_decode_shard_fix",
@@ -446,6 +446,22 @@ class Lib:
         self.check(self.L.dc_halo_decode_device(ct, C.c_void_p(stream_ptr), C.c_longlong(nbytes), C.c_void_p(bits_ptr),
                                                 type_, C.c_uint32(mask17), C.c_void_p(min_ptr), C.c_void_p(p_ptr), *dims,
                                                 ijk, v, *ext), "dc_halo_decode_device")
+
+    def capture_begin(self):
+        """dc_capture_begin: record the following library calls into a HIP graph"""
+        self.check(self.L.dc_capture_begin(), "dc_capture_begin")
+
+    def capture_end(self):
+        """dc_capture_end: the recorded graph (an opaque handle for graph_launch / graph_destroy)"""
+        h = C.c_void_p()
+        self.check(self.L.dc_capture_end(C.byref(h)), "dc_capture_end")
+        return h
+
+    def graph_launch(self, h):
+        self.check(self.L.dc_graph_launch(h), "dc_graph_launch")
+
+    def graph_destroy(self, h):
+        self.check(self.L.dc_graph_destroy(h), "dc_graph_destroy")
 
     def halo_encode2_device(self, ct, p_ptr, dims, ijk, v0, v1, ext, s0_ptr, s1_ptr, bits0_ptr, bits1_ptr, min0_ptr,
                             min1_ptr, type_=0, mask17=0):

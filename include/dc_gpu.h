@@ -153,6 +153,17 @@ int dc_halo_decode2_device(int ct, const void* s0, const void* s1, const unsigne
                            const unsigned long long* bits1, int type, uint32_t mask17, const float* dmin0,
                            const float* dmin1, void* d_p, int mi, int mj, int mk, int ijk, int v0, int v1, int imax,
                            int jmax, int kmax);
+/* HIP graphs (no reference counterpart: the launch-bound Himeno halo step of impl/himenoBMTxps.c:644-690 replayed with
+ * one launch).  dc_capture_begin .. dc_capture_end record the library calls in between into a graph; dc_graph_launch
+ * replays it on the library stream, reading the same device buffers (rewrite the data in place between replays).
+ * Recordable: the encoders (dc_encode_device, dc_halo_encode_device, dc_halo_encode2_device) and async halo decodes
+ * on the small-stream decoder (dc_set_halo_async(1)); any other decode fails and then dc_capture_end fails.  Run the
+ * step once uncaptured first (buffers are sized on first use).  Read dc_encode_status / dc_decode_status after
+ * replays: a replay has no host-side fallback. */
+int dc_capture_begin(void);
+int dc_capture_end(void** graph_out);
+int dc_graph_launch(void* graph);
+int dc_graph_destroy(void* graph);
 
 /* Pre-passes on device data: toSmallDataset_float and med_dataset_float (exact). */
 int dc_to_small_device(const void* d_x, long long n, void* d_out, float* min_out);

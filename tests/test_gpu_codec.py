@@ -654,6 +654,102 @@ def test_halo_encode2_pair(dc, oracle, ct, ijk, v0, v1):
 
 
 @pytest.mark.parametrize("ct", [5, 6, 11])
+@pytest.mark.parametrize("pair_encode", [False, True])
+def test_halo_graph_replay(dc, oracle, ct, pair_encode):
+    """(r06) the halo step recorded into a HIP graph (dc_capture_begin/end) and replayed (dc_graph_launch): each replay
+    re-reads the array rewritten in place and gives the streams, bit counts, minima and decoded planes of the same
+    calls issued directly; direct encodes after the replays stay correct (their epochs restart)"""
+    import torch
+    dc.set_bound(1e-3)
+    mi, mj, mk = 257, 257, 8
+    imax, jmax, kmax = 256, 256, 7
+    n = imax * jmax
+    planes = [1, kmax - 2]
+    rs = np.random.RandomState(ct)
+    fields = [(rs.rand(mi, mj, mk).astype(np.float32) * np.float32(2 + k) - np.float32(k)).astype(np.float32)
+              for k in range(3)]
+    dp = torch.from_numpy(fields[0]).cuda()
+
+    def bufs():
+        return ([torch.zeros(dc.stream_capacity(n), dtype=torch.uint8, device="cuda") for _ in range(2)],
+                torch.zeros(2, dtype=torch.int64, device="cuda"), torch.zeros(2, dtype=torch.float32, device="cuda"),
+                torch.zeros(mi, mj, mk, dtype=torch.float32, device="cuda"))
+
+    def step(b):
+        st, bits, mins, q = b
+        if pair_encode:
+            dc.halo_encode2_device(ct, dp.data_ptr(), (mi, mj, mk), 3, planes[0], planes[1], (imax, jmax, kmax),
+                                   st[0].data_ptr(), st[1].data_ptr(), bits.data_ptr(), bits.data_ptr() + 8,
+                                   mins.data_ptr(), mins.data_ptr() + 4)
+        else:
+            for h, v in enumerate(planes):
+                dc.halo_encode_device(ct, dp.data_ptr(), (mi, mj, mk), 3, v, (imax, jmax, kmax), st[h].data_ptr(),
+                                      bits.data_ptr() + 8 * h, mins.data_ptr() + 4 * h)
+        dc.halo_decode2_device(ct, st[0].data_ptr(), st[1].data_ptr(), bits.data_ptr(), bits.data_ptr() + 8, 0, 0,
+                               mins.data_ptr(), mins.data_ptr() + 4, q.data_ptr(), (mi, mj, mk), 3, planes[0], planes[1],
+                               (imax, jmax, kmax))
+
+    def result(b):
+        st, bits, mins, q = b
+        bb = bits.cpu().tolist()
+        return (bb, [st[h][:(bb[h] + 7) // 8].cpu().numpy() for h in range(2)], mins.cpu().numpy().view(np.uint32),
+                q[:imax, :jmax, planes].cpu().numpy().view(np.uint32))
+
+    def same(a, b):
+        return a[0] == b[0] and all(np.array_equal(x, y) for x, y in zip(a[1], b[1])) and \
+            np.array_equal(a[2], b[2]) and np.array_equal(a[3], b[3])
+
+    prev = dc.L.dc_set_halo_async(1)
+    g = None
+    try:
+        torch.cuda.synchronize()
+        gb = bufs()
+        step(gb)                                   # (sizes the buffers: capture after one direct step)
+        dc.synchronize()
+        dc.capture_begin()
+        step(gb)
+        g = dc.capture_end()
+        for k in (1, 2, 0, 2):
+            dp.copy_(torch.from_numpy(fields[k]))
+            torch.cuda.synchronize()
+            db = bufs()
+            torch.cuda.synchronize()
+            step(db)                               # the same step issued directly
+            dc.synchronize()
+            want = result(db)
+            dc.graph_launch(g)
+            dc.synchronize()
+            assert dc.decode_status() == 0 and dc.encode_status() == 0
+            got = result(gb)
+            assert same(got, want), k
+            for h, v in enumerate(planes):         # and the streams against the oracle's encode of x - min
+                omn, xs = oracle.to_small(fields[k][:imax, :jmax, v].reshape(-1).copy())
+                so, nbo, _ = oracle.compress(ct, xs, 1e-3, 0, 0)
+                assert np.float32(omn).view(np.uint32) == got[2][h]
+                assert (got[0][h] + 7) // 8 == nbo and np.array_equal(got[1][h], so)
+    finally:
+        if g is not None:
+            dc.graph_destroy(g)
+        dc.L.dc_set_halo_async(prev)
+    # a decode other than an async halo plane's cannot be recorded: dc_capture_end fails and nothing is kept
+    x = torch.from_numpy(fields[0][:, :, 1].reshape(-1).copy()).cuda()
+    s = torch.zeros(dc.stream_capacity(x.numel()), dtype=torch.uint8, device="cuda")
+    tb = torch.zeros(1, dtype=torch.int64, device="cuda")
+    dc.encode_device(ct, x.data_ptr(), x.numel(), s.data_ptr(), total_ptr=tb.data_ptr())
+    nb = (dc.encode_result() + 7) // 8
+    out = torch.zeros_like(x)
+    dc.capture_begin()
+    with pytest.raises(Exception):
+        dc.decode_device(ct, s.data_ptr(), nb, x.numel(), out.data_ptr())
+    with pytest.raises(Exception):
+        dc.capture_end()
+    dc.decode_device(ct, s.data_ptr(), nb, x.numel(), out.data_ptr())     # (the library works on after it)
+    dc.decode_finish()
+    spec, _ = oracle.decompress(ct, s[:nb].cpu().numpy(), x.numel(), 1e-3, 0, 0)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), spec.view(np.uint32))
+
+
+@pytest.mark.parametrize("ct", [5, 6, 11])
 @pytest.mark.parametrize("kind", ["initmt", "noise", "negative", "zero_min", "nan", "inf"])
 @pytest.mark.parametrize("ijk,v", [(3, 1), (1, 255), (2, 7)])
 def test_halo_fused_vs_separate(dc, oracle, ct, kind, ijk, v):
