@@ -65,9 +65,14 @@ __global__ __launch_bounds__(256) void min_partial_kernel(const float* __restric
     if (threadIdx.x == 0) { pv[blockIdx.x] = sv[0]; pi[blockIdx.x] = si[0]; }
 }
 
+// (clr64 / clr32: words zeroed on the way -- in a recorded halo step the next encode's tile states and flag, which a
+// graph replay cannot tag with a new epoch; two memset nodes less per plane)
 __global__ __launch_bounds__(256) void min_final_kernel(const float* __restrict__ x, const float* __restrict__ pv,
                                                         const long long* __restrict__ pi, int nparts,
-                                                        float* __restrict__ out_min) {
+                                                        float* __restrict__ out_min, uint64_t* __restrict__ clr64,
+                                                        int n64, uint32_t* __restrict__ clr32, int n32) {
+    for (int i = threadIdx.x; i < n64; i += 256) clr64[i] = 0ull;
+    for (int i = threadIdx.x; i < n32; i += 256) clr32[i] = 0u;
     __shared__ float sv[256];
     __shared__ long long si[256];
     float mv = __int_as_float(0x7fc00000);
@@ -1964,7 +1969,8 @@ extern "C" int dc_launch_to_small(const float* x, long long n, float* y, float* 
     if (n <= 0) return 0;
     const int nparts = (int)std::min<long long>(DC_MIN_PARTS, std::max<long long>(1, n / 4096));
     hipLaunchKernelGGL(min_partial_kernel, dim3(nparts), dim3(256), 0, st, x, n, part_v, part_i);
-    hipLaunchKernelGGL(min_final_kernel, dim3(1), dim3(256), 0, st, x, part_v, part_i, nparts, d_min);
+    hipLaunchKernelGGL(min_final_kernel, dim3(1), dim3(256), 0, st, x, part_v, part_i, nparts, d_min, nullptr, 0,
+                       nullptr, 0);
     if (y) {
         long long g = (n / 4 + 255) / 256;
         if (g > 2048) g = 2048;
@@ -2276,14 +2282,8 @@ extern "C" int dc_launch_occupy(double us, int blocks, int lds, unsigned* sink, 
 
 // Himeno halo planes: the plane ijk = 1/2/3 at index v of a [mi][mj][mk] float array in
 // the order of transform_3d_array_to_1d_array (impl/dataCompression.c:3741-3775), gathered into a
-// contiguous array; and the decoded plane + min scattered back (impl/himenoBMTxps.c:699-706).
-__device__ __forceinline__ long long plane_index(long long a, long long b, int ijk, int v, int mj, int mk) {
-    long long i, j, k;
-    if (ijk == 1) { i = v; j = a; k = b; }
-    else if (ijk == 2) { i = a; j = v; k = b; }
-    else { i = a; j = b; k = v; }
-    return (i * mj + j) * mk + k;
-}
+// contiguous array; and the decoded plane + min scattered back (impl/himenoBMTxps.c:699-706).  (plane_index:
+// dc_device.h, shared with the small-stream decoder's scatter mode)
 __global__ __launch_bounds__(256) void plane_gather_kernel(const float* __restrict__ p, int mj, int mk, int ijk, int v,
                                                            int A, int B, float* __restrict__ out) {
     const long long n = (long long)A * B;
@@ -2341,14 +2341,15 @@ extern "C" int dc_launch_plane_gather(const float* p, int mj, int mk, int ijk, i
 }
 // the gathered plane and its minimum into d_min (toSmallDataset_float's minimum of the plane), two launches
 extern "C" int dc_launch_plane_gather_min(const float* p, int mj, int mk, int ijk, int v, int A, int B, float* out,
-                                          float* part_v, long long* part_i, float* d_min, hipStream_t st) {
+                                          float* part_v, long long* part_i, float* d_min, uint64_t* clr64, int n64,
+                                          uint32_t* clr32, int n32, hipStream_t st) {
     const long long n = (long long)A * B;
     if (n <= 0) return 0;
     const int g = (int)std::min<long long>(DC_MIN_PARTS, std::max<long long>(1, (n + 1023) / 1024));
     hipLaunchKernelGGL(plane_gather_min_kernel, dim3((unsigned)g), dim3(256), 0, st, p, mj, mk, ijk, v, A, B, out,
                        part_v, part_i);
     hipLaunchKernelGGL(min_final_kernel, dim3(1), dim3(256), 0, st, (const float*)out, (const float*)part_v,
-                       (const long long*)part_i, g, d_min);
+                       (const long long*)part_i, g, d_min, clr64, n64, clr32, n32);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 // y = x - *d_min (the reference's x86 subtraction)

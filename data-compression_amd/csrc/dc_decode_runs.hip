@@ -137,13 +137,30 @@ struct RsWords {
     }
 };
 
+// (r06) the values kernel's scatter mode: value g of a Himeno halo plane goes to its element of the array, plus the
+// plane's minimum (the plane_scatter_kernel pass fused into the decode, impl/himenoBMTxps.c:699-706)
+struct RunsScatter {
+    float* p;
+    const float* dmin;
+    int mj, mk, ijk, v, B;
+};
+
 // one block's tokens from its first chunk's entry, the incoming history h (pass 1: symbolic slots; the
-// values kernel: constants), values to out when STORE (and their history constant).  Returns the history
-// after the block.
-template <int CT, bool STORE>
+// values kernel: constants), values stored when STORE (1: out[g]; 2: the plane element of S, + mn) and their
+// history constant.  Returns the history after the block.
+template <int CT, int STORE>
 __device__ __forceinline__ void block_walk(const RsWords& W, const Params& P, long long c0, long long c1, int entry,
                                            const uint8_t* cn, long long g, long long num, unsigned long long nbits,
-                                           Hs& h1, Hs& h2, Hs& h3, bool& sent, float* __restrict__ out) {
+                                           Hs& h1, Hs& h2, Hs& h3, bool& sent, float* __restrict__ out,
+                                           const RunsScatter& S = RunsScatter{}, float mn = 0.0f) {
+    auto put = [&](long long e, float x) {
+        if (STORE == 1) {
+            out[e] = x;
+        } else if (STORE == 2) {
+            const int a = (int)e / S.B;                     // (a plane holds < 2^31 values)
+            S.p[plane_index(a, (int)e - a * S.B, S.ijk, S.v, S.mj, S.mk)] = __fadd_rn(x, mn);
+        }
+    };
     long long pos = 256 * c0 + entry;
     for (int j = 0; j < RUNS_BMAX && g < num; j++) {
         const long long c = c0 + j;
@@ -158,7 +175,7 @@ __device__ __forceinline__ void block_walk(const RsWords& W, const Params& P, lo
                 const Hs v = (t >> 29) == 4u ? Hs{0u, 0.0f} : h1;
                 if ((t >> 29) == 5u && g < 3) sent = true;      // a prediction among the stream's first three
                 if (STORE)
-                    for (int q = 0; q < k; q++) out[g + q] = v.v;
+                    for (int q = 0; q < k; q++) put(g + q, v.v);
                 h3 = k == 2 ? h1 : v;                           // (two tokens keep the value before them)
                 h2 = v; h1 = v;
                 pos += 3 * k;
@@ -181,7 +198,7 @@ __device__ __forceinline__ void block_walk(const RsWords& W, const Params& P, lo
                     v = Hs{4u, 0.0f};
             }
             if (v.k == 0 && __float_as_uint(v.v) == 0xBF800000u) sent = true;   // the history sentinel
-            if (STORE) out[g] = v.v;
+            if (STORE) put(g, v.v);
             h3 = h2; h2 = h1; h1 = v;
             pos += len;
             g++;
@@ -345,7 +362,7 @@ __global__ __launch_bounds__(RUNS_T) void runs_scan_kernel(const uint8_t* __rest
     RsWords W{staged ? pool : nullptr, s, nbytes, 0, 1};
     Hs h1 = {1u, 0.f}, h2 = {2u, 0.f}, h3 = {3u, 0.f};
     bool sent = false;
-    if (c0 < c1) block_walk<CT, false>(W, P, c0, c1, y, cn, T0, num, nbits, h1, h2, h3, sent, nullptr);
+    if (c0 < c1) block_walk<CT, 0>(W, P, c0, c1, y, cn, T0, num, nbits, h1, h2, h3, sent, nullptr);
     if (h1.k == 4u || h2.k == 4u || h3.k == 4u) atomicOr(&bad, 1);
     if (sent) atomicOr(&bad, 2);
     RSTAMP(5);
@@ -416,11 +433,11 @@ __global__ __launch_bounds__(RUNS_T) void runs_scan_kernel(const uint8_t* __rest
 }
 
 // thread = block: its values from its first chunk's entry with the concrete incoming history
-template <int CT>
+template <int CT, bool SCAT>
 __global__ __launch_bounds__(64) void runs_values_kernel(const uint8_t* __restrict__ s, Params P, RunsBufs R,
                                                         const unsigned long long* dev_nbits,
                                                         unsigned long long host_nbits, float* __restrict__ out,
-                                                        long long num) {
+                                                        long long num, RunsScatter S) {
     constexpr int ROW = 8 * RUNS_BMAX + 2;                      // a block's stream words (+ 2 past its end)
     __shared__ uint32_t kw[64 * ROW];
     const unsigned long long nbits = dev_nbits ? *dev_nbits : host_nbits;
@@ -444,13 +461,14 @@ __global__ __launch_bounds__(64) void runs_values_kernel(const uint8_t* __restri
     Hs h1 = {0u, hb.x}, h2 = {0u, hb.y}, h3 = {0u, hb.z};
     bool sent = false;
     RsWords W{row, s, nbytes, 8 * c0, 0};
-    block_walk<CT, true>(W, P, c0, c0 + nc, (int)(b.x & 0xFFu), cn, (long long)b.y, num, nbits, h1, h2, h3, sent, out);
+    block_walk<CT, SCAT ? 2 : 1>(W, P, c0, c0 + nc, (int)(b.x & 0xFFu), cn, (long long)b.y, num, nbits, h1, h2, h3,
+                                 sent, out, S, SCAT ? *S.dmin : 0.0f);
     if (sent) atomicOr(R.err, RUNS_DECLINE | RUNS_WHY_SENT);
 }
 
-extern "C" int dc_launch_decode_runs(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
-                                     long long max_chunks, const Params* P, uint8_t* maps, unsigned* err, float* out,
-                                     long long num, hipStream_t st) {
+static int launch_runs(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                       long long max_chunks, const Params* P, uint8_t* maps, unsigned* err, float* out, long long num,
+                       const RunsScatter* S, hipStream_t st) {
     if (max_chunks > RUNS_MAXC + 8 || max_chunks < 1) return -2;     // (the stream's own length is checked on the device)
     RunsBufs R;
     const size_t mb = (size_t)(RUNS_MAXC + 8) * 32;
@@ -471,8 +489,12 @@ extern "C" int dc_launch_decode_runs(const uint8_t* s, const unsigned long long*
         hipLaunchKernelGGL(runs_scan_kernel<C>, dim3(1), dim3(RUNS_T), 0, st, s, *P, R, dev_nbits, host_nbits, \
                            num);                                                                               \
         dc_mark_phase(5, st);                                                                                  \
-        hipLaunchKernelGGL(runs_values_kernel<C>, dim3(RUNS_T / 64), dim3(64), 0, st, s, *P, R, dev_nbits,     \
-                           host_nbits, out, num);                                                              \
+        if (S)                                                                                                 \
+            hipLaunchKernelGGL((runs_values_kernel<C, true>), dim3(RUNS_T / 64), dim3(64), 0, st, s, *P, R,     \
+                               dev_nbits, host_nbits, out, num, *S);                                           \
+        else                                                                                                   \
+            hipLaunchKernelGGL((runs_values_kernel<C, false>), dim3(RUNS_T / 64), dim3(64), 0, st, s, *P, R,    \
+                               dev_nbits, host_nbits, out, num, RunsScatter{});                                \
         break;
         DC_RUNS_CASE(5)
         DC_RUNS_CASE(6)
@@ -484,6 +506,21 @@ extern "C" int dc_launch_decode_runs(const uint8_t* s, const unsigned long long*
     dc_mark_phase(7, st);
     dc_mark_next_set();
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+extern "C" int dc_launch_decode_runs(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                                     long long max_chunks, const Params* P, uint8_t* maps, unsigned* err, float* out,
+                                     long long num, hipStream_t st) {
+    return launch_runs(s, dev_nbits, host_nbits, max_chunks, P, maps, err, out, num, nullptr, st);
+}
+// (r06) a Himeno halo plane decoded straight into its array: value e of the A x B plane ijk at index v to its element of
+// the [.][mj][mk] array p, plus *d_min (as dc_launch_decode_runs followed by dc_launch_plane_scatter, one launch less)
+extern "C" int dc_launch_decode_runs_scatter(const uint8_t* s, const unsigned long long* dev_nbits,
+                                             unsigned long long host_nbits, long long max_chunks, const Params* P,
+                                             uint8_t* maps, unsigned* err, long long num, float* p, const float* d_min,
+                                             int mj, int mk, int ijk, int v, int B, hipStream_t st) {
+    if (!p || !d_min || B <= 0 || num >= (1ll << 31)) return -2;
+    const RunsScatter S{p, d_min, mj, mk, ijk, v, B};
+    return launch_runs(s, dev_nbits, host_nbits, max_chunks, P, maps, err, nullptr, num, &S, st);
 }
 extern "C" long long dc_decode_runs_max_chunks(void) { return RUNS_MAXC; }
 extern "C" size_t dc_decode_runs_scratch_bytes(void) {

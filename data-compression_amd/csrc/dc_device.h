@@ -536,4 +536,14 @@ __device__ __forceinline__ void st_relaxed(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// a Himeno halo plane's element (a, b) in the [mi][mj][mk] array: the plane ijk = 1/2/3 at index v, in the order of
+// transform_3d_array_to_1d_array (impl/dataCompression.c:3741-3775)
+__device__ __forceinline__ long long plane_index(long long a, long long b, int ijk, int v, int mj, int mk) {
+    long long i, j, k;
+    if (ijk == 1) { i = v; j = a; k = b; }
+    else if (ijk == 2) { i = a; j = v; k = b; }
+    else { i = a; j = b; k = v; }
+    return (i * mj + j) * mk + k;
+}
+
 }  // namespace dc

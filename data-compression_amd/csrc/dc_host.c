@@ -121,6 +121,7 @@ typedef struct {
     uint8_t* runs_maps2;                    /* the second plane's small-stream decoder scratch */
     int halo_unfused;                       /* 1: the halo encode's separate passes (dc_set_halo_unfused, A/B) */
     int capturing;                          /* between dc_capture_begin and dc_capture_end */
+    int enc_precleared;                     /* (capture) the next encode's tile states were zeroed by min_final */
     int capture_bad;                        /* a call inside the capture that a replay cannot repeat */
     char capture_why[160];
     int tiny_used, tiny_last;               /* the pending decode went to / the last finished one stayed on the
@@ -523,9 +524,12 @@ static int encode_on(hipStream_t st, int ct, const void* d_x, long long n, long 
     /* the kernel writes the total to both (no copy node per encode).  Epochs tag the tile states and flags:
        when they wrap, every old tag is cleared (a state of an old encode must never read as published) */
     if (G.capturing) {
-        /* a graph replays the same epoch each time: the tile states this encode reads are cleared in the graph */
-        HIPCHK(hipMemsetAsync(G.enc_desc, 0, (size_t)(dc_encode_desc_words(n) + 8) * sizeof(uint64_t), st));
-        HIPCHK(hipMemsetAsync(G.d_enc_flag, 0, 4096, st));
+        /* a graph replays the same epoch each time: the tile states this encode reads are cleared in the graph
+           (by the halo path's min_final launch, or here) */
+        if (!G.enc_precleared) {
+            HIPCHK(hipMemsetAsync(G.enc_desc, 0, (size_t)(dc_encode_desc_words(n) + 8) * sizeof(uint64_t), st));
+            HIPCHK(hipMemsetAsync(G.d_enc_flag, 0, 4096, st));
+        }
         G.enc_epoch = 1;
     } else if (++G.enc_epoch >= dc_encode_epoch_limit() || G.enc_epoch == 1) {
         HIPCHK(hipMemsetAsync(G.enc_desc, 0, (size_t)G.enc_desc_cap * sizeof(uint64_t), st));
@@ -1396,9 +1400,15 @@ int dc_halo_encode_device(int ct, const void* d_p, int mi, int mj, int mk, int i
            wants it, and the encoder subtracts it while loading (no x - min written, no copy of the minimum): three
            launches instead of six */
         float* dmin = d_min ? d_min : &G.d_f[0];
+        /* recorded into a graph: min_final zeroes the encoder's tile states and flag (no memset nodes), when the
+           encoder's buffer will not grow */
+        const long long dw = dc_encode_desc_words(n) + 8;
+        const int pre = G.capturing && G.enc_desc && dw <= G.enc_desc_cap && dw < (1 << 30);
         if (dc_launch_plane_gather_min((const float*)d_p, mj, mk, ijk, v, A, B, (float*)G.halo_a, G.part_v, G.part_i,
-                                       dmin, G.st))
+                                       dmin, pre ? (uint64_t*)G.enc_desc : NULL, pre ? (int)dw : 0,
+                                       pre ? (uint32_t*)G.d_enc_flag : NULL, pre ? 1024 : 0, G.st))
             return seterr(DC_ERR_HIP, "plane gather launch failed");
+        G.enc_precleared = pre;
         if (type_out) *type_out = type;
         if (mask17_out) *mask17_out = mask17;
         if (G.enc_st) {
@@ -1408,6 +1418,7 @@ int dc_halo_encode_device(int ct, const void* d_p, int mi, int mj, int mk, int i
         G.enc_subp = dmin;
         rc = encode_on(G.st, ct, G.halo_a, n, 0, type, mask17, 0, d_stream, d_bits, NULL);
         G.enc_subp = NULL;
+        G.enc_precleared = 0;
         return rc;
     }
     if (dc_launch_plane_gather((const float*)d_p, mj, mk, ijk, v, A, B, (float*)G.halo_a, G.st))
@@ -1500,16 +1511,21 @@ int dc_halo_encode2_device(int ct, const void* d_p, int mi, int mj, int mk, int 
     if ((rc = dc_halo_encode_device(ct, d_p, mi, mj, mk, ijk, v0, imax, jmax, kmax, type, mask17, s0, bits0, dmin0, NULL,
                                     NULL)))
         return rc;
+    const long long dw = dc_encode_desc_words(n) + 8;     /* (capacity ensured above) */
+    const int pre = G.capturing && dw < (1 << 30);
     if (dc_launch_plane_gather_min((const float*)d_p, mj, mk, ijk, v1, A, B, (float*)G.halo_a2, G.part_v2, G.part_i2,
-                                   dmin1, G.st2))
+                                   dmin1, pre ? (uint64_t*)G.enc_desc2 : NULL, pre ? (int)dw : 0,
+                                   pre ? (uint32_t*)G.d_enc_flag2 : NULL, pre ? 1024 : 0, G.st2))
         return seterr(DC_ERR_HIP, "plane gather launch failed");
     Params P;
     make_params(&P, ct, type, mask17);
     P.sub = 1;
     P.subp = dmin1;
-    if (G.capturing) {                          /* (as encode_on: the graph clears what this encode reads) */
-        HIPCHK(hipMemsetAsync(G.enc_desc2, 0, (size_t)(dc_encode_desc_words(n) + 8) * sizeof(uint64_t), G.st2));
-        HIPCHK(hipMemsetAsync(G.d_enc_flag2, 0, 4096, G.st2));
+    if (G.capturing) {                          /* (as encode_on: min_final cleared what this encode reads) */
+        if (!pre) {
+            HIPCHK(hipMemsetAsync(G.enc_desc2, 0, (size_t)dw * sizeof(uint64_t), G.st2));
+            HIPCHK(hipMemsetAsync(G.d_enc_flag2, 0, 4096, G.st2));
+        }
         G.enc_epoch2 = 1;
     } else if (++G.enc_epoch2 >= dc_encode_epoch_limit() || G.enc_epoch2 == 1) {
         HIPCHK(hipMemsetAsync(G.enc_desc2, 0, (size_t)G.enc_desc2_cap * sizeof(uint64_t), G.st2));
@@ -1560,12 +1576,23 @@ int dc_halo_decode2_device(int ct, const void* s0, const void* s1, const unsigne
     make_params(&P, ct, type, mask17);
     HIPCHK(hipEventRecord(G.ev_h0, G.st));                            /* the second stream after the library's */
     HIPCHK(hipStreamWaitEvent(G.st2, G.ev_h0, 0));
-    if (dc_launch_decode_runs((const uint8_t*)s0, bits0, 0ull, mc256, &P, G.runs_maps, G.D.err, (float*)G.halo_a, n,
-                              G.st) ||
-        dc_launch_plane_scatter((const float*)G.halo_a, dmin0, (float*)d_p, mj, mk, ijk, v0, A, B, G.st) ||
-        dc_launch_decode_runs((const uint8_t*)s1, bits1, 0ull, mc256, &P, G.runs_maps2, G.D.err, (float*)G.halo_a2, n,
-                              G.st2) ||
-        dc_launch_plane_scatter((const float*)G.halo_a2, dmin1, (float*)d_p, mj, mk, ijk, v1, A, B, G.st2))
+    static int scat = -1;                      /* DC_HALO_SCATTER=1: the values kernel scatters (measured slower) */
+    if (scat < 0) scat = getenv("DC_HALO_SCATTER") && atoi(getenv("DC_HALO_SCATTER")) == 1;
+    if (scat && !G.halo_unfused) {
+        /* (r06) each plane decoded straight into the array (the values kernel adds the minimum and scatters): one
+           launch less, but its lanes each write a block's values with the plane's stride, 20.9 us against 10.6 for
+           the values and 4.5 for the coalesced scatter pass (rocprof, CT5 halo planes) */
+        if (dc_launch_decode_runs_scatter((const uint8_t*)s0, bits0, 0ull, mc256, &P, G.runs_maps, G.D.err, n,
+                                          (float*)d_p, dmin0, mj, mk, ijk, v0, B, G.st) ||
+            dc_launch_decode_runs_scatter((const uint8_t*)s1, bits1, 0ull, mc256, &P, G.runs_maps2, G.D.err, n,
+                                          (float*)d_p, dmin1, mj, mk, ijk, v1, B, G.st2))
+            return seterr(DC_ERR_HIP, "halo decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+    } else if (dc_launch_decode_runs((const uint8_t*)s0, bits0, 0ull, mc256, &P, G.runs_maps, G.D.err,
+                                     (float*)G.halo_a, n, G.st) ||
+               dc_launch_plane_scatter((const float*)G.halo_a, dmin0, (float*)d_p, mj, mk, ijk, v0, A, B, G.st) ||
+               dc_launch_decode_runs((const uint8_t*)s1, bits1, 0ull, mc256, &P, G.runs_maps2, G.D.err,
+                                     (float*)G.halo_a2, n, G.st2) ||
+               dc_launch_plane_scatter((const float*)G.halo_a2, dmin1, (float*)d_p, mj, mk, ijk, v1, A, B, G.st2))
         return seterr(DC_ERR_HIP, "halo decode launch failed: %s", hipGetErrorString(hipGetLastError()));
     HIPCHK(hipEventRecord(G.ev_h1, G.st2));                           /* the library stream after both */
     HIPCHK(hipStreamWaitEvent(G.st, G.ev_h1, 0));

@@ -173,6 +173,9 @@ long long dc_tiny_max_values(void);
 int dc_launch_decode_runs(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
                           long long max_chunks, const DC_NS Params* P, uint8_t* maps, unsigned* err, float* out,
                           long long num, dc_hip_stream st);
+int dc_launch_decode_runs_scatter(const uint8_t* s, const unsigned long long* dev_nbits, unsigned long long host_nbits,
+                                  long long max_chunks, const DC_NS Params* P, uint8_t* maps, unsigned* err, long long num,
+                                  float* p, const float* d_min, int mj, int mk, int ijk, int v, int B, dc_hip_stream st);
 long long dc_decode_runs_max_chunks(void);
 /* the maps parse of streams whose token paths merge slowly (dc_decode_maps.hip): fills D3's rec / rel / ptot
    as parse3 would, for dc_launch_decode3_values; scratch: dc_maps_scratch_bytes(max_chunks) bytes */
@@ -235,8 +238,10 @@ int dc_launch_med(const float* x, long long n, float s_init, void* scratch, floa
                   float* d_max, dc_hip_stream st);
 int dc_launch_med_sub(const float* x, long long n, void* scratch, float* d_min, float* pv, long long* pi, float* d_mean,
                       int* d_type, int wide, hipStream_t st);
+/* (clr64[0..n64) and clr32[0..n32) zeroed by the min_final launch; NULL / 0: none) */
 int dc_launch_plane_gather_min(const float* p, int mj, int mk, int ijk, int v, int A, int B, float* out, float* part_v,
-                               long long* part_i, float* d_min, dc_hip_stream st);
+                               long long* part_i, float* d_min, uint64_t* clr64, int n64, uint32_t* clr32, int n32,
+                               dc_hip_stream st);
 int dc_encode_plain(void);
 int dc_launch_sub_ptr(const float* x, long long n, const float* d_min, float* y, dc_hip_stream st);
 int dc_launch_sub_value(const float* x, long long n, float m, float* y, hipStream_t st);

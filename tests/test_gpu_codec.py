@@ -563,9 +563,12 @@ def _halo_plane_case(dc, oracle, ct, size, ijk, v, noise):
 
 @pytest.mark.parametrize("ct", [5, 6, 7, 11])
 @pytest.mark.parametrize("noise", [False, True])
-def test_halo_decode2_pair(dc, oracle, ct, noise):
+@pytest.mark.parametrize("ijk,planes", [(3, (1, 5)), (1, (1, 254)), (2, (7, 200))])
+@pytest.mark.parametrize("unfused", [0, 1])
+def test_halo_decode2_pair(dc, oracle, ct, noise, ijk, planes, unfused):
     """(r06) two planes decoded at once on two streams (dc_halo_decode2_device) write the same values into p as two
-    dc_halo_decode_device calls (async halo mode, as the bench's step)"""
+    dc_halo_decode_device calls (async halo mode, as the bench's step); by default each plane's values kernel adds
+    the minimum and scatters into p itself (unfused=1: the separate scatter pass)"""
     import torch
     dc.set_bound(1e-3)
     mi, mj, mk = 257, 257, 8
@@ -577,16 +580,17 @@ def test_halo_decode2_pair(dc, oracle, ct, noise):
         p = p + np.random.RandomState(3).rand(mi, mj, mk).astype(np.float32) * np.float32(0.01)
     p = p.astype(np.float32)
     dp = torch.from_numpy(p).cuda()
-    n = imax * jmax
+    A, B = {1: (jmax, kmax), 2: (imax, kmax), 3: (imax, jmax)}[ijk]
+    n = A * B
+    a, b = np.meshgrid(np.arange(A), np.arange(B), indexing="ij")
     st = [torch.zeros(dc.stream_capacity(n), dtype=torch.uint8, device="cuda") for _ in range(2)]
     bits = torch.zeros(2, dtype=torch.int64, device="cuda")
     mins = torch.zeros(2, dtype=torch.float32, device="cuda")
-    planes = [1, kmax - 2]
     torch.cuda.synchronize()
     ty = [0, 0]
     m17 = [0, 0]
     for h, v in enumerate(planes):
-        ty[h], m17[h] = dc.halo_encode_device(ct, dp.data_ptr(), (mi, mj, mk), 3, v, (imax, jmax, kmax),
+        ty[h], m17[h] = dc.halo_encode_device(ct, dp.data_ptr(), (mi, mj, mk), ijk, v, (imax, jmax, kmax),
                                               st[h].data_ptr(), bits.data_ptr() + 8 * h, mins.data_ptr() + 4 * h)
         dc.encode_result()
     if ct == 7 and (ty[0], m17[0]) != (ty[1], m17[1]):
@@ -594,25 +598,38 @@ def test_halo_decode2_pair(dc, oracle, ct, noise):
     q1 = torch.zeros_like(dp)
     q2 = torch.zeros_like(dp)
     prev = dc.L.dc_set_halo_async(1)
+    prev_u = dc.L.dc_set_halo_unfused(unfused)
     try:
         for h, v in enumerate(planes):
             dc.halo_decode_device(ct, st[h].data_ptr(), -1, bits.data_ptr() + 8 * h, ty[h], m17[h],
-                                  mins.data_ptr() + 4 * h, q1.data_ptr(), (mi, mj, mk), 3, v, (imax, jmax, kmax))
+                                  mins.data_ptr() + 4 * h, q1.data_ptr(), (mi, mj, mk), ijk, v, (imax, jmax, kmax))
         dc.halo_decode2_device(ct, st[0].data_ptr(), st[1].data_ptr(), bits.data_ptr(), bits.data_ptr() + 8, ty[0],
-                               m17[0], mins.data_ptr(), mins.data_ptr() + 4, q2.data_ptr(), (mi, mj, mk), 3, planes[0],
-                               planes[1], (imax, jmax, kmax))
+                               m17[0], mins.data_ptr(), mins.data_ptr() + 4, q2.data_ptr(), (mi, mj, mk), ijk,
+                               planes[0], planes[1], (imax, jmax, kmax))
         dc.synchronize()
         status = dc.decode_status()
     finally:
+        dc.L.dc_set_halo_unfused(prev_u)
         dc.L.dc_set_halo_async(prev)
-    assert status == 0, hex(status)
-    assert torch.equal(q1, q2)
+    if status != 0:
+        # a plane the small-stream decoder declines (a '110'/'111' carry across its blocks, status 512 | why):
+        # the documented fallback, both planes decoded again synchronously
+        assert status & 512 and ijk != 3, hex(status)
+        dc.decode_status_clear()
+        for h, v in enumerate(planes):
+            dc.halo_decode_device(ct, st[h].data_ptr(), -1, bits.data_ptr() + 8 * h, ty[h], m17[h],
+                                  mins.data_ptr() + 4 * h, q2.data_ptr(), (mi, mj, mk), ijk, v, (imax, jmax, kmax))
+        dc.synchronize()
+    else:
+        assert torch.equal(q1, q2)                        # (every other element of p stays 0 in both)
+    q2h = q2.cpu().numpy()
     for h, v in enumerate(planes):                        # and against the oracle's decode + min
         k = (int(bits[h]) + 7) // 8
         s = st[h][:k].cpu().numpy()
         dec, _ = oracle.decompress(ct, s, n, 1e-3, ty[h], m17[h])
         want = (dec + mins[h].cpu().numpy()).astype(np.float32)
-        assert np.array_equal(q2[:imax, :jmax, v].cpu().numpy().reshape(-1).view(np.uint32), want.view(np.uint32))
+        idx = {1: (v, a, b), 2: (a, v, b), 3: (a, b, v)}[ijk]
+        assert np.array_equal(q2h[idx].reshape(-1).view(np.uint32), want.view(np.uint32))
 
 
 @pytest.mark.parametrize("ct", [5, 6, 7, 11])
