@@ -67,10 +67,11 @@ __global__ __launch_bounds__(256) void min_partial_kernel(const float* __restric
 
 // (clr64 / clr32: words zeroed on the way -- in a recorded halo step the next encode's tile states and flag, which a
 // graph replay cannot tag with a new epoch; two memset nodes less per plane)
-__global__ __launch_bounds__(256) void min_final_kernel(const float* __restrict__ x, const float* __restrict__ pv,
-                                                        const long long* __restrict__ pi, int nparts,
-                                                        float* __restrict__ out_min, uint64_t* __restrict__ clr64,
-                                                        int n64, uint32_t* __restrict__ clr32, int n32) {
+// (one workgroup of 256 threads: min_final_kernel, and the last workgroup of plane_gather_min_kernel)
+__device__ __forceinline__ void min_final_body(const float* __restrict__ x, const float* __restrict__ pv,
+                                               const long long* __restrict__ pi, int nparts, float* __restrict__ out_min,
+                                               uint64_t* __restrict__ clr64, int n64, uint32_t* __restrict__ clr32,
+                                               int n32) {
     for (int i = threadIdx.x; i < n64; i += 256) clr64[i] = 0ull;
     for (int i = threadIdx.x; i < n32; i += 256) clr32[i] = 0u;
     __shared__ float sv[256];
@@ -94,6 +95,12 @@ __global__ __launch_bounds__(256) void min_final_kernel(const float* __restrict_
         if (!(m != m) && m < x0) r = m == 0.f ? x[si[0]] : m;   // (a zero: the first one, with its sign)
         *out_min = r;
     }
+}
+__global__ __launch_bounds__(256) void min_final_kernel(const float* __restrict__ x, const float* __restrict__ pv,
+                                                        const long long* __restrict__ pi, int nparts,
+                                                        float* __restrict__ out_min, uint64_t* __restrict__ clr64,
+                                                        int n64, uint32_t* __restrict__ clr32, int n32) {
+    min_final_body(x, pv, pi, nparts, out_min, clr64, n64, clr32, n32);
 }
 
 // (sub_x86, the reference's x86 subtraction: dc_device.h)
@@ -2293,9 +2300,16 @@ __global__ __launch_bounds__(256) void plane_gather_kernel(const float* __restri
 // (r06) the gather with toSmallDataset's minimum partials of the gathered plane (min_partial_kernel's rule: the
 // minimum of out[1..n), NaN ignored, and the index of its first zero) -- the halo encode then needs min_final and
 // the encoder, which subtracts the minimum while loading (Params.subp): three launches instead of six
+// (cnt != nullptr: the last workgroup to finish -- a counter it resets -- takes the minimum itself, min_final_kernel's
+// launch folded in: the other workgroups' partials and gathered floats are released by an agent-scope fence before
+// their count, which the last one acquires)
 __global__ __launch_bounds__(256) void plane_gather_min_kernel(const float* __restrict__ p, int mj, int mk, int ijk, int v,
                                                                int A, int B, float* __restrict__ out,
-                                                               float* __restrict__ pv, long long* __restrict__ pi) {
+                                                               float* __restrict__ pv, long long* __restrict__ pi,
+                                                               unsigned* __restrict__ cnt, float* __restrict__ out_min,
+                                                               uint64_t* __restrict__ clr64, int n64,
+                                                               uint32_t* __restrict__ clr32, int n32) {
+    __shared__ int last;
     __shared__ float sv[4];
     __shared__ long long si[4];
     const long long n = (long long)A * B;
@@ -2320,6 +2334,16 @@ __global__ __launch_bounds__(256) void plane_gather_min_kernel(const float* __re
         pv[blockIdx.x] = fminf(fminf(sv[0], sv[1]), fminf(sv[2], sv[3]));
         pi[blockIdx.x] = min(min(si[0], si[1]), min(si[2], si[3]));
     }
+    if (!cnt) return;
+    if (threadIdx.x == 0) {
+        __threadfence();                                    // (release this workgroup's floats and partial)
+        last = atomicAdd(cnt, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();                                        // (acquire the others')
+    if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    min_final_body(out, pv, pi, (int)gridDim.x, out_min, clr64, n64, clr32, n32);
 }
 
 __global__ __launch_bounds__(256) void plane_scatter_kernel(const float* __restrict__ x, const float* __restrict__ d_min,
@@ -2339,17 +2363,19 @@ extern "C" int dc_launch_plane_gather(const float* p, int mj, int mk, int ijk, i
     hipLaunchKernelGGL(plane_gather_kernel, dim3((unsigned)g), dim3(256), 0, st, p, mj, mk, ijk, v, A, B, out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-// the gathered plane and its minimum into d_min (toSmallDataset_float's minimum of the plane), two launches
+// the gathered plane and its minimum into d_min (toSmallDataset_float's minimum of the plane): one launch with a
+// zeroed counter cnt (the gather's last workgroup finishes the minimum), else two
 extern "C" int dc_launch_plane_gather_min(const float* p, int mj, int mk, int ijk, int v, int A, int B, float* out,
                                           float* part_v, long long* part_i, float* d_min, uint64_t* clr64, int n64,
-                                          uint32_t* clr32, int n32, hipStream_t st) {
+                                          uint32_t* clr32, int n32, unsigned* cnt, hipStream_t st) {
     const long long n = (long long)A * B;
     if (n <= 0) return 0;
     const int g = (int)std::min<long long>(DC_MIN_PARTS, std::max<long long>(1, (n + 1023) / 1024));
     hipLaunchKernelGGL(plane_gather_min_kernel, dim3((unsigned)g), dim3(256), 0, st, p, mj, mk, ijk, v, A, B, out,
-                       part_v, part_i);
-    hipLaunchKernelGGL(min_final_kernel, dim3(1), dim3(256), 0, st, (const float*)out, (const float*)part_v,
-                       (const long long*)part_i, g, d_min, clr64, n64, clr32, n32);
+                       part_v, part_i, cnt, d_min, clr64, n64, clr32, n32);
+    if (!cnt)
+        hipLaunchKernelGGL(min_final_kernel, dim3(1), dim3(256), 0, st, (const float*)out, (const float*)part_v,
+                           (const long long*)part_i, g, d_min, clr64, n64, clr32, n32);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 // y = x - *d_min (the reference's x86 subtraction)

@@ -67,8 +67,10 @@ constexpr uint32_t D3_DECLINE = 512u;
 // s_memrealtime ticks (100 MHz): 2 ms.  Jobs are dispatched in order on each XCD but not across XCDs, so with
 // another kernel running beside (bench.py's pipelined pass: the next step's encode) a job's predecessor can
 // start more than 200 us after it -- the old bound declined such streams (status 0xa00 with 20-chunk
-// segments); the bound only guards against a wait that never ends, which has not been seen
-constexpr unsigned long long D3_LINK_WAIT = 200000;
+// segments); the bound only guards against a wait that never ends, which has not been seen.  (r06) 20 ms: two
+// ranks sharing one GPU (the gloo rehearsal of the multi-rank bench) still hit 2 ms beside the other process's
+// encode (status 0xa00 after the timed steps); a real hang ends all the same
+constexpr unsigned long long D3_LINK_WAIT = 2000000;
 // why (diagnostic bits beside 512): 1024 runs mode / capacity, 2048 unresolved link, 4096 fewer tokens
 // than values, 8192 a job denser than its buffer, 16384 the history sentinel or an early prediction
 constexpr uint32_t D3_WHY_RUNS = 1024u, D3_WHY_LINK = 2048u, D3_WHY_SHORT = 4096u, D3_WHY_DENSE = 8192u,

@@ -122,6 +122,7 @@ typedef struct {
     int halo_unfused;                       /* 1: the halo encode's separate passes (dc_set_halo_unfused, A/B) */
     int capturing;                          /* between dc_capture_begin and dc_capture_end */
     int enc_precleared;                     /* (capture) the next encode's tile states were zeroed by min_final */
+    unsigned* gcnt;                         /* the halo gathers' last-workgroup counters (one per halo stream) */
     int capture_bad;                        /* a call inside the capture that a replay cannot repeat */
     char capture_why[160];
     int tiny_used, tiny_last;               /* the pending decode went to / the last finished one stayed on the
@@ -1381,6 +1382,21 @@ static int plane_dims(int ijk, int imax, int jmax, int kmax, int* A, int* B) {
     return DC_OK;
 }
 
+/* (r06) the halo gathers finish the plane's minimum in their last workgroup (a counter per halo stream, zeroed once
+   and reset by that workgroup); DC_HALO_MIN2=1: the separate min_final launch (A/B) */
+static int halo_counters(void) {
+    if (!G.gcnt) {
+        HIPCHK(hipMalloc((void**)&G.gcnt, 64));
+        HIPCHK(hipMemset(G.gcnt, 0, 64));
+    }
+    return DC_OK;
+}
+static unsigned* halo_cnt(int i) {
+    static int two = -1;
+    if (two < 0) two = getenv("DC_HALO_MIN2") && atoi(getenv("DC_HALO_MIN2")) == 1;
+    return two ? NULL : G.gcnt + 4 * i;
+}
+
 int dc_halo_encode_device(int ct, const void* d_p, int mi, int mj, int mk, int ijk, int v, int imax, int jmax,
                           int kmax, int type, uint32_t mask17, void* d_stream, unsigned long long* d_bits,
                           float* d_min, int* type_out, uint32_t* mask17_out) {
@@ -1404,9 +1420,10 @@ int dc_halo_encode_device(int ct, const void* d_p, int mi, int mj, int mk, int i
            encoder's buffer will not grow */
         const long long dw = dc_encode_desc_words(n) + 8;
         const int pre = G.capturing && G.enc_desc && dw <= G.enc_desc_cap && dw < (1 << 30);
+        if ((rc = halo_counters())) return rc;
         if (dc_launch_plane_gather_min((const float*)d_p, mj, mk, ijk, v, A, B, (float*)G.halo_a, G.part_v, G.part_i,
                                        dmin, pre ? (uint64_t*)G.enc_desc : NULL, pre ? (int)dw : 0,
-                                       pre ? (uint32_t*)G.d_enc_flag : NULL, pre ? 1024 : 0, G.st))
+                                       pre ? (uint32_t*)G.d_enc_flag : NULL, pre ? 1024 : 0, halo_cnt(0), G.st))
             return seterr(DC_ERR_HIP, "plane gather launch failed");
         G.enc_precleared = pre;
         if (type_out) *type_out = type;
@@ -1490,7 +1507,7 @@ int dc_halo_encode2_device(int ct, const void* d_p, int mi, int mj, int mk, int 
         return dc_halo_encode_device(ct, d_p, mi, mj, mk, ijk, v1, imax, jmax, kmax, type, mask17, s1, bits1, dmin1,
                                      NULL, NULL);
     }
-    if ((rc = halo_streams())) return rc;
+    if ((rc = halo_streams()) || (rc = halo_counters())) return rc;
     if (grow(&G.halo_a2, &G.halo_a2_cap, (size_t)n * 4 + 64)) return DC_ERR_HIP;
     if (!G.part_v2) {
         HIPCHK(hipMalloc((void**)&G.part_v2, DC_MIN_PARTS * sizeof(float)));
@@ -1515,7 +1532,7 @@ int dc_halo_encode2_device(int ct, const void* d_p, int mi, int mj, int mk, int 
     const int pre = G.capturing && dw < (1 << 30);
     if (dc_launch_plane_gather_min((const float*)d_p, mj, mk, ijk, v1, A, B, (float*)G.halo_a2, G.part_v2, G.part_i2,
                                    dmin1, pre ? (uint64_t*)G.enc_desc2 : NULL, pre ? (int)dw : 0,
-                                   pre ? (uint32_t*)G.d_enc_flag2 : NULL, pre ? 1024 : 0, G.st2))
+                                   pre ? (uint32_t*)G.d_enc_flag2 : NULL, pre ? 1024 : 0, halo_cnt(1), G.st2))
         return seterr(DC_ERR_HIP, "plane gather launch failed");
     Params P;
     make_params(&P, ct, type, mask17);

@@ -238,10 +238,11 @@ int dc_launch_med(const float* x, long long n, float s_init, void* scratch, floa
                   float* d_max, dc_hip_stream st);
 int dc_launch_med_sub(const float* x, long long n, void* scratch, float* d_min, float* pv, long long* pi, float* d_mean,
                       int* d_type, int wide, hipStream_t st);
-/* (clr64[0..n64) and clr32[0..n32) zeroed by the min_final launch; NULL / 0: none) */
+/* (clr64[0..n64) and clr32[0..n32) zeroed on the way, NULL / 0: none; cnt: a zeroed counter of this stream's own, the
+   minimum finished by the gather's last workgroup, NULL: a second launch) */
 int dc_launch_plane_gather_min(const float* p, int mj, int mk, int ijk, int v, int A, int B, float* out, float* part_v,
                                long long* part_i, float* d_min, uint64_t* clr64, int n64, uint32_t* clr32, int n32,
-                               dc_hip_stream st);
+                               unsigned* cnt, dc_hip_stream st);
 int dc_encode_plain(void);
 int dc_launch_sub_ptr(const float* x, long long n, const float* d_min, float* y, dc_hip_stream st);
 int dc_launch_sub_value(const float* x, long long n, float m, float* y, hipStream_t st);
