@@ -671,6 +671,52 @@ def test_halo_encode2_pair(dc, oracle, ct, ijk, v0, v1):
 
 
 @pytest.mark.parametrize("ct", [5, 6, 11])
+@pytest.mark.parametrize("dims", [(9, 7, 5), (33, 20, 6), (40, 45, 30), (130, 129, 3)])
+@pytest.mark.parametrize("kind", ["noise", "zero_min", "nan"])
+def test_halo_small_planes(dc, oracle, ct, dims, kind):
+    """(r06) halo planes of every size class of the gather's minimum (one workgroup finishing it alone, a few, many):
+    the minimum's bits and the stream against the oracle's toSmallDataset_float + compress, for the three plane
+    orientations, one encode and the pair encode"""
+    import torch
+    dc.set_bound(1e-3)
+    mi, mj, mk = dims
+    imax, jmax, kmax = mi - 1, mj - 1, mk - 1
+    rs = np.random.RandomState(sum(dims) + len(kind))
+    p = (rs.rand(mi, mj, mk).astype(np.float32) * np.float32(2) - np.float32(0.5)).astype(np.float32)
+    if kind == "zero_min":
+        p = np.abs(p).astype(np.float32)
+        p[1, 1, :] = -0.0
+        p[2, 1, :] = 0.0
+    elif kind == "nan":
+        p[::3, 1::2, :] = np.nan
+    dp = torch.from_numpy(p).cuda()
+    for ijk in (1, 2, 3):
+        A, B = {1: (jmax, kmax), 2: (imax, kmax), 3: (imax, jmax)}[ijk]
+        ext = {1: mi, 2: mj, 3: mk}[ijk]
+        v0, v1 = 1, ext - 2
+        n = A * B
+        a, b = np.meshgrid(np.arange(A), np.arange(B), indexing="ij")
+        st = [torch.zeros(dc.stream_capacity(n), dtype=torch.uint8, device="cuda") for _ in range(2)]
+        bits = torch.zeros(2, dtype=torch.int64, device="cuda")
+        mins = torch.zeros(2, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        dc.halo_encode2_device(ct, dp.data_ptr(), (mi, mj, mk), ijk, v0, v1, (imax, jmax, kmax), st[0].data_ptr(),
+                               st[1].data_ptr(), bits.data_ptr(), bits.data_ptr() + 8, mins.data_ptr(),
+                               mins.data_ptr() + 4)
+        dc.synchronize()
+        assert dc.encode_status() == 0
+        for h, v in enumerate((v0, v1)):
+            idx = {1: (v, a, b), 2: (a, v, b), 3: (a, b, v)}[ijk]
+            omn, xs = oracle.to_small(p[idx].reshape(-1).copy())
+            assert mins.cpu().numpy().view(np.uint32)[h] == np.float32(omn).view(np.uint32), (ijk, h)
+            if ct == 6 and np.isnan(xs).any():
+                continue
+            so, nbo, _ = oracle.compress(ct, xs, 1e-3, 0, 0)
+            k = (int(bits[h]) + 7) // 8
+            assert k == nbo and np.array_equal(st[h][:k].cpu().numpy(), so), (ijk, h)
+
+
+@pytest.mark.parametrize("ct", [5, 6, 11])
 @pytest.mark.parametrize("pair_encode", [False, True])
 def test_halo_graph_replay(dc, oracle, ct, pair_encode):
     """(r06) the halo step recorded into a HIP graph (dc_capture_begin/end) and replayed (dc_graph_launch): each replay
